@@ -1,0 +1,55 @@
+"""beforeholiday_amd -- an MI355X-native (gfx950 / CDNA4) mixed-precision and distributed
+training library with the public API of NVIDIA Apex / SkyHeroesS/beforeholiday.
+
+Layout (reference package ``apex`` -> this package):
+
+* ``amp``, ``fp16_utils``                        mixed precision runtime
+* ``optimizers``, ``multi_tensor_apply``         fused multi-tensor optimizers (HIP kernels)
+* ``normalization``, ``fused_dense``, ``mlp``    fused layers (HIP kernels, MFMA GEMMs)
+* ``parallel``                                   DDP / Reducer / SyncBatchNorm / LARC over RCCL
+* ``transformer``                                Megatron-style TP/SP/PP
+* ``contrib``                                    xentropy, focal loss, MHA, ZeRO optimizers, ...
+* ``ops``                                        op-level entry points (amp_C, syncbn, ...)
+* ``models``                                     ResNet-50 / BERT / GPT reference workloads
+* ``utils``                                      logging, timers, profiling helpers
+
+GPU tensors always run the native extension ``beforeholiday_amd._C`` (built in-tree with
+``python -m beforeholiday_amd._build``); CPU tensors run PyTorch reference implementations.
+"""
+from __future__ import annotations
+
+import importlib
+
+__version__ = "0.1.0"
+
+from . import _native  # noqa: F401
+from ._native import available as native_available  # noqa: F401
+
+_SUBMODULES = [
+    "ops", "multi_tensor_apply", "optimizers", "amp", "fp16_utils", "normalization", "parallel",
+    "fused_dense", "mlp", "transformer", "contrib", "RNN", "models", "utils",
+]
+
+
+def __getattr__(name):
+    if name in _SUBMODULES:
+        mod = importlib.import_module(f".{name}", __name__)
+        globals()[name] = mod
+        return mod
+    raise AttributeError(f"module {__name__!r} has no attribute {name!r}")
+
+
+def install_apex_aliases():
+    """Opt-in: make ``import apex`` / ``import amp_C`` resolve to this package, so code written
+    against the reference runs unchanged (``apex.amp``, ``apex.optimizers.FusedLAMB``, ...)."""
+    import sys
+
+    sys.modules.setdefault("apex", sys.modules[__name__])
+    for sub in _SUBMODULES:
+        try:
+            sys.modules.setdefault(f"apex.{sub}", importlib.import_module(f".{sub}", __name__))
+        except ImportError:
+            pass
+    from .ops import amp_C
+
+    sys.modules.setdefault("amp_C", amp_C)

@@ -1,0 +1,498 @@
+// amp_C front-end: python signatures match the reference's csrc/amp_C_frontend.cpp:165-194
+// (chunk_size, noop_flag, tensor_lists, ...), kernels are bh::mta_* (kernels/multi_tensor.hip).
+#include "common.h"
+
+#include <cmath>
+#include <mutex>
+#include <unordered_map>
+
+namespace bhb {
+
+namespace {
+
+struct KeyHash {
+  size_t operator()(const std::vector<int64_t>& k) const noexcept {
+    uint64_t h = 1469598103934665603ull;
+    for (int64_t x : k) {
+      h ^= static_cast<uint64_t>(x) + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
+    }
+    return static_cast<size_t>(h);
+  }
+};
+
+std::mutex g_plan_mu;
+std::unordered_map<std::vector<int64_t>, MTAPlan, KeyHash> g_plans;
+constexpr size_t kMaxPlans = 4096;
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+int list_dtype(const std::vector<at::Tensor>& l, const char* op) {
+  TORCH_CHECK(!l.empty(), op, ": empty tensor list");
+  const auto st = l[0].scalar_type();
+  for (const auto& t : l) {
+    TORCH_CHECK(t.scalar_type() == st, op, ": all tensors of a list must share a dtype");
+    TORCH_CHECK(t.is_cuda(), op, ": tensors must be on the GPU");
+    TORCH_CHECK(t.is_contiguous() || t.is_contiguous(at::MemoryFormat::ChannelsLast) ||
+                    t.is_contiguous(at::MemoryFormat::ChannelsLast3d),
+                op, ": tensors must be dense (contiguous or channels_last)");
+  }
+  return dtype_code(st);
+}
+
+const MTAPlan& get_plan(const std::vector<std::vector<at::Tensor>>& lists, int64_t chunk) {
+  TORCH_CHECK(!lists.empty(), "multi_tensor: no tensor lists");
+  const int depth = static_cast<int>(lists.size());
+  const int T = static_cast<int>(lists[0].size());
+  for (const auto& l : lists)
+    TORCH_CHECK(static_cast<int>(l.size()) == T, "multi_tensor: tensor lists must have equal length");
+  TORCH_CHECK(chunk > 0 && chunk % 8 == 0, "multi_tensor: chunk_size must be a positive multiple of 8");
+  const auto dev = lists[0][0].device();
+
+  std::vector<int64_t> key;
+  key.reserve(4 + (size_t)T * (depth + 1));
+  key.push_back(dev.index());
+  key.push_back(depth);
+  key.push_back(chunk);
+  key.push_back(T);
+  for (int t = 0; t < T; ++t) {
+    const int64_t n = lists[0][t].numel();
+    key.push_back(n);
+    for (int d = 0; d < depth; ++d) {
+      const auto& x = lists[d][t];
+      TORCH_CHECK(x.numel() == n, "multi_tensor: size mismatch between lists at index ", t);
+      TORCH_CHECK(x.device() == dev, "multi_tensor: all tensors must be on one device");
+      key.push_back(reinterpret_cast<int64_t>(x.data_ptr()));
+    }
+  }
+
+  std::lock_guard<std::mutex> lock(g_plan_mu);
+  auto it = g_plans.find(key);
+  if (it != g_plans.end()) return it->second;
+
+  hipStream_t stream = stream_for(lists[0][0]);
+  if (g_plans.size() >= kMaxPlans && !capturing(stream)) g_plans.clear();
+
+  // chunk schedule
+  std::vector<int> chunk0(T + 1, 0);
+  for (int t = 0; t < T; ++t) {
+    const int64_t n = lists[0][t].numel();
+    const int64_t c = (n + chunk - 1) / chunk;
+    TORCH_CHECK(chunk0[t] + c < (int64_t)INT32_MAX, "multi_tensor: too many chunks");
+    chunk0[t + 1] = chunk0[t] + static_cast<int>(c);
+  }
+  const int C = chunk0[T];
+
+  const size_t o_ptrs = 0;
+  const size_t o_numel = align_up(o_ptrs + sizeof(uint64_t) * depth * T, 16);
+  const size_t o_al = align_up(o_numel + sizeof(int64_t) * T, 16);
+  const size_t o_c0 = align_up(o_al + sizeof(int) * T, 16);
+  const size_t o_ct = align_up(o_c0 + sizeof(int) * (T + 1), 16);
+  const size_t o_cl = align_up(o_ct + sizeof(int) * C, 16);
+  const size_t bytes = align_up(o_cl + sizeof(int) * C, 16) + 16;
+
+  at::Tensor host = at::empty({(int64_t)bytes}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  uint8_t* h = host.data_ptr<uint8_t>();
+  auto* hp = reinterpret_cast<uint64_t*>(h + o_ptrs);
+  auto* hn = reinterpret_cast<int64_t*>(h + o_numel);
+  auto* ha = reinterpret_cast<int*>(h + o_al);
+  auto* hc0 = reinterpret_cast<int*>(h + o_c0);
+  auto* hct = reinterpret_cast<int*>(h + o_ct);
+  auto* hcl = reinterpret_cast<int*>(h + o_cl);
+  for (int t = 0; t < T; ++t) {
+    bool al = true;
+    for (int d = 0; d < depth; ++d) {
+      const uint64_t p = reinterpret_cast<uint64_t>(lists[d][t].data_ptr());
+      hp[(size_t)d * T + t] = p;
+      al = al && (p % 16 == 0);
+    }
+    hn[t] = lists[0][t].numel();
+    ha[t] = al ? 1 : 0;
+  }
+  for (int t = 0; t <= T; ++t) hc0[t] = chunk0[t];
+  for (int t = 0; t < T; ++t)
+    for (int c = chunk0[t]; c < chunk0[t + 1]; ++c) {
+      hct[c] = t;
+      hcl[c] = c - chunk0[t];
+    }
+
+  at::Tensor devbuf = at::empty({(int64_t)bytes}, lists[0][0].options().dtype(at::kByte));
+  devbuf.copy_(host, /*non_blocking=*/true);
+
+  MTAPlan plan;
+  plan.dev = devbuf;
+  plan.host = host;
+  uint8_t* d = devbuf.data_ptr<uint8_t>();
+  plan.view.ptrs = reinterpret_cast<const uint64_t*>(d + o_ptrs);
+  plan.view.numel = reinterpret_cast<const int64_t*>(d + o_numel);
+  plan.view.aligned = reinterpret_cast<const int*>(d + o_al);
+  plan.view.chunk0 = reinterpret_cast<const int*>(d + o_c0);
+  plan.view.chunk_tensor = reinterpret_cast<const int*>(d + o_ct);
+  plan.view.chunk_local = reinterpret_cast<const int*>(d + o_cl);
+  plan.view.T = T;
+  plan.view.C = C;
+  plan.view.depth = depth;
+  plan.view.chunk = static_cast<int>(chunk);
+  auto res = g_plans.emplace(std::move(key), std::move(plan));
+  return res.first->second;
+}
+
+namespace {
+
+using Lists = std::vector<std::vector<at::Tensor>>;
+
+void check_noop(const at::Tensor& noop) {
+  TORCH_CHECK(noop.is_cuda() && noop.scalar_type() == at::kInt && noop.numel() >= 1,
+              "noop_flag must be a GPU int32 tensor");
+}
+
+bool lists_empty(const Lists& l) { return l.empty() || l[0].empty(); }
+
+void multi_tensor_scale(int64_t chunk, at::Tensor noop, Lists lists, double scale) {
+  if (lists_empty(lists)) return;
+  TORCH_CHECK(lists.size() == 2, "multi_tensor_scale expects 2 lists");
+  check_noop(noop);
+  const auto& p = get_plan(lists, chunk);
+  bh::mta_scale(p.view, list_dtype(lists[0], "scale"), list_dtype(lists[1], "scale"), (float)scale,
+                noop.data_ptr<int>(), stream_for(noop));
+}
+
+void multi_tensor_axpby(int64_t chunk, at::Tensor noop, Lists lists, double a, double b, int64_t arg) {
+  if (lists_empty(lists)) return;
+  TORCH_CHECK(lists.size() == 3, "multi_tensor_axpby expects 3 lists");
+  check_noop(noop);
+  const auto& p = get_plan(lists, chunk);
+  bh::mta_axpby(p.view, list_dtype(lists[0], "axpby"), list_dtype(lists[1], "axpby"),
+                list_dtype(lists[2], "axpby"), (float)a, (float)b, (int)arg, noop.data_ptr<int>(),
+                stream_for(noop));
+}
+
+std::tuple<at::Tensor, at::Tensor> norm_impl(int64_t chunk, at::Tensor noop, Lists lists,
+                                             bool per_tensor, int norm_type, bool mp,
+                                             double scale, bool with_scale) {
+  check_noop(noop);
+  auto fopt = noop.options().dtype(at::kFloat);
+  if (lists_empty(lists)) {
+    return {at::zeros({1}, fopt), per_tensor ? at::zeros({0}, fopt) : at::empty({0}, fopt)};
+  }
+  const auto& p = get_plan(lists, chunk);
+  const int T = p.view.T;
+  auto total = mp ? at::zeros({1}, fopt) : at::empty({1}, fopt);
+  auto per = per_tensor ? at::zeros({T}, fopt) : at::empty({0}, fopt);
+  auto partials = at::empty({std::max(p.view.C, 1)}, fopt);
+  hipStream_t s = stream_for(noop);
+  const int dt_in = list_dtype(lists[0], "l2norm");
+  const int dt_out = with_scale ? list_dtype(lists[1], "l2norm_scale") : -1;
+  bh::mta_norm_partials(p.view, dt_in, dt_out, norm_type, (float)scale, partials.data_ptr<float>(),
+                        noop.data_ptr<int>(), mp, s);
+  bh::mta_norm_finalize(p.view, partials.data_ptr<float>(), 1, norm_type,
+                        per_tensor ? per.data_ptr<float>() : nullptr, total.data_ptr<float>(), false,
+                        0.f, 0.f, noop.data_ptr<int>(), mp, s);
+  return {total, per};
+}
+
+std::tuple<at::Tensor, at::Tensor> multi_tensor_l2norm(int64_t chunk, at::Tensor noop, Lists lists,
+                                                       c10::optional<bool> per_tensor) {
+  TORCH_CHECK(lists_empty(lists) || lists.size() == 1, "multi_tensor_l2norm expects 1 list");
+  return norm_impl(chunk, noop, lists, per_tensor.value_or(false), 2, false, 1.0, false);
+}
+std::tuple<at::Tensor, at::Tensor> multi_tensor_l2norm_mp(int64_t chunk, at::Tensor noop, Lists lists,
+                                                          c10::optional<bool> per_tensor) {
+  TORCH_CHECK(lists_empty(lists) || lists.size() == 1, "multi_tensor_l2norm_mp expects 1 list");
+  return norm_impl(chunk, noop, lists, per_tensor.value_or(false), 2, true, 1.0, false);
+}
+std::tuple<at::Tensor, at::Tensor> multi_tensor_l2norm_scale(int64_t chunk, at::Tensor noop, Lists lists,
+                                                             double scale, c10::optional<bool> per_tensor) {
+  TORCH_CHECK(lists_empty(lists) || lists.size() == 2, "multi_tensor_l2norm_scale expects 2 lists");
+  return norm_impl(chunk, noop, lists, per_tensor.value_or(false), 2, false, scale, true);
+}
+
+// out[t] = blend(out[t], norm(list0[t]))  (L2: sqrt(a*o^2+b*n^2), Linf: a*o+b*n)
+void multi_tensor_norm_out(int64_t chunk, at::Tensor noop, Lists lists, at::Tensor out, double alpha,
+                           double beta, int64_t norm_type) {
+  if (lists_empty(lists)) return;
+  check_noop(noop);
+  const auto& p = get_plan({lists[0]}, chunk);
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.numel() == p.view.T,
+              "multi_tensor_norm_out: out must be fp32 with one entry per tensor");
+  auto partials = at::empty({std::max(p.view.C, 1)}, noop.options().dtype(at::kFloat));
+  hipStream_t s = stream_for(noop);
+  const int nt = norm_type == 0 ? 0 : 2;
+  bh::mta_norm_partials(p.view, list_dtype(lists[0], "norm_out"), -1, nt, 1.f,
+                        partials.data_ptr<float>(), noop.data_ptr<int>(), false, s);
+  bh::mta_norm_finalize(p.view, partials.data_ptr<float>(), 1, nt, out.data_ptr<float>(), nullptr, true,
+                        (float)alpha, (float)beta, noop.data_ptr<int>(), false, s);
+}
+
+int copy_dtype(const Lists& lists, size_t idx) {
+  return lists.size() > idx ? list_dtype(lists[idx], "copy-out") : -1;
+}
+
+void multi_tensor_adam(int64_t chunk, at::Tensor noop, Lists lists, double lr, double beta1,
+                       double beta2, double eps, int64_t step, int64_t mode, int64_t bias_correction,
+                       double weight_decay) {
+  if (lists_empty(lists)) return;
+  TORCH_CHECK(lists.size() == 4 || lists.size() == 5, "multi_tensor_adam expects 4 (or 5) lists");
+  const auto& p = get_plan(lists, chunk);
+  bh::AdamArgs a{};
+  a.lr = (float)lr;
+  a.beta1 = (float)beta1;
+  a.beta2 = (float)beta2;
+  a.eps = (float)eps;
+  a.bc1 = bias_correction ? 1.f - (float)std::pow(beta1, (double)step) : 1.f;
+  a.bc2 = bias_correction ? 1.f - (float)std::pow(beta2, (double)step) : 1.f;
+  a.decay = (float)weight_decay;
+  a.mode = (int)mode;
+  a.bias_correction = (int)bias_correction;
+  bh::mta_adam(p.view, list_dtype(lists[0], "adam"), list_dtype(lists[1], "adam"),
+               list_dtype(lists[2], "adam"), copy_dtype(lists, 4), a, stream_for(noop));
+}
+
+// capturable Adam: device lr/step, optional unscale + found_inf skip (GradScaler integration)
+void multi_tensor_adam_capturable(int64_t chunk, at::Tensor noop, Lists lists, at::Tensor lr,
+                                  double beta1, double beta2, double eps, at::Tensor step, int64_t mode,
+                                  int64_t bias_correction, double weight_decay,
+                                  c10::optional<at::Tensor> inv_scale,
+                                  c10::optional<at::Tensor> found_inf) {
+  if (lists_empty(lists)) return;
+  TORCH_CHECK(lists.size() == 4 || lists.size() == 5, "multi_tensor_adam_capturable expects 4 (or 5) lists");
+  const auto& p = get_plan(lists, chunk);
+  bh::AdamArgs a{};
+  a.beta1 = (float)beta1;
+  a.beta2 = (float)beta2;
+  a.eps = (float)eps;
+  a.bc1 = a.bc2 = 1.f;
+  a.decay = (float)weight_decay;
+  a.mode = (int)mode;
+  a.bias_correction = (int)bias_correction;
+  TORCH_CHECK(lr.scalar_type() == at::kFloat && step.scalar_type() == at::kInt, "lr must be fp32, step int32");
+  a.lr_ptr = lr.data_ptr<float>();
+  a.step_ptr = step.data_ptr<int>();
+  a.inv_scale = ptr_or_null<float>(inv_scale);
+  a.found_inf = ptr_or_null<float>(found_inf);
+  bh::mta_adam(p.view, list_dtype(lists[0], "adam"), list_dtype(lists[1], "adam"),
+               list_dtype(lists[2], "adam"), copy_dtype(lists, 4), a, stream_for(noop));
+}
+
+void multi_tensor_sgd(int64_t chunk, at::Tensor noop, Lists lists, double wd, double momentum,
+                      double dampening, double lr, bool nesterov, bool first_run, bool wd_after_momentum,
+                      double scale) {
+  if (lists_empty(lists)) return;
+  TORCH_CHECK(lists.size() == 3 || lists.size() == 4, "multi_tensor_sgd expects 3 or 4 lists");
+  check_noop(noop);
+  const auto& p = get_plan(lists, chunk);
+  bh::SGDArgs a{};
+  a.wd = (float)wd;
+  a.momentum = (float)momentum;
+  a.dampening = (float)dampening;
+  a.lr = (float)lr;
+  a.scale = (float)scale;
+  a.nesterov = nesterov;
+  a.first_run = first_run;
+  a.wd_after_momentum = wd_after_momentum;
+  const int dtg = list_dtype(lists[0], "sgd"), dtp = list_dtype(lists[1], "sgd");
+  TORCH_CHECK(list_dtype(lists[2], "sgd") == dtp, "multi_tensor_sgd: momentum dtype must match params");
+  bh::mta_sgd(p.view, dtg, dtp, copy_dtype(lists, 3), a, noop.data_ptr<int>(), stream_for(noop));
+}
+
+bh::LambArgs lamb_args(double lr, double beta1, double beta2, double eps, int64_t step,
+                       int64_t bias_correction, double weight_decay, int64_t grad_averaging, int64_t mode,
+                       double max_grad_norm, bool nvlamb) {
+  bh::LambArgs a{};
+  a.lr = (float)lr;
+  a.beta1 = (float)beta1;
+  a.beta2 = (float)beta2;
+  a.beta3 = grad_averaging ? 1.f - (float)beta1 : 1.f;
+  a.bc1 = bias_correction ? 1.f - (float)std::pow(beta1, (double)step) : 1.f;
+  a.bc2 = bias_correction ? 1.f - (float)std::pow(beta2, (double)step) : 1.f;
+  a.eps = (float)eps;
+  a.decay = (float)weight_decay;
+  a.max_grad_norm = (float)max_grad_norm;
+  a.mode = (int)mode;
+  a.use_nvlamb = nvlamb;
+  a.bias_correction = (int)bias_correction;
+  return a;
+}
+
+void lamb_run(const Lists& lists, int64_t chunk, const at::Tensor& noop, const bh::LambArgs& a) {
+  const auto& p = get_plan(lists, chunk);
+  auto fopt = noop.options().dtype(at::kFloat);
+  auto partials = at::empty({2 * std::max(p.view.C, 1)}, fopt);
+  auto norms = at::zeros({2 * std::max(p.view.T, 1)}, fopt);
+  hipStream_t s = stream_for(noop);
+  const int dtg = list_dtype(lists[0], "lamb"), dtp = list_dtype(lists[1], "lamb");
+  const int dts = list_dtype(lists[2], "lamb");
+  TORCH_CHECK(list_dtype(lists[3], "lamb") == dts, "multi_tensor_lamb: exp_avg/exp_avg_sq dtype mismatch");
+  bh::mta_lamb_stage1(p.view, dtg, dtp, dts, a, partials.data_ptr<float>(), s);
+  bh::mta_norm_finalize(p.view, partials.data_ptr<float>(), 2, 2, norms.data_ptr<float>(), nullptr, false,
+                        0.f, 0.f, nullptr, false, s);
+  bh::mta_lamb_stage2(p.view, dtp, dts, copy_dtype(lists, 4), a, norms.data_ptr<float>(), s);
+}
+
+void multi_tensor_lamb(int64_t chunk, at::Tensor noop, Lists lists, double lr, double beta1, double beta2,
+                       double eps, int64_t step, int64_t bias_correction, double weight_decay,
+                       int64_t grad_averaging, int64_t mode, at::Tensor global_grad_norm,
+                       double max_grad_norm, c10::optional<bool> use_nvlamb) {
+  if (lists_empty(lists)) return;
+  TORCH_CHECK(lists.size() == 4 || lists.size() == 5, "multi_tensor_lamb expects 4 (or 5) lists");
+  auto a = lamb_args(lr, beta1, beta2, eps, step, bias_correction, weight_decay, grad_averaging, mode,
+                     max_grad_norm, use_nvlamb.value_or(false));
+  TORCH_CHECK(global_grad_norm.is_cuda() && global_grad_norm.scalar_type() == at::kFloat,
+              "global_grad_norm must be a GPU fp32 tensor");
+  a.grad_norm = global_grad_norm.data_ptr<float>();
+  lamb_run(lists, chunk, noop, a);
+}
+
+void multi_tensor_lamb_mp(int64_t chunk, at::Tensor noop, Lists lists, at::Tensor lr, double beta1,
+                          double beta2, double eps, at::Tensor step, int64_t bias_correction,
+                          double weight_decay, int64_t grad_averaging, int64_t mode,
+                          at::Tensor global_grad_norm, at::Tensor max_grad_norm,
+                          c10::optional<bool> use_nvlamb, at::Tensor found_inf, at::Tensor inv_scale) {
+  if (lists_empty(lists)) return;
+  TORCH_CHECK(lists.size() == 4 || lists.size() == 5, "multi_tensor_lamb_mp expects 4 or 5 lists");
+  check_noop(noop);
+  auto a = lamb_args(0.0, beta1, beta2, eps, 1, bias_correction, weight_decay, grad_averaging, mode, 0.0,
+                     use_nvlamb.value_or(false));
+  a.lr_ptr = lr.data_ptr<float>();
+  TORCH_CHECK(step.scalar_type() == at::kInt, "step must be int32");
+  a.step_ptr = step.data_ptr<int>();
+  a.grad_norm = global_grad_norm.data_ptr<float>();
+  a.max_norm_ptr = max_grad_norm.data_ptr<float>();
+  a.found_inf = found_inf.data_ptr<float>();
+  a.inv_scale = inv_scale.data_ptr<float>();
+  a.noop = noop.data_ptr<int>();
+  lamb_run(lists, chunk, noop, a);
+}
+
+void multi_tensor_lamb_stage1_cuda(int64_t chunk, at::Tensor noop, Lists lists, at::Tensor per_tensor_decay,
+                                   int64_t step, double beta1, double beta2, double eps,
+                                   at::Tensor global_grad_norm, double max_global_grad_norm) {
+  if (lists_empty(lists)) return;
+  TORCH_CHECK(lists.size() == 5, "multi_tensor_lamb_stage1_cuda expects 5 lists");
+  const auto& p = get_plan(lists, chunk);
+  // the reference reads the (host-synchronised) norm value here as well
+  const float gn = global_grad_norm.item<float>();
+  const float clipped = gn > max_global_grad_norm ? gn / (float)max_global_grad_norm : 1.f;
+  const float bc1 = 1.f - (float)std::pow(beta1, (double)step);
+  const float bc2 = 1.f - (float)std::pow(beta2, (double)step);
+  TORCH_CHECK(list_dtype(lists[2], "lamb_stage1") == list_dtype(lists[1], "lamb_stage1"),
+              "lamb_stage1: moments must match param dtype");
+  bh::mta_lamb_stage1_standalone(p.view, list_dtype(lists[0], "lamb_stage1"), list_dtype(lists[1], "lamb_stage1"),
+                                 list_dtype(lists[4], "lamb_stage1"), per_tensor_decay.data_ptr<float>(),
+                                 (float)beta1, (float)beta2, bc1, bc2, (float)eps, clipped, stream_for(noop));
+}
+
+void multi_tensor_lamb_stage2_cuda(int64_t chunk, at::Tensor noop, Lists lists, at::Tensor pnorm,
+                                   at::Tensor unorm, double lr, double weight_decay,
+                                   c10::optional<bool> use_nvlamb) {
+  if (lists_empty(lists)) return;
+  TORCH_CHECK(lists.size() == 2, "multi_tensor_lamb_stage2_cuda expects 2 lists");
+  const auto& p = get_plan(lists, chunk);
+  bh::mta_lamb_stage2_standalone(p.view, list_dtype(lists[0], "lamb_stage2"), list_dtype(lists[1], "lamb_stage2"),
+                                 pnorm.data_ptr<float>(), unorm.data_ptr<float>(), (float)lr,
+                                 (float)weight_decay, use_nvlamb.value_or(false), stream_for(noop));
+}
+
+void multi_tensor_novograd(int64_t chunk, at::Tensor noop, Lists lists, at::Tensor grad_norms, double lr,
+                           double beta1, double beta2, double eps, int64_t step, int64_t bias_correction,
+                           double weight_decay, int64_t grad_averaging, int64_t mode, int64_t norm_type) {
+  if (lists_empty(lists)) return;
+  TORCH_CHECK(lists.size() == 3, "multi_tensor_novograd expects 3 lists");
+  float bc1 = 1.f, bc2 = 1.f;
+  if (bias_correction) {
+    bc1 = 1.f - (float)std::pow(beta1, (double)step);
+    bc2 = std::sqrt(1.f - (float)std::pow(beta2, (double)step));
+  }
+  const float beta3 = grad_averaging ? 1.f - (float)beta1 : 1.f;
+  multi_tensor_norm_out(chunk, noop, {lists[0]}, grad_norms, beta2, 1.0 - beta2, norm_type);
+  const auto& p = get_plan(lists, chunk);
+  const int dt = list_dtype(lists[0], "novograd");
+  TORCH_CHECK(list_dtype(lists[1], "novograd") == dt && list_dtype(lists[2], "novograd") == dt,
+              "multi_tensor_novograd: all lists must share a dtype");
+  bh::mta_novograd(p.view, dt, (float)lr, (float)beta1, beta3, bc1, bc2, (float)eps, (int)mode,
+                   (float)weight_decay, grad_norms.data_ptr<float>(), stream_for(noop));
+}
+
+void multi_tensor_adagrad(int64_t chunk, at::Tensor noop, Lists lists, double lr, double eps, int64_t mode,
+                          double weight_decay) {
+  if (lists_empty(lists)) return;
+  TORCH_CHECK(lists.size() == 3, "multi_tensor_adagrad expects 3 lists");
+  const auto& p = get_plan(lists, chunk);
+  const int dt = list_dtype(lists[0], "adagrad");
+  TORCH_CHECK(list_dtype(lists[1], "adagrad") == dt && list_dtype(lists[2], "adagrad") == dt,
+              "multi_tensor_adagrad: all lists must share a dtype");
+  bh::mta_adagrad(p.view, dt, (float)lr, (float)eps, (int)mode, (float)weight_decay, stream_for(noop));
+}
+
+void multi_tensor_lars(int64_t chunk, at::Tensor noop, Lists lists, at::Tensor grad_norms,
+                       at::Tensor param_norms, double lr, double trust_coefficient, double eps,
+                       double weight_decay, double momentum, double dampening, bool nesterov,
+                       bool first_run, bool wd_after_momentum, double scale, bool is_skipped) {
+  if (lists_empty(lists)) return;
+  TORCH_CHECK(lists.size() == 3 || lists.size() == 4, "multi_tensor_lars expects 3 or 4 lists");
+  check_noop(noop);
+  const auto& p = get_plan(lists, chunk);
+  bh::LarsArgs a{};
+  a.lr = (float)lr;
+  a.trust_coefficient = (float)trust_coefficient;
+  a.eps = (float)eps;
+  a.wd = (float)weight_decay;
+  a.momentum = (float)momentum;
+  a.dampening = (float)dampening;
+  a.scale = (float)scale;
+  a.nesterov = nesterov;
+  a.first_run = first_run;
+  a.wd_after_momentum = wd_after_momentum;
+  a.is_skipped = is_skipped;
+  const int dtp = list_dtype(lists[1], "lars");
+  TORCH_CHECK(list_dtype(lists[2], "lars") == dtp, "multi_tensor_lars: momentum dtype must match params");
+  bh::mta_lars(p.view, list_dtype(lists[0], "lars"), dtp, copy_dtype(lists, 3), a, grad_norms.data_ptr<float>(),
+               param_norms.data_ptr<float>(), noop.data_ptr<int>(), stream_for(noop));
+}
+
+size_t plan_cache_size() {
+  std::lock_guard<std::mutex> lock(g_plan_mu);
+  return g_plans.size();
+}
+void plan_cache_clear() {
+  std::lock_guard<std::mutex> lock(g_plan_mu);
+  g_plans.clear();
+}
+
+}  // namespace
+
+void register_amp_C(pybind11::module_& root) {
+  namespace py = pybind11;
+  auto m = root.def_submodule("amp_C", "multi-tensor apply kernels (gfx950)");
+  m.def("multi_tensor_scale", &multi_tensor_scale, "out = in * scale with overflow flag");
+  m.def("multi_tensor_sgd", &multi_tensor_sgd, "fused SGD");
+  m.def("multi_tensor_axpby", &multi_tensor_axpby, "out = a*x + b*y with overflow flag");
+  m.def("multi_tensor_l2norm", &multi_tensor_l2norm, py::arg("chunk_size"), py::arg("noop_flag"),
+        py::arg("tensor_lists"), py::arg("per_tensor") = py::none());
+  m.def("multi_tensor_l2norm_mp", &multi_tensor_l2norm_mp, py::arg("chunk_size"), py::arg("noop_flag"),
+        py::arg("tensor_lists"), py::arg("per_tensor") = py::none());
+  m.def("multi_tensor_l2norm_scale", &multi_tensor_l2norm_scale, py::arg("chunk_size"), py::arg("noop_flag"),
+        py::arg("tensor_lists"), py::arg("scale"), py::arg("per_tensor") = py::none());
+  m.def("multi_tensor_norm_out", &multi_tensor_norm_out, "blended per-tensor norms");
+  m.def("multi_tensor_lamb_stage1_cuda", &multi_tensor_lamb_stage1_cuda);
+  m.def("multi_tensor_lamb_stage2_cuda", &multi_tensor_lamb_stage2_cuda);
+  m.def("multi_tensor_adam", &multi_tensor_adam, "fused Adam/AdamW (5th list: low-precision param copy)");
+  m.def("multi_tensor_adam_capturable", &multi_tensor_adam_capturable, py::arg("chunk_size"),
+        py::arg("noop_flag"), py::arg("tensor_lists"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"),
+        py::arg("eps"), py::arg("step"), py::arg("mode"), py::arg("bias_correction"),
+        py::arg("weight_decay"), py::arg("inv_scale") = py::none(), py::arg("found_inf") = py::none());
+  m.def("multi_tensor_adagrad", &multi_tensor_adagrad);
+  m.def("multi_tensor_novograd", &multi_tensor_novograd);
+  m.def("multi_tensor_lamb", &multi_tensor_lamb, py::arg("chunk_size"), py::arg("noop_flag"),
+        py::arg("tensor_lists"), py::arg("lr"), py::arg("beta1"), py::arg("beta2"), py::arg("epsilon"),
+        py::arg("step"), py::arg("bias_correction"), py::arg("weight_decay"), py::arg("grad_averaging"),
+        py::arg("mode"), py::arg("global_grad_norm"), py::arg("max_grad_norm"),
+        py::arg("use_nvlamb_python") = py::none());
+  m.def("multi_tensor_lamb_mp", &multi_tensor_lamb_mp);
+  m.def("multi_tensor_lars", &multi_tensor_lars);
+  m.def("plan_cache_size", &plan_cache_size);
+  m.def("plan_cache_clear", &plan_cache_clear);
+}
+
+}  // namespace bhb
