@@ -1,0 +1,117 @@
+"""Loss scaler (reference: apex/amp/scaler.py:42-226).
+
+Dynamic scaling (2^16 initial, x2 after ``scale_window`` clean steps, /2 on overflow, clamped by
+min/max). Unscaling of whole gradient lists is ONE multi-tensor launch (convert + scale +
+overflow flag), the flag is read once per step in ``update_scale``.
+"""
+from __future__ import annotations
+
+import torch
+
+from ..multi_tensor_apply import multi_tensor_applier
+from ..ops import amp_C
+from ._amp_state import maybe_print
+
+
+class LossScaler(object):
+    warned_no_fused_kernel = False
+    warned_unscaling_non_fp32_grad = False
+    has_fused_kernel = True
+
+    def __init__(self, loss_scale, init_scale=2.0 ** 16, scale_factor=2.0, scale_window=2000,
+                 min_loss_scale=None, max_loss_scale=2.0 ** 24, device=None):
+        if loss_scale == "dynamic":
+            self.dynamic = True
+            self._loss_scale = min(max_loss_scale, init_scale)
+        else:
+            self.dynamic = False
+            self._loss_scale = loss_scale
+        self._max_loss_scale = max_loss_scale
+        self._min_loss_scale = min_loss_scale
+        self._scale_seq_len = scale_window
+        self._scale_factor = scale_factor
+        self._unskipped = 0
+        self._has_overflow = False
+        if device is None:
+            device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+        self._overflow_buf = torch.zeros(1, dtype=torch.int, device=device)
+        LossScaler.multi_tensor_scale_cuda = amp_C.multi_tensor_scale
+        LossScaler.multi_tensor_axpby_cuda = amp_C.multi_tensor_axpby
+
+    def loss_scale(self):
+        return self._loss_scale
+
+    def _flag_for(self, tensors):
+        # the overflow flag must live on the gradients' device
+        dev = tensors[0].device
+        if self._overflow_buf.device != dev:
+            self._overflow_buf = torch.zeros(1, dtype=torch.int, device=dev)
+        return self._overflow_buf
+
+    def _warn_non_fp32(self, master_grads):
+        if not LossScaler.warned_unscaling_non_fp32_grad and master_grads and master_grads[0].dtype != torch.float32:
+            maybe_print("Attempting to unscale a grad with type {} Unscaling non-fp32 grads may indicate "
+                        "an error. When using Amp, you don't need to call .half() on your model."
+                        .format(master_grads[0].type()))
+            LossScaler.warned_unscaling_non_fp32_grad = True
+
+    def unscale(self, model_grads, master_grads, unused_scale, models_are_masters=False, scale_override=None):
+        if self._has_overflow:
+            return
+        scale = self._loss_scale if scale_override is None else scale_override
+        if scale == 1.0 and models_are_masters and not self.dynamic:
+            return
+        if not model_grads:
+            return
+        self._warn_non_fp32(master_grads)
+        # group by (model dtype, master dtype): each list passed to the kernel is single-dtype
+        groups = {}
+        for m, s in zip(model_grads, master_grads):
+            groups.setdefault((m.dtype, s.dtype), ([], []))
+            groups[(m.dtype, s.dtype)][0].append(m)
+            groups[(m.dtype, s.dtype)][1].append(s)
+        flag = self._flag_for(model_grads)
+        for ins, outs in groups.values():
+            multi_tensor_applier(LossScaler.multi_tensor_scale_cuda, flag, [ins, outs], 1.0 / scale)
+
+    def unscale_with_stashed(self, model_grads, stashed_master_grads, master_grads, scale_override=None):
+        if self._has_overflow:
+            return
+        grads_have_scale, stashed_have_scale, out_scale = self._loss_scale, 1.0, 1.0
+        if scale_override is not None:
+            grads_have_scale, stashed_have_scale, out_scale = scale_override
+        if not model_grads:
+            return
+        self._warn_non_fp32(master_grads)
+        groups = {}
+        for m, st, out in zip(model_grads, stashed_master_grads, master_grads):
+            key = (m.dtype, st.dtype, out.dtype)
+            groups.setdefault(key, ([], [], []))
+            for lst, t in zip(groups[key], (m, st, out)):
+                lst.append(t)
+        flag = self._flag_for(model_grads)
+        for lists in groups.values():
+            multi_tensor_applier(LossScaler.multi_tensor_axpby_cuda, flag, list(lists),
+                                 out_scale / grads_have_scale, out_scale / stashed_have_scale, 0)
+
+    def clear_overflow_state(self):
+        self._has_overflow = False
+        self._overflow_buf.zero_()
+
+    def update_scale(self):
+        if self.dynamic and not self._has_overflow:
+            self._has_overflow = bool(self._overflow_buf.item())
+        if self._has_overflow and self.dynamic:
+            should_skip = True
+            if self._min_loss_scale:
+                self._loss_scale = max(self._min_loss_scale, self._loss_scale / self._scale_factor)
+            else:
+                self._loss_scale = self._loss_scale / self._scale_factor
+            self._unskipped = 0
+        else:
+            should_skip = False
+            self._unskipped += 1
+        if self._unskipped == self._scale_seq_len and self.dynamic:
+            self._loss_scale = min(self._max_loss_scale, self._loss_scale * self._scale_factor)
+            self._unskipped = 0
+        return should_skip

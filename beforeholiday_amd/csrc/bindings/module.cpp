@@ -7,4 +7,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "beforeholiday_amd native kernels (HIP, gfx950)";
   m.attr("arch") = "gfx950";
   bhb::register_amp_C(m);
+  bhb::register_syncbn(m);
 }

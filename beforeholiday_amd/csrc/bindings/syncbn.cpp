@@ -1,0 +1,254 @@
+// `syncbn` front-end: fused BN statistics / normalisation / backward for SyncBatchNorm.
+// Kernels: kernels/batchnorm.hip. Reference API: csrc/syncbn.cpp:98-109 (compat wrappers for those
+// names live in python: beforeholiday_amd/ops/syncbn.py).
+#include "common.h"
+
+#include "bh/bn_api.h"
+
+namespace bhb {
+namespace {
+
+struct Layout {
+  bh::BNShape s;
+  at::Tensor x;  // possibly re-laid-out input
+};
+
+bool aligned16(const at::Tensor& t) { return reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0; }
+
+Layout layout_of(const at::Tensor& x_in) {
+  TORCH_CHECK(x_in.dim() >= 2, "batchnorm expects at least 2 dims (N, C, ...)");
+  Layout L;
+  at::Tensor x = x_in;
+  const int64_t N = x.size(0);
+  const int64_t C = x.size(1);
+  int64_t inner = 1;
+  for (int d = 2; d < x.dim(); ++d) inner *= x.size(d);
+  bool cl = false;
+  if (inner == 1) {
+    if (!x.is_contiguous()) x = x.contiguous();
+    cl = (C % 8 == 0) && aligned16(x);
+  } else if (x.is_contiguous()) {
+    cl = false;
+  } else if ((x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast)) ||
+             (x.dim() == 5 && x.is_contiguous(at::MemoryFormat::ChannelsLast3d))) {
+    cl = (C % 8 == 0) && aligned16(x);
+    if (!cl) x = x.contiguous();
+  } else {
+    x = x.contiguous();
+  }
+  if (!cl && !aligned16(x)) x = x.clone();
+  L.x = x;
+  L.s.C = (int)C;
+  L.s.channels_last = cl;
+  if (cl) {
+    L.s.outer = N * inner;
+    L.s.inner = 1;
+  } else {
+    L.s.outer = N;
+    L.s.inner = inner;
+  }
+  return L;
+}
+
+// bring `t` into exactly the layout of the (re-laid-out) reference input
+at::Tensor like(const at::Tensor& t, const at::Tensor& ref) {
+  if (t.strides() == ref.strides() && aligned16(t)) return t;
+  at::Tensor o = at::empty_like(ref, t.options());
+  o.copy_(t);
+  return o;
+}
+
+int wcode(const c10::optional<at::Tensor>& w) { return (w.has_value() && w->defined()) ? dtype_code(w->scalar_type()) : bh::kF32; }
+const void* wptr(const c10::optional<at::Tensor>& w) { return (w.has_value() && w->defined()) ? w->data_ptr() : nullptr; }
+void* wptr_mut(const c10::optional<at::Tensor>& w) { return (w.has_value() && w->defined()) ? w->data_ptr() : nullptr; }
+
+at::TensorOptions fopt(const at::Tensor& x) { return x.options().dtype(at::kFloat).memory_format(at::MemoryFormat::Contiguous); }
+
+// local stats -> [mean(C), var_biased(C), count(1)] (the all_gather payload)
+at::Tensor stats_local(at::Tensor x_in) {
+  check_cuda(x_in, "input");
+  Layout L = layout_of(x_in);
+  const int C = L.s.C;
+  const int splits = bh::bn_num_splits(L.s);
+  auto part = at::empty({3 * (int64_t)splits * C + splits}, fopt(L.x));
+  float* pm = part.data_ptr<float>();
+  float* pm2 = pm + (int64_t)splits * C;
+  float* pn = pm2 + (int64_t)splits * C;
+  auto out = at::empty({2 * (int64_t)C + 1}, fopt(L.x));
+  hipStream_t st = stream_for(L.x);
+  bh::bn_stats(L.s, dtype_code(L.x.scalar_type()), L.x.data_ptr(), splits, pm, pm2, pn, st);
+  bh::BNFinal fin{};
+  bh::bn_stats_finalize(L.s, splits, pm, pm2, pn, out.data_ptr<float>(), fin, bh::kF32, nullptr, nullptr, nullptr,
+                        nullptr, st);
+  return out;
+}
+
+// returns (mean, invstd, scale, shift, count)
+std::vector<at::Tensor> final_outputs(const at::Tensor& ref, int64_t C) {
+  auto o = fopt(ref);
+  return {at::empty({C}, o), at::empty({C}, o), at::empty({C}, o), at::empty({C}, o), at::empty({1}, o)};
+}
+bh::BNFinal fin_of(std::vector<at::Tensor>& r, double eps, double momentum) {
+  bh::BNFinal f{};
+  f.mean = r[0].data_ptr<float>();
+  f.invstd = r[1].data_ptr<float>();
+  f.scale = r[2].data_ptr<float>();
+  f.shift = r[3].data_ptr<float>();
+  f.count = r[4].data_ptr<float>();
+  f.eps = (float)eps;
+  f.momentum = (float)momentum;
+  return f;
+}
+
+void check_running(const c10::optional<at::Tensor>& rm, const c10::optional<at::Tensor>& rv,
+                   const c10::optional<at::Tensor>& w) {
+  if (rm.has_value() && rm->defined()) {
+    TORCH_CHECK(rv.has_value() && rv->defined(), "running_var required with running_mean");
+    TORCH_CHECK(rm->is_contiguous() && rv->is_contiguous(), "running stats must be contiguous");
+    if (w.has_value() && w->defined())
+      TORCH_CHECK(rm->scalar_type() == w->scalar_type() && rv->scalar_type() == w->scalar_type(),
+                  "running stats must share the weight dtype");
+  }
+}
+
+// single-rank fused statistics (no all_gather needed)
+std::vector<at::Tensor> stats_single(at::Tensor x_in, c10::optional<at::Tensor> w, c10::optional<at::Tensor> b,
+                                     c10::optional<at::Tensor> rmean, c10::optional<at::Tensor> rvar,
+                                     double momentum, double eps) {
+  check_cuda(x_in, "input");
+  check_running(rmean, rvar, w);
+  Layout L = layout_of(x_in);
+  const int C = L.s.C;
+  const int splits = bh::bn_num_splits(L.s);
+  const int64_t nslots = L.s.channels_last ? splits : (int64_t)splits * C;
+  auto part = at::empty({2 * (int64_t)splits * C + nslots}, fopt(L.x));
+  float* pm = part.data_ptr<float>();
+  float* pm2 = pm + (int64_t)splits * C;
+  float* pn = pm2 + (int64_t)splits * C;
+  auto r = final_outputs(L.x, C);
+  auto fin = fin_of(r, eps, momentum);
+  hipStream_t st = stream_for(L.x);
+  bh::bn_stats(L.s, dtype_code(L.x.scalar_type()), L.x.data_ptr(), splits, pm, pm2, pn, st);
+  const bool has_run = rmean.has_value() && rmean->defined();
+  int dtw = wcode(w);
+  if (!(w.has_value() && w->defined()) && has_run) dtw = dtype_code(rmean->scalar_type());
+  bh::bn_stats_finalize(L.s, splits, pm, pm2, pn, nullptr, fin, dtw, wptr(w), wptr(b),
+                        has_run ? rmean->data_ptr() : nullptr, has_run ? rvar->data_ptr() : nullptr, st);
+  return r;
+}
+
+// merge gathered [W, 2C+1] rows (+ running stats update)
+std::vector<at::Tensor> merge_ranks(at::Tensor gathered, c10::optional<at::Tensor> w, c10::optional<at::Tensor> b,
+                                    c10::optional<at::Tensor> rmean, c10::optional<at::Tensor> rvar, double momentum,
+                                    double eps) {
+  check_cuda(gathered, "gathered");
+  TORCH_CHECK(gathered.dim() == 2 && gathered.scalar_type() == at::kFloat, "gathered must be [W, 2C+1] fp32");
+  gathered = gathered.contiguous();
+  check_running(rmean, rvar, w);
+  const int W = (int)gathered.size(0);
+  const int C = (int)((gathered.size(1) - 1) / 2);
+  auto r = final_outputs(gathered, C);
+  auto fin = fin_of(r, eps, momentum);
+  const bool has_run = rmean.has_value() && rmean->defined();
+  int dtw = wcode(w);
+  if (!(w.has_value() && w->defined()) && has_run) dtw = dtype_code(rmean->scalar_type());
+  bh::bn_merge_ranks(W, C, gathered.data_ptr<float>(), fin, dtw, wptr(w), wptr(b),
+                     has_run ? rmean->data_ptr() : nullptr, has_run ? rvar->data_ptr() : nullptr, nullptr,
+                     stream_for(gathered));
+  return r;
+}
+
+at::Tensor forward(at::Tensor x_in, c10::optional<at::Tensor> z, at::Tensor scale, at::Tensor shift, bool relu,
+                   c10::optional<at::ScalarType> out_dtype) {
+  check_cuda(x_in, "input");
+  Layout L = layout_of(x_in);
+  at::Tensor zt;
+  if (z.has_value() && z->defined()) zt = like(*z, L.x);
+  auto y = at::empty_like(L.x, L.x.options().dtype(out_dtype.value_or(L.x.scalar_type())));
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && shift.scalar_type() == at::kFloat && scale.numel() == L.s.C,
+              "scale/shift must be fp32 [C]");
+  bh::bn_forward(L.s, dtype_code(L.x.scalar_type()), L.x.data_ptr(), zt.defined() ? dtype_code(zt.scalar_type()) : -1,
+                 zt.defined() ? zt.data_ptr() : nullptr, dtype_code(y.scalar_type()), y.data_ptr(),
+                 scale.contiguous().data_ptr<float>(), shift.contiguous().data_ptr<float>(), relu, stream_for(L.x));
+  return y;
+}
+
+// returns (sums[2C], grad_weight, grad_bias) -- grads in weight dtype (undefined if weight undefined)
+std::vector<at::Tensor> backward_reduce(at::Tensor dy_in, at::Tensor x_in, c10::optional<at::Tensor> z,
+                                        at::Tensor mean, at::Tensor invstd, c10::optional<at::Tensor> scale,
+                                        c10::optional<at::Tensor> shift, bool relu, c10::optional<at::Tensor> weight,
+                                        bool need_weight_grads) {
+  check_cuda(x_in, "input");
+  Layout L = layout_of(x_in);
+  at::Tensor dy = like(dy_in, L.x);
+  at::Tensor zt;
+  if (relu && z.has_value() && z->defined()) zt = like(*z, L.x);
+  if (relu) TORCH_CHECK(scale.has_value() && shift.has_value(), "relu recompute needs scale/shift");
+  const int C = L.s.C;
+  const int splits = bh::bn_num_splits(L.s);
+  auto part = at::empty({2 * (int64_t)splits * C}, fopt(L.x));
+  auto sums = at::empty({2 * (int64_t)C}, fopt(L.x));
+  at::Tensor gw, gb;
+  const bool wdef = weight.has_value() && weight->defined();
+  if (need_weight_grads && wdef) {
+    gw = at::empty_like(*weight, at::MemoryFormat::Contiguous);
+    gb = at::empty_like(*weight, at::MemoryFormat::Contiguous);
+  }
+  hipStream_t st = stream_for(L.x);
+  bh::bn_backward_reduce(L.s, dtype_code(L.x.scalar_type()), dy.data_ptr(), L.x.data_ptr(),
+                         zt.defined() ? dtype_code(zt.scalar_type()) : -1, zt.defined() ? zt.data_ptr() : nullptr,
+                         mean.data_ptr<float>(), relu ? scale->data_ptr<float>() : nullptr,
+                         relu ? shift->data_ptr<float>() : nullptr, relu, splits, part.data_ptr<float>(),
+                         part.data_ptr<float>() + (int64_t)splits * C, st);
+  bh::bn_backward_reduce_finalize(C, splits, part.data_ptr<float>(), part.data_ptr<float>() + (int64_t)splits * C,
+                                  invstd.data_ptr<float>(), sums.data_ptr<float>(),
+                                  gw.defined() ? dtype_code(gw.scalar_type()) : bh::kF32,
+                                  gw.defined() ? gw.data_ptr() : nullptr, gb.defined() ? gb.data_ptr() : nullptr, st);
+  return {sums, gw, gb};
+}
+
+// returns (dx, dz) ; dz undefined unless need_dz
+std::vector<at::Tensor> backward_dgrad(at::Tensor dy_in, at::Tensor x_in, c10::optional<at::Tensor> z,
+                                       at::Tensor mean, at::Tensor invstd, c10::optional<at::Tensor> weight,
+                                       at::Tensor sums, at::Tensor count, c10::optional<at::Tensor> scale,
+                                       c10::optional<at::Tensor> shift, bool relu, bool need_dz) {
+  check_cuda(x_in, "input");
+  Layout L = layout_of(x_in);
+  at::Tensor dy = like(dy_in, L.x);
+  at::Tensor zt;
+  if (z.has_value() && z->defined()) zt = like(*z, L.x);
+  if (relu) TORCH_CHECK(scale.has_value() && shift.has_value(), "relu recompute needs scale/shift");
+  TORCH_CHECK(count.scalar_type() == at::kFloat && count.numel() >= 1, "count must be fp32");
+  auto dx = at::empty_like(L.x);
+  at::Tensor dz;
+  if (need_dz) dz = at::empty_like(zt.defined() ? zt : L.x);
+  bh::bn_backward_dgrad(L.s, dtype_code(L.x.scalar_type()), dy.data_ptr(), L.x.data_ptr(),
+                        zt.defined() ? dtype_code(zt.scalar_type()) : (dz.defined() ? dtype_code(dz.scalar_type()) : -1),
+                        zt.defined() ? zt.data_ptr() : nullptr, mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                        wcode(weight), wptr(weight), sums.data_ptr<float>(), count.data_ptr<float>(),
+                        relu ? scale->data_ptr<float>() : nullptr, relu ? shift->data_ptr<float>() : nullptr, relu,
+                        dx.data_ptr(), dz.defined() ? dz.data_ptr() : nullptr, stream_for(L.x));
+  return {dx, dz};
+}
+
+}  // namespace
+
+void register_syncbn(pybind11::module_& root) {
+  namespace py = pybind11;
+  auto m = root.def_submodule("syncbn", "batch-norm statistics / normalisation kernels (gfx950)");
+  m.def("stats_local", &stats_local, "local [mean, var_biased, count] of x (all_gather payload)");
+  m.def("stats_single", &stats_single, py::arg("x"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"),
+        py::arg("running_var"), py::arg("momentum"), py::arg("eps"));
+  m.def("merge_ranks", &merge_ranks, py::arg("gathered"), py::arg("weight"), py::arg("bias"),
+        py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"));
+  m.def("forward", &forward, py::arg("x"), py::arg("z"), py::arg("scale"), py::arg("shift"), py::arg("relu"),
+        py::arg("out_dtype") = py::none());
+  m.def("backward_reduce", &backward_reduce, py::arg("dy"), py::arg("x"), py::arg("z"), py::arg("mean"),
+        py::arg("invstd"), py::arg("scale"), py::arg("shift"), py::arg("relu"), py::arg("weight"),
+        py::arg("need_weight_grads"));
+  m.def("backward_dgrad", &backward_dgrad, py::arg("dy"), py::arg("x"), py::arg("z"), py::arg("mean"),
+        py::arg("invstd"), py::arg("weight"), py::arg("sums"), py::arg("count"), py::arg("scale"), py::arg("shift"),
+        py::arg("relu"), py::arg("need_dz"));
+}
+
+}  // namespace bhb

@@ -1,0 +1,696 @@
+// Batch-norm / SyncBatchNorm kernels for gfx950 (the `syncbn` extension equivalent).
+//
+// Reference behaviour: csrc/welford.cu (welford_kernel :272, welford_kernel_c_last :453,
+// welford_kernel_parallel :597, batchnorm_forward(_c_last) :314/:633, reduce_bn(_c_last)
+// :344/:739, batchnorm_backward(_c_last) :411/:895, relu_backward_c_last :686).
+//
+// MI355X design:
+//  * every reduction is two-level and deterministic: a big streaming kernel writes per-(split,
+//    channel) partials, a tiny finalize kernel merges them (no grid semaphores / atomics, no
+//    reliance on block scheduling -- the reference's c_last kernels spin on a global semaphore).
+//  * channels_last: a thread owns 8 consecutive channels (one 16-byte load of fp16/bf16), the
+//    Welford update shares 1/n across the 8 channels (one v_rcp per 8 elements).
+//  * the forward normalisation is a single FMA per element: the finalize/merge kernel emits
+//    per-channel (scale, shift) = (w*invstd, b - mean*w*invstd) and updates running stats.
+//  * fused residual-add + ReLU in the forward, and the ReLU mask is *recomputed* from x (and z) in
+//    the backward reduce and dgrad kernels instead of materialising a masked dy (reference:
+//    relu_bw_c_last writes a full extra tensor).
+#include "bh/api.h"
+#include "bh/device.h"
+#include "bh/bn_api.h"
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+
+namespace bh {
+namespace {
+
+constexpr int kBlock = 256;
+
+#define BN_DISPATCH(code, T, ...)                                         \
+  switch (code) {                                                         \
+    case kF32: { using T = float; __VA_ARGS__; } break;                   \
+    case kF16: { using T = f16; __VA_ARGS__; } break;                     \
+    case kBF16: { using T = bf16; __VA_ARGS__; } break;                   \
+    case kF64: { using T = double; __VA_ARGS__; } break;                  \
+    default: throw std::runtime_error("batchnorm: unsupported dtype " + std::to_string(code)); \
+  }
+
+inline void check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <typename T> BH_DEVICE float ld(const T* p, int64_t i) { return to_f<T>(p[i]); }
+template <typename T> BH_DEVICE float ld_or(const T* p, int64_t i, float d) { return p ? to_f<T>(p[i]) : d; }
+
+// per-thread Welford state for 8 channels sharing one count
+struct W8 {
+  float n;
+  float mean[8];
+  float m2[8];
+};
+
+// ------------------------------------------------------------------------------------------
+// NHWC statistics: grid (channel tiles, splits). Thread t: channel vector v = t % cvb,
+// row lane r = t / cvb (R = blockDim/cvb lanes, a power of two).
+// Partials: mean[s][C], m2[s][C], n[s].
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_stats_nhwc(const T* __restrict__ x, int64_t M, int C, int cvb, int R,
+                                                       int64_t rows_per_split, float* __restrict__ pmean,
+                                                       float* __restrict__ pm2, float* __restrict__ pn) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  const int v = tid % cvb;
+  const int r = tid / cvb;
+  const int c0 = (blockIdx.x * cvb + v) * 8;
+  const int split = blockIdx.y;
+  const int64_t row0 = (int64_t)split * rows_per_split;
+  const int64_t row1 = min(M, row0 + rows_per_split);
+  const bool active = (r < R) && (c0 < C);
+  const bool vec = ((C & 7) == 0);
+
+  float n = 0.f, mean[8], m2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) mean[k] = m2[k] = 0.f;
+  if (active) {
+    for (int64_t row = row0 + r; row < row1; row += R) {
+      float xv[8];
+      const T* p = x + row * C + c0;
+      if (vec) {
+        VecIO<T>::load(p, xv);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) xv[k] = (c0 + k < C) ? to_f<T>(p[k]) : 0.f;
+      }
+      n += 1.f;
+      const float inv = __frcp_rn(n);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float d = xv[k] - mean[k];
+        mean[k] = fmaf(d, inv, mean[k]);
+        m2[k] = fmaf(d, xv[k] - mean[k], m2[k]);
+      }
+    }
+  }
+  // tree-merge the R row lanes through LDS: layout [R][cvb*8] for mean and m2, counts [R]
+  float* s_mean = smem;
+  float* s_m2 = smem + R * cvb * 8;
+  float* s_n = smem + 2 * R * cvb * 8;
+  if (r < R) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s_mean[(r * cvb + v) * 8 + k] = mean[k];
+      s_m2[(r * cvb + v) * 8 + k] = m2[k];
+    }
+    if (v == 0) s_n[r] = n;
+  }
+  __syncthreads();
+  for (int s = R / 2; s > 0; s >>= 1) {
+    if (r < s) {
+      const float na = s_n[r], nb = s_n[r + s];
+      const float nt = na + nb;
+      const float wb = nt > 0.f ? nb / nt : 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int ia = (r * cvb + v) * 8 + k, ib = ((r + s) * cvb + v) * 8 + k;
+        const float d = s_mean[ib] - s_mean[ia];
+        s_mean[ia] = s_mean[ia] + d * wb;
+        s_m2[ia] = s_m2[ia] + s_m2[ib] + d * d * na * wb;
+      }
+    }
+    __syncthreads();
+    if (r < s && v == 0) s_n[r] = s_n[r] + s_n[r + s];
+    __syncthreads();
+  }
+  if (r == 0 && c0 < C) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (c0 + k < C) {
+        pmean[(int64_t)split * C + c0 + k] = s_mean[v * 8 + k];
+        pm2[(int64_t)split * C + c0 + k] = s_m2[v * 8 + k];
+      }
+    }
+    if (blockIdx.x == 0 && v == 0) pn[split] = s_n[0];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// NCHW statistics: grid (C, splits); a block reduces channel c over its slab of the flattened
+// (n, hw) index space. Partials pmean[s][C], pm2[s][C], pn[s][C] (counts may differ per channel
+// slab only at tails; stored per channel for simplicity).
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_stats_nchw(const T* __restrict__ x, int64_t N, int C, int64_t HW,
+                                                       int64_t per_split, float* __restrict__ pmean,
+                                                       float* __restrict__ pm2, float* __restrict__ pn) {
+  __shared__ float red[3 * (kBlock / kWave)];
+  const int c = blockIdx.x;
+  const int split = blockIdx.y;
+  const int64_t total = N * HW;
+  const int64_t f0 = (int64_t)split * per_split;
+  const int64_t f1 = min(total, f0 + per_split);
+  Welford w{0.f, 0.f, 0.f};
+  const bool vec = (HW % 8 == 0) && (f0 % 8 == 0);
+  if (vec) {
+    for (int64_t f = f0 + (int64_t)threadIdx.x * 8; f < f1; f += (int64_t)kBlock * 8) {
+      const int64_t nidx = f / HW, hw = f - nidx * HW;
+      float xv[8];
+      VecIO<T>::load(x + (nidx * C + c) * HW + hw, xv);
+      const int cnt = (int)min((int64_t)8, f1 - f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (k < cnt) {
+          w.n += 1.f;
+          const float d = xv[k] - w.mean;
+          w.mean += d / w.n;
+          w.m2 = fmaf(d, xv[k] - w.mean, w.m2);
+        }
+      }
+    }
+  } else {
+    for (int64_t f = f0 + threadIdx.x; f < f1; f += kBlock) {
+      const int64_t nidx = f / HW, hw = f - nidx * HW;
+      const float xv = to_f<T>(x[(nidx * C + c) * HW + hw]);
+      w.n += 1.f;
+      const float d = xv - w.mean;
+      w.mean += d / w.n;
+      w.m2 = fmaf(d, xv - w.mean, w.m2);
+    }
+  }
+  w = block_welford(w, red);
+  if (threadIdx.x == 0) {
+    pmean[(int64_t)split * C + c] = w.mean;
+    pm2[(int64_t)split * C + c] = w.m2;
+    pn[(int64_t)split * C + c] = w.n;
+  }
+}
+
+// merge split partials -> local (mean, biased var, count); optionally also the "merge ranks"
+// work for a single rank (running stats, invstd, scale/shift) to save a launch.
+template <typename Tw>
+__global__ __launch_bounds__(kBlock) void k_stats_finalize(int C, int splits, bool per_channel_n,
+                                                           const float* __restrict__ pmean, const float* __restrict__ pm2,
+                                                           const float* __restrict__ pn, float* __restrict__ out_local,
+                                                           BNFinal fin, const Tw* w, const Tw* b, Tw* rmean, Tw* rvar) {
+  const int c = blockIdx.x * kBlock + threadIdx.x;
+  if (c >= C) return;
+  Welford acc{0.f, 0.f, 0.f};
+  for (int s = 0; s < splits; ++s) {
+    const float n = per_channel_n ? pn[(int64_t)s * C + c] : pn[s];
+    acc = welford_merge(acc, Welford{n, pmean[(int64_t)s * C + c], pm2[(int64_t)s * C + c]});
+  }
+  const float var_b = acc.n > 0.f ? acc.m2 / acc.n : 0.f;
+  if (out_local) {
+    // all_gather layout of the reference: [mean(C), var_biased(C), count(1)]
+    out_local[c] = acc.mean;
+    out_local[C + c] = var_b;
+    if (c == 0) out_local[2 * C] = acc.n;
+  }
+  if (fin.mean) {
+    const float invstd = rsqrtf(var_b + fin.eps);
+    fin.mean[c] = acc.mean;
+    fin.invstd[c] = invstd;
+    if (fin.count) if (c == 0) fin.count[0] = acc.n;
+    const float wv = w ? to_f<Tw>(w[c]) : 1.f;
+    const float bv = b ? to_f<Tw>(b[c]) : 0.f;
+    fin.scale[c] = wv * invstd;
+    fin.shift[c] = bv - acc.mean * wv * invstd;
+    if (rmean) {
+      const float unb = acc.n > 1.f ? acc.m2 / (acc.n - 1.f) : var_b;
+      rmean[c] = from_f<Tw>((1.f - fin.momentum) * to_f<Tw>(rmean[c]) + fin.momentum * acc.mean);
+      rvar[c] = from_f<Tw>((1.f - fin.momentum) * to_f<Tw>(rvar[c]) + fin.momentum * unb);
+    }
+  }
+}
+
+// merge W ranks' [mean(C), var_b(C), count(1)] rows (reference welford_kernel_parallel :597)
+template <typename Tw>
+__global__ __launch_bounds__(kBlock) void k_merge_ranks(int W, int C, const float* __restrict__ g, BNFinal fin,
+                                                        const Tw* w, const Tw* b, Tw* rmean, Tw* rvar,
+                                                        float* var_unbiased) {
+  const int c = blockIdx.x * kBlock + threadIdx.x;
+  if (c >= C) return;
+  Welford acc{0.f, 0.f, 0.f};
+  const int stride = 2 * C + 1;
+  for (int r = 0; r < W; ++r) {
+    const float n = g[(int64_t)r * stride + 2 * C];
+    const float m = g[(int64_t)r * stride + c];
+    const float vb = g[(int64_t)r * stride + C + c];
+    acc = welford_merge(acc, Welford{n, m, vb * n});
+  }
+  const float var_b = acc.n > 0.f ? acc.m2 / acc.n : 0.f;
+  const float unb = acc.n > 1.f ? acc.m2 / (acc.n - 1.f) : var_b;
+  const float invstd = rsqrtf(var_b + fin.eps);
+  fin.mean[c] = acc.mean;
+  fin.invstd[c] = invstd;
+  if (fin.count && c == 0) fin.count[0] = acc.n;
+  if (var_unbiased) var_unbiased[c] = unb;
+  if (fin.scale) {
+    const float wv = w ? to_f<Tw>(w[c]) : 1.f;
+    const float bv = b ? to_f<Tw>(b[c]) : 0.f;
+    fin.scale[c] = wv * invstd;
+    fin.shift[c] = bv - acc.mean * wv * invstd;
+  }
+  if (rmean) {
+    rmean[c] = from_f<Tw>((1.f - fin.momentum) * to_f<Tw>(rmean[c]) + fin.momentum * acc.mean);
+    rvar[c] = from_f<Tw>((1.f - fin.momentum) * to_f<Tw>(rvar[c]) + fin.momentum * unb);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// forward: y = x*scale[c] + shift[c] (+ z) (relu)
+// ------------------------------------------------------------------------------------------
+template <typename T, typename Tz, typename Ty>
+__global__ __launch_bounds__(kBlock) void k_fwd_nhwc(const T* __restrict__ x, const Tz* __restrict__ z,
+                                                     Ty* __restrict__ y, const float* __restrict__ scale,
+                                                     const float* __restrict__ shift, int64_t M, int C, bool relu) {
+  const int64_t nvec = M * (C / 8);
+  const int cv = C / 8;
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * kBlock) {
+    const int c0 = (int)(i % cv) * 8;
+    float xv[8], sc[8], sh[8];
+    VecIO<T>::load(x + i * 8, xv);
+    VecIO<float>::load(scale + c0, sc);
+    VecIO<float>::load(shift + c0, sh);
+    float zv[8];
+    if (z) VecIO<Tz>::load(z + i * 8, zv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float o = fmaf(xv[k], sc[k], sh[k]);
+      if (z) o += zv[k];
+      if (relu) o = fmaxf(o, 0.f);
+      xv[k] = o;
+    }
+    VecIO<Ty>::store(y + i * 8, xv);
+  }
+}
+
+// generic (NCHW or unaligned NHWC): element i -> channel (i / inner) % C
+template <typename T, typename Tz, typename Ty>
+__global__ __launch_bounds__(kBlock) void k_fwd_generic(const T* __restrict__ x, const Tz* __restrict__ z,
+                                                        Ty* __restrict__ y, const float* __restrict__ scale,
+                                                        const float* __restrict__ shift, int64_t total, int C,
+                                                        int64_t inner, bool relu) {
+  const bool vec = (inner % 8 == 0);
+  if (vec) {
+    for (int64_t i = (blockIdx.x * (int64_t)kBlock + threadIdx.x) * 8; i < total; i += (int64_t)gridDim.x * kBlock * 8) {
+      const int c = (int)((i / inner) % C);
+      float xv[8], zv[8];
+      VecIO<T>::load(x + i, xv);
+      if (z) VecIO<Tz>::load(z + i, zv);
+      const float sc = scale[c], sh = shift[c];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float o = fmaf(xv[k], sc, sh);
+        if (z) o += zv[k];
+        if (relu) o = fmaxf(o, 0.f);
+        xv[k] = o;
+      }
+      VecIO<Ty>::store(y + i, xv);
+    }
+  } else {
+    for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < total; i += (int64_t)gridDim.x * kBlock) {
+      const int c = (int)((i / inner) % C);
+      float o = fmaf(to_f<T>(x[i]), scale[c], shift[c]);
+      if (z) o += to_f<Tz>(z[i]);
+      if (relu) o = fmaxf(o, 0.f);
+      y[i] = from_f<Ty>(o);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// backward reduce: per channel sum(dy'), sum(dy' * (x - mean)) with dy' = relu-masked dy
+// (mask recomputed as x*scale+shift(+z) > 0). Partials [splits][C] each.
+// ------------------------------------------------------------------------------------------
+template <typename T, typename Tz>
+__global__ __launch_bounds__(kBlock) void k_bwd_reduce_nhwc(const T* __restrict__ dy, const T* __restrict__ x,
+                                                            const Tz* __restrict__ z, const float* __restrict__ mean,
+                                                            const float* __restrict__ scale, const float* __restrict__ shift,
+                                                            bool relu, int64_t M, int C, int cvb, int R,
+                                                            int64_t rows_per_split, float* __restrict__ p_dy,
+                                                            float* __restrict__ p_dyx) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  const int v = tid % cvb;
+  const int r = tid / cvb;
+  const int c0 = (blockIdx.x * cvb + v) * 8;
+  const int split = blockIdx.y;
+  const int64_t row0 = (int64_t)split * rows_per_split;
+  const int64_t row1 = min(M, row0 + rows_per_split);
+  const bool active = (r < R) && (c0 < C);
+  float sdy[8], sdx[8], mu[8], sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sdy[k] = sdx[k] = 0.f;
+  if (active) {
+    VecIO<float>::load(mean + c0, mu);
+    if (relu) {
+      VecIO<float>::load(scale + c0, sc);
+      VecIO<float>::load(shift + c0, sh);
+    }
+    for (int64_t row = row0 + r; row < row1; row += R) {
+      float g[8], xv[8];
+      VecIO<T>::load(dy + row * C + c0, g);
+      VecIO<T>::load(x + row * C + c0, xv);
+      if (relu) {
+        float zv[8];
+        if (z) VecIO<Tz>::load(z + row * C + c0, zv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float o = fmaf(xv[k], sc[k], sh[k]);
+          if (z) o += zv[k];
+          if (o <= 0.f) g[k] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        sdy[k] += g[k];
+        sdx[k] = fmaf(g[k], xv[k] - mu[k], sdx[k]);
+      }
+    }
+  }
+  float* s_a = smem;
+  float* s_b = smem + R * cvb * 8;
+  if (r < R) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s_a[(r * cvb + v) * 8 + k] = sdy[k];
+      s_b[(r * cvb + v) * 8 + k] = sdx[k];
+    }
+  }
+  __syncthreads();
+  for (int s = R / 2; s > 0; s >>= 1) {
+    if (r < s) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s_a[(r * cvb + v) * 8 + k] += s_a[((r + s) * cvb + v) * 8 + k];
+        s_b[(r * cvb + v) * 8 + k] += s_b[((r + s) * cvb + v) * 8 + k];
+      }
+    }
+    __syncthreads();
+  }
+  if (r == 0 && c0 < C) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (c0 + k < C) {
+        p_dy[(int64_t)split * C + c0 + k] = s_a[v * 8 + k];
+        p_dyx[(int64_t)split * C + c0 + k] = s_b[v * 8 + k];
+      }
+    }
+  }
+}
+
+template <typename T, typename Tz>
+__global__ __launch_bounds__(kBlock) void k_bwd_reduce_generic(const T* __restrict__ dy, const T* __restrict__ x,
+                                                               const Tz* __restrict__ z, const float* __restrict__ mean,
+                                                               const float* __restrict__ scale,
+                                                               const float* __restrict__ shift, bool relu, int64_t N,
+                                                               int C, int64_t HW, int64_t per_split,
+                                                               float* __restrict__ p_dy, float* __restrict__ p_dyx) {
+  __shared__ float red[kBlock / kWave];
+  const int c = blockIdx.x;
+  const int split = blockIdx.y;
+  const int64_t total = N * HW;
+  const int64_t f0 = (int64_t)split * per_split;
+  const int64_t f1 = min(total, f0 + per_split);
+  const float mu = mean[c];
+  const float sc = relu ? scale[c] : 0.f, sh = relu ? shift[c] : 0.f;
+  float a = 0.f, bsum = 0.f;
+  for (int64_t f = f0 + threadIdx.x; f < f1; f += kBlock) {
+    const int64_t nidx = f / HW, hw = f - nidx * HW;
+    const int64_t off = (nidx * C + c) * HW + hw;
+    float g = to_f<T>(dy[off]);
+    const float xv = to_f<T>(x[off]);
+    if (relu) {
+      float o = fmaf(xv, sc, sh);
+      if (z) o += to_f<Tz>(z[off]);
+      if (o <= 0.f) g = 0.f;
+    }
+    a += g;
+    bsum = fmaf(g, xv - mu, bsum);
+  }
+  const float ta = block_sum(a, red);
+  const float tb = block_sum(bsum, red);
+  if (threadIdx.x == 0) {
+    p_dy[(int64_t)split * C + c] = ta;
+    p_dyx[(int64_t)split * C + c] = tb;
+  }
+}
+
+// sum partials; grad_weight = sum_dy_xmu * invstd, grad_bias = sum_dy (local, pre-all-reduce)
+template <typename Tw>
+__global__ __launch_bounds__(kBlock) void k_bwd_reduce_finalize(int C, int splits, const float* __restrict__ p_dy,
+                                                                const float* __restrict__ p_dyx,
+                                                                const float* __restrict__ invstd,
+                                                                float* __restrict__ sums, Tw* gw, Tw* gb) {
+  const int c = blockIdx.x * kBlock + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f, b = 0.f;
+  for (int s = 0; s < splits; ++s) {
+    a += p_dy[(int64_t)s * C + c];
+    b += p_dyx[(int64_t)s * C + c];
+  }
+  sums[c] = a;
+  sums[C + c] = b;
+  if (gw) gw[c] = from_f<Tw>(b * invstd[c]);
+  if (gb) gb[c] = from_f<Tw>(a);
+}
+
+// ------------------------------------------------------------------------------------------
+// dgrad: dx = (dy' - sum_dy/N - (x-mean)*invstd^2*sum_dy_xmu/N) * invstd * w ; dz = dy'
+// ------------------------------------------------------------------------------------------
+template <typename T, typename Tz, typename Tw>
+__global__ __launch_bounds__(kBlock) void k_dgrad_nhwc(const T* __restrict__ dy, const T* __restrict__ x,
+                                                       const Tz* __restrict__ z, const float* __restrict__ mean,
+                                                       const float* __restrict__ invstd, const Tw* __restrict__ w,
+                                                       const float* __restrict__ sums, const float* __restrict__ count,
+                                                       const float* __restrict__ scale, const float* __restrict__ shift,
+                                                       bool relu, T* __restrict__ dx, Tz* __restrict__ dz, int64_t M,
+                                                       int C) {
+  const int cv = C / 8;
+  const int64_t nvec = M * cv;
+  const float inv_n = 1.f / count[0];
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * kBlock) {
+    const int c0 = (int)(i % cv) * 8;
+    float g[8], xv[8];
+    VecIO<T>::load(dy + i * 8, g);
+    VecIO<T>::load(x + i * 8, xv);
+    if (relu) {
+      float sc[8], sh[8], zv[8];
+      VecIO<float>::load(scale + c0, sc);
+      VecIO<float>::load(shift + c0, sh);
+      if (z) VecIO<Tz>::load(z + i * 8, zv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float o = fmaf(xv[k], sc[k], sh[k]);
+        if (z) o += zv[k];
+        if (o <= 0.f) g[k] = 0.f;
+      }
+    }
+    if (dz) VecIO<Tz>::store(dz + i * 8, g);
+    float out[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = c0 + k;
+      const float is = invstd[c];
+      const float mdy = sums[c] * inv_n;
+      const float mdyx = sums[C + c] * inv_n;
+      const float wv = w ? to_f<Tw>(w[c]) : 1.f;
+      out[k] = (g[k] - mdy - (xv[k] - mean[c]) * is * is * mdyx) * is * wv;
+    }
+    VecIO<T>::store(dx + i * 8, out);
+  }
+}
+
+template <typename T, typename Tz, typename Tw>
+__global__ __launch_bounds__(kBlock) void k_dgrad_generic(const T* __restrict__ dy, const T* __restrict__ x,
+                                                          const Tz* __restrict__ z, const float* __restrict__ mean,
+                                                          const float* __restrict__ invstd, const Tw* __restrict__ w,
+                                                          const float* __restrict__ sums, const float* __restrict__ count,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, bool relu,
+                                                          T* __restrict__ dx, Tz* __restrict__ dz, int64_t total, int C,
+                                                          int64_t inner) {
+  const float inv_n = 1.f / count[0];
+  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < total; i += (int64_t)gridDim.x * kBlock) {
+    const int c = (int)((i / inner) % C);
+    float g = to_f<T>(dy[i]);
+    const float xv = to_f<T>(x[i]);
+    if (relu) {
+      float o = fmaf(xv, scale[c], shift[c]);
+      if (z) o += to_f<Tz>(z[i]);
+      if (o <= 0.f) g = 0.f;
+    }
+    if (dz) dz[i] = from_f<Tz>(g);
+    const float is = invstd[c];
+    const float wv = w ? to_f<Tw>(w[c]) : 1.f;
+    const float r = (g - sums[c] * inv_n - (xv - mean[c]) * is * is * sums[C + c] * inv_n) * is * wv;
+    dx[i] = from_f<T>(r);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// launch geometry helpers
+// ------------------------------------------------------------------------------------------
+struct NhwcGeom {
+  int cvb, R, gx;
+};
+NhwcGeom nhwc_geom(int C) {
+  const int cv = (C + 7) / 8;
+  NhwcGeom g;
+  g.cvb = std::min(cv, kBlock);
+  int R = kBlock / g.cvb;
+  int p = 1;
+  while (p * 2 <= R) p *= 2;
+  g.R = p;
+  g.gx = (cv + g.cvb - 1) / g.cvb;
+  return g;
+}
+
+int grid_for(int64_t work_items) {
+  const int64_t b = (work_items + kBlock - 1) / kBlock;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(b, 256 * 16));
+}
+
+}  // namespace
+
+// ==========================================================================================
+// host API (bh/bn_api.h)
+// ==========================================================================================
+int bn_num_splits(const BNShape& s) {
+  if (s.channels_last) {
+    const NhwcGeom g = nhwc_geom(s.C);
+    const int64_t rows = s.outer;
+    // aim for ~2048 workgroups, at least 32 row iterations per lane
+    int64_t splits = std::max<int64_t>(1, 2048 / g.gx);
+    splits = std::min<int64_t>(splits, std::max<int64_t>(1, rows / (g.R * 32)));
+    return (int)std::max<int64_t>(1, splits);
+  }
+  const int64_t per_c = s.outer * s.inner;
+  int64_t splits = std::max<int64_t>(1, 2048 / std::max(1, s.C));
+  splits = std::min<int64_t>(splits, std::max<int64_t>(1, per_c / (kBlock * 16)));
+  return (int)std::max<int64_t>(1, splits);
+}
+
+void bn_stats(const BNShape& s, int dt_x, const void* x, int splits, float* pmean, float* pm2, float* pn,
+              hipStream_t st) {
+  if (s.channels_last) {
+    const NhwcGeom g = nhwc_geom(s.C);
+    const int64_t rows_per_split = (s.outer + splits - 1) / splits;
+    const size_t shm = sizeof(float) * (2 * g.R * g.cvb * 8 + g.R);
+    BN_DISPATCH(dt_x, T,
+        hipLaunchKernelGGL((k_stats_nhwc<T>), dim3(g.gx, splits), dim3(kBlock), shm, st, (const T*)x, s.outer, s.C,
+                           g.cvb, g.R, rows_per_split, pmean, pm2, pn));
+  } else {
+    int64_t per = (s.outer * s.inner + splits - 1) / splits;
+    per = (per + 7) / 8 * 8;
+    BN_DISPATCH(dt_x, T,
+        hipLaunchKernelGGL((k_stats_nchw<T>), dim3(s.C, splits), dim3(kBlock), 0, st, (const T*)x, s.outer, s.C,
+                           s.inner, per, pmean, pm2, pn));
+  }
+  check_launch("bn_stats");
+}
+
+void bn_stats_finalize(const BNShape& s, int splits, const float* pmean, const float* pm2, const float* pn,
+                       float* out_local, const BNFinal& fin, int dt_w, const void* w, const void* b, void* rmean,
+                       void* rvar, hipStream_t st) {
+  const int grid = (s.C + kBlock - 1) / kBlock;
+  const bool per_channel_n = !s.channels_last;
+  BN_DISPATCH(dt_w, Tw,
+      hipLaunchKernelGGL((k_stats_finalize<Tw>), dim3(grid), dim3(kBlock), 0, st, s.C, splits, per_channel_n, pmean, pm2,
+                         pn, out_local, fin, (const Tw*)w, (const Tw*)b, (Tw*)rmean, (Tw*)rvar));
+  check_launch("bn_stats_finalize");
+}
+
+void bn_merge_ranks(int W, int C, const float* gathered, const BNFinal& fin, int dt_w, const void* w, const void* b,
+                    void* rmean, void* rvar, float* var_unbiased, hipStream_t st) {
+  const int grid = (C + kBlock - 1) / kBlock;
+  BN_DISPATCH(dt_w, Tw,
+      hipLaunchKernelGGL((k_merge_ranks<Tw>), dim3(grid), dim3(kBlock), 0, st, W, C, gathered, fin, (const Tw*)w,
+                         (const Tw*)b, (Tw*)rmean, (Tw*)rvar, var_unbiased));
+  check_launch("bn_merge_ranks");
+}
+
+void bn_forward(const BNShape& s, int dt_x, const void* x, int dt_z, const void* z, int dt_y, void* y,
+                const float* scale, const float* shift, bool relu, hipStream_t st) {
+  const int64_t total = s.outer * s.C * s.inner;
+  if (total == 0) return;
+  if (dt_z < 0) dt_z = dt_x;
+  if (s.channels_last && s.C % 8 == 0) {
+    const int grid = grid_for(total / 8);
+    BN_DISPATCH(dt_x, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_y, Ty,
+        hipLaunchKernelGGL((k_fwd_nhwc<T, Tz, Ty>), dim3(grid), dim3(kBlock), 0, st, (const T*)x, (const Tz*)z, (Ty*)y,
+                           scale, shift, s.outer, s.C, relu))));
+  } else {
+    const int64_t inner = s.channels_last ? 1 : s.inner;
+    const int grid = grid_for(inner % 8 == 0 ? total / 8 : total);
+    BN_DISPATCH(dt_x, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_y, Ty,
+        hipLaunchKernelGGL((k_fwd_generic<T, Tz, Ty>), dim3(grid), dim3(kBlock), 0, st, (const T*)x, (const Tz*)z,
+                           (Ty*)y, scale, shift, total, s.C, inner, relu))));
+  }
+  check_launch("bn_forward");
+}
+
+void bn_backward_reduce(const BNShape& s, int dt, const void* dy, const void* x, int dt_z, const void* z,
+                        const float* mean, const float* scale, const float* shift, bool relu, int splits, float* p_dy,
+                        float* p_dyx, hipStream_t st) {
+  if (dt_z < 0) dt_z = dt;
+  if (s.channels_last && s.C % 8 == 0) {
+    const NhwcGeom g = nhwc_geom(s.C);
+    const int64_t rows_per_split = (s.outer + splits - 1) / splits;
+    const size_t shm = sizeof(float) * (2 * g.R * g.cvb * 8);
+    BN_DISPATCH(dt, T, BN_DISPATCH(dt_z, Tz,
+        hipLaunchKernelGGL((k_bwd_reduce_nhwc<T, Tz>), dim3(g.gx, splits), dim3(kBlock), shm, st, (const T*)dy,
+                           (const T*)x, (const Tz*)z, mean, scale, shift, relu, s.outer, s.C, g.cvb, g.R,
+                           rows_per_split, p_dy, p_dyx)));
+  } else {
+    // NCHW (or channels_last with C % 8 != 0 viewed as N=M, HW=1 per channel)
+    const int64_t N = s.channels_last ? 1 : s.outer;
+    const int64_t HW = s.channels_last ? s.outer : s.inner;
+    // channels_last with HW=rows needs stride C between rows: handled by the generic indexing only for
+    // NCHW; for NHWC with C%8!=0 we rely on the caller having made the tensor contiguous NCHW.
+    const int64_t per = (N * HW + splits - 1) / splits;
+    BN_DISPATCH(dt, T, BN_DISPATCH(dt_z, Tz,
+        hipLaunchKernelGGL((k_bwd_reduce_generic<T, Tz>), dim3(s.C, splits), dim3(kBlock), 0, st, (const T*)dy,
+                           (const T*)x, (const Tz*)z, mean, scale, shift, relu, N, s.C, HW, per, p_dy, p_dyx)));
+  }
+  check_launch("bn_backward_reduce");
+}
+
+void bn_backward_reduce_finalize(int C, int splits, const float* p_dy, const float* p_dyx, const float* invstd,
+                                 float* sums, int dt_w, void* gw, void* gb, hipStream_t st) {
+  const int grid = (C + kBlock - 1) / kBlock;
+  BN_DISPATCH(dt_w, Tw,
+      hipLaunchKernelGGL((k_bwd_reduce_finalize<Tw>), dim3(grid), dim3(kBlock), 0, st, C, splits, p_dy, p_dyx, invstd,
+                         sums, (Tw*)gw, (Tw*)gb));
+  check_launch("bn_backward_reduce_finalize");
+}
+
+void bn_backward_dgrad(const BNShape& s, int dt, const void* dy, const void* x, int dt_z, const void* z,
+                       const float* mean, const float* invstd, int dt_w, const void* w, const float* sums,
+                       const float* count, const float* scale, const float* shift, bool relu, void* dx, void* dz,
+                       hipStream_t st) {
+  const int64_t total = s.outer * s.C * s.inner;
+  if (total == 0) return;
+  if (dt_z < 0) dt_z = dt;
+  if (s.channels_last && s.C % 8 == 0) {
+    const int grid = grid_for(total / 8);
+    BN_DISPATCH(dt, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_w, Tw,
+        hipLaunchKernelGGL((k_dgrad_nhwc<T, Tz, Tw>), dim3(grid), dim3(kBlock), 0, st, (const T*)dy, (const T*)x,
+                           (const Tz*)z, mean, invstd, (const Tw*)w, sums, count, scale, shift, relu, (T*)dx, (Tz*)dz,
+                           s.outer, s.C))));
+  } else {
+    const int64_t inner = s.channels_last ? 1 : s.inner;
+    const int grid = grid_for(total);
+    BN_DISPATCH(dt, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_w, Tw,
+        hipLaunchKernelGGL((k_dgrad_generic<T, Tz, Tw>), dim3(grid), dim3(kBlock), 0, st, (const T*)dy, (const T*)x,
+                           (const Tz*)z, mean, invstd, (const Tw*)w, sums, count, scale, shift, relu, (T*)dx, (Tz*)dz,
+                           total, s.C, inner))));
+  }
+  check_launch("bn_backward_dgrad");
+}
+
+}  // namespace bh

@@ -1,0 +1,197 @@
+"""``syncbn``: batch-norm statistics / normalisation ops.
+
+GPU tensors run ``beforeholiday_amd._C.syncbn`` (kernels/batchnorm.hip); CPU tensors run the
+PyTorch reference below with identical semantics. The second half of this module provides the
+reference extension's function names (csrc/syncbn.cpp:98-109: ``welford_mean_var``,
+``welford_parallel``, ``batchnorm_forward``, ``reduce_bn``, ``batchnorm_backward`` and the
+``_c_last`` variants, ``relu_bw_c_last``) on top of the fused ops.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .._native import submodule
+
+
+def _native():
+    return submodule("syncbn")
+
+
+def _bcast(v: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    return v.view([1, -1] + [1] * (x.dim() - 2))
+
+
+def _reduce_dims(x):
+    return [0] + list(range(2, x.dim()))
+
+
+# --------------------------------------------------------------------------------- reference
+
+
+def _ref_stats(x):
+    xf = x.float()
+    dims = _reduce_dims(x)
+    mean = xf.mean(dims)
+    var_b = xf.var(dims, unbiased=False)
+    n = float(x.numel() // x.size(1))
+    return mean, var_b, n
+
+
+def _ref_final(mean, var_b, n, w, b, rm, rv, momentum, eps):
+    invstd = torch.rsqrt(var_b + eps)
+    wv = w.float() if w is not None else torch.ones_like(mean)
+    bv = b.float() if b is not None else torch.zeros_like(mean)
+    scale = wv * invstd
+    shift = bv - mean * scale
+    if rm is not None:
+        unb = var_b * n / (n - 1) if n > 1 else var_b
+        rm.copy_(((1 - momentum) * rm.float() + momentum * mean).to(rm.dtype))
+        rv.copy_(((1 - momentum) * rv.float() + momentum * unb).to(rv.dtype))
+    count = torch.full((1,), n, dtype=torch.float32, device=mean.device)
+    return [mean, invstd, scale, shift, count]
+
+
+def stats_local(x):
+    if x.is_cuda:
+        return _native().stats_local(x)
+    mean, var_b, n = _ref_stats(x)
+    return torch.cat([mean, var_b, torch.tensor([n], dtype=torch.float32, device=x.device)])
+
+
+def stats_single(x, weight, bias, running_mean, running_var, momentum, eps):
+    if x.is_cuda:
+        return _native().stats_single(x, weight, bias, running_mean, running_var, momentum, eps)
+    mean, var_b, n = _ref_stats(x)
+    return _ref_final(mean, var_b, n, weight, bias, running_mean, running_var, momentum, eps)
+
+
+def merge_ranks(gathered, weight, bias, running_mean, running_var, momentum, eps):
+    if gathered.is_cuda:
+        return _native().merge_ranks(gathered, weight, bias, running_mean, running_var, momentum, eps)
+    C = (gathered.size(1) - 1) // 2
+    means, vars_b, ns = gathered[:, :C], gathered[:, C:2 * C], gathered[:, 2 * C:]
+    n = ns.sum()
+    mean = (means * ns).sum(0) / n
+    m2 = (vars_b * ns).sum(0) + (ns * (means - mean) ** 2).sum(0)
+    var_b = m2 / n
+    return _ref_final(mean, var_b, float(n), weight, bias, running_mean, running_var, momentum, eps)
+
+
+def forward(x, z, scale, shift, relu, out_dtype=None):
+    if x.is_cuda:
+        return _native().forward(x, z, scale, shift, relu, out_dtype)
+    y = x.float() * _bcast(scale, x) + _bcast(shift, x)
+    if z is not None:
+        y = y + z.float()
+    if relu:
+        y = torch.relu(y)
+    return y.to(out_dtype or x.dtype)
+
+
+def _ref_masked_dy(dy, x, z, scale, shift, relu):
+    g = dy.float()
+    if relu:
+        pre = x.float() * _bcast(scale, x) + _bcast(shift, x)
+        if z is not None:
+            pre = pre + z.float()
+        g = torch.where(pre > 0, g, torch.zeros_like(g))
+    return g
+
+
+def backward_reduce(dy, x, z, mean, invstd, scale, shift, relu, weight, need_weight_grads):
+    if x.is_cuda:
+        return _native().backward_reduce(dy, x, z, mean, invstd, scale, shift, relu, weight, need_weight_grads)
+    g = _ref_masked_dy(dy, x, z, scale, shift, relu)
+    dims = _reduce_dims(x)
+    sum_dy = g.sum(dims)
+    sum_dy_xmu = (g * (x.float() - _bcast(mean, x))).sum(dims)
+    gw = gb = None
+    if need_weight_grads and weight is not None:
+        gw = (sum_dy_xmu * invstd).to(weight.dtype)
+        gb = sum_dy.to(weight.dtype)
+    return [torch.cat([sum_dy, sum_dy_xmu]), gw, gb]
+
+
+def backward_dgrad(dy, x, z, mean, invstd, weight, sums, count, scale, shift, relu, need_dz):
+    if x.is_cuda:
+        return _native().backward_dgrad(dy, x, z, mean, invstd, weight, sums, count, scale, shift, relu, need_dz)
+    C = x.size(1)
+    g = _ref_masked_dy(dy, x, z, scale, shift, relu)
+    n = count.float().reshape(-1)[0]
+    mdy, mdyx = sums[:C] / n, sums[C:] / n
+    wv = weight.float() if weight is not None else torch.ones_like(mean)
+    dx = (g - _bcast(mdy, x) - (x.float() - _bcast(mean, x)) * _bcast(invstd * invstd * mdyx, x)) * _bcast(invstd * wv, x)
+    dz = g.to(z.dtype if z is not None else x.dtype) if need_dz else None
+    return [dx.to(x.dtype), dz]
+
+
+# ------------------------------------------------------------------- reference-compatible API
+
+
+def welford_mean_var(input):
+    """Returns (mean, biased var) per channel (NCHW input)."""
+    local = stats_local(input)
+    C = input.size(1)
+    return local[:C], local[C:2 * C]
+
+
+welford_mean_var_c_last = welford_mean_var
+
+
+def welford_parallel(mean_feature_nodes, var_biased_feature_nodes, numel, eps):
+    """Merge per-rank stats -> (mean, unbiased var, inv_std) (reference welford_kernel_parallel)."""
+    W, C = mean_feature_nodes.shape
+    g = torch.cat([mean_feature_nodes.float(), var_biased_feature_nodes.float(),
+                   numel.float().reshape(W, 1).to(mean_feature_nodes.device)], dim=1)
+    mean, invstd, _, _, count = merge_ranks(g, None, None, None, None, 0.0, eps)
+    n = count.reshape(-1)[0]
+    var_b = 1.0 / (invstd * invstd) - eps
+    var = var_b * n / torch.clamp(n - 1, min=1)
+    return mean, var, invstd
+
+
+def _scale_shift(mean, inv_std, weight, shift):
+    w = weight.float() if weight is not None else torch.ones_like(mean)
+    b = shift.float() if shift is not None else torch.zeros_like(mean)
+    sc = w * inv_std
+    return sc.contiguous(), (b - mean * sc).contiguous()
+
+
+def batchnorm_forward(input, mean, inv_std, weight=None, shift=None):
+    sc, sh = _scale_shift(mean.float(), inv_std.float(), weight, shift)
+    return forward(input, None, sc, sh, False)
+
+
+def batchnorm_forward_c_last(input, z, mean, inv_std, weight=None, shift=None, fuse_relu=False):
+    sc, sh = _scale_shift(mean.float(), inv_std.float(), weight, shift)
+    return forward(input, z, sc, sh, fuse_relu)
+
+
+def reduce_bn(grad_output, input, mean, inv_std, weight=None):
+    sums, gw, gb = backward_reduce(grad_output, input, None, mean.float().contiguous(), inv_std.float().contiguous(),
+                                   None, None, False, weight, weight is not None)
+    C = input.size(1)
+    return sums[:C], sums[C:], gw, gb
+
+
+reduce_bn_c_last = reduce_bn
+
+
+def batchnorm_backward(grad_output, input, mean, inv_std, weight, sum_dy, sum_dy_xmu, count):
+    """``count``: per-rank element counts (int tensor) or a total; the reference divides by sum(count)."""
+    total = count.float().sum().reshape(1).to(input.device)
+    sums = torch.cat([sum_dy.float(), sum_dy_xmu.float()])
+    dx, _ = backward_dgrad(grad_output, input, None, mean.float().contiguous(), inv_std.float().contiguous(),
+                           weight, sums, total, None, None, False, False)
+    return dx
+
+
+batchnorm_backward_c_last = batchnorm_backward
+
+
+def relu_bw_c_last(grad_output, input, z, mean, inv_std, weight=None, shift=None):
+    sc, sh = _scale_shift(mean.float(), inv_std.float(), weight, shift)
+    pre = forward(input, z, sc, sh, False, torch.float32)
+    return torch.where(pre > 0, grad_output, torch.zeros_like(grad_output))

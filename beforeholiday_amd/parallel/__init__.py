@@ -1,0 +1,52 @@
+"""Data parallelism: DDP, Reducer, SyncBatchNorm, LARC (reference: apex/parallel/__init__.py)."""
+import torch
+
+ReduceOp = torch.distributed.ReduceOp
+
+from .distributed import DistributedDataParallel, Reducer  # noqa: E402
+from .optimized_sync_batchnorm import SyncBatchNorm  # noqa: E402
+from .sync_batchnorm import SyncBatchNorm as PythonSyncBatchNorm  # noqa: E402
+from .LARC import LARC  # noqa: E402
+
+
+def convert_syncbn_model(module, process_group=None, channel_last=False):
+    """Recursively replace every ``_BatchNorm`` (not InstanceNorm) with :class:`SyncBatchNorm`,
+    carrying over running stats and affine parameters."""
+    mod = module
+    if isinstance(module, torch.nn.modules.instancenorm._InstanceNorm):
+        return module
+    if isinstance(module, torch.nn.modules.batchnorm._BatchNorm):
+        mod = SyncBatchNorm(module.num_features, module.eps, module.momentum, module.affine,
+                            module.track_running_stats, process_group, channel_last=channel_last)
+        mod.running_mean = module.running_mean
+        mod.running_var = module.running_var
+        mod.num_batches_tracked = module.num_batches_tracked
+        if module.affine:
+            mod.weight.data = module.weight.data.clone().detach()
+            mod.bias.data = module.bias.data.clone().detach()
+    for name, child in module.named_children():
+        mod.add_module(name, convert_syncbn_model(child, process_group=process_group, channel_last=channel_last))
+    del module
+    return mod
+
+
+def create_syncbn_process_group(group_size):
+    """Create process groups of ``group_size`` consecutive ranks; return the caller's group
+    (``None`` for group_size 0, i.e. the whole world)."""
+    if group_size == 0:
+        return None
+    world_size = torch.distributed.get_world_size()
+    assert world_size >= group_size
+    assert world_size % group_size == 0
+    group = None
+    for group_num in range(world_size // group_size):
+        ids = list(range(group_num * group_size, (group_num + 1) * group_size))
+        cur = torch.distributed.new_group(ranks=ids)
+        if torch.distributed.get_rank() // group_size == group_num:
+            group = cur
+    assert group is not None
+    return group
+
+
+__all__ = ["DistributedDataParallel", "Reducer", "SyncBatchNorm", "PythonSyncBatchNorm", "LARC",
+           "convert_syncbn_model", "create_syncbn_process_group", "ReduceOp"]

@@ -1,0 +1,439 @@
+"""DistributedDataParallel and Reducer (reference: apex/parallel/distributed.py:89-640).
+
+Behaviour kept from the reference:
+* parameters (and buffers) are broadcast from rank 0 at construction, flattened per dtype;
+* gradient buckets are built from the order gradients ARRIVE in the first backward pass (the
+  order that gives the best overlap), ``message_size`` elements per bucket, one bucket chain per
+  dtype; rank 0's bucket structure is broadcast so every rank issues identical collectives;
+* buckets are all-reduced in order while the rest of backward is still running;
+* ``delay_allreduce``, ``allreduce_trigger_params``, ``retain_allreduce_buffers``,
+  ``allreduce_always_fp32``, ``gradient_predivide_factor``, ``num_allreduce_streams`` (one
+  process group per stream, round-robin), ``allreduce_communicators``.
+
+MI355X / RCCL design:
+* collectives are issued with ``async_op=True`` on the RCCL backend: RCCL runs them on its own HIP
+  stream, so bucket all-reduces overlap the remaining backward kernels without a hand-managed side
+  stream; the end-of-backward callback makes the compute stream wait on each work handle.
+* averaging uses ``ReduceOp.AVG`` inside the collective when the backend supports it (RCCL), so no
+  extra scaling kernel runs per bucket.
+* each bucket owns a persistent flat buffer: the gather is one ``torch.cat(out=)`` and the scatter
+  back one fused ``_foreach_copy_`` launch (fixed pointers, no allocator churn).
+* device-agnostic: the same code runs on CPU tensors over gloo (the reference hard-codes CUDA).
+* a single-process world skips every collective.
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+from torch.nn.modules import Module
+from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
+
+
+def _raw(t: torch.Tensor) -> torch.Tensor:
+    """1-D view of a dense tensor in its storage order (contiguous or channels_last)."""
+    if t.is_contiguous():
+        return t.view(-1)
+    for fmt in (torch.channels_last, torch.channels_last_3d):
+        try:
+            if t.is_contiguous(memory_format=fmt):
+                return t.as_strided((t.numel(),), (1,))
+        except RuntimeError:
+            pass
+    raise RuntimeError("DistributedDataParallel: gradients must be dense (contiguous or channels_last)")
+
+
+def flatten(bucket):
+    return _flatten_dense_tensors(bucket)
+
+
+def unflatten(coalesced, bucket):
+    return _unflatten_dense_tensors(coalesced, bucket)
+
+
+def apply_flat_dist_call(bucket, call, extra_args=None):
+    coalesced = flatten(bucket)
+    if extra_args is not None:
+        call(coalesced, *extra_args)
+    else:
+        call(coalesced)
+    if call is dist.all_reduce:
+        coalesced /= dist.get_world_size()
+    for buf, synced in zip(bucket, unflatten(coalesced, bucket)):
+        buf.copy_(synced)
+
+
+def split_by_type(tensors):
+    buckets = {}
+    for t in tensors:
+        buckets.setdefault(t.dtype, []).append(t)
+    return list(buckets.values())
+
+
+# reference name kept
+split_half_float_double_bfloat16 = split_by_type
+
+
+def flat_dist_call(tensors, call, extra_args=None):
+    for bucket in split_by_type(tensors):
+        apply_flat_dist_call(bucket, call, extra_args)
+
+
+def extract_tensors(maybe_tensor, tensor_list):
+    if torch.is_tensor(maybe_tensor):
+        tensor_list.append(maybe_tensor)
+    else:
+        try:
+            for item in maybe_tensor:
+                extract_tensors(item, tensor_list)
+        except TypeError:
+            return
+
+
+class Reducer(object):
+    """Manual all-reduce (average) of a module's gradients, triggered by ``reduce()``.
+
+    Constructed from a module the parameters are broadcast from rank 0; constructed from a
+    gradient list the caller owns parameter synchronisation.
+    """
+
+    def __init__(self, module_or_grads_list, process_group=None):
+        self.process_group = process_group
+        if isinstance(module_or_grads_list, Module):
+            self.module = module_or_grads_list
+            flat_dist_call([p.data for p in self.module.parameters()], self._broadcast)
+        else:
+            self.module = None
+            self.grads = []
+            extract_tensors(module_or_grads_list, self.grads)
+
+    def _broadcast(self, t):
+        dist.broadcast(t, _group_rank0(self.process_group), group=self.process_group)
+
+    def _allreduce(self, t):
+        dist.all_reduce(t, group=self.process_group)
+
+    def reduce(self):
+        grads = ([p.grad.data for p in self.module.parameters() if p.grad is not None] if self.module
+                 else self.grads)
+        ws = dist.get_world_size(self.process_group)
+        for bucket in split_by_type(grads):
+            coalesced = flatten(bucket)
+            self._allreduce(coalesced)
+            coalesced /= ws
+            for buf, synced in zip(bucket, unflatten(coalesced, bucket)):
+                buf.copy_(synced)
+
+
+def _group_rank0(pg):
+    if pg is None:
+        return 0
+    try:
+        return dist.get_global_rank(pg, 0)
+    except Exception:
+        return 0
+
+
+def _supports_avg(pg) -> bool:
+    try:
+        return dist.get_backend(pg) == "nccl"
+    except Exception:
+        return False
+
+
+class _Bucket:
+    __slots__ = ("params", "numel", "dtype", "flat", "work", "launched", "ready", "outputs")
+
+    def __init__(self, params, dtype):
+        self.params = params  # list of param indices
+        self.dtype = dtype
+        self.numel = 0
+        self.flat = None
+        self.work = None
+        self.launched = False
+        self.ready = 0
+        self.outputs = None
+
+
+class DistributedDataParallel(Module):
+    """Data-parallel wrapper with overlapped, bucketed gradient all-reduce over RCCL / gloo.
+
+    Args mirror the reference (apex/parallel/distributed.py:162-175); ``process_group`` selects the
+    data-parallel group (default: WORLD).
+    """
+
+    def __init__(self, module, message_size=10000000, delay_allreduce=False, shared_param=None,
+                 allreduce_trigger_params=None, retain_allreduce_buffers=False, allreduce_always_fp32=False,
+                 num_allreduce_streams=1, allreduce_communicators=None, gradient_average=True,
+                 gradient_predivide_factor=1.0, gradient_average_split_factor=None, prof=False,
+                 process_group=None):
+        super().__init__()
+        if shared_param is not None:
+            raise ValueError("shared_param is no longer supported as an option.  It was misleadingly named "
+                             "from the start.  It turns out overlapping communication with computation should "
+                             "work fine with shared parameters.  If you still wish to delay communication to "
+                             "the end of the backward pass, use delay_allreduce=True|False instead.")
+        if gradient_average_split_factor is not None:
+            print("Warning:  gradient_average_split_factor has been renamed to gradient_predivide_factor.  "
+                  "For now, gradient_average_split_factor will also work, but please update to "
+                  "gradient_predivide_factor instead.")
+            gradient_predivide_factor = gradient_average_split_factor
+        self.module = module
+        self.process_group = process_group
+        self.world_size = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
+        self.message_size = int(message_size)
+        self.delay_allreduce = delay_allreduce
+        self.retain_allreduce_buffers = retain_allreduce_buffers
+        self.allreduce_always_fp32 = allreduce_always_fp32
+        self.gradient_average = gradient_average
+        self.gradient_predivide_factor = gradient_predivide_factor
+        self.prof = prof
+        self.allreduce_buffers = []
+        self.num_allreduce_streams = num_allreduce_streams
+        self.custom_allreduce_triggers = False
+        self.allreduce_trigger_params = None
+        if allreduce_trigger_params is not None:
+            if delay_allreduce:
+                raise ValueError("Setting allreduce_trigger_params is only valid if delay_allreduce=False.")
+            self.custom_allreduce_triggers = True
+            self.allreduce_trigger_params = set(id(p) for p in allreduce_trigger_params)
+        if allreduce_communicators is not None:
+            groups = allreduce_communicators[0] if isinstance(allreduce_communicators, tuple) else allreduce_communicators
+            self._groups = list(groups)
+            self.num_allreduce_streams = len(self._groups)
+        else:
+            self._groups = None  # created lazily (collective)
+        self._use_avg = (gradient_average and gradient_predivide_factor == 1.0 and not allreduce_always_fp32
+                         and _supports_avg(process_group))
+        self._sync_enabled = True
+        self._callback_queued = False
+        self._hooks = []
+
+        # sync parameters and buffers from rank 0
+        if self.world_size > 1:
+            root = _group_rank0(process_group)
+            tensors = [p.data for p in module.parameters()] + [b.data for b in module.buffers()]
+            for bucket in split_by_type(tensors):
+                coalesced = flatten(bucket)
+                dist.broadcast(coalesced, root, group=process_group)
+                for buf, synced in zip(bucket, unflatten(coalesced, bucket)):
+                    buf.copy_(synced)
+        self._refresh_params()
+
+    # ------------------------------------------------------------------ bookkeeping
+    def __setstate__(self, state):
+        super().__setstate__(state)
+        self._hooks = []
+        self._refresh_params()
+
+    def __getstate__(self):
+        attrs = dict(self.__dict__)
+        for k in ("_hooks", "_buckets", "_groups", "_param_to_bucket", "_arrival"):
+            attrs.pop(k, None)
+        return attrs
+
+    def _refresh_params(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        self.active_params = [p for p in self.module.parameters() if p.requires_grad]
+        self._param_ids = [id(p) for p in self.active_params]
+        self.needs_refresh = True
+        self._buckets: List[_Bucket] = []
+        self._param_to_bucket = {}
+        self._arrival = []
+        self._next_bucket = 0
+        if self.world_size > 1:
+            for idx, p in enumerate(self.active_params):
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(idx)))
+
+    def _pg_for(self, bucket_idx):
+        if self.num_allreduce_streams <= 1:
+            return self.process_group
+        if self._groups is None:
+            ranks = None
+            if self.process_group is not None:
+                ranks = dist.get_process_group_ranks(self.process_group)
+            self._groups = [dist.new_group(ranks=ranks) for _ in range(self.num_allreduce_streams)]
+        return self._groups[bucket_idx % len(self._groups)]
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Accumulate gradients locally (no all-reduce) inside this context."""
+        prev = self._sync_enabled
+        self._sync_enabled = False
+        try:
+            yield
+        finally:
+            self._sync_enabled = prev
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, *inputs, **kwargs):
+        if self.prof:
+            torch.cuda.nvtx.range_push("forward pass DDP logic")
+        if self.world_size > 1:
+            if [id(p) for p in self.module.parameters() if p.requires_grad] != self._param_ids:
+                self._refresh_params()
+            self._callback_queued = False
+            self._next_bucket = 0
+            for b in self._buckets:
+                b.work, b.launched, b.ready, b.outputs = None, False, 0, None
+            if self.needs_refresh:
+                self._arrival = []
+            if self.retain_allreduce_buffers:
+                self.allreduce_buffers = [None for _ in self._buckets]
+        if self.prof:
+            torch.cuda.nvtx.range_pop()
+        return self.module(*inputs, **kwargs)
+
+    # ------------------------------------------------------------------ backward hooks
+    def _make_hook(self, idx):
+        def hook(param):
+            if not self._sync_enabled:
+                return
+            if self.prof:
+                torch.cuda.nvtx.range_push("allreduce_hook")
+            if not self._callback_queued:
+                torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
+                self._callback_queued = True
+            if self.needs_refresh or self.delay_allreduce:
+                if self.needs_refresh:
+                    self._arrival.append(idx)
+            else:
+                b_idx = self._param_to_bucket.get(idx)
+                if b_idx is not None:
+                    b = self._buckets[b_idx]
+                    b.ready += 1
+                    if b.ready == len(b.params):
+                        self._launch_ready_in_order()
+            if self.prof:
+                torch.cuda.nvtx.range_pop()
+        return hook
+
+    def _launch_ready_in_order(self):
+        while self._next_bucket < len(self._buckets):
+            b = self._buckets[self._next_bucket]
+            if b.ready < len(b.params):
+                break
+            self._launch(self._next_bucket)
+            self._next_bucket += 1
+
+    def _build_buckets(self, order: List[int]):
+        """Cut buckets from an arrival order (per dtype, message_size elements or trigger params)."""
+        seen = set(order)
+        order = list(order) + [i for i in range(len(self.active_params)) if i not in seen]
+        open_b = {}
+        buckets = []
+        for idx in order:
+            p = self.active_params[idx]
+            b = open_b.get(p.dtype)
+            if b is None:
+                b = _Bucket([], p.dtype)
+                open_b[p.dtype] = b
+                buckets.append(b)
+            b.params.append(idx)
+            b.numel += p.numel()
+            cut = (id(p) in self.allreduce_trigger_params) if self.custom_allreduce_triggers else \
+                (b.numel >= self.message_size)
+            if cut:
+                open_b.pop(p.dtype)
+        return buckets
+
+    def _sync_bucket_structure(self, buckets):
+        """Broadcast rank 0's bucket structure: [nb, sizes(nb), param indices...] padded to 1+2P."""
+        P = len(self.active_params)
+        dev = self.active_params[0].device if P else torch.device("cpu")
+        if dist.get_backend(self.process_group) == "gloo":
+            dev = torch.device("cpu")
+        info = torch.zeros(1 + 2 * P, dtype=torch.int64, device=dev)
+        if self.rank == 0:
+            flat = [len(buckets)] + [len(b.params) for b in buckets] + [i for b in buckets for i in b.params]
+            info[: len(flat)] = torch.tensor(flat, dtype=torch.int64)
+        dist.broadcast(info, _group_rank0(self.process_group), group=self.process_group)
+        info = info.cpu().tolist()
+        nb = info[0]
+        sizes = info[1:1 + nb]
+        idxs = info[1 + nb:1 + nb + sum(sizes)]
+        out, pos = [], 0
+        for s in sizes:
+            ps = idxs[pos:pos + s]
+            pos += s
+            b = _Bucket(ps, self.active_params[ps[0]].dtype)
+            b.numel = sum(self.active_params[i].numel() for i in ps)
+            out.append(b)
+        return out
+
+    def _launch(self, b_idx):
+        b = self._buckets[b_idx]
+        if b.launched:
+            return
+        grads = []
+        for i in b.params:
+            p = self.active_params[i]
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            grads.append(p.grad)
+        views = [_raw(g) for g in grads]
+        if self.retain_allreduce_buffers or b.flat is None or b.flat.device != views[0].device \
+                or b.flat.numel() != b.numel or b.flat.dtype != views[0].dtype:
+            b.flat = torch.empty(b.numel, dtype=views[0].dtype, device=views[0].device)
+        torch.cat(views, out=b.flat)
+        tensor = b.flat.float() if self.allreduce_always_fp32 and b.flat.dtype != torch.float32 else b.flat
+        if self.gradient_predivide_factor != 1.0:
+            tensor.mul_(1.0 / self.gradient_predivide_factor)
+        op = dist.ReduceOp.AVG if self._use_avg else dist.ReduceOp.SUM
+        b.work = dist.all_reduce(tensor, op=op, group=self._pg_for(b_idx), async_op=True)
+        b.outputs = (tensor, grads)
+        b.launched = True
+
+    def _finish(self, b_idx):
+        b = self._buckets[b_idx]
+        if b.work is not None:
+            b.work.wait()
+            b.work = None
+        tensor, grads = b.outputs
+        if self.gradient_average and not self._use_avg:
+            tensor.mul_(self.gradient_predivide_factor / self.world_size)
+        if tensor is not b.flat:
+            b.flat.copy_(tensor)
+        if self.retain_allreduce_buffers:
+            self.allreduce_buffers[b_idx] = b.flat
+            off = 0
+            for i, g in zip(b.params, grads):
+                p = self.active_params[i]
+                n = g.numel()
+                p.grad = b.flat[off:off + n].view_as(g) if g.is_contiguous() else \
+                    b.flat[off:off + n].as_strided(g.size(), g.stride())
+                off += n
+        else:
+            outs, off = [], 0
+            for g in grads:
+                n = g.numel()
+                outs.append(b.flat[off:off + n])
+                off += n
+            torch._foreach_copy_([_raw(g) for g in grads], outs)
+        b.outputs = None
+
+    def _end_of_backward(self):
+        if self.prof:
+            torch.cuda.nvtx.range_push("allreduce_params")
+        if self.needs_refresh:
+            buckets = self._build_buckets(self._arrival)
+            self._buckets = self._sync_bucket_structure(buckets)
+            self._param_to_bucket = {i: bi for bi, b in enumerate(self._buckets) for i in b.params}
+            self.needs_refresh = False
+            if self.retain_allreduce_buffers:
+                self.allreduce_buffers = [None for _ in self._buckets]
+        for bi in range(len(self._buckets)):
+            self._launch(bi)  # buckets not yet launched (first / delayed / unused-param iterations)
+        for bi in range(len(self._buckets)):
+            self._finish(bi)
+        self._callback_queued = False
+        self._next_bucket = 0
+        for b in self._buckets:
+            b.launched, b.ready = False, 0
+        if self.prof:
+            torch.cuda.nvtx.range_pop()

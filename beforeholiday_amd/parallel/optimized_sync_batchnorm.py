@@ -1,0 +1,112 @@
+"""SyncBatchNorm (reference: apex/parallel/optimized_sync_batchnorm.py:9-85 and
+optimized_sync_batchnorm_kernel.py:7-119).
+
+Training forward: local Welford statistics (HIP kernel) -> all_gather of the [mean, var_biased,
+count] rows over the process group -> rank merge + running-stat update + per-channel scale/shift
+(one tiny kernel) -> a single fused  y = x*scale + shift (+ z) (ReLU)  pass. Backward: one reduce
+kernel (ReLU mask recomputed from x, no masked-dy tensor), all_reduce of [sum_dy, sum_dy_xmu],
+one dgrad kernel that also emits dz for the fused residual branch. With a single rank the
+collectives are skipped and the merge is fused into the statistics finalize.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+from torch.nn import functional as F
+from torch.nn.modules.batchnorm import _BatchNorm
+
+from ..ops import syncbn
+
+
+def _world(pg):
+    if not (dist.is_available() and dist.is_initialized()):
+        return 1
+    return dist.get_world_size(pg)
+
+
+class SyncBatchnormFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, input, z, weight, bias, running_mean, running_var, eps, momentum, process_group,
+                channel_last, fuse_relu):
+        input = input.contiguous(memory_format=torch.channels_last) if (channel_last and input.dim() == 4) else input
+        world = _world(process_group)
+        if world > 1:
+            local = syncbn.stats_local(input)
+            gathered = torch.empty(world * local.numel(), dtype=local.dtype, device=local.device)
+            dist.all_gather_into_tensor(gathered, local, group=process_group)
+            gathered = gathered.view(world, local.numel())
+            mean, invstd, scale, shift, count = syncbn.merge_ranks(gathered, weight, bias, running_mean,
+                                                                   running_var, momentum, eps)
+        else:
+            mean, invstd, scale, shift, count = syncbn.stats_single(input, weight, bias, running_mean,
+                                                                    running_var, momentum, eps)
+        out = syncbn.forward(input, z, scale, shift, fuse_relu)
+        ctx.save_for_backward(input, z, weight, mean, invstd, scale, shift, count)
+        ctx.process_group = process_group
+        ctx.world = world
+        ctx.fuse_relu = fuse_relu
+        ctx.has_z = z is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        input, z, weight, mean, invstd, scale, shift, count = ctx.saved_tensors
+        need_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        sums, gw, gb = syncbn.backward_reduce(grad_output, input, z, mean, invstd, scale, shift, ctx.fuse_relu,
+                                              weight, need_w)
+        grad_input = grad_z = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            if ctx.world > 1:
+                dist.all_reduce(sums, group=ctx.process_group)
+            grad_input, grad_z = syncbn.backward_dgrad(grad_output, input, z, mean, invstd, weight, sums, count,
+                                                       scale, shift, ctx.fuse_relu,
+                                                       ctx.has_z and ctx.needs_input_grad[1])
+        return grad_input, grad_z, (gw if need_w else None), (gb if need_w else None), None, None, None, None, None, \
+            None, None
+
+
+class SyncBatchNorm(_BatchNorm):
+    """Synchronized batch norm over ``process_group`` (default: WORLD).
+
+    ``channel_last=True`` expects/keeps NHWC (channels_last) activations; ``fuse_relu=True`` applies
+    ReLU after the optional residual input ``z`` (``forward(input, z=None)``).
+    """
+
+    warned = False
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True, track_running_stats=True,
+                 process_group=None, channel_last=False, fuse_relu=False):
+        super().__init__(num_features, eps=eps, momentum=momentum, affine=affine,
+                         track_running_stats=track_running_stats)
+        self.process_group = process_group
+        self.channel_last = channel_last
+        self.fuse_relu = fuse_relu
+
+    def _specify_process_group(self, process_group):
+        self.process_group = process_group
+
+    def _specify_channel_last(self, channel_last):
+        self.channel_last = channel_last
+
+    def _check_input_dim(self, input):
+        if input.dim() < 2:
+            raise ValueError("expected at least 2D input (got {}D input)".format(input.dim()))
+
+    def forward(self, input, z=None):
+        self._check_input_dim(input)
+        if not self.training and self.track_running_stats:
+            # inference: fold running stats into scale/shift, one fused pass (z / relu included)
+            w = self.weight.float() if self.weight is not None else torch.ones_like(self.running_mean, dtype=torch.float32)
+            b = self.bias.float() if self.bias is not None else torch.zeros_like(self.running_mean, dtype=torch.float32)
+            invstd = torch.rsqrt(self.running_var.float() + self.eps)
+            scale = (w * invstd).contiguous()
+            shift = (b - self.running_mean.float() * scale).contiguous()
+            return syncbn.forward(input, z, scale, shift, self.fuse_relu)
+        exp_avg = 0.0
+        if self.training and self.track_running_stats:
+            self.num_batches_tracked += 1
+            exp_avg = (1.0 / float(self.num_batches_tracked)) if self.momentum is None else self.momentum
+        rm = self.running_mean if (self.training and self.track_running_stats) else None
+        rv = self.running_var if (self.training and self.track_running_stats) else None
+        return SyncBatchnormFunction.apply(input, z, self.weight, self.bias, rm, rv, self.eps, exp_avg,
+                                           self.process_group, self.channel_last, self.fuse_relu)

@@ -1,0 +1,140 @@
+"""Headline benchmark: ResNet-50 amp O2 training images/sec (BASELINE.json), one rank per GPU.
+
+Configuration (BASELINE.json configs[2]): ResNet-50 (v1.5, 25.6 M params), amp O2 (fp16 model,
+fp32 BatchNorm + fp32 master weights, dynamic loss scaling), FusedLAMB, SyncBatchNorm (fused
+BN+ReLU / BN+add+ReLU, synchronised across all ranks), beforeholiday_amd DistributedDataParallel
+over RCCL. Synthetic 224x224 channels_last images, random-init weights, weak scaling
+(--batch images per GPU).
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Rank 0 prints ONE json line; ``value`` is the whole-job images/sec over N GPUs; the timed region is
+exactly K full training steps (forward, scaled backward with overlapped all-reduce, unscale,
+optimizer step, master->model copy) bracketed by barrier + synchronize, max over ranks.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "ResNet-50 amp O2 images/sec"
+BASELINE_VALUE = None  # BASELINE.json "published" is empty for this metric
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU")
+    ap.add_argument("--opt-level", default="O2", choices=["O2", "O5"], help="O2: fp16 (reference), O5: bf16")
+    ap.add_argument("--optimizer", default="lamb", choices=["lamb", "adam", "sgd"])
+    ap.add_argument("--no-syncbn", action="store_true")
+    ap.add_argument("--message-size", type=int, default=12_500_000, help="DDP bucket size (elements)")
+    ap.add_argument("--profile-steps", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    torch.backends.cudnn.benchmark = True
+
+    from beforeholiday_amd import amp
+    from beforeholiday_amd._native import require_native
+    from beforeholiday_amd.models import resnet50, resnet50_fused
+    from beforeholiday_amd.optimizers import FusedAdam, FusedLAMB, FusedSGD
+    from beforeholiday_amd.parallel import DistributedDataParallel
+
+    require_native("bench")
+    torch.manual_seed(1234 + rank)
+    model = (resnet50() if args.no_syncbn else resnet50_fused(channel_last=True)).cuda()
+    model = model.to(memory_format=torch.channels_last)
+    global_batch = args.batch * world
+    if args.optimizer == "lamb":
+        opt = FusedLAMB(model.parameters(), lr=4e-3 * global_batch / 4096, weight_decay=0.01)
+    elif args.optimizer == "adam":
+        opt = FusedAdam(model.parameters(), lr=1e-3, weight_decay=0.01)
+    else:
+        opt = FusedSGD(model.parameters(), lr=0.1 * global_batch / 256, momentum=0.9, weight_decay=1e-4)
+    model, opt = amp.initialize(model, opt, opt_level=args.opt_level, keep_batchnorm_fp32=True, verbosity=0)
+    model = DistributedDataParallel(model, message_size=args.message_size)
+
+    dt = torch.float16 if args.opt_level == "O2" else torch.bfloat16
+    x = torch.randn(args.batch, 3, 224, 224, device="cuda", dtype=dt).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (args.batch,), device="cuda")
+
+    def step():
+        out = model(x)
+        loss = F.cross_entropy(out, y)
+        with amp.scale_loss(loss, opt) as scaled:
+            scaled.backward()
+        opt.step()
+        opt.zero_grad()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed / args.steps * 1e3
+    img_s = global_batch * args.steps / elapsed
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC,
+            "value": round(img_s, 2),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (round(img_s / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
+            "dtype": "fp16" if dt == torch.float16 else "bf16",
+            "data": "synthetic 224x224 channels_last images, random-init weights",
+            "config": {
+                "model": "ResNet-50 amp O2 + FusedLAMB + SyncBatchNorm, DDP" if args.optimizer == "lamb" and not args.no_syncbn
+                else f"ResNet-50 amp {args.opt_level} + {args.optimizer}",
+                "opt_level": args.opt_level,
+                "optimizer": {"lamb": "FusedLAMB", "adam": "FusedAdam", "sgd": "FusedSGD"}[args.optimizer],
+                "sync_batchnorm": not args.no_syncbn,
+                "global_batch": global_batch,
+                "batch_per_gpu": args.batch,
+                "image_size": 224,
+                "parallelism": f"dp{world}",
+                "final_loss": round(float(loss.item()), 4),
+            },
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,129 @@
+"""DistributedDataParallel / Reducer on gloo world_size=2 (the BASELINE "plumbing" config:
+2-layer MLP wrapped in DDP, CPU). Race-style check modelled on
+tests/distributed/DDP/ddp_race_condition_test.py: analytic gradient sums every iteration."""
+import pytest
+import torch
+import torch.distributed as dist
+
+from beforeholiday_amd.parallel import DistributedDataParallel as DDP, Reducer
+
+from _dist import run_distributed
+
+
+class MLP(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.fc1 = torch.nn.Linear(32, 64)
+        self.fc2 = torch.nn.Linear(64, 8)
+
+    def forward(self, x):
+        return self.fc2(torch.relu(self.fc1(x)))
+
+
+def _mlp_ddp(rank, world, kwargs):
+    torch.manual_seed(100 + rank)  # different init per rank: DDP must broadcast rank 0's params
+    model = MLP()
+    ddp = DDP(model, **kwargs)
+    ref = MLP()
+    torch.manual_seed(100)
+    ref_state = MLP().state_dict()
+    ref.load_state_dict(ref_state)
+    for p, q in zip(model.parameters(), ref.parameters()):
+        torch.testing.assert_close(p, q)
+    opt = torch.optim.SGD(ddp.parameters(), lr=0.1)
+    ref_opt = torch.optim.SGD(ref.parameters(), lr=0.1)
+    for it in range(4):
+        torch.manual_seed(it)
+        x = torch.randn(8 * world, 32)
+        y = torch.randn(8 * world, 8)
+        xs, ys = x[rank * 8:(rank + 1) * 8], y[rank * 8:(rank + 1) * 8]
+        loss = torch.nn.functional.mse_loss(ddp(xs), ys)
+        opt.zero_grad()
+        loss.backward()
+        # reference: full batch on one process == average of per-rank mean losses
+        ref_opt.zero_grad()
+        rl = sum(torch.nn.functional.mse_loss(ref(x[r * 8:(r + 1) * 8]), y[r * 8:(r + 1) * 8]) for r in range(world)) / world
+        rl.backward()
+        for p, q in zip(model.parameters(), ref.parameters()):
+            torch.testing.assert_close(p.grad, q.grad, rtol=1e-5, atol=1e-6)
+        opt.step()
+        ref_opt.step()
+
+
+@pytest.mark.parametrize("kwargs", [
+    {},
+    {"message_size": 1},
+    {"message_size": 100, "num_allreduce_streams": 2},
+    {"delay_allreduce": True},
+    {"allreduce_always_fp32": True, "gradient_predivide_factor": 2.0},
+    {"retain_allreduce_buffers": True, "message_size": 500},
+])
+def test_ddp_mlp_gloo(kwargs):
+    run_distributed(_mlp_ddp, 2, kwargs)
+
+
+def _race(rank, world):
+    # two large params, tiny buckets, trigger params: grads must equal the analytic sum each iter
+    a = torch.nn.Parameter(torch.ones(100000))
+    b = torch.nn.Parameter(torch.ones(100000))
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a, self.b = a, b
+
+        def forward(self, x):
+            return self.a * x, self.b * x
+
+    m = DDP(M(), message_size=1, allreduce_trigger_params=[b], num_allreduce_streams=3)
+    for it in range(5):
+        x = torch.full((100000,), float(rank + 1 + it))
+        ya, yb = m(x)
+        a.grad = None
+        b.grad = None
+        (ya.sum() + yb.sum()).backward()
+        expect = sum(r + 1 + it for r in range(world)) / world
+        assert torch.all(a.grad == expect), (a.grad[:3], expect)
+        assert torch.all(b.grad == expect)
+
+
+def test_ddp_race_gloo():
+    run_distributed(_race, 2)
+
+
+def _reducer(rank, world):
+    torch.manual_seed(rank)
+    model = MLP()
+    red = Reducer(model)
+    x = torch.randn(4, 32) * (rank + 1)
+    model(x).sum().backward()
+    grads = [p.grad.clone() for p in model.parameters()]
+    red.reduce()
+    for g, p in zip(grads, model.parameters()):
+        tot = g.clone()
+        dist.all_reduce(tot)
+        torch.testing.assert_close(p.grad, tot / world)
+
+
+def test_reducer_gloo():
+    run_distributed(_reducer, 2)
+
+
+def _no_sync(rank, world):
+    torch.manual_seed(0)
+    m = DDP(MLP())
+    x = torch.randn(4, 32) * (rank + 1)
+    with m.no_sync():
+        m(x).sum().backward()
+    local = [p.grad.clone() for p in m.parameters()]
+    for p in m.parameters():
+        p.grad = None
+    m(x).sum().backward()
+    for g, p in zip(local, m.parameters()):
+        tot = g.clone()
+        dist.all_reduce(tot)
+        torch.testing.assert_close(p.grad, tot / world, rtol=1e-5, atol=1e-6)
+
+
+def test_ddp_no_sync_gloo():
+    run_distributed(_no_sync, 2)

@@ -219,7 +219,8 @@ def test_lamb_gpu(dt, mode, nvlamb, decay, gnorm):
     g, p, m, v = _lists(4, dt, "cuda", seed=7)
     v = [x.abs() for x in v]
     gn = torch.tensor([gnorm], device="cuda")
-    tol = (2e-5, 2e-5) if dt == torch.float32 else TOL[dt]
+    # trust ratios come from norms summed in a different order: allow 1-2 ulp flips in 16-bit
+    tol = {torch.float32: (2e-5, 2e-5), torch.float16: (4e-3, 4e-3), torch.bfloat16: (2e-2, 2e-2)}[dt]
     _run_both("multi_tensor_lamb", [g, p, m, v], 1e-2, 0.9, 0.999, 1e-6, 2, 1, decay, 1, mode, gn, 1.0, nvlamb,
               rtol=tol[0], atol=tol[1])
 

@@ -1,0 +1,154 @@
+"""SyncBatchNorm / batch-norm kernels vs torch batch norm (fp32 reference), single and multi rank.
+
+Modelled on tests/distributed/synced_batchnorm/{single_gpu_unit_test,two_gpu_unit_test}.py.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from beforeholiday_amd.parallel import SyncBatchNorm, PythonSyncBatchNorm, convert_syncbn_model
+
+from _dist import run_distributed
+from conftest import devices
+
+
+def _ref_bn(x, w, b, z=None, relu=False, eps=1e-5):
+    xf = x.float()
+    y = F.batch_norm(xf, None, None, w.float(), b.float(), training=True, eps=eps)
+    if z is not None:
+        y = y + z.float()
+    if relu:
+        y = torch.relu(y)
+    return y
+
+
+SHAPES = [(8, 64, 14, 14), (4, 24, 7, 7), (16, 256, 1, 1), (3, 40, 9, 5), (32, 128), (2, 2048, 7, 7)]
+TOL = {torch.float32: 2e-4, torch.float16: 4e-3, torch.bfloat16: 3e-2}
+
+
+@pytest.mark.parametrize("device", devices())
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("channels_last", [False, True])
+@pytest.mark.parametrize("fuse", ["none", "relu", "add_relu"])
+def test_syncbn_single_rank(device, shape, dtype, channels_last, fuse):
+    if device == "cpu" and dtype != torch.float32:
+        pytest.skip("cpu reference path is exercised in fp32")
+    if channels_last and len(shape) != 4:
+        pytest.skip("channels_last needs 4D")
+    torch.manual_seed(0)
+    C = shape[1]
+    x = (torch.randn(shape) * 2 + 0.5).to(dtype)
+    z = torch.randn(shape).to(dtype) if fuse == "add_relu" else None
+    dy = torch.randn(shape).to(dtype)
+    bn = SyncBatchNorm(C, fuse_relu=(fuse != "none"), channel_last=channels_last)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+    bn = bn.to(device)
+    x, dy = x.to(device), dy.to(device)
+    if z is not None:
+        z = z.to(device)
+    if channels_last:
+        x = x.contiguous(memory_format=torch.channels_last)
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        if z is not None:
+            z = z.contiguous(memory_format=torch.channels_last)
+    xr = x.detach().float().cpu().requires_grad_(True)
+    zr = z.detach().float().cpu().requires_grad_(True) if z is not None else None
+    wr = bn.weight.detach().float().cpu().requires_grad_(True)
+    br = bn.bias.detach().float().cpu().requires_grad_(True)
+    yr = _ref_bn(xr, wr, br, zr, fuse != "none")
+    yr.backward(dy.float().cpu())
+
+    xg = x.detach().requires_grad_(True)
+    zg = z.detach().requires_grad_(True) if z is not None else None
+    y = bn(xg, zg) if zg is not None else bn(xg)
+    y.backward(dy)
+    tol = TOL[dtype]
+    torch.testing.assert_close(y.float().cpu(), yr.detach(), rtol=tol, atol=tol)
+    torch.testing.assert_close(xg.grad.float().cpu(), xr.grad, rtol=tol * 5, atol=tol * 5)
+    torch.testing.assert_close(bn.weight.grad.float().cpu(), wr.grad, rtol=tol * 10, atol=tol * 20)
+    torch.testing.assert_close(bn.bias.grad.float().cpu(), br.grad, rtol=tol * 10, atol=tol * 20)
+    if zg is not None:
+        torch.testing.assert_close(zg.grad.float().cpu(), zr.grad, rtol=tol * 5, atol=tol * 5)
+    # running stats: momentum 0.1 from (0, 1)
+    xf = x.float().cpu()
+    dims = [0] + list(range(2, xf.dim()))
+    n = xf.numel() // C
+    torch.testing.assert_close(bn.running_mean.cpu(), 0.1 * xf.mean(dims), rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(bn.running_var.cpu(), 0.9 + 0.1 * xf.var(dims, unbiased=True), rtol=1e-3, atol=1e-3)
+    if channels_last:
+        assert y.is_contiguous(memory_format=torch.channels_last)
+
+
+@pytest.mark.parametrize("device", devices())
+def test_syncbn_eval_matches_torch(device):
+    torch.manual_seed(1)
+    bn = SyncBatchNorm(32).to(device)
+    ref = torch.nn.BatchNorm2d(32).to(device)
+    ref.load_state_dict(bn.state_dict())
+    for _ in range(3):
+        x = torch.randn(4, 32, 6, 6, device=device)
+        bn(x), ref(x)
+    bn.eval(), ref.eval()
+    x = torch.randn(4, 32, 6, 6, device=device)
+    torch.testing.assert_close(bn(x), ref(x), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(bn.running_var, ref.running_var, rtol=1e-5, atol=1e-5)
+
+
+def test_fused_resnet_matches_unfused_cpu():
+    from beforeholiday_amd.models import resnet18_like
+    from beforeholiday_amd.models.resnet import Bottleneck, ResNet
+
+    torch.manual_seed(0)
+    ref = resnet18_like(num_classes=10)
+
+    def norm(c, fuse_relu=False):
+        return SyncBatchNorm(c, fuse_relu=fuse_relu)
+
+    fused = ResNet(Bottleneck, [1, 1, 1, 1], num_classes=10, norm_layer=norm, fused=True)
+    fused.load_state_dict(ref.state_dict())
+    x = torch.randn(2, 3, 32, 32)
+    torch.testing.assert_close(fused(x), ref(x), rtol=1e-4, atol=1e-4)
+
+
+def _dist_syncbn(rank, world, channels_last):
+    torch.manual_seed(0)
+    N, C = 4 * world, 16
+    x = torch.randn(N, C, 5, 5) * 3 + 1
+    dy = torch.randn(N, C, 5, 5)
+    ref = torch.nn.BatchNorm2d(C)
+    for impl in (SyncBatchNorm, PythonSyncBatchNorm):
+        bn = impl(C)
+        bn.load_state_dict(ref.state_dict())
+        xs = x[rank * 4:(rank + 1) * 4].clone().requires_grad_(True)
+        y = bn(xs)
+        y.backward(dy[rank * 4:(rank + 1) * 4])
+        r = torch.nn.BatchNorm2d(C)
+        r.load_state_dict(ref.state_dict())
+        xr = x.clone().requires_grad_(True)
+        yr = r(xr)
+        yr.backward(dy)
+        torch.testing.assert_close(y, yr[rank * 4:(rank + 1) * 4], rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(xs.grad, xr.grad[rank * 4:(rank + 1) * 4], rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(bn.running_mean, r.running_mean, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(bn.running_var, r.running_var, rtol=1e-5, atol=1e-5)
+        # weight grads are local sums; DDP averages them -> all_reduce(sum) equals the full-batch grad
+        gw = bn.weight.grad.clone()
+        torch.distributed.all_reduce(gw)
+        torch.testing.assert_close(gw, r.weight.grad, rtol=1e-4, atol=1e-4)
+
+
+def test_syncbn_two_ranks_gloo():
+    run_distributed(_dist_syncbn, 2, False)
+
+
+def test_convert_syncbn_model():
+    m = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.BatchNorm2d(8), torch.nn.Sequential(torch.nn.BatchNorm1d(4)),
+                            torch.nn.InstanceNorm2d(8))
+    m[1].running_mean.fill_(0.3)
+    c = convert_syncbn_model(m)
+    assert isinstance(c[1], SyncBatchNorm) and isinstance(c[2][0], SyncBatchNorm)
+    assert isinstance(c[3], torch.nn.InstanceNorm2d)
+    assert float(c[1].running_mean[0]) == pytest.approx(0.3)
