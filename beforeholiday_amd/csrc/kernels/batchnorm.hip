@@ -195,13 +195,37 @@ __global__ __launch_bounds__(kBlock) void k_stats_finalize(int C, int splits, bo
                                                            const float* __restrict__ pmean, const float* __restrict__ pm2,
                                                            const float* __restrict__ pn, float* __restrict__ out_local,
                                                            BNFinal fin, const Tw* w, const Tw* b, Tw* rmean, Tw* rvar) {
-  const int c = blockIdx.x * kBlock + threadIdx.x;
-  if (c >= C) return;
+  // 64 channels x 4 split-lanes per block; each lane walks every 4th split with 4 independent
+  // loads in flight, then the 4 lanes are merged through LDS (no serial latency chain).
+  __shared__ float sh[3][4][64];
+  const int cl = threadIdx.x & 63, lane = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   Welford acc{0.f, 0.f, 0.f};
-  for (int s = 0; s < splits; ++s) {
-    const float n = per_channel_n ? pn[(int64_t)s * C + c] : pn[s];
-    acc = welford_merge(acc, Welford{n, pmean[(int64_t)s * C + c], pm2[(int64_t)s * C + c]});
+  if (c < C) {
+    int s = lane;
+    for (; s + 12 < splits; s += 16) {
+      float n[4], m[4], q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int ss = s + 4 * u;
+        n[u] = per_channel_n ? pn[(int64_t)ss * C + c] : pn[ss];
+        m[u] = pmean[(int64_t)ss * C + c];
+        q[u] = pm2[(int64_t)ss * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = welford_merge(acc, Welford{n[u], m[u], q[u]});
+    }
+    for (; s < splits; s += 4) {
+      const float n = per_channel_n ? pn[(int64_t)s * C + c] : pn[s];
+      acc = welford_merge(acc, Welford{n, pmean[(int64_t)s * C + c], pm2[(int64_t)s * C + c]});
+    }
   }
+  sh[0][lane][cl] = acc.n;
+  sh[1][lane][cl] = acc.mean;
+  sh[2][lane][cl] = acc.m2;
+  __syncthreads();
+  if (lane != 0 || c >= C) return;
+  for (int l = 1; l < 4; ++l) acc = welford_merge(acc, Welford{sh[0][l][cl], sh[1][l][cl], sh[2][l][cl]});
   const float var_b = acc.n > 0.f ? acc.m2 / acc.n : 0.f;
   if (out_local) {
     // all_gather layout of the reference: [mean(C), var_biased(C), count(1)]
@@ -213,7 +237,7 @@ __global__ __launch_bounds__(kBlock) void k_stats_finalize(int C, int splits, bo
     const float invstd = rsqrtf(var_b + fin.eps);
     fin.mean[c] = acc.mean;
     fin.invstd[c] = invstd;
-    if (fin.count) if (c == 0) fin.count[0] = acc.n;
+    if (fin.count && c == 0) fin.count[0] = acc.n;
     const float wv = w ? to_f<Tw>(w[c]) : 1.f;
     const float bv = b ? to_f<Tw>(b[c]) : 0.f;
     fin.scale[c] = wv * invstd;
@@ -266,17 +290,22 @@ __global__ __launch_bounds__(kBlock) void k_merge_ranks(int W, int C, const floa
 template <typename T, typename Tz, typename Ty>
 __global__ __launch_bounds__(kBlock) void k_fwd_nhwc(const T* __restrict__ x, const Tz* __restrict__ z,
                                                      Ty* __restrict__ y, const float* __restrict__ scale,
-                                                     const float* __restrict__ shift, int64_t M, int C, bool relu) {
-  const int64_t nvec = M * (C / 8);
-  const int cv = C / 8;
-  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * kBlock) {
-    const int c0 = (int)(i % cv) * 8;
-    float xv[8], sc[8], sh[8];
-    VecIO<T>::load(x + i * 8, xv);
-    VecIO<float>::load(scale + c0, sc);
-    VecIO<float>::load(shift + c0, sh);
-    float zv[8];
-    if (z) VecIO<Tz>::load(z + i * 8, zv);
+                                                     const float* __restrict__ shift, int64_t M, int C, int cvb, int R,
+                                                     int64_t rows_per_split, bool relu) {
+  // thread owns 8 channels (scale/shift in registers for its whole row range), rows strided by R
+  const int v = threadIdx.x % cvb, r = threadIdx.x / cvb;
+  const int c0 = (blockIdx.x * cvb + v) * 8;
+  if (r >= R || c0 >= C) return;
+  const int64_t row0 = (int64_t)blockIdx.y * rows_per_split;
+  const int64_t row1 = min(M, row0 + rows_per_split);
+  float sc[8], sh[8];
+  VecIO<float>::load(scale + c0, sc);
+  VecIO<float>::load(shift + c0, sh);
+  for (int64_t row = row0 + r; row < row1; row += R) {
+    const int64_t off = row * C + c0;
+    float xv[8], zv[8];
+    VecIO<T>::load(x + off, xv);
+    if (z) VecIO<Tz>::load(z + off, zv);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float o = fmaf(xv[k], sc[k], sh[k]);
@@ -284,7 +313,7 @@ __global__ __launch_bounds__(kBlock) void k_fwd_nhwc(const T* __restrict__ x, co
       if (relu) o = fmaxf(o, 0.f);
       xv[k] = o;
     }
-    VecIO<Ty>::store(y + i * 8, xv);
+    VecIO<Ty>::store(y + off, xv);
   }
 }
 
@@ -446,13 +475,36 @@ __global__ __launch_bounds__(kBlock) void k_bwd_reduce_finalize(int C, int split
                                                                 const float* __restrict__ p_dyx,
                                                                 const float* __restrict__ invstd,
                                                                 float* __restrict__ sums, Tw* gw, Tw* gb) {
-  const int c = blockIdx.x * kBlock + threadIdx.x;
-  if (c >= C) return;
+  __shared__ float sh[2][4][64];
+  const int cl = threadIdx.x & 63, lane = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float a = 0.f, b = 0.f;
-  for (int s = 0; s < splits; ++s) {
-    a += p_dy[(int64_t)s * C + c];
-    b += p_dyx[(int64_t)s * C + c];
+  if (c < C) {
+    int s = lane;
+    for (; s + 12 < splits; s += 16) {
+      float x0[4], x1[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        x0[u] = p_dy[(int64_t)(s + 4 * u) * C + c];
+        x1[u] = p_dyx[(int64_t)(s + 4 * u) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a += x0[u];
+        b += x1[u];
+      }
+    }
+    for (; s < splits; s += 4) {
+      a += p_dy[(int64_t)s * C + c];
+      b += p_dyx[(int64_t)s * C + c];
+    }
   }
+  sh[0][lane][cl] = a;
+  sh[1][lane][cl] = b;
+  __syncthreads();
+  if (lane != 0 || c >= C) return;
+  a = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
+  b = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
   sums[c] = a;
   sums[C + c] = b;
   if (gw) gw[c] = from_f<Tw>(b * invstd[c]);
@@ -469,20 +521,37 @@ __global__ __launch_bounds__(kBlock) void k_dgrad_nhwc(const T* __restrict__ dy,
                                                        const float* __restrict__ sums, const float* __restrict__ count,
                                                        const float* __restrict__ scale, const float* __restrict__ shift,
                                                        bool relu, T* __restrict__ dx, Tz* __restrict__ dz, int64_t M,
-                                                       int C) {
-  const int cv = C / 8;
-  const int64_t nvec = M * cv;
+                                                       int C, int cvb, int R, int64_t rows_per_split) {
+  // dx = dy'*A + x*B + D with per-channel A, B, D computed once per thread (8 channels)
+  const int v = threadIdx.x % cvb, r = threadIdx.x / cvb;
+  const int c0 = (blockIdx.x * cvb + v) * 8;
+  if (r >= R || c0 >= C) return;
+  const int64_t row0 = (int64_t)blockIdx.y * rows_per_split;
+  const int64_t row1 = min(M, row0 + rows_per_split);
   const float inv_n = 1.f / count[0];
-  for (int64_t i = blockIdx.x * (int64_t)kBlock + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * kBlock) {
-    const int c0 = (int)(i % cv) * 8;
+  float A[8], B[8], D[8], sc[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = c0 + k;
+    const float is = invstd[c];
+    const float wv = w ? to_f<Tw>(w[c]) : 1.f;
+    const float mdy = sums[c] * inv_n, mdyx = sums[C + c] * inv_n;
+    A[k] = is * wv;
+    B[k] = -is * is * is * wv * mdyx;
+    D[k] = is * wv * (mean[c] * is * is * mdyx - mdy);
+  }
+  if (relu) {
+    VecIO<float>::load(scale + c0, sc);
+    VecIO<float>::load(shift + c0, sh);
+  }
+  for (int64_t row = row0 + r; row < row1; row += R) {
+    const int64_t off = row * C + c0;
     float g[8], xv[8];
-    VecIO<T>::load(dy + i * 8, g);
-    VecIO<T>::load(x + i * 8, xv);
+    VecIO<T>::load(dy + off, g);
+    VecIO<T>::load(x + off, xv);
     if (relu) {
-      float sc[8], sh[8], zv[8];
-      VecIO<float>::load(scale + c0, sc);
-      VecIO<float>::load(shift + c0, sh);
-      if (z) VecIO<Tz>::load(z + i * 8, zv);
+      float zv[8];
+      if (z) VecIO<Tz>::load(z + off, zv);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float o = fmaf(xv[k], sc[k], sh[k]);
@@ -490,18 +559,10 @@ __global__ __launch_bounds__(kBlock) void k_dgrad_nhwc(const T* __restrict__ dy,
         if (o <= 0.f) g[k] = 0.f;
       }
     }
-    if (dz) VecIO<Tz>::store(dz + i * 8, g);
-    float out[8];
+    if (dz) VecIO<Tz>::store(dz + off, g);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int c = c0 + k;
-      const float is = invstd[c];
-      const float mdy = sums[c] * inv_n;
-      const float mdyx = sums[C + c] * inv_n;
-      const float wv = w ? to_f<Tw>(w[c]) : 1.f;
-      out[k] = (g[k] - mdy - (xv[k] - mean[c]) * is * is * mdyx) * is * wv;
-    }
-    VecIO<T>::store(dx + i * 8, out);
+    for (int k = 0; k < 8; ++k) xv[k] = fmaf(g[k], A[k], fmaf(xv[k], B[k], D[k]));
+    VecIO<T>::store(dx + off, xv);
   }
 }
 
@@ -560,15 +621,16 @@ int grid_for(int64_t work_items) {
 // ==========================================================================================
 // host API (bh/bn_api.h)
 // ==========================================================================================
+// row splits for a streaming NHWC pass: ~target workgroups, >= min_iter rows per lane
+int64_t nhwc_splits(const BNShape& s, int64_t target, int64_t min_iter) {
+  const NhwcGeom g = nhwc_geom(s.C);
+  int64_t splits = std::max<int64_t>(1, target / g.gx);
+  splits = std::min<int64_t>(splits, std::max<int64_t>(1, s.outer / (g.R * min_iter)));
+  return std::max<int64_t>(1, splits);
+}
+
 int bn_num_splits(const BNShape& s) {
-  if (s.channels_last) {
-    const NhwcGeom g = nhwc_geom(s.C);
-    const int64_t rows = s.outer;
-    // aim for ~2048 workgroups, at least 32 row iterations per lane
-    int64_t splits = std::max<int64_t>(1, 2048 / g.gx);
-    splits = std::min<int64_t>(splits, std::max<int64_t>(1, rows / (g.R * 32)));
-    return (int)std::max<int64_t>(1, splits);
-  }
+  if (s.channels_last) return (int)nhwc_splits(s, 1024, 32);
   const int64_t per_c = s.outer * s.inner;
   int64_t splits = std::max<int64_t>(1, 2048 / std::max(1, s.C));
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, per_c / (kBlock * 16)));
@@ -597,7 +659,7 @@ void bn_stats(const BNShape& s, int dt_x, const void* x, int splits, float* pmea
 void bn_stats_finalize(const BNShape& s, int splits, const float* pmean, const float* pm2, const float* pn,
                        float* out_local, const BNFinal& fin, int dt_w, const void* w, const void* b, void* rmean,
                        void* rvar, hipStream_t st) {
-  const int grid = (s.C + kBlock - 1) / kBlock;
+  const int grid = (s.C + 63) / 64;
   const bool per_channel_n = !s.channels_last;
   BN_DISPATCH(dt_w, Tw,
       hipLaunchKernelGGL((k_stats_finalize<Tw>), dim3(grid), dim3(kBlock), 0, st, s.C, splits, per_channel_n, pmean, pm2,
@@ -620,10 +682,12 @@ void bn_forward(const BNShape& s, int dt_x, const void* x, int dt_z, const void*
   if (total == 0) return;
   if (dt_z < 0) dt_z = dt_x;
   if (s.channels_last && s.C % 8 == 0) {
-    const int grid = grid_for(total / 8);
+    const NhwcGeom g = nhwc_geom(s.C);
+    const int64_t splits = nhwc_splits(s, 2048, 4);
+    const int64_t rps = (s.outer + splits - 1) / splits;
     BN_DISPATCH(dt_x, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_y, Ty,
-        hipLaunchKernelGGL((k_fwd_nhwc<T, Tz, Ty>), dim3(grid), dim3(kBlock), 0, st, (const T*)x, (const Tz*)z, (Ty*)y,
-                           scale, shift, s.outer, s.C, relu))));
+        hipLaunchKernelGGL((k_fwd_nhwc<T, Tz, Ty>), dim3(g.gx, splits), dim3(kBlock), 0, st, (const T*)x, (const Tz*)z,
+                           (Ty*)y, scale, shift, s.outer, s.C, g.cvb, g.R, rps, relu))));
   } else {
     const int64_t inner = s.channels_last ? 1 : s.inner;
     const int grid = grid_for(inner % 8 == 0 ? total / 8 : total);
@@ -662,7 +726,7 @@ void bn_backward_reduce(const BNShape& s, int dt, const void* dy, const void* x,
 
 void bn_backward_reduce_finalize(int C, int splits, const float* p_dy, const float* p_dyx, const float* invstd,
                                  float* sums, int dt_w, void* gw, void* gb, hipStream_t st) {
-  const int grid = (C + kBlock - 1) / kBlock;
+  const int grid = (C + 63) / 64;
   BN_DISPATCH(dt_w, Tw,
       hipLaunchKernelGGL((k_bwd_reduce_finalize<Tw>), dim3(grid), dim3(kBlock), 0, st, C, splits, p_dy, p_dyx, invstd,
                          sums, (Tw*)gw, (Tw*)gb));
@@ -677,11 +741,13 @@ void bn_backward_dgrad(const BNShape& s, int dt, const void* dy, const void* x, 
   if (total == 0) return;
   if (dt_z < 0) dt_z = dt;
   if (s.channels_last && s.C % 8 == 0) {
-    const int grid = grid_for(total / 8);
+    const NhwcGeom g = nhwc_geom(s.C);
+    const int64_t splits = nhwc_splits(s, 2048, 4);
+    const int64_t rps = (s.outer + splits - 1) / splits;
     BN_DISPATCH(dt, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_w, Tw,
-        hipLaunchKernelGGL((k_dgrad_nhwc<T, Tz, Tw>), dim3(grid), dim3(kBlock), 0, st, (const T*)dy, (const T*)x,
-                           (const Tz*)z, mean, invstd, (const Tw*)w, sums, count, scale, shift, relu, (T*)dx, (Tz*)dz,
-                           s.outer, s.C))));
+        hipLaunchKernelGGL((k_dgrad_nhwc<T, Tz, Tw>), dim3(g.gx, splits), dim3(kBlock), 0, st, (const T*)dy,
+                           (const T*)x, (const Tz*)z, mean, invstd, (const Tw*)w, sums, count, scale, shift, relu,
+                           (T*)dx, (Tz*)dz, s.outer, s.C, g.cvb, g.R, rps))));
   } else {
     const int64_t inner = s.channels_last ? 1 : s.inner;
     const int grid = grid_for(total);

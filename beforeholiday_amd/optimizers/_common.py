@@ -34,6 +34,7 @@ def grad_like_param(p: torch.Tensor) -> torch.Tensor:
 
 def zero_grad(opt, set_grad_none: bool, set_to_none=None):
     none = set_grad_none if set_to_none is None else set_to_none
+    grads = []
     for group in opt.param_groups:
         for p in group["params"]:
             if p.grad is None:
@@ -45,4 +46,6 @@ def zero_grad(opt, set_grad_none: bool, set_to_none=None):
                     p.grad.detach_()
                 else:
                     p.grad.requires_grad_(False)
-                p.grad.zero_()
+                grads.append(p.grad)
+    if grads:
+        torch._foreach_zero_(grads)

@@ -88,17 +88,21 @@ class FusedAdam(torch.optim.Optimizer):
                 use_master = self.master_weights and p.dtype in (torch.float16, torch.bfloat16)
                 target = self._master(p) if use_master else p
                 if "exp_avg" not in state:
-                    state["exp_avg"] = torch.zeros_like(target)
-                    state["exp_avg_sq"] = torch.zeros_like(target)
+                    # 16-bit params keep fp32 moments: an fp16 exp_avg_sq underflows to 0 for
+                    # |g| < 8e-3 and the update then blows up to inf (the reference stores them in
+                    # the param dtype); the kernel reads/writes fp32 state natively.
+                    sdt = torch.float32 if target.dtype in (torch.float16, torch.bfloat16) else target.dtype
+                    state["exp_avg"] = torch.zeros_like(target, dtype=sdt)
+                    state["exp_avg_sq"] = torch.zeros_like(target, dtype=sdt)
                 g = grad_like_param(p)
-                key = (target.dtype, use_master)
+                key = (target.dtype, state["exp_avg"].dtype, use_master)
                 lists = buckets.setdefault(key, [[], [], [], [], []])
                 lists[0].append(g)
                 lists[1].append(target)
                 lists[2].append(state["exp_avg"])
                 lists[3].append(state["exp_avg_sq"])
                 lists[4].append(p)
-            for (dt, use_master), lists in buckets.items():
+            for (dt, sdt, use_master), lists in buckets.items():
                 if not use_master:
                     lists = lists[:4]
                 if self.capturable:

@@ -1,0 +1,63 @@
+"""Summarise a rocprofv3 kernel trace for steady-state training steps.
+
+Usage: python scripts/prof_summary.py <dir with *_kernel_trace.csv> <marker-regex> [steps] [out.md]
+
+Steps are delimited by occurrences of a marker kernel (one launch per training step, e.g. the
+optimizer's last kernel). The last ``steps`` complete intervals are aggregated by kernel name:
+total / per-step time, share, launch count, and GPU-busy vs. wall span per step (a gap means the
+GPU waited for the host). The big trace CSVs are deleted afterwards so gpurun_out stays small.
+"""
+import collections
+import csv
+import glob
+import os
+import re
+import sys
+
+
+def main():
+    d, marker = sys.argv[1], re.compile(sys.argv[2])
+    nsteps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    out = sys.argv[4] if len(sys.argv) > 4 else os.path.join(d, "summary.md")
+    files = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)
+    rows = []
+    for f in files:
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    marks = [i for i, r in enumerate(rows) if marker.search(r[2])]
+    lines = []
+    if len(marks) < 2:
+        lines.append(f"marker {marker.pattern!r} found {len(marks)} times; aggregating whole trace")
+        lo, hi, n = 0, len(rows), 1
+    else:
+        use = marks[-(nsteps + 1):]
+        lo, hi, n = use[0] + 1, use[-1] + 1, len(use) - 1
+    seg = rows[lo:hi]
+    agg = collections.defaultdict(lambda: [0, 0])
+    busy = 0
+    for s, e, name in seg:
+        short = re.sub(r"\(.*", "", name)[:110]
+        agg[short][0] += e - s
+        agg[short][1] += 1
+        busy += e - s
+    span = (seg[-1][1] - seg[0][0]) if seg else 0
+    lines.append(f"# kernel time per step (last {n} steps, marker {marker.pattern!r})\n")
+    lines.append(f"wall span/step: {span / n / 1e6:.3f} ms; GPU busy/step (sum of kernel times): "
+                 f"{busy / n / 1e6:.3f} ms; kernels/step: {len(seg) / n:.0f}\n")
+    lines.append("| kernel | ms/step | share | launches/step |")
+    lines.append("|---|---|---|---|")
+    for k, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:60]:
+        lines.append(f"| `{k}` | {t / n / 1e6:.3f} | {100.0 * t / max(busy, 1):.1f}% | {c / n:.1f} |")
+    text = "\n".join(lines) + "\n"
+    with open(out, "w") as fh:
+        fh.write(text)
+    print(text)
+    for f in glob.glob(os.path.join(d, "**", "*.csv"), recursive=True):
+        if "kernel_stats" not in f:
+            os.remove(f)
+
+
+if __name__ == "__main__":
+    main()
