@@ -88,6 +88,13 @@ std::vector<at::Tensor> final_outputs(const at::Tensor& ref, int64_t C) {
   auto o = fopt(ref);
   return {at::empty({C}, o), at::empty({C}, o), at::empty({C}, o), at::empty({C}, o), at::empty({1}, o)};
 }
+int64_t* counter_ptr(const c10::optional<at::Tensor>& t) {
+  if (!(t.has_value() && t->defined())) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kLong && t->numel() == 1,
+              "num_batches_tracked must be a GPU int64 scalar tensor");
+  return t->data_ptr<int64_t>();
+}
+
 bh::BNFinal fin_of(std::vector<at::Tensor>& r, double eps, double momentum) {
   bh::BNFinal f{};
   f.mean = r[0].data_ptr<float>();
@@ -114,7 +121,7 @@ void check_running(const c10::optional<at::Tensor>& rm, const c10::optional<at::
 // single-rank fused statistics (no all_gather needed)
 std::vector<at::Tensor> stats_single(at::Tensor x_in, c10::optional<at::Tensor> w, c10::optional<at::Tensor> b,
                                      c10::optional<at::Tensor> rmean, c10::optional<at::Tensor> rvar,
-                                     double momentum, double eps) {
+                                     double momentum, double eps, c10::optional<at::Tensor> num_batches) {
   check_cuda(x_in, "input");
   check_running(rmean, rvar, w);
   Layout L = layout_of(x_in);
@@ -127,6 +134,7 @@ std::vector<at::Tensor> stats_single(at::Tensor x_in, c10::optional<at::Tensor> 
   float* pn = pm2 + (int64_t)splits * C;
   auto r = final_outputs(L.x, C);
   auto fin = fin_of(r, eps, momentum);
+  fin.num_batches = counter_ptr(num_batches);
   hipStream_t st = stream_for(L.x);
   bh::bn_stats(L.s, dtype_code(L.x.scalar_type()), L.x.data_ptr(), splits, pm, pm2, pn, st);
   const bool has_run = rmean.has_value() && rmean->defined();
@@ -140,7 +148,7 @@ std::vector<at::Tensor> stats_single(at::Tensor x_in, c10::optional<at::Tensor> 
 // merge gathered [W, 2C+1] rows (+ running stats update)
 std::vector<at::Tensor> merge_ranks(at::Tensor gathered, c10::optional<at::Tensor> w, c10::optional<at::Tensor> b,
                                     c10::optional<at::Tensor> rmean, c10::optional<at::Tensor> rvar, double momentum,
-                                    double eps) {
+                                    double eps, c10::optional<at::Tensor> num_batches) {
   check_cuda(gathered, "gathered");
   TORCH_CHECK(gathered.dim() == 2 && gathered.scalar_type() == at::kFloat, "gathered must be [W, 2C+1] fp32");
   gathered = gathered.contiguous();
@@ -149,6 +157,7 @@ std::vector<at::Tensor> merge_ranks(at::Tensor gathered, c10::optional<at::Tenso
   const int C = (int)((gathered.size(1) - 1) / 2);
   auto r = final_outputs(gathered, C);
   auto fin = fin_of(r, eps, momentum);
+  fin.num_batches = counter_ptr(num_batches);
   const bool has_run = rmean.has_value() && rmean->defined();
   int dtw = wcode(w);
   if (!(w.has_value() && w->defined()) && has_run) dtw = dtype_code(rmean->scalar_type());
@@ -159,7 +168,7 @@ std::vector<at::Tensor> merge_ranks(at::Tensor gathered, c10::optional<at::Tenso
 }
 
 at::Tensor forward(at::Tensor x_in, c10::optional<at::Tensor> z, at::Tensor scale, at::Tensor shift, bool relu,
-                   c10::optional<at::ScalarType> out_dtype) {
+                   c10::optional<at::ScalarType> out_dtype, c10::optional<at::Tensor> num_batches) {
   check_cuda(x_in, "input");
   Layout L = layout_of(x_in);
   at::Tensor zt;
@@ -169,7 +178,8 @@ at::Tensor forward(at::Tensor x_in, c10::optional<at::Tensor> z, at::Tensor scal
               "scale/shift must be fp32 [C]");
   bh::bn_forward(L.s, dtype_code(L.x.scalar_type()), L.x.data_ptr(), zt.defined() ? dtype_code(zt.scalar_type()) : -1,
                  zt.defined() ? zt.data_ptr() : nullptr, dtype_code(y.scalar_type()), y.data_ptr(),
-                 scale.contiguous().data_ptr<float>(), shift.contiguous().data_ptr<float>(), relu, stream_for(L.x));
+                 scale.contiguous().data_ptr<float>(), shift.contiguous().data_ptr<float>(), relu,
+                 counter_ptr(num_batches), stream_for(L.x));
   return y;
 }
 
@@ -238,11 +248,12 @@ void register_syncbn(pybind11::module_& root) {
   auto m = root.def_submodule("syncbn", "batch-norm statistics / normalisation kernels (gfx950)");
   m.def("stats_local", &stats_local, "local [mean, var_biased, count] of x (all_gather payload)");
   m.def("stats_single", &stats_single, py::arg("x"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"),
-        py::arg("running_var"), py::arg("momentum"), py::arg("eps"));
+        py::arg("running_var"), py::arg("momentum"), py::arg("eps"), py::arg("num_batches") = py::none());
   m.def("merge_ranks", &merge_ranks, py::arg("gathered"), py::arg("weight"), py::arg("bias"),
-        py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"));
+        py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
+        py::arg("num_batches") = py::none());
   m.def("forward", &forward, py::arg("x"), py::arg("z"), py::arg("scale"), py::arg("shift"), py::arg("relu"),
-        py::arg("out_dtype") = py::none());
+        py::arg("out_dtype") = py::none(), py::arg("num_batches") = py::none());
   m.def("backward_reduce", &backward_reduce, py::arg("dy"), py::arg("x"), py::arg("z"), py::arg("mean"),
         py::arg("invstd"), py::arg("scale"), py::arg("shift"), py::arg("relu"), py::arg("weight"),
         py::arg("need_weight_grads"));

@@ -24,7 +24,8 @@ struct BNFinal {
   float* shift;   // b - mean * w * invstd
   float* count;   // total element count per channel (1 float)
   float eps;
-  float momentum; // running stats EMA factor (used when running buffers are passed)
+  float momentum;        // running stats EMA factor; < 0 means cumulative average (momentum=None)
+  int64_t* num_batches;  // optional num_batches_tracked counter, incremented on the device
 };
 
 int bn_num_splits(const BNShape& s);
@@ -41,7 +42,7 @@ void bn_merge_ranks(int W, int C, const float* gathered, const BNFinal& fin, int
                     const void* b, void* rmean, void* rvar, float* var_unbiased, hipStream_t st);
 // y = x*scale + shift (+z) (relu); dt_z = -1 when z is null
 void bn_forward(const BNShape& s, int dt_x, const void* x, int dt_z, const void* z, int dt_y, void* y,
-                const float* scale, const float* shift, bool relu, hipStream_t st);
+                const float* scale, const float* shift, bool relu, int64_t* counter, hipStream_t st);
 // partial sums of dy' and dy'*(x-mean); dy' = dy masked by (x*scale+shift(+z) > 0) when relu
 void bn_backward_reduce(const BNShape& s, int dt, const void* dy, const void* x, int dt_z, const void* z,
                         const float* mean, const float* scale, const float* shift, bool relu, int splits,

@@ -45,12 +45,16 @@ inline void check_launch(const char* what) {
 template <typename T> BH_DEVICE float ld(const T* p, int64_t i) { return to_f<T>(p[i]); }
 template <typename T> BH_DEVICE float ld_or(const T* p, int64_t i, float d) { return p ? to_f<T>(p[i]) : d; }
 
-// per-thread Welford state for 8 channels sharing one count
-struct W8 {
-  float n;
-  float mean[8];
-  float m2[8];
-};
+constexpr int kFinLanes = 16;  // split-lanes of the finalize kernels (block = 64 ch x 16 = 1024)
+
+// running-stat factor: momentum, or 1/(num_batches_tracked+1) for momentum=None (cumulative
+// average). The counter is only READ here; it is incremented by the following forward kernel
+// (stream-ordered after every reader), so all channel threads see the same pre-increment value.
+BH_DEVICE float bn_momentum(const BNFinal& f) {
+  if (f.momentum >= 0.f) return f.momentum;
+  return f.num_batches ? 1.f / (float)(*f.num_batches + 1) : 1.f;
+}
+BH_DEVICE void bn_count_batch(const BNFinal&, int) {}
 
 // ------------------------------------------------------------------------------------------
 // NHWC statistics: grid (channel tiles, splits). Thread t: channel vector v = t % cvb,
@@ -191,23 +195,23 @@ __global__ __launch_bounds__(kBlock) void k_stats_nchw(const T* __restrict__ x, 
 // merge split partials -> local (mean, biased var, count); optionally also the "merge ranks"
 // work for a single rank (running stats, invstd, scale/shift) to save a launch.
 template <typename Tw>
-__global__ __launch_bounds__(kBlock) void k_stats_finalize(int C, int splits, bool per_channel_n,
+__global__ __launch_bounds__(64 * kFinLanes) void k_stats_finalize(int C, int splits, bool per_channel_n,
                                                            const float* __restrict__ pmean, const float* __restrict__ pm2,
                                                            const float* __restrict__ pn, float* __restrict__ out_local,
                                                            BNFinal fin, const Tw* w, const Tw* b, Tw* rmean, Tw* rvar) {
-  // 64 channels x 4 split-lanes per block; each lane walks every 4th split with 4 independent
-  // loads in flight, then the 4 lanes are merged through LDS (no serial latency chain).
-  __shared__ float sh[3][4][64];
+  // 64 channels x kFinLanes split-lanes per block; each lane walks every kFinLanes-th split with 4
+  // independent loads in flight, then the lanes are merged through LDS (short latency chain).
+  __shared__ float sh[3][kFinLanes][64];
   const int cl = threadIdx.x & 63, lane = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   Welford acc{0.f, 0.f, 0.f};
   if (c < C) {
     int s = lane;
-    for (; s + 12 < splits; s += 16) {
+    for (; s + 3 * kFinLanes < splits; s += 4 * kFinLanes) {
       float n[4], m[4], q[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int ss = s + 4 * u;
+        const int ss = s + kFinLanes * u;
         n[u] = per_channel_n ? pn[(int64_t)ss * C + c] : pn[ss];
         m[u] = pmean[(int64_t)ss * C + c];
         q[u] = pm2[(int64_t)ss * C + c];
@@ -215,7 +219,7 @@ __global__ __launch_bounds__(kBlock) void k_stats_finalize(int C, int splits, bo
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc = welford_merge(acc, Welford{n[u], m[u], q[u]});
     }
-    for (; s < splits; s += 4) {
+    for (; s < splits; s += kFinLanes) {
       const float n = per_channel_n ? pn[(int64_t)s * C + c] : pn[s];
       acc = welford_merge(acc, Welford{n, pmean[(int64_t)s * C + c], pm2[(int64_t)s * C + c]});
     }
@@ -225,7 +229,7 @@ __global__ __launch_bounds__(kBlock) void k_stats_finalize(int C, int splits, bo
   sh[2][lane][cl] = acc.m2;
   __syncthreads();
   if (lane != 0 || c >= C) return;
-  for (int l = 1; l < 4; ++l) acc = welford_merge(acc, Welford{sh[0][l][cl], sh[1][l][cl], sh[2][l][cl]});
+  for (int l = 1; l < kFinLanes; ++l) acc = welford_merge(acc, Welford{sh[0][l][cl], sh[1][l][cl], sh[2][l][cl]});
   const float var_b = acc.n > 0.f ? acc.m2 / acc.n : 0.f;
   if (out_local) {
     // all_gather layout of the reference: [mean(C), var_biased(C), count(1)]
@@ -244,9 +248,11 @@ __global__ __launch_bounds__(kBlock) void k_stats_finalize(int C, int splits, bo
     fin.shift[c] = bv - acc.mean * wv * invstd;
     if (rmean) {
       const float unb = acc.n > 1.f ? acc.m2 / (acc.n - 1.f) : var_b;
-      rmean[c] = from_f<Tw>((1.f - fin.momentum) * to_f<Tw>(rmean[c]) + fin.momentum * acc.mean);
-      rvar[c] = from_f<Tw>((1.f - fin.momentum) * to_f<Tw>(rvar[c]) + fin.momentum * unb);
+      const float mom = bn_momentum(fin);
+      rmean[c] = from_f<Tw>((1.f - mom) * to_f<Tw>(rmean[c]) + mom * acc.mean);
+      rvar[c] = from_f<Tw>((1.f - mom) * to_f<Tw>(rvar[c]) + mom * unb);
     }
+    bn_count_batch(fin, c);
   }
 }
 
@@ -279,9 +285,11 @@ __global__ __launch_bounds__(kBlock) void k_merge_ranks(int W, int C, const floa
     fin.shift[c] = bv - acc.mean * wv * invstd;
   }
   if (rmean) {
-    rmean[c] = from_f<Tw>((1.f - fin.momentum) * to_f<Tw>(rmean[c]) + fin.momentum * acc.mean);
-    rvar[c] = from_f<Tw>((1.f - fin.momentum) * to_f<Tw>(rvar[c]) + fin.momentum * unb);
+    const float mom = bn_momentum(fin);
+    rmean[c] = from_f<Tw>((1.f - mom) * to_f<Tw>(rmean[c]) + mom * acc.mean);
+    rvar[c] = from_f<Tw>((1.f - mom) * to_f<Tw>(rvar[c]) + mom * unb);
   }
+  bn_count_batch(fin, c);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -291,8 +299,9 @@ template <typename T, typename Tz, typename Ty>
 __global__ __launch_bounds__(kBlock) void k_fwd_nhwc(const T* __restrict__ x, const Tz* __restrict__ z,
                                                      Ty* __restrict__ y, const float* __restrict__ scale,
                                                      const float* __restrict__ shift, int64_t M, int C, int cvb, int R,
-                                                     int64_t rows_per_split, bool relu) {
+                                                     int64_t rows_per_split, bool relu, int64_t* counter) {
   // thread owns 8 channels (scale/shift in registers for its whole row range), rows strided by R
+  if (counter && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *counter += 1;
   const int v = threadIdx.x % cvb, r = threadIdx.x / cvb;
   const int c0 = (blockIdx.x * cvb + v) * 8;
   if (r >= R || c0 >= C) return;
@@ -322,7 +331,8 @@ template <typename T, typename Tz, typename Ty>
 __global__ __launch_bounds__(kBlock) void k_fwd_generic(const T* __restrict__ x, const Tz* __restrict__ z,
                                                         Ty* __restrict__ y, const float* __restrict__ scale,
                                                         const float* __restrict__ shift, int64_t total, int C,
-                                                        int64_t inner, bool relu) {
+                                                        int64_t inner, bool relu, int64_t* counter) {
+  if (counter && blockIdx.x == 0 && threadIdx.x == 0) *counter += 1;
   const bool vec = (inner % 8 == 0);
   if (vec) {
     for (int64_t i = (blockIdx.x * (int64_t)kBlock + threadIdx.x) * 8; i < total; i += (int64_t)gridDim.x * kBlock * 8) {
@@ -471,22 +481,22 @@ __global__ __launch_bounds__(kBlock) void k_bwd_reduce_generic(const T* __restri
 
 // sum partials; grad_weight = sum_dy_xmu * invstd, grad_bias = sum_dy (local, pre-all-reduce)
 template <typename Tw>
-__global__ __launch_bounds__(kBlock) void k_bwd_reduce_finalize(int C, int splits, const float* __restrict__ p_dy,
+__global__ __launch_bounds__(64 * kFinLanes) void k_bwd_reduce_finalize(int C, int splits, const float* __restrict__ p_dy,
                                                                 const float* __restrict__ p_dyx,
                                                                 const float* __restrict__ invstd,
                                                                 float* __restrict__ sums, Tw* gw, Tw* gb) {
-  __shared__ float sh[2][4][64];
+  __shared__ float sh[2][kFinLanes][64];
   const int cl = threadIdx.x & 63, lane = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   float a = 0.f, b = 0.f;
   if (c < C) {
     int s = lane;
-    for (; s + 12 < splits; s += 16) {
+    for (; s + 3 * kFinLanes < splits; s += 4 * kFinLanes) {
       float x0[4], x1[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        x0[u] = p_dy[(int64_t)(s + 4 * u) * C + c];
-        x1[u] = p_dyx[(int64_t)(s + 4 * u) * C + c];
+        x0[u] = p_dy[(int64_t)(s + kFinLanes * u) * C + c];
+        x1[u] = p_dyx[(int64_t)(s + kFinLanes * u) * C + c];
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -494,7 +504,7 @@ __global__ __launch_bounds__(kBlock) void k_bwd_reduce_finalize(int C, int split
         b += x1[u];
       }
     }
-    for (; s < splits; s += 4) {
+    for (; s < splits; s += kFinLanes) {
       a += p_dy[(int64_t)s * C + c];
       b += p_dyx[(int64_t)s * C + c];
     }
@@ -503,8 +513,12 @@ __global__ __launch_bounds__(kBlock) void k_bwd_reduce_finalize(int C, int split
   sh[1][lane][cl] = b;
   __syncthreads();
   if (lane != 0 || c >= C) return;
-  a = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
-  b = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
+  a = 0.f;
+  b = 0.f;
+  for (int l = 0; l < kFinLanes; ++l) {
+    a += sh[0][l][cl];
+    b += sh[1][l][cl];
+  }
   sums[c] = a;
   sums[C + c] = b;
   if (gw) gw[c] = from_f<Tw>(b * invstd[c]);
@@ -662,7 +676,7 @@ void bn_stats_finalize(const BNShape& s, int splits, const float* pmean, const f
   const int grid = (s.C + 63) / 64;
   const bool per_channel_n = !s.channels_last;
   BN_DISPATCH(dt_w, Tw,
-      hipLaunchKernelGGL((k_stats_finalize<Tw>), dim3(grid), dim3(kBlock), 0, st, s.C, splits, per_channel_n, pmean, pm2,
+      hipLaunchKernelGGL((k_stats_finalize<Tw>), dim3(grid), dim3(64 * kFinLanes), 0, st, s.C, splits, per_channel_n, pmean, pm2,
                          pn, out_local, fin, (const Tw*)w, (const Tw*)b, (Tw*)rmean, (Tw*)rvar));
   check_launch("bn_stats_finalize");
 }
@@ -677,7 +691,7 @@ void bn_merge_ranks(int W, int C, const float* gathered, const BNFinal& fin, int
 }
 
 void bn_forward(const BNShape& s, int dt_x, const void* x, int dt_z, const void* z, int dt_y, void* y,
-                const float* scale, const float* shift, bool relu, hipStream_t st) {
+                const float* scale, const float* shift, bool relu, int64_t* counter, hipStream_t st) {
   const int64_t total = s.outer * s.C * s.inner;
   if (total == 0) return;
   if (dt_z < 0) dt_z = dt_x;
@@ -687,13 +701,13 @@ void bn_forward(const BNShape& s, int dt_x, const void* x, int dt_z, const void*
     const int64_t rps = (s.outer + splits - 1) / splits;
     BN_DISPATCH(dt_x, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_y, Ty,
         hipLaunchKernelGGL((k_fwd_nhwc<T, Tz, Ty>), dim3(g.gx, splits), dim3(kBlock), 0, st, (const T*)x, (const Tz*)z,
-                           (Ty*)y, scale, shift, s.outer, s.C, g.cvb, g.R, rps, relu))));
+                           (Ty*)y, scale, shift, s.outer, s.C, g.cvb, g.R, rps, relu, counter))));
   } else {
     const int64_t inner = s.channels_last ? 1 : s.inner;
     const int grid = grid_for(inner % 8 == 0 ? total / 8 : total);
     BN_DISPATCH(dt_x, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_y, Ty,
         hipLaunchKernelGGL((k_fwd_generic<T, Tz, Ty>), dim3(grid), dim3(kBlock), 0, st, (const T*)x, (const Tz*)z,
-                           (Ty*)y, scale, shift, total, s.C, inner, relu))));
+                           (Ty*)y, scale, shift, total, s.C, inner, relu, counter))));
   }
   check_launch("bn_forward");
 }
@@ -728,7 +742,7 @@ void bn_backward_reduce_finalize(int C, int splits, const float* p_dy, const flo
                                  float* sums, int dt_w, void* gw, void* gb, hipStream_t st) {
   const int grid = (C + 63) / 64;
   BN_DISPATCH(dt_w, Tw,
-      hipLaunchKernelGGL((k_bwd_reduce_finalize<Tw>), dim3(grid), dim3(kBlock), 0, st, C, splits, p_dy, p_dyx, invstd,
+      hipLaunchKernelGGL((k_bwd_reduce_finalize<Tw>), dim3(grid), dim3(64 * kFinLanes), 0, st, C, splits, p_dy, p_dyx, invstd,
                          sums, (Tw*)gw, (Tw*)gb));
   check_launch("bn_backward_reduce_finalize");
 }

@@ -39,7 +39,9 @@ def _ref_stats(x):
     return mean, var_b, n
 
 
-def _ref_final(mean, var_b, n, w, b, rm, rv, momentum, eps):
+def _ref_final(mean, var_b, n, w, b, rm, rv, momentum, eps, num_batches=None):
+    if momentum < 0:  # momentum=None: cumulative average over num_batches_tracked + 1 batches
+        momentum = 1.0 / (float(num_batches.item()) + 1.0) if num_batches is not None else 1.0
     invstd = torch.rsqrt(var_b + eps)
     wv = w.float() if w is not None else torch.ones_like(mean)
     bv = b.float() if b is not None else torch.zeros_like(mean)
@@ -60,28 +62,33 @@ def stats_local(x):
     return torch.cat([mean, var_b, torch.tensor([n], dtype=torch.float32, device=x.device)])
 
 
-def stats_single(x, weight, bias, running_mean, running_var, momentum, eps):
+def stats_single(x, weight, bias, running_mean, running_var, momentum, eps, num_batches=None):
+    """Single-rank statistics -> [mean, invstd, scale, shift, count]; updates running stats with
+    ``momentum`` (< 0: cumulative average using ``num_batches`` = num_batches_tracked)."""
     if x.is_cuda:
-        return _native().stats_single(x, weight, bias, running_mean, running_var, momentum, eps)
+        return _native().stats_single(x, weight, bias, running_mean, running_var, momentum, eps, num_batches)
     mean, var_b, n = _ref_stats(x)
-    return _ref_final(mean, var_b, n, weight, bias, running_mean, running_var, momentum, eps)
+    return _ref_final(mean, var_b, n, weight, bias, running_mean, running_var, momentum, eps, num_batches)
 
 
-def merge_ranks(gathered, weight, bias, running_mean, running_var, momentum, eps):
+def merge_ranks(gathered, weight, bias, running_mean, running_var, momentum, eps, num_batches=None):
     if gathered.is_cuda:
-        return _native().merge_ranks(gathered, weight, bias, running_mean, running_var, momentum, eps)
+        return _native().merge_ranks(gathered, weight, bias, running_mean, running_var, momentum, eps, num_batches)
     C = (gathered.size(1) - 1) // 2
     means, vars_b, ns = gathered[:, :C], gathered[:, C:2 * C], gathered[:, 2 * C:]
     n = ns.sum()
     mean = (means * ns).sum(0) / n
     m2 = (vars_b * ns).sum(0) + (ns * (means - mean) ** 2).sum(0)
     var_b = m2 / n
-    return _ref_final(mean, var_b, float(n), weight, bias, running_mean, running_var, momentum, eps)
+    return _ref_final(mean, var_b, float(n), weight, bias, running_mean, running_var, momentum, eps, num_batches)
 
 
-def forward(x, z, scale, shift, relu, out_dtype=None):
+def forward(x, z, scale, shift, relu, out_dtype=None, num_batches=None):
+    """y = x*scale + shift (+z) (relu); increments ``num_batches`` (num_batches_tracked) if given."""
     if x.is_cuda:
-        return _native().forward(x, z, scale, shift, relu, out_dtype)
+        return _native().forward(x, z, scale, shift, relu, out_dtype, num_batches)
+    if num_batches is not None:
+        num_batches += 1
     y = x.float() * _bcast(scale, x) + _bcast(shift, x)
     if z is not None:
         y = y + z.float()

@@ -27,7 +27,7 @@ def _world(pg):
 class SyncBatchnormFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, input, z, weight, bias, running_mean, running_var, eps, momentum, process_group,
-                channel_last, fuse_relu):
+                channel_last, fuse_relu, num_batches=None):
         input = input.contiguous(memory_format=torch.channels_last) if (channel_last and input.dim() == 4) else input
         world = _world(process_group)
         if world > 1:
@@ -36,11 +36,12 @@ class SyncBatchnormFunction(torch.autograd.Function):
             dist.all_gather_into_tensor(gathered, local, group=process_group)
             gathered = gathered.view(world, local.numel())
             mean, invstd, scale, shift, count = syncbn.merge_ranks(gathered, weight, bias, running_mean,
-                                                                   running_var, momentum, eps)
+                                                                   running_var, momentum, eps, num_batches)
         else:
             mean, invstd, scale, shift, count = syncbn.stats_single(input, weight, bias, running_mean,
-                                                                    running_var, momentum, eps)
-        out = syncbn.forward(input, z, scale, shift, fuse_relu)
+                                                                    running_var, momentum, eps, num_batches)
+        # the normalisation kernel also bumps num_batches_tracked (no separate add kernel)
+        out = syncbn.forward(input, z, scale, shift, fuse_relu, None, num_batches)
         ctx.save_for_backward(input, z, weight, mean, invstd, scale, shift, count)
         ctx.process_group = process_group
         ctx.world = world
@@ -62,7 +63,7 @@ class SyncBatchnormFunction(torch.autograd.Function):
                                                        scale, shift, ctx.fuse_relu,
                                                        ctx.has_z and ctx.needs_input_grad[1])
         return grad_input, grad_z, (gw if need_w else None), (gb if need_w else None), None, None, None, None, None, \
-            None, None
+            None, None, None
 
 
 class SyncBatchNorm(_BatchNorm):
@@ -102,11 +103,11 @@ class SyncBatchNorm(_BatchNorm):
             scale = (w * invstd).contiguous()
             shift = (b - self.running_mean.float() * scale).contiguous()
             return syncbn.forward(input, z, scale, shift, self.fuse_relu)
-        exp_avg = 0.0
-        if self.training and self.track_running_stats:
-            self.num_batches_tracked += 1
-            exp_avg = (1.0 / float(self.num_batches_tracked)) if self.momentum is None else self.momentum
-        rm = self.running_mean if (self.training and self.track_running_stats) else None
-        rv = self.running_var if (self.training and self.track_running_stats) else None
+        tracking = self.training and self.track_running_stats
+        # momentum=None -> cumulative average, computed on the device from num_batches_tracked
+        exp_avg = (self.momentum if self.momentum is not None else -1.0) if tracking else 0.0
+        rm = self.running_mean if tracking else None
+        rv = self.running_var if tracking else None
+        nbt = self.num_batches_tracked if tracking else None
         return SyncBatchnormFunction.apply(input, z, self.weight, self.bias, rm, rv, self.eps, exp_avg,
-                                           self.process_group, self.channel_last, self.fuse_relu)
+                                           self.process_group, self.channel_last, self.fuse_relu, nbt)

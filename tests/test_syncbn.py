@@ -152,3 +152,17 @@ def test_convert_syncbn_model():
     assert isinstance(c[1], SyncBatchNorm) and isinstance(c[2][0], SyncBatchNorm)
     assert isinstance(c[3], torch.nn.InstanceNorm2d)
     assert float(c[1].running_mean[0]) == pytest.approx(0.3)
+
+
+@pytest.mark.parametrize("device", devices())
+@pytest.mark.parametrize("momentum", [0.1, None])
+def test_num_batches_and_cumulative_momentum(device, momentum):
+    torch.manual_seed(3)
+    bn = SyncBatchNorm(16, momentum=momentum).to(device)
+    ref = torch.nn.BatchNorm2d(16, momentum=momentum).to(device)
+    for _ in range(3):
+        x = torch.randn(4, 16, 5, 5, device=device)
+        bn(x), ref(x)
+    assert int(bn.num_batches_tracked) == 3
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(bn.running_var, ref.running_var, rtol=1e-5, atol=1e-5)
