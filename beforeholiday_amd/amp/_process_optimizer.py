@@ -251,16 +251,23 @@ def _process_optimizer(optimizer, properties):
 
         optimizer.step = types.MethodType(new_step, optimizer)
 
-        def new_zero_grad(self, set_to_none=None):
+        def new_zero_grad(self, set_to_none=True):
+            # Default set_to_none=True (PyTorch >= 2.0 semantics): the next _prepare_amp_backward
+            # stashes / drops these grads anyway, so zero-filling them only adds one fill kernel per
+            # parameter plus a stashed-gradient axpby pass after backward. set_to_none=False keeps
+            # the reference's zeroing behaviour.
             stash = self._amp_stash
             self._amp_lazy_init()
             grads = []
             for param in stash.all_fp16_params + stash.all_fp32_from_fp32_params:
                 if param.grad is not None:
-                    param.grad.detach_()
-                    grads.append(param.grad)
+                    if set_to_none:
+                        param.grad = None
+                    else:
+                        param.grad.detach_()
+                        grads.append(param.grad)
             if grads:
-                torch._foreach_zero_(grads)  # one fused launch per dtype instead of one per param
+                torch._foreach_zero_(grads)
             for param in stash.all_fp32_from_fp16_params:
                 param.grad = None
 

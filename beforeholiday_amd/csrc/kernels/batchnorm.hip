@@ -636,6 +636,16 @@ int grid_for(int64_t work_items) {
 // host API (bh/bn_api.h)
 // ==========================================================================================
 // row splits for a streaming NHWC pass: ~target workgroups, >= min_iter rows per lane
+// launch-geometry knobs (env overrides for tuning sweeps: benchmarks/bench_bn.py)
+int64_t env_knob(const char* name, int64_t dflt) {
+  const char* v = getenv(name);
+  return v ? atoll(v) : dflt;
+}
+int64_t knob_ew_blocks() { static const int64_t v = env_knob("BH_BN_EW_BLOCKS", 2048); return v; }
+int64_t knob_ew_rows() { static const int64_t v = env_knob("BH_BN_EW_ROWS", 4); return v; }
+int64_t knob_red_blocks() { static const int64_t v = env_knob("BH_BN_RED_BLOCKS", 1024); return v; }
+int64_t knob_red_rows() { static const int64_t v = env_knob("BH_BN_RED_ROWS", 32); return v; }
+
 int64_t nhwc_splits(const BNShape& s, int64_t target, int64_t min_iter) {
   const NhwcGeom g = nhwc_geom(s.C);
   int64_t splits = std::max<int64_t>(1, target / g.gx);
@@ -644,7 +654,7 @@ int64_t nhwc_splits(const BNShape& s, int64_t target, int64_t min_iter) {
 }
 
 int bn_num_splits(const BNShape& s) {
-  if (s.channels_last) return (int)nhwc_splits(s, 1024, 32);
+  if (s.channels_last) return (int)nhwc_splits(s, knob_red_blocks(), knob_red_rows());
   const int64_t per_c = s.outer * s.inner;
   int64_t splits = std::max<int64_t>(1, 2048 / std::max(1, s.C));
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, per_c / (kBlock * 16)));
@@ -697,7 +707,7 @@ void bn_forward(const BNShape& s, int dt_x, const void* x, int dt_z, const void*
   if (dt_z < 0) dt_z = dt_x;
   if (s.channels_last && s.C % 8 == 0) {
     const NhwcGeom g = nhwc_geom(s.C);
-    const int64_t splits = nhwc_splits(s, 2048, 4);
+    const int64_t splits = nhwc_splits(s, knob_ew_blocks(), knob_ew_rows());
     const int64_t rps = (s.outer + splits - 1) / splits;
     BN_DISPATCH(dt_x, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_y, Ty,
         hipLaunchKernelGGL((k_fwd_nhwc<T, Tz, Ty>), dim3(g.gx, splits), dim3(kBlock), 0, st, (const T*)x, (const Tz*)z,
@@ -756,7 +766,7 @@ void bn_backward_dgrad(const BNShape& s, int dt, const void* dy, const void* x, 
   if (dt_z < 0) dt_z = dt;
   if (s.channels_last && s.C % 8 == 0) {
     const NhwcGeom g = nhwc_geom(s.C);
-    const int64_t splits = nhwc_splits(s, 2048, 4);
+    const int64_t splits = nhwc_splits(s, knob_ew_blocks(), knob_ew_rows());
     const int64_t rps = (s.outer + splits - 1) / splits;
     BN_DISPATCH(dt, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_w, Tw,
         hipLaunchKernelGGL((k_dgrad_nhwc<T, Tz, Tw>), dim3(g.gx, splits), dim3(kBlock), 0, st, (const T*)dy,
