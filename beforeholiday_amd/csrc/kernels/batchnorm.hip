@@ -543,16 +543,24 @@ __global__ __launch_bounds__(kBlock) void k_dgrad_nhwc(const T* __restrict__ dy,
   const int64_t row0 = (int64_t)blockIdx.y * rows_per_split;
   const int64_t row1 = min(M, row0 + rows_per_split);
   const float inv_n = 1.f / count[0];
-  float A[8], B[8], D[8], sc[8], sh[8];
+  // per-channel coefficients from 16-byte vector loads (one latency round, not 40 scalar loads)
+  float A[8], B[8], D[8], sc[8], sh[8], is[8], mu[8], sdy[8], sdx[8], wv[8];
+  VecIO<float>::load(invstd + c0, is);
+  VecIO<float>::load(mean + c0, mu);
+  VecIO<float>::load(sums + c0, sdy);
+  VecIO<float>::load(sums + C + c0, sdx);
+  if (w) {
+    VecIO<Tw>::load(w + c0, wv);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) wv[k] = 1.f;
+  }
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const int c = c0 + k;
-    const float is = invstd[c];
-    const float wv = w ? to_f<Tw>(w[c]) : 1.f;
-    const float mdy = sums[c] * inv_n, mdyx = sums[C + c] * inv_n;
-    A[k] = is * wv;
-    B[k] = -is * is * is * wv * mdyx;
-    D[k] = is * wv * (mean[c] * is * is * mdyx - mdy);
+    const float mdy = sdy[k] * inv_n, mdyx = sdx[k] * inv_n;
+    A[k] = is[k] * wv[k];
+    B[k] = -is[k] * is[k] * is[k] * wv[k] * mdyx;
+    D[k] = is[k] * wv[k] * (mu[k] * is[k] * is[k] * mdyx - mdy);
   }
   if (relu) {
     VecIO<float>::load(scale + c0, sc);
@@ -642,7 +650,7 @@ int64_t env_knob(const char* name, int64_t dflt) {
   return v ? atoll(v) : dflt;
 }
 int64_t knob_ew_blocks() { static const int64_t v = env_knob("BH_BN_EW_BLOCKS", 2048); return v; }
-int64_t knob_ew_rows() { static const int64_t v = env_knob("BH_BN_EW_ROWS", 4); return v; }
+int64_t knob_ew_rows() { static const int64_t v = env_knob("BH_BN_EW_ROWS", 8); return v; }
 int64_t knob_red_blocks() { static const int64_t v = env_knob("BH_BN_RED_BLOCKS", 1024); return v; }
 int64_t knob_red_rows() { static const int64_t v = env_knob("BH_BN_RED_ROWS", 32); return v; }
 
