@@ -8,4 +8,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("arch") = "gfx950";
   bhb::register_amp_C(m);
   bhb::register_syncbn(m);
+  bhb::register_norms(m);
 }

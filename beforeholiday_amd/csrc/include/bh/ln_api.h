@@ -1,0 +1,26 @@
+// LayerNorm / RMSNorm launcher API (kernels: csrc/kernels/layer_norm.hip).
+// Rows: n1 (product of the leading dims), row length n2 (product of normalized_shape).
+// `vec` = n2 % 8 == 0 and every pointer 16-byte aligned (host decides).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bh {
+
+// y = (x - mean) * invvar * gamma + beta   (rms: mean = 0, no beta); gamma/beta may be null.
+// dt_w = -1 when there are no affine params. mean may be null for rms.
+void ln_forward(int64_t n1, int n2, int dt_x, const void* x, int dt_w, const void* gamma, const void* beta,
+                int dt_y, void* y, float* mean, float* invvar, float eps, bool rms, bool vec, hipStream_t st);
+// dx; xin is the input x, or the output y when from_output (memory-efficient mode)
+void ln_backward_dx(int64_t n1, int n2, int dt_dy, const void* dy, int dt_x, const void* xin, const float* mean,
+                    const float* invvar, int dt_w, const void* gamma, const void* beta, void* dx, bool rms,
+                    bool from_output, bool vec, hipStream_t st);
+int ln_wgrad_splits(int64_t n1, int n2);
+// grad_gamma / grad_beta (may be null); partials: 2 * splits * n2 floats of scratch
+void ln_backward_wgrad(int64_t n1, int n2, int dt_dy, const void* dy, int dt_x, const void* xin, const float* mean,
+                       const float* invvar, int dt_w, const void* gamma, const void* beta, void* grad_gamma,
+                       void* grad_beta, float* partials, int splits, bool rms, bool from_output, bool vec,
+                       hipStream_t st);
+
+}  // namespace bh
