@@ -9,4 +9,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   bhb::register_amp_C(m);
   bhb::register_syncbn(m);
   bhb::register_norms(m);
+  bhb::register_softmax(m);
 }
