@@ -93,16 +93,21 @@ def rms_forward(input, normalized_shape, eps):
     return _ref_fwd(input, normalized_shape, None, None, eps, True, input.dtype)
 
 
+def _mean_or_empty(mean, ref):
+    # memory-efficient backward recomputes x_hat from the output: mean is not needed (None)
+    return mean if mean is not None else ref.new_empty(0, dtype=torch.float32)
+
+
 def backward_affine(dout, mean, invvar, input_or_output, normalized_shape, gamma, beta, eps, memory_efficient=False):
     if dout.is_cuda:
-        return _n().backward_affine(dout, mean, invvar, input_or_output, normalized_shape, gamma, beta, eps,
+        return _n().backward_affine(dout, _mean_or_empty(mean, dout), invvar, input_or_output, normalized_shape, gamma, beta, eps,
                                     memory_efficient)
     return _ref_bwd(dout, mean, invvar, input_or_output, normalized_shape, gamma, beta, eps, False, memory_efficient)
 
 
 def backward(dout, mean, invvar, input_or_output, normalized_shape, eps, memory_efficient=False):
     if dout.is_cuda:
-        return _n().backward(dout, mean, invvar, input_or_output, normalized_shape, eps, memory_efficient)
+        return _n().backward(dout, _mean_or_empty(mean, dout), invvar, input_or_output, normalized_shape, eps, memory_efficient)
     return _ref_bwd(dout, mean, invvar, input_or_output, normalized_shape, None, None, eps, False, memory_efficient)[0]
 
 
