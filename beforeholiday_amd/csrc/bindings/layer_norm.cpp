@@ -72,7 +72,11 @@ std::vector<at::Tensor> bwd_impl(at::Tensor dout, at::Tensor mean, at::Tensor in
   auto dx = at::empty_like(xin);
   const bool vec = use_vec(d.n2, {dout, xin, gamma, beta, dx});
   hipStream_t s = stream_for(xin);
-  const float* mp = rms ? nullptr : mean.data_ptr<float>();
+  // memory-efficient backward recomputes x_hat from the output: mean is not saved and never read
+  const float* mp = (rms || memory_efficient) ? nullptr : mean.data_ptr<float>();
+  TORCH_CHECK(rms || memory_efficient || mean.numel() == d.n1, "layer_norm backward: mean has ", mean.numel(),
+              " elements, expected ", d.n1);
+  TORCH_CHECK(invvar.numel() == d.n1, "layer_norm backward: invvar has ", invvar.numel(), " elements, expected ", d.n1);
   bh::ln_backward_dx(d.n1, d.n2, dtype_code(dout.scalar_type()), dout.data_ptr(), dtype_code(xin.scalar_type()),
                      xin.data_ptr(), mp, invvar.data_ptr<float>(), wc(gamma), wp(gamma), wp(beta), dx.data_ptr(), rms,
                      memory_efficient, vec, s);

@@ -10,4 +10,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   bhb::register_syncbn(m);
   bhb::register_norms(m);
   bhb::register_softmax(m);
+  bhb::register_dense(m);
 }

@@ -110,6 +110,34 @@ at::Tensor xent_bwd(at::Tensor grad_loss, at::Tensor logits, at::Tensor lse, at:
   return dx;
 }
 
+// vocab-parallel CE: logits [rows, V] (this rank's shard), target [rows] global ids
+at::Tensor vp_stats(at::Tensor logits, at::Tensor target, int64_t start) {
+  check_cuda(logits, "logits");
+  logits = logits.contiguous();
+  target = target.to(at::kLong).contiguous();
+  const int64_t V = logits.size(-1), N = logits.numel() / std::max<int64_t>(V, 1);
+  TORCH_CHECK(target.numel() == N, "vocab_parallel_xent: target has ", target.numel(), " elements, expected ", N);
+  auto stats = at::empty({N, 4}, logits.options().dtype(at::kFloat));
+  const bool vec = (V % 8 == 0) && al16(logits);
+  bh::vocab_xent_stats(dtype_code(logits.scalar_type()), logits.data_ptr(), target.data_ptr<int64_t>(),
+                       stats.data_ptr<float>(), N, (int)V, start, vec, stream_for(logits));
+  return stats;
+}
+
+// gathered [world, rows, 4] -> (loss[rows] in out_dtype, lse[rows] fp32)
+std::vector<at::Tensor> vp_combine(at::Tensor gathered, at::ScalarType out_dtype) {
+  check_cuda(gathered, "stats");
+  gathered = gathered.contiguous();
+  TORCH_CHECK(gathered.dim() == 3 && gathered.size(2) == 4 && gathered.scalar_type() == at::kFloat,
+              "vocab_parallel_xent: stats must be float [world, rows, 4]");
+  const int64_t rows = gathered.size(1);
+  auto loss = at::empty({rows}, gathered.options().dtype(out_dtype));
+  auto lse = at::empty({rows}, gathered.options());
+  bh::vocab_xent_combine(gathered.data_ptr<float>(), (int)gathered.size(0), rows, dtype_code(out_dtype),
+                         loss.data_ptr(), lse.data_ptr<float>(), stream_for(gathered));
+  return {loss, lse};
+}
+
 }  // namespace
 
 void register_softmax(pybind11::module_& root) {
@@ -130,6 +158,8 @@ void register_softmax(pybind11::module_& root) {
   auto xent = root.def_submodule("xentropy_cuda", "softmax cross-entropy with label smoothing");
   xent.def("forward", &xent_fwd);
   xent.def("backward", &xent_bwd);
+  xent.def("vocab_parallel_stats", &vp_stats);
+  xent.def("vocab_parallel_combine", &vp_combine);
 }
 
 }  // namespace bhb

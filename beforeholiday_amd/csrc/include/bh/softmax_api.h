@@ -19,4 +19,11 @@ void xentropy_forward(int dt, const void* x, const int64_t* labels, int dt_loss,
 void xentropy_backward(int dt, const void* x, int dt_g, const void* gloss, const float* lse, const int64_t* labels,
                        void* dx, int64_t rows, int V, float smoothing, bool vec, hipStream_t st);
 
+// vocab-parallel cross-entropy: per-row shard partials stats[rows][4] = {max, sumexp, target logit, 0}
+void vocab_xent_stats(int dt, const void* x, const int64_t* target, float* stats, int64_t rows, int V, int64_t start,
+                      bool vec, hipStream_t st);
+// stats [world][rows][4] -> loss[rows] (dtype dt_loss), lse[rows]
+void vocab_xent_combine(const float* stats, int world, int64_t rows, int dt_loss, void* loss, float* lse,
+                        hipStream_t st);
+
 }  // namespace bh

@@ -1,0 +1,196 @@
+// Dense-layer epilogue kernels (gfx950): activation forward, fused activation-backward + bias-grad.
+//
+// Reference behaviour: csrc/fused_dense_cuda.cu (hipBLASLt epilogues BIAS / BGRADB / GELU_AUX_BIAS /
+// DGELU_BGRAD, :223-294) and csrc/mlp_cuda.cu (bias+ReLU/sigmoid kernels, bias-grad reductions).
+// The reference's linear_gelu_linear_backward never applies dGELU; here it does.
+//
+// MI355X design: the GEMMs run on hipBLASLt (bias folded into its epilogue by at::addmm); these
+// kernels are the memory-bound halves, each a single pass over the activation:
+//  * act_fwd:   y = act(x (+ bias)), 16-byte vectors, in place allowed.
+//  * act_bwd:   dx = dy * act'(aux) AND the bias gradient sum_m dx in the same pass. Columns are
+//    owned by lanes (8 columns per lane, 32 lanes = 256 columns per workgroup, 8 row lanes), each
+//    workgroup reduces a row-chunk into an fp32 partial [split][N]; a second tiny kernel sums the
+//    splits in a fixed order (deterministic, no atomics).
+#include "bh/api.h"
+#include "bh/dense_api.h"
+#include "bh/device.h"
+
+#include <stdexcept>
+#include <string>
+
+namespace bh {
+namespace {
+
+constexpr int kColLanes = 32;
+constexpr int kRowLanes = 8;
+constexpr int kCols = kColLanes * 8;  // columns per workgroup
+
+#define DN_DISPATCH(code, T, ...)                                          \
+  switch (code) {                                                          \
+    case kF32: { using T = float; __VA_ARGS__; } break;                    \
+    case kF16: { using T = f16; __VA_ARGS__; } break;                      \
+    case kBF16: { using T = bf16; __VA_ARGS__; } break;                    \
+    default: throw std::runtime_error("dense: unsupported dtype " + std::to_string(code)); \
+  }
+
+inline void check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+BH_DEVICE float act_f(float v, int act) {
+  switch (act) {
+    case kActRelu: return fmaxf(v, 0.f);
+    case kActSigmoid: return 1.f / (1.f + __expf(-v));
+    case kActGelu: return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+    case kActGeluTanh: {
+      const float u = 0.7978845608028654f * (v + 0.044715f * v * v * v);
+      return 0.5f * v * (1.f + tanhf(u));
+    }
+    default: return v;
+  }
+}
+
+// derivative given aux: ReLU/sigmoid take the activation OUTPUT, GELU the pre-activation
+BH_DEVICE float act_d(float a, int act) {
+  switch (act) {
+    case kActRelu: return a > 0.f ? 1.f : 0.f;
+    case kActSigmoid: return a * (1.f - a);
+    case kActGelu: {
+      const float cdf = 0.5f * (1.f + erff(a * 0.70710678118654752f));
+      const float pdf = 0.3989422804014327f * __expf(-0.5f * a * a);
+      return cdf + a * pdf;
+    }
+    case kActGeluTanh: {
+      const float k = 0.7978845608028654f;
+      const float u = k * (a + 0.044715f * a * a * a);
+      const float t = tanhf(u);
+      return 0.5f * (1.f + t) + 0.5f * a * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * a * a);
+    }
+    default: return 1.f;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_act_fwd(const T* __restrict__ x, const T* __restrict__ bias,
+                                                 T* __restrict__ y, int64_t M, int N, int act, bool vec) {
+  const int64_t total = M * (int64_t)N;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < total; i += stride) {
+    float v[8];
+    if (vec && i + 8 <= total) {
+      VecIO<T>::load(x + i, v);
+      if (bias) {
+        float b[8];
+        VecIO<T>::load(bias + (i % N), b);  // N % 8 == 0 on the vector path: 8 columns of one row
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] += b[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = act_f(v[k], act);
+      VecIO<T>::store(y + i, v);
+    } else {
+      for (int k = 0; k < 8 && i + k < total; ++k) {
+        float a = to_f<T>(x[i + k]);
+        if (bias) a += to_f<T>(bias[(i + k) % N]);
+        y[i + k] = from_f<T>(act_f(a, act));
+      }
+    }
+  }
+}
+
+// grid (ceil(N / kCols), splits); block (kColLanes, kRowLanes)
+template <typename T>
+__global__ __launch_bounds__(256) void k_act_bwd(const T* __restrict__ dy, const T* __restrict__ aux,
+                                                 T* __restrict__ dx, float* __restrict__ part, int64_t M, int N,
+                                                 int64_t rows_per_split, int act, bool vec) {
+  __shared__ float red[kRowLanes][kCols + 4];
+  const int col0 = blockIdx.x * kCols + threadIdx.x * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_split;
+  const int64_t r1 = r0 + rows_per_split < M ? r0 + rows_per_split : M;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (col0 < N) {
+    for (int64_t r = r0 + threadIdx.y; r < r1; r += kRowLanes) {
+      const int64_t off = r * N + col0;
+      float g[8], a[8];
+      if (vec && col0 + 8 <= N) {
+        VecIO<T>::load(dy + off, g);
+        if (act != kActNone) VecIO<T>::load(aux + off, a);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (act != kActNone) g[k] *= act_d(a[k], act);
+          acc[k] += g[k];
+        }
+        if (dx) VecIO<T>::store(dx + off, g);
+      } else {
+        for (int k = 0; k < 8 && col0 + k < N; ++k) {
+          float gv = to_f<T>(dy[off + k]);
+          if (act != kActNone) gv *= act_d(to_f<T>(aux[off + k]), act);
+          acc[k] += gv;
+          if (dx) dx[off + k] = from_f<T>(gv);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[threadIdx.y][threadIdx.x * 8 + k] = acc[k];
+  __syncthreads();
+  const int t = threadIdx.y * kColLanes + threadIdx.x;  // 256 threads -> 256 columns
+  const int c = blockIdx.x * kCols + t;
+  if (c < N) {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < kRowLanes; ++j) s += red[j][t];
+    part[(int64_t)blockIdx.y * N + c] = s;
+  }
+}
+
+template <typename T>
+__global__ void k_colsum_finalize(const float* __restrict__ part, int splits, int N, T* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= N) return;
+  float s = 0.f;
+  for (int j = 0; j < splits; ++j) s += part[(int64_t)j * N + c];
+  out[c] = from_f<T>(s);
+}
+
+}  // namespace
+
+void dense_act_forward(int dt, const void* x, const void* bias, void* y, int64_t M, int N, int act, bool vec,
+                       hipStream_t st) {
+  const int64_t total = M * (int64_t)N;
+  if (total == 0) return;
+  int64_t blocks = (total / 8 + 255) / 256 + 1;
+  if (blocks > 8192) blocks = 8192;
+  DN_DISPATCH(dt, T, hipLaunchKernelGGL((k_act_fwd<T>), dim3((unsigned)blocks), dim3(256), 0, st, (const T*)x,
+                                        (const T*)bias, (T*)y, M, N, act, vec));
+  check_launch("dense_act_forward");
+}
+
+int dense_bgrad_splits(int64_t M, int N) {
+  const int64_t col_blocks = (N + kCols - 1) / kCols;
+  int64_t splits = (2048 + col_blocks - 1) / col_blocks;       // aim for ~2048 workgroups
+  const int64_t max_splits = (M + 63) / 64;                    // >= 64 rows per split
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  if (splits > 1024) splits = 1024;
+  return (int)splits;
+}
+
+void dense_act_backward(int dt, const void* dy, const void* aux, void* dx, void* bgrad, float* part, int splits,
+                        int64_t M, int N, int act, bool vec, hipStream_t st) {
+  if (N == 0) return;
+  const int64_t rps = M > 0 ? (M + splits - 1) / splits : 1;
+  dim3 grid((unsigned)((N + kCols - 1) / kCols), (unsigned)splits);
+  DN_DISPATCH(dt, T,
+      hipLaunchKernelGGL((k_act_bwd<T>), grid, dim3(kColLanes, kRowLanes), 0, st, (const T*)dy, (const T*)aux,
+                         (T*)dx, part, M, N, rps, act, vec);
+      check_launch("dense_act_backward");
+      if (bgrad) {
+        hipLaunchKernelGGL((k_colsum_finalize<T>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, part, splits,
+                           N, (T*)bgrad);
+        check_launch("dense_bgrad_finalize");
+      });
+}
+
+}  // namespace bh

@@ -164,7 +164,7 @@ __global__ __launch_bounds__(kBlock) void k_ln_bwd_dx(const Tdy* __restrict__ dy
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
   if (row >= n1) return;
-  const float mean = RMS ? 0.f : mean_in[row];
+  const float mean = (RMS || from_output) ? 0.f : mean_in[row];  // memory-efficient: mean not saved
   const float invvar = invvar_in[row];
   float xh[VPT][8], dg[VPT][8];
   float s1 = 0.f, s2 = 0.f;
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(kBlock) void k_ln_bwd_dx_long(const Tdy* __restrict
                                                            T* __restrict__ dx, int n2, bool from_output) {
   __shared__ float red[kBlock / kWave];
   const int64_t row = blockIdx.x;
-  const float mean = RMS ? 0.f : mean_in[row];
+  const float mean = (RMS || from_output) ? 0.f : mean_in[row];  // memory-efficient: mean not saved
   const float invvar = invvar_in[row];
   auto xhat = [&](int i) -> float {
     const float xv = to_f<T>(xin[row * n2 + i]);

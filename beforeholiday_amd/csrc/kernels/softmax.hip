@@ -248,6 +248,76 @@ __global__ __launch_bounds__(kBlock) void k_xent_bwd(const Tg* __restrict__ glos
   }
 }
 
+
+// ------------------------------------------------------------------------------------------
+// vocab-parallel cross-entropy partials: ONE pass over this rank's vocab shard per row with an
+// online (max, sum-exp) pair, plus the target logit when the target falls in [start, start+V).
+// stats[row] = {max, sum exp(x - max), target logit or 0, 0}. Ranks exchange these 16 bytes per row
+// with a single all-gather (instead of three full-row all-reduces) and combine them in k_vp_combine.
+// ------------------------------------------------------------------------------------------
+BH_DEVICE void ms_merge(float& m, float& s, float m2, float s2) {
+  const float mn = fmaxf(m, m2);
+  if (mn == -INFINITY) return;
+  s = s * __expf(m - mn) + s2 * __expf(m2 - mn);
+  m = mn;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_vp_stats(const T* __restrict__ x, const int64_t* __restrict__ target,
+                                                     float4* __restrict__ stats, int V, int64_t start, bool vec) {
+  __shared__ float red[2 * (kBlock / kWave)];
+  const int64_t row = blockIdx.x;
+  const T* xr = x + row * V;
+  float m = -INFINITY, s = 0.f;
+  for (int col = threadIdx.x * 8; col < V; col += kBlock * 8) {
+    float v[8];
+    ld8(xr, col, V, vec, v, -INFINITY);
+    float cm = v[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) cm = fmaxf(cm, v[k]);
+    float cs = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cs += __expf(v[k] - cm);
+    ms_merge(m, s, cm, cs);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(m, o, kWave);
+    const float s2 = __shfl_xor(s, o, kWave);
+    ms_merge(m, s, m2, s2);
+  }
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (lane == 0) {
+    red[2 * wid] = m;
+    red[2 * wid + 1] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = red[0], S = red[1];
+    for (int w = 1; w < kBlock / kWave; ++w) ms_merge(M, S, red[2 * w], red[2 * w + 1]);
+    const int64_t t = target[row] - start;
+    const float xt = (t >= 0 && t < V) ? to_f<T>(xr[t]) : 0.f;
+    stats[row] = make_float4(M, S, xt, 0.f);
+  }
+}
+
+// gathered stats [world][rows] -> loss[row] = log(sum_r S_r e^{M_r - M}) + M - sum_r t_r, lse[row]
+template <typename To>
+__global__ void k_vp_combine(const float4* __restrict__ stats, int world, int64_t rows, To* __restrict__ loss,
+                             float* __restrict__ lse) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= rows) return;
+  float M = -INFINITY, S = 0.f, xt = 0.f;
+  for (int r = 0; r < world; ++r) {
+    const float4 st = stats[(int64_t)r * rows + row];
+    ms_merge(M, S, st.x, st.y);
+    xt += st.z;
+  }
+  const float l = M + __logf(S);
+  lse[row] = l;
+  loss[row] = from_f<To>(l - xt);
+}
+
 #define SM_SHAPE_DISPATCH(sk, G, V, ...)                                               \
   if (sk <= 512) { constexpr int G = kWave; constexpr int V = 1; __VA_ARGS__; }        \
   else if (sk <= 1024) { constexpr int G = kWave; constexpr int V = 2; __VA_ARGS__; }  \
@@ -299,6 +369,23 @@ void xentropy_backward(int dt, const void* x, int dt_g, const void* gloss, const
       hipLaunchKernelGGL((k_xent_bwd<T, Tg>), dim3((unsigned)rows), dim3(kBlock), 0, st, (const Tg*)gloss, (const T*)x,
                          lse, labels, (T*)dx, V, smoothing, vec)));
   check_launch("xentropy_backward");
+}
+
+void vocab_xent_stats(int dt, const void* x, const int64_t* target, float* stats, int64_t rows, int V, int64_t start,
+                      bool vec, hipStream_t st) {
+  if (rows == 0) return;
+  SM_DISPATCH(dt, T, hipLaunchKernelGGL((k_vp_stats<T>), dim3((unsigned)rows), dim3(kBlock), 0, st, (const T*)x, target,
+                                        (float4*)stats, V, start, vec));
+  check_launch("vocab_xent_stats");
+}
+
+void vocab_xent_combine(const float* stats, int world, int64_t rows, int dt_loss, void* loss, float* lse,
+                        hipStream_t st) {
+  if (rows == 0) return;
+  const unsigned grid = (unsigned)((rows + kBlock - 1) / kBlock);
+  SM_DISPATCH(dt_loss, To, hipLaunchKernelGGL((k_vp_combine<To>), dim3(grid), dim3(kBlock), 0, st,
+                                              (const float4*)stats, world, rows, (To*)loss, lse));
+  check_launch("vocab_xent_combine");
 }
 
 }  // namespace bh

@@ -1,0 +1,144 @@
+"""``fused_dense_cuda`` / ``mlp_cuda`` / ``fused_weight_gradient_mlp_cuda`` ops.
+
+GPU tensors run ``beforeholiday_amd._C`` (GEMMs on hipBLASLt via ATen, activation / dActivation /
+bias-grad passes in kernels/dense.hip); CPU tensors run the PyTorch reference below with the same
+semantics (exact-erf GELU; ReLU / sigmoid derivatives taken from the activation output).
+"""
+from typing import List, Optional
+
+import torch
+import torch.nn.functional as F
+
+from .._native import submodule
+
+ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_GELU, ACT_GELU_TANH = 0, 1, 2, 3, 4
+
+
+def _fd():
+    return submodule("fused_dense_cuda")
+
+
+def _act_ref(x, act):
+    if act == ACT_RELU:
+        return torch.relu(x)
+    if act == ACT_SIGMOID:
+        return torch.sigmoid(x)
+    if act == ACT_GELU:
+        return F.gelu(x)
+    if act == ACT_GELU_TANH:
+        return F.gelu(x, approximate="tanh")
+    return x
+
+
+def _act_grad_ref(dy, aux, act):
+    a = aux.float()
+    if act == ACT_RELU:
+        d = (a > 0).float()
+    elif act == ACT_SIGMOID:
+        d = a * (1 - a)
+    elif act == ACT_GELU:
+        d = 0.5 * (1 + torch.erf(a * 0.7071067811865476)) + a * 0.3989422804014327 * torch.exp(-0.5 * a * a)
+    elif act == ACT_GELU_TANH:
+        k = 0.7978845608028654
+        t = torch.tanh(k * (a + 0.044715 * a ** 3))
+        d = 0.5 * (1 + t) + 0.5 * a * (1 - t * t) * k * (1 + 3 * 0.044715 * a * a)
+    else:
+        return dy
+    return (dy.float() * d).to(dy.dtype)
+
+
+def bias_act_forward(x: torch.Tensor, bias: Optional[torch.Tensor], act: int) -> torch.Tensor:
+    """act(x + bias) in one pass."""
+    if x.is_cuda:
+        return _fd().act_forward(x, bias, act)
+    return _act_ref(x + bias if bias is not None else x, act)
+
+
+def act_backward(dy: torch.Tensor, aux: torch.Tensor, act: int, want_bgrad: bool):
+    """(dy * act'(aux), sum over rows of it) in one pass."""
+    if dy.is_cuda:
+        dx, db = _fd().act_backward(dy, aux, act, want_bgrad)
+        return dx, (db if want_bgrad else None)
+    dx = _act_grad_ref(dy, aux, act)
+    return dx, (dx.reshape(-1, dx.size(-1)).float().sum(0).to(dx.dtype) if want_bgrad else None)
+
+
+def linear_bias_forward(input, weight, bias):
+    if input.is_cuda:
+        return _fd().linear_bias_forward(input, weight, bias)
+    return F.linear(input, weight, bias)
+
+
+def linear_bias_backward(input, weight, d_output):
+    if input.is_cuda:
+        return _fd().linear_bias_backward(input, weight, d_output)
+    dy = d_output.reshape(-1, d_output.size(-1))
+    x = input.reshape(-1, input.size(-1))
+    return (dy.mm(weight).view(input.shape), dy.t().mm(x), dy.sum(0))
+
+
+def linear_gelu_linear_forward(input, weight1, bias1, weight2, bias2):
+    """Returns (gelu_in, gelu_out, output)."""
+    if input.is_cuda:
+        return _fd().linear_gelu_linear_forward(input, weight1, bias1, weight2, bias2)
+    x = input.reshape(-1, input.size(-1))
+    gelu_in = F.linear(x, weight1, bias1)
+    h = F.gelu(gelu_in)
+    return gelu_in, h, F.linear(h, weight2, bias2)
+
+
+def linear_gelu_linear_backward(input, gelu_in, output1, weight1, weight2, d_output2):
+    """Returns (d_input, d_weight1, d_bias1, d_weight2, d_bias2) — with the dGELU applied."""
+    if input.is_cuda:
+        return _fd().linear_gelu_linear_backward(input, gelu_in, output1, weight1, weight2, d_output2)
+    x = input.reshape(-1, input.size(-1))
+    dy = d_output2.reshape(-1, d_output2.size(-1))
+    d_w2 = dy.t().mm(output1)
+    d_b2 = dy.sum(0)
+    d_h = _act_grad_ref(dy.mm(weight2), gelu_in, ACT_GELU)
+    return d_h.mm(weight1).view(input.shape), d_h.t().mm(x), d_h.sum(0), d_w2, d_b2
+
+
+def mlp_forward(use_bias: int, activation: int, inputs: List[torch.Tensor]) -> List[torch.Tensor]:
+    """Layer outputs (last = result). activation: 0 none, 1 relu, 2 sigmoid, after every layer."""
+    if inputs[0].is_cuda:
+        return submodule("mlp_cuda").forward(use_bias, activation, list(inputs))
+    n = (len(inputs) - 1) // 2 if use_bias else len(inputs) - 1
+    act = {0: ACT_NONE, 1: ACT_RELU, 2: ACT_SIGMOID}[activation]
+    h, outs = inputs[0], []
+    for i in range(n):
+        h = _act_ref(F.linear(h, inputs[1 + i], inputs[1 + n + i] if use_bias else None), act)
+        outs.append(h)
+    return outs
+
+
+def mlp_backward(use_bias: int, activation: int, grad_o, outputs, inputs) -> List[torch.Tensor]:
+    if inputs[0].is_cuda:
+        return submodule("mlp_cuda").backward(use_bias, activation, grad_o, list(outputs), list(inputs))
+    n = (len(inputs) - 1) // 2 if use_bias else len(inputs) - 1
+    act = {0: ACT_NONE, 1: ACT_RELU, 2: ACT_SIGMOID}[activation]
+    grads = [None] * len(inputs)
+    g = grad_o
+    for i in range(n - 1, -1, -1):
+        dpre = _act_grad_ref(g, outputs[i], act)
+        x = inputs[0] if i == 0 else outputs[i - 1]
+        grads[1 + i] = dpre.t().mm(x)
+        if use_bias:
+            grads[1 + n + i] = dpre.sum(0)
+        g = dpre.mm(inputs[1 + i])
+    grads[0] = g
+    return grads
+
+
+def wgrad_gemm_accum_fp32(input, d_output, main_grad):
+    """main_grad (fp32) += d_output^T @ input, accumulated in fp32 in place."""
+    if input.is_cuda:
+        return submodule("fused_weight_gradient_mlp_cuda").wgrad_gemm_accum_fp32(input, d_output, main_grad)
+    main_grad.add_(d_output.reshape(-1, d_output.size(-1)).float().t().mm(input.reshape(-1, input.size(-1)).float()))
+
+
+def wgrad_gemm_accum_fp16(input, d_output, main_grad):
+    """main_grad (same 16-bit dtype as input) += d_output^T @ input."""
+    if input.is_cuda:
+        return submodule("fused_weight_gradient_mlp_cuda").wgrad_gemm_accum_fp16(input, d_output, main_grad)
+    main_grad.add_(d_output.reshape(-1, d_output.size(-1)).t().mm(input.reshape(-1, input.size(-1))))

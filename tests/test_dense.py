@@ -1,0 +1,138 @@
+"""FusedDense / FusedDenseGeluDense / MLP / wgrad accumulation vs. plain PyTorch fp32 references
+(reference tests: tests/L0/run_mlp/test_mlp.py, apex/contrib fused_dense tests)."""
+import pytest
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from tests.conftest import devices
+
+TOL = {torch.float32: dict(rtol=1e-4, atol=1e-4), torch.float16: dict(rtol=2e-2, atol=2e-2),
+       torch.bfloat16: dict(rtol=5e-2, atol=5e-2)}
+
+
+@pytest.mark.parametrize("device", devices())
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+def test_fused_dense(device, dtype):
+    if device == "cpu" and dtype != torch.float32:
+        pytest.skip("CPU reference path runs fp32")
+    from beforeholiday_amd.fused_dense import FusedDense
+    torch.manual_seed(0)
+    m = FusedDense(64, 40).to(device, dtype)
+    ref = nn.Linear(64, 40).to(device)
+    with torch.no_grad():
+        ref.weight.copy_(m.weight.float())
+        ref.bias.copy_(m.bias.float())
+    x = torch.randn(3, 10, 64, device=device, dtype=dtype, requires_grad=True)
+    xr = x.detach().float().requires_grad_()
+    y = m(x)
+    yr = ref(xr)
+    torch.testing.assert_close(y.float(), yr, **TOL[dtype])
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g)
+    torch.testing.assert_close(x.grad.float(), xr.grad, **TOL[dtype])
+    scale = dict(rtol=TOL[dtype]["rtol"], atol=TOL[dtype]["atol"] * 10)
+    torch.testing.assert_close(m.weight.grad.float(), ref.weight.grad, **scale)
+    torch.testing.assert_close(m.bias.grad.float(), ref.bias.grad, **scale)
+
+
+@pytest.mark.parametrize("device", devices())
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_fused_dense_gelu_dense(device, dtype):
+    if device == "cpu" and dtype != torch.float32:
+        pytest.skip("CPU reference path runs fp32")
+    from beforeholiday_amd.fused_dense import FusedDenseGeluDense
+    torch.manual_seed(1)
+    m = FusedDenseGeluDense(32, 96, 48).to(device, dtype)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.mul_(0.2)
+    params = [p.detach().float().clone().requires_grad_() for p in (m.weight, m.bias, m.weight2, m.bias2)]
+    x = torch.randn(20, 32, device=device, dtype=dtype, requires_grad=True)
+    xr = x.detach().float().requires_grad_()
+    y = m(x)
+    yr = F.linear(F.gelu(F.linear(xr, params[0], params[1])), params[2], params[3])
+    torch.testing.assert_close(y.float(), yr, **TOL[dtype])
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g)
+    torch.testing.assert_close(x.grad.float(), xr.grad, **TOL[dtype])
+    for p, r in zip((m.weight, m.bias, m.weight2, m.bias2), params):
+        torch.testing.assert_close(p.grad.float(), r.grad, rtol=TOL[dtype]["rtol"], atol=TOL[dtype]["atol"] * 10)
+
+
+@pytest.mark.parametrize("device", devices())
+@pytest.mark.parametrize("activation", ["relu", "sigmoid", "none"])
+@pytest.mark.parametrize("bias", [True, False])
+def test_mlp(device, activation, bias):
+    from beforeholiday_amd.mlp import MLP
+    sizes = [48, 64, 32, 8]
+    torch.manual_seed(2)
+    mlp = MLP(sizes, bias=bias, activation=activation).to(device)
+    layers = []
+    for i in range(mlp.num_layers):
+        lin = nn.Linear(sizes[i], sizes[i + 1], bias=bias)
+        with torch.no_grad():
+            lin.weight.copy_(mlp.weights[i])
+            if bias:
+                lin.bias.copy_(mlp.biases[i])
+        layers.append(lin)
+        if activation == "relu":
+            layers.append(nn.ReLU())
+        elif activation == "sigmoid":
+            layers.append(nn.Sigmoid())
+    ref = nn.Sequential(*layers).to(device)
+    x = torch.empty(33, sizes[0], device=device).uniform_(-1, 1).requires_grad_()
+    xr = x.detach().clone().requires_grad_()
+    y, yr = mlp(x), ref(xr)
+    torch.testing.assert_close(y, yr, rtol=1e-5, atol=1e-5)
+    y.mean().mul(10).backward()
+    yr.mean().mul(10).backward()
+    torch.testing.assert_close(x.grad, xr.grad, rtol=1e-4, atol=1e-6)
+    for i in range(mlp.num_layers):
+        lin = ref[i * (1 if activation == "none" else 2)]
+        torch.testing.assert_close(mlp.weights[i].grad, lin.weight.grad, rtol=1e-4, atol=1e-6)
+        if bias:
+            torch.testing.assert_close(mlp.biases[i].grad, lin.bias.grad, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("device", devices())
+@pytest.mark.parametrize("act", [1, 2, 3, 4])
+def test_act_backward_bgrad(device, act):
+    """The fused dActivation + bias-gradient pass vs autograd (odd widths exercise the scalar path)."""
+    from beforeholiday_amd.ops import fused_dense as fd
+    torch.manual_seed(3)
+    for M, N in [(257, 40), (64, 1000), (3, 13)]:
+        pre = torch.randn(M, N, device=device)
+        fn = {1: torch.relu, 2: torch.sigmoid, 3: F.gelu, 4: lambda t: F.gelu(t, approximate="tanh")}[act]
+        p = pre.clone().requires_grad_()
+        out = fn(p)
+        dy = torch.randn(M, N, device=device)
+        out.backward(dy)
+        aux = pre if act in (3, 4) else out.detach()
+        dx, db = fd.act_backward(dy, aux, act, True)
+        torch.testing.assert_close(dx, p.grad, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(db, p.grad.sum(0), rtol=1e-4, atol=1e-4)
+        y = fd.bias_act_forward(pre, torch.ones(N, device=device), act)
+        torch.testing.assert_close(y, fn(pre + 1), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("device", devices())
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+def test_wgrad_gemm_accum(device, dtype):
+    if device == "cpu" and dtype != torch.float32:
+        pytest.skip("CPU reference path runs fp32")
+    from beforeholiday_amd.ops import fused_dense as fd
+    torch.manual_seed(4)
+    x = torch.randn(4, 16, 24, device=device, dtype=dtype)
+    dy = torch.randn(4, 16, 40, device=device, dtype=dtype)
+    main = torch.randn(40, 24, device=device)
+    expect = main + dy.reshape(-1, 40).float().t() @ x.reshape(-1, 24).float()
+    fd.wgrad_gemm_accum_fp32(x, dy, main)
+    torch.testing.assert_close(main, expect, rtol=1e-3, atol=1e-2)
+    if dtype != torch.float32:
+        m16 = torch.zeros(40, 24, device=device, dtype=dtype)
+        fd.wgrad_gemm_accum_fp16(x, dy, m16)
+        prod = dy.reshape(-1, 40).float().t() @ x.reshape(-1, 24).float()
+        torch.testing.assert_close(m16.float(), prod, rtol=5e-2, atol=5e-1)

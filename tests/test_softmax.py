@@ -93,3 +93,30 @@ def test_xentropy(device, smoothing, dtype, half_to_float, V):
     tol = 1e-4 if dtype == torch.float32 else 2e-2
     torch.testing.assert_close(loss.float(), ref.detach(), rtol=tol, atol=tol)
     torch.testing.assert_close(logits.grad.float(), lr.grad, rtol=tol, atol=tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("V,shards", [(1000, 2), (50304, 4), (37, 1)])
+def test_vocab_parallel_xent_kernels(dtype, V, shards):
+    """Shard partials (one pass each) + combine == full-vocab cross-entropy; backward per shard."""
+    from beforeholiday_amd._native import submodule
+    xent = submodule("xentropy_cuda")
+    torch.manual_seed(0)
+    rows = 67
+    logits = (torch.randn(rows, V, device="cuda") * 3).to(dtype)
+    target = torch.randint(0, V, (rows,), device="cuda")
+    ref = torch.nn.functional.cross_entropy(logits.float(), target, reduction="none")
+    part = V // shards
+    stats = torch.stack([xent.vocab_parallel_stats(logits[:, s * part:(s + 1) * part].contiguous(), target, s * part)
+                         for s in range(shards)])
+    loss, lse = xent.vocab_parallel_combine(stats, dtype)
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(loss.float(), ref, rtol=tol, atol=tol)
+    g = torch.rand(rows, device="cuda")
+    lr = logits.float().requires_grad_()
+    (torch.nn.functional.cross_entropy(lr, target, reduction="none") * g).sum().backward()
+    for s in range(shards):
+        shard = logits[:, s * part:(s + 1) * part].contiguous()
+        dx = xent.backward(g, shard, lse, target - s * part, 0.0)
+        torch.testing.assert_close(dx.float(), lr.grad[:, s * part:(s + 1) * part], rtol=tol, atol=tol)
