@@ -158,6 +158,18 @@ void multi_tensor_scale(int64_t chunk, at::Tensor noop, Lists lists, double scal
                 noop.data_ptr<int>(), stream_for(noop));
 }
 
+// scale given as a 1-element fp32 GPU tensor (read on device: no host synchronisation)
+void multi_tensor_scale_tensor(int64_t chunk, at::Tensor noop, Lists lists, at::Tensor scale) {
+  if (lists_empty(lists)) return;
+  TORCH_CHECK(lists.size() == 2, "multi_tensor_scale expects 2 lists");
+  check_noop(noop);
+  TORCH_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat && scale.numel() == 1,
+              "scale must be a 1-element fp32 GPU tensor");
+  const auto& p = get_plan(lists, chunk);
+  bh::mta_scale(p.view, list_dtype(lists[0], "scale"), list_dtype(lists[1], "scale"), 1.f, noop.data_ptr<int>(),
+                stream_for(noop), scale.data_ptr<float>());
+}
+
 void multi_tensor_axpby(int64_t chunk, at::Tensor noop, Lists lists, double a, double b, int64_t arg) {
   if (lists_empty(lists)) return;
   TORCH_CHECK(lists.size() == 3, "multi_tensor_axpby expects 3 lists");
@@ -466,6 +478,7 @@ void register_amp_C(pybind11::module_& root) {
   namespace py = pybind11;
   auto m = root.def_submodule("amp_C", "multi-tensor apply kernels (gfx950)");
   m.def("multi_tensor_scale", &multi_tensor_scale, "out = in * scale with overflow flag");
+  m.def("multi_tensor_scale_tensor", &multi_tensor_scale_tensor, "out = in * scale[0] (device scalar)");
   m.def("multi_tensor_sgd", &multi_tensor_sgd, "fused SGD");
   m.def("multi_tensor_axpby", &multi_tensor_axpby, "out = a*x + b*y with overflow flag");
   m.def("multi_tensor_l2norm", &multi_tensor_l2norm, py::arg("chunk_size"), py::arg("noop_flag"),

@@ -39,7 +39,9 @@ struct MTAView {
   int chunk;
 };
 
-void mta_scale(const MTAView& v, int dt_in, int dt_out, float scale, int* noop, hipStream_t s);
+// scale_dev (optional): device fp32 scalar used instead of `scale`
+void mta_scale(const MTAView& v, int dt_in, int dt_out, float scale, int* noop, hipStream_t s,
+               const float* scale_dev = nullptr);
 void mta_axpby(const MTAView& v, int dt_x, int dt_y, int dt_out, float a, float b, int arg_to_check,
                int* noop, hipStream_t s);
 // Per-chunk partial reductions of list 0: norm_type 2 -> sum of squares, 0 -> max |x|.

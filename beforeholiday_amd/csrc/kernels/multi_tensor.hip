@@ -71,8 +71,9 @@ inline void check_launch(const char* what) {
 // scale: out = in * scale; non-finite input -> *noop = 1
 // ------------------------------------------------------------------------------------
 template <typename Ti, typename To>
-__global__ __launch_bounds__(kBlock) void k_scale(MTAView v, float scale, int* noop) {
+__global__ __launch_bounds__(kBlock) void k_scale(MTAView v, float scale, const float* scale_dev, int* noop) {
   MTA_PROLOGUE(v);
+  if (scale_dev) scale = *scale_dev;  // device-resident factor (e.g. a clip coefficient): no host sync
   const Ti* in = mta_ptr<const Ti>(v, 0, t, base);
   To* out = mta_ptr<To>(v, 1, t, base);
   bool finite = true;
@@ -524,10 +525,11 @@ __global__ __launch_bounds__(kBlock) void k_lamb_s2(MTAView v, const float* pn_t
 // ======================================================================================
 // launchers
 // ======================================================================================
-void mta_scale(const MTAView& v, int dt_in, int dt_out, float scale, int* noop, hipStream_t s) {
+void mta_scale(const MTAView& v, int dt_in, int dt_out, float scale, int* noop, hipStream_t s,
+               const float* scale_dev) {
   if (v.C == 0) return;
   BH_DISPATCH_FLOAT(dt_in, Ti, BH_DISPATCH_FLOAT(dt_out, To,
-      hipLaunchKernelGGL((k_scale<Ti, To>), dim3(v.C), dim3(kBlock), 0, s, v, scale, noop)));
+      hipLaunchKernelGGL((k_scale<Ti, To>), dim3(v.C), dim3(kBlock), 0, s, v, scale, scale_dev, noop)));
   check_launch("multi_tensor_scale");
 }
 

@@ -35,3 +35,17 @@ def _make(name):
 for _n in __all__:
     globals()[_n] = _make(_n)
 del _n
+
+_scale_float = multi_tensor_scale  # noqa: F821
+
+
+def multi_tensor_scale(chunk_size, noop_flag, tensor_lists, scale):  # noqa: F811
+    """out = in * scale. ``scale`` may be a 1-element GPU tensor: it is then read on the device
+    (no host synchronisation), e.g. a gradient-clipping coefficient."""
+    import torch
+    if isinstance(scale, torch.Tensor):
+        if noop_flag.is_cuda:
+            return submodule("amp_C").multi_tensor_scale_tensor(chunk_size, noop_flag, tensor_lists,
+                                                                scale.reshape(1).float())
+        scale = float(scale)
+    return _scale_float(chunk_size, noop_flag, tensor_lists, scale)
