@@ -1,0 +1,123 @@
+"""Attention building blocks shared by the self / encoder-decoder multi-head attention modules
+(reference: apex/contrib/multihead_attn/*_func.py, apex/contrib/csrc/multihead_attn/*).
+
+GEMMs (QKV projection, Q·K^T, P·V, output projection) run on hipBLASLt through differentiable
+torch ops; the memory-bound middle — mask, softmax, dropout — is ONE HIP pass forward and one
+backward (``fast_multihead_attn`` in kernels/mha.hip, dropout regenerated from a Philox seed so no
+mask tensor is stored). On CPU the same math runs as torch ops.
+"""
+import torch
+import torch.nn.functional as F
+
+from ..._native import submodule
+
+MASK_NONE, MASK_PAD, MASK_ADDITIVE, MASK_TIME = 0, 1, 2, 3
+
+
+def _seed():
+    return int(torch.empty((), dtype=torch.int64).random_(0, 2 ** 62).item())
+
+
+class MaskSoftmaxDropoutFn(torch.autograd.Function):
+    """scores [B*heads, sq, sk] -> dropout(softmax(masked scores))."""
+
+    @staticmethod
+    def forward(ctx, scores, mask, mask_mode, heads, p, training):
+        native = scores.is_cuda and scores.size(-1) <= submodule("fast_multihead_attn").max_sk()
+        ctx.native = native
+        ctx.p = p if training else 0.0
+        if native:
+            seed = _seed()
+            sm, dropped = submodule("fast_multihead_attn").mask_softmax_dropout_forward(
+                scores, mask, mask_mode, heads, p, seed, 0, training)
+            ctx.seed = seed
+            ctx.save_for_backward(sm)
+            return dropped
+        x = scores.float()
+        bh, sq, sk = x.shape
+        if mask_mode == MASK_TIME:
+            x = x.masked_fill(mask.to(torch.bool).view(1, sq, sk), float("-inf"))
+        elif mask_mode in (MASK_PAD, MASK_ADDITIVE):
+            x = x.view(-1, heads, sq, sk)
+            m = mask.view(-1, 1, 1, sk)
+            x = x + m.float() if mask_mode == MASK_ADDITIVE else x.masked_fill(m.to(torch.bool), float("-inf"))
+            x = x.view(bh, sq, sk)
+        sm = torch.softmax(x, dim=-1).nan_to_num(0.0).to(scores.dtype)
+        if training and p > 0:
+            keep = (torch.rand_like(sm, dtype=torch.float32) >= p)
+            out = sm * keep.to(sm.dtype) / (1.0 - p)
+        else:
+            keep = None
+            out = sm
+        ctx.save_for_backward(sm, keep)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        if ctx.native:
+            (sm,) = ctx.saved_tensors
+            dx = submodule("fast_multihead_attn").mask_softmax_dropout_backward(dy, sm, ctx.p, ctx.seed, 0,
+                                                                                  ctx.p > 0)
+            return dx, None, None, None, None, None
+        sm, keep = ctx.saved_tensors
+        g = dy.float()
+        if keep is not None:
+            g = g * keep.float() / (1.0 - ctx.p)
+        smf = sm.float()
+        dx = smf * (g - (g * smf).sum(-1, keepdim=True))
+        return dx.to(sm.dtype), None, None, None, None, None
+
+
+def mask_mode_for(mask, use_time_mask, mask_additive):
+    if mask is None:
+        return MASK_NONE
+    if use_time_mask:
+        return MASK_TIME
+    return MASK_ADDITIVE if mask_additive else MASK_PAD
+
+
+def attention(q, k, v, heads, scale, mask, mask_mode, p, training):
+    """q [sq, B*heads, hd], k/v [sk, B*heads, hd] -> context [sq, B*heads, hd]."""
+    scores = torch.baddbmm(q.new_empty(q.size(1), q.size(0), k.size(0)), q.transpose(0, 1),
+                           k.transpose(0, 1).transpose(1, 2), beta=0.0, alpha=scale)
+    probs = MaskSoftmaxDropoutFn.apply(scores, mask, mask_mode, heads, p, training)
+    return torch.bmm(probs, v.transpose(0, 1)).transpose(0, 1)
+
+
+def _linear(x2d, w, b):
+    return torch.addmm(b, x2d, w.t()) if b is not None else torch.mm(x2d, w.t())
+
+
+def self_attention(use_time_mask, is_training, heads, scale, inputs, input_weights, output_weights, input_biases,
+                   output_biases, mask, mask_additive, dropout_prob):
+    s, b, e = inputs.shape
+    hd = e // heads
+    qkv = _linear(inputs.reshape(s * b, e), input_weights, input_biases).view(s, b * heads, 3, hd)
+    q, k, v = qkv[:, :, 0, :], qkv[:, :, 1, :], qkv[:, :, 2, :]
+    ctxt = attention(q, k, v, heads, scale, mask, mask_mode_for(mask, use_time_mask, mask_additive), dropout_prob,
+                     is_training)
+    out = _linear(ctxt.reshape(s * b, e), output_weights, output_biases)
+    return out.view(s, b, e)
+
+
+def encdec_attention(use_time_mask, is_training, heads, scale, inputs_q, inputs_kv, input_weights_q,
+                     input_weights_kv, output_weights, input_biases_q, input_biases_kv, output_biases, mask,
+                     dropout_prob):
+    sq, b, e = inputs_q.shape
+    sk = inputs_kv.size(0)
+    hd = e // heads
+    q = _linear(inputs_q.reshape(sq * b, e), input_weights_q, input_biases_q).view(sq, b * heads, hd)
+    kv = _linear(inputs_kv.reshape(sk * b, e), input_weights_kv, input_biases_kv).view(sk, b * heads, 2, hd)
+    k, v = kv[:, :, 0, :], kv[:, :, 1, :]
+    ctxt = attention(q, k, v, heads, scale, mask, mask_mode_for(mask, use_time_mask, False), dropout_prob,
+                     is_training)
+    return _linear(ctxt.reshape(sq * b, e), output_weights, output_biases).view(sq, b, e)
+
+
+def layer_norm(x, gamma, beta):
+    from ...normalization.fused_layer_norm import fused_layer_norm_affine
+    return fused_layer_norm_affine(x, gamma, beta, (x.size(-1),), 1e-5)
+
+
+def dropout_add(x, residual, p, training):
+    return residual + F.dropout(x, p=p, training=training)

@@ -4,6 +4,7 @@
 #include "common.h"
 
 #include "bh/contrib_api.h"
+#include "bh/mha_api.h"
 
 namespace bhb {
 namespace {
@@ -82,12 +83,60 @@ void imul_bwd_bwd(at::Tensor grad_grad_out, at::Tensor grad_in1, at::Tensor grad
                                      (int)in2.size(1), stream_for(in1));
 }
 
+// scores [B*heads, sq, sk] -> (softmax, dropped probabilities or undefined)
+std::vector<at::Tensor> mha_softmax_fwd(at::Tensor scores, c10::optional<at::Tensor> mask, int64_t mask_mode,
+                                        int64_t heads, double p_drop, int64_t seed, int64_t offset, bool training) {
+  check_cuda(scores, "scores");
+  scores = scores.contiguous();
+  TORCH_CHECK(scores.dim() == 3, "mha softmax: scores must be [B*heads, sq, sk]");
+  const int64_t sq = scores.size(1), sk = scores.size(2), rows = scores.size(0) * sq;
+  TORCH_CHECK(sk <= bh::mha_max_sk(), "mha softmax: sk ", sk, " > ", bh::mha_max_sk());
+  at::Tensor m;
+  int dt_mask = bh::kF32;
+  if (mask_mode != 0) {
+    TORCH_CHECK(mask.has_value() && mask->defined(), "mha softmax: mask required");
+    m = mask->contiguous();
+    if (mask_mode == 1 || mask_mode == 3) m = m.to(at::kByte);
+    else dt_mask = dtype_code(m.scalar_type());
+    const int64_t expect = (mask_mode == 3) ? sq * sk : (scores.size(0) / heads) * sk;
+    TORCH_CHECK(m.numel() == expect, "mha softmax: mask has ", m.numel(), " elements, expected ", expect);
+  }
+  auto sm = at::empty_like(scores);
+  at::Tensor dropped;
+  const bool drop = training && p_drop > 0.0;
+  if (drop) dropped = at::empty_like(scores);
+  const bool vec = (sk % 8 == 0) && reinterpret_cast<uintptr_t>(scores.data_ptr()) % 16 == 0;
+  bh::mha_softmax_dropout_forward(dtype_code(scores.scalar_type()), scores.data_ptr(), (int)mask_mode, dt_mask,
+                                  m.defined() ? m.data_ptr() : nullptr, sm.data_ptr(),
+                                  drop ? dropped.data_ptr() : nullptr, rows, (int)sq, (int)sk, (int)heads,
+                                  (float)p_drop, (uint64_t)seed, (uint64_t)offset, vec, stream_for(scores));
+  return {sm, drop ? dropped : sm};
+}
+
+at::Tensor mha_softmax_bwd(at::Tensor dy, at::Tensor sm, double p_drop, int64_t seed, int64_t offset,
+                           bool use_dropout) {
+  check_cuda(dy, "dy");
+  dy = dy.contiguous();
+  sm = sm.contiguous();
+  const int64_t sk = sm.size(-1), rows = sm.numel() / sk;
+  auto dx = at::empty_like(sm);
+  const bool vec = (sk % 8 == 0);
+  bh::mha_softmax_dropout_backward(dtype_code(sm.scalar_type()), dy.data_ptr(), sm.data_ptr(), dx.data_ptr(), rows,
+                                   (int)sk, (float)p_drop, (uint64_t)seed, (uint64_t)offset, use_dropout && p_drop > 0,
+                                   vec, stream_for(sm));
+  return dx;
+}
+
 }  // namespace
 
 void register_contrib(pybind11::module_& root) {
   auto fl = root.def_submodule("focal_loss_cuda", "sigmoid focal loss");
   fl.def("forward", &focal_fwd);
   fl.def("backward", &focal_bwd);
+  auto mha = root.def_submodule("fast_multihead_attn", "MHA mask + softmax + dropout block");
+  mha.def("mask_softmax_dropout_forward", &mha_softmax_fwd);
+  mha.def("mask_softmax_dropout_backward", &mha_softmax_bwd);
+  mha.def("max_sk", &bh::mha_max_sk);
   auto im = root.def_submodule("fused_index_mul_2d", "out = in1[idx] * in2");
   for (const char* p : {"float_", "half_", "bfloat16_", ""}) {
     im.def((std::string(p) + "forward").c_str(), &imul_fwd);
