@@ -50,6 +50,17 @@ def install_apex_aliases():
             sys.modules.setdefault(f"apex.{sub}", importlib.import_module(f".{sub}", __name__))
         except ImportError:
             pass
-    from .ops import amp_C
+    from .ops import amp_C, apex_C
 
     sys.modules.setdefault("amp_C", amp_C)
+    sys.modules.setdefault("apex_C", apex_C)
+    # the reference's other top-level extension modules map onto submodules of the native _C
+    if _native.available():
+        for ext in ("syncbn", "fused_layer_norm_cuda", "fused_dense_cuda", "mlp_cuda", "fused_weight_gradient_mlp_cuda",
+                    "scaled_upper_triang_masked_softmax_cuda", "scaled_masked_softmax_cuda", "scaled_softmax_cuda",
+                    "generic_scaled_masked_softmax_cuda", "xentropy_cuda", "focal_loss_cuda", "fused_index_mul_2d",
+                    "fast_multihead_attn", "transducer_joint_cuda", "transducer_loss_cuda"):
+            try:
+                sys.modules.setdefault(ext, _native.submodule(ext))
+            except (AttributeError, ImportError):
+                pass
