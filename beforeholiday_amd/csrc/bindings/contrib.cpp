@@ -5,6 +5,7 @@
 
 #include "bh/contrib_api.h"
 #include "bh/mha_api.h"
+#include "bh/transducer_api.h"
 
 namespace bhb {
 namespace {
@@ -127,6 +128,55 @@ at::Tensor mha_softmax_bwd(at::Tensor dy, at::Tensor sm, double p_drop, int64_t 
   return dx;
 }
 
+// transducer loss: returns (alpha, beta, loss)
+std::vector<at::Tensor> td_loss_fwd(at::Tensor x, at::Tensor label, at::Tensor f_len, at::Tensor y_len,
+                                    at::Tensor batch_offset, int64_t max_f_len, int64_t blank_idx, int64_t opt,
+                                    bool packed_input) {
+  check_cuda(x, "x");
+  x = x.contiguous();
+  label = label.to(at::kLong).contiguous();
+  auto fl = f_len.to(at::kInt).contiguous();
+  auto yl = y_len.to(at::kInt).contiguous();
+  const int64_t B = fl.numel();
+  const int64_t V = x.size(-1);
+  const int64_t max_u1 = packed_input ? (label.size(1) + 1) : x.size(2);
+  const int64_t max_t = packed_input ? max_f_len : x.size(1);
+  at::Tensor bo;
+  if (packed_input) bo = batch_offset.to(at::kLong).contiguous();
+  auto fopt = x.options().dtype(at::kFloat);
+  auto alpha = at::empty({B, max_t, max_u1}, fopt);
+  auto beta = at::empty({B, max_t, max_u1}, fopt);
+  auto loss = at::empty({B}, fopt);
+  bh::transducer_loss_forward(dtype_code(x.scalar_type()), x.data_ptr(), label.data_ptr<int64_t>(),
+                              (int)label.size(1), fl.data_ptr<int>(), yl.data_ptr<int>(),
+                              packed_input ? bo.data_ptr<int64_t>() : nullptr, (int)B, (int)max_t, (int)max_u1,
+                              (int)V, (int)blank_idx, alpha.data_ptr<float>(), beta.data_ptr<float>(),
+                              loss.data_ptr<float>(), stream_for(x));
+  return {alpha, beta, loss};
+}
+
+at::Tensor td_loss_bwd(at::Tensor x, at::Tensor loss_grad, at::Tensor alpha, at::Tensor beta, at::Tensor f_len,
+                       at::Tensor y_len, at::Tensor label, at::Tensor batch_offset, int64_t max_f_len,
+                       int64_t blank_idx, int64_t opt, bool fuse_softmax_backward, bool packed_input) {
+  check_cuda(x, "x");
+  x = x.contiguous();
+  label = label.to(at::kLong).contiguous();
+  auto fl = f_len.to(at::kInt).contiguous();
+  auto yl = y_len.to(at::kInt).contiguous();
+  auto lg = loss_grad.to(at::kFloat).contiguous();
+  const int64_t B = fl.numel();
+  at::Tensor bo;
+  if (packed_input) bo = batch_offset.to(at::kLong).contiguous();
+  auto dx = packed_input ? at::zeros_like(x) : at::empty_like(x);
+  bh::transducer_loss_backward(dtype_code(x.scalar_type()), x.data_ptr(), lg.data_ptr<float>(),
+                               alpha.data_ptr<float>(), beta.data_ptr<float>(), label.data_ptr<int64_t>(),
+                               (int)label.size(1), fl.data_ptr<int>(), yl.data_ptr<int>(),
+                               packed_input ? bo.data_ptr<int64_t>() : nullptr, (int)B, (int)alpha.size(1),
+                               (int)alpha.size(2), (int)x.size(-1), (int)blank_idx, fuse_softmax_backward,
+                               dx.data_ptr(), stream_for(x));
+  return dx;
+}
+
 }  // namespace
 
 void register_contrib(pybind11::module_& root) {
@@ -137,6 +187,9 @@ void register_contrib(pybind11::module_& root) {
   mha.def("mask_softmax_dropout_forward", &mha_softmax_fwd);
   mha.def("mask_softmax_dropout_backward", &mha_softmax_bwd);
   mha.def("max_sk", &bh::mha_max_sk);
+  auto tl = root.def_submodule("transducer_loss_cuda", "RNN-T loss");
+  tl.def("forward", &td_loss_fwd);
+  tl.def("backward", &td_loss_bwd);
   auto im = root.def_submodule("fused_index_mul_2d", "out = in1[idx] * in2");
   for (const char* p : {"float_", "half_", "bfloat16_", ""}) {
     im.def((std::string(p) + "forward").c_str(), &imul_fwd);
