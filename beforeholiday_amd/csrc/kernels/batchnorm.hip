@@ -76,12 +76,14 @@ __global__ __launch_bounds__(kBlock) void k_stats_nhwc(const T* __restrict__ x, 
   const bool active = (r < R) && (c0 < C);
   const bool vec = ((C & 7) == 0);
 
-  float n = 0.f, mean[8], m2[8];
+  // Shifted sums (shift = the split's first row, identical for every lane of a channel): per element
+  // one subtract, one add, one FMA -- no per-row reciprocal and no loop-carried Welford chain, and 4
+  // rows of loads in flight per lane. Converted to (mean, M2) before the LDS merge.
+  float n = 0.f, mean[8], m2[8], cs[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) mean[k] = m2[k] = 0.f;
+  for (int k = 0; k < 8; ++k) mean[k] = m2[k] = cs[k] = 0.f;
   if (active) {
-    for (int64_t row = row0 + r; row < row1; row += R) {
-      float xv[8];
+    auto ld = [&](int64_t row, float (&xv)[8]) {
       const T* p = x + row * C + c0;
       if (vec) {
         VecIO<T>::load(p, xv);
@@ -89,14 +91,41 @@ __global__ __launch_bounds__(kBlock) void k_stats_nhwc(const T* __restrict__ x, 
 #pragma unroll
         for (int k = 0; k < 8; ++k) xv[k] = (c0 + k < C) ? to_f<T>(p[k]) : 0.f;
       }
-      n += 1.f;
-      const float inv = __frcp_rn(n);
+    };
+    if (row0 < row1) ld(row0, cs);
+    int64_t row = row0 + r;
+    for (; row + 3 * (int64_t)R < row1; row += 4 * (int64_t)R) {
+      float xv[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ld(row + u * (int64_t)R, xv[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float d = xv[u][k] - cs[k];
+          mean[k] += d;
+          m2[k] = fmaf(d, d, m2[k]);
+        }
+      n += 4.f;
+    }
+    for (; row < row1; row += R) {
+      float xv[8];
+      ld(row, xv);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const float d = xv[k] - mean[k];
-        mean[k] = fmaf(d, inv, mean[k]);
-        m2[k] = fmaf(d, xv[k] - mean[k], m2[k]);
+        const float d = xv[k] - cs[k];
+        mean[k] += d;
+        m2[k] = fmaf(d, d, m2[k]);
       }
+      n += 1.f;
+    }
+    // (sum d, sum d^2) -> (mean, M2)
+    const float inv = n > 0.f ? 1.f / n : 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float md = mean[k] * inv;
+      m2[k] = fmaxf(m2[k] - mean[k] * md, 0.f);
+      mean[k] = cs[k] + md;
     }
   }
   // tree-merge the R row lanes through LDS: layout [R][cvb*8] for mean and m2, counts [R]
@@ -310,11 +339,7 @@ __global__ __launch_bounds__(kBlock) void k_fwd_nhwc(const T* __restrict__ x, co
   float sc[8], sh[8];
   VecIO<float>::load(scale + c0, sc);
   VecIO<float>::load(shift + c0, sh);
-  for (int64_t row = row0 + r; row < row1; row += R) {
-    const int64_t off = row * C + c0;
-    float xv[8], zv[8];
-    VecIO<T>::load(x + off, xv);
-    if (z) VecIO<Tz>::load(z + off, zv);
+  auto apply = [&](float (&xv)[8], const float (&zv)[8]) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float o = fmaf(xv[k], sc[k], sh[k]);
@@ -322,6 +347,28 @@ __global__ __launch_bounds__(kBlock) void k_fwd_nhwc(const T* __restrict__ x, co
       if (relu) o = fmaxf(o, 0.f);
       xv[k] = o;
     }
+  };
+  int64_t row = row0 + r;
+  for (; row + 3 * (int64_t)R < row1; row += 4 * (int64_t)R) {
+    float xv[4][8], zv[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t off = (row + u * (int64_t)R) * C + c0;
+      VecIO<T>::load(x + off, xv[u]);
+      if (z) VecIO<Tz>::load(z + off, zv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      apply(xv[u], zv[u]);
+      VecIO<Ty>::store(y + (row + u * (int64_t)R) * C + c0, xv[u]);
+    }
+  }
+  for (; row < row1; row += R) {
+    const int64_t off = row * C + c0;
+    float xv[8], zv[8];
+    VecIO<T>::load(x + off, xv);
+    if (z) VecIO<Tz>::load(z + off, zv);
+    apply(xv, zv);
     VecIO<Ty>::store(y + off, xv);
   }
 }
@@ -390,13 +437,12 @@ __global__ __launch_bounds__(kBlock) void k_bwd_reduce_nhwc(const T* __restrict_
       VecIO<float>::load(scale + c0, sc);
       VecIO<float>::load(shift + c0, sh);
     }
-    for (int64_t row = row0 + r; row < row1; row += R) {
-      float g[8], xv[8];
-      VecIO<T>::load(dy + row * C + c0, g);
-      VecIO<T>::load(x + row * C + c0, xv);
+    // 4 rows of dy / x (/ z) loads in flight per lane before any arithmetic
+    auto body = [&](const float (&gi)[8], const float (&xv)[8], const float (&zv)[8]) {
+      float g[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = gi[k];
       if (relu) {
-        float zv[8];
-        if (z) VecIO<Tz>::load(z + row * C + c0, zv);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           float o = fmaf(xv[k], sc[k], sh[k]);
@@ -409,6 +455,28 @@ __global__ __launch_bounds__(kBlock) void k_bwd_reduce_nhwc(const T* __restrict_
         sdy[k] += g[k];
         sdx[k] = fmaf(g[k], xv[k] - mu[k], sdx[k]);
       }
+    };
+    const bool use_z = relu && z;
+    int64_t row = row0 + r;
+    for (; row + 3 * (int64_t)R < row1; row += 4 * (int64_t)R) {
+      float g[4][8], xv[4][8], zv[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t off = (row + u * (int64_t)R) * C + c0;
+        VecIO<T>::load(dy + off, g[u]);
+        VecIO<T>::load(x + off, xv[u]);
+        if (use_z) VecIO<Tz>::load(z + off, zv[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) body(g[u], xv[u], zv[u]);
+    }
+    for (; row < row1; row += R) {
+      const int64_t off = row * C + c0;
+      float g[8], xv[8], zv[8];
+      VecIO<T>::load(dy + off, g);
+      VecIO<T>::load(x + off, xv);
+      if (use_z) VecIO<Tz>::load(z + off, zv);
+      body(g, xv, zv);
     }
   }
   float* s_a = smem;
@@ -566,18 +634,13 @@ __global__ __launch_bounds__(kBlock) void k_dgrad_nhwc(const T* __restrict__ dy,
     VecIO<float>::load(scale + c0, sc);
     VecIO<float>::load(shift + c0, sh);
   }
-  for (int64_t row = row0 + r; row < row1; row += R) {
-    const int64_t off = row * C + c0;
-    float g[8], xv[8];
-    VecIO<T>::load(dy + off, g);
-    VecIO<T>::load(x + off, xv);
+  const bool use_z = relu && z;
+  auto apply = [&](int64_t off, float (&g)[8], float (&xv)[8], const float (&zv)[8]) {
     if (relu) {
-      float zv[8];
-      if (z) VecIO<Tz>::load(z + off, zv);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float o = fmaf(xv[k], sc[k], sh[k]);
-        if (z) o += zv[k];
+        if (use_z) o += zv[k];
         if (o <= 0.f) g[k] = 0.f;
       }
     }
@@ -585,6 +648,28 @@ __global__ __launch_bounds__(kBlock) void k_dgrad_nhwc(const T* __restrict__ dy,
 #pragma unroll
     for (int k = 0; k < 8; ++k) xv[k] = fmaf(g[k], A[k], fmaf(xv[k], B[k], D[k]));
     VecIO<T>::store(dx + off, xv);
+  };
+  // 2 rows of dy / x (/ z) loads in flight per lane before any arithmetic
+  int64_t row = row0 + r;
+  for (; row + (int64_t)R < row1; row += 2 * (int64_t)R) {
+    float g[2][8], xv[2][8], zv[2][8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t off = (row + u * (int64_t)R) * C + c0;
+      VecIO<T>::load(dy + off, g[u]);
+      VecIO<T>::load(x + off, xv[u]);
+      if (use_z) VecIO<Tz>::load(z + off, zv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) apply((row + u * (int64_t)R) * C + c0, g[u], xv[u], zv[u]);
+  }
+  for (; row < row1; row += R) {
+    const int64_t off = row * C + c0;
+    float g[8], xv[8], zv[8];
+    VecIO<T>::load(dy + off, g);
+    VecIO<T>::load(x + off, xv);
+    if (use_z) VecIO<Tz>::load(z + off, zv);
+    apply(off, g, xv, zv);
   }
 }
 
