@@ -15,7 +15,49 @@ def conv3x3(cin, cout, stride=1):
     return nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
 
 
+class _Conv1x1GemmFn(torch.autograd.Function):
+    """1x1 / stride-1 convolution of a channels_last activation as ONE GEMM on its [N*H*W, C] view
+    (no layout change): forward x2d @ W^T, backward dY @ W and dY^T @ x2d (hipBLASLt)."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        n, c, h, w = x.shape
+        x2d = x.permute(0, 2, 3, 1).reshape(-1, c)
+        w2d = weight.view(weight.size(0), c)
+        y2d = torch.mm(x2d, w2d.t())
+        ctx.save_for_backward(x, weight)
+        return y2d.view(n, h, w, -1).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        n, c, h, w = x.shape
+        gy2d = gy.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, weight.size(0))
+        w2d = weight.view(weight.size(0), c)
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.mm(gy2d, w2d).view(n, h, w, c).permute(0, 3, 1, 2)
+        gw = torch.mm(gy2d.t(), x.permute(0, 2, 3, 1).reshape(-1, c)).view_as(weight)
+        return gx, gw
+
+
+class Conv1x1(nn.Conv2d):
+    """nn.Conv2d(k=1, bias=False) that runs as a GEMM on channels_last GPU activations (stride 1),
+    and as a regular convolution otherwise."""
+
+    def forward(self, x):
+        if (x.is_cuda and self.stride == (1, 1) and self.groups == 1 and x.dim() == 4 and
+                x.is_contiguous(memory_format=torch.channels_last) and x.dtype == self.weight.dtype):
+            return _Conv1x1GemmFn.apply(x, self.weight)
+        return super().forward(x)
+
+
+_GEMM_1X1 = False
+
+
 def conv1x1(cin, cout, stride=1):
+    if _GEMM_1X1 and stride == 1:
+        return Conv1x1(cin, cout, 1, stride=stride, bias=False)
     return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
 
 
@@ -107,15 +149,21 @@ def resnet50(**kw) -> ResNet:
     return ResNet(Bottleneck, [3, 4, 6, 3], **kw)
 
 
-def resnet50_fused(process_group=None, channel_last=True, **kw) -> ResNet:
+def resnet50_fused(process_group=None, channel_last=True, gemm_1x1=False, **kw) -> ResNet:
     """ResNet-50 whose BatchNorms are fused SyncBatchNorms (BN+ReLU and BN+add+ReLU in one pass),
-    synchronised over ``process_group`` -- the 'amp O2 + SyncBatchNorm' benchmark model."""
+    synchronised over ``process_group`` -- the 'amp O2 + SyncBatchNorm' benchmark model.
+    ``gemm_1x1``: stride-1 1x1 convolutions run as GEMMs on the channels_last view."""
+    global _GEMM_1X1
     from ..parallel import SyncBatchNorm
 
     def norm(c, fuse_relu=False):
         return SyncBatchNorm(c, process_group=process_group, channel_last=channel_last, fuse_relu=fuse_relu)
 
-    return ResNet(Bottleneck, [3, 4, 6, 3], norm_layer=norm, fused=True, **kw)
+    old, _GEMM_1X1 = _GEMM_1X1, gemm_1x1
+    try:
+        return ResNet(Bottleneck, [3, 4, 6, 3], norm_layer=norm, fused=True, **kw)
+    finally:
+        _GEMM_1X1 = old
 
 
 def resnet18_like(**kw) -> ResNet:

@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--no-syncbn", action="store_true")
     ap.add_argument("--message-size", type=int, default=12_500_000, help="DDP bucket size (elements)")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--conv1x1", default="miopen", choices=["miopen", "gemm"],
+                    help="stride-1 1x1 convolutions: MIOpen, or GEMMs on the channels_last view")
     return ap.parse_args()
 
 
@@ -62,7 +64,7 @@ def main():
 
     require_native("bench")
     torch.manual_seed(1234 + rank)
-    model = (resnet50() if args.no_syncbn else resnet50_fused(channel_last=True)).cuda()
+    model = (resnet50() if args.no_syncbn else resnet50_fused(channel_last=True, gemm_1x1=args.conv1x1 == "gemm")).cuda()
     model = model.to(memory_format=torch.channels_last)
     global_batch = args.batch * world
     if args.optimizer == "lamb":

@@ -166,3 +166,24 @@ def test_num_batches_and_cumulative_momentum(device, momentum):
     assert int(bn.num_batches_tracked) == 3
     torch.testing.assert_close(bn.running_mean, ref.running_mean, rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(bn.running_var, ref.running_var, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
+def test_conv1x1_gemm_matches_conv(dtype):
+    from beforeholiday_amd.models.resnet import Conv1x1
+    torch.manual_seed(0)
+    m = Conv1x1(64, 96, 1, bias=False).cuda().to(dtype)
+    x = torch.randn(4, 64, 14, 14, device="cuda", dtype=dtype).to(memory_format=torch.channels_last)
+    x.requires_grad_()
+    y = m(x)
+    xr = x.detach().float().requires_grad_()
+    w = m.weight.detach().float().requires_grad_()
+    yr = torch.nn.functional.conv2d(xr, w)
+    tol = 1e-3 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(y.float(), yr, rtol=tol, atol=tol)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g)
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=tol, atol=tol)
+    torch.testing.assert_close(m.weight.grad.float(), w.grad, rtol=tol, atol=tol * 20)
