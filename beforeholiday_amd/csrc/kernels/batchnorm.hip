@@ -228,37 +228,37 @@ __global__ __launch_bounds__(64 * kFinLanes) void k_stats_finalize(int C, int sp
                                                            const float* __restrict__ pmean, const float* __restrict__ pm2,
                                                            const float* __restrict__ pn, float* __restrict__ out_local,
                                                            BNFinal fin, const Tw* w, const Tw* b, Tw* rmean, Tw* rvar) {
-  // one wave64 per channel (kFinLanes channels per block): lanes stride over the splits with 4
-  // independent (L2-resident) loads in flight, then a 6-step shuffle butterfly merges the lanes.
-  // Many small workgroups instead of one 64-channel block per 64 channels: for the narrow early
-  // layers (C = 64, hundreds of splits) the merge is spread over C/16 CUs instead of one.
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * kFinLanes + (threadIdx.x >> 6);
-  if (c >= C) return;
+  // 64 channels x kFinLanes split-lanes per block; each lane walks every kFinLanes-th split with 4
+  // independent loads in flight, then the lanes are merged through LDS (short latency chain).
+  __shared__ float sh[3][kFinLanes][64];
+  const int cl = threadIdx.x & 63, lane = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   Welford acc{0.f, 0.f, 0.f};
-  int s = lane;
-  for (; s + 3 * 64 < splits; s += 4 * 64) {
-    float n[4], m[4], q[4];
+  if (c < C) {
+    int s = lane;
+    for (; s + 3 * kFinLanes < splits; s += 4 * kFinLanes) {
+      float n[4], m[4], q[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int ss = s + 64 * u;
-      n[u] = per_channel_n ? pn[(int64_t)ss * C + c] : pn[ss];
-      m[u] = pmean[(int64_t)ss * C + c];
-      q[u] = pm2[(int64_t)ss * C + c];
+      for (int u = 0; u < 4; ++u) {
+        const int ss = s + kFinLanes * u;
+        n[u] = per_channel_n ? pn[(int64_t)ss * C + c] : pn[ss];
+        m[u] = pmean[(int64_t)ss * C + c];
+        q[u] = pm2[(int64_t)ss * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = welford_merge(acc, Welford{n[u], m[u], q[u]});
     }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) acc = welford_merge(acc, Welford{n[u], m[u], q[u]});
+    for (; s < splits; s += kFinLanes) {
+      const float n = per_channel_n ? pn[(int64_t)s * C + c] : pn[s];
+      acc = welford_merge(acc, Welford{n, pmean[(int64_t)s * C + c], pm2[(int64_t)s * C + c]});
+    }
   }
-  for (; s < splits; s += 64) {
-    const float n = per_channel_n ? pn[(int64_t)s * C + c] : pn[s];
-    acc = welford_merge(acc, Welford{n, pmean[(int64_t)s * C + c], pm2[(int64_t)s * C + c]});
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const Welford other{__shfl_xor(acc.n, o, kWave), __shfl_xor(acc.mean, o, kWave), __shfl_xor(acc.m2, o, kWave)};
-    acc = welford_merge(acc, other);
-  }
-  if (lane != 0) return;
+  sh[0][lane][cl] = acc.n;
+  sh[1][lane][cl] = acc.mean;
+  sh[2][lane][cl] = acc.m2;
+  __syncthreads();
+  if (lane != 0 || c >= C) return;
+  for (int l = 1; l < kFinLanes; ++l) acc = welford_merge(acc, Welford{sh[0][l][cl], sh[1][l][cl], sh[2][l][cl]});
   const float var_b = acc.n > 0.f ? acc.m2 / acc.n : 0.f;
   if (out_local) {
     // all_gather layout of the reference: [mean(C), var_biased(C), count(1)]
@@ -553,32 +553,40 @@ __global__ __launch_bounds__(64 * kFinLanes) void k_bwd_reduce_finalize(int C, i
                                                                 const float* __restrict__ p_dyx,
                                                                 const float* __restrict__ invstd,
                                                                 float* __restrict__ sums, Tw* gw, Tw* gb) {
-  // one wave64 per channel, lanes stride over the splits (fixed order: deterministic), shuffle reduce
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * kFinLanes + (threadIdx.x >> 6);
-  if (c >= C) return;
+  __shared__ float sh[2][kFinLanes][64];
+  const int cl = threadIdx.x & 63, lane = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float a = 0.f, b = 0.f;
-  int s = lane;
-  for (; s + 3 * 64 < splits; s += 4 * 64) {
-    float x0[4], x1[4];
+  if (c < C) {
+    int s = lane;
+    for (; s + 3 * kFinLanes < splits; s += 4 * kFinLanes) {
+      float x0[4], x1[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      x0[u] = p_dy[(int64_t)(s + 64 * u) * C + c];
-      x1[u] = p_dyx[(int64_t)(s + 64 * u) * C + c];
+      for (int u = 0; u < 4; ++u) {
+        x0[u] = p_dy[(int64_t)(s + kFinLanes * u) * C + c];
+        x1[u] = p_dyx[(int64_t)(s + kFinLanes * u) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a += x0[u];
+        b += x1[u];
+      }
     }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      a += x0[u];
-      b += x1[u];
+    for (; s < splits; s += kFinLanes) {
+      a += p_dy[(int64_t)s * C + c];
+      b += p_dyx[(int64_t)s * C + c];
     }
   }
-  for (; s < splits; s += 64) {
-    a += p_dy[(int64_t)s * C + c];
-    b += p_dyx[(int64_t)s * C + c];
+  sh[0][lane][cl] = a;
+  sh[1][lane][cl] = b;
+  __syncthreads();
+  if (lane != 0 || c >= C) return;
+  a = 0.f;
+  b = 0.f;
+  for (int l = 0; l < kFinLanes; ++l) {
+    a += sh[0][l][cl];
+    b += sh[1][l][cl];
   }
-  a = wave_sum(a);
-  b = wave_sum(b);
-  if (lane != 0) return;
   sums[c] = a;
   sums[C + c] = b;
   if (gw) gw[c] = from_f<Tw>(b * invstd[c]);
@@ -768,7 +776,7 @@ void bn_stats(const BNShape& s, int dt_x, const void* x, int splits, float* pmea
 void bn_stats_finalize(const BNShape& s, int splits, const float* pmean, const float* pm2, const float* pn,
                        float* out_local, const BNFinal& fin, int dt_w, const void* w, const void* b, void* rmean,
                        void* rvar, hipStream_t st) {
-  const int grid = (s.C + kFinLanes - 1) / kFinLanes;
+  const int grid = (s.C + 63) / 64;
   const bool per_channel_n = !s.channels_last;
   BN_DISPATCH(dt_w, Tw,
       hipLaunchKernelGGL((k_stats_finalize<Tw>), dim3(grid), dim3(64 * kFinLanes), 0, st, s.C, splits, per_channel_n, pmean, pm2,
@@ -835,7 +843,7 @@ void bn_backward_reduce(const BNShape& s, int dt, const void* dy, const void* x,
 
 void bn_backward_reduce_finalize(int C, int splits, const float* p_dy, const float* p_dyx, const float* invstd,
                                  float* sums, int dt_w, void* gw, void* gb, hipStream_t st) {
-  const int grid = (C + kFinLanes - 1) / kFinLanes;
+  const int grid = (C + 63) / 64;
   BN_DISPATCH(dt_w, Tw,
       hipLaunchKernelGGL((k_bwd_reduce_finalize<Tw>), dim3(grid), dim3(64 * kFinLanes), 0, st, C, splits, p_dy, p_dyx, invstd,
                          sums, (Tw*)gw, (Tw*)gb));
