@@ -28,7 +28,8 @@ struct BNFinal {
   int64_t* num_batches;  // optional num_batches_tracked counter, incremented on the device
 };
 
-int bn_num_splits(const BNShape& s);
+int bn_num_splits(const BNShape& s);         // statistics partials
+int bn_num_splits_reduce(const BNShape& s);  // backward-reduction partials
 // partial Welford stats: pmean/pm2 [splits][C]; pn [splits] (channels_last) or [splits][C] (NCHW)
 void bn_stats(const BNShape& s, int dt_x, const void* x, int splits, float* pmean, float* pm2, float* pn,
               hipStream_t st);

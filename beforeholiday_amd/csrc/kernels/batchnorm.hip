@@ -736,7 +736,10 @@ int64_t env_knob(const char* name, int64_t dflt) {
 }
 int64_t knob_ew_blocks() { static const int64_t v = env_knob("BH_BN_EW_BLOCKS", 2048); return v; }
 int64_t knob_ew_rows() { static const int64_t v = env_knob("BH_BN_EW_ROWS", 8); return v; }
-int64_t knob_red_blocks() { static const int64_t v = env_knob("BH_BN_RED_BLOCKS", 1024); return v; }
+// statistics and backward-reduction launches are tuned separately (bench_bn.py sweep on MI355X:
+// stats best at ~1024 workgroups x 32 rows/lane, the two-input backward reduction at ~256)
+int64_t knob_stat_blocks() { static const int64_t v = env_knob("BH_BN_STAT_BLOCKS", 1024); return v; }
+int64_t knob_red_blocks() { static const int64_t v = env_knob("BH_BN_RED_BLOCKS", 256); return v; }
 int64_t knob_red_rows() { static const int64_t v = env_knob("BH_BN_RED_ROWS", 32); return v; }
 
 int64_t nhwc_splits(const BNShape& s, int64_t target, int64_t min_iter) {
@@ -746,13 +749,16 @@ int64_t nhwc_splits(const BNShape& s, int64_t target, int64_t min_iter) {
   return std::max<int64_t>(1, splits);
 }
 
-int bn_num_splits(const BNShape& s) {
-  if (s.channels_last) return (int)nhwc_splits(s, knob_red_blocks(), knob_red_rows());
+static int splits_for(const BNShape& s, int64_t target_blocks) {
+  if (s.channels_last) return (int)nhwc_splits(s, target_blocks, knob_red_rows());
   const int64_t per_c = s.outer * s.inner;
   int64_t splits = std::max<int64_t>(1, 2048 / std::max(1, s.C));
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, per_c / (kBlock * 16)));
   return (int)std::max<int64_t>(1, splits);
 }
+
+int bn_num_splits(const BNShape& s) { return splits_for(s, knob_stat_blocks()); }
+int bn_num_splits_reduce(const BNShape& s) { return splits_for(s, knob_red_blocks()); }
 
 void bn_stats(const BNShape& s, int dt_x, const void* x, int splits, float* pmean, float* pm2, float* pn,
               hipStream_t st) {
