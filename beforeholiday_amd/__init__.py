@@ -22,12 +22,17 @@ import importlib
 
 __version__ = "0.1.0"
 
+import logging as _logging
+
 from . import _native  # noqa: F401
+
+# library root logger (reference: apex/__init__.py:27-39); handlers / rank-aware format in utils.logging
+_library_root_logger = _logging.getLogger(__name__)
 from ._native import available as native_available  # noqa: F401
 
 _SUBMODULES = [
     "ops", "multi_tensor_apply", "optimizers", "amp", "fp16_utils", "normalization", "parallel",
-    "fused_dense", "mlp", "transformer", "contrib", "RNN", "models", "utils",
+    "fused_dense", "mlp", "transformer", "contrib", "RNN", "models", "utils", "testing",
 ]
 
 

@@ -1,0 +1,56 @@
+"""utils: logging formatter, profiling ranges / timers, checkpoint round trip; package imports."""
+import importlib
+
+import pytest
+import torch
+
+
+def test_all_subpackages_import():
+    import beforeholiday_amd as bh
+    for name in bh._SUBMODULES:
+        importlib.import_module(f"beforeholiday_amd.{name}")
+    for sub in ["contrib.bottleneck", "contrib.clip_grad", "contrib.conv_bias_relu", "contrib.fmha",
+                "contrib.focal_loss", "contrib.groupbn", "contrib.index_mul_2d", "contrib.layer_norm",
+                "contrib.multihead_attn", "contrib.nccl_p2p", "contrib.optimizers", "contrib.peer_memory",
+                "contrib.sparsity", "contrib.transducer", "contrib.xentropy", "transformer.amp",
+                "transformer.pipeline_parallel", "transformer.tensor_parallel", "transformer.testing.commons",
+                "transformer.testing.standalone_gpt", "transformer.testing.standalone_bert", "transformer._data",
+                "transformer.layers", "transformer.microbatches"]:
+        importlib.import_module(f"beforeholiday_amd.{sub}")
+
+
+def test_logging_and_profiling(caplog):
+    from beforeholiday_amd.utils import EventTimer, get_logger, profile_range, report_memory
+    log = get_logger("beforeholiday_amd.test")
+    log.warning("hello")
+    with profile_range("region"):
+        t = EventTimer().start()
+        torch.ones(10).sum()
+        t.stop()
+    assert t.elapsed_ms() >= 0
+    assert "memory" in report_memory("x")
+
+
+def test_checkpoint_round_trip(tmp_path):
+    from beforeholiday_amd.optimizers import FusedAdam
+    from beforeholiday_amd.utils import load_checkpoint, save_checkpoint
+    m = torch.nn.Linear(4, 3)
+    opt = FusedAdam(m.parameters(), lr=0.1)
+    m(torch.randn(2, 4)).sum().backward()
+    opt.step()
+    p = save_checkpoint(str(tmp_path / "c.pt"), m, opt, epoch=3)
+    m2 = torch.nn.Linear(4, 3)
+    opt2 = FusedAdam(m2.parameters(), lr=0.1)
+    st = load_checkpoint(p, m2, opt2)
+    assert st["epoch"] == 3
+    torch.testing.assert_close(m2.weight, m.weight)
+    assert opt2.state_dict()["state"].keys() == opt.state_dict()["state"].keys()
+
+
+def test_install_apex_aliases():
+    import sys
+    import beforeholiday_amd as bh
+    bh.install_apex_aliases()
+    import apex  # noqa: F401
+    from apex.optimizers import FusedLAMB  # noqa: F401
+    assert "amp_C" in sys.modules and "apex_C" in sys.modules
