@@ -3,15 +3,16 @@
 ``init_model_for_pruning`` registers a boolean mask buffer per eligible weight,
 ``init_optimizer_for_pruning`` wraps ``optimizer.step`` to mask gradients before and weights after
 the update, ``compute_sparse_masks`` computes the m:n masks (optionally stowing pruned values on the
-CPU so ``restore_pruned_weights`` can undo it). The reference's offline input-channel permutation
-search (torch.fx graph + CUDA search kernels) is not provided: ``allow_permutation`` is accepted and
-ignored with a warning.
+CPU so ``restore_pruned_weights`` can undo it). With ``allow_permutation`` the first mask computation
+is preceded by the offline input-channel permutation (permutation_lib.py: torch.fx channel spaces +
+stripe-pair search on the HIP kernels) that raises the magnitude kept by 2:4 pruning without
+changing the network function.
 """
 import types
-import warnings
 
 import torch
 
+from .permutation_lib import Permutation
 from .sparse_masklib import create_mask
 
 
@@ -32,6 +33,7 @@ class ASP:
     __sparse_parameters = []
     __calculate_mask = None
     __allow_permutation = False
+    __permuted = False
 
     @classmethod
     def init_model_for_pruning(cls, model, mask_calculator="m4n2_1d", verbosity=3,
@@ -41,9 +43,8 @@ class ASP:
         assert cls.__model is None, "ASP has been initialized already."
         cls.__model = model
         cls.__verbosity = verbosity
-        if allow_permutation and verbosity >= 1:
-            warnings.warn("[ASP] channel permutation search is not available; pruning without permutation")
-        cls.__allow_permutation = False
+        cls.__allow_permutation = allow_permutation
+        cls.__permuted = False
         if isinstance(mask_calculator, str):
             cls.__calculate_mask = lambda p: create_mask(p, mask_calculator).bool()
         else:
@@ -106,6 +107,17 @@ class ASP:
 
     @classmethod
     def compute_sparse_masks(cls):
+        if cls.__allow_permutation and not cls.__permuted:
+            model = cls.__model.module if hasattr(cls.__model, "module") and \
+                isinstance(cls.__model.module, torch.nn.Module) else cls.__model
+            all_params = [(n, p) for n, p in model.named_parameters()]
+            Permutation.set_permutation_params_from_asp(model, cls.__sparse_parameters, all_params, cls.__optimizer)
+            Permutation.set_identical_seed()
+            groups = Permutation.permute_model(model)
+            cls.__permuted = True
+            if cls.__verbosity >= 2 and groups is not None:
+                n = sum(1 for g in groups if g.get("permutation_sequence") is not None)
+                print(f"[ASP] input-channel permutation applied to {n} of {len(groups)} channel groups")
         with torch.no_grad():
             for name, module, p_name, p, mask, pruned in cls.__sparse_parameters:
                 if mask.sum() < mask.numel():
@@ -152,7 +164,8 @@ class ASP:
     @classmethod
     def set_permutation_saving_params(cls, allow_permutation=True, save_permutation_graph=False,
                                       permutation_output_dir="."):
-        cls.__allow_permutation = False
+        cls.__allow_permutation = allow_permutation
+        Permutation.set_permutation_saving_params(allow_permutation, save_permutation_graph, permutation_output_dir)
 
     @classmethod
     def _reset(cls):
@@ -161,3 +174,4 @@ class ASP:
         cls.__optimizer = None
         cls.__sparse_parameters = []
         cls.__calculate_mask = None
+        cls.__permuted = False

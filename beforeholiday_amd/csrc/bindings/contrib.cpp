@@ -5,6 +5,7 @@
 
 #include "bh/contrib_api.h"
 #include "bh/mha_api.h"
+#include "bh/sparsity_api.h"
 #include "bh/transducer_api.h"
 
 namespace bhb {
@@ -177,6 +178,41 @@ at::Tensor td_loss_bwd(at::Tensor x, at::Tensor loss_grad, at::Tensor alpha, at:
   return dx;
 }
 
+void check_perm_matrix(const at::Tensor& m) {
+  check_cuda(m, "matrix");
+  TORCH_CHECK(m.dim() == 2 && m.scalar_type() == at::kFloat && m.is_contiguous(),
+              "permutation search: matrix must be a contiguous 2-D fp32 tensor");
+  TORCH_CHECK(m.size(1) % 4 == 0, "permutation search: column count must be a multiple of 4");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(m.data_ptr()) % 16 == 0, "permutation search: matrix must be 16B aligned");
+}
+
+at::Tensor perm_sum24(at::Tensor m) {
+  check_perm_matrix(m);
+  const int parts = bh::perm_sum_parts(m.size(0), m.size(1));
+  auto part = at::empty({parts}, m.options());
+  auto out = at::empty({}, m.options());
+  bh::perm_sum_after_2to4(m.data_ptr<float>(), m.size(0), m.size(1), part.data_ptr<float>(), out.data_ptr<float>(),
+                          stream_for(m));
+  return out;
+}
+
+std::vector<at::Tensor> perm_pair_gains(at::Tensor m, at::Tensor pairs) {
+  check_perm_matrix(m);
+  TORCH_CHECK(pairs.is_cuda() && pairs.scalar_type() == at::kInt && pairs.dim() == 2 && pairs.size(1) == 2 &&
+                  pairs.is_contiguous(), "permutation search: pairs must be a contiguous int32 [P, 2] GPU tensor");
+  const int64_t stripes = m.size(1) / 4;
+  if (pairs.numel() > 0) {
+    TORCH_CHECK(pairs.min().item<int>() >= 0 && pairs.max().item<int>() < stripes,
+                "permutation search: stripe index out of range");
+  }
+  const int64_t P = pairs.size(0);
+  auto gain = at::empty({P}, m.options());
+  auto split = at::empty({P}, pairs.options());
+  bh::perm_stripe_pair_gains(m.data_ptr<float>(), m.size(0), m.size(1), pairs.data_ptr<int32_t>(), P,
+                             gain.data_ptr<float>(), split.data_ptr<int32_t>(), stream_for(m));
+  return {gain, split};
+}
+
 }  // namespace
 
 void register_contrib(pybind11::module_& root) {
@@ -190,6 +226,9 @@ void register_contrib(pybind11::module_& root) {
   auto tl = root.def_submodule("transducer_loss_cuda", "RNN-T loss");
   tl.def("forward", &td_loss_fwd);
   tl.def("backward", &td_loss_bwd);
+  auto ps = root.def_submodule("permutation_search_cuda", "2:4 sparsity channel-permutation search");
+  ps.def("sum_after_2_to_4", &perm_sum24, "kept |w| after 2:4 pruning along rows of a [R, C] fp32 matrix");
+  ps.def("stripe_pair_gains", &perm_pair_gains, "best re-split gain and split index per stripe pair");
   auto im = root.def_submodule("fused_index_mul_2d", "out = in1[idx] * in2");
   for (const char* p : {"float_", "half_", "bfloat16_", ""}) {
     im.def((std::string(p) + "forward").c_str(), &imul_fwd);
