@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--no-syncbn", action="store_true")
     ap.add_argument("--message-size", type=int, default=12_500_000, help="DDP bucket size (elements)")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--autotune", action="store_true",
+                    help="MIOpen find (cudnn.benchmark): minutes of first-step tuning on a fresh box and measured "
+                         "slower (35.1 ms/step) than the immediate-mode solvers (33.1 ms/step) at batch 256")
     ap.add_argument("--conv1x1", default="miopen", choices=["miopen", "gemm"],
                     help="stride-1 1x1 convolutions: MIOpen, or GEMMs on the channels_last view")
     return ap.parse_args()
@@ -54,7 +57,7 @@ def main():
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.benchmark = args.autotune
 
     from beforeholiday_amd import amp
     from beforeholiday_amd._native import require_native
@@ -89,8 +92,13 @@ def main():
         opt.zero_grad()
         return loss
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
+        tw = time.perf_counter()
         step()
+        torch.cuda.synchronize()
+        if rank == 0:
+            print(f"[bench] warmup {i + 1}/{args.warmup}: {(time.perf_counter() - tw) * 1e3:.1f} ms",
+                  file=sys.stderr, flush=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -127,3 +127,41 @@ def _no_sync(rank, world):
 
 def test_ddp_no_sync_gloo():
     run_distributed(_no_sync, 2)
+
+
+def _amp_master_params(rank, world, opt_level):
+    # reference: tests/distributed/amp_master_params/amp_master_params.py:1-71 + compare.py:1-31 —
+    # O2 training under DDP, then every rank must hold identical model AND master params, and the
+    # fp16 model params must equal the fp32 masters rounded to fp16.
+    from beforeholiday_amd import amp
+    from beforeholiday_amd.amp._amp_state import _amp_state
+
+    torch.manual_seed(rank)
+    model = MLP()
+    opt = torch.optim.SGD(model.parameters(), lr=0.05, momentum=0.9)
+    model, opt = amp.initialize(model, opt, opt_level=opt_level, verbosity=0)
+    ddp = DDP(model, message_size=300)
+    for it in range(12):
+        torch.manual_seed(1000 * rank + it)
+        x, y = torch.randn(8, 32), torch.randn(8, 8)
+        loss = torch.nn.functional.mse_loss(ddp(x).float(), y)
+        with amp.scale_loss(loss, opt) as scaled:
+            scaled.backward()
+        opt.step()
+        opt.zero_grad()
+    low = next(model.parameters()).dtype
+    for p, m in zip(model.parameters(), amp.master_params(opt)):
+        assert m.dtype == torch.float32
+        assert torch.equal(p, m.to(low))
+        for t in (p.detach().float(), m.detach()):
+            gathered = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(gathered, t)
+            for g in gathered[1:]:
+                assert torch.equal(g, gathered[0])
+    assert _amp_state.loss_scalers[0].loss_scale() > 0
+    amp.deactivate()
+
+
+@pytest.mark.parametrize("opt_level", ["O2", "O5"])
+def test_amp_master_params_ddp_gloo(opt_level):
+    run_distributed(_amp_master_params, 2, opt_level)
