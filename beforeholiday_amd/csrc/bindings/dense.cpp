@@ -9,6 +9,9 @@
 #include "common.h"
 
 #include "bh/dense_api.h"
+#include "bh/gemm_api.h"
+
+#include <cstdlib>
 
 namespace bhb {
 namespace {
@@ -45,6 +48,83 @@ at::Tensor act_backward(const at::Tensor& dy, const at::Tensor& aux, at::Tensor 
 at::Tensor bias_grad(const at::Tensor& dy) { return act_backward(dy, at::Tensor(), at::Tensor(), bh::kActNone, true); }
 
 // ------------------------------------------------------------------------------------------------
+// MFMA GEMM with fused epilogue (kernels/gemm.hip). BH_DENSE_MFMA=0 routes everything back to
+// hipBLASLt + the separate epilogue passes (A/B switch for benchmarks).
+// ------------------------------------------------------------------------------------------------
+bool mfma_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("BH_DENSE_MFMA");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
+bool mfma_ok(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c) {
+  const auto t = a.scalar_type();
+  if (!mfma_enabled() || (t != at::kHalf && t != at::kBFloat16) || b.scalar_type() != t || c.scalar_type() != t)
+    return false;
+  if (a.stride(1) != 1 || b.stride(1) != 1 || c.stride(1) != 1) return false;
+  return bh::gemm_supported(a.size(0), b.size(0), a.size(1), a.stride(0), b.stride(0), c.stride(0), a.data_ptr(),
+                            b.data_ptr(), c.data_ptr());
+}
+
+// y = act(x . w^T + bias), optionally also the pre-activation. x [M,K], w [N,K].
+std::vector<at::Tensor> linear_act(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int act,
+                                   bool want_pre) {
+  auto y = at::empty({x.size(0), w.size(0)}, x.options());
+  at::Tensor pre;
+  if (want_pre) pre = at::empty_like(y);
+  const bool bias_ok = !bias.defined() || (bias.is_contiguous() && al16(bias) && bias.scalar_type() == x.scalar_type());
+  if (bias_ok && mfma_ok(x, w, y)) {
+    bh::GemmEpilogue e;
+    e.bias = bias.defined() ? bias.data_ptr() : nullptr;
+    e.act = act;
+    e.pre_out = want_pre ? pre.data_ptr() : nullptr;
+    e.ld_aux = y.size(1);
+    bh::gemm_nt(dtype_code(x.scalar_type()), x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), y.data_ptr(),
+                y.stride(0), x.size(0), w.size(0), x.size(1), e, stream_for(x));
+    return {y, pre};
+  }
+  y = bias.defined() ? at::addmm(bias, x, w.t()) : at::mm(x, w.t());
+  if (want_pre) pre.copy_(y);
+  act_inplace(y, at::Tensor(), act);
+  return {y, pre};
+}
+
+// dx = (dy . wt^T) * act'(aux) and its column sum. dy [M,N], wt [K,N] (the weight transposed).
+std::vector<at::Tensor> linear_dact(const at::Tensor& dy, const at::Tensor& wt, const at::Tensor& aux, int act,
+                                    bool want_bgrad) {
+  auto dx = at::empty({dy.size(0), wt.size(0)}, dy.options());
+  const bool aux_ok = act == bh::kActNone ||
+                      (aux.defined() && aux.dim() == 2 && aux.stride(1) == 1 && aux.stride(0) % 8 == 0 && al16(aux) &&
+                       aux.scalar_type() == dy.scalar_type());
+  if (aux_ok && mfma_ok(dy, wt, dx)) {
+    at::Tensor part, db;
+    bh::GemmEpilogue e;
+    e.act = act;
+    e.bwd_act = true;
+    e.aux_in = act != bh::kActNone ? aux.data_ptr() : nullptr;
+    e.ld_aux = act != bh::kActNone ? aux.stride(0) : dx.size(1);
+    const int64_t slabs = bh::gemm_bgrad_slabs(dy.size(0));
+    if (want_bgrad) {
+      part = at::empty({slabs, dx.size(1)}, dy.options().dtype(at::kFloat));
+      e.bgrad_part = part.data_ptr<float>();
+    }
+    bh::gemm_nt(dtype_code(dy.scalar_type()), dy.data_ptr(), dy.stride(0), wt.data_ptr(), wt.stride(0),
+                dx.data_ptr(), dx.stride(0), dy.size(0), wt.size(0), dy.size(1), e, stream_for(dy));
+    if (want_bgrad) {
+      db = at::empty({dx.size(1)}, dy.options());
+      bh::gemm_colsum_finalize(dtype_code(dy.scalar_type()), part.data_ptr<float>(), slabs, dx.size(1), db.data_ptr(),
+                               stream_for(dy));
+    }
+    return {dx, db};
+  }
+  dx = at::mm(dy, wt.t());
+  auto db = act_backward(dx, aux, dx, act, want_bgrad);
+  return {dx, db};
+}
+
+// ------------------------------------------------------------------------------------------------
 // fused_dense_cuda
 // ------------------------------------------------------------------------------------------------
 at::Tensor linear_bias_forward(at::Tensor input, at::Tensor weight, at::Tensor bias) {
@@ -69,11 +149,8 @@ std::vector<at::Tensor> linear_gelu_linear_forward(at::Tensor input, at::Tensor 
                                                    at::Tensor weight2, at::Tensor bias2) {
   check_cuda(input, "input");
   auto x = as2d(input.contiguous());
-  auto gelu_in = at::addmm(bias1, x, weight1.t());
-  auto out1 = at::empty_like(gelu_in);
-  const int64_t N = gelu_in.size(1), M = gelu_in.size(0);
-  bh::dense_act_forward(dtype_code(gelu_in.scalar_type()), gelu_in.data_ptr(), nullptr, out1.data_ptr(), M, (int)N,
-                        bh::kActGelu, (N % 8 == 0) && al16(gelu_in) && al16(out1), stream_for(x));
+  auto h = linear_act(x, weight1.contiguous(), bias1.contiguous(), bh::kActGelu, true);
+  auto gelu_in = h[1], out1 = h[0];
   auto out2 = at::addmm(bias2, out1, weight2.t());
   return {gelu_in, out1, out2};
 }
@@ -87,8 +164,8 @@ std::vector<at::Tensor> linear_gelu_linear_backward(at::Tensor input, at::Tensor
   auto h = as2d(output1.contiguous());
   auto d_weight2 = at::mm(dy.t(), h);
   auto d_bias2 = bias_grad(dy);
-  auto d_h = at::mm(dy, weight2);
-  auto d_bias1 = act_backward(d_h, as2d(gelu_in.contiguous()), d_h, bh::kActGelu, true);  // d_h := dGELU in place
+  auto dh = linear_dact(dy, weight2.t().contiguous(), as2d(gelu_in.contiguous()), bh::kActGelu, true);
+  auto d_h = dh[0], d_bias1 = dh[1];
   auto d_weight1 = at::mm(d_h.t(), x);
   auto d_input = at::mm(d_h, weight1).view(input.sizes());
   return {d_input, d_weight1, d_bias1, d_weight2, d_bias2};
@@ -116,11 +193,8 @@ std::vector<at::Tensor> mlp_forward(int use_bias, int activation, std::vector<at
   std::vector<at::Tensor> outs;
   at::Tensor h = inputs[0].contiguous();
   for (int64_t i = 0; i < n; ++i) {
-    const at::Tensor& w = inputs[1 + i];
-    at::Tensor y;
-    if (use_bias) y = at::addmm(inputs[1 + n + i], h, w.t());
-    else y = at::mm(h, w.t());
-    act_inplace(y, at::Tensor(), act);
+    const at::Tensor w = inputs[1 + i].contiguous();
+    at::Tensor y = linear_act(h, w, use_bias ? inputs[1 + n + i].contiguous() : at::Tensor(), act, false)[0];
     outs.push_back(y);
     h = y;
   }
@@ -132,16 +206,23 @@ std::vector<at::Tensor> mlp_backward(int use_bias, int activation, at::Tensor gr
   const int64_t n = use_bias ? (int64_t)(inputs.size() - 1) / 2 : (int64_t)inputs.size() - 1;
   const int act = mlp_act(activation);
   std::vector<at::Tensor> grads(inputs.size());
+  // dpre := dL/d(pre-activation of layer i). The last layer's comes from one dActivation pass over
+  // grad_o; every earlier one straight out of the dgrad GEMM's epilogue (dActivation + bias grad).
   at::Tensor g = grad_o.contiguous();
+  at::Tensor dpre = (act == bh::kActNone) ? g : at::empty_like(g);
+  at::Tensor db = act_backward(g, outputs[n - 1], dpre, act, use_bias != 0);
+  if (act == bh::kActNone) dpre = g;
   for (int64_t i = n - 1; i >= 0; --i) {
-    // g := dL/d(pre-activation of layer i), bias grad fused into the same pass
-    at::Tensor dpre = (act == bh::kActNone) ? g : at::empty_like(g);
-    at::Tensor db = act_backward(g, outputs[i], dpre, act, use_bias != 0);
-    if (act == bh::kActNone) dpre = g;
     const at::Tensor& x = (i == 0) ? inputs[0] : outputs[i - 1];
     grads[1 + i] = at::mm(dpre.t(), x.contiguous());
     if (use_bias) grads[1 + n + i] = db;
-    if (i > 0 || inputs[0].requires_grad()) g = at::mm(dpre, inputs[1 + i]);
+    if (i > 0) {
+      auto r = linear_dact(dpre, inputs[1 + i].t().contiguous(), outputs[i - 1].contiguous(), act, use_bias != 0);
+      dpre = r[0];
+      db = r[1];
+    } else {
+      g = inputs[0].requires_grad() ? at::mm(dpre, inputs[1]) : at::Tensor();
+    }
   }
   grads[0] = inputs[0].requires_grad() ? g : at::zeros_like(inputs[0]);
   return grads;
@@ -200,6 +281,16 @@ void register_dense(pybind11::module_& root) {
   auto mlp = root.def_submodule("mlp_cuda", "N-layer MLP");
   mlp.def("forward", &mlp_forward);
   mlp.def("backward", &mlp_backward);
+  auto gm = root.def_submodule("gemm", "MFMA GEMM with fused dense epilogues (kernels/gemm.hip)");
+  gm.def("linear_act", [](at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bias, int act, bool want_pre) {
+    check_cuda(x, "x");
+    return linear_act(x, w, bias.has_value() ? *bias : at::Tensor(), act, want_pre);
+  }, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("act"), py::arg("want_pre"));
+  gm.def("linear_dact", [](at::Tensor dy, at::Tensor wt, c10::optional<at::Tensor> aux, int act, bool want_bgrad) {
+    check_cuda(dy, "dy");
+    return linear_dact(dy, wt, aux.has_value() ? *aux : at::Tensor(), act, want_bgrad);
+  }, py::arg("dy"), py::arg("wt"), py::arg("aux"), py::arg("act"), py::arg("want_bgrad"));
+  gm.def("mfma_enabled", &mfma_enabled);
   auto wg = root.def_submodule("fused_weight_gradient_mlp_cuda", "weight-gradient GEMM accumulated into main_grad");
   wg.def("wgrad_gemm_accum_fp32", &wgrad_gemm_accum_fp32);
   wg.def("wgrad_gemm_accum_fp16", &wgrad_gemm_accum_fp16);

@@ -1,0 +1,39 @@
+// MFMA GEMM with fused dense-layer epilogues (kernels: csrc/kernels/gemm.hip).
+//
+//   C[M,N] = epilogue( A[M,K] . B[N,K]^T )      A, B, C row-major, fp16 or bf16, fp32 accumulate
+//
+// Forward epilogue (bwd_act == false):  v = acc (+ bias[n]);  pre_out[m,n] = v (if given);
+//                                       C = act(v)
+// Backward epilogue (bwd_act == true):  v = acc * act'(aux_in[m,n]) (ReLU / sigmoid: aux is the
+//                                       activation OUTPUT, GELU: the pre-activation); C = v; and, if
+//                                       bgrad_part is given, bgrad_part[r][n] = sum over the r-th
+//                                       64-row slab of v (fixed-order, no atomics; finalise with
+//                                       gemm_colsum_finalize).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bh {
+
+struct GemmEpilogue {
+  const void* bias = nullptr;     // [N]
+  int act = 0;                    // DenseAct
+  bool bwd_act = false;
+  void* pre_out = nullptr;        // [M, ld_aux] forward pre-activation (GELU aux)
+  const void* aux_in = nullptr;   // [M, ld_aux] backward
+  int64_t ld_aux = 0;
+  float* bgrad_part = nullptr;    // [gemm_bgrad_slabs(M), N]
+};
+
+// Shape / layout requirements of the MFMA path (else the caller must fall back):
+// K % 8 == 0, N % 8 == 0, lda / ldb / ldc / ld_aux % 8 == 0, 16-byte aligned bases.
+bool gemm_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, const void* A,
+                    const void* B, const void* C);
+int64_t gemm_bgrad_slabs(int64_t M);
+void gemm_nt(int dt, const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M,
+             int64_t N, int64_t K, const GemmEpilogue& epi, hipStream_t st);
+// out[N] (dtype dt) = sum_r part[r][N]
+void gemm_colsum_finalize(int dt, const float* part, int64_t slabs, int64_t N, void* out, hipStream_t st);
+
+}  // namespace bh

@@ -1,0 +1,429 @@
+// MFMA GEMM with fused dense-layer epilogues for gfx950 (CDNA4).
+//
+// Used where the reference calls hipBLASLt with an epilogue (csrc/fused_dense_cuda.cu:223-294:
+// BIAS, GELU_AUX_BIAS, DGELU_BGRAD) or runs separate bias/activation kernels after a GEMM
+// (csrc/mlp_cuda.cu:445-958): the activation / activation-derivative / bias-gradient work happens
+// on the accumulator tile instead of in a second pass over the [M,N] activation.
+//
+// Kernel structure (C = A . B^T, A [M,K], B [N,K], both K-contiguous):
+//  * 128x128 output tile per 256-thread workgroup; 4 waves in a 2x2 grid, each wave owns 64x64 =
+//    4x4 tiles of v_mfma_f32_16x16x32_{f16,bf16} accumulators (64 fp32 VGPRs).
+//  * BK = 64. Global -> register (16-byte loads, one 128-B row per 8 lanes) -> LDS staging with two
+//    LDS buffers: the loads for K-step t+1 are issued before the MFMAs of step t and written to the
+//    other buffer after them, so there is one barrier per K-step.
+//  * LDS rows are 128 B; the 16-byte chunk index is XOR-swizzled with (row>>1)&7 so the 16 lanes of
+//    a ds_read_b128 group (16 consecutive rows, same chunk) and of a ds_write_b128 group (2 rows x
+//    8 chunks) each hit 16 distinct bank slots: conflict-free both ways.
+//  * XCD-aware tile order: the bijective remap puts a contiguous range of tiles on each of the 8
+//    XCDs (shared B panels stay in one L2).
+//  * Epilogue: the fp32 tile is staged through LDS (68-float padded rows) and every lane then owns
+//    8 consecutive columns of a row: bias, activation, pre-activation aux and dActivation run on
+//    16-byte vectors, C is written with 16-byte stores, and bias-gradient column sums are reduced
+//    over the wave's 64 rows with xor-shuffles into a deterministic per-slab partial.
+#include "bh/act.h"
+#include "bh/api.h"
+#include "bh/device.h"
+#include "bh/gemm_api.h"
+
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+
+namespace bh {
+namespace {
+
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef __bf16 b8v __attribute__((ext_vector_type(8)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef int i4v __attribute__((ext_vector_type(4)));
+
+constexpr int BK = 64;
+constexpr int kEpiLd = 68;                          // padded fp32 row of the epilogue image
+constexpr int kEpiWaveBytes = 64 * kEpiLd * 4;      // 17 KiB per wave
+
+// Tile configurations: waves arranged WM x WN, each wave owns a (16*TM) x (16*TN) output sub-tile
+// of 16x16 MFMA accumulators.
+//   Small: 128x128, 4 waves of 64x64, 2 LDS stages (64 KiB, 2 workgroups/CU) - grids too small to
+//          fill the chip with the big tile.
+//   Big:   256x256, 8 waves of 128x64, 2 LDS stages (128 KiB, 1 workgroup/CU): half the L2 bytes
+//          per FLOP of the small tile, 12 ds_read_b128 per 32 MFMAs.
+// Tiles are walked in GROUP_M-row groups inside each XCD's contiguous range so the blocks that
+// run together on one XCD share A row-panels and B column-panels in its L2.
+template <int WM_, int WN_, int TM_, int TN_, int STAGES_> struct Cfg {
+  static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_, STAGES = STAGES_;
+  static constexpr int WTM = 16 * TM, WTN = 16 * TN;             // wave tile
+  static constexpr int BM = WM * WTM, BN = WN * WTN;
+  static constexpr int kThreads = 64 * WM * WN;
+  static constexpr int kABytes = BM * BK * 2, kBBytes = BN * BK * 2;
+  static constexpr int kStageBytes = kABytes + kBBytes;
+  static constexpr int kPieces = (BM + BN) / 8;                   // 1-KiB LDS-DMA pieces per stage
+  static constexpr int kPiecesPerWave = kPieces / (WM * WN);
+  static constexpr int kMainBytes = STAGES * kStageBytes;
+  static constexpr int kEpiBytes = WM * WN * kEpiWaveBytes;
+  static constexpr int kSmemBytes = kMainBytes > kEpiBytes ? kMainBytes : kEpiBytes;
+  static_assert(kPieces % (WM * WN) == 0, "pieces must split evenly over waves");
+  static_assert(WTN == 64, "the epilogue image is 64 columns wide");
+  static_assert(WTM % 64 == 0, "the epilogue walks 64-row chunks");
+};
+using CfgSmall = Cfg<2, 2, 4, 4, 2>;
+using CfgBig = Cfg<2, 4, 8, 4, 2>;
+constexpr int kGroupM = 8;
+
+template <typename T> struct Mfma;
+template <> struct Mfma<f16> {
+  static BH_DEVICE f4v run(i4v a, i4v b, f4v c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8v, a), __builtin_bit_cast(h8v, b), c, 0, 0, 0);
+  }
+};
+template <> struct Mfma<bf16> {
+  static BH_DEVICE f4v run(i4v a, i4v b, f4v c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8v, a), __builtin_bit_cast(b8v, b), c, 0, 0,
+                                                   0);
+  }
+};
+
+BH_DEVICE int swz(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4); }
+
+template <int N> BH_DEVICE void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// raw workgroup barrier (no implicit vmcnt(0) drain) that the compiler may not move LDS reads across
+BH_DEVICE void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+struct Args {
+  const void* A;
+  const void* B;
+  void* C;
+  int64_t lda, ldb, ldc;
+  int M, N, K;
+  int tiles_m, tiles_n;
+  GemmEpilogue epi;
+};
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// One K-step of A and B via LDS-DMA (global_load_lds, 16 B per lane): each wave-instruction fills
+// one 1-KiB piece = 8 rows of 128 B. The LDS destination is lane-linear, so the XOR swizzle is
+// applied to the per-lane SOURCE chunk (logical chunk = physical ^ ((row>>1)&7)). Pieces
+// [0, BM/8) are A rows, the rest B rows. Source pointers are computed once per workgroup; a
+// K-step only adds k0.
+template <typename C, typename T> struct GldsSrc {
+  const T* src[C::kPiecesPerWave];
+  BH_DEVICE void init(const T* A, const T* B, int64_t lda, int64_t ldb, int brow, int bcol, int M, int N, int wave,
+                      int lane) {
+    const int prow = lane >> 3, pch = lane & 7;
+#pragma unroll
+    for (int i = 0; i < C::kPiecesPerWave; ++i) {
+      const int piece = wave * C::kPiecesPerWave + i;
+      const bool is_a = piece < C::BM / 8;
+      const int row = (is_a ? piece : piece - C::BM / 8) * 8 + prow;
+      const int ch = pch ^ ((row >> 1) & 7);
+      src[i] = is_a ? A + (int64_t)min(brow + row, M - 1) * lda + ch * 8
+                    : B + (int64_t)min(bcol + row, N - 1) * ldb + ch * 8;
+    }
+  }
+  BH_DEVICE void issue(char* buf, int k0, int wave) const {
+#pragma unroll
+    for (int i = 0; i < C::kPiecesPerWave; ++i)
+      __builtin_amdgcn_global_load_lds(src[i] + k0, (lds_ptr_t)(buf + (wave * C::kPiecesPerWave + i) * 1024), 16, 0,
+                                       0);
+  }
+};
+
+// GLDS: LDS-DMA staging (requires K % 64 == 0); otherwise register staging with zero-filled K tail
+// (small config only).
+template <typename C, typename T, bool GLDS>
+__global__ __launch_bounds__(C::kThreads, 1) void k_gemm_nt(Args p) {
+  __shared__ __attribute__((aligned(16))) char smem[C::kSmemBytes];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave / C::WN, wc = wave % C::WN;
+
+  // XCD-aware bijective remap of the linear workgroup id
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int per_group = kGroupM * p.tiles_n;
+  const int first_m = (wgid / per_group) * kGroupM;
+  const int gsize = min(p.tiles_m - first_m, kGroupM);
+  const int tm = first_m + (wgid % per_group) % gsize, tn = (wgid % per_group) / gsize;
+  const int brow = tm * C::BM, bcol = tn * C::BN;
+
+  const T* __restrict__ A = reinterpret_cast<const T*>(p.A);
+  const T* __restrict__ B = reinterpret_cast<const T*>(p.B);
+
+  f4v acc[C::TM][C::TN];
+#pragma unroll
+  for (int m = 0; m < C::TM; ++m)
+#pragma unroll
+    for (int n = 0; n < C::TN; ++n) acc[m][n] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  // Both 32-deep k-slices' fragments are read up front (the second slice's LDS latency hides
+  // behind the first slice's MFMAs); sched_barrier keeps hipcc from re-interleaving the reads into
+  // read-pair / lgkmcnt(0) / 8-MFMA groups.
+  auto compute = [&](const char* sa) {
+    const char* sb = sa + C::kABytes;
+    i4v af[2][C::TM], bf[2][C::TN];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int n = 0; n < C::TN; ++n)
+        bf[s][n] = *reinterpret_cast<const i4v*>(sb + swz(wc * C::WTN + n * 16 + fr, s * 4 + fq));
+#pragma unroll
+      for (int m = 0; m < C::TM; ++m)
+        af[s][m] = *reinterpret_cast<const i4v*>(sa + swz(wr * C::WTM + m * 16 + fr, s * 4 + fq));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int m = 0; m < C::TM; ++m)
+#pragma unroll
+        for (int n = 0; n < C::TN; ++n) acc[m][n] = Mfma<T>::run(af[s][m], bf[s][n], acc[m][n]);
+    }
+  };
+
+  const int nk = (p.K + BK - 1) / BK;
+  if constexpr (GLDS) {
+    static_assert(C::STAGES >= 2, "");
+    GldsSrc<C, T> g;
+    g.init(A, B, p.lda, p.ldb, brow, bcol, p.M, p.N, wave, lane);
+    // prologue: STAGES-1 K-steps in flight
+#pragma unroll
+    for (int s = 0; s < C::STAGES - 1; ++s)
+      if (s < nk) g.issue(smem + s * C::kStageBytes, s * BK, wave);
+    if (C::STAGES == 3 && nk > 1) wait_vmcnt<C::kPiecesPerWave>();  // step 0 landed, step 1 may fly
+    else wait_vmcnt<0>();
+    raw_barrier();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int nxt = kt + C::STAGES - 1;
+      if (nxt < nk) g.issue(smem + (nxt % C::STAGES) * C::kStageBytes, nxt * BK, wave);
+      compute(smem + (kt % C::STAGES) * C::kStageBytes);
+      __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs ahead of the DMA wait + barrier
+      // retire step kt+1 (leave the newest STAGES-2 steps in flight); then every wave's DMA for it
+      // has landed once all waves pass the barrier. The barrier also orders this step's LDS reads
+      // before the buffer is restaged.
+      if (C::STAGES == 3 && nxt < nk) wait_vmcnt<C::kPiecesPerWave>();
+      else wait_vmcnt<0>();
+      raw_barrier();
+    }
+  } else {
+    static_assert(C::BM == 128 && C::BN == 128 && C::kThreads == 256, "register staging: 128x128 config only");
+    const int ld_row = tid >> 3, ld_ch = tid & 7;
+    const T* a_src[4];
+    const T* b_src[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      a_src[i] = A + (int64_t)min(brow + ld_row + 32 * i, p.M - 1) * p.lda + ld_ch * 8;
+      b_src[i] = B + (int64_t)min(bcol + ld_row + 32 * i, p.N - 1) * p.ldb + ld_ch * 8;
+    }
+    i4v ra[4], rb[4];
+    auto load = [&](int kt) {
+      const int k0 = kt * BK;
+      const bool ok = k0 + ld_ch * 8 < p.K;
+      const int koff = ok ? k0 : (p.K - 8 - ld_ch * 8);  // clamped, always in bounds (K >= 8)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        i4v va = *reinterpret_cast<const i4v*>(a_src[i] + koff);
+        i4v vb = *reinterpret_cast<const i4v*>(b_src[i] + koff);
+        ra[i] = ok ? va : i4v{0, 0, 0, 0};
+        rb[i] = ok ? vb : i4v{0, 0, 0, 0};
+      }
+    };
+    auto store = [&](int buf) {
+      char* sa = smem + buf * C::kStageBytes;
+      char* sb = sa + C::kABytes;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = ld_row + 32 * i;
+        *reinterpret_cast<i4v*>(sa + swz(row, ld_ch)) = ra[i];
+        *reinterpret_cast<i4v*>(sb + swz(row, ld_ch)) = rb[i];
+      }
+    };
+    load(0);
+    store(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) load(kt + 1);
+      compute(smem + cur * C::kStageBytes);
+      if (kt + 1 < nk) store(cur ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue, in 64-row chunks of the wave tile: stage the fp32 chunk in this wave's private
+  // LDS image (C/D map: col = lane&15, row = 4*(lane>>4)+j), then every lane owns 8 consecutive
+  // columns of 8 rows: 16-byte bias / aux loads, 16-byte C stores, shuffle-reduced bias-grad sums.
+  __syncthreads();  // all waves are done reading the staging buffers
+  float* img = reinterpret_cast<float*>(smem + wave * kEpiWaveBytes);
+  const GemmEpilogue& e = p.epi;
+  const int cg = lane & 7;
+  const int gcol = bcol + wc * C::WTN + cg * 8;
+  const bool col_ok = gcol < p.N;
+  float bias[8];
+  if (e.bias && col_ok && !e.bwd_act) {
+    VecIO<T>::load(reinterpret_cast<const T*>(e.bias) + gcol, bias);
+  } else {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) bias[c] = 0.f;
+  }
+  T* __restrict__ Cp = reinterpret_cast<T*>(p.C);
+#pragma unroll
+  for (int chunk = 0; chunk < C::TM / 4; ++chunk) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < C::TN; ++n)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) img[(m * 16 + fq * 4 + j) * kEpiLd + n * 16 + fr] = acc[chunk * 4 + m][n][j];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // image is wave-private: in-order LDS suffices
+    const int row0 = brow + wr * C::WTM + chunk * 64;
+    float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+    for (int i = 0; i < 8; ++i) {
+      const int lr = (lane >> 3) + 8 * i;
+      const int grow = row0 + lr;
+      float v[8];
+      const f4v lo = *reinterpret_cast<const f4v*>(img + lr * kEpiLd + cg * 8);
+      const f4v hi = *reinterpret_cast<const f4v*>(img + lr * kEpiLd + cg * 8 + 4);
+      v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+      v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+      if (grow < p.M && col_ok) {
+        if (e.bwd_act) {
+          if (e.act != kActNone) {
+            float a[8];
+            VecIO<T>::load(reinterpret_cast<const T*>(e.aux_in) + (int64_t)grow * e.ld_aux + gcol, a);
+#pragma unroll
+            for (int c = 0; c < 8; ++c) v[c] *= act_d(a[c], e.act);
+          }
+          // bias grad of the value actually stored (rounded like the reference's separate pass)
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            v[c] = to_f<T>(from_f<T>(v[c]));
+            csum[c] += v[c];
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < 8; ++c) v[c] += bias[c];
+          if (e.pre_out) VecIO<T>::store(reinterpret_cast<T*>(e.pre_out) + (int64_t)grow * e.ld_aux + gcol, v);
+          if (e.act != kActNone) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) v[c] = act_f(v[c], e.act);
+          }
+        }
+        VecIO<T>::store(Cp + (int64_t)grow * p.ldc + gcol, v);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // image reads done before the next chunk
+    if (e.bgrad_part) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        float sacc = csum[c];
+        sacc += __shfl_xor(sacc, 8);
+        sacc += __shfl_xor(sacc, 16);
+        sacc += __shfl_xor(sacc, 32);
+        csum[c] = sacc;
+      }
+      const int slab = row0 / 64;  // global 64-row slab; slabs past M are never read
+      if (lane < 8 && col_ok && row0 < p.M) {
+        float* dst = e.bgrad_part + (int64_t)slab * p.N + gcol;
+        *reinterpret_cast<float4*>(dst) = make_float4(csum[0], csum[1], csum[2], csum[3]);
+        *reinterpret_cast<float4*>(dst + 4) = make_float4(csum[4], csum[5], csum[6], csum[7]);
+      }
+    }
+  }
+}
+
+template <typename T>
+__global__ void k_colsum(const float* __restrict__ part, int64_t slabs, int64_t N, T* __restrict__ out) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= N) return;
+  float s = 0.f;
+  for (int64_t j = 0; j < slabs; ++j) s += part[j * N + c];
+  out[c] = from_f<T>(s);
+}
+
+inline void check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+inline bool al16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
+
+}  // namespace
+
+bool gemm_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, const void* A,
+                    const void* B, const void* C) {
+  return M > 0 && N > 0 && K >= 8 && K % 8 == 0 && N % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0 &&
+         lda >= K && ldb >= K && ldc >= N && al16(A) && al16(B) && al16(C) && M < (1ll << 31) && N < (1ll << 31) &&
+         K < (1ll << 31);
+}
+
+int64_t gemm_bgrad_slabs(int64_t M) { return (M + 63) / 64; }
+
+namespace {
+template <typename C, typename T>
+void launch(const Args& a0, bool glds, hipStream_t st) {
+  Args a = a0;
+  a.tiles_m = (a.M + C::BM - 1) / C::BM;
+  a.tiles_n = (a.N + C::BN - 1) / C::BN;
+  const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
+  if (nwg >= (1ll << 31)) throw std::runtime_error("gemm_nt: grid too large");
+  if (glds) hipLaunchKernelGGL((k_gemm_nt<C, T, true>), dim3((unsigned)nwg), dim3(C::kThreads), 0, st, a);
+  else hipLaunchKernelGGL((k_gemm_nt<CfgSmall, T, false>), dim3((unsigned)nwg), dim3(CfgSmall::kThreads), 0, st, a);
+}
+
+int env_mode(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v && v[0] ? std::atoi(v) : dflt;
+}
+}  // namespace
+
+void gemm_nt(int dt, const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M,
+             int64_t N, int64_t K, const GemmEpilogue& epi, hipStream_t st) {
+  if (!gemm_supported(M, N, K, lda, ldb, ldc, A, B, C))
+    throw std::runtime_error("gemm_nt: unsupported shape/layout (need K%8==0, N%8==0, ld%8==0, 16B-aligned)");
+  if ((epi.pre_out || epi.aux_in) && (epi.ld_aux % 8 != 0 || epi.ld_aux < N))
+    throw std::runtime_error("gemm_nt: aux leading dimension must be >= N and a multiple of 8");
+  Args a;
+  a.A = A; a.B = B; a.C = C;
+  a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+  a.M = (int)M; a.N = (int)N; a.K = (int)K;
+  a.epi = epi;
+  // BH_GEMM_GLDS=0 forces register staging; BH_GEMM_TILE=1 small / 2 big / 0 auto
+  static const bool glds_on = env_mode("BH_GEMM_GLDS", 1) != 0;
+  static const int tile_mode = env_mode("BH_GEMM_TILE", 0);
+  const bool glds = glds_on && (K % BK) == 0;
+  const int64_t big_wgs = ((M + CfgBig::BM - 1) / CfgBig::BM) * ((N + CfgBig::BN - 1) / CfgBig::BN);
+  const bool big = glds && (tile_mode == 2 || (tile_mode == 0 && big_wgs >= 256));
+  switch (dt) {
+    case kF16:
+      if (big) launch<CfgBig, f16>(a, true, st);
+      else launch<CfgSmall, f16>(a, glds, st);
+      break;
+    case kBF16:
+      if (big) launch<CfgBig, bf16>(a, true, st);
+      else launch<CfgSmall, bf16>(a, glds, st);
+      break;
+    default: throw std::runtime_error("gemm_nt: fp16 / bf16 only");
+  }
+  check_launch("gemm_nt");
+}
+
+void gemm_colsum_finalize(int dt, const float* part, int64_t slabs, int64_t N, void* out, hipStream_t st) {
+  const unsigned blocks = (unsigned)((N + 255) / 256);
+  switch (dt) {
+    case kF16: hipLaunchKernelGGL(k_colsum<f16>, dim3(blocks), dim3(256), 0, st, part, slabs, N, (f16*)out); break;
+    case kBF16: hipLaunchKernelGGL(k_colsum<bf16>, dim3(blocks), dim3(256), 0, st, part, slabs, N, (bf16*)out); break;
+    default: throw std::runtime_error("gemm_colsum_finalize: fp16 / bf16 only");
+  }
+  check_launch("gemm_colsum_finalize");
+}
+
+}  // namespace bh
