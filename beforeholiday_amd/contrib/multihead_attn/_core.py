@@ -6,6 +6,8 @@ torch ops; the memory-bound middle — mask, softmax, dropout — is ONE HIP pas
 backward (``fast_multihead_attn`` in kernels/mha.hip, dropout regenerated from a Philox seed so no
 mask tensor is stored). On CPU the same math runs as torch ops.
 """
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -84,6 +86,64 @@ def attention(q, k, v, heads, scale, mask, mask_mode, p, training):
     return torch.bmm(probs, v.transpose(0, 1)).transpose(0, 1)
 
 
+def _fused_ok(x, hd, sk):
+    """MFMA fused attention (kernels/attn.hip): head_dim 64, <= 128 keys, 16-bit GPU tensors."""
+    if not x.is_cuda or x.dtype not in (torch.float16, torch.bfloat16) or hd != 64:
+        return False
+    if os.environ.get("BH_MHA_FUSED", "1") == "0":
+        return False
+    return sk <= submodule("fused_attention").max_sk()
+
+
+class FusedSelfAttnFn(torch.autograd.Function):
+    """qkv [s, B*heads, 3, 64] (the QKV projection output, viewed) -> context [s, B*heads, 64].
+    Backward writes d(qkv) in the same layout, so the projection's dgrad / wgrad GEMMs consume it
+    without any gather of separate dq / dk / dv tensors."""
+
+    @staticmethod
+    def forward(ctx, qkv, heads, scale, mask, mask_mode, p, training):
+        seed = _seed()
+        fa = submodule("fused_attention")
+        out = fa.forward(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], mask_mode, mask, heads, scale, p, training, seed)
+        ctx.save_for_backward(qkv, mask if mask is not None else torch.empty(0))
+        ctx.args = (heads, scale, mask_mode, p, training, seed, mask is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, mask = ctx.saved_tensors
+        heads, scale, mask_mode, p, training, seed, has_mask = ctx.args
+        dqkv = torch.empty_like(qkv)
+        submodule("fused_attention").backward(
+            dout.contiguous(), qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], mask_mode, mask if has_mask else None,
+            heads, scale, p, training, seed, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2])
+        return dqkv, None, None, None, None, None, None
+
+
+class FusedEncdecAttnFn(torch.autograd.Function):
+    """q [sq, B*heads, 64], kv [sk, B*heads, 2, 64] -> context [sq, B*heads, 64]."""
+
+    @staticmethod
+    def forward(ctx, q, kv, heads, scale, mask, mask_mode, p, training):
+        seed = _seed()
+        out = submodule("fused_attention").forward(q, kv[:, :, 0], kv[:, :, 1], mask_mode, mask, heads, scale, p,
+                                                   training, seed)
+        ctx.save_for_backward(q, kv, mask if mask is not None else torch.empty(0))
+        ctx.args = (heads, scale, mask_mode, p, training, seed, mask is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, kv, mask = ctx.saved_tensors
+        heads, scale, mask_mode, p, training, seed, has_mask = ctx.args
+        dq = torch.empty_like(q)
+        dkv = torch.empty_like(kv)
+        submodule("fused_attention").backward(
+            dout.contiguous(), q, kv[:, :, 0], kv[:, :, 1], mask_mode, mask if has_mask else None, heads, scale, p,
+            training, seed, dq, dkv[:, :, 0], dkv[:, :, 1])
+        return dq, dkv, None, None, None, None, None, None
+
+
 def _linear(x2d, w, b):
     return torch.addmm(b, x2d, w.t()) if b is not None else torch.mm(x2d, w.t())
 
@@ -93,9 +153,12 @@ def self_attention(use_time_mask, is_training, heads, scale, inputs, input_weigh
     s, b, e = inputs.shape
     hd = e // heads
     qkv = _linear(inputs.reshape(s * b, e), input_weights, input_biases).view(s, b * heads, 3, hd)
-    q, k, v = qkv[:, :, 0, :], qkv[:, :, 1, :], qkv[:, :, 2, :]
-    ctxt = attention(q, k, v, heads, scale, mask, mask_mode_for(mask, use_time_mask, mask_additive), dropout_prob,
-                     is_training)
+    mode = mask_mode_for(mask, use_time_mask, mask_additive)
+    if _fused_ok(qkv, hd, s):
+        ctxt = FusedSelfAttnFn.apply(qkv, heads, scale, mask, mode, dropout_prob, is_training)
+    else:
+        q, k, v = qkv[:, :, 0, :], qkv[:, :, 1, :], qkv[:, :, 2, :]
+        ctxt = attention(q, k, v, heads, scale, mask, mode, dropout_prob, is_training)
     out = _linear(ctxt.reshape(s * b, e), output_weights, output_biases)
     return out.view(s, b, e)
 
@@ -108,9 +171,12 @@ def encdec_attention(use_time_mask, is_training, heads, scale, inputs_q, inputs_
     hd = e // heads
     q = _linear(inputs_q.reshape(sq * b, e), input_weights_q, input_biases_q).view(sq, b * heads, hd)
     kv = _linear(inputs_kv.reshape(sk * b, e), input_weights_kv, input_biases_kv).view(sk, b * heads, 2, hd)
-    k, v = kv[:, :, 0, :], kv[:, :, 1, :]
-    ctxt = attention(q, k, v, heads, scale, mask, mask_mode_for(mask, use_time_mask, False), dropout_prob,
-                     is_training)
+    mode = mask_mode_for(mask, use_time_mask, False)
+    if _fused_ok(q, hd, sk):
+        ctxt = FusedEncdecAttnFn.apply(q, kv, heads, scale, mask, mode, dropout_prob, is_training)
+    else:
+        k, v = kv[:, :, 0, :], kv[:, :, 1, :]
+        ctxt = attention(q, k, v, heads, scale, mask, mode, dropout_prob, is_training)
     return _linear(ctxt.reshape(sq * b, e), output_weights, output_biases).view(sq, b, e)
 
 

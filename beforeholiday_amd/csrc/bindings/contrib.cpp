@@ -4,6 +4,7 @@
 #include "common.h"
 
 #include "bh/contrib_api.h"
+#include "bh/attn_api.h"
 #include "bh/mha_api.h"
 #include "bh/sparsity_api.h"
 #include "bh/transducer_api.h"
@@ -213,9 +214,89 @@ std::vector<at::Tensor> perm_pair_gains(at::Tensor m, at::Tensor pairs) {
   return {gain, split};
 }
 
+
+// ---- fused attention (kernels/attn.hip). q/k/v/outputs are [time, batch*heads, 64] views with a
+// contiguous last dim (arbitrary time / batch*heads strides).
+void attn_check(const at::Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.dim() == 3 && t.size(2) == 64 && t.stride(2) == 1, name, ": expected a [t, bh, 64] view with stride(2)==1");
+  TORCH_CHECK(t.stride(0) % 8 == 0 && t.stride(1) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              name, ": strides must be multiples of 8 elements and the base 16-byte aligned");
+}
+
+bh::AttnArgs attn_args(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, int mask_mode,
+                       const c10::optional<at::Tensor>& mask, int64_t heads, double scale, double p, bool training,
+                       int64_t seed, at::Tensor& mask_keep) {
+  attn_check(q, "q");
+  attn_check(k, "k");
+  attn_check(v, "v");
+  TORCH_CHECK(q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type(), "attn: dtype mismatch");
+  TORCH_CHECK(k.size(0) == v.size(0) && q.size(1) == k.size(1) && q.size(1) == v.size(1), "attn: shape mismatch");
+  TORCH_CHECK(k.size(0) <= bh::attn_max_sk(), "attn: sk > ", bh::attn_max_sk());
+  bh::AttnArgs a;
+  a.q = q.data_ptr(); a.k = k.data_ptr(); a.v = v.data_ptr();
+  a.q_st = q.stride(0); a.q_sbh = q.stride(1);
+  a.k_st = k.stride(0); a.k_sbh = k.stride(1);
+  a.v_st = v.stride(0); a.v_sbh = v.stride(1);
+  a.sq = (int)q.size(0); a.sk = (int)k.size(0); a.BH = (int)q.size(1); a.heads = (int)heads;
+  a.mask_mode = mask_mode;
+  if (mask_mode != 0) {
+    TORCH_CHECK(mask.has_value() && mask->defined(), "attn: mask_mode needs a mask");
+    if (mask_mode == 2) mask_keep = mask->to(at::kFloat).contiguous();
+    else mask_keep = mask->to(at::kByte).contiguous();
+    const int64_t want = mask_mode == 3 ? (int64_t)a.sq * a.sk : (int64_t)(a.BH / a.heads) * a.sk;
+    TORCH_CHECK(mask_keep.numel() == want, "attn: mask has ", mask_keep.numel(), " elements, expected ", want);
+    a.mask = mask_keep.data_ptr();
+  }
+  a.scale = (float)scale;
+  a.p_drop = (float)p;
+  a.training = training;
+  a.seed = (uint64_t)seed;
+  return a;
+}
+
+at::Tensor attn_fwd(at::Tensor q, at::Tensor k, at::Tensor v, int mask_mode, c10::optional<at::Tensor> mask,
+                    int64_t heads, double scale, double p, bool training, int64_t seed) {
+  at::Tensor mk;
+  auto a = attn_args(q, k, v, mask_mode, mask, heads, scale, p, training, seed, mk);
+  auto o = at::empty({q.size(0), q.size(1), 64}, q.options());
+  a.o = o.data_ptr();
+  a.o_st = o.stride(0);
+  a.o_sbh = o.stride(1);
+  bh::attn_forward(dtype_code(q.scalar_type()), a, stream_for(q));
+  return o;
+}
+
+void attn_bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, int mask_mode,
+              c10::optional<at::Tensor> mask, int64_t heads, double scale, double p, bool training, int64_t seed,
+              at::Tensor dq, at::Tensor dk, at::Tensor dv) {
+  at::Tensor mk;
+  auto a = attn_args(q, k, v, mask_mode, mask, heads, scale, p, training, seed, mk);
+  attn_check(dout, "dout");
+  attn_check(dq, "dq");
+  attn_check(dk, "dk");
+  attn_check(dv, "dv");
+  a.dout = dout.data_ptr(); a.do_st = dout.stride(0); a.do_sbh = dout.stride(1);
+  a.dq = dq.data_ptr(); a.dq_st = dq.stride(0); a.dq_sbh = dq.stride(1);
+  a.dk = dk.data_ptr(); a.dk_st = dk.stride(0); a.dk_sbh = dk.stride(1);
+  a.dv = dv.data_ptr(); a.dv_st = dv.stride(0); a.dv_sbh = dv.stride(1);
+  bh::attn_backward(dtype_code(q.scalar_type()), a, stream_for(q));
+}
+
+void register_contrib_impl(pybind11::module_& root);
+
 }  // namespace
 
 void register_contrib(pybind11::module_& root) {
+  register_contrib_impl(root);
+  auto fa = root.def_submodule("fused_attention", "MFMA fused short-sequence attention (head_dim 64, sk <= 128)");
+  fa.def("forward", &attn_fwd);
+  fa.def("backward", &attn_bwd);
+  fa.def("max_sk", &bh::attn_max_sk);
+}
+
+namespace {
+void register_contrib_impl(pybind11::module_& root) {
   auto fl = root.def_submodule("focal_loss_cuda", "sigmoid focal loss");
   fl.def("forward", &focal_fwd);
   fl.def("backward", &focal_bwd);
@@ -236,5 +317,7 @@ void register_contrib(pybind11::module_& root) {
     im.def((std::string(p) + "backward_backward").c_str(), &imul_bwd_bwd);
   }
 }
+
+}  // namespace
 
 }  // namespace bhb

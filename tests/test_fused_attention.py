@@ -1,0 +1,136 @@
+"""MFMA fused short-sequence attention (kernels/attn.hip) vs an fp32 PyTorch reference.
+
+Forward O = dropout(softmax(scale * Q K^T + mask)) V and the backward dQ / dK / dV, with q / k / v
+as strided views of a fused [t, B*heads, 3, 64] QKV tensor (the MHA layout). Dropout is checked by
+recovering the kernel's keep mask through V = I (O then equals the dropped probabilities) and
+running the reference backward with that same mask.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _fa():
+    from beforeholiday_amd._native import submodule
+
+    return submodule("fused_attention")
+
+
+def _reference(q, k, v, scale, mask_mode, mask, heads, keep=None, p=0.0):
+    # q [sq, BH, 64], k/v [sk, BH, 64] fp32 -> [sq, BH, 64]
+    s = torch.einsum("qbd,kbd->bqk", q, k) * scale
+    BH, sq, sk = s.shape
+    if mask_mode == 1:
+        s = s.view(-1, heads, sq, sk).masked_fill(mask.view(-1, 1, 1, sk).bool(), float("-inf")).view(BH, sq, sk)
+    elif mask_mode == 2:
+        s = (s.view(-1, heads, sq, sk) + mask.view(-1, 1, 1, sk).float()).view(BH, sq, sk)
+    elif mask_mode == 3:
+        s = s.masked_fill(mask.view(1, sq, sk).bool(), float("-inf"))
+    pr = torch.softmax(s, -1).nan_to_num(0.0)
+    if keep is not None:
+        pr = pr * keep / (1 - p)
+    return torch.einsum("bqk,kbd->qbd", pr, v)
+
+
+def _make(sq, sk, B, heads, dtype, mask_mode, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    BH = B * heads
+    q_src = torch.randn(sq, BH, 3, 64, device="cuda", dtype=dtype, generator=g)
+    kv_src = torch.randn(sk, BH, 3, 64, device="cuda", dtype=dtype, generator=g) if sk != sq else q_src
+    q, k, v = q_src[:, :, 0], kv_src[:, :, 1], kv_src[:, :, 2]
+    mask = None
+    if mask_mode == 1:
+        mask = torch.rand(B, sk, device="cuda", generator=g) < 0.3
+        mask[0, :] = True  # a fully masked batch row -> zeros
+    elif mask_mode == 2:
+        mask = torch.randn(B, sk, device="cuda", generator=g)
+    elif mask_mode == 3:
+        mask = torch.triu(torch.ones(sq, sk, device="cuda", dtype=torch.bool), diagonal=1)
+    return q, k, v, mask
+
+
+SHAPES = [(64, 64), (37, 50), (128, 128), (100, 128), (130, 64), (16, 120)]
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("mask_mode", [0, 1, 2, 3])
+def test_forward_backward_no_dropout(dtype, shape, mask_mode):
+    sq, sk = shape
+    if mask_mode == 3 and sq != sk:
+        pytest.skip("time mask is square in the MHA module")
+    B, heads = 3, 2
+    q, k, v, mask = _make(sq, sk, B, heads, dtype, mask_mode)
+    scale = 64 ** -0.5
+    out = _fa().forward(q, k, v, mask_mode, mask, heads, scale, 0.0, True, 123)
+    qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
+    ref = _reference(qf, kf, vf, scale, mask_mode, mask, heads)
+    tol = 2e-2 if dtype == torch.float16 else 5e-2
+    torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol)
+
+    dout = torch.randn_like(out)
+    ref.backward(dout.float())
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    _fa().backward(dout, q, k, v, mask_mode, mask, heads, scale, 0.0, True, 123, dq, dk, dv)
+    for got, want in ((dq, qf.grad), (dk, kf.grad), (dv, vf.grad)):
+        torch.testing.assert_close(got.float(), want, rtol=tol, atol=tol * 2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("sq", [64, 96])
+def test_dropout_mask_regenerated_in_backward(dtype, sq):
+    sk, B, heads, p = 64, 2, 4, 0.25
+    BH = B * heads
+    q, k, _, _ = _make(sq, sk, B, heads, dtype, 0, seed=5)
+    eye = torch.eye(64, device="cuda", dtype=dtype).unsqueeze(1).expand(64, BH, 64).contiguous()
+    scale = 0.125
+    o1 = _fa().forward(q, k, eye, 0, None, heads, scale, p, True, 777)
+    o2 = _fa().forward(q, k, eye, 0, None, heads, scale, p, True, 777)
+    assert torch.equal(o1, o2)  # counter-based RNG: same seed, same mask
+    keep = (o1.float() != 0).permute(1, 0, 2).float()  # [BH, sq, sk]; P > 0 everywhere (no mask)
+    frac = keep.mean().item()
+    assert abs(frac - (1 - p)) < 0.03, frac
+    qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, eye))
+    ref = _reference(qf, kf, vf, scale, 0, None, heads, keep=keep, p=p)
+    tol = 2e-2 if dtype == torch.float16 else 5e-2
+    torch.testing.assert_close(o1.float(), ref, rtol=tol, atol=tol)
+    dout = torch.randn_like(o1)
+    ref.backward(dout.float())
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(eye)
+    _fa().backward(dout, q, k, eye, 0, None, heads, scale, p, True, 777, dq, dk, dv)
+    for got, want in ((dq, qf.grad), (dk, kf.grad), (dv, vf.grad)):
+        torch.testing.assert_close(got.float(), want, rtol=tol, atol=tol * 2)
+
+
+def test_eval_mode_ignores_dropout():
+    q, k, v, _ = _make(64, 64, 2, 2, torch.float16, 0)
+    a = _fa().forward(q, k, v, 0, None, 2, 0.125, 0.5, False, 1)
+    b = _fa().forward(q, k, v, 0, None, 2, 0.125, 0.0, True, 2)
+    torch.testing.assert_close(a, b)
+
+
+@pytest.mark.parametrize("impl", ["fast", "default"])
+@pytest.mark.parametrize("mask", [None, "pad"])
+def test_self_mha_module_fused_matches_unfused(impl, mask, monkeypatch):
+    """The module's fused path (MFMA attention) vs its unfused path (baddbmm + softmax kernel + bmm)."""
+    from beforeholiday_amd.contrib.multihead_attn import SelfMultiheadAttn
+
+    torch.manual_seed(0)
+    m = SelfMultiheadAttn(1024, 16, dropout=0.0, bias=True, impl=impl).cuda().half()
+    x = torch.randn(64, 8, 1024, device="cuda", dtype=torch.half)
+    kpm = (torch.rand(8, 64, device="cuda") < 0.2) if mask == "pad" else None
+
+    def run(fused):
+        monkeypatch.setenv("BH_MHA_FUSED", "1" if fused else "0")
+        xi = x.clone().requires_grad_(True)
+        m.zero_grad()
+        out, _ = m(xi, xi, xi, key_padding_mask=kpm, need_weights=False, attn_mask=None, is_training=True)
+        out.backward(torch.ones_like(out) * 0.01)
+        return out.float(), xi.grad.float(), m.in_proj_weight.grad.float()
+
+    o1, g1, w1 = run(True)
+    o0, g0, w0 = run(False)
+    torch.testing.assert_close(o1, o0, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(g1, g0, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(w1, w0, rtol=5e-2, atol=5e-2)
