@@ -2,13 +2,15 @@
 (reference: apex/contrib/fmha/fmha.py:34-76, ``fmhalib``: sm80-only kernels for seq <= 512, head 64).
 
 Input ``qkv`` [total_tokens, 3, heads, head_dim] with ``cu_seqlens`` [batch + 1]. Sequences are
-scattered into a padded [B, S] batch once; Q·K^T and P·V are batched GEMMs (hipBLASLt) and the
-key-padding mask + softmax + dropout is the fused HIP kernel of ``contrib.multihead_attn``
-(Philox dropout regenerated in backward). Any sequence length up to 4096 and any head size.
+scattered into a padded batch once. Head size 64 with at most 128 tokens per sequence (the
+reference's own limits are 512 / 64) runs the MFMA fused attention kernel (kernels/attn.hip, key
+padding mask, Philox dropout regenerated in backward) on a [S, B*heads, 3, 64] padded layout;
+anything else uses batched GEMMs (hipBLASLt) around the fused mask + softmax + dropout kernel of
+``contrib.multihead_attn``. Any sequence length up to 4096 and any head size.
 """
 import torch
 
-from ..multihead_attn._core import MASK_PAD, MaskSoftmaxDropoutFn
+from ..multihead_attn._core import MASK_PAD, FusedSelfAttnFn, MaskSoftmaxDropoutFn, _fused_ok
 
 
 def fmha_varlen(qkv, cu_seqlens, p_dropout, max_s, is_training):
@@ -19,6 +21,16 @@ def fmha_varlen(qkv, cu_seqlens, p_dropout, max_s, is_training):
     S = max(max(lens), 1) if lens else 1
     pos = torch.arange(S, device=qkv.device).unsqueeze(0)
     valid = pos < torch.tensor(lens, device=qkv.device).unsqueeze(1)  # [B, S]
+    if _fused_ok(qkv, d, S):
+        # [S, B, heads, 3, d] -> q/k/v are [S, B*heads, d] views with a uniform batch*head stride
+        padded = qkv.new_zeros(S, B, h, 3, d)
+        tok = valid.t().nonzero(as_tuple=True)  # (t, b) of every valid token
+        src = qkv[(cu_seqlens[:-1][tok[1]] + tok[0]).long()]  # [n, 3, h, d]
+        padded[tok[0], tok[1]] = src.permute(0, 2, 1, 3)
+        ctx = FusedSelfAttnFn.apply(padded.view(S, B * h, 3, d), h, d ** -0.5, ~valid, MASK_PAD, p_dropout,
+                                    is_training)
+        ctx = ctx.view(S, B, h, d).transpose(0, 1)  # [B, S, h, d]
+        return ctx[valid]
     padded = qkv.new_zeros(B, S, 3, h, d)
     padded = padded.index_put((valid.nonzero(as_tuple=True)), qkv)
     q, k, v = (padded[:, :, i].permute(0, 2, 1, 3) for i in range(3))  # [B, h, S, d]

@@ -1,0 +1,43 @@
+"""Average rocprofv3 counter values per kernel over all passes under <dir>/p*/ and print a table
+(MFMA busy share, LDS bank-conflict share, L2 hit rate where the counters are present)."""
+import collections
+import csv
+import glob
+import os
+import sys
+
+
+def main():
+    d = sys.argv[1]
+    vals = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                name = r.get("Kernel_Name", "?")
+                if "gemm_nt" in name:
+                    big = "Li8ELi4E" in name or "Cfg<2, 4, 8, 4, 2>" in name
+                    name = "gemm_nt<" + ("256x256" if big else "128x128") + ">"
+                elif "attn_fwd" in name:
+                    name = "attn_fwd"
+                elif "attn_bwd" in name:
+                    name = "attn_bwd"
+                else:
+                    continue
+                vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                vals[name]["duration_us"].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    print("| kernel | counter | mean per dispatch |")
+    print("|---|---|---|")
+    for k in sorted(vals):
+        m = {c: sum(v) / len(v) for c, v in vals[k].items()}
+        for c in sorted(m):
+            print(f"| {k} | {c} | {m[c]:.4g} |")
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in m and "SQ_BUSY_CYCLES" in m and m["SQ_BUSY_CYCLES"]:
+            print(f"| {k} | MFMA busy / SQ busy | {m['SQ_VALU_MFMA_BUSY_CYCLES'] / m['SQ_BUSY_CYCLES']:.3f} |")
+        if "SQ_LDS_BANK_CONFLICT" in m and m.get("SQ_LDS_IDX_ACTIVE"):
+            print(f"| {k} | LDS bank-conflict cycles / LDS active | {m['SQ_LDS_BANK_CONFLICT'] / m['SQ_LDS_IDX_ACTIVE']:.3f} |")
+        if "TCC_HIT_sum" in m and (m["TCC_HIT_sum"] + m.get("TCC_MISS_sum", 0)):
+            print(f"| {k} | L2 hit rate | {m['TCC_HIT_sum'] / (m['TCC_HIT_sum'] + m['TCC_MISS_sum']):.3f} |")
+
+
+if __name__ == "__main__":
+    main()

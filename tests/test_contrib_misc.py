@@ -163,3 +163,32 @@ def test_fmha_varlen(device):
     g1 = torch.autograd.grad(out.sum(), qkv, retain_graph=True)[0]
     g2 = torch.autograd.grad(ref.sum(), qkv)[0]
     torch.testing.assert_close(g1, g2, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_fmha_varlen_fused_attention_path(dtype):
+    """head 64, <= 128 tokens: FMHA runs the MFMA fused attention kernel; compare with fp32 math."""
+    from beforeholiday_amd.contrib.fmha import FMHA
+    torch.manual_seed(5)
+    h, d = 4, 64
+    lens = [37, 64, 100, 1]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), device="cuda")
+    qkv = torch.randn(sum(lens), 3 * h * d, device="cuda", dtype=dtype, requires_grad=True)
+    cfg = types.SimpleNamespace(attention_probs_dropout_prob=0.0, num_attention_heads=h, hidden_size=h * d)
+    out = FMHA(cfg)(qkv, cu, max(lens), is_training=True)
+    qf = qkv.detach().float().requires_grad_(True)
+    q3 = qf.view(-1, 3, h, d)
+    refs = []
+    for i, n in enumerate(lens):
+        s = slice(int(cu[i]), int(cu[i + 1]))
+        q, k, v = (q3[s, j].transpose(0, 1) for j in range(3))
+        p = torch.softmax(q @ k.transpose(-1, -2) / d ** 0.5, -1)
+        refs.append((p @ v).transpose(0, 1).reshape(n, h * d))
+    ref = torch.cat(refs)
+    tol = 2e-2 if dtype == torch.float16 else 5e-2
+    torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol)
+    g = torch.randn_like(out)
+    g1 = torch.autograd.grad(out, qkv, g)[0]
+    g2 = torch.autograd.grad(ref, qf, g.float())[0]
+    torch.testing.assert_close(g1.float(), g2, rtol=tol, atol=tol * 2)
