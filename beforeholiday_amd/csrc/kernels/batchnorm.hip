@@ -742,10 +742,19 @@ int64_t knob_stat_blocks() { static const int64_t v = env_knob("BH_BN_STAT_BLOCK
 int64_t knob_red_blocks() { static const int64_t v = env_knob("BH_BN_RED_BLOCKS", 256); return v; }
 int64_t knob_red_rows() { static const int64_t v = env_knob("BH_BN_RED_ROWS", 32); return v; }
 
+// small-layer split boost: measured slower on MI355X (bench_bn.py: 28x28x128 stats 27 -> 35 us, the
+// finalize merges more partials), so off by default; BH_BN_SMALL_ELEMS=<elements> enables it.
+int64_t knob_small_elems() { static const int64_t v = env_knob("BH_BN_SMALL_ELEMS", 0); return v; }
+
 int64_t nhwc_splits(const BNShape& s, int64_t target, int64_t min_iter) {
   const NhwcGeom g = nhwc_geom(s.C);
   int64_t splits = std::max<int64_t>(1, target / g.gx);
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, s.outer / (g.R * min_iter)));
+  // Small layers (ResNet stages 2-4 at batch 256: 6-32 M elements) are latency-bound with the
+  // big-layer geometry: each lane walks 32+ rows in dependent rounds of 4 loads (15 us for a 13 MB
+  // tensor). Spread them over up to 1024 workgroups at >= 8 rows per lane instead.
+  if (s.outer * (int64_t)s.C <= knob_small_elems() && g.gx * splits < 1024)
+    splits = std::max<int64_t>(splits, std::min<int64_t>(1024 / g.gx, std::max<int64_t>(1, s.outer / (g.R * 8))));
   return std::max<int64_t>(1, splits);
 }
 

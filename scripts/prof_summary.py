@@ -50,6 +50,16 @@ def main():
     lines.append("|---|---|---|---|")
     for k, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:60]:
         lines.append(f"| `{k}` | {t / n / 1e6:.3f} | {100.0 * t / max(busy, 1):.1f}% | {c / n:.1f} |")
+    # per-launch durations (us) of the last step for the top kernels, in launch order
+    last = rows[marks[-2] + 1: marks[-1] + 1] if len(marks) >= 2 else seg
+    per = collections.defaultdict(list)
+    for s_, e_, name in last:
+        per[re.sub(r"\(.*", "", name)[:110]].append(round((e_ - s_) / 1e3, 1))
+    lines.append("\n## per-launch us (last step, launch order) for kernels > 0.5 ms/step\n")
+    for k, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0]):
+        if t / n / 1e6 < 0.5:
+            break
+        lines.append(f"* `{k[:60]}`: {per[k]}")
     text = "\n".join(lines) + "\n"
     with open(out, "w") as fh:
         fh.write(text)
