@@ -36,7 +36,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256, help="images per GPU")
-    ap.add_argument("--opt-level", default="O2", choices=["O2", "O5"], help="O2: fp16 (reference), O5: bf16")
+    ap.add_argument("--opt-level", default="O2", choices=["O1", "O2", "O4", "O5"],
+                    help="O2: fp16 model + fp32 master weights (reference headline), O5: its bf16 twin; "
+                         "O1 / O4: fp32 model with fp16 / bf16 casts around torch functions")
     ap.add_argument("--optimizer", default="lamb", choices=["lamb", "adam", "sgd"])
     ap.add_argument("--no-syncbn", action="store_true")
     ap.add_argument("--message-size", type=int, default=12_500_000, help="DDP bucket size (elements)")
@@ -44,6 +46,9 @@ def parse():
     ap.add_argument("--autotune", action="store_true",
                     help="MIOpen find (cudnn.benchmark): minutes of first-step tuning on a fresh box and measured "
                          "slower (35.1 ms/step) than the immediate-mode solvers (33.1 ms/step) at batch 256")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo only to rehearse the "
+                         "multi-rank code path, e.g. several ranks sharing one GPU)")
     ap.add_argument("--conv1x1", default="miopen", choices=["miopen", "gemm"],
                     help="stride-1 1x1 convolutions: MIOpen, or GEMMs on the channels_last view")
     return ap.parse_args()
@@ -54,9 +59,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("gloo")
     torch.backends.cudnn.benchmark = args.autotune
 
     from beforeholiday_amd import amp
@@ -76,11 +85,13 @@ def main():
         opt = FusedAdam(model.parameters(), lr=1e-3, weight_decay=0.01)
     else:
         opt = FusedSGD(model.parameters(), lr=0.1 * global_batch / 256, momentum=0.9, weight_decay=1e-4)
-    model, opt = amp.initialize(model, opt, opt_level=args.opt_level, keep_batchnorm_fp32=True, verbosity=0)
+    model, opt = amp.initialize(model, opt, opt_level=args.opt_level, verbosity=0,
+                                keep_batchnorm_fp32=True if args.opt_level in ("O2", "O5") else None)
     model = DistributedDataParallel(model, message_size=args.message_size)
 
-    dt = torch.float16 if args.opt_level == "O2" else torch.bfloat16
-    x = torch.randn(args.batch, 3, 224, 224, device="cuda", dtype=dt).contiguous(memory_format=torch.channels_last)
+    dt = torch.float16 if args.opt_level in ("O1", "O2") else torch.bfloat16
+    in_dt = dt if args.opt_level in ("O2", "O5") else torch.float32  # O1/O4 models stay fp32
+    x = torch.randn(args.batch, 3, 224, 224, device="cuda", dtype=in_dt).contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 1000, (args.batch,), device="cuda")
 
     def step():
@@ -117,7 +128,7 @@ def main():
     img_s = global_batch * args.steps / elapsed
     if rank == 0:
         print(json.dumps({
-            "metric": METRIC,
+            "metric": METRIC if args.opt_level == "O2" else f"ResNet-50 amp {args.opt_level} images/sec",
             "value": round(img_s, 2),
             "unit": "images/sec",
             "n_gpus": world,
@@ -130,8 +141,9 @@ def main():
             "dtype": "fp16" if dt == torch.float16 else "bf16",
             "data": "synthetic 224x224 channels_last images, random-init weights",
             "config": {
-                "model": "ResNet-50 amp O2 + FusedLAMB + SyncBatchNorm, DDP" if args.optimizer == "lamb" and not args.no_syncbn
-                else f"ResNet-50 amp {args.opt_level} + {args.optimizer}",
+                "model": "ResNet-50 amp O2 + FusedLAMB + SyncBatchNorm, DDP"
+                if args.optimizer == "lamb" and not args.no_syncbn and args.opt_level == "O2"
+                else f"ResNet-50 amp {args.opt_level} + {args.optimizer}" + ("" if args.no_syncbn else " + SyncBatchNorm"),
                 "opt_level": args.opt_level,
                 "optimizer": {"lamb": "FusedLAMB", "adam": "FusedAdam", "sgd": "FusedSGD"}[args.optimizer],
                 "sync_batchnorm": not args.no_syncbn,
