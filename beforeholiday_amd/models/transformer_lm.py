@@ -125,6 +125,47 @@ def bias_gelu_impl(x, bias):
     return _BiasGeLU.apply(x, bias)
 
 
+class _FusedGeluMLP(torch.autograd.Function):
+    """This rank's MLP shard  y = GELU(x W1^T + b1) W2^T  on the MFMA GEMM (kernels/gemm.hip):
+    bias + GELU run in the first GEMM's epilogue (pre-activation kept as aux), and in backward the
+    dGELU and the b1 gradient run in the epilogue of the W2 dgrad GEMM. The weight-gradient and
+    input-gradient GEMMs are plain hipBLASLt GEMMs. TP collectives stay outside (ParallelMLP)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2):
+        from .._native import submodule
+
+        gm = submodule("gemm")
+        x2d = x.reshape(-1, x.size(-1))
+        inter, pre = gm.linear_act(x2d, w1, b1, _fd.ACT_GELU, True)
+        y = torch.mm(inter, w2.t())
+        ctx.save_for_backward(x2d, pre, inter, w1, w2)
+        ctx.in_shape = x.shape
+        return y.view(*x.shape[:-1], w2.size(0))
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .._native import submodule
+
+        x2d, pre, inter, w1, w2 = ctx.saved_tensors
+        dy2d = dy.reshape(-1, dy.size(-1)).contiguous()
+        dw2 = torch.mm(dy2d.t(), inter)
+        dpre, db1 = submodule("gemm").linear_dact(dy2d, w2.t().contiguous(), pre, _fd.ACT_GELU, True)
+        dw1 = torch.mm(dpre.t(), x2d)
+        dx = torch.mm(dpre, w1).view(ctx.in_shape)
+        return dx, dw1, db1, dw2
+
+
+def _fused_mlp_ok(x, mlp) -> bool:
+    import os
+
+    c, r = mlp.dense_h_to_4h, mlp.dense_4h_to_h
+    return (x.is_cuda and x.dtype in (torch.float16, torch.bfloat16) and mlp.bias_gelu_fusion
+            and c.weight.dtype == x.dtype and r.weight.dtype == x.dtype and c.bias is not None
+            and not c.gradient_accumulation_fusion and not r.gradient_accumulation_fusion
+            and os.environ.get("BH_FUSED_MLP", "1") != "0")
+
+
 def openai_gelu(x):
     return 0.5 * x * (1.0 + torch.tanh(0.7978845608028654 * x * (1.0 + 0.044715 * x * x)))
 
@@ -186,6 +227,19 @@ class ParallelMLP(MegatronModule):
             gradient_accumulation_fusion=config.gradient_accumulation_fusion)
 
     def forward(self, hidden_states):
+        if _fused_mlp_ok(hidden_states, self):
+            # same collectives as ColumnParallelLinear -> RowParallelLinear, one fused compute core
+            c, r = self.dense_h_to_4h, self.dense_4h_to_h
+            if c.sequence_parallel_enabled:
+                x = tensor_parallel.mappings.gather_from_sequence_parallel_region(hidden_states)
+            else:
+                x = tensor_parallel.mappings.copy_to_tensor_model_parallel_region(hidden_states)
+            y = _FusedGeluMLP.apply(x, c.weight, c.bias, r.weight)
+            if r.sequence_parallel_enabled:
+                y = tensor_parallel.mappings.reduce_scatter_to_sequence_parallel_region(y)
+            else:
+                y = tensor_parallel.mappings.reduce_from_tensor_model_parallel_region(y)
+            return y, r.bias
         inter, bias = self.dense_h_to_4h(hidden_states)
         if self.bias_gelu_fusion:
             inter = bias_gelu_impl(inter, bias)

@@ -211,3 +211,38 @@ def _gpt_gpu_vs_cpu(rank, world):
 @pytest.mark.gpu
 def test_gpt_gpu_fused_kernels_match_cpu():
     run_distributed(_gpt_gpu_vs_cpu, 1)
+
+
+def _gpt_fused_mlp(rank, world):
+    import os
+    from beforeholiday_amd.models import GPTModel
+    from beforeholiday_amd.transformer import parallel_state as ps
+    from beforeholiday_amd.transformer.pipeline_parallel.utils import get_ltor_masks_and_position_ids
+    ps.initialize_model_parallel(1, 1, default_backend="gloo")
+    _seed()
+    cfg = _cfg(params_dtype=torch.bfloat16, masked_softmax_fusion=True, hidden_size=256, num_attention_heads=4,
+               vocab_size=512, max_position_embeddings=64)
+    torch.manual_seed(7)
+    model = GPTModel(cfg).cuda()
+    tokens = torch.randint(0, 512, (4, 64)).cuda()
+    labels = torch.randint(0, 512, (4, 64)).cuda()
+    mask, _, pos = get_ltor_masks_and_position_ids(tokens, -1, False, False, False)
+    res = {}
+    for fused in ("1", "0"):
+        os.environ["BH_FUSED_MLP"] = fused
+        model.zero_grad(set_to_none=True)
+        loss = model(tokens, pos, mask, labels=labels)
+        loss.float().mean().backward()
+        mlp = model.language_model.encoder.layers[0].mlp
+        res[fused] = (loss.detach().float(), mlp.dense_h_to_4h.weight.grad.float(), mlp.dense_h_to_4h.bias.grad.float(),
+                      mlp.dense_4h_to_h.weight.grad.float(), model.language_model.embedding.word_embeddings.weight.grad.float())
+    os.environ.pop("BH_FUSED_MLP")
+    for a, b in zip(res["1"], res["0"]):
+        torch.testing.assert_close(a, b, rtol=5e-2, atol=5e-2)
+    ps.destroy_model_parallel()
+
+
+@pytest.mark.gpu
+def test_gpt_fused_mfma_mlp_matches_unfused():
+    """ParallelMLP on the MFMA GEMM (bias+GELU epilogue, dGELU+bias-grad epilogue) == the unfused path."""
+    run_distributed(_gpt_fused_mlp, 1)
