@@ -67,6 +67,7 @@ template <int WM_, int WN_, int TM_, int TN_, int STAGES_> struct Cfg {
 };
 using CfgSmall = Cfg<2, 2, 4, 4, 2>;
 using CfgBig = Cfg<2, 4, 8, 4, 2>;
+using CfgMid = Cfg<4, 2, 4, 4, 3>;  // 256x128, 8 waves of 64x64, 3-stage LDS-DMA ring (144 KiB)
 constexpr int kGroupM = 8;
 
 template <typename T> struct Mfma;
@@ -396,19 +397,22 @@ void gemm_nt(int dt, const void* A, int64_t lda, const void* B, int64_t ldb, voi
   a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.M = (int)M; a.N = (int)N; a.K = (int)K;
   a.epi = epi;
-  // BH_GEMM_GLDS=0 forces register staging; BH_GEMM_TILE=1 small / 2 big / 0 auto
+  // BH_GEMM_GLDS=0 forces register staging; BH_GEMM_TILE=1 small / 2 big / 3 mid / 0 auto
   static const bool glds_on = env_mode("BH_GEMM_GLDS", 1) != 0;
   static const int tile_mode = env_mode("BH_GEMM_TILE", 0);
   const bool glds = glds_on && (K % BK) == 0;
   const int64_t big_wgs = ((M + CfgBig::BM - 1) / CfgBig::BM) * ((N + CfgBig::BN - 1) / CfgBig::BN);
   const bool big = glds && (tile_mode == 2 || (tile_mode == 0 && big_wgs >= 256));
+  const bool mid = glds && tile_mode == 3;
   switch (dt) {
     case kF16:
-      if (big) launch<CfgBig, f16>(a, true, st);
+      if (mid) launch<CfgMid, f16>(a, true, st);
+      else if (big) launch<CfgBig, f16>(a, true, st);
       else launch<CfgSmall, f16>(a, glds, st);
       break;
     case kBF16:
-      if (big) launch<CfgBig, bf16>(a, true, st);
+      if (mid) launch<CfgMid, bf16>(a, true, st);
+      else if (big) launch<CfgBig, bf16>(a, true, st);
       else launch<CfgSmall, bf16>(a, glds, st);
       break;
     default: throw std::runtime_error("gemm_nt: fp16 / bf16 only");
