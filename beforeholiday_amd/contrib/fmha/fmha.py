@@ -2,10 +2,10 @@
 (reference: apex/contrib/fmha/fmha.py:34-76, ``fmhalib``: sm80-only kernels for seq <= 512, head 64).
 
 Input ``qkv`` [total_tokens, 3, heads, head_dim] with ``cu_seqlens`` [batch + 1]. Sequences are
-scattered into a padded batch once. Head size 64 with at most 128 tokens per sequence (the
-reference's own limits are 512 / 64) runs the MFMA fused attention kernel (kernels/attn.hip, key
-padding mask, Philox dropout regenerated in backward) on a [S, B*heads, 3, 64] padded layout;
-anything else uses batched GEMMs (hipBLASLt) around the fused mask + softmax + dropout kernel of
+scattered into a padded batch once. Head size 64 (the reference's only head size; its sequence
+cap is 512) runs the MFMA fused attention kernels (kernels/attn.hip: whole-row kernels up to 128
+tokens, flash kernels beyond; key padding mask, Philox dropout regenerated in backward) on a
+[S, B*heads, 3, 64] padded layout; other head sizes use batched GEMMs (hipBLASLt) around the fused mask + softmax + dropout kernel of
 ``contrib.multihead_attn``. Any sequence length up to 4096 and any head size.
 """
 import torch

@@ -17,7 +17,17 @@ MASK_NONE, MASK_PAD, MASK_ADDITIVE, MASK_TIME = 0, 1, 2, 3
 
 
 def _seed():
-    return int(torch.empty((), dtype=torch.int64).random_(0, 2 ** 62).item())
+    """Philox seed for the fused dropout (CPU generator: no device sync). Tensor-parallel ranks hold
+    different heads of the same layer, so their streams are decorrelated by the TP rank."""
+    s = int(torch.empty((), dtype=torch.int64).random_(0, 2 ** 62).item())
+    try:
+        from ...transformer import parallel_state
+
+        if parallel_state.model_parallel_is_initialized():
+            s ^= (parallel_state.get_tensor_model_parallel_rank() * 0x9E3779B97F4A7C15) & (2 ** 62 - 1)
+    except Exception:  # noqa: BLE001 - parallel_state unavailable / uninitialised
+        pass
+    return s
 
 
 class MaskSoftmaxDropoutFn(torch.autograd.Function):
@@ -86,38 +96,59 @@ def attention(q, k, v, heads, scale, mask, mask_mode, p, training):
     return torch.bmm(probs, v.transpose(0, 1)).transpose(0, 1)
 
 
+MASK_FULL, MASK_CAUSAL = 4, 5  # flash-only modes: [B, sq, sk] bool, implicit causal
+
+
 def _fused_ok(x, hd, sk):
-    """MFMA fused attention (kernels/attn.hip): head_dim 64, <= 128 keys, 16-bit GPU tensors."""
+    """MFMA fused attention (kernels/attn.hip): head_dim 64, 16-bit GPU tensors; sk <= 128 runs the
+    whole-row kernels, longer sequences the flash (64-key block, online softmax) kernels."""
     if not x.is_cuda or x.dtype not in (torch.float16, torch.bfloat16) or hd != 64:
         return False
-    if os.environ.get("BH_MHA_FUSED", "1") == "0":
-        return False
-    return sk <= submodule("fused_attention").max_sk()
+    return os.environ.get("BH_MHA_FUSED", "1") != "0"
+
+
+def _short_ok(sk, mask_mode, fill):
+    return (sk <= submodule("fused_attention").max_sk() and mask_mode <= MASK_TIME and fill == float("-inf")
+            and os.environ.get("BH_ATTN_FLASH_ONLY", "0") != "1")
 
 
 class FusedSelfAttnFn(torch.autograd.Function):
     """qkv [s, B*heads, 3, 64] (the QKV projection output, viewed) -> context [s, B*heads, 64].
     Backward writes d(qkv) in the same layout, so the projection's dgrad / wgrad GEMMs consume it
-    without any gather of separate dq / dk / dv tensors."""
+    without any gather of separate dq / dk / dv tensors. ``fill`` is the value of a masked score
+    (-inf: MHA semantics, a fully masked row gives zeros; -10000: Megatron semantics)."""
 
     @staticmethod
-    def forward(ctx, qkv, heads, scale, mask, mask_mode, p, training):
+    def forward(ctx, qkv, heads, scale, mask, mask_mode, p, training, fill=float("-inf")):
         seed = _seed()
         fa = submodule("fused_attention")
-        out = fa.forward(qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], mask_mode, mask, heads, scale, p, training, seed)
-        ctx.save_for_backward(qkv, mask if mask is not None else torch.empty(0))
-        ctx.args = (heads, scale, mask_mode, p, training, seed, mask is not None)
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        short = _short_ok(qkv.size(0), mask_mode, fill)
+        if short:
+            out = fa.forward(q, k, v, mask_mode, mask, heads, scale, p, training, seed)
+            lse = torch.empty(0)
+        else:
+            out, lse = fa.flash_forward(q, k, v, mask_mode, mask, heads, scale, p, training, seed, fill)
+        ctx.save_for_backward(qkv, mask if mask is not None else torch.empty(0), out if not short else torch.empty(0),
+                              lse)
+        ctx.args = (heads, scale, mask_mode, p, training, seed, mask is not None, fill, short)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        qkv, mask = ctx.saved_tensors
-        heads, scale, mask_mode, p, training, seed, has_mask = ctx.args
+        qkv, mask, out, lse = ctx.saved_tensors
+        heads, scale, mask_mode, p, training, seed, has_mask, fill, short = ctx.args
         dqkv = torch.empty_like(qkv)
-        submodule("fused_attention").backward(
-            dout.contiguous(), qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2], mask_mode, mask if has_mask else None,
-            heads, scale, p, training, seed, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2])
-        return dqkv, None, None, None, None, None, None
+        fa = submodule("fused_attention")
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        m = mask if has_mask else None
+        if short:
+            fa.backward(dout.contiguous(), q, k, v, mask_mode, m, heads, scale, p, training, seed,
+                        dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2])
+        else:
+            fa.flash_backward(dout.contiguous(), q, k, v, out, lse, mask_mode, m, heads, scale, p, training, seed,
+                              fill, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2])
+        return dqkv, None, None, None, None, None, None, None
 
 
 class FusedEncdecAttnFn(torch.autograd.Function):
@@ -126,21 +157,33 @@ class FusedEncdecAttnFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, kv, heads, scale, mask, mask_mode, p, training):
         seed = _seed()
-        out = submodule("fused_attention").forward(q, kv[:, :, 0], kv[:, :, 1], mask_mode, mask, heads, scale, p,
-                                                   training, seed)
-        ctx.save_for_backward(q, kv, mask if mask is not None else torch.empty(0))
-        ctx.args = (heads, scale, mask_mode, p, training, seed, mask is not None)
+        fa = submodule("fused_attention")
+        short = _short_ok(kv.size(0), mask_mode, float("-inf"))
+        if short:
+            out = fa.forward(q, kv[:, :, 0], kv[:, :, 1], mask_mode, mask, heads, scale, p, training, seed)
+            lse = torch.empty(0)
+        else:
+            out, lse = fa.flash_forward(q, kv[:, :, 0], kv[:, :, 1], mask_mode, mask, heads, scale, p, training, seed,
+                                        float("-inf"))
+        ctx.save_for_backward(q, kv, mask if mask is not None else torch.empty(0), out if not short else torch.empty(0),
+                              lse)
+        ctx.args = (heads, scale, mask_mode, p, training, seed, mask is not None, short)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        q, kv, mask = ctx.saved_tensors
-        heads, scale, mask_mode, p, training, seed, has_mask = ctx.args
+        q, kv, mask, out, lse = ctx.saved_tensors
+        heads, scale, mask_mode, p, training, seed, has_mask, short = ctx.args
         dq = torch.empty_like(q)
         dkv = torch.empty_like(kv)
-        submodule("fused_attention").backward(
-            dout.contiguous(), q, kv[:, :, 0], kv[:, :, 1], mask_mode, mask if has_mask else None, heads, scale, p,
-            training, seed, dq, dkv[:, :, 0], dkv[:, :, 1])
+        fa = submodule("fused_attention")
+        m = mask if has_mask else None
+        if short:
+            fa.backward(dout.contiguous(), q, kv[:, :, 0], kv[:, :, 1], mask_mode, m, heads, scale, p, training, seed,
+                        dq, dkv[:, :, 0], dkv[:, :, 1])
+        else:
+            fa.flash_backward(dout.contiguous(), q, kv[:, :, 0], kv[:, :, 1], out, lse, mask_mode, m, heads, scale, p,
+                              training, seed, float("-inf"), dq, dkv[:, :, 0], dkv[:, :, 1])
         return dq, dkv, None, None, None, None, None, None
 
 

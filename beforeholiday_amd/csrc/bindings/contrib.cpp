@@ -226,13 +226,14 @@ void attn_check(const at::Tensor& t, const char* name) {
 
 bh::AttnArgs attn_args(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, int mask_mode,
                        const c10::optional<at::Tensor>& mask, int64_t heads, double scale, double p, bool training,
-                       int64_t seed, at::Tensor& mask_keep) {
+                       int64_t seed, at::Tensor& mask_keep, bool flash = false) {
   attn_check(q, "q");
   attn_check(k, "k");
   attn_check(v, "v");
   TORCH_CHECK(q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type(), "attn: dtype mismatch");
   TORCH_CHECK(k.size(0) == v.size(0) && q.size(1) == k.size(1) && q.size(1) == v.size(1), "attn: shape mismatch");
-  TORCH_CHECK(k.size(0) <= bh::attn_max_sk(), "attn: sk > ", bh::attn_max_sk());
+  TORCH_CHECK(flash || k.size(0) <= bh::attn_max_sk(), "attn: sk > ", bh::attn_max_sk());
+  TORCH_CHECK(flash || (mask_mode >= 0 && mask_mode <= 3), "attn: short kernels take mask modes 0-3");
   bh::AttnArgs a;
   a.q = q.data_ptr(); a.k = k.data_ptr(); a.v = v.data_ptr();
   a.q_st = q.stride(0); a.q_sbh = q.stride(1);
@@ -241,10 +242,13 @@ bh::AttnArgs attn_args(const at::Tensor& q, const at::Tensor& k, const at::Tenso
   a.sq = (int)q.size(0); a.sk = (int)k.size(0); a.BH = (int)q.size(1); a.heads = (int)heads;
   a.mask_mode = mask_mode;
   if (mask_mode != 0) {
-    TORCH_CHECK(mask.has_value() && mask->defined(), "attn: mask_mode needs a mask");
+    TORCH_CHECK(mask_mode == 5 || (mask.has_value() && mask->defined()), "attn: mask_mode needs a mask");
+  }
+  if (mask_mode != 0 && mask_mode != 5) {
     if (mask_mode == 2) mask_keep = mask->to(at::kFloat).contiguous();
     else mask_keep = mask->to(at::kByte).contiguous();
-    const int64_t want = mask_mode == 3 ? (int64_t)a.sq * a.sk : (int64_t)(a.BH / a.heads) * a.sk;
+    const int64_t B = a.BH / a.heads;
+    const int64_t want = mask_mode == 3 ? (int64_t)a.sq * a.sk : mask_mode == 4 ? B * a.sq * a.sk : B * a.sk;
     TORCH_CHECK(mask_keep.numel() == want, "attn: mask has ", mask_keep.numel(), " elements, expected ", want);
     a.mask = mask_keep.data_ptr();
   }
@@ -285,6 +289,45 @@ void attn_bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, int mas
 
 void register_contrib_impl(pybind11::module_& root);
 
+std::vector<at::Tensor> flash_fwd(at::Tensor q, at::Tensor k, at::Tensor v, int mask_mode,
+                                  c10::optional<at::Tensor> mask, int64_t heads, double scale, double p, bool training,
+                                  int64_t seed, double mask_fill) {
+  at::Tensor mk;
+  auto a = attn_args(q, k, v, mask_mode, mask, heads, scale, p, training, seed, mk, /*flash=*/true);
+  a.mask_fill = (float)mask_fill;
+  auto o = at::empty({q.size(0), q.size(1), 64}, q.options());
+  auto lse = at::empty({q.size(1), q.size(0)}, q.options().dtype(at::kFloat));
+  a.o = o.data_ptr(); a.o_st = o.stride(0); a.o_sbh = o.stride(1);
+  a.lse = lse.data_ptr<float>();
+  bh::flash_forward(dtype_code(q.scalar_type()), a, stream_for(q));
+  return {o, lse};
+}
+
+void flash_bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse, int mask_mode,
+               c10::optional<at::Tensor> mask, int64_t heads, double scale, double p, bool training, int64_t seed,
+               double mask_fill, at::Tensor dq, at::Tensor dk, at::Tensor dv) {
+  at::Tensor mk;
+  auto a = attn_args(q, k, v, mask_mode, mask, heads, scale, p, training, seed, mk, /*flash=*/true);
+  a.mask_fill = (float)mask_fill;
+  attn_check(dout, "dout");
+  attn_check(o, "o");
+  attn_check(dq, "dq");
+  attn_check(dk, "dk");
+  attn_check(dv, "dv");
+  TORCH_CHECK(lse.is_contiguous() && lse.numel() == (int64_t)a.BH * a.sq, "flash_bwd: lse must be [BH, sq]");
+  a.o = o.data_ptr(); a.o_st = o.stride(0); a.o_sbh = o.stride(1);
+  a.dout = dout.data_ptr(); a.do_st = dout.stride(0); a.do_sbh = dout.stride(1);
+  a.dq = dq.data_ptr(); a.dq_st = dq.stride(0); a.dq_sbh = dq.stride(1);
+  a.dk = dk.data_ptr(); a.dk_st = dk.stride(0); a.dk_sbh = dk.stride(1);
+  a.dv = dv.data_ptr(); a.dv_st = dv.stride(0); a.dv_sbh = dv.stride(1);
+  auto delta = at::empty_like(lse);
+  a.lse = lse.data_ptr<float>();
+  const int dt = dtype_code(q.scalar_type());
+  bh::flash_delta(dt, a, delta.data_ptr<float>(), stream_for(q));
+  a.delta = delta.data_ptr<float>();
+  bh::flash_backward(dt, a, stream_for(q));
+}
+
 }  // namespace
 
 void register_contrib(pybind11::module_& root) {
@@ -293,6 +336,8 @@ void register_contrib(pybind11::module_& root) {
   fa.def("forward", &attn_fwd);
   fa.def("backward", &attn_bwd);
   fa.def("max_sk", &bh::attn_max_sk);
+  fa.def("flash_forward", &flash_fwd, "any-length attention forward -> (o, lse)");
+  fa.def("flash_backward", &flash_bwd, "any-length attention backward into dq / dk / dv");
 }
 
 namespace {

@@ -1,10 +1,16 @@
-// Fused short-sequence attention (kernels/attn.hip): head_dim 64, sk <= 128, fp16 / bf16.
+// Fused attention (kernels/attn.hip), head_dim 64, fp16 / bf16:
+//  * attn_forward / attn_backward: short sequences (sk <= 128), whole key row in registers.
+//  * flash_forward / flash_backward: any length, 64-key blocks with online softmax; forward also
+//    writes the per-row log-sum-exp (fp32 [BH, sq]) that backward uses to rebuild P, and backward
+//    takes delta = rowsum(dO * O) (fp32 [BH, sq], flash_delta) and runs a dK/dV kernel (one
+//    workgroup per key block) plus a dQ kernel (one per query block): no atomics, deterministic.
 // Tensors are addressed as base + t * st + bh * sbh + d (t = time index, bh = batch*heads index,
 // d < 64 contiguous), so q / k / v can be strided views into a fused QKV projection output and the
 // gradients can be written straight into the fused QKV gradient.
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdint.h>
 
 namespace bh {
@@ -16,7 +22,10 @@ struct AttnArgs {
   void* o = nullptr;
   int64_t q_st = 0, q_sbh = 0, k_st = 0, k_sbh = 0, v_st = 0, v_sbh = 0, o_st = 0, o_sbh = 0;
   int sq = 0, sk = 0, heads = 1, BH = 0;
-  int mask_mode = 0;            // 0 none, 1 key padding uint8 [B, sk], 2 additive fp32 [B, sk], 3 time uint8 [sq, sk]
+  // 0 none, 1 key padding uint8 [B, sk], 2 additive fp32 [B, sk], 3 time uint8 [sq, sk],
+  // 4 full uint8 [B, sq, sk] (broadcast over heads), 5 causal (key > query masked, no tensor)
+  int mask_mode = 0;
+  float mask_fill = -INFINITY;  // value of a masked score (-inf: MHA semantics; -10000: Megatron)
   const void* mask = nullptr;
   float scale = 1.f, p_drop = 0.f;
   bool training = false;
@@ -28,10 +37,17 @@ struct AttnArgs {
   void* dk = nullptr;
   void* dv = nullptr;
   int64_t dq_st = 0, dq_sbh = 0, dk_st = 0, dk_sbh = 0, dv_st = 0, dv_sbh = 0;
+  // flash
+  float* lse = nullptr;          // [BH, sq]
+  const float* delta = nullptr;  // [BH, sq]
 };
 
 int attn_max_sk();
 void attn_forward(int dt, const AttnArgs& a, hipStream_t st);
 void attn_backward(int dt, const AttnArgs& a, hipStream_t st);
+void flash_forward(int dt, const AttnArgs& a, hipStream_t st);          // needs a.lse
+// delta[bh, q] = sum_d dout * o  (o given in a.o / a.o_st / a.o_sbh, dout in a.dout)
+void flash_delta(int dt, const AttnArgs& a, float* delta, hipStream_t st);
+void flash_backward(int dt, const AttnArgs& a, hipStream_t st);         // needs a.lse, a.delta
 
 }  // namespace bh

@@ -107,12 +107,28 @@ BH_DEVICE float wsum16(float v) {
 
 // masked, scaled score of (query row q, key col k); -inf when masked / out of range
 BH_DEVICE float apply_mask(float s, const AttnArgs& a, int b, int q, int k) {
-  if (k >= a.sk) return -INFINITY;
+  if (k >= a.sk) return -INFINITY;  // padding columns of the last key block never count
+  const uint8_t* m8 = reinterpret_cast<const uint8_t*>(a.mask);
   switch (a.mask_mode) {
-    case 1: return reinterpret_cast<const uint8_t*>(a.mask)[(int64_t)b * a.sk + k] ? -INFINITY : s;
+    case 1: return m8[(int64_t)b * a.sk + k] ? a.mask_fill : s;
     case 2: return s + reinterpret_cast<const float*>(a.mask)[(int64_t)b * a.sk + k];
-    case 3: return (q < a.sq && reinterpret_cast<const uint8_t*>(a.mask)[(int64_t)q * a.sk + k]) ? -INFINITY : s;
+    case 3: return (q < a.sq && m8[(int64_t)q * a.sk + k]) ? a.mask_fill : s;
+    case 4: return (q < a.sq && m8[((int64_t)b * a.sq + q) * a.sk + k]) ? a.mask_fill : s;
+    case 5: return k > q ? a.mask_fill : s;
     default: return s;
+  }
+}
+
+// true when the mask REPLACES the score (fill value; blocks the gradient like masked_fill)
+BH_DEVICE bool is_masked(const AttnArgs& a, int b, int q, int k) {
+  if (k >= a.sk) return true;
+  const uint8_t* m8 = reinterpret_cast<const uint8_t*>(a.mask);
+  switch (a.mask_mode) {
+    case 1: return m8[(int64_t)b * a.sk + k] != 0;
+    case 3: return q < a.sq && m8[(int64_t)q * a.sk + k] != 0;
+    case 4: return q < a.sq && m8[((int64_t)b * a.sq + q) * a.sk + k] != 0;
+    case 5: return k > q;
+    default: return false;
   }
 }
 
@@ -372,6 +388,485 @@ __global__ __launch_bounds__(kThreads) void k_attn_bwd(AttnArgs a) {
     }
 }
 
+// =============================================================================================
+// Flash kernels: 64-key blocks, online softmax (forward), LSE-rebuilt probabilities (backward).
+// Dropout keep flags use the same Philox mapping as the short kernels with skt = round_up(sk, 64).
+// Every streamed 64-row operand block is prefetched into registers while the previous block is
+// being computed and written to the other of two LDS buffers afterwards (one barrier per block);
+// mask data for the block (key flags / additive row / [64 q x 64 k] byte tile) rides along, so the
+// inner loop never issues a global load.
+// =============================================================================================
+constexpr int kKB = 64;  // keys per block
+
+BH_DEVICE int skt_pad(int sk) { return (sk + kKB - 1) / kKB * kKB; }
+
+// 64 rows x 128 B of a head operand: 2 x 16-byte chunks per thread
+struct RowRegs {
+  i4v v[2];
+};
+template <typename T>
+BH_DEVICE void rows_load(RowRegs& r, const T* src, int64_t st, int valid, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = tid + i * kThreads, row = idx >> 3, ch = idx & 7;
+    r.v[i] = i4v{0, 0, 0, 0};
+    if (row < valid) r.v[i] = *reinterpret_cast<const i4v*>(src + (int64_t)row * st + ch * 8);
+  }
+}
+BH_DEVICE void rows_store(char* img, const RowRegs& r, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = tid + i * kThreads;
+    *reinterpret_cast<i4v*>(img + img_off(idx >> 3, idx & 7, 128)) = r.v[i];
+  }
+}
+
+// mask data of one (64 q rows) x (64 keys) block, staged in LDS: 4 KiB byte tile for modes 3 / 4,
+// 64 key flags (mode 1) or 64 additive floats (mode 2)
+constexpr int kMaskBytes = 64 * 64;
+struct MaskRegs {
+  int4 t;  // one 16-byte piece per thread (tile row = tid/4, cols 16*(tid%4)) or the key vector
+};
+BH_DEVICE void mask_load(MaskRegs& m, const AttnArgs& a, int b, int q0, int k0, int tid) {
+  // one 16-byte vector load per thread when the piece is in bounds and aligned (every piece but the
+  // key tail when sk % 16 == 0); the byte-wise tail path is taken by whole pieces, never per byte
+  // inside a vector load (a per-element select there makes hipcc wait on every load).
+  m.t = make_int4(0, 0, 0, 0);
+  const uint8_t* m8 = reinterpret_cast<const uint8_t*>(a.mask);
+  const bool aligned = (a.sk & 15) == 0;
+  if (a.mask_mode == 3 || a.mask_mode == 4) {
+    const int r = tid >> 2, c = (tid & 3) * 16, q = q0 + r;
+    if (q < a.sq) {
+      const uint8_t* src = (a.mask_mode == 3 ? m8 + (int64_t)q * a.sk : m8 + ((int64_t)b * a.sq + q) * a.sk) + k0 + c;
+      if (aligned && k0 + c + 16 <= a.sk) {
+        m.t = *reinterpret_cast<const int4*>(src);
+      } else {
+        uint8_t buf[16];
+        for (int i = 0; i < 16; ++i) buf[i] = (k0 + c + i < a.sk) ? src[i] : 1;
+        m.t = *reinterpret_cast<const int4*>(buf);
+      }
+    }
+  } else if (a.mask_mode == 1 && tid < 4) {
+    const uint8_t* src = m8 + (int64_t)b * a.sk + k0 + tid * 16;
+    if (aligned && k0 + tid * 16 + 16 <= a.sk) {
+      m.t = *reinterpret_cast<const int4*>(src);
+    } else {
+      uint8_t buf[16];
+      for (int i = 0; i < 16; ++i) buf[i] = (k0 + tid * 16 + i < a.sk) ? src[i] : 1;
+      m.t = *reinterpret_cast<const int4*>(buf);
+    }
+  } else if (a.mask_mode == 2 && tid < 16) {
+    const float* src = reinterpret_cast<const float*>(a.mask) + (int64_t)b * a.sk + k0 + tid * 4;
+    if ((a.sk & 3) == 0 && k0 + tid * 4 + 4 <= a.sk) {
+      m.t = *reinterpret_cast<const int4*>(src);
+    } else {
+      float buf[4];
+      for (int i = 0; i < 4; ++i) buf[i] = (k0 + tid * 4 + i < a.sk) ? src[i] : 0.f;
+      m.t = *reinterpret_cast<const int4*>(buf);
+    }
+  }
+}
+BH_DEVICE void mask_store(char* img, const MaskRegs& m, const AttnArgs& a, int tid) {
+  if (a.mask_mode == 3 || a.mask_mode == 4) *reinterpret_cast<int4*>(img + tid * 16) = m.t;
+  else if ((a.mask_mode == 1 && tid < 4) || (a.mask_mode == 2 && tid < 16)) *reinterpret_cast<int4*>(img + tid * 16) = m.t;
+}
+// (masked?, score) for local query row ql (0..63 of the block), local key kl, global q / k
+BH_DEVICE float mask_apply(float s, const AttnArgs& a, const char* mimg, int ql, int kl, int q, int k, bool& masked) {
+  masked = false;
+  if (k >= a.sk) {
+    masked = true;
+    return -INFINITY;
+  }
+  switch (a.mask_mode) {
+    case 1: masked = mimg[kl] != 0; break;
+    case 2: return s + reinterpret_cast<const float*>(mimg)[kl];
+    case 3:
+    case 4: masked = mimg[ql * 64 + kl] != 0; break;
+    case 5: masked = k > q; break;
+    default: break;
+  }
+  return masked ? a.mask_fill : s;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void k_flash_fwd(AttnArgs a) {
+  constexpr int PRB = kKB * 2;
+  constexpr int kBuf = 2 * kKB * 128 + kMaskBytes;  // K, V, mask of one block
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + kQB * PRB];
+  char* pimg = smem + 2 * kBuf;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int bh = blockIdx.y, b = bh / a.heads;
+  const int q0 = blockIdx.x * kQB;
+  const int qbase = q0 + wave * 16;
+  const int skt = skt_pad(a.sk);
+
+  const T* K = reinterpret_cast<const T*>(a.k) + (int64_t)bh * a.k_sbh;
+  const T* V = reinterpret_cast<const T*>(a.v) + (int64_t)bh * a.v_sbh;
+  const T* Q = reinterpret_cast<const T*>(a.q) + (int64_t)bh * a.q_sbh;
+  i4v qa[2];
+  {
+    const int qr = min(qbase + fr, a.sq - 1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) qa[s] = *reinterpret_cast<const i4v*>(Q + (int64_t)qr * a.q_st + 32 * s + 8 * fq);
+  }
+  const bool drop = a.training && a.p_drop > 0.f;
+  const float kscale = a.p_drop < 1.f ? 1.f / (1.f - a.p_drop) : 0.f;
+  float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY}, l[4] = {0.f, 0.f, 0.f, 0.f};
+  f4v O[4];
+#pragma unroll
+  for (int dn = 0; dn < 4; ++dn) O[dn] = f4v{0.f, 0.f, 0.f, 0.f};
+  // causal: key blocks past this workgroup's last query row contribute nothing
+  const int kend = a.mask_mode == 5 ? min(a.sk, q0 + kQB) : a.sk;
+  const int nb = (kend + kKB - 1) / kKB;
+
+  RowRegs rk, rv;
+  MaskRegs rm;
+  rows_load<T>(rk, K, a.k_st, min(kKB, a.sk), tid);
+  rows_load<T>(rv, V, a.v_st, min(kKB, a.sk), tid);
+  mask_load(rm, a, b, q0, 0, tid);
+  rows_store(smem, rk, tid);
+  rows_store(smem + kKB * 128, rv, tid);
+  mask_store(smem + 2 * kKB * 128, rm, a, tid);
+  __syncthreads();
+  for (int ib = 0; ib < nb; ++ib) {
+    const int kb = ib * kKB;
+    char* kimg = smem + (ib & 1) * kBuf;
+    char* vimg = kimg + kKB * 128;
+    const char* mimg = vimg + kKB * 128;
+    if (ib + 1 < nb) {  // prefetch the next block while this one is computed
+      const int kn = kb + kKB;
+      rows_load<T>(rk, K + (int64_t)kn * a.k_st, a.k_st, min(kKB, a.sk - kn), tid);
+      rows_load<T>(rv, V + (int64_t)kn * a.v_st, a.v_st, min(kKB, a.sk - kn), tid);
+      mask_load(rm, a, b, q0, kn, tid);
+    }
+    f4v S[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      S[n] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) S[n] = Mfma<T>::run(qa[s], frag_row(kimg, 128, 16 * n, 32 * s, lane), S[n]);
+    }
+    float mb[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bool mk;
+        const int ql = wave * 16 + 4 * fq + j, kl = 16 * n + fr;
+        const float v = mask_apply(S[n][j] * a.scale, a, mimg, ql, kl, q0 + ql, kb + kl, mk);
+        S[n][j] = v;
+        mb[j] = fmaxf(mb[j], v);
+      }
+    float corr[4], ls[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float mn = fmaxf(m[j], wmax16(mb[j]));
+      corr[j] = (m[j] == -INFINITY) ? 0.f : __expf(m[j] - mn);
+      m[j] = mn;
+      ls[j] = 0.f;
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      float4 kp = make_float4(1.f, 1.f, 1.f, 1.f);
+      if (drop) kp = keep4(a, bh, qbase + 4 * fq, kb + 16 * n + fr, skt);
+      const float kk[4] = {kp.x * kscale, kp.y * kscale, kp.z * kscale, kp.w * kscale};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float p = m[j] == -INFINITY ? 0.f : __expf(S[n][j] - m[j]);
+        ls[j] += p;
+        const float pd = drop ? p * kk[j] : p;
+        *reinterpret_cast<T*>(pimg + img_elem(wave * 16 + 4 * fq + j, 16 * n + fr, PRB)) = from_f<T>(pd);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) l[j] = l[j] * corr[j] + wsum16(ls[j]);
+#pragma unroll
+    for (int dn = 0; dn < 4; ++dn)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) O[dn][j] *= corr[j];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's P rows are written (wave-private)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const i4v pa = frag_row(pimg, PRB, wave * 16, 32 * ks, lane);
+#pragma unroll
+      for (int dn = 0; dn < 4; ++dn) O[dn] = Mfma<T>::run(pa, frag_tr(vimg, 128, 32 * ks, 16 * dn, lane), O[dn]);
+    }
+    if (ib + 1 < nb) {
+      char* nk = smem + ((ib + 1) & 1) * kBuf;
+      rows_store(nk, rk, tid);
+      rows_store(nk + kKB * 128, rv, tid);
+      mask_store(nk + 2 * kKB * 128, rm, a, tid);
+    }
+    __syncthreads();  // next buffer complete; this buffer free for the block after next
+  }
+  T* Out = reinterpret_cast<T*>(a.o) + (int64_t)bh * a.o_sbh;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = qbase + 4 * fq + j;
+    const float inv = l[j] > 0.f ? 1.f / l[j] : 0.f;
+    if (q < a.sq) {
+#pragma unroll
+      for (int dn = 0; dn < 4; ++dn) Out[(int64_t)q * a.o_st + 16 * dn + fr] = from_f<T>(O[dn][j] * inv);
+      if (fr == 0) a.lse[(int64_t)bh * a.sq + q] = l[j] > 0.f ? m[j] + __logf(l[j]) : INFINITY;
+    }
+  }
+}
+
+// delta[bh, q] = sum_d dO[q, bh, d] * O[q, bh, d]; one 16-lane group per row
+template <typename T>
+__global__ __launch_bounds__(256) void k_flash_delta(AttnArgs a, float* __restrict__ delta) {
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / 16;  // row = bh * sq + q
+  const int sub = threadIdx.x & 15;
+  if (row >= (int64_t)a.BH * a.sq) return;
+  const int bh = (int)(row / a.sq), q = (int)(row % a.sq);
+  const T* o = reinterpret_cast<const T*>(a.o) + (int64_t)q * a.o_st + (int64_t)bh * a.o_sbh + sub * 4;
+  const T* d = reinterpret_cast<const T*>(a.dout) + (int64_t)q * a.do_st + (int64_t)bh * a.do_sbh + sub * 4;
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc += to_f<T>(o[i]) * to_f<T>(d[i]);
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1) acc += __shfl_xor(acc, off);
+  if (sub == 0) delta[row] = acc;
+}
+
+// P (dropped, via LSE) and dS for one wave's 16 query rows (local rows wave*16..) x one key block
+template <typename T>
+BH_DEVICE void flash_bwd_tile(const AttnArgs& a, int bh, int q0, int qbase, int kb, int skt, const i4v (&qa)[2],
+                              const i4v (&da)[2], const char* kimg, const char* vimg, const char* mimg,
+                              const float (&lse)[4], const float (&dl)[4], f4v (&P)[4], f4v (&dS)[4], int lane) {
+  const int fr = lane & 15, fq = lane >> 4;
+  const bool drop = a.training && a.p_drop > 0.f;
+  const float kscale = a.p_drop < 1.f ? 1.f / (1.f - a.p_drop) : 0.f;
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    f4v S = f4v{0.f, 0.f, 0.f, 0.f}, dP = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      S = Mfma<T>::run(qa[s], frag_row(kimg, 128, 16 * n, 32 * s, lane), S);
+      dP = Mfma<T>::run(da[s], frag_row(vimg, 128, 16 * n, 32 * s, lane), dP);
+    }
+    float4 kp = make_float4(1.f, 1.f, 1.f, 1.f);
+    if (drop) kp = keep4(a, bh, qbase + 4 * fq, kb + 16 * n + fr, skt);
+    const float kk[4] = {kp.x * kscale, kp.y * kscale, kp.z * kscale, kp.w * kscale};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = qbase + 4 * fq + j, kl = 16 * n + fr;
+      bool mk;
+      const float v = mask_apply(S[j] * a.scale, a, mimg, q - q0, kl, q, kb + kl, mk);
+      const float p = (q < a.sq && v != -INFINITY && lse[j] != INFINITY) ? __expf(v - lse[j]) : 0.f;
+      const float dpd = drop ? dP[j] * kk[j] : dP[j];
+      P[n][j] = drop ? p * kk[j] : p;  // dropped probability (dV operand)
+      // a masked score is a constant: no gradient flows to Q / K through it (matters for fully
+      // masked rows under a finite fill, where p is uniform rather than 0)
+      dS[n][j] = mk ? 0.f : p * (dpd - dl[j]) * a.scale;
+    }
+  }
+}
+
+// dQ: one workgroup per (64-row query block, head); streams key blocks (double-buffered)
+template <typename T>
+__global__ __launch_bounds__(kThreads) void k_flash_bwd_dq(AttnArgs a) {
+  constexpr int PRB = kKB * 2;
+  constexpr int kBuf = 2 * kKB * 128 + kMaskBytes;
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + kQB * PRB];
+  char* dsimg = smem + 2 * kBuf;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int bh = blockIdx.y, b = bh / a.heads;
+  const int q0 = blockIdx.x * kQB;
+  const int qbase = q0 + wave * 16;
+  const int skt = skt_pad(a.sk);
+  const T* K = reinterpret_cast<const T*>(a.k) + (int64_t)bh * a.k_sbh;
+  const T* V = reinterpret_cast<const T*>(a.v) + (int64_t)bh * a.v_sbh;
+  const T* Q = reinterpret_cast<const T*>(a.q) + (int64_t)bh * a.q_sbh;
+  const T* dO = reinterpret_cast<const T*>(a.dout) + (int64_t)bh * a.do_sbh;
+  i4v qa[2], da[2];
+  {
+    const int qr = min(qbase + fr, a.sq - 1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      qa[s] = *reinterpret_cast<const i4v*>(Q + (int64_t)qr * a.q_st + 32 * s + 8 * fq);
+      da[s] = *reinterpret_cast<const i4v*>(dO + (int64_t)qr * a.do_st + 32 * s + 8 * fq);
+    }
+  }
+  float lse[4], dl[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = min(qbase + 4 * fq + j, a.sq - 1);
+    lse[j] = a.lse[(int64_t)bh * a.sq + q];
+    dl[j] = a.delta[(int64_t)bh * a.sq + q];
+  }
+  f4v acc[4];
+#pragma unroll
+  for (int dn = 0; dn < 4; ++dn) acc[dn] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int kend = a.mask_mode == 5 ? min(a.sk, q0 + kQB) : a.sk;
+  const int nb = (kend + kKB - 1) / kKB;
+  RowRegs rk, rv;
+  MaskRegs rm;
+  rows_load<T>(rk, K, a.k_st, min(kKB, a.sk), tid);
+  rows_load<T>(rv, V, a.v_st, min(kKB, a.sk), tid);
+  mask_load(rm, a, b, q0, 0, tid);
+  rows_store(smem, rk, tid);
+  rows_store(smem + kKB * 128, rv, tid);
+  mask_store(smem + 2 * kKB * 128, rm, a, tid);
+  __syncthreads();
+  for (int ib = 0; ib < nb; ++ib) {
+    const int kb = ib * kKB;
+    char* kimg = smem + (ib & 1) * kBuf;
+    char* vimg = kimg + kKB * 128;
+    const char* mimg = vimg + kKB * 128;
+    if (ib + 1 < nb) {
+      const int kn = kb + kKB;
+      rows_load<T>(rk, K + (int64_t)kn * a.k_st, a.k_st, min(kKB, a.sk - kn), tid);
+      rows_load<T>(rv, V + (int64_t)kn * a.v_st, a.v_st, min(kKB, a.sk - kn), tid);
+      mask_load(rm, a, b, q0, kn, tid);
+    }
+    f4v P[4], dS[4];
+    flash_bwd_tile<T>(a, bh, q0, qbase, kb, skt, qa, da, kimg, vimg, mimg, lse, dl, P, dS, lane);
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<T*>(dsimg + img_elem(wave * 16 + 4 * fq + j, 16 * n + fr, PRB)) = from_f<T>(dS[n][j]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const i4v dsa = frag_row(dsimg, PRB, wave * 16, 32 * ks, lane);
+#pragma unroll
+      for (int dn = 0; dn < 4; ++dn) acc[dn] = Mfma<T>::run(dsa, frag_tr(kimg, 128, 32 * ks, 16 * dn, lane), acc[dn]);
+    }
+    if (ib + 1 < nb) {
+      char* nk = smem + ((ib + 1) & 1) * kBuf;
+      rows_store(nk, rk, tid);
+      rows_store(nk + kKB * 128, rv, tid);
+      mask_store(nk + 2 * kKB * 128, rm, a, tid);
+    }
+    __syncthreads();
+  }
+  T* dQ = reinterpret_cast<T*>(a.dq) + (int64_t)bh * a.dq_sbh;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = qbase + 4 * fq + j;
+    if (q < a.sq) {
+#pragma unroll
+      for (int dn = 0; dn < 4; ++dn) dQ[(int64_t)q * a.dq_st + 16 * dn + fr] = from_f<T>(acc[dn][j]);
+    }
+  }
+}
+
+// dK, dV: one workgroup per (64-key block, head); streams query blocks (double-buffered Q / dO /
+// mask), keeps dK / dV of its keys in registers (wave w owns keys 16w..16w+15 of the block)
+template <typename T>
+__global__ __launch_bounds__(kThreads) void k_flash_bwd_dkdv(AttnArgs a) {
+  constexpr int PRB = kKB * 2;
+  constexpr int kBuf = 2 * kQB * 128 + kMaskBytes;  // Q, dO, mask of one query block
+  __shared__ __attribute__((aligned(16))) char smem[2 * kKB * 128 + 2 * kBuf + 2 * kQB * PRB];
+  char* kimg = smem;
+  char* vimg = kimg + kKB * 128;
+  char* bufs = vimg + kKB * 128;
+  char* pdimg = bufs + 2 * kBuf;
+  char* dsimg = pdimg + kQB * PRB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int bh = blockIdx.y, b = bh / a.heads;
+  const int kb = blockIdx.x * kKB;
+  const int skt = skt_pad(a.sk);
+  const T* K = reinterpret_cast<const T*>(a.k) + (int64_t)bh * a.k_sbh;
+  const T* V = reinterpret_cast<const T*>(a.v) + (int64_t)bh * a.v_sbh;
+  const T* Q = reinterpret_cast<const T*>(a.q) + (int64_t)bh * a.q_sbh;
+  const T* dO = reinterpret_cast<const T*>(a.dout) + (int64_t)bh * a.do_sbh;
+  {
+    RowRegs r;
+    rows_load<T>(r, K + (int64_t)kb * a.k_st, a.k_st, min(kKB, a.sk - kb), tid);
+    rows_store(kimg, r, tid);
+    rows_load<T>(r, V + (int64_t)kb * a.v_st, a.v_st, min(kKB, a.sk - kb), tid);
+    rows_store(vimg, r, tid);
+  }
+  f4v dK[4], dV[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) dK[n] = dV[n] = f4v{0.f, 0.f, 0.f, 0.f};
+  // causal: query blocks entirely above this key block see none of its keys
+  const int qstart = a.mask_mode == 5 ? (kb / kQB) * kQB : 0;
+  const int nqb = (a.sq - qstart + kQB - 1) / kQB;
+  RowRegs rq, rd;
+  MaskRegs rm;
+  rows_load<T>(rq, Q + (int64_t)qstart * a.q_st, a.q_st, min(kQB, a.sq - qstart), tid);
+  rows_load<T>(rd, dO + (int64_t)qstart * a.do_st, a.do_st, min(kQB, a.sq - qstart), tid);
+  mask_load(rm, a, b, qstart, kb, tid);
+  rows_store(bufs, rq, tid);
+  rows_store(bufs + kQB * 128, rd, tid);
+  mask_store(bufs + 2 * kQB * 128, rm, a, tid);
+  __syncthreads();
+  for (int iq = 0; iq < nqb; ++iq) {
+    const int q0 = qstart + iq * kQB;
+    char* qimg = bufs + (iq & 1) * kBuf;
+    char* doimg = qimg + kQB * 128;
+    const char* mimg = doimg + kQB * 128;
+    if (iq + 1 < nqb) {
+      const int qn = q0 + kQB;
+      rows_load<T>(rq, Q + (int64_t)qn * a.q_st, a.q_st, min(kQB, a.sq - qn), tid);
+      rows_load<T>(rd, dO + (int64_t)qn * a.do_st, a.do_st, min(kQB, a.sq - qn), tid);
+      mask_load(rm, a, b, qn, kb, tid);
+    }
+    const int qbase = q0 + wave * 16;
+    i4v qa[2], da[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      qa[s] = frag_row(qimg, 128, wave * 16, 32 * s, lane);
+      da[s] = frag_row(doimg, 128, wave * 16, 32 * s, lane);
+    }
+    float lse[4], dl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = min(qbase + 4 * fq + j, a.sq - 1);
+      lse[j] = a.lse[(int64_t)bh * a.sq + q];
+      dl[j] = a.delta[(int64_t)bh * a.sq + q];
+    }
+    f4v P[4], dS[4];
+    flash_bwd_tile<T>(a, bh, q0, qbase, kb, skt, qa, da, kimg, vimg, mimg, lse, dl, P, dS, lane);
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = wave * 16 + 4 * fq + j;
+        *reinterpret_cast<T*>(pdimg + img_elem(row, 16 * n + fr, PRB)) = from_f<T>(P[n][j]);
+        *reinterpret_cast<T*>(dsimg + img_elem(row, 16 * n + fr, PRB)) = from_f<T>(dS[n][j]);
+      }
+    __syncthreads();  // Pd / dS images of all 64 query rows complete
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const i4v pa = frag_tr(pdimg, PRB, 32 * ks, wave * 16, lane);
+      const i4v sa = frag_tr(dsimg, PRB, 32 * ks, wave * 16, lane);
+#pragma unroll
+      for (int dn = 0; dn < 4; ++dn) {
+        dV[dn] = Mfma<T>::run(pa, frag_tr(doimg, 128, 32 * ks, 16 * dn, lane), dV[dn]);
+        dK[dn] = Mfma<T>::run(sa, frag_tr(qimg, 128, 32 * ks, 16 * dn, lane), dK[dn]);
+      }
+    }
+    if (iq + 1 < nqb) {
+      char* nb_ = bufs + ((iq + 1) & 1) * kBuf;
+      rows_store(nb_, rq, tid);
+      rows_store(nb_ + kQB * 128, rd, tid);
+      mask_store(nb_ + 2 * kQB * 128, rm, a, tid);
+    }
+    __syncthreads();  // next buffer complete; Pd / dS images free
+  }
+  T* dKp = reinterpret_cast<T*>(a.dk) + (int64_t)bh * a.dk_sbh;
+  T* dVp = reinterpret_cast<T*>(a.dv) + (int64_t)bh * a.dv_sbh;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int key = kb + wave * 16 + 4 * fq + j;
+    if (key < a.sk) {
+#pragma unroll
+      for (int dn = 0; dn < 4; ++dn) {
+        dKp[(int64_t)key * a.dk_st + 16 * dn + fr] = from_f<T>(dK[dn][j]);
+        dVp[(int64_t)key * a.dv_st + 16 * dn + fr] = from_f<T>(dV[dn][j]);
+      }
+    }
+  }
+}
+
 inline void check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
@@ -411,6 +906,46 @@ void attn_backward(int dt, const AttnArgs& a, hipStream_t st) {
   }
 #undef BH_ATTN_BWD
   check_launch("attn_backward");
+}
+
+void flash_forward(int dt, const AttnArgs& a, hipStream_t st) {
+  if (a.sk < 1 || a.sq < 1 || !a.lse) throw std::runtime_error("flash_forward: bad shape or missing lse");
+  const dim3 grid((unsigned)((a.sq + kQB - 1) / kQB), (unsigned)a.BH);
+  switch (dt) {
+    case kF16: hipLaunchKernelGGL((k_flash_fwd<f16>), grid, dim3(kThreads), 0, st, a); break;
+    case kBF16: hipLaunchKernelGGL((k_flash_fwd<bf16>), grid, dim3(kThreads), 0, st, a); break;
+    default: throw std::runtime_error("flash_forward: fp16 / bf16 only");
+  }
+  check_launch("flash_forward");
+}
+
+void flash_delta(int dt, const AttnArgs& a, float* delta, hipStream_t st) {
+  const int64_t rows = (int64_t)a.BH * a.sq;
+  const dim3 grid((unsigned)((rows * 16 + 255) / 256));
+  switch (dt) {
+    case kF16: hipLaunchKernelGGL((k_flash_delta<f16>), grid, dim3(256), 0, st, a, delta); break;
+    case kBF16: hipLaunchKernelGGL((k_flash_delta<bf16>), grid, dim3(256), 0, st, a, delta); break;
+    default: throw std::runtime_error("flash_delta: fp16 / bf16 only");
+  }
+  check_launch("flash_delta");
+}
+
+void flash_backward(int dt, const AttnArgs& a, hipStream_t st) {
+  if (a.sk < 1 || a.sq < 1 || !a.lse || !a.delta) throw std::runtime_error("flash_backward: bad args");
+  const dim3 gq((unsigned)((a.sq + kQB - 1) / kQB), (unsigned)a.BH);
+  const dim3 gk((unsigned)((a.sk + kKB - 1) / kKB), (unsigned)a.BH);
+  switch (dt) {
+    case kF16:
+      hipLaunchKernelGGL((k_flash_bwd_dkdv<f16>), gk, dim3(kThreads), 0, st, a);
+      hipLaunchKernelGGL((k_flash_bwd_dq<f16>), gq, dim3(kThreads), 0, st, a);
+      break;
+    case kBF16:
+      hipLaunchKernelGGL((k_flash_bwd_dkdv<bf16>), gk, dim3(kThreads), 0, st, a);
+      hipLaunchKernelGGL((k_flash_bwd_dq<bf16>), gq, dim3(kThreads), 0, st, a);
+      break;
+    default: throw std::runtime_error("flash_backward: fp16 / bf16 only");
+  }
+  check_launch("flash_backward");
 }
 
 }  // namespace bh

@@ -273,6 +273,35 @@ class CoreAttention(MegatronModule):
                                                         self.attention_softmax_in_fp32, coeff)
         self.attention_dropout = torch.nn.Dropout(config.attention_dropout)
 
+    def flash_ok(self, x, hn) -> bool:
+        """MFMA flash attention (kernels/attn.hip) for head size 64 on fp16 / bf16 GPU tensors."""
+        import os
+
+        return (x.is_cuda and x.dtype in (torch.float16, torch.bfloat16) and hn == 64
+                and os.environ.get("BH_FLASH_ATTN", "1") != "0")
+
+    def flash(self, qkv, attention_mask):
+        """qkv [sq, b*np, 3, 64] (the fused QKV projection output, viewed) -> context [sq, b, np*64].
+        Same math as forward(): scale 1/sqrt(hn) (the query-key layer-scaling coefficient cancels),
+        padding masks fill -10000 like attention_mask_func, causal masks are implicit, attention
+        dropout is Philox-regenerated in backward; d(qkv) comes back in the projection layout."""
+        from ..contrib.multihead_attn._core import MASK_CAUSAL, MASK_FULL, MASK_NONE, FusedSelfAttnFn
+
+        sq, bnp = qkv.shape[0], qkv.shape[1]
+        b = bnp // self.num_attention_heads_per_partition
+        if self.attn_mask_type == AttnMaskType.causal:
+            mode, mask, fill = MASK_CAUSAL, None, float("-inf")
+        elif attention_mask is not None:
+            mode, fill = MASK_FULL, -10000.0
+            mask = attention_mask.expand(b, 1, sq, sq).reshape(b, sq, sq)
+        else:
+            mode, mask, fill = MASK_NONE, None, float("-inf")
+        p = self.attention_dropout.p if self.training else 0.0
+        ctx = FusedSelfAttnFn.apply(qkv, self.num_attention_heads_per_partition,
+                                    1.0 / math.sqrt(self.hidden_size_per_attention_head), mask, mode, p,
+                                    self.training, fill)
+        return ctx.view(sq, b, self.hidden_size_per_partition)
+
     def forward(self, query, key, value, attention_mask):
         sq, b, np_, hn = query.shape
         sk = key.size(0)
@@ -324,6 +353,9 @@ class ParallelAttention(MegatronModule):
         np_, hn = self.num_attention_heads_per_partition, self.hidden_size_per_attention_head
         if self.attention_type == AttnType.self_attn:
             mixed, _ = self.query_key_value(hidden_states)
+            if self.core_attention.flash_ok(mixed, hn):
+                qkv = mixed.view(mixed.shape[0], mixed.shape[1] * np_, 3, hn)
+                return self.dense(self.core_attention.flash(qkv, attention_mask))
             mixed = mixed.view(*mixed.shape[:-1], np_, 3 * hn)
             q, k, v = tensor_parallel.split_tensor_along_last_dim(mixed, 3)
         else:

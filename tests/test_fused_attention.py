@@ -134,3 +134,96 @@ def test_self_mha_module_fused_matches_unfused(impl, mask, monkeypatch):
     torch.testing.assert_close(o1, o0, rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(g1, g0, rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(w1, w0, rtol=5e-2, atol=5e-2)
+
+
+# ------------------------------------------------------------------------------------------ flash
+def _reference_full(q, k, v, scale, mask_mode, mask, heads, fill, keep=None, p=0.0):
+    s = torch.einsum("qbd,kbd->bqk", q, k) * scale
+    BH, sq, sk = s.shape
+    B = BH // heads
+    if mask_mode == 1:
+        m = mask.view(B, 1, 1, sk).expand(B, heads, sq, sk)
+    elif mask_mode == 3:
+        m = mask.view(1, 1, sq, sk).expand(B, heads, sq, sk)
+    elif mask_mode == 4:
+        m = mask.view(B, 1, sq, sk).expand(B, heads, sq, sk)
+    elif mask_mode == 5:
+        m = torch.ones(sq, sk, device=q.device, dtype=torch.bool).triu(1).view(1, 1, sq, sk).expand(B, heads, sq, sk)
+    else:
+        m = None
+    s = s.view(B, heads, sq, sk)
+    if mask_mode == 2:
+        s = s + mask.view(B, 1, 1, sk).float()
+    elif m is not None:
+        s = s.masked_fill(m.bool(), fill)
+    pr = torch.softmax(s.view(BH, sq, sk), -1).nan_to_num(0.0)
+    if keep is not None:
+        pr = pr * keep / (1 - p)
+    return torch.einsum("bqk,kbd->qbd", pr, v)
+
+
+FLASH_SHAPES = [(512, 512), (200, 300), (64, 1000), (129, 129), (1, 77)]
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("shape", FLASH_SHAPES)
+@pytest.mark.parametrize("mask_mode", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("fill", [float("-inf"), -10000.0])
+def test_flash_forward_backward(dtype, shape, mask_mode, fill):
+    sq, sk = shape
+    if mask_mode in (3, 5) and sq != sk:
+        pytest.skip("time / causal masks are square")
+    if mask_mode == 2 and fill != float("-inf"):
+        pytest.skip("additive masks have no fill value")
+    B, heads = 2, 3
+    g = torch.Generator(device="cuda").manual_seed(sq * 7 + sk + mask_mode)
+    q = torch.randn(sq, B * heads, 3, 64, device="cuda", dtype=dtype, generator=g)[:, :, 0]
+    kv = torch.randn(sk, B * heads, 3, 64, device="cuda", dtype=dtype, generator=g)
+    k, v = kv[:, :, 1], kv[:, :, 2]
+    mask = None
+    if mask_mode == 1:
+        mask = torch.rand(B, sk, device="cuda", generator=g) < 0.3
+    elif mask_mode == 2:
+        mask = torch.randn(B, sk, device="cuda", generator=g)
+    elif mask_mode == 3:
+        mask = torch.rand(sq, sk, device="cuda", generator=g) < 0.2
+    elif mask_mode == 4:
+        mask = torch.rand(B, sq, sk, device="cuda", generator=g) < 0.25
+        mask[0, 0, :] = True  # one fully masked row: zeros (-inf) / uniform (-10000)
+    scale = 0.125
+    o, lse = _fa().flash_forward(q, k, v, mask_mode, mask, heads, scale, 0.0, True, 5, fill)
+    qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, v))
+    ref = _reference_full(qf, kf, vf, scale, mask_mode, mask, heads, fill)
+    tol = 2e-2 if dtype == torch.float16 else 5e-2
+    torch.testing.assert_close(o.float(), ref, rtol=tol, atol=tol)
+    dout = torch.randn_like(o)
+    ref.backward(dout.float())
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    _fa().flash_backward(dout, q, k, v, o, lse, mask_mode, mask, heads, scale, 0.0, True, 5, fill, dq, dk, dv)
+    for got, want in ((dq, qf.grad), (dk, kf.grad), (dv, vf.grad)):
+        torch.testing.assert_close(got.float(), want, rtol=tol, atol=tol * 2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_flash_dropout_regenerated(dtype):
+    sq, sk, B, heads, p = 200, 64, 2, 2, 0.2
+    BH = B * heads
+    g = torch.Generator(device="cuda").manual_seed(11)
+    q = torch.randn(sq, BH, 64, device="cuda", dtype=dtype, generator=g)
+    k = torch.randn(sk, BH, 64, device="cuda", dtype=dtype, generator=g)
+    eye = torch.eye(64, device="cuda", dtype=dtype).unsqueeze(1).expand(64, BH, 64).contiguous()
+    o, lse = _fa().flash_forward(q, k, eye, 0, None, heads, 0.125, p, True, 99, float("-inf"))
+    o2, _ = _fa().flash_forward(q, k, eye, 0, None, heads, 0.125, p, True, 99, float("-inf"))
+    assert torch.equal(o, o2)
+    keep = (o.float() != 0).permute(1, 0, 2).float()
+    assert abs(keep.mean().item() - (1 - p)) < 0.03
+    qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, eye))
+    ref = _reference_full(qf, kf, vf, 0.125, 0, None, heads, float("-inf"), keep=keep, p=p)
+    tol = 2e-2 if dtype == torch.float16 else 5e-2
+    torch.testing.assert_close(o.float(), ref, rtol=tol, atol=tol)
+    dout = torch.randn_like(o)
+    ref.backward(dout.float())
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(eye)
+    _fa().flash_backward(dout, q, k, eye, o, lse, 0, None, heads, 0.125, p, True, 99, float("-inf"), dq, dk, dv)
+    for got, want in ((dq, qf.grad), (dk, kf.grad), (dv, vf.grad)):
+        torch.testing.assert_close(got.float(), want, rtol=tol, atol=tol * 2)

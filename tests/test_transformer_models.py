@@ -246,3 +246,53 @@ def _gpt_fused_mlp(rank, world):
 def test_gpt_fused_mfma_mlp_matches_unfused():
     """ParallelMLP on the MFMA GEMM (bias+GELU epilogue, dGELU+bias-grad epilogue) == the unfused path."""
     run_distributed(_gpt_fused_mlp, 1)
+
+
+def _flash_vs_unfused(rank, world, kind):
+    import os
+    from beforeholiday_amd.models import BertModel, GPTModel
+    from beforeholiday_amd.transformer import parallel_state as ps
+    from beforeholiday_amd.transformer.pipeline_parallel.utils import get_ltor_masks_and_position_ids
+    ps.initialize_model_parallel(1, 1, default_backend="gloo")
+    _seed()
+    cfg = _cfg(params_dtype=torch.bfloat16, masked_softmax_fusion=True, hidden_size=256, num_attention_heads=4,
+               vocab_size=512, max_position_embeddings=256)
+    torch.manual_seed(3)
+    S = 200
+    tokens = torch.randint(0, 512, (2, S)).cuda()
+    labels = torch.randint(0, 512, (2, S)).cuda()
+    if kind == "gpt":
+        model = GPTModel(cfg).cuda()
+        mask, _, pos = get_ltor_masks_and_position_ids(tokens, -1, False, False, False)
+        run = lambda: model(tokens, pos, mask, labels=labels).float().mean()  # noqa: E731
+    else:
+        model = BertModel(cfg, num_tokentypes=2).cuda()
+        att = torch.ones(2, S, dtype=torch.long, device="cuda")
+        att[1, 150:] = 0  # padded tail: padding-mask path with the -10000 fill
+        types = torch.zeros(2, S, dtype=torch.long, device="cuda")
+
+        def run():
+            loss, binary = model(tokens, att, tokentype_ids=types, lm_labels=labels)
+            return loss.float().mean() + binary.float().sum() * 0.01
+    res = {}
+    for flash in ("1", "0"):
+        os.environ["BH_FLASH_ATTN"] = flash
+        model.zero_grad(set_to_none=True)
+        loss = run()
+        loss.backward()
+        layer = model.language_model.encoder.layers[1]
+        res[flash] = (loss.detach(), layer.self_attention.query_key_value.weight.grad.float(),
+                      layer.self_attention.dense.weight.grad.float(),
+                      model.language_model.embedding.word_embeddings.weight.grad.float())
+    os.environ.pop("BH_FLASH_ATTN")
+    for a, b in zip(res["1"], res["0"]):
+        torch.testing.assert_close(a, b, rtol=5e-2, atol=5e-2)
+    ps.destroy_model_parallel()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["gpt", "bert"])
+def test_flash_attention_matches_unfused_megatron_path(kind):
+    """CoreAttention on the MFMA flash kernels (causal for GPT, -10000 padding fill for BERT) == the
+    bmm + fused-softmax + bmm path."""
+    run_distributed(_flash_vs_unfused, 1, kind)
