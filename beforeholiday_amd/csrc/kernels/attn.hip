@@ -409,8 +409,8 @@ BH_DEVICE void rows_load(RowRegs& r, const T* src, int64_t st, int valid, int ti
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int idx = tid + i * kThreads, row = idx >> 3, ch = idx & 7;
-    r.v[i] = i4v{0, 0, 0, 0};
-    if (row < valid) r.v[i] = *reinterpret_cast<const i4v*>(src + (int64_t)row * st + ch * 8);
+    const i4v v = *reinterpret_cast<const i4v*>(src + (int64_t)min(row, valid - 1) * st + ch * 8);
+    r.v[i] = row < valid ? v : i4v{0, 0, 0, 0};
   }
 }
 BH_DEVICE void rows_store(char* img, const RowRegs& r, int tid) {
@@ -488,35 +488,95 @@ BH_DEVICE float mask_apply(float s, const AttnArgs& a, const char* mimg, int ql,
   return masked ? a.mask_fill : s;
 }
 
+// ---- operand helpers of the register-resident P formulation ----------------------------------
+// A 16x16x32 operand whose k index is the ROW of a row-major image, in the k order in which two
+// stacked C/D tiles (rows 0-15, 16-31 of a 32-deep step) already sit in a lane's registers:
+// element e of lane group g <-> row k0 + 16*(e>>2) + 4*g + (e&3). Two ds_read_b64_tr_b16.
+BH_DEVICE i4v frag_tr_perm(const char* img, int rb, int k0, int n0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int r = k0 + 4 * g + q;
+  const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(img + img_elem(r, n0 + 4 * p, rb)));
+  const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(img + img_elem(r + 16, n0 + 4 * p, rb)));
+  i4v out;
+  out[0] = (int)(uint16_t)lo[0] | ((int)(uint16_t)lo[1] << 16);
+  out[1] = (int)(uint16_t)lo[2] | ((int)(uint16_t)lo[3] << 16);
+  out[2] = (int)(uint16_t)hi[0] | ((int)(uint16_t)hi[1] << 16);
+  out[3] = (int)(uint16_t)hi[2] | ((int)(uint16_t)hi[3] << 16);
+  return out;
+}
+// the matching B (or A) operand straight from two accumulator tiles (no lane movement, no LDS)
+template <typename T> BH_DEVICE i4v pack_pair(const f4v& lo, const f4v& hi) {
+  T v[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = from_f<T>(lo[j]);
+    v[4 + j] = from_f<T>(hi[j]);
+  }
+  return *reinterpret_cast<const i4v*>(v);
+}
+// store 4 consecutive head-dim values (C/D rows 4g..4g+3 of one d-tile) with one 8-byte store
+template <typename T> BH_DEVICE void store4(T* dst, const f4v& v, float mul) {
+  T o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = from_f<T>(v[j] * mul);
+  *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(o);
+}
+
+// counter-based dropout for the flash kernels: a 32-bit avalanche hash of (seed, head, query) per
+// row and of (row hash, key) per element. It is independent of the lane layout, so the forward
+// and dQ kernels (query on the lane) and the dK/dV kernel (key on the lane) regenerate the same
+// keep mask; cheaper per element than Philox4x32-10 split four ways.
+BH_DEVICE uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+BH_DEVICE uint32_t row_hash(const AttnArgs& a, int bh, int q) {
+  return mix32((uint32_t)a.seed ^ mix32((uint32_t)(a.seed >> 32) ^ ((uint32_t)bh * 0x9E3779B1u) ^
+                                        ((uint32_t)q * 0x85EBCA77u)));
+}
+BH_DEVICE bool keep_elem(uint32_t rowh, int k, uint32_t thresh) {
+  return mix32(rowh ^ ((uint32_t)k * 0xC2B2AE3Du)) < thresh;
+}
+BH_DEVICE uint32_t keep_thresh(float p) {
+  const double t = (1.0 - (double)p) * 4294967296.0;
+  return t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+}
+
+// Forward. Workgroup = 64 query rows x one head; wave w = 16 rows, query on the LANE: S^T = K.Q^T
+// puts each query's 16 scores of a 64-key block in one lane's registers, so the online-softmax max
+// and sum are in-lane plus two xor-shuffles, and P^T feeds O^T = V^T.P^T as the B operand without
+// leaving registers. K / V / mask blocks are double-buffered through LDS.
 template <typename T>
 __global__ __launch_bounds__(kThreads) void k_flash_fwd(AttnArgs a) {
-  constexpr int PRB = kKB * 2;
-  constexpr int kBuf = 2 * kKB * 128 + kMaskBytes;  // K, V, mask of one block
-  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + kQB * PRB];
-  char* pimg = smem + 2 * kBuf;
+  constexpr int kBuf = 2 * kKB * 128 + kMaskBytes;
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int bh = blockIdx.y, b = bh / a.heads;
   const int q0 = blockIdx.x * kQB;
-  const int qbase = q0 + wave * 16;
-  const int skt = skt_pad(a.sk);
+  const int myq = q0 + wave * 16 + fr;  // this lane's query
 
   const T* K = reinterpret_cast<const T*>(a.k) + (int64_t)bh * a.k_sbh;
   const T* V = reinterpret_cast<const T*>(a.v) + (int64_t)bh * a.v_sbh;
   const T* Q = reinterpret_cast<const T*>(a.q) + (int64_t)bh * a.q_sbh;
-  i4v qa[2];
+  i4v qb[2];
   {
-    const int qr = min(qbase + fr, a.sq - 1);
+    const int qr = min(myq, a.sq - 1);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) qa[s] = *reinterpret_cast<const i4v*>(Q + (int64_t)qr * a.q_st + 32 * s + 8 * fq);
+    for (int s = 0; s < 2; ++s) qb[s] = *reinterpret_cast<const i4v*>(Q + (int64_t)qr * a.q_st + 32 * s + 8 * fq);
   }
   const bool drop = a.training && a.p_drop > 0.f;
   const float kscale = a.p_drop < 1.f ? 1.f / (1.f - a.p_drop) : 0.f;
-  float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY}, l[4] = {0.f, 0.f, 0.f, 0.f};
+  const uint32_t thresh = keep_thresh(a.p_drop);
+  const uint32_t rowh = drop ? row_hash(a, bh, myq) : 0u;
+  float m = -INFINITY, l = 0.f;
   f4v O[4];
 #pragma unroll
   for (int dn = 0; dn < 4; ++dn) O[dn] = f4v{0.f, 0.f, 0.f, 0.f};
-  // causal: key blocks past this workgroup's last query row contribute nothing
   const int kend = a.mask_mode == 5 ? min(a.sk, q0 + kQB) : a.sk;
   const int nb = (kend + kKB - 1) / kKB;
 
@@ -534,63 +594,53 @@ __global__ __launch_bounds__(kThreads) void k_flash_fwd(AttnArgs a) {
     char* kimg = smem + (ib & 1) * kBuf;
     char* vimg = kimg + kKB * 128;
     const char* mimg = vimg + kKB * 128;
-    if (ib + 1 < nb) {  // prefetch the next block while this one is computed
+    if (ib + 1 < nb) {
       const int kn = kb + kKB;
       rows_load<T>(rk, K + (int64_t)kn * a.k_st, a.k_st, min(kKB, a.sk - kn), tid);
       rows_load<T>(rv, V + (int64_t)kn * a.v_st, a.v_st, min(kKB, a.sk - kn), tid);
       mask_load(rm, a, b, q0, kn, tid);
     }
-    f4v S[4];
+    f4v S[4];  // S^T: row = key 16mt + 4fq + j, column = this lane's query
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      S[n] = f4v{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < 4; ++mt) {
+      S[mt] = f4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 2; ++s) S[n] = Mfma<T>::run(qa[s], frag_row(kimg, 128, 16 * n, 32 * s, lane), S[n]);
+      for (int s = 0; s < 2; ++s) S[mt] = Mfma<T>::run(frag_row(kimg, 128, 16 * mt, 32 * s, lane), qb[s], S[mt]);
     }
-    float mb[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    float mb = -INFINITY;
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         bool mk;
-        const int ql = wave * 16 + 4 * fq + j, kl = 16 * n + fr;
-        const float v = mask_apply(S[n][j] * a.scale, a, mimg, ql, kl, q0 + ql, kb + kl, mk);
-        S[n][j] = v;
-        mb[j] = fmaxf(mb[j], v);
+        const int kl = 16 * mt + 4 * fq + j;
+        S[mt][j] = mask_apply(S[mt][j] * a.scale, a, mimg, myq - q0, kl, myq, kb + kl, mk);
+        mb = fmaxf(mb, S[mt][j]);
       }
-    float corr[4], ls[4];
+    mb = fmaxf(mb, __shfl_xor(mb, 16));
+    mb = fmaxf(mb, __shfl_xor(mb, 32));
+    const float mn = fmaxf(m, mb);
+    const float corr = (m == -INFINITY) ? 0.f : __expf(m - mn);
+    m = mn;
+    float ls = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float mn = fmaxf(m[j], wmax16(mb[j]));
-      corr[j] = (m[j] == -INFINITY) ? 0.f : __expf(m[j] - mn);
-      m[j] = mn;
-      ls[j] = 0.f;
-    }
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      float4 kp = make_float4(1.f, 1.f, 1.f, 1.f);
-      if (drop) kp = keep4(a, bh, qbase + 4 * fq, kb + 16 * n + fr, skt);
-      const float kk[4] = {kp.x * kscale, kp.y * kscale, kp.z * kscale, kp.w * kscale};
+    for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float p = m[j] == -INFINITY ? 0.f : __expf(S[n][j] - m[j]);
-        ls[j] += p;
-        const float pd = drop ? p * kk[j] : p;
-        *reinterpret_cast<T*>(pimg + img_elem(wave * 16 + 4 * fq + j, 16 * n + fr, PRB)) = from_f<T>(pd);
+        const float p = m == -INFINITY ? 0.f : __expf(S[mt][j] - m);
+        ls += p;
+        S[mt][j] = (drop && !keep_elem(rowh, kb + 16 * mt + 4 * fq + j, thresh)) ? 0.f : p;
       }
-    }
+    ls += __shfl_xor(ls, 16);
+    ls += __shfl_xor(ls, 32);
+    l = l * corr + ls;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) l[j] = l[j] * corr[j] + wsum16(ls[j]);
+    for (int dn = 0; dn < 4; ++dn) O[dn] *= corr;
 #pragma unroll
-    for (int dn = 0; dn < 4; ++dn)
+    for (int t = 0; t < 2; ++t) {
+      const i4v pb = pack_pair<T>(S[2 * t], S[2 * t + 1]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) O[dn][j] *= corr[j];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's P rows are written (wave-private)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const i4v pa = frag_row(pimg, PRB, wave * 16, 32 * ks, lane);
-#pragma unroll
-      for (int dn = 0; dn < 4; ++dn) O[dn] = Mfma<T>::run(pa, frag_tr(vimg, 128, 32 * ks, 16 * dn, lane), O[dn]);
+      for (int dn = 0; dn < 4; ++dn) O[dn] = Mfma<T>::run(frag_tr_perm(vimg, 128, 32 * t, 16 * dn, lane), pb, O[dn]);
     }
     if (ib + 1 < nb) {
       char* nk = smem + ((ib + 1) & 1) * kBuf;
@@ -598,18 +648,14 @@ __global__ __launch_bounds__(kThreads) void k_flash_fwd(AttnArgs a) {
       rows_store(nk + kKB * 128, rv, tid);
       mask_store(nk + 2 * kKB * 128, rm, a, tid);
     }
-    __syncthreads();  // next buffer complete; this buffer free for the block after next
+    __syncthreads();
   }
-  T* Out = reinterpret_cast<T*>(a.o) + (int64_t)bh * a.o_sbh;
+  if (myq < a.sq) {
+    const float inv = l > 0.f ? (drop ? kscale : 1.f) / l : 0.f;
+    T* out = reinterpret_cast<T*>(a.o) + (int64_t)bh * a.o_sbh + (int64_t)myq * a.o_st;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int q = qbase + 4 * fq + j;
-    const float inv = l[j] > 0.f ? 1.f / l[j] : 0.f;
-    if (q < a.sq) {
-#pragma unroll
-      for (int dn = 0; dn < 4; ++dn) Out[(int64_t)q * a.o_st + 16 * dn + fr] = from_f<T>(O[dn][j] * inv);
-      if (fr == 0) a.lse[(int64_t)bh * a.sq + q] = l[j] > 0.f ? m[j] + __logf(l[j]) : INFINITY;
-    }
+    for (int dn = 0; dn < 4; ++dn) store4<T>(out + 16 * dn + 4 * fq, O[dn], inv);
+    if (fq == 0) a.lse[(int64_t)bh * a.sq + myq] = l > 0.f ? m + __logf(l) : INFINITY;
   }
 }
 
@@ -630,73 +676,35 @@ __global__ __launch_bounds__(256) void k_flash_delta(AttnArgs a, float* __restri
   if (sub == 0) delta[row] = acc;
 }
 
-// P (dropped, via LSE) and dS for one wave's 16 query rows (local rows wave*16..) x one key block
-template <typename T>
-BH_DEVICE void flash_bwd_tile(const AttnArgs& a, int bh, int q0, int qbase, int kb, int skt, const i4v (&qa)[2],
-                              const i4v (&da)[2], const char* kimg, const char* vimg, const char* mimg,
-                              const float (&lse)[4], const float (&dl)[4], f4v (&P)[4], f4v (&dS)[4], int lane) {
-  const int fr = lane & 15, fq = lane >> 4;
-  const bool drop = a.training && a.p_drop > 0.f;
-  const float kscale = a.p_drop < 1.f ? 1.f / (1.f - a.p_drop) : 0.f;
-#pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    f4v S = f4v{0.f, 0.f, 0.f, 0.f}, dP = f4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      S = Mfma<T>::run(qa[s], frag_row(kimg, 128, 16 * n, 32 * s, lane), S);
-      dP = Mfma<T>::run(da[s], frag_row(vimg, 128, 16 * n, 32 * s, lane), dP);
-    }
-    float4 kp = make_float4(1.f, 1.f, 1.f, 1.f);
-    if (drop) kp = keep4(a, bh, qbase + 4 * fq, kb + 16 * n + fr, skt);
-    const float kk[4] = {kp.x * kscale, kp.y * kscale, kp.z * kscale, kp.w * kscale};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int q = qbase + 4 * fq + j, kl = 16 * n + fr;
-      bool mk;
-      const float v = mask_apply(S[j] * a.scale, a, mimg, q - q0, kl, q, kb + kl, mk);
-      const float p = (q < a.sq && v != -INFINITY && lse[j] != INFINITY) ? __expf(v - lse[j]) : 0.f;
-      const float dpd = drop ? dP[j] * kk[j] : dP[j];
-      P[n][j] = drop ? p * kk[j] : p;  // dropped probability (dV operand)
-      // a masked score is a constant: no gradient flows to Q / K through it (matters for fully
-      // masked rows under a finite fill, where p is uniform rather than 0)
-      dS[n][j] = mk ? 0.f : p * (dpd - dl[j]) * a.scale;
-    }
-  }
-}
-
-// dQ: one workgroup per (64-row query block, head); streams key blocks (double-buffered)
+// dQ. Same layout as the forward (query on the lane): S^T = K.Q^T and dP^T = V.dO^T, P^T from
+// the saved LSE, dS^T in registers feeds dQ^T = K^T.dS^T directly.
 template <typename T>
 __global__ __launch_bounds__(kThreads) void k_flash_bwd_dq(AttnArgs a) {
-  constexpr int PRB = kKB * 2;
   constexpr int kBuf = 2 * kKB * 128 + kMaskBytes;
-  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + kQB * PRB];
-  char* dsimg = smem + 2 * kBuf;
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int bh = blockIdx.y, b = bh / a.heads;
   const int q0 = blockIdx.x * kQB;
-  const int qbase = q0 + wave * 16;
-  const int skt = skt_pad(a.sk);
+  const int myq = q0 + wave * 16 + fr;
   const T* K = reinterpret_cast<const T*>(a.k) + (int64_t)bh * a.k_sbh;
   const T* V = reinterpret_cast<const T*>(a.v) + (int64_t)bh * a.v_sbh;
   const T* Q = reinterpret_cast<const T*>(a.q) + (int64_t)bh * a.q_sbh;
   const T* dO = reinterpret_cast<const T*>(a.dout) + (int64_t)bh * a.do_sbh;
-  i4v qa[2], da[2];
-  {
-    const int qr = min(qbase + fr, a.sq - 1);
+  i4v qb[2], db[2];
+  const int qr = min(myq, a.sq - 1);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      qa[s] = *reinterpret_cast<const i4v*>(Q + (int64_t)qr * a.q_st + 32 * s + 8 * fq);
-      da[s] = *reinterpret_cast<const i4v*>(dO + (int64_t)qr * a.do_st + 32 * s + 8 * fq);
-    }
+  for (int s = 0; s < 2; ++s) {
+    qb[s] = *reinterpret_cast<const i4v*>(Q + (int64_t)qr * a.q_st + 32 * s + 8 * fq);
+    db[s] = *reinterpret_cast<const i4v*>(dO + (int64_t)qr * a.do_st + 32 * s + 8 * fq);
   }
-  float lse[4], dl[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int q = min(qbase + 4 * fq + j, a.sq - 1);
-    lse[j] = a.lse[(int64_t)bh * a.sq + q];
-    dl[j] = a.delta[(int64_t)bh * a.sq + q];
-  }
+  const float lse = a.lse[(int64_t)bh * a.sq + qr];
+  const float dl = a.delta[(int64_t)bh * a.sq + qr];
+  const bool rowok = myq < a.sq && lse != INFINITY;
+  const bool drop = a.training && a.p_drop > 0.f;
+  const float kscale = a.p_drop < 1.f ? 1.f / (1.f - a.p_drop) : 0.f;
+  const uint32_t thresh = keep_thresh(a.p_drop);
+  const uint32_t rowh = drop ? row_hash(a, bh, myq) : 0u;
   f4v acc[4];
 #pragma unroll
   for (int dn = 0; dn < 4; ++dn) acc[dn] = f4v{0.f, 0.f, 0.f, 0.f};
@@ -722,19 +730,31 @@ __global__ __launch_bounds__(kThreads) void k_flash_bwd_dq(AttnArgs a) {
       rows_load<T>(rv, V + (int64_t)kn * a.v_st, a.v_st, min(kKB, a.sk - kn), tid);
       mask_load(rm, a, b, q0, kn, tid);
     }
-    f4v P[4], dS[4];
-    flash_bwd_tile<T>(a, bh, q0, qbase, kb, skt, qa, da, kimg, vimg, mimg, lse, dl, P, dS, lane);
+    f4v dS[4];
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int mt = 0; mt < 4; ++mt) {
+      f4v S = f4v{0.f, 0.f, 0.f, 0.f}, dP = f4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        *reinterpret_cast<T*>(dsimg + img_elem(wave * 16 + 4 * fq + j, 16 * n + fr, PRB)) = from_f<T>(dS[n][j]);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (int s = 0; s < 2; ++s) {
+        S = Mfma<T>::run(frag_row(kimg, 128, 16 * mt, 32 * s, lane), qb[s], S);
+        dP = Mfma<T>::run(frag_row(vimg, 128, 16 * mt, 32 * s, lane), db[s], dP);
+      }
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const i4v dsa = frag_row(dsimg, PRB, wave * 16, 32 * ks, lane);
+      for (int j = 0; j < 4; ++j) {
+        const int kl = 16 * mt + 4 * fq + j;
+        bool mk;
+        const float v = mask_apply(S[j] * a.scale, a, mimg, myq - q0, kl, myq, kb + kl, mk);
+        const float p = (rowok && v != -INFINITY) ? __expf(v - lse) : 0.f;
+        const float dpd = drop ? (keep_elem(rowh, kb + kl, thresh) ? dP[j] * kscale : 0.f) : dP[j];
+        dS[mt][j] = mk ? 0.f : p * (dpd - dl) * a.scale;
+      }
+    }
 #pragma unroll
-      for (int dn = 0; dn < 4; ++dn) acc[dn] = Mfma<T>::run(dsa, frag_tr(kimg, 128, 32 * ks, 16 * dn, lane), acc[dn]);
+    for (int t = 0; t < 2; ++t) {
+      const i4v sb = pack_pair<T>(dS[2 * t], dS[2 * t + 1]);
+#pragma unroll
+      for (int dn = 0; dn < 4; ++dn)
+        acc[dn] = Mfma<T>::run(frag_tr_perm(kimg, 128, 32 * t, 16 * dn, lane), sb, acc[dn]);
     }
     if (ib + 1 < nb) {
       char* nk = smem + ((ib + 1) & 1) * kBuf;
@@ -744,125 +764,120 @@ __global__ __launch_bounds__(kThreads) void k_flash_bwd_dq(AttnArgs a) {
     }
     __syncthreads();
   }
-  T* dQ = reinterpret_cast<T*>(a.dq) + (int64_t)bh * a.dq_sbh;
+  if (myq < a.sq) {
+    T* dq = reinterpret_cast<T*>(a.dq) + (int64_t)bh * a.dq_sbh + (int64_t)myq * a.dq_st;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int q = qbase + 4 * fq + j;
-    if (q < a.sq) {
-#pragma unroll
-      for (int dn = 0; dn < 4; ++dn) dQ[(int64_t)q * a.dq_st + 16 * dn + fr] = from_f<T>(acc[dn][j]);
-    }
+    for (int dn = 0; dn < 4; ++dn) store4<T>(dq + 16 * dn + 4 * fq, acc[dn], 1.f);
   }
 }
 
-// dK, dV: one workgroup per (64-key block, head); streams query blocks (double-buffered Q / dO /
-// mask), keeps dK / dV of its keys in registers (wave w owns keys 16w..16w+15 of the block)
+// dK / dV. Workgroup = 64 keys x one head, wave w owns keys 16w..16w+15 with the KEY on the lane:
+// S = Q.K^T and dP = dO.V^T per 16-query tile put 4 queries of one key in a lane's registers, so
+// Pd and dS feed dV^T = dO^T.Pd and dK^T = Q^T.dS as B operands straight from registers (no
+// cross-wave reduction, no LDS round trip). Q / dO / LSE / delta / mask blocks are double-buffered.
 template <typename T>
 __global__ __launch_bounds__(kThreads) void k_flash_bwd_dkdv(AttnArgs a) {
-  constexpr int PRB = kKB * 2;
-  constexpr int kBuf = 2 * kQB * 128 + kMaskBytes;  // Q, dO, mask of one query block
-  __shared__ __attribute__((aligned(16))) char smem[2 * kKB * 128 + 2 * kBuf + 2 * kQB * PRB];
-  char* kimg = smem;
-  char* vimg = kimg + kKB * 128;
-  char* bufs = vimg + kKB * 128;
-  char* pdimg = bufs + 2 * kBuf;
-  char* dsimg = pdimg + kQB * PRB;
+  constexpr int kBuf = 2 * kQB * 128 + kMaskBytes + 2 * kQB * 4;  // Q, dO, mask, LSE, delta
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int bh = blockIdx.y, b = bh / a.heads;
   const int kb = blockIdx.x * kKB;
-  const int skt = skt_pad(a.sk);
+  const int mykey = kb + wave * 16 + fr;
   const T* K = reinterpret_cast<const T*>(a.k) + (int64_t)bh * a.k_sbh;
   const T* V = reinterpret_cast<const T*>(a.v) + (int64_t)bh * a.v_sbh;
   const T* Q = reinterpret_cast<const T*>(a.q) + (int64_t)bh * a.q_sbh;
   const T* dO = reinterpret_cast<const T*>(a.dout) + (int64_t)bh * a.do_sbh;
+  i4v kbf[2], vbf[2];
   {
-    RowRegs r;
-    rows_load<T>(r, K + (int64_t)kb * a.k_st, a.k_st, min(kKB, a.sk - kb), tid);
-    rows_store(kimg, r, tid);
-    rows_load<T>(r, V + (int64_t)kb * a.v_st, a.v_st, min(kKB, a.sk - kb), tid);
-    rows_store(vimg, r, tid);
+    const int kr = min(mykey, a.sk - 1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      kbf[s] = *reinterpret_cast<const i4v*>(K + (int64_t)kr * a.k_st + 32 * s + 8 * fq);
+      vbf[s] = *reinterpret_cast<const i4v*>(V + (int64_t)kr * a.v_st + 32 * s + 8 * fq);
+    }
   }
+  const bool drop = a.training && a.p_drop > 0.f;
+  const float kscale = a.p_drop < 1.f ? 1.f / (1.f - a.p_drop) : 0.f;
+  const uint32_t thresh = keep_thresh(a.p_drop);
   f4v dK[4], dV[4];
 #pragma unroll
-  for (int n = 0; n < 4; ++n) dK[n] = dV[n] = f4v{0.f, 0.f, 0.f, 0.f};
-  // causal: query blocks entirely above this key block see none of its keys
+  for (int dn = 0; dn < 4; ++dn) dK[dn] = dV[dn] = f4v{0.f, 0.f, 0.f, 0.f};
   const int qstart = a.mask_mode == 5 ? (kb / kQB) * kQB : 0;
   const int nqb = (a.sq - qstart + kQB - 1) / kQB;
+  const float* lseg = a.lse + (int64_t)bh * a.sq;
+  const float* dlg = a.delta + (int64_t)bh * a.sq;
   RowRegs rq, rd;
   MaskRegs rm;
-  rows_load<T>(rq, Q + (int64_t)qstart * a.q_st, a.q_st, min(kQB, a.sq - qstart), tid);
-  rows_load<T>(rd, dO + (int64_t)qstart * a.do_st, a.do_st, min(kQB, a.sq - qstart), tid);
-  mask_load(rm, a, b, qstart, kb, tid);
-  rows_store(bufs, rq, tid);
-  rows_store(bufs + kQB * 128, rd, tid);
-  mask_store(bufs + 2 * kQB * 128, rm, a, tid);
+  float rl = 0.f;
+  auto load_blk = [&](int qs) {
+    rows_load<T>(rq, Q + (int64_t)qs * a.q_st, a.q_st, min(kQB, a.sq - qs), tid);
+    rows_load<T>(rd, dO + (int64_t)qs * a.do_st, a.do_st, min(kQB, a.sq - qs), tid);
+    mask_load(rm, a, b, qs, kb, tid);
+    if (tid < 2 * kQB) {
+      const int q = min(qs + (tid & (kQB - 1)), a.sq - 1);
+      const float v = tid < kQB ? lseg[q] : dlg[q];
+      rl = qs + (tid & (kQB - 1)) < a.sq ? v : (tid < kQB ? INFINITY : 0.f);  // p = 0 there; keep dS finite
+    }
+  };
+  auto store_blk = [&](char* buf) {
+    rows_store(buf, rq, tid);
+    rows_store(buf + kQB * 128, rd, tid);
+    mask_store(buf + 2 * kQB * 128, rm, a, tid);
+    if (tid < 2 * kQB) reinterpret_cast<float*>(buf + 2 * kQB * 128 + kMaskBytes)[tid] = rl;
+  };
+  load_blk(qstart);
+  store_blk(smem);
   __syncthreads();
   for (int iq = 0; iq < nqb; ++iq) {
     const int q0 = qstart + iq * kQB;
-    char* qimg = bufs + (iq & 1) * kBuf;
+    char* qimg = smem + (iq & 1) * kBuf;
     char* doimg = qimg + kQB * 128;
     const char* mimg = doimg + kQB * 128;
-    if (iq + 1 < nqb) {
-      const int qn = q0 + kQB;
-      rows_load<T>(rq, Q + (int64_t)qn * a.q_st, a.q_st, min(kQB, a.sq - qn), tid);
-      rows_load<T>(rd, dO + (int64_t)qn * a.do_st, a.do_st, min(kQB, a.sq - qn), tid);
-      mask_load(rm, a, b, qn, kb, tid);
-    }
-    const int qbase = q0 + wave * 16;
-    i4v qa[2], da[2];
+    const float* lsel = reinterpret_cast<const float*>(mimg + kMaskBytes);
+    const float* dll = lsel + kQB;
+    if (iq + 1 < nqb) load_blk(q0 + kQB);
+    f4v Pd[4], dS[4];  // row = query 16qt + 4fq + j of the block, column = this lane's key
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      qa[s] = frag_row(qimg, 128, wave * 16, 32 * s, lane);
-      da[s] = frag_row(doimg, 128, wave * 16, 32 * s, lane);
-    }
-    float lse[4], dl[4];
+    for (int qt = 0; qt < 4; ++qt) {
+      f4v S = f4v{0.f, 0.f, 0.f, 0.f}, dP = f4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int q = min(qbase + 4 * fq + j, a.sq - 1);
-      lse[j] = a.lse[(int64_t)bh * a.sq + q];
-      dl[j] = a.delta[(int64_t)bh * a.sq + q];
-    }
-    f4v P[4], dS[4];
-    flash_bwd_tile<T>(a, bh, q0, qbase, kb, skt, qa, da, kimg, vimg, mimg, lse, dl, P, dS, lane);
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
+      for (int s = 0; s < 2; ++s) {
+        S = Mfma<T>::run(frag_row(qimg, 128, 16 * qt, 32 * s, lane), kbf[s], S);
+        dP = Mfma<T>::run(frag_row(doimg, 128, 16 * qt, 32 * s, lane), vbf[s], dP);
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int row = wave * 16 + 4 * fq + j;
-        *reinterpret_cast<T*>(pdimg + img_elem(row, 16 * n + fr, PRB)) = from_f<T>(P[n][j]);
-        *reinterpret_cast<T*>(dsimg + img_elem(row, 16 * n + fr, PRB)) = from_f<T>(dS[n][j]);
+        const int ql = 16 * qt + 4 * fq + j, q = q0 + ql;
+        const float lse = lsel[ql], dl = dll[ql];
+        bool mk;
+        const float v = mask_apply(S[j] * a.scale, a, mimg, ql, wave * 16 + fr, q, mykey, mk);
+        const float p = (q < a.sq && v != -INFINITY && lse != INFINITY) ? __expf(v - lse) : 0.f;
+        const float kk = drop ? (keep_elem(row_hash(a, bh, q), mykey, thresh) ? kscale : 0.f) : 1.f;
+        Pd[qt][j] = p * kk;
+        dS[qt][j] = mk ? 0.f : p * (dP[j] * kk - dl) * a.scale;
       }
-    __syncthreads();  // Pd / dS images of all 64 query rows complete
+    }
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const i4v pa = frag_tr(pdimg, PRB, 32 * ks, wave * 16, lane);
-      const i4v sa = frag_tr(dsimg, PRB, 32 * ks, wave * 16, lane);
+    for (int t = 0; t < 2; ++t) {
+      const i4v pb = pack_pair<T>(Pd[2 * t], Pd[2 * t + 1]);
+      const i4v sb = pack_pair<T>(dS[2 * t], dS[2 * t + 1]);
 #pragma unroll
       for (int dn = 0; dn < 4; ++dn) {
-        dV[dn] = Mfma<T>::run(pa, frag_tr(doimg, 128, 32 * ks, 16 * dn, lane), dV[dn]);
-        dK[dn] = Mfma<T>::run(sa, frag_tr(qimg, 128, 32 * ks, 16 * dn, lane), dK[dn]);
+        dV[dn] = Mfma<T>::run(frag_tr_perm(doimg, 128, 32 * t, 16 * dn, lane), pb, dV[dn]);
+        dK[dn] = Mfma<T>::run(frag_tr_perm(qimg, 128, 32 * t, 16 * dn, lane), sb, dK[dn]);
       }
     }
-    if (iq + 1 < nqb) {
-      char* nb_ = bufs + ((iq + 1) & 1) * kBuf;
-      rows_store(nb_, rq, tid);
-      rows_store(nb_ + kQB * 128, rd, tid);
-      mask_store(nb_ + 2 * kQB * 128, rm, a, tid);
-    }
-    __syncthreads();  // next buffer complete; Pd / dS images free
+    if (iq + 1 < nqb) store_blk(smem + ((iq + 1) & 1) * kBuf);
+    __syncthreads();
   }
-  T* dKp = reinterpret_cast<T*>(a.dk) + (int64_t)bh * a.dk_sbh;
-  T* dVp = reinterpret_cast<T*>(a.dv) + (int64_t)bh * a.dv_sbh;
+  if (mykey < a.sk) {
+    T* dk = reinterpret_cast<T*>(a.dk) + (int64_t)bh * a.dk_sbh + (int64_t)mykey * a.dk_st;
+    T* dv = reinterpret_cast<T*>(a.dv) + (int64_t)bh * a.dv_sbh + (int64_t)mykey * a.dv_st;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int key = kb + wave * 16 + 4 * fq + j;
-    if (key < a.sk) {
-#pragma unroll
-      for (int dn = 0; dn < 4; ++dn) {
-        dKp[(int64_t)key * a.dk_st + 16 * dn + fr] = from_f<T>(dK[dn][j]);
-        dVp[(int64_t)key * a.dv_st + 16 * dn + fr] = from_f<T>(dV[dn][j]);
-      }
+    for (int dn = 0; dn < 4; ++dn) {
+      store4<T>(dk + 16 * dn + 4 * fq, dK[dn], 1.f);
+      store4<T>(dv + 16 * dn + 4 * fq, dV[dn], 1.f);
     }
   }
 }
