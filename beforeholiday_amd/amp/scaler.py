@@ -6,6 +6,8 @@ overflow flag), the flag is read once per step in ``update_scale``.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..multi_tensor_apply import multi_tensor_applier
@@ -13,10 +15,18 @@ from ..ops import amp_C
 from ._amp_state import maybe_print
 
 
+def _has_inf_or_nan(t):
+    # one host sync per tensor, like the reference's python fallback (apex/amp/scaler.py:6-21)
+    v = float(t.float().sum())
+    return v != v or v in (float("inf"), float("-inf"))
+
+
 class LossScaler(object):
     warned_no_fused_kernel = False
     warned_unscaling_non_fp32_grad = False
-    has_fused_kernel = True
+    # False = the reference's "python-only install" path (per-tensor checks and copies, no
+    # multi-tensor kernel); the L1 cross-product test compares both bitwise. BH_AMP_PYTHON_SCALER=1.
+    has_fused_kernel = os.environ.get("BH_AMP_PYTHON_SCALER", "0") != "1"
 
     def __init__(self, loss_scale, init_scale=2.0 ** 16, scale_factor=2.0, scale_window=2000,
                  min_loss_scale=None, max_loss_scale=2.0 ** 24, device=None):
@@ -64,6 +74,18 @@ class LossScaler(object):
         if not model_grads:
             return
         self._warn_non_fp32(master_grads)
+        if not LossScaler.has_fused_kernel:
+            for m, s in zip(model_grads, master_grads):
+                if m is None:
+                    continue
+                if self.dynamic and _has_inf_or_nan(m):
+                    self._has_overflow = True
+                    return
+                if s is not m:
+                    s.copy_(m)
+                if scale != 1.0:
+                    s.mul_(1.0 / scale)
+            return
         # group by (model dtype, master dtype): each list passed to the kernel is single-dtype
         groups = {}
         for m, s in zip(model_grads, master_grads):
@@ -83,6 +105,14 @@ class LossScaler(object):
         if not model_grads:
             return
         self._warn_non_fp32(master_grads)
+        if not LossScaler.has_fused_kernel:
+            a, b = out_scale / grads_have_scale, out_scale / stashed_have_scale
+            for m, st, out in zip(model_grads, stashed_master_grads, master_grads):
+                if self.dynamic and _has_inf_or_nan(m):
+                    self._has_overflow = True
+                    return
+                out.copy_(m.float() * a + st.float() * b)
+            return
         groups = {}
         for m, st, out in zip(model_grads, stashed_master_grads, master_grads):
             key = (m.dtype, st.dtype, out.dtype)
@@ -99,7 +129,7 @@ class LossScaler(object):
         self._overflow_buf.zero_()
 
     def update_scale(self):
-        if self.dynamic and not self._has_overflow:
+        if self.dynamic and not self._has_overflow and LossScaler.has_fused_kernel:
             self._has_overflow = bool(self._overflow_buf.item())
         if self._has_overflow and self.dynamic:
             should_skip = True

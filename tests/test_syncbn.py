@@ -187,3 +187,63 @@ def test_conv1x1_gemm_matches_conv(dtype):
     yr.backward(g)
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=tol, atol=tol)
     torch.testing.assert_close(m.weight.grad.float(), w.grad, rtol=tol, atol=tol * 20)
+
+
+def _dist_syncbn_uneven(rank, world):
+    """Different per-rank batch sizes (reference: tests/distributed/synced_batchnorm/
+    two_gpu_test_different_batch_size.py): stats are count-weighted, so the split run equals BN
+    over the concatenated batch."""
+    torch.manual_seed(1)
+    sizes = [3 + 2 * r for r in range(world)]
+    off = [sum(sizes[:r]) for r in range(world)]
+    C = 8
+    x = torch.randn(sum(sizes), C, 4, 3) * 2 - 0.5
+    dy = torch.randn_like(x)
+    ref = torch.nn.BatchNorm2d(C)
+    for impl in (SyncBatchNorm, PythonSyncBatchNorm):
+        bn = impl(C)
+        bn.load_state_dict(ref.state_dict())
+        sl = slice(off[rank], off[rank] + sizes[rank])
+        xs = x[sl].clone().requires_grad_(True)
+        bn(xs).backward(dy[sl])
+        r = torch.nn.BatchNorm2d(C)
+        r.load_state_dict(ref.state_dict())
+        xr = x.clone().requires_grad_(True)
+        yr = r(xr)
+        yr.backward(dy)
+        torch.testing.assert_close(xs.grad, xr.grad[sl], rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(bn.running_mean, r.running_mean, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(bn.running_var, r.running_var, rtol=1e-5, atol=1e-5)
+
+
+def test_syncbn_uneven_batches_gloo():
+    run_distributed(_dist_syncbn_uneven, 2)
+
+
+def _dist_syncbn_groups(rank, world):
+    """Sub-group sync (reference: tests/distributed/synced_batchnorm/test_groups.py): 4 ranks in
+    two BN groups of 2; each group's statistics are those of its own two shards only."""
+    from beforeholiday_amd.parallel import create_syncbn_process_group
+    group = create_syncbn_process_group(2)
+    torch.manual_seed(2)
+    C, n = 6, 3
+    x = torch.randn(world * n, C, 5) + torch.arange(world * n).view(-1, 1, 1) * 0.1
+    dy = torch.randn_like(x)
+    g0 = (rank // 2) * 2
+    for impl in (SyncBatchNorm, PythonSyncBatchNorm):
+        bn = impl(C, process_group=group)
+        xs = x[rank * n:(rank + 1) * n].clone().requires_grad_(True)
+        y = bn(xs)
+        y.backward(dy[rank * n:(rank + 1) * n])
+        r = torch.nn.BatchNorm1d(C)
+        xr = x[g0 * n:(g0 + 2) * n].clone().requires_grad_(True)
+        yr = r(xr)
+        yr.backward(dy[g0 * n:(g0 + 2) * n])
+        loc = slice((rank - g0) * n, (rank - g0 + 1) * n)
+        torch.testing.assert_close(y, yr[loc], rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(xs.grad, xr.grad[loc], rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(bn.running_var, r.running_var, rtol=1e-5, atol=1e-5)
+
+
+def test_syncbn_process_subgroups_gloo():
+    run_distributed(_dist_syncbn_groups, 4)
