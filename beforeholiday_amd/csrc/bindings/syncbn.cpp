@@ -2,6 +2,7 @@
 // Kernels: kernels/batchnorm.hip. Reference API: csrc/syncbn.cpp:98-109 (compat wrappers for those
 // names live in python: beforeholiday_amd/ops/syncbn.py).
 #include "common.h"
+#include "bh/pool_api.h"
 
 #include "bh/bn_api.h"
 
@@ -241,6 +242,56 @@ std::vector<at::Tensor> backward_dgrad(at::Tensor dy_in, at::Tensor x_in, c10::o
   return {dx, dz};
 }
 
+// ---- NHWC max pooling, optionally fused with the BN affine + ReLU (kernels/pool.hip) ----
+bh::PoolArgs pool_args(const at::Tensor& x, int64_t H, int64_t W, int64_t k, int64_t s, int64_t p, bool relu) {
+  bh::PoolArgs a;
+  a.N = (int)x.size(0);
+  a.C = (int)x.size(1);
+  a.H = (int)H;
+  a.W = (int)W;
+  a.k = (int)k;
+  a.stride = (int)s;
+  a.pad = (int)p;
+  a.OH = (int)((H + 2 * p - k) / s + 1);
+  a.OW = (int)((W + 2 * p - k) / s + 1);
+  a.relu = relu;
+  TORCH_CHECK(a.C % 8 == 0 && k * k <= 255 && p <= k / 2 && a.OH > 0 && a.OW > 0,
+              "maxpool_nhwc: needs C % 8 == 0, k*k <= 255, pad <= k/2");
+  return a;
+}
+
+std::vector<at::Tensor> maxpool_forward(at::Tensor x, c10::optional<at::Tensor> scale, c10::optional<at::Tensor> shift,
+                                        bool relu, int64_t k, int64_t s, int64_t p, bool want_idx,
+                                        c10::optional<at::Tensor> num_batches) {
+  check_cuda(x, "input");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "maxpool_nhwc: 4-D channels_last input");
+  const bool bn = scale.has_value() && scale->defined();
+  if (bn)
+    TORCH_CHECK(scale->scalar_type() == at::kFloat && shift->scalar_type() == at::kFloat && scale->numel() == x.size(1)
+                    && scale->is_contiguous() && shift->is_contiguous(), "scale/shift must be contiguous fp32 [C]");
+  bh::PoolArgs a = pool_args(x, x.size(2), x.size(3), k, s, p, relu);
+  auto y = at::empty({a.N, a.C, a.OH, a.OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  at::Tensor idx;
+  if (want_idx) idx = at::empty({a.N, a.C, a.OH, a.OW}, x.options().dtype(at::kByte).memory_format(at::MemoryFormat::ChannelsLast));
+  bh::maxpool_forward_nhwc(a, dtype_code(x.scalar_type()), x.data_ptr(), bn ? scale->data_ptr<float>() : nullptr,
+                           bn ? shift->data_ptr<float>() : nullptr, y.data_ptr(),
+                           want_idx ? idx.data_ptr<uint8_t>() : nullptr, counter_ptr(num_batches), stream_for(x));
+  return {y, idx};
+}
+
+at::Tensor maxpool_backward(at::Tensor gy, at::Tensor idx, int64_t H, int64_t W, int64_t k, int64_t s, int64_t p) {
+  check_cuda(gy, "grad_output");
+  gy = gy.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(idx.scalar_type() == at::kByte && idx.sizes() == gy.sizes() &&
+              idx.is_contiguous(at::MemoryFormat::ChannelsLast), "maxpool_backward: idx must match grad_output");
+  bh::PoolArgs a = pool_args(gy, H, W, k, s, p, false);
+  TORCH_CHECK(a.OH == gy.size(2) && a.OW == gy.size(3), "maxpool_backward: output size mismatch");
+  auto gx = at::empty({a.N, a.C, H, W}, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  bh::maxpool_backward_nhwc(a, dtype_code(gy.scalar_type()), gy.data_ptr(), idx.data_ptr<uint8_t>(), gx.data_ptr(),
+                            stream_for(gy));
+  return gx;
+}
+
 }  // namespace
 
 void register_syncbn(pybind11::module_& root) {
@@ -260,6 +311,12 @@ void register_syncbn(pybind11::module_& root) {
   m.def("backward_dgrad", &backward_dgrad, py::arg("dy"), py::arg("x"), py::arg("z"), py::arg("mean"),
         py::arg("invstd"), py::arg("weight"), py::arg("sums"), py::arg("count"), py::arg("scale"), py::arg("shift"),
         py::arg("relu"), py::arg("need_dz"));
+  m.def("maxpool_forward", &maxpool_forward, py::arg("x"), py::arg("scale"), py::arg("shift"), py::arg("relu"),
+        py::arg("kernel_size"), py::arg("stride"), py::arg("padding"), py::arg("want_idx"),
+        py::arg("num_batches") = py::none(),
+        "NHWC max pool of (relu)(x*scale+shift): returns (y, uint8 argmax offsets)");
+  m.def("maxpool_backward", &maxpool_backward, py::arg("grad_output"), py::arg("idx"), py::arg("H"), py::arg("W"),
+        py::arg("kernel_size"), py::arg("stride"), py::arg("padding"));
 }
 
 }  // namespace bhb

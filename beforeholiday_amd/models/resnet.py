@@ -99,13 +99,19 @@ class Bottleneck(nn.Module):
 
 class ResNet(nn.Module):
     def __init__(self, block: Type[Bottleneck], layers: List[int], num_classes=1000,
-                 zero_init_residual=False, norm_layer=nn.BatchNorm2d, fused=False):
+                 zero_init_residual=False, norm_layer=nn.BatchNorm2d, fused=False, stem_pool_fused=False):
         super().__init__()
         self._norm_layer = norm_layer
         self.fused = fused
+        # stem_pool_fused: bn1 also applies the 3x3/2 max pool (one pass, the normalised stem
+        # activation is never materialised); same parameters / state_dict as the unfused stem
+        self.stem_pool_fused = fused and stem_pool_fused
         self.inplanes = 64
         self.conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
-        self.bn1 = norm_layer(64, fuse_relu=True) if fused else norm_layer(64)
+        if self.stem_pool_fused:
+            self.bn1 = norm_layer(64, fuse_relu=True, fuse_maxpool=(3, 2, 1))
+        else:
+            self.bn1 = norm_layer(64, fuse_relu=True) if fused else norm_layer(64)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
@@ -138,8 +144,11 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.bn1(self.conv1(x)) if self.fused else self.relu(self.bn1(self.conv1(x)))
-        x = self.maxpool(x)
+        if self.stem_pool_fused:
+            x = self.bn1(self.conv1(x))
+        else:
+            x = self.bn1(self.conv1(x)) if self.fused else self.relu(self.bn1(self.conv1(x)))
+            x = self.maxpool(x)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
@@ -149,19 +158,20 @@ def resnet50(**kw) -> ResNet:
     return ResNet(Bottleneck, [3, 4, 6, 3], **kw)
 
 
-def resnet50_fused(process_group=None, channel_last=True, gemm_1x1=False, **kw) -> ResNet:
+def resnet50_fused(process_group=None, channel_last=True, gemm_1x1=False, stem_pool_fused=True, **kw) -> ResNet:
     """ResNet-50 whose BatchNorms are fused SyncBatchNorms (BN+ReLU and BN+add+ReLU in one pass),
     synchronised over ``process_group`` -- the 'amp O2 + SyncBatchNorm' benchmark model.
     ``gemm_1x1``: stride-1 1x1 convolutions run as GEMMs on the channels_last view."""
     global _GEMM_1X1
     from ..parallel import SyncBatchNorm
 
-    def norm(c, fuse_relu=False):
-        return SyncBatchNorm(c, process_group=process_group, channel_last=channel_last, fuse_relu=fuse_relu)
+    def norm(c, fuse_relu=False, fuse_maxpool=None):
+        return SyncBatchNorm(c, process_group=process_group, channel_last=channel_last, fuse_relu=fuse_relu,
+                             fuse_maxpool=fuse_maxpool)
 
     old, _GEMM_1X1 = _GEMM_1X1, gemm_1x1
     try:
-        return ResNet(Bottleneck, [3, 4, 6, 3], norm_layer=norm, fused=True, **kw)
+        return ResNet(Bottleneck, [3, 4, 6, 3], norm_layer=norm, fused=True, stem_pool_fused=stem_pool_fused, **kw)
     finally:
         _GEMM_1X1 = old
 

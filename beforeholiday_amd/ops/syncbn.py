@@ -97,6 +97,54 @@ def forward(x, z, scale, shift, relu, out_dtype=None, num_batches=None):
     return y.to(out_dtype or x.dtype)
 
 
+def _pool_out(n, k, s, p):
+    return (n + 2 * p - k) // s + 1
+
+
+def maxpool_forward(x, scale, shift, relu, kernel_size, stride, padding, want_idx=True, num_batches=None):
+    """Max pool (NHWC) of ``(relu)(x*scale + shift)`` (scale/shift may be None). Returns ``(y, idx)``:
+    ``idx`` holds the window offset ``kh*k + kw`` of each maximum as uint8 (None if not wanted);
+    increments ``num_batches`` if given."""
+    if x.is_cuda:
+        y, idx = _native().maxpool_forward(x, scale, shift, relu, kernel_size, stride, padding, want_idx,
+                                           num_batches)
+        return y, (idx if want_idx else None)
+    if num_batches is not None:
+        num_batches += 1
+    v = x.float()
+    if scale is not None:
+        v = v * _bcast(scale, x) + _bcast(shift, x)
+    if relu:
+        v = torch.relu(v)
+    y, flat = torch.nn.functional.max_pool2d(v, kernel_size, stride, padding, return_indices=True)
+    y = y.to(x.dtype).contiguous(memory_format=torch.channels_last)
+    if not want_idx:
+        return y, None
+    W = x.size(3)
+    OH, OW = y.shape[2], y.shape[3]
+    oh = torch.arange(OH, device=x.device).view(1, 1, OH, 1)
+    ow = torch.arange(OW, device=x.device).view(1, 1, 1, OW)
+    kh = flat // W - (oh * stride - padding)
+    kw = flat % W - (ow * stride - padding)
+    return y, (kh * kernel_size + kw).to(torch.uint8).contiguous(memory_format=torch.channels_last)
+
+
+def maxpool_backward(grad_output, idx, H, W, kernel_size, stride, padding):
+    """Gradient of :func:`maxpool_forward` w.r.t. its pooled input (pre-ReLU masking is the caller's)."""
+    if grad_output.is_cuda:
+        return _native().maxpool_backward(grad_output, idx, H, W, kernel_size, stride, padding)
+    N, C, OH, OW = grad_output.shape
+    off = idx.long()
+    oh = torch.arange(OH).view(1, 1, OH, 1)
+    ow = torch.arange(OW).view(1, 1, 1, OW)
+    ih = oh * stride - padding + off // kernel_size
+    iw = ow * stride - padding + off % kernel_size
+    flat = (ih * W + iw).reshape(N, C, -1)
+    gx = torch.zeros(N, C, H * W, dtype=torch.float32)
+    gx.scatter_add_(2, flat, grad_output.float().reshape(N, C, -1))
+    return gx.view(N, C, H, W).to(grad_output.dtype).contiguous(memory_format=torch.channels_last)
+
+
 def _ref_masked_dy(dy, x, z, scale, shift, relu):
     g = dy.float()
     if relu:

@@ -27,7 +27,7 @@ def _world(pg):
 class SyncBatchnormFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, input, z, weight, bias, running_mean, running_var, eps, momentum, process_group,
-                channel_last, fuse_relu, num_batches=None):
+                channel_last, fuse_relu, num_batches=None, pool=None):
         input = input.contiguous(memory_format=torch.channels_last) if (channel_last and input.dim() == 4) else input
         world = _world(process_group)
         if world > 1:
@@ -41,8 +41,13 @@ class SyncBatchnormFunction(torch.autograd.Function):
             mean, invstd, scale, shift, count = syncbn.stats_single(input, weight, bias, running_mean,
                                                                     running_var, momentum, eps, num_batches)
         # the normalisation kernel also bumps num_batches_tracked (no separate add kernel)
-        out = syncbn.forward(input, z, scale, shift, fuse_relu, None, num_batches)
-        ctx.save_for_backward(input, z, weight, mean, invstd, scale, shift, count)
+        if pool is not None:
+            # BN + ReLU + max pool in one pass: the normalised activation is never written
+            out, idx = syncbn.maxpool_forward(input, scale, shift, fuse_relu, *pool, True, num_batches)
+        else:
+            out, idx = syncbn.forward(input, z, scale, shift, fuse_relu, None, num_batches), None
+        ctx.save_for_backward(input, z, weight, mean, invstd, scale, shift, count, idx)
+        ctx.pool = pool
         ctx.process_group = process_group
         ctx.world = world
         ctx.fuse_relu = fuse_relu
@@ -51,7 +56,9 @@ class SyncBatchnormFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_output):
-        input, z, weight, mean, invstd, scale, shift, count = ctx.saved_tensors
+        input, z, weight, mean, invstd, scale, shift, count, idx = ctx.saved_tensors
+        if ctx.pool is not None:
+            grad_output = syncbn.maxpool_backward(grad_output, idx, input.size(2), input.size(3), *ctx.pool)
         need_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         sums, gw, gb = syncbn.backward_reduce(grad_output, input, z, mean, invstd, scale, shift, ctx.fuse_relu,
                                               weight, need_w)
@@ -63,7 +70,7 @@ class SyncBatchnormFunction(torch.autograd.Function):
                                                        scale, shift, ctx.fuse_relu,
                                                        ctx.has_z and ctx.needs_input_grad[1])
         return grad_input, grad_z, (gw if need_w else None), (gb if need_w else None), None, None, None, None, None, \
-            None, None, None
+            None, None, None, None
 
 
 class SyncBatchNorm(_BatchNorm):
@@ -71,17 +78,20 @@ class SyncBatchNorm(_BatchNorm):
 
     ``channel_last=True`` expects/keeps NHWC (channels_last) activations; ``fuse_relu=True`` applies
     ReLU after the optional residual input ``z`` (``forward(input, z=None)``).
+    ``fuse_maxpool=(kernel, stride, padding)`` additionally max-pools the (ReLU'd) output in the same
+    pass (the ResNet stem); the module then returns the pooled tensor.
     """
 
     warned = False
 
     def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True, track_running_stats=True,
-                 process_group=None, channel_last=False, fuse_relu=False):
+                 process_group=None, channel_last=False, fuse_relu=False, fuse_maxpool=None):
         super().__init__(num_features, eps=eps, momentum=momentum, affine=affine,
                          track_running_stats=track_running_stats)
         self.process_group = process_group
         self.channel_last = channel_last
         self.fuse_relu = fuse_relu
+        self.fuse_maxpool = tuple(fuse_maxpool) if fuse_maxpool is not None else None
 
     def _specify_process_group(self, process_group):
         self.process_group = process_group
@@ -93,15 +103,26 @@ class SyncBatchNorm(_BatchNorm):
         if input.dim() < 2:
             raise ValueError("expected at least 2D input (got {}D input)".format(input.dim()))
 
+    def _pool_ok(self, input, z):
+        return (self.fuse_maxpool is not None and z is None and input.dim() == 4 and input.size(1) % 8 == 0
+                and self.channel_last and input.is_contiguous(memory_format=torch.channels_last))
+
     def forward(self, input, z=None):
         self._check_input_dim(input)
+        if self.fuse_maxpool is not None and not self._pool_ok(input, z):
+            return F.max_pool2d(self._bn(input, z, None), *self.fuse_maxpool)
+        return self._bn(input, z, self.fuse_maxpool)
+
+    def _bn(self, input, z, pool):
         if not self.training and self.track_running_stats:
-            # inference: fold running stats into scale/shift, one fused pass (z / relu included)
+            # inference: fold running stats into scale/shift, one fused pass (z / relu / pool included)
             w = self.weight.float() if self.weight is not None else torch.ones_like(self.running_mean, dtype=torch.float32)
             b = self.bias.float() if self.bias is not None else torch.zeros_like(self.running_mean, dtype=torch.float32)
             invstd = torch.rsqrt(self.running_var.float() + self.eps)
             scale = (w * invstd).contiguous()
             shift = (b - self.running_mean.float() * scale).contiguous()
+            if pool is not None:
+                return syncbn.maxpool_forward(input, scale, shift, self.fuse_relu, *pool, False)[0]
             return syncbn.forward(input, z, scale, shift, self.fuse_relu)
         tracking = self.training and self.track_running_stats
         # momentum=None -> cumulative average, computed on the device from num_batches_tracked
@@ -110,4 +131,4 @@ class SyncBatchNorm(_BatchNorm):
         rv = self.running_var if tracking else None
         nbt = self.num_batches_tracked if tracking else None
         return SyncBatchnormFunction.apply(input, z, self.weight, self.bias, rm, rv, self.eps, exp_avg,
-                                           self.process_group, self.channel_last, self.fuse_relu, nbt)
+                                           self.process_group, self.channel_last, self.fuse_relu, nbt, pool)

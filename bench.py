@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo only to rehearse the "
                          "multi-rank code path, e.g. several ranks sharing one GPU)")
+    ap.add_argument("--stem", default="fused", choices=["fused", "unfused"],
+                    help="fused: bn1+ReLU+maxpool in one HIP pass; unfused: SyncBN+ReLU then torch max_pool2d")
     ap.add_argument("--conv1x1", default="miopen", choices=["miopen", "gemm"],
                     help="stride-1 1x1 convolutions: MIOpen, or GEMMs on the channels_last view")
     return ap.parse_args()
@@ -76,7 +78,8 @@ def main():
 
     require_native("bench")
     torch.manual_seed(1234 + rank)
-    model = (resnet50() if args.no_syncbn else resnet50_fused(channel_last=True, gemm_1x1=args.conv1x1 == "gemm")).cuda()
+    model = (resnet50() if args.no_syncbn else resnet50_fused(channel_last=True, gemm_1x1=args.conv1x1 == "gemm",
+                                                                   stem_pool_fused=args.stem == "fused")).cuda()
     model = model.to(memory_format=torch.channels_last)
     global_batch = args.batch * world
     if args.optimizer == "lamb":

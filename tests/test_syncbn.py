@@ -247,3 +247,68 @@ def _dist_syncbn_groups(rank, world):
 
 def test_syncbn_process_subgroups_gloo():
     run_distributed(_dist_syncbn_groups, 4)
+
+
+@pytest.mark.parametrize("device", devices())
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("shape,pool", [((4, 64, 18, 18), (3, 2, 1)), ((2, 16, 9, 7), (3, 2, 1)),
+                                        ((2, 32, 8, 8), (2, 2, 0)), ((3, 8, 11, 10), (3, 1, 1))])
+def test_bn_relu_maxpool_fused(device, dtype, shape, pool):
+    """ResNet stem: SyncBN(fuse_relu, fuse_maxpool) == max_pool2d(relu(batch_norm(x))) fwd + bwd."""
+    torch.manual_seed(7)
+    C = shape[1]
+    x = (torch.randn(shape, device=device) * 2 + 0.3).to(dtype).contiguous(memory_format=torch.channels_last)
+    bn = SyncBatchNorm(C, channel_last=True, fuse_relu=True, fuse_maxpool=pool).to(device)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.3, 0.3)
+    w, b = bn.weight.detach().clone(), bn.bias.detach().clone()
+    xs = x.clone().requires_grad_(True)
+    y = bn(xs)
+    xr = x.float().clone().requires_grad_(True)
+    yr = F.max_pool2d(_ref_bn(xr, w, b, relu=True), *pool)
+    tol = TOL[dtype]
+    torch.testing.assert_close(y.float(), yr, rtol=tol, atol=tol)
+    gy = torch.randn_like(yr)
+    y.backward(gy.to(dtype))
+    yr.backward(gy)
+    # ties between equal rounded values may route a gradient differently: compare in norm
+    err = (xs.grad.float() - xr.grad).norm() / xr.grad.norm()
+    assert err < (2e-3 if dtype == torch.float32 else 3e-2), float(err)
+    assert int(bn.num_batches_tracked) == 1
+    bn.eval()
+    ye = bn(x)
+    ref_e = F.max_pool2d(torch.relu(F.batch_norm(x.float(), bn.running_mean, bn.running_var, w, b, False)), *pool)
+    torch.testing.assert_close(ye.float(), ref_e, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("device", devices())
+def test_maxpool_ties_and_nan_match_torch(device):
+    """Exact argmax semantics: first maximum of the window wins, NaN propagates."""
+    x = torch.randint(0, 3, (2, 16, 9, 9), device=device).float().contiguous(memory_format=torch.channels_last)
+    x[0, 3, 4, 4] = float("nan")
+    from beforeholiday_amd.ops import syncbn
+    y, idx = syncbn.maxpool_forward(x, None, None, False, 3, 2, 1, True)
+    yr, _ = F.max_pool2d(x, 3, 2, 1, return_indices=True)
+    torch.testing.assert_close(y, yr, equal_nan=True)
+    gy = torch.randn_like(yr).contiguous(memory_format=torch.channels_last)
+    gx = syncbn.maxpool_backward(gy, idx, 9, 9, 3, 2, 1)
+    xr = x.clone().requires_grad_(True)
+    F.max_pool2d(xr, 3, 2, 1).backward(gy)
+    torch.testing.assert_close(gx, xr.grad)
+
+
+def test_fused_stem_resnet_matches_unfused_cpu():
+    from beforeholiday_amd.models import resnet18_like
+    from beforeholiday_amd.models.resnet import Bottleneck, ResNet
+
+    torch.manual_seed(0)
+    ref = resnet18_like(num_classes=10)
+
+    def norm(c, fuse_relu=False, fuse_maxpool=None):
+        return SyncBatchNorm(c, fuse_relu=fuse_relu, channel_last=True, fuse_maxpool=fuse_maxpool)
+
+    fused = ResNet(Bottleneck, [1, 1, 1, 1], num_classes=10, norm_layer=norm, fused=True, stem_pool_fused=True)
+    fused.load_state_dict(ref.state_dict())
+    x = torch.randn(2, 3, 32, 32).contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(fused(x), ref(x), rtol=1e-3, atol=3e-4)
