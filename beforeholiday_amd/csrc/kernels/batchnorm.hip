@@ -228,37 +228,58 @@ __global__ __launch_bounds__(64 * kFinLanes) void k_stats_finalize(int C, int sp
                                                            const float* __restrict__ pmean, const float* __restrict__ pm2,
                                                            const float* __restrict__ pn, float* __restrict__ out_local,
                                                            BNFinal fin, const Tw* w, const Tw* b, Tw* rmean, Tw* rvar) {
-  // 64 channels x kFinLanes split-lanes per block; each lane walks every kFinLanes-th split with 4
-  // independent loads in flight, then the lanes are merged through LDS (short latency chain).
+  // 64 channels x kFinLanes split-lanes per block. The split partials were written by workgroups on
+  // all 8 XCDs, so every load here is a cross-XCD miss (~1 us): the merge is written as plain sums
+  // about a common shift K (split 0's mean) -- S1 = sum n_s (m_s - K), S2 = sum m2_s + n_s (m_s - K)^2
+  // -- so a lane keeps 8 splits of loads in flight with no division in the chain (a sequential Chan
+  // merge serialised one latency round per 4 splits: 14 us per layer at 1024 splits).
   __shared__ float sh[3][kFinLanes][64];
   const int cl = threadIdx.x & 63, lane = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
-  Welford acc{0.f, 0.f, 0.f};
+  float N = 0.f, S1 = 0.f, S2 = 0.f, K = 0.f;
   if (c < C) {
+    K = pmean[c];
     int s = lane;
-    for (; s + 3 * kFinLanes < splits; s += 4 * kFinLanes) {
-      float n[4], m[4], q[4];
+    for (; s + 7 * kFinLanes < splits; s += 8 * kFinLanes) {
+      float n[8], m[8], q[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         const int ss = s + kFinLanes * u;
         n[u] = per_channel_n ? pn[(int64_t)ss * C + c] : pn[ss];
         m[u] = pmean[(int64_t)ss * C + c];
         q[u] = pm2[(int64_t)ss * C + c];
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc = welford_merge(acc, Welford{n[u], m[u], q[u]});
+      for (int u = 0; u < 8; ++u) {
+        const float d = m[u] - K;
+        N += n[u];
+        S1 = fmaf(n[u], d, S1);
+        S2 += fmaf(n[u] * d, d, q[u]);
+      }
     }
     for (; s < splits; s += kFinLanes) {
       const float n = per_channel_n ? pn[(int64_t)s * C + c] : pn[s];
-      acc = welford_merge(acc, Welford{n, pmean[(int64_t)s * C + c], pm2[(int64_t)s * C + c]});
+      const float d = pmean[(int64_t)s * C + c] - K;
+      N += n;
+      S1 = fmaf(n, d, S1);
+      S2 += fmaf(n * d, d, pm2[(int64_t)s * C + c]);
     }
   }
-  sh[0][lane][cl] = acc.n;
-  sh[1][lane][cl] = acc.mean;
-  sh[2][lane][cl] = acc.m2;
+  sh[0][lane][cl] = N;
+  sh[1][lane][cl] = S1;
+  sh[2][lane][cl] = S2;
   __syncthreads();
   if (lane != 0 || c >= C) return;
-  for (int l = 1; l < kFinLanes; ++l) acc = welford_merge(acc, Welford{sh[0][l][cl], sh[1][l][cl], sh[2][l][cl]});
+  for (int l = 1; l < kFinLanes; ++l) {
+    N += sh[0][l][cl];
+    S1 += sh[1][l][cl];
+    S2 += sh[2][l][cl];
+  }
+  Welford acc;
+  acc.n = N;
+  const float dm = N > 0.f ? S1 / N : 0.f;
+  acc.mean = K + dm;
+  acc.m2 = fmaxf(S2 - S1 * dm, 0.f);
   const float var_b = acc.n > 0.f ? acc.m2 / acc.n : 0.f;
   if (out_local) {
     // all_gather layout of the reference: [mean(C), var_biased(C), count(1)]
@@ -559,15 +580,15 @@ __global__ __launch_bounds__(64 * kFinLanes) void k_bwd_reduce_finalize(int C, i
   float a = 0.f, b = 0.f;
   if (c < C) {
     int s = lane;
-    for (; s + 3 * kFinLanes < splits; s += 4 * kFinLanes) {
-      float x0[4], x1[4];
+    for (; s + 7 * kFinLanes < splits; s += 8 * kFinLanes) {
+      float x0[8], x1[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         x0[u] = p_dy[(int64_t)(s + kFinLanes * u) * C + c];
         x1[u] = p_dyx[(int64_t)(s + kFinLanes * u) * C + c];
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         a += x0[u];
         b += x1[u];
       }
