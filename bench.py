@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo only to rehearse the "
                          "multi-rank code path, e.g. several ranks sharing one GPU)")
+    ap.add_argument("--bn-group", default="separate", choices=["separate", "world"],
+                    help="separate: SyncBN stats use their own communicator (all ranks), so a BN all_reduce "
+                         "never queues behind a DDP gradient bucket on the same RCCL stream")
     ap.add_argument("--stem", default="fused", choices=["fused", "unfused"],
                     help="fused: bn1+ReLU+maxpool in one HIP pass; unfused: SyncBN+ReLU then torch max_pool2d")
     ap.add_argument("--conv1x1", default="miopen", choices=["miopen", "gemm"],
@@ -78,7 +81,9 @@ def main():
 
     require_native("bench")
     torch.manual_seed(1234 + rank)
-    model = (resnet50() if args.no_syncbn else resnet50_fused(channel_last=True, gemm_1x1=args.conv1x1 == "gemm",
+    bn_group = dist.new_group(list(range(world))) if (world > 1 and args.bn_group == "separate") else None
+    model = (resnet50() if args.no_syncbn else resnet50_fused(process_group=bn_group, channel_last=True,
+                                                                   gemm_1x1=args.conv1x1 == "gemm",
                                                                    stem_pool_fused=args.stem == "fused")).cuda()
     model = model.to(memory_format=torch.channels_last)
     global_batch = args.batch * world
