@@ -184,11 +184,45 @@ at::Tensor forward(at::Tensor x_in, c10::optional<at::Tensor> z, at::Tensor scal
   return y;
 }
 
+// true when the 1-bit ReLU mask path applies (NHWC rows x C with C % 8 == 0)
+bool mask_ok(const at::Tensor& x) {
+  if (!x.is_cuda()) return false;
+  Layout L = layout_of(x);
+  return L.s.channels_last && L.s.C % 8 == 0;
+}
+
+// forward that also returns the ReLU mask as uint8 [rows, C/8] (bit k: channel 8j+k > 0), so the
+// backward of BN + add + ReLU does not keep reading the residual input z
+std::vector<at::Tensor> forward_mask(at::Tensor x_in, c10::optional<at::Tensor> z, at::Tensor scale, at::Tensor shift,
+                                     c10::optional<at::Tensor> num_batches) {
+  check_cuda(x_in, "input");
+  Layout L = layout_of(x_in);
+  TORCH_CHECK(L.s.channels_last && L.s.C % 8 == 0, "forward_mask: needs channels_last with C % 8 == 0");
+  at::Tensor zt;
+  if (z.has_value() && z->defined()) zt = like(*z, L.x);
+  auto y = at::empty_like(L.x);
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && shift.scalar_type() == at::kFloat && scale.numel() == L.s.C,
+              "scale/shift must be fp32 [C]");
+  auto mask = at::empty({L.s.outer, (int64_t)(L.s.C / 8)}, L.x.options().dtype(at::kByte).memory_format(at::MemoryFormat::Contiguous));
+  bh::bn_forward(L.s, dtype_code(L.x.scalar_type()), L.x.data_ptr(), zt.defined() ? dtype_code(zt.scalar_type()) : -1,
+                 zt.defined() ? zt.data_ptr() : nullptr, dtype_code(y.scalar_type()), y.data_ptr(),
+                 scale.contiguous().data_ptr<float>(), shift.contiguous().data_ptr<float>(), true,
+                 counter_ptr(num_batches), stream_for(L.x), mask.data_ptr<uint8_t>());
+  return {y, mask};
+}
+
+const uint8_t* mask_ptr(const c10::optional<at::Tensor>& mask, const Layout& L) {
+  if (!(mask.has_value() && mask->defined())) return nullptr;
+  TORCH_CHECK(mask->scalar_type() == at::kByte && mask->is_contiguous() && L.s.channels_last && L.s.C % 8 == 0 &&
+                  mask->numel() == L.s.outer * (L.s.C / 8), "relu mask must be uint8 [rows, C/8] from forward_mask");
+  return mask->data_ptr<uint8_t>();
+}
+
 // returns (sums[2C], grad_weight, grad_bias) -- grads in weight dtype (undefined if weight undefined)
 std::vector<at::Tensor> backward_reduce(at::Tensor dy_in, at::Tensor x_in, c10::optional<at::Tensor> z,
                                         at::Tensor mean, at::Tensor invstd, c10::optional<at::Tensor> scale,
                                         c10::optional<at::Tensor> shift, bool relu, c10::optional<at::Tensor> weight,
-                                        bool need_weight_grads) {
+                                        bool need_weight_grads, c10::optional<at::Tensor> mask) {
   check_cuda(x_in, "input");
   Layout L = layout_of(x_in);
   at::Tensor dy = like(dy_in, L.x);
@@ -210,7 +244,7 @@ std::vector<at::Tensor> backward_reduce(at::Tensor dy_in, at::Tensor x_in, c10::
                          zt.defined() ? dtype_code(zt.scalar_type()) : -1, zt.defined() ? zt.data_ptr() : nullptr,
                          mean.data_ptr<float>(), relu ? scale->data_ptr<float>() : nullptr,
                          relu ? shift->data_ptr<float>() : nullptr, relu, splits, part.data_ptr<float>(),
-                         part.data_ptr<float>() + (int64_t)splits * C, st);
+                         part.data_ptr<float>() + (int64_t)splits * C, st, relu ? mask_ptr(mask, L) : nullptr);
   bh::bn_backward_reduce_finalize(C, splits, part.data_ptr<float>(), part.data_ptr<float>() + (int64_t)splits * C,
                                   invstd.data_ptr<float>(), sums.data_ptr<float>(),
                                   gw.defined() ? dtype_code(gw.scalar_type()) : bh::kF32,
@@ -222,7 +256,8 @@ std::vector<at::Tensor> backward_reduce(at::Tensor dy_in, at::Tensor x_in, c10::
 std::vector<at::Tensor> backward_dgrad(at::Tensor dy_in, at::Tensor x_in, c10::optional<at::Tensor> z,
                                        at::Tensor mean, at::Tensor invstd, c10::optional<at::Tensor> weight,
                                        at::Tensor sums, at::Tensor count, c10::optional<at::Tensor> scale,
-                                       c10::optional<at::Tensor> shift, bool relu, bool need_dz) {
+                                       c10::optional<at::Tensor> shift, bool relu, bool need_dz,
+                                       c10::optional<at::Tensor> mask) {
   check_cuda(x_in, "input");
   Layout L = layout_of(x_in);
   at::Tensor dy = like(dy_in, L.x);
@@ -238,7 +273,8 @@ std::vector<at::Tensor> backward_dgrad(at::Tensor dy_in, at::Tensor x_in, c10::o
                         zt.defined() ? zt.data_ptr() : nullptr, mean.data_ptr<float>(), invstd.data_ptr<float>(),
                         wcode(weight), wptr(weight), sums.data_ptr<float>(), count.data_ptr<float>(),
                         relu ? scale->data_ptr<float>() : nullptr, relu ? shift->data_ptr<float>() : nullptr, relu,
-                        dx.data_ptr(), dz.defined() ? dz.data_ptr() : nullptr, stream_for(L.x));
+                        dx.data_ptr(), dz.defined() ? dz.data_ptr() : nullptr, stream_for(L.x),
+                        relu ? mask_ptr(mask, L) : nullptr);
   return {dx, dz};
 }
 
@@ -307,10 +343,13 @@ void register_syncbn(pybind11::module_& root) {
         py::arg("out_dtype") = py::none(), py::arg("num_batches") = py::none());
   m.def("backward_reduce", &backward_reduce, py::arg("dy"), py::arg("x"), py::arg("z"), py::arg("mean"),
         py::arg("invstd"), py::arg("scale"), py::arg("shift"), py::arg("relu"), py::arg("weight"),
-        py::arg("need_weight_grads"));
+        py::arg("need_weight_grads"), py::arg("mask") = py::none());
   m.def("backward_dgrad", &backward_dgrad, py::arg("dy"), py::arg("x"), py::arg("z"), py::arg("mean"),
         py::arg("invstd"), py::arg("weight"), py::arg("sums"), py::arg("count"), py::arg("scale"), py::arg("shift"),
-        py::arg("relu"), py::arg("need_dz"));
+        py::arg("relu"), py::arg("need_dz"), py::arg("mask") = py::none());
+  m.def("forward_mask", &forward_mask, py::arg("x"), py::arg("z"), py::arg("scale"), py::arg("shift"),
+        py::arg("num_batches") = py::none(), "fused BN + (z) + ReLU that also returns the uint8 [rows, C/8] ReLU bit mask");
+  m.def("mask_ok", &mask_ok);
   m.def("maxpool_forward", &maxpool_forward, py::arg("x"), py::arg("scale"), py::arg("shift"), py::arg("relu"),
         py::arg("kernel_size"), py::arg("stride"), py::arg("padding"), py::arg("want_idx"),
         py::arg("num_batches") = py::none(),

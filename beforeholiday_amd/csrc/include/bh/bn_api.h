@@ -43,11 +43,12 @@ void bn_merge_ranks(int W, int C, const float* gathered, const BNFinal& fin, int
                     const void* b, void* rmean, void* rvar, float* var_unbiased, hipStream_t st);
 // y = x*scale + shift (+z) (relu); dt_z = -1 when z is null
 void bn_forward(const BNShape& s, int dt_x, const void* x, int dt_z, const void* z, int dt_y, void* y,
-                const float* scale, const float* shift, bool relu, int64_t* counter, hipStream_t st);
+                const float* scale, const float* shift, bool relu, int64_t* counter, hipStream_t st,
+                uint8_t* mbits = nullptr);  // mbits: optional [rows][C/8] ReLU bit mask (NHWC, C % 8 == 0)
 // partial sums of dy' and dy'*(x-mean); dy' = dy masked by (x*scale+shift(+z) > 0) when relu
 void bn_backward_reduce(const BNShape& s, int dt, const void* dy, const void* x, int dt_z, const void* z,
                         const float* mean, const float* scale, const float* shift, bool relu, int splits,
-                        float* p_dy, float* p_dyx, hipStream_t st);
+                        float* p_dy, float* p_dyx, hipStream_t st, const uint8_t* mbits = nullptr);
 // sums[2C] = (sum_dy, sum_dy_xmu); grad_w = sum_dy_xmu*invstd; grad_b = sum_dy (may be null)
 void bn_backward_reduce_finalize(int C, int splits, const float* p_dy, const float* p_dyx, const float* invstd,
                                  float* sums, int dt_w, void* gw, void* gb, hipStream_t st);
@@ -55,6 +56,6 @@ void bn_backward_reduce_finalize(int C, int splits, const float* p_dy, const flo
 void bn_backward_dgrad(const BNShape& s, int dt, const void* dy, const void* x, int dt_z, const void* z,
                        const float* mean, const float* invstd, int dt_w, const void* w, const float* sums,
                        const float* count, const float* scale, const float* shift, bool relu, void* dx, void* dz,
-                       hipStream_t st);
+                       hipStream_t st, const uint8_t* mbits = nullptr);
 
 }  // namespace bh

@@ -349,8 +349,11 @@ template <typename T, typename Tz, typename Ty>
 __global__ __launch_bounds__(kBlock) void k_fwd_nhwc(const T* __restrict__ x, const Tz* __restrict__ z,
                                                      Ty* __restrict__ y, const float* __restrict__ scale,
                                                      const float* __restrict__ shift, int64_t M, int C, int cvb, int R,
-                                                     int64_t rows_per_split, bool relu, int64_t* counter) {
-  // thread owns 8 channels (scale/shift in registers for its whole row range), rows strided by R
+                                                     int64_t rows_per_split, bool relu, int64_t* counter,
+                                                     uint8_t* __restrict__ mbits) {
+  // thread owns 8 channels (scale/shift in registers for its whole row range), rows strided by R.
+  // mbits (relu only): bit k of byte [row][c0/8] = (x*scale+shift+z > 0) for channel c0+k, so the
+  // backward never re-reads the residual input z just to rebuild the ReLU mask (1 bit vs 16).
   if (counter && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *counter += 1;
   const int v = threadIdx.x % cvb, r = threadIdx.x / cvb;
   const int c0 = (blockIdx.x * cvb + v) * 8;
@@ -360,14 +363,18 @@ __global__ __launch_bounds__(kBlock) void k_fwd_nhwc(const T* __restrict__ x, co
   float sc[8], sh[8];
   VecIO<float>::load(scale + c0, sc);
   VecIO<float>::load(shift + c0, sh);
-  auto apply = [&](float (&xv)[8], const float (&zv)[8]) {
+  const int C8 = C >> 3;
+  auto apply = [&](float (&xv)[8], const float (&zv)[8]) -> uint32_t {
+    uint32_t bits = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float o = fmaf(xv[k], sc[k], sh[k]);
       if (z) o += zv[k];
+      bits |= (o > 0.f ? 1u : 0u) << k;
       if (relu) o = fmaxf(o, 0.f);
       xv[k] = o;
     }
+    return bits;
   };
   int64_t row = row0 + r;
   for (; row + 3 * (int64_t)R < row1; row += 4 * (int64_t)R) {
@@ -380,8 +387,9 @@ __global__ __launch_bounds__(kBlock) void k_fwd_nhwc(const T* __restrict__ x, co
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      apply(xv[u], zv[u]);
+      const uint32_t bits = apply(xv[u], zv[u]);
       VecIO<Ty>::store(y + (row + u * (int64_t)R) * C + c0, xv[u]);
+      if (mbits) mbits[(row + u * (int64_t)R) * C8 + (c0 >> 3)] = (uint8_t)bits;
     }
   }
   for (; row < row1; row += R) {
@@ -389,8 +397,9 @@ __global__ __launch_bounds__(kBlock) void k_fwd_nhwc(const T* __restrict__ x, co
     float xv[8], zv[8];
     VecIO<T>::load(x + off, xv);
     if (z) VecIO<Tz>::load(z + off, zv);
-    apply(xv, zv);
+    const uint32_t bits = apply(xv, zv);
     VecIO<Ty>::store(y + off, xv);
+    if (mbits) mbits[row * C8 + (c0 >> 3)] = (uint8_t)bits;
   }
 }
 
@@ -439,7 +448,9 @@ __global__ __launch_bounds__(kBlock) void k_bwd_reduce_nhwc(const T* __restrict_
                                                             const float* __restrict__ scale, const float* __restrict__ shift,
                                                             bool relu, int64_t M, int C, int cvb, int R,
                                                             int64_t rows_per_split, float* __restrict__ p_dy,
-                                                            float* __restrict__ p_dyx) {
+                                                            float* __restrict__ p_dyx,
+                                                            const uint8_t* __restrict__ mbits) {
+  // mbits: ReLU mask saved by the forward (z is then not read at all)
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x;
   const int v = tid % cvb;
@@ -458,12 +469,17 @@ __global__ __launch_bounds__(kBlock) void k_bwd_reduce_nhwc(const T* __restrict_
       VecIO<float>::load(scale + c0, sc);
       VecIO<float>::load(shift + c0, sh);
     }
+    const int C8 = C >> 3;
     // 4 rows of dy / x (/ z) loads in flight per lane before any arithmetic
-    auto body = [&](const float (&gi)[8], const float (&xv)[8], const float (&zv)[8]) {
+    auto body = [&](const float (&gi)[8], const float (&xv)[8], const float (&zv)[8], uint32_t bits) {
       float g[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) g[k] = gi[k];
-      if (relu) {
+      if (mbits) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (!((bits >> k) & 1u)) g[k] = 0.f;
+      } else if (relu) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           float o = fmaf(xv[k], sc[k], sh[k]);
@@ -477,19 +493,21 @@ __global__ __launch_bounds__(kBlock) void k_bwd_reduce_nhwc(const T* __restrict_
         sdx[k] = fmaf(g[k], xv[k] - mu[k], sdx[k]);
       }
     };
-    const bool use_z = relu && z;
+    const bool use_z = relu && z && !mbits;
     int64_t row = row0 + r;
     for (; row + 3 * (int64_t)R < row1; row += 4 * (int64_t)R) {
       float g[4][8], xv[4][8], zv[4][8];
+      uint32_t bits[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t off = (row + u * (int64_t)R) * C + c0;
         VecIO<T>::load(dy + off, g[u]);
         VecIO<T>::load(x + off, xv[u]);
         if (use_z) VecIO<Tz>::load(z + off, zv[u]);
+        if (mbits) bits[u] = mbits[(row + u * (int64_t)R) * C8 + (c0 >> 3)];
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) body(g[u], xv[u], zv[u]);
+      for (int u = 0; u < 4; ++u) body(g[u], xv[u], zv[u], bits[u]);
     }
     for (; row < row1; row += R) {
       const int64_t off = row * C + c0;
@@ -497,7 +515,7 @@ __global__ __launch_bounds__(kBlock) void k_bwd_reduce_nhwc(const T* __restrict_
       VecIO<T>::load(dy + off, g);
       VecIO<T>::load(x + off, xv);
       if (use_z) VecIO<Tz>::load(z + off, zv);
-      body(g, xv, zv);
+      body(g, xv, zv, mbits ? (uint32_t)mbits[row * C8 + (c0 >> 3)] : 0u);
     }
   }
   float* s_a = smem;
@@ -624,7 +642,8 @@ __global__ __launch_bounds__(kBlock) void k_dgrad_nhwc(const T* __restrict__ dy,
                                                        const float* __restrict__ sums, const float* __restrict__ count,
                                                        const float* __restrict__ scale, const float* __restrict__ shift,
                                                        bool relu, T* __restrict__ dx, Tz* __restrict__ dz, int64_t M,
-                                                       int C, int cvb, int R, int64_t rows_per_split) {
+                                                       int C, int cvb, int R, int64_t rows_per_split,
+                                                       const uint8_t* __restrict__ mbits) {
   // dx = dy'*A + x*B + D with per-channel A, B, D computed once per thread (8 channels)
   const int v = threadIdx.x % cvb, r = threadIdx.x / cvb;
   const int c0 = (blockIdx.x * cvb + v) * 8;
@@ -655,9 +674,14 @@ __global__ __launch_bounds__(kBlock) void k_dgrad_nhwc(const T* __restrict__ dy,
     VecIO<float>::load(scale + c0, sc);
     VecIO<float>::load(shift + c0, sh);
   }
-  const bool use_z = relu && z;
-  auto apply = [&](int64_t off, float (&g)[8], float (&xv)[8], const float (&zv)[8]) {
-    if (relu) {
+  const bool use_z = relu && z && !mbits;
+  const int C8 = C >> 3;
+  auto apply = [&](int64_t off, float (&g)[8], float (&xv)[8], const float (&zv)[8], uint32_t bits) {
+    if (mbits) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (!((bits >> k) & 1u)) g[k] = 0.f;
+    } else if (relu) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float o = fmaf(xv[k], sc[k], sh[k]);
@@ -674,15 +698,17 @@ __global__ __launch_bounds__(kBlock) void k_dgrad_nhwc(const T* __restrict__ dy,
   int64_t row = row0 + r;
   for (; row + (int64_t)R < row1; row += 2 * (int64_t)R) {
     float g[2][8], xv[2][8], zv[2][8];
+    uint32_t bits[2] = {0u, 0u};
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int64_t off = (row + u * (int64_t)R) * C + c0;
       VecIO<T>::load(dy + off, g[u]);
       VecIO<T>::load(x + off, xv[u]);
       if (use_z) VecIO<Tz>::load(z + off, zv[u]);
+      if (mbits) bits[u] = mbits[(row + u * (int64_t)R) * C8 + (c0 >> 3)];
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) apply((row + u * (int64_t)R) * C + c0, g[u], xv[u], zv[u]);
+    for (int u = 0; u < 2; ++u) apply((row + u * (int64_t)R) * C + c0, g[u], xv[u], zv[u], bits[u]);
   }
   for (; row < row1; row += R) {
     const int64_t off = row * C + c0;
@@ -690,7 +716,7 @@ __global__ __launch_bounds__(kBlock) void k_dgrad_nhwc(const T* __restrict__ dy,
     VecIO<T>::load(dy + off, g);
     VecIO<T>::load(x + off, xv);
     if (use_z) VecIO<Tz>::load(z + off, zv);
-    apply(off, g, xv, zv);
+    apply(off, g, xv, zv, mbits ? (uint32_t)mbits[row * C8 + (c0 >> 3)] : 0u);
   }
 }
 
@@ -830,7 +856,8 @@ void bn_merge_ranks(int W, int C, const float* gathered, const BNFinal& fin, int
 }
 
 void bn_forward(const BNShape& s, int dt_x, const void* x, int dt_z, const void* z, int dt_y, void* y,
-                const float* scale, const float* shift, bool relu, int64_t* counter, hipStream_t st) {
+                const float* scale, const float* shift, bool relu, int64_t* counter, hipStream_t st,
+                uint8_t* mbits) {
   const int64_t total = s.outer * s.C * s.inner;
   if (total == 0) return;
   if (dt_z < 0) dt_z = dt_x;
@@ -840,8 +867,9 @@ void bn_forward(const BNShape& s, int dt_x, const void* x, int dt_z, const void*
     const int64_t rps = (s.outer + splits - 1) / splits;
     BN_DISPATCH(dt_x, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_y, Ty,
         hipLaunchKernelGGL((k_fwd_nhwc<T, Tz, Ty>), dim3(g.gx, splits), dim3(kBlock), 0, st, (const T*)x, (const Tz*)z,
-                           (Ty*)y, scale, shift, s.outer, s.C, g.cvb, g.R, rps, relu, counter))));
+                           (Ty*)y, scale, shift, s.outer, s.C, g.cvb, g.R, rps, relu, counter, mbits))));
   } else {
+    if (mbits) throw std::runtime_error("bn_forward: the ReLU bit mask needs channels_last with C % 8 == 0");
     const int64_t inner = s.channels_last ? 1 : s.inner;
     const int grid = grid_for(inner % 8 == 0 ? total / 8 : total);
     BN_DISPATCH(dt_x, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_y, Ty,
@@ -853,7 +881,7 @@ void bn_forward(const BNShape& s, int dt_x, const void* x, int dt_z, const void*
 
 void bn_backward_reduce(const BNShape& s, int dt, const void* dy, const void* x, int dt_z, const void* z,
                         const float* mean, const float* scale, const float* shift, bool relu, int splits, float* p_dy,
-                        float* p_dyx, hipStream_t st) {
+                        float* p_dyx, hipStream_t st, const uint8_t* mbits) {
   if (dt_z < 0) dt_z = dt;
   if (s.channels_last && s.C % 8 == 0) {
     const NhwcGeom g = nhwc_geom(s.C);
@@ -862,8 +890,9 @@ void bn_backward_reduce(const BNShape& s, int dt, const void* dy, const void* x,
     BN_DISPATCH(dt, T, BN_DISPATCH(dt_z, Tz,
         hipLaunchKernelGGL((k_bwd_reduce_nhwc<T, Tz>), dim3(g.gx, splits), dim3(kBlock), shm, st, (const T*)dy,
                            (const T*)x, (const Tz*)z, mean, scale, shift, relu, s.outer, s.C, g.cvb, g.R,
-                           rows_per_split, p_dy, p_dyx)));
+                           rows_per_split, p_dy, p_dyx, mbits)));
   } else {
+    if (mbits) throw std::runtime_error("bn_backward_reduce: the ReLU bit mask needs channels_last with C % 8 == 0");
     // NCHW (or channels_last with C % 8 != 0 viewed as N=M, HW=1 per channel)
     const int64_t N = s.channels_last ? 1 : s.outer;
     const int64_t HW = s.channels_last ? s.outer : s.inner;
@@ -889,7 +918,7 @@ void bn_backward_reduce_finalize(int C, int splits, const float* p_dy, const flo
 void bn_backward_dgrad(const BNShape& s, int dt, const void* dy, const void* x, int dt_z, const void* z,
                        const float* mean, const float* invstd, int dt_w, const void* w, const float* sums,
                        const float* count, const float* scale, const float* shift, bool relu, void* dx, void* dz,
-                       hipStream_t st) {
+                       hipStream_t st, const uint8_t* mbits) {
   const int64_t total = s.outer * s.C * s.inner;
   if (total == 0) return;
   if (dt_z < 0) dt_z = dt;
@@ -900,8 +929,9 @@ void bn_backward_dgrad(const BNShape& s, int dt, const void* dy, const void* x, 
     BN_DISPATCH(dt, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_w, Tw,
         hipLaunchKernelGGL((k_dgrad_nhwc<T, Tz, Tw>), dim3(g.gx, splits), dim3(kBlock), 0, st, (const T*)dy,
                            (const T*)x, (const Tz*)z, mean, invstd, (const Tw*)w, sums, count, scale, shift, relu,
-                           (T*)dx, (Tz*)dz, s.outer, s.C, g.cvb, g.R, rps))));
+                           (T*)dx, (Tz*)dz, s.outer, s.C, g.cvb, g.R, rps, mbits))));
   } else {
+    if (mbits) throw std::runtime_error("bn_backward_dgrad: the ReLU bit mask needs channels_last with C % 8 == 0");
     const int64_t inner = s.channels_last ? 1 : s.inner;
     const int grid = grid_for(total);
     BN_DISPATCH(dt, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_w, Tw,

@@ -97,6 +97,17 @@ def forward(x, z, scale, shift, relu, out_dtype=None, num_batches=None):
     return y.to(out_dtype or x.dtype)
 
 
+def mask_ok(x, z):
+    """Whether :func:`forward_mask` applies: a GPU NHWC (C % 8 == 0) input with a same-dtype residual."""
+    return x.is_cuda and z is not None and z.dtype == x.dtype and z.shape == x.shape and _native().mask_ok(x)
+
+
+def forward_mask(x, z, scale, shift, num_batches=None):
+    """Fused ``relu(x*scale + shift + z)`` that also returns the ReLU mask packed 8 channels per byte
+    (uint8 ``[rows, C/8]``); backward then reads 1 bit per element instead of the residual ``z``."""
+    return _native().forward_mask(x, z, scale, shift, num_batches)
+
+
 def _pool_out(n, k, s, p):
     return (n + 2 * p - k) // s + 1
 
@@ -155,9 +166,9 @@ def _ref_masked_dy(dy, x, z, scale, shift, relu):
     return g
 
 
-def backward_reduce(dy, x, z, mean, invstd, scale, shift, relu, weight, need_weight_grads):
+def backward_reduce(dy, x, z, mean, invstd, scale, shift, relu, weight, need_weight_grads, mask=None):
     if x.is_cuda:
-        return _native().backward_reduce(dy, x, z, mean, invstd, scale, shift, relu, weight, need_weight_grads)
+        return _native().backward_reduce(dy, x, z, mean, invstd, scale, shift, relu, weight, need_weight_grads, mask)
     g = _ref_masked_dy(dy, x, z, scale, shift, relu)
     dims = _reduce_dims(x)
     sum_dy = g.sum(dims)
@@ -169,9 +180,10 @@ def backward_reduce(dy, x, z, mean, invstd, scale, shift, relu, weight, need_wei
     return [torch.cat([sum_dy, sum_dy_xmu]), gw, gb]
 
 
-def backward_dgrad(dy, x, z, mean, invstd, weight, sums, count, scale, shift, relu, need_dz):
+def backward_dgrad(dy, x, z, mean, invstd, weight, sums, count, scale, shift, relu, need_dz, mask=None):
     if x.is_cuda:
-        return _native().backward_dgrad(dy, x, z, mean, invstd, weight, sums, count, scale, shift, relu, need_dz)
+        return _native().backward_dgrad(dy, x, z, mean, invstd, weight, sums, count, scale, shift, relu, need_dz,
+                                        mask)
     C = x.size(1)
     g = _ref_masked_dy(dy, x, z, scale, shift, relu)
     n = count.float().reshape(-1)[0]

@@ -5,7 +5,8 @@ Training forward: local Welford statistics (HIP kernel) -> all_gather of the [me
 count] rows over the process group -> rank merge + running-stat update + per-channel scale/shift
 (one tiny kernel) -> a single fused  y = x*scale + shift (+ z) (ReLU)  pass. Backward: one reduce
 kernel (ReLU mask recomputed from x, no masked-dy tensor), all_reduce of [sum_dy, sum_dy_xmu],
-one dgrad kernel that also emits dz for the fused residual branch. With a single rank the
+one dgrad kernel that also emits dz for the fused residual branch (BN + add + ReLU saves a 1-bit
+ReLU mask in the forward, so neither backward pass reads z). With a single rank the
 collectives are skipped and the merge is fused into the statistics finalize.
 """
 from __future__ import annotations
@@ -41,12 +42,17 @@ class SyncBatchnormFunction(torch.autograd.Function):
             mean, invstd, scale, shift, count = syncbn.stats_single(input, weight, bias, running_mean,
                                                                     running_var, momentum, eps, num_batches)
         # the normalisation kernel also bumps num_batches_tracked (no separate add kernel)
+        mask = None
         if pool is not None:
             # BN + ReLU + max pool in one pass: the normalised activation is never written
             out, idx = syncbn.maxpool_forward(input, scale, shift, fuse_relu, *pool, True, num_batches)
+        elif fuse_relu and syncbn.mask_ok(input, z):
+            # BN + add + ReLU: keep a 1-bit ReLU mask instead of re-reading z in both backward passes
+            (out, mask), idx = syncbn.forward_mask(input, z, scale, shift, num_batches), None
         else:
             out, idx = syncbn.forward(input, z, scale, shift, fuse_relu, None, num_batches), None
-        ctx.save_for_backward(input, z, weight, mean, invstd, scale, shift, count, idx)
+        ctx.save_for_backward(input, None if mask is not None else z, weight, mean, invstd, scale, shift, count, idx,
+                              mask)
         ctx.pool = pool
         ctx.process_group = process_group
         ctx.world = world
@@ -56,19 +62,19 @@ class SyncBatchnormFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_output):
-        input, z, weight, mean, invstd, scale, shift, count, idx = ctx.saved_tensors
+        input, z, weight, mean, invstd, scale, shift, count, idx, mask = ctx.saved_tensors
         if ctx.pool is not None:
             grad_output = syncbn.maxpool_backward(grad_output, idx, input.size(2), input.size(3), *ctx.pool)
         need_w = weight is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         sums, gw, gb = syncbn.backward_reduce(grad_output, input, z, mean, invstd, scale, shift, ctx.fuse_relu,
-                                              weight, need_w)
+                                              weight, need_w, mask)
         grad_input = grad_z = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             if ctx.world > 1:
                 dist.all_reduce(sums, group=ctx.process_group)
             grad_input, grad_z = syncbn.backward_dgrad(grad_output, input, z, mean, invstd, weight, sums, count,
                                                        scale, shift, ctx.fuse_relu,
-                                                       ctx.has_z and ctx.needs_input_grad[1])
+                                                       ctx.has_z and ctx.needs_input_grad[1], mask)
         return grad_input, grad_z, (gw if need_w else None), (gb if need_w else None), None, None, None, None, None, \
             None, None, None, None
 

@@ -25,6 +25,13 @@ def main():
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    # rocprofv3 >= ROCm 7 writes a rocpd SQLite database by default (``kernels`` view)
+    for f in glob.glob(os.path.join(d, "**", "*_results.db"), recursive=True):
+        import sqlite3
+
+        con = sqlite3.connect(f)
+        rows.extend((int(s), int(e), n) for s, e, n in con.execute("select start, end, name from kernels"))
+        con.close()
     rows.sort()
     marks = [i for i, r in enumerate(rows) if marker.search(r[2])]
     lines = []

@@ -312,3 +312,30 @@ def test_fused_stem_resnet_matches_unfused_cpu():
     fused.load_state_dict(ref.state_dict())
     x = torch.randn(2, 3, 32, 32).contiguous(memory_format=torch.channels_last)
     torch.testing.assert_close(fused(x), ref(x), rtol=1e-3, atol=3e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(4, 64, 9, 7), (3, 24, 5, 5), (64, 16)])
+def test_relu_bitmask_forward(shape):
+    """forward_mask packs (x*scale + shift + z > 0) 8 channels per byte, row-major [rows, C/8], and the
+    BN + add + ReLU autograd function takes that path (z is not saved for backward)."""
+    from beforeholiday_amd.ops import syncbn
+
+    torch.manual_seed(3)
+    C = shape[1]
+    x = torch.randn(shape, device="cuda", dtype=torch.float16)
+    z = torch.randn(shape, device="cuda", dtype=torch.float16)
+    if x.dim() == 4:
+        x = x.contiguous(memory_format=torch.channels_last)
+        z = z.contiguous(memory_format=torch.channels_last)
+    scale = torch.rand(C, device="cuda") + 0.5
+    shift = torch.randn(C, device="cuda") * 0.1
+    assert syncbn.mask_ok(x, z)
+    y, mask = syncbn.forward_mask(x, z, scale, shift)
+    view = (lambda t: t.permute(0, 2, 3, 1).reshape(-1, C)) if x.dim() == 4 else (lambda t: t)
+    pre = view(x).float() * scale + shift + view(z).float()
+    bits = (pre > 0).to(torch.int32).view(-1, C // 8, 8)
+    ref = (bits << torch.arange(8, device="cuda", dtype=torch.int32)).sum(-1).to(torch.uint8)
+    assert mask.shape == (pre.shape[0], C // 8) and mask.dtype == torch.uint8
+    torch.testing.assert_close(mask, ref, rtol=0, atol=0)
+    torch.testing.assert_close(view(y).float(), torch.relu(pre), rtol=4e-3, atol=4e-3)
