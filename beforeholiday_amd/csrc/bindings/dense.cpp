@@ -278,6 +278,10 @@ void register_dense(pybind11::module_& root) {
   fd.def("linear_gelu_linear_backward", &linear_gelu_linear_backward);
   fd.def("act_forward", &act_forward_py, py::arg("x"), py::arg("bias"), py::arg("act"));
   fd.def("act_backward", &act_backward_py, py::arg("dy"), py::arg("aux"), py::arg("act"), py::arg("want_bgrad"));
+  fd.def("bias_grad", [](at::Tensor dy) {
+    check_cuda(dy, "dy");
+    return bias_grad(dy.contiguous());
+  }, py::arg("dy"), "column sum of dy[..., N] over all leading dims (fp32 accumulation, dy dtype out)");
   auto mlp = root.def_submodule("mlp_cuda", "N-layer MLP");
   mlp.def("forward", &mlp_forward);
   mlp.def("backward", &mlp_backward);

@@ -267,4 +267,38 @@ struct Philox {
 
 BH_DEVICE bool is_finite(float x) { return __builtin_isfinite(x); }
 
+
+// Column sums of fp32 split partials part[slabs][N] -> out[N] (optionally scaled), for a block of
+// 64 columns x kColsumLanes split-lanes (blockDim 64 * kColsumLanes, grid ceil(N / 64)). Each lane
+// keeps 8 independent loads in flight; lanes merge through LDS. Replaces one-thread-per-column loops
+// that walk all slabs serially (latency-bound: 20-40 us for a 2 MB partial buffer).
+constexpr int kColsumLanes = 16;
+template <typename T>
+BH_DEVICE void colsum_partials_block(const float* __restrict__ part, int64_t slabs, int64_t N, T* __restrict__ out,
+                                     float (&sh)[kColsumLanes][64]) {
+  const int cl = threadIdx.x & 63, lane = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + cl;
+  float acc = 0.f;
+  if (c < N) {
+    int64_t s = lane;
+    for (; s + 7 * kColsumLanes < slabs; s += 8 * kColsumLanes) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(s + u * kColsumLanes) * N + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; s < slabs; s += kColsumLanes) acc += part[s * N + c];
+  }
+  sh[lane][cl] = acc;
+  __syncthreads();
+  if (lane == 0 && c < N && out) {
+    float t = 0.f;
+#pragma unroll
+    for (int l = 0; l < kColsumLanes; ++l) t += sh[l][cl];
+    out[c] = from_f<T>(t);
+  }
+  __syncthreads();
+}
+
 }  // namespace bh

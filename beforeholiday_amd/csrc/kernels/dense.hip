@@ -114,12 +114,10 @@ __global__ __launch_bounds__(256) void k_act_bwd(const T* __restrict__ dy, const
 }
 
 template <typename T>
-__global__ void k_colsum_finalize(const float* __restrict__ part, int splits, int N, T* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N) return;
-  float s = 0.f;
-  for (int j = 0; j < splits; ++j) s += part[(int64_t)j * N + c];
-  out[c] = from_f<T>(s);
+__global__ __launch_bounds__(64 * kColsumLanes) void k_colsum_finalize(const float* __restrict__ part, int splits, int N,
+                                                                        T* __restrict__ out) {
+  __shared__ float sh[kColsumLanes][64];
+  colsum_partials_block<T>(part, splits, N, out, sh);
 }
 
 }  // namespace
@@ -155,8 +153,8 @@ void dense_act_backward(int dt, const void* dy, const void* aux, void* dx, void*
                          (T*)dx, part, M, N, rps, act, vec);
       check_launch("dense_act_backward");
       if (bgrad) {
-        hipLaunchKernelGGL((k_colsum_finalize<T>), dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, part, splits,
-                           N, (T*)bgrad);
+        hipLaunchKernelGGL((k_colsum_finalize<T>), dim3((unsigned)((N + 63) / 64)), dim3(64 * kColsumLanes), 0, st,
+                           part, splits, N, (T*)bgrad);
         check_launch("dense_bgrad_finalize");
       });
 }

@@ -342,12 +342,10 @@ __global__ __launch_bounds__(C::kThreads, 1) void k_gemm_nt(Args p) {
 }
 
 template <typename T>
-__global__ void k_colsum(const float* __restrict__ part, int64_t slabs, int64_t N, T* __restrict__ out) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N) return;
-  float s = 0.f;
-  for (int64_t j = 0; j < slabs; ++j) s += part[j * N + c];
-  out[c] = from_f<T>(s);
+__global__ __launch_bounds__(64 * kColsumLanes) void k_colsum(const float* __restrict__ part, int64_t slabs, int64_t N,
+                                                               T* __restrict__ out) {
+  __shared__ float sh[kColsumLanes][64];
+  colsum_partials_block<T>(part, slabs, N, out, sh);
 }
 
 inline void check_launch(const char* what) {
@@ -421,10 +419,10 @@ void gemm_nt(int dt, const void* A, int64_t lda, const void* B, int64_t ldb, voi
 }
 
 void gemm_colsum_finalize(int dt, const float* part, int64_t slabs, int64_t N, void* out, hipStream_t st) {
-  const unsigned blocks = (unsigned)((N + 255) / 256);
+  const unsigned blocks = (unsigned)((N + 63) / 64);
   switch (dt) {
-    case kF16: hipLaunchKernelGGL(k_colsum<f16>, dim3(blocks), dim3(256), 0, st, part, slabs, N, (f16*)out); break;
-    case kBF16: hipLaunchKernelGGL(k_colsum<bf16>, dim3(blocks), dim3(256), 0, st, part, slabs, N, (bf16*)out); break;
+    case kF16: hipLaunchKernelGGL(k_colsum<f16>, dim3(blocks), dim3(64 * kColsumLanes), 0, st, part, slabs, N, (f16*)out); break;
+    case kBF16: hipLaunchKernelGGL(k_colsum<bf16>, dim3(blocks), dim3(64 * kColsumLanes), 0, st, part, slabs, N, (bf16*)out); break;
     default: throw std::runtime_error("gemm_colsum_finalize: fp16 / bf16 only");
   }
   check_launch("gemm_colsum_finalize");

@@ -269,12 +269,7 @@ __global__ __launch_bounds__(kBlock) void k_ln_wgrad_partials(const Tdy* __restr
       if (g) load8(g, c0, n2, vec, gv);
       if (b && !RMS) load8(b, c0, n2, vec, bv);
     }
-    for (int64_t row = row0 + r; row < row1; row += R) {
-      float dv[8], xv[8];
-      load8(dy + row * n2, c0, n2, vec, dv);
-      load8(xin + row * n2, c0, n2, vec, xv);
-      const float mean = (RMS || from_output) ? 0.f : mean_in[row];
-      const float invvar = from_output ? 0.f : invvar_in[row];
+    auto body = [&](const float (&dv)[8], const float (&xv)[8], float mean, float invvar) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float h;
@@ -288,6 +283,27 @@ __global__ __launch_bounds__(kBlock) void k_ln_wgrad_partials(const Tdy* __restr
         ag[k] = fmaf(dv[k], h, ag[k]);
         ab[k] += dv[k];
       }
+    };
+    // 4 rows of dy / x loads in flight per lane before any arithmetic
+    int64_t row = row0 + r;
+    for (; row + 3 * (int64_t)R < row1; row += 4 * (int64_t)R) {
+      float dv[4][8], xv[4][8], mu[4], iv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t rr = row + u * (int64_t)R;
+        load8(dy + rr * n2, c0, n2, vec, dv[u]);
+        load8(xin + rr * n2, c0, n2, vec, xv[u]);
+        mu[u] = (RMS || from_output) ? 0.f : mean_in[rr];
+        iv[u] = from_output ? 0.f : invvar_in[rr];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) body(dv[u], xv[u], mu[u], iv[u]);
+    }
+    for (; row < row1; row += R) {
+      float dv[8], xv[8];
+      load8(dy + row * n2, c0, n2, vec, dv);
+      load8(xin + row * n2, c0, n2, vec, xv);
+      body(dv, xv, (RMS || from_output) ? 0.f : mean_in[row], from_output ? 0.f : invvar_in[row]);
     }
   }
   float* sa = smem;
@@ -322,27 +338,12 @@ __global__ __launch_bounds__(kBlock) void k_ln_wgrad_partials(const Tdy* __restr
 }
 
 template <typename Tw>
-__global__ __launch_bounds__(kBlock) void k_ln_wgrad_finalize(int n2, int splits, const float* __restrict__ pg,
-                                                              const float* __restrict__ pb, Tw* __restrict__ gg,
-                                                              Tw* __restrict__ gb) {
-  __shared__ float sh[2][4][64];
-  const int cl = threadIdx.x & 63, lane = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  float a = 0.f, bsum = 0.f;
-  if (c < n2) {
-    for (int s = lane; s < splits; s += 4) {
-      a += pg[(int64_t)s * n2 + c];
-      bsum += pb[(int64_t)s * n2 + c];
-    }
-  }
-  sh[0][lane][cl] = a;
-  sh[1][lane][cl] = bsum;
-  __syncthreads();
-  if (lane != 0 || c >= n2) return;
-  a = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
-  bsum = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
-  if (gg) gg[c] = from_f<Tw>(a);
-  if (gb) gb[c] = from_f<Tw>(bsum);
+__global__ __launch_bounds__(64 * kColsumLanes) void k_ln_wgrad_finalize(int n2, int splits, const float* __restrict__ pg,
+                                                                          const float* __restrict__ pb,
+                                                                          Tw* __restrict__ gg, Tw* __restrict__ gb) {
+  __shared__ float sh[kColsumLanes][64];
+  colsum_partials_block<Tw>(pg, splits, n2, gg, sh);
+  colsum_partials_block<Tw>(pb, splits, n2, gb, sh);
 }
 
 // vectors per lane for the wave-per-row kernels; 0 selects the block-per-row kernel. The backward
@@ -449,8 +450,8 @@ void ln_backward_wgrad(int64_t n1, int n2, int dt_dy, const void* dy, int dt_x, 
       else hipLaunchKernelGGL((k_ln_wgrad_partials<T, Tw, Tdy, false>), dim3(gx, splits), dim3(kBlock), shm, st,
                               (const Tdy*)dy, (const T*)xin, mean, invvar, (const Tw*)gamma, (const Tw*)beta, n1, n2,
                               cvb, R, rps, from_output, vec, pg, pb);
-      hipLaunchKernelGGL((k_ln_wgrad_finalize<Tw>), dim3((n2 + 63) / 64), dim3(kBlock), 0, st, n2, splits, pg, pb,
-                         (Tw*)grad_gamma, (Tw*)grad_beta))));
+      hipLaunchKernelGGL((k_ln_wgrad_finalize<Tw>), dim3((n2 + 63) / 64), dim3(64 * kColsumLanes), 0, st, n2, splits,
+                         pg, pb, (Tw*)grad_gamma, (Tw*)grad_beta))));
   check_launch("ln_backward_wgrad");
 }
 

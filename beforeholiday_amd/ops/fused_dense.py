@@ -63,6 +63,14 @@ def act_backward(dy: torch.Tensor, aux: torch.Tensor, act: int, want_bgrad: bool
     return dx, (dx.reshape(-1, dx.size(-1)).float().sum(0).to(dx.dtype) if want_bgrad else None)
 
 
+def bias_grad(dy: torch.Tensor) -> torch.Tensor:
+    """Bias gradient: sum of ``dy`` over every leading dim (fp32 accumulation, ``dy``'s dtype).
+    GPU: one split-row partial-sum pass + a column-sum finalize (kernels/dense.hip)."""
+    if dy.is_cuda and dy.dtype in (torch.float16, torch.bfloat16, torch.float32) and dy.size(-1) > 0:
+        return _fd().bias_grad(dy)
+    return dy.reshape(-1, dy.size(-1)).float().sum(0).to(dy.dtype)
+
+
 def linear_bias_forward(input, weight, bias):
     if input.is_cuda:
         return _fd().linear_bias_forward(input, weight, bias)

@@ -136,3 +136,21 @@ def test_wgrad_gemm_accum(device, dtype):
         fd.wgrad_gemm_accum_fp16(x, dy, m16)
         prod = dy.reshape(-1, 40).float().t() @ x.reshape(-1, 24).float()
         torch.testing.assert_close(m16.float(), prod, rtol=5e-2, atol=5e-1)
+
+
+@pytest.mark.parametrize("device", devices())
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(8192, 1024), (3, 77, 40), (1000, 4096), (5, 8)])
+def test_bias_grad_colsum(device, dtype, shape):
+    """bias_grad == fp32 column sum over all leading dims (covers the split partial + finalize kernels)."""
+    if device == "cpu" and dtype != torch.float32:
+        pytest.skip("cpu reference path is exercised in fp32")
+    from beforeholiday_amd.ops.fused_dense import bias_grad
+
+    torch.manual_seed(0)
+    dy = torch.randn(shape, device=device).to(dtype)
+    ref = dy.float().reshape(-1, shape[-1]).sum(0)
+    out = bias_grad(dy)
+    assert out.dtype == dtype and out.shape == (shape[-1],)
+    tol = 1e-3 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol * max(1.0, shape[0] ** 0.5))
