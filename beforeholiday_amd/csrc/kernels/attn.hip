@@ -30,6 +30,7 @@
 #include "bh/device.h"
 
 #include <stdexcept>
+#include <type_traits>
 #include <string>
 
 namespace bh {
@@ -400,6 +401,24 @@ constexpr int kKB = 64;  // keys per block
 
 BH_DEVICE int skt_pad(int sk) { return (sk + kKB - 1) / kKB * kKB; }
 
+// XCD-aware (tile, head) of a flash workgroup on a (tiles, BH) grid. Workgroups are dispatched in
+// x-fastest order and dealt round-robin to the 8 XCDs (linear id % 8), so the natural mapping
+// spreads the tiles of one head over all 8 XCDs and every XCD's L2 misses on the same K / V
+// (or Q / dO) panels. This bijection keeps all tiles of a head on one XCD: the 8 XCDs each own
+// every 8th head. Falls back to the natural order when BH % 8 != 0.
+BH_DEVICE void flash_tile(int& tile, int& bh) {
+  const int nx = gridDim.x, ny = gridDim.y;
+  if (ny & 7) {
+    tile = blockIdx.x;
+    bh = blockIdx.y;
+    return;
+  }
+  const int id = blockIdx.x + blockIdx.y * nx;
+  const int slot = id >> 3;
+  tile = slot % nx;
+  bh = (slot / nx) * 8 + (id & 7);
+}
+
 // 64 rows x 128 B of a head operand: 2 x 16-byte chunks per thread
 struct RowRegs {
   i4v v[2];
@@ -427,6 +446,7 @@ constexpr int kMaskBytes = 64 * 64;
 struct MaskRegs {
   int4 t;  // one 16-byte piece per thread (tile row = tid/4, cols 16*(tid%4)) or the key vector
 };
+template <int MODE>
 BH_DEVICE void mask_load(MaskRegs& m, const AttnArgs& a, int b, int q0, int k0, int tid) {
   // one 16-byte vector load per thread when the piece is in bounds and aligned (every piece but the
   // key tail when sk % 16 == 0); the byte-wise tail path is taken by whole pieces, never per byte
@@ -434,10 +454,10 @@ BH_DEVICE void mask_load(MaskRegs& m, const AttnArgs& a, int b, int q0, int k0, 
   m.t = make_int4(0, 0, 0, 0);
   const uint8_t* m8 = reinterpret_cast<const uint8_t*>(a.mask);
   const bool aligned = (a.sk & 15) == 0;
-  if (a.mask_mode == 3 || a.mask_mode == 4) {
+  if (MODE == 3 || MODE == 4) {
     const int r = tid >> 2, c = (tid & 3) * 16, q = q0 + r;
     if (q < a.sq) {
-      const uint8_t* src = (a.mask_mode == 3 ? m8 + (int64_t)q * a.sk : m8 + ((int64_t)b * a.sq + q) * a.sk) + k0 + c;
+      const uint8_t* src = (MODE == 3 ? m8 + (int64_t)q * a.sk : m8 + ((int64_t)b * a.sq + q) * a.sk) + k0 + c;
       if (aligned && k0 + c + 16 <= a.sk) {
         m.t = *reinterpret_cast<const int4*>(src);
       } else {
@@ -446,7 +466,7 @@ BH_DEVICE void mask_load(MaskRegs& m, const AttnArgs& a, int b, int q0, int k0, 
         m.t = *reinterpret_cast<const int4*>(buf);
       }
     }
-  } else if (a.mask_mode == 1 && tid < 4) {
+  } else if (MODE == 1 && tid < 4) {
     const uint8_t* src = m8 + (int64_t)b * a.sk + k0 + tid * 16;
     if (aligned && k0 + tid * 16 + 16 <= a.sk) {
       m.t = *reinterpret_cast<const int4*>(src);
@@ -455,7 +475,7 @@ BH_DEVICE void mask_load(MaskRegs& m, const AttnArgs& a, int b, int q0, int k0, 
       for (int i = 0; i < 16; ++i) buf[i] = (k0 + tid * 16 + i < a.sk) ? src[i] : 1;
       m.t = *reinterpret_cast<const int4*>(buf);
     }
-  } else if (a.mask_mode == 2 && tid < 16) {
+  } else if (MODE == 2 && tid < 16) {
     const float* src = reinterpret_cast<const float*>(a.mask) + (int64_t)b * a.sk + k0 + tid * 4;
     if ((a.sk & 3) == 0 && k0 + tid * 4 + 4 <= a.sk) {
       m.t = *reinterpret_cast<const int4*>(src);
@@ -466,18 +486,20 @@ BH_DEVICE void mask_load(MaskRegs& m, const AttnArgs& a, int b, int q0, int k0, 
     }
   }
 }
+template <int MODE>
 BH_DEVICE void mask_store(char* img, const MaskRegs& m, const AttnArgs& a, int tid) {
-  if (a.mask_mode == 3 || a.mask_mode == 4) *reinterpret_cast<int4*>(img + tid * 16) = m.t;
-  else if ((a.mask_mode == 1 && tid < 4) || (a.mask_mode == 2 && tid < 16)) *reinterpret_cast<int4*>(img + tid * 16) = m.t;
+  if (MODE == 3 || MODE == 4) *reinterpret_cast<int4*>(img + tid * 16) = m.t;
+  else if ((MODE == 1 && tid < 4) || (MODE == 2 && tid < 16)) *reinterpret_cast<int4*>(img + tid * 16) = m.t;
 }
 // (masked?, score) for local query row ql (0..63 of the block), local key kl, global q / k
+template <int MODE>
 BH_DEVICE float mask_apply(float s, const AttnArgs& a, const char* mimg, int ql, int kl, int q, int k, bool& masked) {
   masked = false;
   if (k >= a.sk) {
     masked = true;
     return -INFINITY;
   }
-  switch (a.mask_mode) {
+  switch (MODE) {
     case 1: masked = mimg[kl] != 0; break;
     case 2: return s + reinterpret_cast<const float*>(mimg)[kl];
     case 3:
@@ -497,12 +519,10 @@ BH_DEVICE i4v frag_tr_perm(const char* img, int rb, int k0, int n0, int lane) {
   const int r = k0 + 4 * g + q;
   const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(img + img_elem(r, n0 + 4 * p, rb)));
   const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(img + img_elem(r + 16, n0 + 4 * p, rb)));
-  i4v out;
-  out[0] = (int)(uint16_t)lo[0] | ((int)(uint16_t)lo[1] << 16);
-  out[1] = (int)(uint16_t)lo[2] | ((int)(uint16_t)lo[3] << 16);
-  out[2] = (int)(uint16_t)hi[0] | ((int)(uint16_t)hi[1] << 16);
-  out[3] = (int)(uint16_t)hi[2] | ((int)(uint16_t)hi[3] << 16);
-  return out;
+  // the two 4 x 16-bit results already sit in the operand's dword order: reinterpret, no repacking
+  typedef int bh_i2v __attribute__((ext_vector_type(2)));
+  const bh_i2v l = __builtin_bit_cast(bh_i2v, lo), h = __builtin_bit_cast(bh_i2v, hi);
+  return i4v{l[0], l[1], h[0], h[1]};
 }
 // the matching B (or A) operand straight from two accumulator tiles (no lane movement, no LDS)
 template <typename T> BH_DEVICE i4v pack_pair(const f4v& lo, const f4v& hi) {
@@ -538,26 +558,38 @@ BH_DEVICE uint32_t row_hash(const AttnArgs& a, int bh, int q) {
   return mix32((uint32_t)a.seed ^ mix32((uint32_t)(a.seed >> 32) ^ ((uint32_t)bh * 0x9E3779B1u) ^
                                         ((uint32_t)q * 0x85EBCA77u)));
 }
+// one 32-bit hash per (query, key pair): keys 2i and 2i+1 use its low / high 16 bits, so the
+// query-on-lane kernels (forward, dQ) hash once per two scores; thresh is (1 - p) * 65536
+BH_DEVICE uint32_t pair_hash(uint32_t rowh, int k) { return mix32(rowh ^ ((uint32_t)(k >> 1) * 0xC2B2AE3Du)); }
 BH_DEVICE bool keep_elem(uint32_t rowh, int k, uint32_t thresh) {
-  return mix32(rowh ^ ((uint32_t)k * 0xC2B2AE3Du)) < thresh;
+  const uint32_t h = pair_hash(rowh, k);
+  return ((k & 1) ? (h >> 16) : (h & 0xffffu)) < thresh;
+}
+// keep flags of keys k0, k0+1 (k0 even)
+BH_DEVICE void keep_pair(uint32_t rowh, int k0, uint32_t thresh, bool& a, bool& b) {
+  const uint32_t h = pair_hash(rowh, k0);
+  a = (h & 0xffffu) < thresh;
+  b = (h >> 16) < thresh;
 }
 BH_DEVICE uint32_t keep_thresh(float p) {
-  const double t = (1.0 - (double)p) * 4294967296.0;
-  return t >= 4294967295.0 ? 0xffffffffu : (uint32_t)t;
+  const double t = (1.0 - (double)p) * 65536.0;
+  return t >= 65536.0 ? 65536u : (uint32_t)t;
 }
 
 // Forward. Workgroup = 64 query rows x one head; wave w = 16 rows, query on the LANE: S^T = K.Q^T
 // puts each query's 16 scores of a 64-key block in one lane's registers, so the online-softmax max
 // and sum are in-lane plus two xor-shuffles, and P^T feeds O^T = V^T.P^T as the B operand without
 // leaving registers. K / V / mask blocks are double-buffered through LDS.
-template <typename T>
+template <typename T, int MODE>
 __global__ __launch_bounds__(kThreads) void k_flash_fwd(AttnArgs a) {
   constexpr int kBuf = 2 * kKB * 128 + kMaskBytes;
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
-  const int bh = blockIdx.y, b = bh / a.heads;
-  const int q0 = blockIdx.x * kQB;
+  int qtile, bh;
+  flash_tile(qtile, bh);
+  const int b = bh / a.heads;
+  const int q0 = qtile * kQB;
   const int myq = q0 + wave * 16 + fr;  // this lane's query
 
   const T* K = reinterpret_cast<const T*>(a.k) + (int64_t)bh * a.k_sbh;
@@ -577,17 +609,17 @@ __global__ __launch_bounds__(kThreads) void k_flash_fwd(AttnArgs a) {
   f4v O[4];
 #pragma unroll
   for (int dn = 0; dn < 4; ++dn) O[dn] = f4v{0.f, 0.f, 0.f, 0.f};
-  const int kend = a.mask_mode == 5 ? min(a.sk, q0 + kQB) : a.sk;
+  const int kend = MODE == 5 ? min(a.sk, q0 + kQB) : a.sk;
   const int nb = (kend + kKB - 1) / kKB;
 
   RowRegs rk, rv;
   MaskRegs rm;
   rows_load<T>(rk, K, a.k_st, min(kKB, a.sk), tid);
   rows_load<T>(rv, V, a.v_st, min(kKB, a.sk), tid);
-  mask_load(rm, a, b, q0, 0, tid);
+  mask_load<MODE>(rm, a, b, q0, 0, tid);
   rows_store(smem, rk, tid);
   rows_store(smem + kKB * 128, rv, tid);
-  mask_store(smem + 2 * kKB * 128, rm, a, tid);
+  mask_store<MODE>(smem + 2 * kKB * 128, rm, a, tid);
   __syncthreads();
   for (int ib = 0; ib < nb; ++ib) {
     const int kb = ib * kKB;
@@ -598,7 +630,7 @@ __global__ __launch_bounds__(kThreads) void k_flash_fwd(AttnArgs a) {
       const int kn = kb + kKB;
       rows_load<T>(rk, K + (int64_t)kn * a.k_st, a.k_st, min(kKB, a.sk - kn), tid);
       rows_load<T>(rv, V + (int64_t)kn * a.v_st, a.v_st, min(kKB, a.sk - kn), tid);
-      mask_load(rm, a, b, q0, kn, tid);
+      mask_load<MODE>(rm, a, b, q0, kn, tid);
     }
     f4v S[4];  // S^T: row = key 16mt + 4fq + j, column = this lane's query
 #pragma unroll
@@ -614,7 +646,7 @@ __global__ __launch_bounds__(kThreads) void k_flash_fwd(AttnArgs a) {
       for (int j = 0; j < 4; ++j) {
         bool mk;
         const int kl = 16 * mt + 4 * fq + j;
-        S[mt][j] = mask_apply(S[mt][j] * a.scale, a, mimg, myq - q0, kl, myq, kb + kl, mk);
+        S[mt][j] = mask_apply<MODE>(S[mt][j] * a.scale, a, mimg, myq - q0, kl, myq, kb + kl, mk);
         mb = fmaxf(mb, S[mt][j]);
       }
     mb = fmaxf(mb, __shfl_xor(mb, 16));
@@ -623,14 +655,21 @@ __global__ __launch_bounds__(kThreads) void k_flash_fwd(AttnArgs a) {
     const float corr = (m == -INFINITY) ? 0.f : __expf(m - mn);
     m = mn;
     float ls = 0.f;
+    const float mref = m == -INFINITY ? 0.f : m;  // all scores -inf then: exp -> 0
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < 4; ++mt) {
+      bool kp[4] = {true, true, true, true};
+      if (drop) {
+        keep_pair(rowh, kb + 16 * mt + 4 * fq, thresh, kp[0], kp[1]);
+        keep_pair(rowh, kb + 16 * mt + 4 * fq + 2, thresh, kp[2], kp[3]);
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float p = m == -INFINITY ? 0.f : __expf(S[mt][j] - m);
+        const float p = __expf(S[mt][j] - mref);
         ls += p;
-        S[mt][j] = (drop && !keep_elem(rowh, kb + 16 * mt + 4 * fq + j, thresh)) ? 0.f : p;
+        S[mt][j] = kp[j] ? p : 0.f;
       }
+    }
     ls += __shfl_xor(ls, 16);
     ls += __shfl_xor(ls, 32);
     l = l * corr + ls;
@@ -646,7 +685,7 @@ __global__ __launch_bounds__(kThreads) void k_flash_fwd(AttnArgs a) {
       char* nk = smem + ((ib + 1) & 1) * kBuf;
       rows_store(nk, rk, tid);
       rows_store(nk + kKB * 128, rv, tid);
-      mask_store(nk + 2 * kKB * 128, rm, a, tid);
+      mask_store<MODE>(nk + 2 * kKB * 128, rm, a, tid);
     }
     __syncthreads();
   }
@@ -678,14 +717,16 @@ __global__ __launch_bounds__(256) void k_flash_delta(AttnArgs a, float* __restri
 
 // dQ. Same layout as the forward (query on the lane): S^T = K.Q^T and dP^T = V.dO^T, P^T from
 // the saved LSE, dS^T in registers feeds dQ^T = K^T.dS^T directly.
-template <typename T>
+template <typename T, int MODE>
 __global__ __launch_bounds__(kThreads) void k_flash_bwd_dq(AttnArgs a) {
   constexpr int kBuf = 2 * kKB * 128 + kMaskBytes;
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
-  const int bh = blockIdx.y, b = bh / a.heads;
-  const int q0 = blockIdx.x * kQB;
+  int qtile, bh;
+  flash_tile(qtile, bh);
+  const int b = bh / a.heads;
+  const int q0 = qtile * kQB;
   const int myq = q0 + wave * 16 + fr;
   const T* K = reinterpret_cast<const T*>(a.k) + (int64_t)bh * a.k_sbh;
   const T* V = reinterpret_cast<const T*>(a.v) + (int64_t)bh * a.v_sbh;
@@ -708,16 +749,16 @@ __global__ __launch_bounds__(kThreads) void k_flash_bwd_dq(AttnArgs a) {
   f4v acc[4];
 #pragma unroll
   for (int dn = 0; dn < 4; ++dn) acc[dn] = f4v{0.f, 0.f, 0.f, 0.f};
-  const int kend = a.mask_mode == 5 ? min(a.sk, q0 + kQB) : a.sk;
+  const int kend = MODE == 5 ? min(a.sk, q0 + kQB) : a.sk;
   const int nb = (kend + kKB - 1) / kKB;
   RowRegs rk, rv;
   MaskRegs rm;
   rows_load<T>(rk, K, a.k_st, min(kKB, a.sk), tid);
   rows_load<T>(rv, V, a.v_st, min(kKB, a.sk), tid);
-  mask_load(rm, a, b, q0, 0, tid);
+  mask_load<MODE>(rm, a, b, q0, 0, tid);
   rows_store(smem, rk, tid);
   rows_store(smem + kKB * 128, rv, tid);
-  mask_store(smem + 2 * kKB * 128, rm, a, tid);
+  mask_store<MODE>(smem + 2 * kKB * 128, rm, a, tid);
   __syncthreads();
   for (int ib = 0; ib < nb; ++ib) {
     const int kb = ib * kKB;
@@ -728,7 +769,7 @@ __global__ __launch_bounds__(kThreads) void k_flash_bwd_dq(AttnArgs a) {
       const int kn = kb + kKB;
       rows_load<T>(rk, K + (int64_t)kn * a.k_st, a.k_st, min(kKB, a.sk - kn), tid);
       rows_load<T>(rv, V + (int64_t)kn * a.v_st, a.v_st, min(kKB, a.sk - kn), tid);
-      mask_load(rm, a, b, q0, kn, tid);
+      mask_load<MODE>(rm, a, b, q0, kn, tid);
     }
     f4v dS[4];
 #pragma unroll
@@ -739,13 +780,18 @@ __global__ __launch_bounds__(kThreads) void k_flash_bwd_dq(AttnArgs a) {
         S = Mfma<T>::run(frag_row(kimg, 128, 16 * mt, 32 * s, lane), qb[s], S);
         dP = Mfma<T>::run(frag_row(vimg, 128, 16 * mt, 32 * s, lane), db[s], dP);
       }
+      bool kp[4] = {true, true, true, true};
+      if (drop) {
+        keep_pair(rowh, kb + 16 * mt + 4 * fq, thresh, kp[0], kp[1]);
+        keep_pair(rowh, kb + 16 * mt + 4 * fq + 2, thresh, kp[2], kp[3]);
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int kl = 16 * mt + 4 * fq + j;
         bool mk;
-        const float v = mask_apply(S[j] * a.scale, a, mimg, myq - q0, kl, myq, kb + kl, mk);
+        const float v = mask_apply<MODE>(S[j] * a.scale, a, mimg, myq - q0, kl, myq, kb + kl, mk);
         const float p = (rowok && v != -INFINITY) ? __expf(v - lse) : 0.f;
-        const float dpd = drop ? (keep_elem(rowh, kb + kl, thresh) ? dP[j] * kscale : 0.f) : dP[j];
+        const float dpd = drop ? (kp[j] ? dP[j] * kscale : 0.f) : dP[j];
         dS[mt][j] = mk ? 0.f : p * (dpd - dl) * a.scale;
       }
     }
@@ -760,7 +806,7 @@ __global__ __launch_bounds__(kThreads) void k_flash_bwd_dq(AttnArgs a) {
       char* nk = smem + ((ib + 1) & 1) * kBuf;
       rows_store(nk, rk, tid);
       rows_store(nk + kKB * 128, rv, tid);
-      mask_store(nk + 2 * kKB * 128, rm, a, tid);
+      mask_store<MODE>(nk + 2 * kKB * 128, rm, a, tid);
     }
     __syncthreads();
   }
@@ -775,14 +821,16 @@ __global__ __launch_bounds__(kThreads) void k_flash_bwd_dq(AttnArgs a) {
 // S = Q.K^T and dP = dO.V^T per 16-query tile put 4 queries of one key in a lane's registers, so
 // Pd and dS feed dV^T = dO^T.Pd and dK^T = Q^T.dS as B operands straight from registers (no
 // cross-wave reduction, no LDS round trip). Q / dO / LSE / delta / mask blocks are double-buffered.
-template <typename T>
+template <typename T, int MODE>
 __global__ __launch_bounds__(kThreads) void k_flash_bwd_dkdv(AttnArgs a) {
   constexpr int kBuf = 2 * kQB * 128 + kMaskBytes + 2 * kQB * 4;  // Q, dO, mask, LSE, delta
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
-  const int bh = blockIdx.y, b = bh / a.heads;
-  const int kb = blockIdx.x * kKB;
+  int ktile, bh;
+  flash_tile(ktile, bh);
+  const int b = bh / a.heads;
+  const int kb = ktile * kKB;
   const int mykey = kb + wave * 16 + fr;
   const T* K = reinterpret_cast<const T*>(a.k) + (int64_t)bh * a.k_sbh;
   const T* V = reinterpret_cast<const T*>(a.v) + (int64_t)bh * a.v_sbh;
@@ -803,7 +851,7 @@ __global__ __launch_bounds__(kThreads) void k_flash_bwd_dkdv(AttnArgs a) {
   f4v dK[4], dV[4];
 #pragma unroll
   for (int dn = 0; dn < 4; ++dn) dK[dn] = dV[dn] = f4v{0.f, 0.f, 0.f, 0.f};
-  const int qstart = a.mask_mode == 5 ? (kb / kQB) * kQB : 0;
+  const int qstart = MODE == 5 ? (kb / kQB) * kQB : 0;
   const int nqb = (a.sq - qstart + kQB - 1) / kQB;
   const float* lseg = a.lse + (int64_t)bh * a.sq;
   const float* dlg = a.delta + (int64_t)bh * a.sq;
@@ -813,7 +861,7 @@ __global__ __launch_bounds__(kThreads) void k_flash_bwd_dkdv(AttnArgs a) {
   auto load_blk = [&](int qs) {
     rows_load<T>(rq, Q + (int64_t)qs * a.q_st, a.q_st, min(kQB, a.sq - qs), tid);
     rows_load<T>(rd, dO + (int64_t)qs * a.do_st, a.do_st, min(kQB, a.sq - qs), tid);
-    mask_load(rm, a, b, qs, kb, tid);
+    mask_load<MODE>(rm, a, b, qs, kb, tid);
     if (tid < 2 * kQB) {
       const int q = min(qs + (tid & (kQB - 1)), a.sq - 1);
       const float v = tid < kQB ? lseg[q] : dlg[q];
@@ -823,7 +871,7 @@ __global__ __launch_bounds__(kThreads) void k_flash_bwd_dkdv(AttnArgs a) {
   auto store_blk = [&](char* buf) {
     rows_store(buf, rq, tid);
     rows_store(buf + kQB * 128, rd, tid);
-    mask_store(buf + 2 * kQB * 128, rm, a, tid);
+    mask_store<MODE>(buf + 2 * kQB * 128, rm, a, tid);
     if (tid < 2 * kQB) reinterpret_cast<float*>(buf + 2 * kQB * 128 + kMaskBytes)[tid] = rl;
   };
   load_blk(qstart);
@@ -851,7 +899,7 @@ __global__ __launch_bounds__(kThreads) void k_flash_bwd_dkdv(AttnArgs a) {
         const int ql = 16 * qt + 4 * fq + j, q = q0 + ql;
         const float lse = lsel[ql], dl = dll[ql];
         bool mk;
-        const float v = mask_apply(S[j] * a.scale, a, mimg, ql, wave * 16 + fr, q, mykey, mk);
+        const float v = mask_apply<MODE>(S[j] * a.scale, a, mimg, ql, wave * 16 + fr, q, mykey, mk);
         const float p = (q < a.sq && v != -INFINITY && lse != INFINITY) ? __expf(v - lse) : 0.f;
         const float kk = drop ? (keep_elem(row_hash(a, bh, q), mykey, thresh) ? kscale : 0.f) : 1.f;
         Pd[qt][j] = p * kk;
@@ -879,6 +927,27 @@ __global__ __launch_bounds__(kThreads) void k_flash_bwd_dkdv(AttnArgs a) {
       store4<T>(dk + 16 * dn + 4 * fq, dK[dn], 1.f);
       store4<T>(dv + 16 * dn + 4 * fq, dV[dn], 1.f);
     }
+  }
+}
+
+// (dtype, mask mode) -> compile-time kernel instance: the per-score mask logic has no runtime switch
+template <typename T> struct TypeTag { using type = T; };
+template <typename F> void flash_modes(int mode, const char* what, F&& f) {
+  switch (mode) {
+    case 0: f(std::integral_constant<int, 0>{}); break;
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 3: f(std::integral_constant<int, 3>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 5: f(std::integral_constant<int, 5>{}); break;
+    default: throw std::runtime_error(std::string(what) + ": unknown mask mode");
+  }
+}
+template <typename F> void flash_dispatch(int dt, int mode, const char* what, F&& f) {
+  switch (dt) {
+    case kF16: flash_modes(mode, what, [&](auto mm) { f(TypeTag<f16>{}, mm); }); break;
+    case kBF16: flash_modes(mode, what, [&](auto mm) { f(TypeTag<bf16>{}, mm); }); break;
+    default: throw std::runtime_error(std::string(what) + ": fp16 / bf16 only");
   }
 }
 
@@ -926,11 +995,10 @@ void attn_backward(int dt, const AttnArgs& a, hipStream_t st) {
 void flash_forward(int dt, const AttnArgs& a, hipStream_t st) {
   if (a.sk < 1 || a.sq < 1 || !a.lse) throw std::runtime_error("flash_forward: bad shape or missing lse");
   const dim3 grid((unsigned)((a.sq + kQB - 1) / kQB), (unsigned)a.BH);
-  switch (dt) {
-    case kF16: hipLaunchKernelGGL((k_flash_fwd<f16>), grid, dim3(kThreads), 0, st, a); break;
-    case kBF16: hipLaunchKernelGGL((k_flash_fwd<bf16>), grid, dim3(kThreads), 0, st, a); break;
-    default: throw std::runtime_error("flash_forward: fp16 / bf16 only");
-  }
+  flash_dispatch(dt, a.mask_mode, "flash_forward", [&](auto tt, auto mm) {
+    using T = typename decltype(tt)::type;
+    hipLaunchKernelGGL((k_flash_fwd<T, decltype(mm)::value>), grid, dim3(kThreads), 0, st, a);
+  });
   check_launch("flash_forward");
 }
 
@@ -949,17 +1017,11 @@ void flash_backward(int dt, const AttnArgs& a, hipStream_t st) {
   if (a.sk < 1 || a.sq < 1 || !a.lse || !a.delta) throw std::runtime_error("flash_backward: bad args");
   const dim3 gq((unsigned)((a.sq + kQB - 1) / kQB), (unsigned)a.BH);
   const dim3 gk((unsigned)((a.sk + kKB - 1) / kKB), (unsigned)a.BH);
-  switch (dt) {
-    case kF16:
-      hipLaunchKernelGGL((k_flash_bwd_dkdv<f16>), gk, dim3(kThreads), 0, st, a);
-      hipLaunchKernelGGL((k_flash_bwd_dq<f16>), gq, dim3(kThreads), 0, st, a);
-      break;
-    case kBF16:
-      hipLaunchKernelGGL((k_flash_bwd_dkdv<bf16>), gk, dim3(kThreads), 0, st, a);
-      hipLaunchKernelGGL((k_flash_bwd_dq<bf16>), gq, dim3(kThreads), 0, st, a);
-      break;
-    default: throw std::runtime_error("flash_backward: fp16 / bf16 only");
-  }
+  flash_dispatch(dt, a.mask_mode, "flash_backward", [&](auto tt, auto mm) {
+    using T = typename decltype(tt)::type;
+    hipLaunchKernelGGL((k_flash_bwd_dkdv<T, decltype(mm)::value>), gk, dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL((k_flash_bwd_dq<T, decltype(mm)::value>), gq, dim3(kThreads), 0, st, a);
+  });
   check_launch("flash_backward");
 }
 

@@ -17,6 +17,12 @@ def main():
                 if "gemm_nt" in name:
                     big = "Li8ELi4E" in name or "Cfg<2, 4, 8, 4, 2>" in name
                     name = "gemm_nt<" + ("256x256" if big else "128x128") + ">"
+                elif "k_flash_fwd" in name:
+                    name = "flash_fwd"
+                elif "k_flash_bwd_dq" in name:
+                    name = "flash_bwd_dq"
+                elif "k_flash_bwd_dkdv" in name:
+                    name = "flash_bwd_dkdv"
                 elif "attn_fwd" in name:
                     name = "attn_fwd"
                 elif "attn_bwd" in name:
