@@ -821,8 +821,10 @@ __global__ __launch_bounds__(kThreads) void k_flash_bwd_dq(AttnArgs a) {
 // S = Q.K^T and dP = dO.V^T per 16-query tile put 4 queries of one key in a lane's registers, so
 // Pd and dS feed dV^T = dO^T.Pd and dK^T = Q^T.dS as B operands straight from registers (no
 // cross-wave reduction, no LDS round trip). Q / dO / LSE / delta / mask blocks are double-buffered.
+// 3 waves per SIMD (<= 168 VGPRs): the LDS footprint (2 x 20.5 KiB) already caps the kernel at
+// 3 workgroups per CU, so registers beyond that only cost occupancy
 template <typename T, int MODE>
-__global__ __launch_bounds__(kThreads) void k_flash_bwd_dkdv(AttnArgs a) {
+__global__ __launch_bounds__(kThreads, 3) void k_flash_bwd_dkdv(AttnArgs a) {
   constexpr int kBuf = 2 * kQB * 128 + kMaskBytes + 2 * kQB * 4;  // Q, dO, mask, LSE, delta
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
