@@ -1,0 +1,124 @@
+"""GPT-2-medium tensor-parallel training step throughput (BASELINE.json configs[4]: GPT-2-medium via
+beforeholiday_amd.transformer tensor_parallel, fused scaled-masked-softmax + bias-GELU, TP over xGMI).
+
+Model: Megatron-style GPT-2-medium (24 layers, hidden 1024, 16 heads, FFN 4096, vocab 50257 padded to
+50304, seq 1024) built from ColumnParallelLinear / RowParallelLinear / VocabParallelEmbedding with
+causal flash attention, fused bias-GELU MLP, FusedLayerNorm and vocab-parallel cross-entropy
+(reference: apex/transformer/testing/standalone_gpt.py:33-111, tensor_parallel/layers.py:167-780).
+amp O5 (bf16 model, fp32 master weights, no loss scale) + FusedAdam: an elementwise optimizer keeps
+TP-replicated parameters (LayerNorms, row-parallel biases) bit-identical across TP ranks without a
+cross-rank norm. ``--tp`` ranks form one tensor-parallel group; the remaining factor of the world is
+data parallel (DDP over the DP group). ``--sp`` turns on Megatron sequence parallelism.
+Synthetic token ids, random-init weights. Prints one JSON line (whole-job tokens/s).
+
+    python benchmarks/bench_gpt.py --batch 8 --steps 10 --warmup 3
+    python -m torch.distributed.run --nproc-per-node 4 --master-addr 127.0.0.1 benchmarks/bench_gpt.py --tp 4 --sp
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=8, help="sequences per data-parallel rank")
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--layers", type=int, default=24)
+    ap.add_argument("--tp", type=int, default=0, help="tensor-parallel size (default: whole world)")
+    ap.add_argument("--sp", action="store_true", help="sequence parallelism inside the TP group")
+    ap.add_argument("--opt-level", default="O5", choices=["O2", "O5"])
+    ap.add_argument("--dropout", type=float, default=0.1)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29534")
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+    tp = args.tp or world
+    assert world % tp == 0, f"world {world} not divisible by tp {tp}"
+    dp = world // tp
+
+    from beforeholiday_amd import amp
+    from beforeholiday_amd._native import require_native
+    from beforeholiday_amd.models import GPTModel, TransformerConfig, finalize_model_grads
+    from beforeholiday_amd.optimizers import FusedAdam
+    from beforeholiday_amd.parallel import DistributedDataParallel
+    from beforeholiday_amd.transformer import parallel_state, tensor_parallel
+    from beforeholiday_amd.transformer.pipeline_parallel.utils import get_ltor_masks_and_position_ids
+
+    require_native("bench_gpt")
+    parallel_state.initialize_model_parallel(tp, 1)
+    tensor_parallel.model_parallel_cuda_manual_seed(1234)
+    fp16 = args.opt_level == "O2"
+    cfg = TransformerConfig(hidden_size=1024, num_layers=args.layers, num_attention_heads=16, ffn_hidden_size=4096,
+                            vocab_size=50304, max_position_embeddings=args.seq, hidden_dropout=args.dropout,
+                            attention_dropout=args.dropout, fp16=fp16, bf16=not fp16, masked_softmax_fusion=True,
+                            bias_gelu_fusion=True, sequence_parallel=args.sp and tp > 1)
+    model = GPTModel(cfg, parallel_output=True).cuda()
+    nparams_local = sum(p.numel() for p in model.parameters())
+    opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=0.01)
+    model, opt = amp.initialize(model, opt, opt_level=args.opt_level, verbosity=0)
+    if dp > 1:
+        model = DistributedDataParallel(model, process_group=parallel_state.get_data_parallel_group())
+
+    # every TP rank of one DP replica sees the same tokens
+    g = torch.Generator(device="cuda").manual_seed(1000 + parallel_state.get_data_parallel_rank())
+    B, S = args.batch, args.seq
+    tokens = torch.randint(0, 50257, (B, S), device="cuda", generator=g)
+    labels = torch.randint(0, 50257, (B, S), device="cuda", generator=g)
+    mask, _, pos = get_ltor_masks_and_position_ids(tokens, -1, False, False, False)
+
+    def step():
+        loss = model(tokens, pos, mask, labels=labels).float().mean()
+        with amp.scale_loss(loss, opt) as scaled:
+            scaled.backward()
+        if tp > 1:
+            finalize_model_grads(getattr(model, "module", model))
+        opt.step()
+        opt.zero_grad()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], device="cuda", dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = float(el)
+    toks = B * dp * S * args.steps / el
+    # 6*N*T matmul FLOPs + causal attention (12*L*h*S per token, halved by the causal skip)
+    nparams = 354_871_296
+    flops_per_tok = 6 * nparams + 6 * args.layers * 1024 * S
+    if rank == 0:
+        print(json.dumps({
+            "metric": "GPT-2-medium tensor-parallel training tokens/sec", "value": round(toks, 1),
+            "unit": "tokens/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 2), "higher_is_better": True, "scaling": "weak",
+            "model_tflops_per_gpu": round(toks * flops_per_tok / world / 1e12, 1),
+            "dtype": "fp16" if fp16 else "bf16", "data": "synthetic token ids, random-init weights",
+            "config": {"model": f"GPT-2-medium ({args.layers} layers, {nparams_local / 1e6:.0f}M params per TP rank) "
+                       "+ FusedAdam", "global_batch": B * dp, "seq_len": S,
+                       "parallelism": f"tp{tp}{'-sp' if cfg.sequence_parallel else ''}-dp{dp}",
+                       "final_loss": round(float(loss), 4)}}), flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
