@@ -47,6 +47,48 @@ at::Tensor act_backward(const at::Tensor& dy, const at::Tensor& aux, at::Tensor 
 
 at::Tensor bias_grad(const at::Tensor& dy) { return act_backward(dy, at::Tensor(), at::Tensor(), bh::kActNone, true); }
 
+// Megatron bias-dropout-add: out = residual + dropout(x + bias); returns (out, keep bits uint8 [numel/8]).
+// p == 0 (or eval) -> keep is an empty tensor and no dropout is applied.
+std::vector<at::Tensor> bias_dropout_add(const at::Tensor& x, const c10::optional<at::Tensor>& bias,
+                                         const at::Tensor& residual, double p, int64_t seed) {
+  check_cuda(x, "x");
+  TORCH_CHECK(residual.sizes() == x.sizes() && residual.scalar_type() == x.scalar_type(),
+              "bias_dropout_add: residual must match x in shape and dtype");
+  TORCH_CHECK(p >= 0.0 && p < 1.0, "bias_dropout_add: p must be in [0, 1)");
+  auto xc = x.contiguous(), rc = residual.contiguous();
+  const int64_t N = xc.size(-1), M = xc.numel() / std::max<int64_t>(N, 1);
+  TORCH_CHECK(N % 8 == 0 && al16(xc) && al16(rc), "bias_dropout_add: needs N % 8 == 0 and 16-byte aligned tensors");
+  at::Tensor b;
+  if (bias.has_value() && bias->defined()) {
+    b = bias->contiguous();
+    TORCH_CHECK(b.numel() == N && b.scalar_type() == x.scalar_type() && al16(b), "bias_dropout_add: bad bias");
+  }
+  auto out = at::empty_like(xc);
+  at::Tensor keep = at::empty({p > 0.0 ? xc.numel() / 8 : 0}, xc.options().dtype(at::kByte));
+  bh::dense_bias_dropout_add(dtype_code(xc.scalar_type()), xc.data_ptr(), b.defined() ? b.data_ptr() : nullptr,
+                             rc.data_ptr(), out.data_ptr(), p > 0.0 ? keep.data_ptr<uint8_t>() : nullptr, M, (int)N,
+                             (float)p, (uint32_t)seed, stream_for(xc));
+  return {out, keep};
+}
+
+// backward of the dropout branch: dx = dy * keep / (1 - p) (dy itself when there is no mask), bias grad = sum dx
+std::vector<at::Tensor> dropout_backward(const at::Tensor& dy, const at::Tensor& keep, double p, bool want_bgrad) {
+  check_cuda(dy, "dy");
+  auto g = dy.contiguous();
+  const int64_t N = g.size(-1), M = g.numel() / std::max<int64_t>(N, 1);
+  if (keep.numel() == 0) return {g, want_bgrad ? bias_grad(g) : at::Tensor()};
+  TORCH_CHECK(keep.numel() * 8 == g.numel() && N % 8 == 0 && al16(g), "dropout_backward: mask / shape mismatch");
+  auto dx = at::empty_like(g);
+  at::Tensor bgrad;
+  if (want_bgrad) bgrad = at::empty({N}, g.options());
+  const int splits = bh::dense_bgrad_splits(M, (int)N);
+  auto part = at::empty({(int64_t)splits * N}, g.options().dtype(at::kFloat));
+  bh::dense_dropout_backward(dtype_code(g.scalar_type()), g.data_ptr(), keep.data_ptr<uint8_t>(),
+                             (float)(1.0 / (1.0 - p)), dx.data_ptr(), want_bgrad ? bgrad.data_ptr() : nullptr,
+                             part.data_ptr<float>(), splits, M, (int)N, stream_for(g));
+  return {dx, bgrad};
+}
+
 // ------------------------------------------------------------------------------------------------
 // MFMA GEMM with fused epilogue (kernels/gemm.hip). BH_DENSE_MFMA=0 routes everything back to
 // hipBLASLt + the separate epilogue passes (A/B switch for benchmarks).
@@ -282,6 +324,10 @@ void register_dense(pybind11::module_& root) {
     check_cuda(dy, "dy");
     return bias_grad(dy.contiguous());
   }, py::arg("dy"), "column sum of dy[..., N] over all leading dims (fp32 accumulation, dy dtype out)");
+  fd.def("bias_dropout_add", &bias_dropout_add, py::arg("x"), py::arg("bias"), py::arg("residual"), py::arg("p"),
+         py::arg("seed"), "out = residual + dropout(x + bias) in one pass; returns (out, keep bits)");
+  fd.def("dropout_backward", &dropout_backward, py::arg("dy"), py::arg("keep"), py::arg("p"), py::arg("want_bgrad"),
+         "dx = dy * keep / (1 - p) with the bias gradient sum(dx) from the same pass; returns (dx, bgrad)");
   auto mlp = root.def_submodule("mlp_cuda", "N-layer MLP");
   mlp.def("forward", &mlp_forward);
   mlp.def("backward", &mlp_backward);

@@ -67,11 +67,58 @@ __global__ __launch_bounds__(256) void k_act_fwd(const T* __restrict__ x, const 
   }
 }
 
+// counter-based dropout bits: one 32-bit hash per element index (seed-keyed), keep iff u >= p
+BH_DEVICE uint32_t bda_hash(uint32_t seed, uint64_t i) {
+  uint32_t h = seed ^ (uint32_t)i ^ ((uint32_t)(i >> 32) * 0x9E3779B9u);
+  h ^= h >> 16;
+  h *= 0x7feb352du;
+  h ^= h >> 15;
+  h *= 0x846ca68bu;
+  h ^= h >> 16;
+  return h;
+}
+
+// out = residual + dropout(x + bias) with the keep bits stored 1 per element (uint8 [M*N/8]).
+// Vector path only (N % 8 == 0, 16-byte aligned): each lane owns 8 consecutive elements = 1 mask byte.
+template <typename T>
+__global__ __launch_bounds__(256) void k_bias_dropout_add(const T* __restrict__ x, const T* __restrict__ bias,
+                                                          const T* __restrict__ res, T* __restrict__ out,
+                                                          uint8_t* __restrict__ keep, int64_t total, int N,
+                                                          uint32_t thresh, float scale, uint32_t seed) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < total; i += stride) {
+    float v[8], r[8];
+    VecIO<T>::load(x + i, v);
+    VecIO<T>::load(res + i, r);
+    if (bias) {
+      float b[8];
+      VecIO<T>::load(bias + (i % N), b);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += b[k];
+    }
+    if (keep) {
+      uint32_t bits = 0u;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const bool kp = bda_hash(seed, (uint64_t)(i + k)) >= thresh;
+        bits |= (uint32_t)kp << k;
+        v[k] = kp ? v[k] * scale : 0.f;
+      }
+      keep[i >> 3] = (uint8_t)bits;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += r[k];
+    VecIO<T>::store(out + i, v);
+  }
+}
+
 // grid (ceil(N / kCols), splits); block (kColLanes, kRowLanes)
 template <typename T>
 __global__ __launch_bounds__(256) void k_act_bwd(const T* __restrict__ dy, const T* __restrict__ aux,
                                                  T* __restrict__ dx, float* __restrict__ part, int64_t M, int N,
-                                                 int64_t rows_per_split, int act, bool vec) {
+                                                 int64_t rows_per_split, int act, bool vec,
+                                                 const uint8_t* __restrict__ keep, float keep_scale) {
+  // keep (vec path only): dropout keep bits, byte (off / 8) holds columns col0..col0+7 of a row
   __shared__ float red[kRowLanes][kCols + 4];
   const int col0 = blockIdx.x * kCols + threadIdx.x * 8;
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_split;
@@ -84,6 +131,11 @@ __global__ __launch_bounds__(256) void k_act_bwd(const T* __restrict__ dy, const
       if (vec && col0 + 8 <= N) {
         VecIO<T>::load(dy + off, g);
         if (act != kActNone) VecIO<T>::load(aux + off, a);
+        if (keep) {
+          const uint32_t bits = keep[off >> 3];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) g[k] = ((bits >> k) & 1u) ? g[k] * keep_scale : 0.f;
+        }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           if (act != kActNone) g[k] *= act_d(a[k], act);
@@ -150,12 +202,45 @@ void dense_act_backward(int dt, const void* dy, const void* aux, void* dx, void*
   dim3 grid((unsigned)((N + kCols - 1) / kCols), (unsigned)splits);
   DN_DISPATCH(dt, T,
       hipLaunchKernelGGL((k_act_bwd<T>), grid, dim3(kColLanes, kRowLanes), 0, st, (const T*)dy, (const T*)aux,
-                         (T*)dx, part, M, N, rps, act, vec);
+                         (T*)dx, part, M, N, rps, act, vec, (const uint8_t*)nullptr, 1.f);
       check_launch("dense_act_backward");
       if (bgrad) {
         hipLaunchKernelGGL((k_colsum_finalize<T>), dim3((unsigned)((N + 63) / 64)), dim3(64 * kColsumLanes), 0, st,
                            part, splits, N, (T*)bgrad);
         check_launch("dense_bgrad_finalize");
+      });
+}
+
+void dense_bias_dropout_add(int dt, const void* x, const void* bias, const void* residual, void* out, uint8_t* keep,
+                            int64_t M, int N, float p, uint32_t seed, hipStream_t st) {
+  const int64_t total = M * (int64_t)N;
+  if (total == 0) return;
+  if (N % 8 != 0) throw std::runtime_error("dense_bias_dropout_add: N % 8 != 0");
+  int64_t blocks = (total / 8 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  // keep iff hash >= p * 2^32 (p < 1 is checked by the caller)
+  const uint32_t thresh = (uint32_t)((double)p * 4294967296.0);
+  const float scale = keep ? 1.f / (1.f - p) : 1.f;
+  DN_DISPATCH(dt, T, hipLaunchKernelGGL((k_bias_dropout_add<T>), dim3((unsigned)blocks), dim3(256), 0, st,
+                                        (const T*)x, (const T*)bias, (const T*)residual, (T*)out, keep, total, N,
+                                        thresh, scale, seed));
+  check_launch("dense_bias_dropout_add");
+}
+
+void dense_dropout_backward(int dt, const void* dy, const uint8_t* keep, float keep_scale, void* dx, void* bgrad,
+                            float* part, int splits, int64_t M, int N, hipStream_t st) {
+  if (N == 0) return;
+  if (N % 8 != 0) throw std::runtime_error("dense_dropout_backward: N % 8 != 0");
+  const int64_t rps = M > 0 ? (M + splits - 1) / splits : 1;
+  dim3 grid((unsigned)((N + kCols - 1) / kCols), (unsigned)splits);
+  DN_DISPATCH(dt, T,
+      hipLaunchKernelGGL((k_act_bwd<T>), grid, dim3(kColLanes, kRowLanes), 0, st, (const T*)dy, (const T*)nullptr,
+                         (T*)dx, part, M, N, rps, (int)kActNone, true, keep, keep_scale);
+      check_launch("dense_dropout_backward");
+      if (bgrad) {
+        hipLaunchKernelGGL((k_colsum_finalize<T>), dim3((unsigned)((N + 63) / 64)), dim3(64 * kColsumLanes), 0, st,
+                           part, splits, N, (T*)bgrad);
+        check_launch("dense_dropout_bgrad_finalize");
       });
 }
 

@@ -369,8 +369,8 @@ class ParallelAttention(MegatronModule):
 
 
 def bias_dropout_add(x, bias, residual, prob: float, training: bool):
-    out = torch.nn.functional.dropout(x + bias if bias is not None else x, p=prob, training=training)
-    return residual + out
+    """residual + dropout(x + bias): one fused HIP pass on GPU (ops/fused_dense.py), PyTorch on CPU."""
+    return _fd.bias_dropout_add(x, bias, residual, prob, training)
 
 
 class ParallelTransformerLayer(MegatronModule):

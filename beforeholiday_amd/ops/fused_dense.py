@@ -150,3 +150,44 @@ def wgrad_gemm_accum_fp16(input, d_output, main_grad):
     if input.is_cuda:
         return submodule("fused_weight_gradient_mlp_cuda").wgrad_gemm_accum_fp16(input, d_output, main_grad)
     main_grad.add_(d_output.reshape(-1, d_output.size(-1)).t().mm(input.reshape(-1, input.size(-1))))
+
+
+class _BiasDropoutAddFn(torch.autograd.Function):
+    """out = residual + dropout(x + bias) as ONE HIP pass that also stores 1 keep bit per element;
+    backward is one pass that applies the bits and reduces the bias gradient from the same data
+    (replaces Megatron's three elementwise kernels + a separate bias-grad reduction;
+    reference: apex/transformer/testing/standalone_transformer_lm.py:188-207 bias_dropout_add)."""
+
+    @staticmethod
+    def forward(ctx, x, bias, residual, p):
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())  # host generator: no device sync
+        out, keep = _fd().bias_dropout_add(x, bias, residual, p, seed)
+        ctx.save_for_backward(keep)
+        ctx.p = p
+        ctx.has_bias = bias is not None
+        return out.view_as(x)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (keep,) = ctx.saved_tensors
+        want_b = ctx.has_bias and ctx.needs_input_grad[1]
+        dx, db = _fd().dropout_backward(dout, keep, ctx.p, want_b)
+        return dx.view_as(dout), (db if want_b else None), dout, None
+
+
+def _bda_native_ok(x, bias, residual) -> bool:
+    return (x.is_cuda and residual.is_cuda and x.dtype == residual.dtype and x.shape == residual.shape and
+            x.dtype in (torch.float16, torch.bfloat16, torch.float32) and x.size(-1) % 8 == 0 and
+            x.is_contiguous() and residual.is_contiguous() and x.data_ptr() % 16 == 0 and
+            residual.data_ptr() % 16 == 0 and
+            (bias is None or (bias.dtype == x.dtype and bias.numel() == x.size(-1))))
+
+
+def bias_dropout_add(x: torch.Tensor, bias: Optional[torch.Tensor], residual: torch.Tensor, prob: float,
+                     training: bool) -> torch.Tensor:
+    """``residual + dropout(x + bias, prob, training)``; fused HIP kernels on GPU, PyTorch on CPU."""
+    p = float(prob) if training else 0.0
+    if _bda_native_ok(x, bias, residual):
+        return _BiasDropoutAddFn.apply(x, bias, residual, p)
+    out = F.dropout(x + bias if bias is not None else x, p=prob, training=training)
+    return residual + out

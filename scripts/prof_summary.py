@@ -45,7 +45,7 @@ def main():
     agg = collections.defaultdict(lambda: [0, 0])
     busy = 0
     for s, e, name in seg:
-        short = re.sub(r"\(.*", "", name)[:110]
+        short = re.sub(r"\(.*", "", name.replace("(anonymous namespace)::", ""))[:110]
         agg[short][0] += e - s
         agg[short][1] += 1
         busy += e - s
@@ -61,7 +61,7 @@ def main():
     last = rows[marks[-2] + 1: marks[-1] + 1] if len(marks) >= 2 else seg
     per = collections.defaultdict(list)
     for s_, e_, name in last:
-        per[re.sub(r"\(.*", "", name)[:110]].append(round((e_ - s_) / 1e3, 1))
+        per[re.sub(r"\(.*", "", name.replace("(anonymous namespace)::", ""))[:110]].append(round((e_ - s_) / 1e3, 1))
     lines.append("\n## per-launch us (last step, launch order) for kernels > 0.5 ms/step\n")
     for k, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0]):
         if t / n / 1e6 < 0.5:
