@@ -603,6 +603,9 @@ def post_language_model_processing(lm_output, labels, logit_weights, parallel_ou
     if fp16_lm_cross_entropy:
         assert output.dtype == torch.half
         loss = tensor_parallel.vocab_parallel_cross_entropy(output, labels)
+    elif output.is_cuda:
+        # fp32 math inside the kernels and an fp32 loss, without materialising fp32 logits
+        loss = tensor_parallel.vocab_parallel_cross_entropy(output, labels, loss_dtype=torch.float32)
     else:
         loss = tensor_parallel.vocab_parallel_cross_entropy(output.float(), labels)
     return loss.transpose(0, 1).contiguous()  # [b, s]
@@ -709,8 +712,13 @@ class BertModel(MegatronModule):
         if lm_labels is None:
             return lm_logits.transpose(0, 1).contiguous(), binary_logits
         labels = lm_labels.transpose(0, 1).contiguous()
-        logits = lm_logits if self.fp16_lm_cross_entropy else lm_logits.float()
-        loss = tensor_parallel.vocab_parallel_cross_entropy(logits, labels).transpose(0, 1).contiguous()
+        if self.fp16_lm_cross_entropy:
+            loss = tensor_parallel.vocab_parallel_cross_entropy(lm_logits, labels)
+        elif lm_logits.is_cuda:  # fp32 math in the kernels, fp32 loss, no fp32 copy of the logits
+            loss = tensor_parallel.vocab_parallel_cross_entropy(lm_logits, labels, loss_dtype=torch.float32)
+        else:
+            loss = tensor_parallel.vocab_parallel_cross_entropy(lm_logits.float(), labels)
+        loss = loss.transpose(0, 1).contiguous()
         return loss, binary_logits
 
 

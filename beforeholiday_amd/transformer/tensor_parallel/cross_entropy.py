@@ -35,7 +35,7 @@ def _combine_ref(gathered, out_dtype):
 
 class _VocabParallelCrossEntropy(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, vocab_parallel_logits, target):
+    def forward(ctx, vocab_parallel_logits, target, loss_dtype=None):
         V = vocab_parallel_logits.size(-1)
         rank = get_tensor_model_parallel_rank()
         world = get_tensor_model_parallel_world_size()
@@ -54,10 +54,11 @@ class _VocabParallelCrossEntropy(torch.autograd.Function):
                                                      group=get_tensor_model_parallel_group())
         else:
             gathered = stats.unsqueeze(0)
+        out_dtype = loss_dtype or vocab_parallel_logits.dtype
         if native:
-            loss, lse = xent.vocab_parallel_combine(gathered, vocab_parallel_logits.dtype)
+            loss, lse = xent.vocab_parallel_combine(gathered, out_dtype)
         else:
-            loss, lse = _combine_ref(gathered, vocab_parallel_logits.dtype)
+            loss, lse = _combine_ref(gathered, out_dtype)
         ctx.start = start
         ctx.save_for_backward(logits2d, lse, target1d)
         ctx.shape = vocab_parallel_logits.shape
@@ -76,9 +77,12 @@ class _VocabParallelCrossEntropy(torch.autograd.Function):
             inside = (local >= 0) & (local < V)
             p[torch.arange(p.size(0))[inside], local[inside]] -= 1.0
             dx = (p * g.float().unsqueeze(-1)).to(logits2d.dtype)
-        return dx.view(ctx.shape), None
+        return dx.view(ctx.shape), None, None
 
 
-def vocab_parallel_cross_entropy(vocab_parallel_logits, target):
-    """Per-token loss of logits sharded along the vocab over the TP group. Shapes [..., V/tp], [...]."""
-    return _VocabParallelCrossEntropy.apply(vocab_parallel_logits, target)
+def vocab_parallel_cross_entropy(vocab_parallel_logits, target, loss_dtype=None):
+    """Per-token loss of logits sharded along the vocab over the TP group. Shapes [..., V/tp], [...].
+    The kernels accumulate in fp32 whatever the logits dtype; ``loss_dtype`` (default: the logits
+    dtype) only sets the dtype of the returned loss, so 16-bit logits need no fp32 copy (the
+    gradient comes back in the logits dtype)."""
+    return _VocabParallelCrossEntropy.apply(vocab_parallel_logits, target, loss_dtype)

@@ -296,3 +296,31 @@ def test_flash_attention_matches_unfused_megatron_path(kind):
     """CoreAttention on the MFMA flash kernels (causal for GPT, -10000 padding fill for BERT) == the
     bmm + fused-softmax + bmm path."""
     run_distributed(_flash_vs_unfused, 1, kind)
+
+
+@pytest.mark.gpu
+def test_vocab_ce_16bit_logits_fp32_loss_matches_fp32_logits():
+    """bf16 logits + loss_dtype=fp32 (no fp32 logits copy) == the .float() path: same loss, same grad."""
+    from beforeholiday_amd.transformer import parallel_state as ps
+    from beforeholiday_amd.transformer import tensor_parallel as tp
+
+    ps.set_tensor_model_parallel_rank(0)
+    ps.set_tensor_model_parallel_world_size(1)
+    try:
+        torch.manual_seed(0)
+        logits = (torch.randn(64, 4, 50304, device="cuda") * 3).to(torch.bfloat16)
+        labels = torch.randint(0, 50304, (64, 4), device="cuda")
+        a = logits.clone().requires_grad_(True)
+        b = logits.clone().requires_grad_(True)
+        la = tp.vocab_parallel_cross_entropy(a, labels, loss_dtype=torch.float32)
+        lb = tp.vocab_parallel_cross_entropy(b.float(), labels)
+        assert la.dtype == torch.float32
+        torch.testing.assert_close(la, lb, atol=1e-5, rtol=1e-5)
+        g = torch.randn_like(la)
+        la.backward(g)
+        lb.backward(g)
+        assert a.grad.dtype == torch.bfloat16
+        torch.testing.assert_close(a.grad.float(), b.grad.float(), atol=1e-2, rtol=1e-2)
+    finally:
+        ps.set_tensor_model_parallel_rank(None)
+        ps.set_tensor_model_parallel_world_size(None)
