@@ -37,15 +37,21 @@ def main():
     ap.add_argument("--sp", action="store_true", help="sequence parallelism inside the TP group")
     ap.add_argument("--opt-level", default="O5", choices=["O2", "O5"])
     ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI; gloo only to rehearse multi-rank TP/SP on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29534")
-    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+    if args.backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     tp = args.tp or world
     assert world % tp == 0, f"world {world} not divisible by tp {tp}"
     dp = world // tp
@@ -59,7 +65,7 @@ def main():
     from beforeholiday_amd.transformer.pipeline_parallel.utils import get_ltor_masks_and_position_ids
 
     require_native("bench_gpt")
-    parallel_state.initialize_model_parallel(tp, 1)
+    parallel_state.initialize_model_parallel(tp, 1, default_backend=args.backend)
     tensor_parallel.model_parallel_cuda_manual_seed(1234)
     fp16 = args.opt_level == "O2"
     cfg = TransformerConfig(hidden_size=1024, num_layers=args.layers, num_attention_heads=16, ffn_hidden_size=4096,
@@ -104,7 +110,7 @@ def main():
     el = float(el)
     toks = B * dp * S * args.steps / el
     # 6*N*T matmul FLOPs + causal attention (12*L*h*S per token, halved by the causal skip)
-    nparams = 354_871_296
+    nparams = 50304 * 1024 + S * 1024 + 2048 + args.layers * 12_596_224  # whole model (355 M at 24 x 1024)
     flops_per_tok = 6 * nparams + 6 * args.layers * 1024 * S
     if rank == 0:
         print(json.dumps({
@@ -116,7 +122,7 @@ def main():
             "config": {"model": f"GPT-2-medium ({args.layers} layers, {nparams_local / 1e6:.0f}M params per TP rank) "
                        "+ FusedAdam", "global_batch": B * dp, "seq_len": S,
                        "parallelism": f"tp{tp}{'-sp' if cfg.sequence_parallel else ''}-dp{dp}",
-                       "final_loss": round(float(loss), 4)}}), flush=True)
+                       "final_loss": round(float(loss.detach()), 4)}}), flush=True)
     dist.destroy_process_group()
 
 
