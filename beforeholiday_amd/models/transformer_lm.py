@@ -368,9 +368,9 @@ class ParallelAttention(MegatronModule):
         return self.dense(ctx)
 
 
-def bias_dropout_add(x, bias, residual, prob: float, training: bool):
+def bias_dropout_add(x, bias, residual, prob: float, training: bool, seed_offset: int = 0):
     """residual + dropout(x + bias): one fused HIP pass on GPU (ops/fused_dense.py), PyTorch on CPU."""
-    return _fd.bias_dropout_add(x, bias, residual, prob, training)
+    return _fd.bias_dropout_add(x, bias, residual, prob, training, seed_offset)
 
 
 class ParallelTransformerLayer(MegatronModule):
@@ -384,6 +384,7 @@ class ParallelTransformerLayer(MegatronModule):
         self.apply_residual_connection_post_layernorm = config.apply_residual_connection_post_layernorm
         self.fp32_residual_connection = config.fp32_residual_connection
         self.hidden_dropout = config.hidden_dropout
+        self.sequence_parallel = config.sequence_parallel
         ln = dict(eps=config.layernorm_epsilon, sequence_parallel_enabled=config.sequence_parallel)
         self.input_layernorm = LayerNorm(config.hidden_size, **ln)
         self.self_attention = ParallelAttention(config, init_method, output_layer_init_method, layer_number,
@@ -396,7 +397,12 @@ class ParallelTransformerLayer(MegatronModule):
         self.mlp = ParallelMLP(config, init_method, output_layer_init_method)
 
     def _bda(self, out, bias, residual):
-        return bias_dropout_add(out, bias, residual, self.hidden_dropout, self.training)
+        # sequence parallel: each TP rank holds a different sequence shard -> its own dropout mask
+        # (Megatron forks the model-parallel RNG here); otherwise the replicas must agree
+        off = 0
+        if self.sequence_parallel:
+            off = 1_000_003 * parallel_state.get_tensor_model_parallel_rank()
+        return bias_dropout_add(out, bias, residual, self.hidden_dropout, self.training, off)
 
     def forward(self, hidden_states, attention_mask, encoder_output=None, enc_dec_attn_mask=None):
         ln_out = self.input_layernorm(hidden_states)

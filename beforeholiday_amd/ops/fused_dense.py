@@ -159,8 +159,9 @@ class _BiasDropoutAddFn(torch.autograd.Function):
     reference: apex/transformer/testing/standalone_transformer_lm.py:188-207 bias_dropout_add)."""
 
     @staticmethod
-    def forward(ctx, x, bias, residual, p):
-        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())  # host generator: no device sync
+    def forward(ctx, x, bias, residual, p, seed_offset=0):
+        # host generator (no device sync; identical on ranks seeded alike, so TP replicas agree)
+        seed = (int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) + seed_offset) % (2 ** 31 - 1)
         out, keep = _fd().bias_dropout_add(x, bias, residual, p, seed)
         ctx.save_for_backward(keep)
         ctx.p = p
@@ -172,7 +173,7 @@ class _BiasDropoutAddFn(torch.autograd.Function):
         (keep,) = ctx.saved_tensors
         want_b = ctx.has_bias and ctx.needs_input_grad[1]
         dx, db = _fd().dropout_backward(dout, keep, ctx.p, want_b)
-        return dx.view_as(dout), (db if want_b else None), dout, None
+        return dx.view_as(dout), (db if want_b else None), dout, None, None
 
 
 def _bda_native_ok(x, bias, residual) -> bool:
@@ -184,10 +185,11 @@ def _bda_native_ok(x, bias, residual) -> bool:
 
 
 def bias_dropout_add(x: torch.Tensor, bias: Optional[torch.Tensor], residual: torch.Tensor, prob: float,
-                     training: bool) -> torch.Tensor:
-    """``residual + dropout(x + bias, prob, training)``; fused HIP kernels on GPU, PyTorch on CPU."""
+                     training: bool, seed_offset: int = 0) -> torch.Tensor:
+    """``residual + dropout(x + bias, prob, training)``; fused HIP kernels on GPU, PyTorch on CPU.
+    ``seed_offset`` decorrelates the masks of ranks that hold different shards (sequence parallel)."""
     p = float(prob) if training else 0.0
     if _bda_native_ok(x, bias, residual):
-        return _BiasDropoutAddFn.apply(x, bias, residual, p)
+        return _BiasDropoutAddFn.apply(x, bias, residual, p, int(seed_offset))
     out = F.dropout(x + bias if bias is not None else x, p=prob, training=training)
     return residual + out
