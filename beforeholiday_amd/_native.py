@@ -25,6 +25,7 @@ def native():
         _tried = True
         try:
             _C = importlib.import_module("beforeholiday_amd._C")
+            _register_exit_cleanup(_C)
         except Exception as e:  # pragma: no cover - depends on the build
             _err = e
             _C = None
@@ -35,6 +36,16 @@ def native():
                 _C = importlib.import_module("beforeholiday_amd._C")
                 _err = None
     return _C
+
+
+def _register_exit_cleanup(mod):
+    """Release the multi-tensor plan cache (device + pinned tensors) at interpreter exit while
+    PyTorch's allocators are still alive (the C++ cache itself is never destroyed)."""
+    import atexit
+
+    fn = getattr(getattr(mod, "amp_C", None), "clear_plan_cache", None)
+    if fn is not None:
+        atexit.register(fn)
 
 
 def available() -> bool:

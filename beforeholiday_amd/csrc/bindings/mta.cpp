@@ -21,7 +21,10 @@ struct KeyHash {
 };
 
 std::mutex g_plan_mu;
-std::unordered_map<std::vector<int64_t>, MTAPlan, KeyHash> g_plans;
+// Heap-allocated and never destroyed: the cached plans own device / pinned tensors, and a static
+// destructor running at process exit would free them into PyTorch's caching allocators after those
+// were torn down (an exit-time segfault). clear_plan_cache() releases them while torch is alive.
+auto& g_plans = *new std::unordered_map<std::vector<int64_t>, MTAPlan, KeyHash>();
 constexpr size_t kMaxPlans = 4096;
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -477,6 +480,10 @@ void plan_cache_clear() {
 void register_amp_C(pybind11::module_& root) {
   namespace py = pybind11;
   auto m = root.def_submodule("amp_C", "multi-tensor apply kernels (gfx950)");
+  m.def("clear_plan_cache", [] {
+    std::lock_guard<std::mutex> lock(g_plan_mu);
+    g_plans.clear();
+  }, "drop the cached device-resident chunk plans (registered with atexit by the python package)");
   m.def("multi_tensor_scale", &multi_tensor_scale, "out = in * scale with overflow flag");
   m.def("multi_tensor_scale_tensor", &multi_tensor_scale_tensor, "out = in * scale[0] (device scalar)");
   m.def("multi_tensor_sgd", &multi_tensor_sgd, "fused SGD");

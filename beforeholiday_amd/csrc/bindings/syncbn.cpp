@@ -84,6 +84,30 @@ at::Tensor stats_local(at::Tensor x_in) {
   return out;
 }
 
+// local shifted sums -> [sum(x-K) (C), sum((x-K)^2) (C), count (1)] (the all_reduce SUM payload);
+// K = running_mean (shared by every rank), or 0 when stats are not tracked
+at::Tensor stats_local_sums(at::Tensor x_in, c10::optional<at::Tensor> running_mean) {
+  check_cuda(x_in, "input");
+  Layout L = layout_of(x_in);
+  const int C = L.s.C;
+  const int splits = bh::bn_num_splits(L.s);
+  const int64_t nslots = L.s.channels_last ? splits : (int64_t)splits * C;
+  auto part = at::empty({2 * (int64_t)splits * C + nslots}, fopt(L.x));
+  float* pm = part.data_ptr<float>();
+  float* pm2 = pm + (int64_t)splits * C;
+  float* pn = pm2 + (int64_t)splits * C;
+  auto out = at::empty({2 * (int64_t)C + 1}, fopt(L.x));
+  hipStream_t st = stream_for(L.x);
+  bh::bn_stats(L.s, dtype_code(L.x.scalar_type()), L.x.data_ptr(), splits, pm, pm2, pn, st);
+  const bool has_k = running_mean.has_value() && running_mean->defined();
+  if (has_k) TORCH_CHECK(running_mean->is_contiguous() && running_mean->numel() == C, "running_mean must be [C]");
+  bh::BNFinal fin{};
+  bh::bn_stats_finalize(L.s, splits, pm, pm2, pn, nullptr, fin, has_k ? dtype_code(running_mean->scalar_type()) : bh::kF32,
+                        nullptr, nullptr, nullptr, nullptr, st, has_k ? running_mean->data_ptr() : nullptr,
+                        out.data_ptr<float>());
+  return out;
+}
+
 // returns (mean, invstd, scale, shift, count)
 std::vector<at::Tensor> final_outputs(const at::Tensor& ref, int64_t C) {
   auto o = fopt(ref);
@@ -165,6 +189,26 @@ std::vector<at::Tensor> merge_ranks(at::Tensor gathered, c10::optional<at::Tenso
   bh::bn_merge_ranks(W, C, gathered.data_ptr<float>(), fin, dtw, wptr(w), wptr(b),
                      has_run ? rmean->data_ptr() : nullptr, has_run ? rvar->data_ptr() : nullptr, nullptr,
                      stream_for(gathered));
+  return r;
+}
+
+// finalize all-reduced shifted sums [2C+1] (+ running stats update, scale/shift)
+std::vector<at::Tensor> merge_sums(at::Tensor sums, c10::optional<at::Tensor> w, c10::optional<at::Tensor> b,
+                                   c10::optional<at::Tensor> rmean, c10::optional<at::Tensor> rvar, double momentum,
+                                   double eps, c10::optional<at::Tensor> num_batches) {
+  check_cuda(sums, "sums");
+  TORCH_CHECK(sums.dim() == 1 && sums.scalar_type() == at::kFloat && sums.numel() % 2 == 1, "sums must be fp32 [2C+1]");
+  sums = sums.contiguous();
+  check_running(rmean, rvar, w);
+  const int C = (int)((sums.numel() - 1) / 2);
+  auto r = final_outputs(sums, C);
+  auto fin = fin_of(r, eps, momentum);
+  fin.num_batches = counter_ptr(num_batches);
+  const bool has_run = rmean.has_value() && rmean->defined();
+  int dtw = wcode(w);
+  if (!(w.has_value() && w->defined()) && has_run) dtw = dtype_code(rmean->scalar_type());
+  bh::bn_merge_sums(C, sums.data_ptr<float>(), fin, dtw, wptr(w), wptr(b), has_run ? rmean->data_ptr() : nullptr,
+                    has_run ? rvar->data_ptr() : nullptr, stream_for(sums));
   return r;
 }
 
@@ -339,6 +383,10 @@ void register_syncbn(pybind11::module_& root) {
   m.def("merge_ranks", &merge_ranks, py::arg("gathered"), py::arg("weight"), py::arg("bias"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
         py::arg("num_batches") = py::none());
+  m.def("stats_local_sums", &stats_local_sums, py::arg("x"), py::arg("running_mean") = py::none(),
+        "local [sum(x-K), sum((x-K)^2), count] about K = running_mean (all_reduce SUM payload)");
+  m.def("merge_sums", &merge_sums, py::arg("sums"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"),
+        py::arg("running_var"), py::arg("momentum"), py::arg("eps"), py::arg("num_batches") = py::none());
   m.def("forward", &forward, py::arg("x"), py::arg("z"), py::arg("scale"), py::arg("shift"), py::arg("relu"),
         py::arg("out_dtype") = py::none(), py::arg("num_batches") = py::none());
   m.def("backward_reduce", &backward_reduce, py::arg("dy"), py::arg("x"), py::arg("z"), py::arg("mean"),

@@ -37,7 +37,11 @@ void bn_stats(const BNShape& s, int dt_x, const void* x, int splits, float* pmea
 // all_gather payload); fin (if fin.mean) receives the single-rank final values.
 void bn_stats_finalize(const BNShape& s, int splits, const float* pmean, const float* pm2, const float* pn,
                        float* out_local, const BNFinal& fin, int dt_w, const void* w, const void* b, void* rmean,
-                       void* rvar, hipStream_t st);
+                       void* rvar, hipStream_t st, const void* kref = nullptr, float* out_sums = nullptr);
+// out_sums (optional, [2C+1]): the all_reduce(SUM) payload [sum(x-K), sum((x-K)^2), n] about the shared
+// per-channel reference K = kref (dtype dt_w; null = 0), finalized by bn_merge_sums after the reduction
+void bn_merge_sums(int C, const float* sums, const BNFinal& fin, int dt_w, const void* w, const void* b, void* rmean,
+                   void* rvar, hipStream_t st);
 // merge W gathered rows [W][2C+1] into final stats (+ running stats update, scale/shift)
 void bn_merge_ranks(int W, int C, const float* gathered, const BNFinal& fin, int dt_w, const void* w,
                     const void* b, void* rmean, void* rvar, float* var_unbiased, hipStream_t st);

@@ -227,7 +227,8 @@ template <typename Tw>
 __global__ __launch_bounds__(64 * kFinLanes) void k_stats_finalize(int C, int splits, bool per_channel_n,
                                                            const float* __restrict__ pmean, const float* __restrict__ pm2,
                                                            const float* __restrict__ pn, float* __restrict__ out_local,
-                                                           BNFinal fin, const Tw* w, const Tw* b, Tw* rmean, Tw* rvar) {
+                                                           BNFinal fin, const Tw* w, const Tw* b, Tw* rmean, Tw* rvar,
+                                                           const Tw* kref, float* __restrict__ out_sums) {
   // 64 channels x kFinLanes split-lanes per block. The split partials were written by workgroups on
   // all 8 XCDs, so every load here is a cross-XCD miss (~1 us): the merge is written as plain sums
   // about a common shift K (split 0's mean) -- S1 = sum n_s (m_s - K), S2 = sum m2_s + n_s (m_s - K)^2
@@ -287,6 +288,15 @@ __global__ __launch_bounds__(64 * kFinLanes) void k_stats_finalize(int C, int sp
     out_local[C + c] = var_b;
     if (c == 0) out_local[2 * C] = acc.n;
   }
+  if (out_sums) {
+    // all_reduce(SUM) payload: sums about a per-channel reference K that every rank shares (the
+    // running mean, identical on all ranks) -- [sum(x-K) (C), sum((x-K)^2) (C), count (1)]
+    const float kc = kref ? to_f<Tw>(kref[c]) : 0.f;
+    const float d = acc.mean - kc;
+    out_sums[c] = acc.n * d;
+    out_sums[C + c] = fmaf(acc.n * d, d, acc.m2);
+    if (c == 0) out_sums[2 * C] = acc.n;
+  }
   if (fin.mean) {
     const float invstd = rsqrtf(var_b + fin.eps);
     fin.mean[c] = acc.mean;
@@ -340,6 +350,35 @@ __global__ __launch_bounds__(kBlock) void k_merge_ranks(int W, int C, const floa
     rvar[c] = from_f<Tw>((1.f - mom) * to_f<Tw>(rvar[c]) + mom * unb);
   }
   bn_count_batch(fin, c);
+}
+
+// finalize all-reduced [sum(x-K), sum((x-K)^2), n] with K = running mean (read before the update)
+template <typename Tw>
+__global__ __launch_bounds__(kBlock) void k_merge_sums(int C, const float* __restrict__ sums, BNFinal fin,
+                                                       const Tw* w, const Tw* b, Tw* rmean, Tw* rvar) {
+  const int c = blockIdx.x * kBlock + threadIdx.x;
+  if (c >= C) return;
+  const float n = sums[2 * C];
+  const float s1 = sums[c], s2 = sums[C + c];
+  const float kc = rmean ? to_f<Tw>(rmean[c]) : 0.f;
+  const float dm = n > 0.f ? s1 / n : 0.f;
+  const float mean = kc + dm;
+  const float m2 = fmaxf(s2 - s1 * dm, 0.f);
+  const float var_b = n > 0.f ? m2 / n : 0.f;
+  const float unb = n > 1.f ? m2 / (n - 1.f) : var_b;
+  const float invstd = rsqrtf(var_b + fin.eps);
+  fin.mean[c] = mean;
+  fin.invstd[c] = invstd;
+  if (fin.count && c == 0) fin.count[0] = n;
+  const float wv = w ? to_f<Tw>(w[c]) : 1.f;
+  const float bv = b ? to_f<Tw>(b[c]) : 0.f;
+  fin.scale[c] = wv * invstd;
+  fin.shift[c] = bv - mean * wv * invstd;
+  if (rmean) {
+    const float mom = bn_momentum(fin);
+    rmean[c] = from_f<Tw>((1.f - mom) * kc + mom * mean);
+    rvar[c] = from_f<Tw>((1.f - mom) * to_f<Tw>(rvar[c]) + mom * unb);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -837,12 +876,13 @@ void bn_stats(const BNShape& s, int dt_x, const void* x, int splits, float* pmea
 
 void bn_stats_finalize(const BNShape& s, int splits, const float* pmean, const float* pm2, const float* pn,
                        float* out_local, const BNFinal& fin, int dt_w, const void* w, const void* b, void* rmean,
-                       void* rvar, hipStream_t st) {
+                       void* rvar, hipStream_t st, const void* kref, float* out_sums) {
   const int grid = (s.C + 63) / 64;
   const bool per_channel_n = !s.channels_last;
   BN_DISPATCH(dt_w, Tw,
       hipLaunchKernelGGL((k_stats_finalize<Tw>), dim3(grid), dim3(64 * kFinLanes), 0, st, s.C, splits, per_channel_n, pmean, pm2,
-                         pn, out_local, fin, (const Tw*)w, (const Tw*)b, (Tw*)rmean, (Tw*)rvar));
+                         pn, out_local, fin, (const Tw*)w, (const Tw*)b, (Tw*)rmean, (Tw*)rvar, (const Tw*)kref,
+                         out_sums));
   check_launch("bn_stats_finalize");
 }
 
@@ -853,6 +893,15 @@ void bn_merge_ranks(int W, int C, const float* gathered, const BNFinal& fin, int
       hipLaunchKernelGGL((k_merge_ranks<Tw>), dim3(grid), dim3(kBlock), 0, st, W, C, gathered, fin, (const Tw*)w,
                          (const Tw*)b, (Tw*)rmean, (Tw*)rvar, var_unbiased));
   check_launch("bn_merge_ranks");
+}
+
+void bn_merge_sums(int C, const float* sums, const BNFinal& fin, int dt_w, const void* w, const void* b, void* rmean,
+                   void* rvar, hipStream_t st) {
+  const int grid = (C + kBlock - 1) / kBlock;
+  BN_DISPATCH(dt_w, Tw,
+      hipLaunchKernelGGL((k_merge_sums<Tw>), dim3(grid), dim3(kBlock), 0, st, C, sums, fin, (const Tw*)w, (const Tw*)b,
+                         (Tw*)rmean, (Tw*)rvar));
+  check_launch("bn_merge_sums");
 }
 
 void bn_forward(const BNShape& s, int dt_x, const void* x, int dt_z, const void* z, int dt_y, void* y,

@@ -67,15 +67,22 @@ __global__ __launch_bounds__(256) void k_act_fwd(const T* __restrict__ x, const 
   }
 }
 
-// counter-based dropout bits: one 32-bit hash per element index (seed-keyed), keep iff u >= p
-BH_DEVICE uint32_t bda_hash(uint32_t seed, uint64_t i) {
-  uint32_t h = seed ^ (uint32_t)i ^ ((uint32_t)(i >> 32) * 0x9E3779B9u);
+BH_DEVICE uint32_t fmix32(uint32_t h) {
   h ^= h >> 16;
   h *= 0x7feb352du;
   h ^= h >> 15;
   h *= 0x846ca68bu;
   h ^= h >> 16;
   return h;
+}
+
+// counter-based dropout bits: one 32-bit keyed hash per element index, keep iff u >= p. The seed is
+// mixed into a key first and enters both rounds non-linearly, so two seeds give unrelated streams
+// (XOR-ing a raw seed into the index would make every seed's mask a permutation of the same bits).
+BH_DEVICE uint32_t bda_hash(uint32_t seed, uint64_t i) {
+  const uint32_t k = fmix32(seed * 0x9E3779B9u + 0x632BE5ABu);
+  const uint32_t h = fmix32((uint32_t)i ^ k);
+  return fmix32(h + k * 0x85EBCA6Bu + (uint32_t)(i >> 32) * 0xC2B2AE35u);
 }
 
 // out = residual + dropout(x + bias) with the keep bits stored 1 per element (uint8 [M*N/8]).

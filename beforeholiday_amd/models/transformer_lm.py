@@ -368,9 +368,9 @@ class ParallelAttention(MegatronModule):
         return self.dense(ctx)
 
 
-def bias_dropout_add(x, bias, residual, prob: float, training: bool, seed_offset: int = 0):
+def bias_dropout_add(x, bias, residual, prob: float, training: bool, model_parallel: bool = False):
     """residual + dropout(x + bias): one fused HIP pass on GPU (ops/fused_dense.py), PyTorch on CPU."""
-    return _fd.bias_dropout_add(x, bias, residual, prob, training, seed_offset)
+    return _fd.bias_dropout_add(x, bias, residual, prob, training, model_parallel)
 
 
 class ParallelTransformerLayer(MegatronModule):
@@ -399,10 +399,7 @@ class ParallelTransformerLayer(MegatronModule):
     def _bda(self, out, bias, residual):
         # sequence parallel: each TP rank holds a different sequence shard -> its own dropout mask
         # (Megatron forks the model-parallel RNG here); otherwise the replicas must agree
-        off = 0
-        if self.sequence_parallel:
-            off = 1_000_003 * parallel_state.get_tensor_model_parallel_rank()
-        return bias_dropout_add(out, bias, residual, self.hidden_dropout, self.training, off)
+        return bias_dropout_add(out, bias, residual, self.hidden_dropout, self.training, self.sequence_parallel)
 
     def forward(self, hidden_states, attention_mask, encoder_output=None, enc_dec_attn_mask=None):
         ln_out = self.input_layernorm(hidden_states)

@@ -159,9 +159,12 @@ class _BiasDropoutAddFn(torch.autograd.Function):
     reference: apex/transformer/testing/standalone_transformer_lm.py:188-207 bias_dropout_add)."""
 
     @staticmethod
-    def forward(ctx, x, bias, residual, p, seed_offset=0):
-        # host generator (no device sync; identical on ranks seeded alike, so TP replicas agree)
-        seed = (int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) + seed_offset) % (2 ** 31 - 1)
+    def forward(ctx, x, bias, residual, p, model_parallel=False):
+        # host-side seed stream (no device sync): "replicated" is identical on every TP rank,
+        # "model-parallel" differs per TP rank (sequence-parallel shards); see random.dropout_seed
+        from ..transformer.tensor_parallel.random import dropout_seed
+
+        seed = dropout_seed(model_parallel)
         out, keep = _fd().bias_dropout_add(x, bias, residual, p, seed)
         ctx.save_for_backward(keep)
         ctx.p = p
@@ -185,11 +188,21 @@ def _bda_native_ok(x, bias, residual) -> bool:
 
 
 def bias_dropout_add(x: torch.Tensor, bias: Optional[torch.Tensor], residual: torch.Tensor, prob: float,
-                     training: bool, seed_offset: int = 0) -> torch.Tensor:
-    """``residual + dropout(x + bias, prob, training)``; fused HIP kernels on GPU, PyTorch on CPU.
-    ``seed_offset`` decorrelates the masks of ranks that hold different shards (sequence parallel)."""
+                     training: bool, model_parallel: bool = False) -> torch.Tensor:
+    """``residual + dropout(x + bias, prob, training)``; fused HIP kernels on GPU, PyTorch otherwise.
+
+    ``model_parallel=True`` (sequence parallelism: every TP rank holds a different shard) draws the
+    mask from the per-TP-rank stream -- the fused kernel's model-parallel seed stream, or the
+    tracker's "model-parallel-rng" state for the PyTorch fallback; otherwise TP replicas draw
+    identical masks from the replicated stream."""
     p = float(prob) if training else 0.0
     if _bda_native_ok(x, bias, residual):
-        return _BiasDropoutAddFn.apply(x, bias, residual, p, int(seed_offset))
-    out = F.dropout(x + bias if bias is not None else x, p=prob, training=training)
+        return _BiasDropoutAddFn.apply(x, bias, residual, p, bool(model_parallel))
+    if model_parallel and training and prob > 0:
+        from ..transformer.tensor_parallel.random import get_cuda_rng_tracker
+
+        with get_cuda_rng_tracker().fork():
+            out = F.dropout(x + bias if bias is not None else x, p=prob, training=training)
+    else:
+        out = F.dropout(x + bias if bias is not None else x, p=prob, training=training)
     return residual + out

@@ -83,6 +83,34 @@ def merge_ranks(gathered, weight, bias, running_mean, running_var, momentum, eps
     return _ref_final(mean, var_b, float(n), weight, bias, running_mean, running_var, momentum, eps, num_batches)
 
 
+def stats_local_sums(x, running_mean=None):
+    """Local ``[sum(x-K) (C), sum((x-K)^2) (C), count (1)]`` about ``K = running_mean`` (0 if None).
+
+    This is the ``all_reduce(SUM)`` payload of the multi-rank forward: one fixed-size collective
+    instead of an all_gather of W rows plus a merge. ``K`` must be the same on every rank (the
+    running mean is: it starts at 0 and is updated from the reduced statistics only), and keeps the
+    sums centred so ``E[(x-K)^2] - E[x-K]^2`` does not cancel."""
+    if x.is_cuda:
+        return _native().stats_local_sums(x, running_mean)
+    mean, var_b, n = _ref_stats(x)
+    k = running_mean.float() if running_mean is not None else torch.zeros_like(mean)
+    d = mean - k
+    return torch.cat([n * d, n * var_b + n * d * d, torch.tensor([n], dtype=torch.float32, device=x.device)])
+
+
+def merge_sums(sums, weight, bias, running_mean, running_var, momentum, eps, num_batches=None):
+    """Final stats from all-reduced :func:`stats_local_sums` -> [mean, invstd, scale, shift, count]."""
+    if sums.is_cuda:
+        return _native().merge_sums(sums, weight, bias, running_mean, running_var, momentum, eps, num_batches)
+    C = (sums.numel() - 1) // 2
+    s1, s2, n = sums[:C], sums[C:2 * C], float(sums[2 * C])
+    k = running_mean.float() if running_mean is not None else torch.zeros_like(s1)
+    dm = s1 / n
+    mean = k + dm
+    var_b = torch.clamp(s2 - s1 * dm, min=0) / n
+    return _ref_final(mean, var_b, n, weight, bias, running_mean, running_var, momentum, eps, num_batches)
+
+
 def forward(x, z, scale, shift, relu, out_dtype=None, num_batches=None):
     """y = x*scale + shift (+z) (relu); increments ``num_batches`` (num_batches_tracked) if given."""
     if x.is_cuda:

@@ -14,6 +14,8 @@ MI355X / RCCL design:
 * collectives are issued with ``async_op=True`` on the RCCL backend: RCCL runs them on its own HIP
   stream, so bucket all-reduces overlap the remaining backward kernels without a hand-managed side
   stream; the end-of-backward callback makes the compute stream wait on each work handle.
+* buckets can be cut by BYTES (``bucket_cap_mb``, plus a smaller ``first_bucket_mb``) instead of the
+  reference's element count, sized per xGMI peer (:func:`xgmi_bucket_mb`).
 * averaging uses ``ReduceOp.AVG`` inside the collective when the backend supports it (RCCL), so no
   extra scaling kernel runs per bucket.
 * each bucket owns a persistent flat buffer: the gather is one ``torch.cat(out=)`` and the scatter
@@ -30,6 +32,22 @@ import torch
 import torch.distributed as dist
 from torch.nn.modules import Module
 from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
+
+from . import comm_stats
+
+
+def xgmi_bucket_mb(world_size: int, grad_bytes: int, min_per_peer_mb: float = 2.0, max_buckets: int = 8):
+    """(bucket_cap_mb, first_bucket_mb) for a fully connected xGMI node.
+
+    A ring all-reduce of B bytes over W ranks moves B/W-byte slices per step on one link, so each
+    slice must be >= ~``min_per_peer_mb`` MB to stay bandwidth-bound (~153 GB/s per link) rather
+    than latency-bound -> bucket >= W * min_per_peer_mb. At most ``max_buckets`` buckets keep the
+    per-collective launch/latency overhead small; the first bucket is 1/4 size so communication
+    starts early in backward.
+    """
+    total_mb = grad_bytes / 2 ** 20
+    cap = max(world_size * min_per_peer_mb, total_mb / max_buckets)
+    return cap, max(world_size * min_per_peer_mb / 4, cap / 4)
 
 
 def _raw(t: torch.Tensor) -> torch.Tensor:
@@ -168,7 +186,7 @@ class DistributedDataParallel(Module):
                  allreduce_trigger_params=None, retain_allreduce_buffers=False, allreduce_always_fp32=False,
                  num_allreduce_streams=1, allreduce_communicators=None, gradient_average=True,
                  gradient_predivide_factor=1.0, gradient_average_split_factor=None, prof=False,
-                 process_group=None):
+                 process_group=None, bucket_cap_mb=None, first_bucket_mb=None):
         super().__init__()
         if shared_param is not None:
             raise ValueError("shared_param is no longer supported as an option.  It was misleadingly named "
@@ -185,6 +203,11 @@ class DistributedDataParallel(Module):
         self.world_size = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
         self.message_size = int(message_size)
+        # byte-based bucket policy (MI355X): ``bucket_cap_mb`` replaces the element-count
+        # ``message_size`` cut; ``first_bucket_mb`` makes the first bucket of each dtype small so its
+        # all-reduce starts while most of backward is still ahead. See :func:`xgmi_bucket_mb`.
+        self.bucket_cap_bytes = int(float(bucket_cap_mb) * 2 ** 20) if bucket_cap_mb else None
+        self.first_bucket_bytes = int(float(first_bucket_mb) * 2 ** 20) if first_bucket_mb else None
         self.delay_allreduce = delay_allreduce
         self.retain_allreduce_buffers = retain_allreduce_buffers
         self.allreduce_always_fp32 = allreduce_always_fp32
@@ -321,11 +344,22 @@ class DistributedDataParallel(Module):
             self._launch(self._next_bucket)
             self._next_bucket += 1
 
+    def _cut_threshold(self, dtype, n_closed: int) -> int:
+        """Bucket size (elements) for the next bucket of ``dtype`` after ``n_closed`` closed ones."""
+        esize = torch.empty((), dtype=dtype).element_size()
+        if n_closed == 0 and self.first_bucket_bytes:
+            return max(1, self.first_bucket_bytes // esize)
+        if self.bucket_cap_bytes:
+            return max(1, self.bucket_cap_bytes // esize)
+        return self.message_size
+
     def _build_buckets(self, order: List[int]):
-        """Cut buckets from an arrival order (per dtype, message_size elements or trigger params)."""
+        """Cut buckets from an arrival order (per dtype; message_size elements, bucket_cap_mb bytes,
+        or trigger params)."""
         seen = set(order)
         order = list(order) + [i for i in range(len(self.active_params)) if i not in seen]
         open_b = {}
+        closed = {}
         buckets = []
         for idx in order:
             p = self.active_params[idx]
@@ -337,10 +371,15 @@ class DistributedDataParallel(Module):
             b.params.append(idx)
             b.numel += p.numel()
             cut = (id(p) in self.allreduce_trigger_params) if self.custom_allreduce_triggers else \
-                (b.numel >= self.message_size)
+                (b.numel >= self._cut_threshold(p.dtype, closed.get(p.dtype, 0)))
             if cut:
                 open_b.pop(p.dtype)
+                closed[p.dtype] = closed.get(p.dtype, 0) + 1
         return buckets
+
+    def bucket_sizes(self):
+        """(dtype, elements) of each bucket, in all-reduce order (empty before the first backward)."""
+        return [(b.dtype, b.numel) for b in self._buckets]
 
     def _sync_bucket_structure(self, buckets):
         """Broadcast rank 0's bucket structure: [nb, sizes(nb), param indices...] padded to 1+2P."""
@@ -392,7 +431,8 @@ class DistributedDataParallel(Module):
     def _finish(self, b_idx):
         b = self._buckets[b_idx]
         if b.work is not None:
-            b.work.wait()
+            with comm_stats.timed("ddp_wait", b.flat):
+                b.work.wait()
             b.work = None
         tensor, grads = b.outputs
         if self.gradient_average and not self._use_avg:

@@ -1,9 +1,10 @@
 """SyncBatchNorm (reference: apex/parallel/optimized_sync_batchnorm.py:9-85 and
 optimized_sync_batchnorm_kernel.py:7-119).
 
-Training forward: local Welford statistics (HIP kernel) -> all_gather of the [mean, var_biased,
-count] rows over the process group -> rank merge + running-stat update + per-channel scale/shift
-(one tiny kernel) -> a single fused  y = x*scale + shift (+ z) (ReLU)  pass. Backward: one reduce
+Training forward: local Welford statistics (HIP kernel) -> ONE fixed-size [2C+1] SUM all-reduce of
+sums centred on the running mean (``BH_SYNCBN_STATS=allgather`` selects the reference's all_gather of
+[mean, var_biased, count] rows + Welford merge instead) -> finalize + running-stat update +
+per-channel scale/shift (one tiny kernel) -> a single fused  y = x*scale + shift (+ z) (ReLU)  pass. Backward: one reduce
 kernel (ReLU mask recomputed from x, no masked-dy tensor), all_reduce of [sum_dy, sum_dy_xmu],
 one dgrad kernel that also emits dz for the fused residual branch (BN + add + ReLU saves a 1-bit
 ReLU mask in the forward, so neither backward pass reads z). With a single rank the
@@ -11,12 +12,30 @@ collectives are skipped and the merge is fused into the statistics finalize.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 from torch.nn import functional as F
 from torch.nn.modules.batchnorm import _BatchNorm
 
 from ..ops import syncbn
+from . import comm_stats
+
+_STATS_MODE = os.environ.get("BH_SYNCBN_STATS", "allreduce")
+
+
+def stats_mode() -> str:
+    """How ranks combine forward statistics: ``"allreduce"`` (default; one [2C+1] SUM all-reduce of
+    shifted sums) or ``"allgather"`` (the reference's [W, 2C+1] all_gather + Welford merge)."""
+    return _STATS_MODE
+
+
+def set_stats_mode(mode: str) -> None:
+    global _STATS_MODE
+    if mode not in ("allreduce", "allgather"):
+        raise ValueError(f"SyncBatchNorm stats mode must be 'allreduce' or 'allgather', got {mode!r}")
+    _STATS_MODE = mode
 
 
 def _world(pg):
@@ -31,10 +50,19 @@ class SyncBatchnormFunction(torch.autograd.Function):
                 channel_last, fuse_relu, num_batches=None, pool=None):
         input = input.contiguous(memory_format=torch.channels_last) if (channel_last and input.dim() == 4) else input
         world = _world(process_group)
-        if world > 1:
+        if world > 1 and stats_mode() == "allreduce":
+            # one fixed-size [2C+1] SUM all-reduce of shifted sums (K = running mean, shared by all ranks)
+            sums = syncbn.stats_local_sums(input, running_mean)
+            with comm_stats.timed("syncbn_fwd", sums):
+                dist.all_reduce(sums, group=process_group)
+            mean, invstd, scale, shift, count = syncbn.merge_sums(sums, weight, bias, running_mean, running_var,
+                                                                  momentum, eps, num_batches)
+        elif world > 1:
+            # reference form (optimized_sync_batchnorm_kernel.py:34-43): all_gather [W, 2C+1] + Welford merge
             local = syncbn.stats_local(input)
             gathered = torch.empty(world * local.numel(), dtype=local.dtype, device=local.device)
-            dist.all_gather_into_tensor(gathered, local, group=process_group)
+            with comm_stats.timed("syncbn_fwd", local):
+                dist.all_gather_into_tensor(gathered, local, group=process_group)
             gathered = gathered.view(world, local.numel())
             mean, invstd, scale, shift, count = syncbn.merge_ranks(gathered, weight, bias, running_mean,
                                                                    running_var, momentum, eps, num_batches)
@@ -71,7 +99,8 @@ class SyncBatchnormFunction(torch.autograd.Function):
         grad_input = grad_z = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             if ctx.world > 1:
-                dist.all_reduce(sums, group=ctx.process_group)
+                with comm_stats.timed("syncbn_bwd", sums):
+                    dist.all_reduce(sums, group=ctx.process_group)
             grad_input, grad_z = syncbn.backward_dgrad(grad_output, input, z, mean, invstd, weight, sums, count,
                                                        scale, shift, ctx.fuse_relu,
                                                        ctx.has_z and ctx.needs_input_grad[1], mask)

@@ -108,6 +108,37 @@ class CudaRNGStatesTracker:
 
 _CUDA_RNG_STATE_TRACKER = CudaRNGStatesTracker()
 
+# Host-side seed streams for the fused dropout kernels (bias-dropout-add): each call draws a 31-bit
+# kernel seed on the CPU (no device sync). "replicated" is seeded identically on every TP rank (TP
+# replicas hold the same activations and must drop the same elements); "model-parallel" is seeded per
+# TP rank (sequence-parallel shards need independent masks) -- the two roles the device generator and
+# the tracker's "model-parallel-rng" state play for torch dropout (reference: random.py:124-311,
+# standalone_transformer_lm.py:1009-1014). Saved/restored by CheckpointFunction like the device states.
+_DROPOUT_SEED_GENS = {}
+
+
+def _seed_dropout_streams(seed, tp_seed):
+    for name, s in (("replicated", seed), ("model-parallel", tp_seed)):
+        g = torch.Generator()
+        g.manual_seed(int(s))
+        _DROPOUT_SEED_GENS[name] = g
+
+
+def dropout_seed(model_parallel: bool = False) -> int:
+    """Next fused-dropout kernel seed from the replicated or the per-TP-rank stream (falls back to
+    the default CPU generator before :func:`model_parallel_cuda_manual_seed` was called)."""
+    g = _DROPOUT_SEED_GENS.get("model-parallel" if model_parallel else "replicated")
+    return int(torch.randint(0, 2 ** 31 - 1, (1,), generator=g).item())
+
+
+def get_dropout_seed_states():
+    return {k: g.get_state() for k, g in _DROPOUT_SEED_GENS.items()}
+
+
+def set_dropout_seed_states(states):
+    for k, st in states.items():
+        _DROPOUT_SEED_GENS.setdefault(k, torch.Generator()).set_state(st)
+
 
 def get_cuda_rng_tracker():
     return _CUDA_RNG_STATE_TRACKER
@@ -119,6 +150,7 @@ def model_parallel_cuda_manual_seed(seed):
     _CUDA_RNG_STATE_TRACKER.reset()
     _device_manual_seed(seed)
     _CUDA_RNG_STATE_TRACKER.add(_MODEL_PARALLEL_RNG_TRACKER_NAME, tp_seed)
+    _seed_dropout_streams(seed, tp_seed)
 
 
 class CheckpointFunction(torch.autograd.Function):
@@ -132,6 +164,7 @@ class CheckpointFunction(torch.autograd.Function):
         ctx.fwd_cpu_rng_state = torch.get_rng_state()
         ctx.fwd_cuda_rng_state = _get_device_rng_state()
         ctx.fwd_cuda_rng_state_tracker = get_cuda_rng_tracker().get_states()
+        ctx.fwd_dropout_seed_states = get_dropout_seed_states()
         with torch.no_grad():
             outputs = run_function(*args)
         if distribute_saved_activations:
@@ -151,15 +184,18 @@ class CheckpointFunction(torch.autograd.Function):
         bwd_cpu = torch.get_rng_state()
         bwd_dev = _get_device_rng_state()
         bwd_tracker = get_cuda_rng_tracker().get_states()
+        bwd_seeds = get_dropout_seed_states()
         torch.set_rng_state(ctx.fwd_cpu_rng_state)
         _set_cuda_rng_state(ctx.fwd_cuda_rng_state)
         get_cuda_rng_tracker().set_states(ctx.fwd_cuda_rng_state_tracker)
+        set_dropout_seed_states(ctx.fwd_dropout_seed_states)
         detached = detach_variable(tuple(inputs))
         with torch.enable_grad():
             outputs = ctx.run_function(*detached)
         torch.set_rng_state(bwd_cpu)
         _set_cuda_rng_state(bwd_dev)
         get_cuda_rng_tracker().set_states(bwd_tracker)
+        set_dropout_seed_states(bwd_seeds)
         if isinstance(outputs, torch.Tensor):
             outputs = (outputs,)
         pairs = [(o, g) for o, g in zip(outputs, grads) if isinstance(o, torch.Tensor) and o.requires_grad]

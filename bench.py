@@ -6,8 +6,13 @@ BN+ReLU / BN+add+ReLU, synchronised across all ranks), beforeholiday_amd Distrib
 over RCCL. Synthetic 224x224 channels_last images, random-init weights, weak scaling
 (--batch images per GPU).
 
-    python bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --steps K --warmup W          (spawns N rank processes itself)
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Without ``WORLD_SIZE`` in the environment and ``--gpus N > 1`` the script starts N children of itself
+(one per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, 127.0.0.1 rendezvous) BEFORE touching HIP, and
+exits with their combined status; under torchrun it is one rank. Either way the job asserts that the
+process group really has N ranks.
 
 Rank 0 prints ONE json line; ``value`` is the whole-job images/sec over N GPUs; the timed region is
 exactly K full training steps (forward, scaled backward with overlapped all-reduce, unscale,
@@ -26,6 +31,18 @@ import torch.nn.functional as F
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+
+def _launch_module():
+    """beforeholiday_amd/parallel/launch.py loaded by path: stdlib only, so the parent of a spawned
+    job never imports the package (or its HIP library) before its children start."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location(
+        "_bh_launch", os.path.join(ROOT, "beforeholiday_amd", "parallel", "launch.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
 METRIC = "ResNet-50 amp O2 images/sec"
 BASELINE_VALUE = None  # BASELINE.json "published" is empty for this metric
 
@@ -41,7 +58,14 @@ def parse():
                          "O1 / O4: fp32 model with fp16 / bf16 casts around torch functions")
     ap.add_argument("--optimizer", default="lamb", choices=["lamb", "adam", "sgd"])
     ap.add_argument("--no-syncbn", action="store_true")
-    ap.add_argument("--message-size", type=int, default=12_500_000, help="DDP bucket size (elements)")
+    ap.add_argument("--message-size", type=int, default=12_500_000,
+                    help="DDP bucket size in elements (reference policy; used when --bucket-cap-mb is 0)")
+    ap.add_argument("--bucket-cap-mb", type=float, default=-1,
+                    help="DDP bucket size in MB (-1: sized per xGMI peer by xgmi_bucket_mb, 0: use --message-size)")
+    ap.add_argument("--syncbn-stats", default="allreduce", choices=["allreduce", "allgather"],
+                    help="SyncBN forward statistics: one [2C+1] SUM all-reduce, or the reference all_gather + merge")
+    ap.add_argument("--diag-steps", type=int, default=3,
+                    help="untimed steps AFTER the timed region with collective timing events (comm_ms_per_step)")
     ap.add_argument("--profile-steps", type=int, default=0)
     ap.add_argument("--autotune", action="store_true",
                     help="MIOpen find (cudnn.benchmark): minutes of first-step tuning on a fresh box and measured "
@@ -61,25 +85,39 @@ def parse():
 
 def main():
     args = parse()
+    rc = _launch_module().maybe_spawn(args.gpus)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    local_rank = local_rank % max(1, torch.cuda.device_count())
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; run `python bench.py --gpus N` (spawns the "
+                 f"ranks) or torchrun with --nproc-per-node N")
+    ndev = torch.cuda.device_count()
+    if args.backend == "gloo":
+        local_rank %= max(1, ndev)  # rehearsal: several ranks may share one GPU
+    elif local_rank >= ndev:
+        sys.exit(f"bench.py: rank {rank} wants GPU {local_rank} but only {ndev} are visible (RCCL needs one GPU per rank)")
     torch.cuda.set_device(local_rank)
     if world > 1:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
             dist.init_process_group("gloo")
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     torch.backends.cudnn.benchmark = args.autotune
 
     from beforeholiday_amd import amp
     from beforeholiday_amd._native import require_native
     from beforeholiday_amd.models import resnet50, resnet50_fused
     from beforeholiday_amd.optimizers import FusedAdam, FusedLAMB, FusedSGD
-    from beforeholiday_amd.parallel import DistributedDataParallel
+    from beforeholiday_amd.parallel import DistributedDataParallel, comm_stats
+    from beforeholiday_amd.parallel.distributed import xgmi_bucket_mb
+    from beforeholiday_amd.parallel.optimized_sync_batchnorm import set_stats_mode
 
     require_native("bench")
+    set_stats_mode(args.syncbn_stats)
     torch.manual_seed(1234 + rank)
     bn_group = dist.new_group(list(range(world))) if (world > 1 and args.bn_group == "separate") else None
     model = (resnet50() if args.no_syncbn else resnet50_fused(process_group=bn_group, channel_last=True,
@@ -95,7 +133,15 @@ def main():
         opt = FusedSGD(model.parameters(), lr=0.1 * global_batch / 256, momentum=0.9, weight_decay=1e-4)
     model, opt = amp.initialize(model, opt, opt_level=args.opt_level, verbosity=0,
                                 keep_batchnorm_fp32=True if args.opt_level in ("O2", "O5") else None)
-    model = DistributedDataParallel(model, message_size=args.message_size)
+    grad_bytes = sum(p.numel() * p.element_size() for p in model.parameters())
+    if args.bucket_cap_mb < 0:
+        cap_mb, first_mb = xgmi_bucket_mb(world, grad_bytes)
+    elif args.bucket_cap_mb == 0:
+        cap_mb = first_mb = None
+    else:
+        cap_mb, first_mb = args.bucket_cap_mb, args.bucket_cap_mb / 4
+    model = DistributedDataParallel(model, message_size=args.message_size, bucket_cap_mb=cap_mb,
+                                    first_bucket_mb=first_mb)
 
     dt = torch.float16 if args.opt_level in ("O1", "O2") else torch.bfloat16
     in_dt = dt if args.opt_level in ("O2", "O5") else torch.float32  # O1/O4 models stay fp32
@@ -134,6 +180,18 @@ def main():
         elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3
     img_s = global_batch * args.steps / elapsed
+
+    # untimed diagnostics after the timed region: how long the compute stream waited on collectives
+    comm = {}
+    if world > 1 and args.diag_steps > 0:
+        comm_stats.reset()
+        with comm_stats.collect():
+            for _ in range(args.diag_steps):
+                step()
+        comm = {k: round(v["ms"] / args.diag_steps, 3) for k, v in comm_stats.summary().items()}
+        comm["syncbn_calls_per_step"] = sum(v["calls"] for k, v in comm_stats.summary().items()
+                                            if k.startswith("syncbn")) // args.diag_steps
+    buckets = [round(n * torch.empty((), dtype=d).element_size() / 2 ** 20, 2) for d, n in model.bucket_sizes()]
     if rank == 0:
         print(json.dumps({
             "metric": METRIC if args.opt_level == "O2" else f"ResNet-50 amp {args.opt_level} images/sec",
@@ -161,6 +219,11 @@ def main():
                 "parallelism": f"dp{world}",
                 "final_loss": round(float(loss.item()), 4),
             },
+            "rccl_world": dist.get_world_size() if world > 1 else 1,
+            "backend": (args.backend if world > 1 else "none"),
+            "ddp_bucket_mb": buckets,
+            "syncbn_stats": args.syncbn_stats,
+            "comm_ms_per_step": comm,
         }), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -169,7 +169,7 @@ def test_bias_dropout_add_native(dtype, p, use_bias):
     x = torch.randn(s, b, h, device="cuda", dtype=dtype, requires_grad=True)
     bias = torch.randn(h, device="cuda", dtype=dtype, requires_grad=True) if use_bias else None
     res = torch.randn(s, b, h, device="cuda", dtype=dtype, requires_grad=True)
-    out = fd._BiasDropoutAddFn.apply(x, bias, res, p)
+    out = fd._BiasDropoutAddFn.apply(x, bias, res, p, False)
     keep_bits = fd._fd().bias_dropout_add(x.detach(), bias.detach() if use_bias else None, res.detach(), p, 123)[1]
     assert out.grad_fn is not None
     if p > 0:
@@ -206,3 +206,24 @@ def test_bias_dropout_add_eval_matches_reference(device):
     bias = torch.randn(64, device=device)
     out = bias_dropout_add(x, bias, res, 0.1, training=False)
     torch.testing.assert_close(out, res + (x + bias), atol=1e-6, rtol=1e-6)
+
+
+@pytest.mark.gpu
+def test_bias_dropout_add_seeds_give_unrelated_masks():
+    """Keyed hash: the mask of seed s2 is not the mask of seed s1 re-indexed by i ^ (s1 ^ s2) (the
+    failure mode of XOR-ing a raw seed into the index), and two seeds agree on ~p^2 + (1-p)^2."""
+    from beforeholiday_amd.ops import fused_dense as fd
+
+    x = torch.zeros(256, 1024, device="cuda", dtype=torch.bfloat16)
+    res = torch.zeros_like(x)
+
+    def bits(seed):
+        kb = fd._fd().bias_dropout_add(x, None, res, 0.5, seed)[1]
+        return torch.stack([(kb >> k) & 1 for k in range(8)], -1).reshape(-1)
+
+    b1, b2 = bits(5), bits(5 ^ 64)
+    idx = torch.arange(b1.numel(), device="cuda")
+    assert not torch.equal(b2, b1[idx ^ 64])
+    agree = (b1 == b2).float().mean().item()
+    assert abs(agree - 0.5) < 0.01, agree
+    assert abs(b1.float().mean().item() - 0.5) < 0.01

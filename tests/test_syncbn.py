@@ -339,3 +339,43 @@ def test_relu_bitmask_forward(shape):
     assert mask.shape == (pre.shape[0], C // 8) and mask.dtype == torch.uint8
     torch.testing.assert_close(mask, ref, rtol=0, atol=0)
     torch.testing.assert_close(view(y).float(), torch.relu(pre), rtol=4e-3, atol=4e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["allgather", "allreduce"])
+@pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
+@pytest.mark.parametrize("channels_last", [True, False])
+def test_multirank_stats_kernels_on_shards(mode, dtype, channels_last):
+    """The native multi-rank path of SyncBatchNorm (the one every 8-GPU BN layer takes), driven on one
+    GPU: W shards -> per-shard payloads (stats_local / stats_local_sums) -> the collective emulated by
+    stacking / summing -> merge_ranks / merge_sums, vs fp32 full-batch statistics and running stats."""
+    from beforeholiday_amd.ops import syncbn as sb
+
+    torch.manual_seed(7)
+    W, C = 4, 64
+    shards = [torch.randn(3 + r, C, 7, 5, device="cuda") * 2.5 + 40 for r in range(W)]  # uneven, large mean
+    if channels_last:
+        shards = [s.to(memory_format=torch.channels_last) for s in shards]
+    shards = [s.to(dtype) for s in shards]
+    full = torch.cat([s.float() for s in shards])
+    w = torch.rand(C, device="cuda") + 0.5
+    b = torch.randn(C, device="cuda")
+    rm = torch.randn(C, device="cuda") + 39.0
+    rv = torch.rand(C, device="cuda") + 1.0
+    rm_ref, rv_ref = rm.clone(), rv.clone()
+    if mode == "allgather":
+        g = torch.stack([sb.stats_local(s) for s in shards])
+        mean, invstd, scale, shift, count = sb.merge_ranks(g, w, b, rm, rv, 0.1, 1e-5)
+    else:
+        tot = sum(sb.stats_local_sums(s, rm) for s in shards)
+        mean, invstd, scale, shift, count = sb.merge_sums(tot, w, b, rm, rv, 0.1, 1e-5)
+    m_ref = full.mean((0, 2, 3))
+    v_ref = full.var((0, 2, 3), unbiased=False)
+    n = full.numel() // C
+    torch.testing.assert_close(mean, m_ref, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(invstd, torch.rsqrt(v_ref + 1e-5), rtol=2e-4, atol=1e-5)
+    torch.testing.assert_close(scale, w * torch.rsqrt(v_ref + 1e-5), rtol=2e-4, atol=1e-5)
+    torch.testing.assert_close(shift, b - m_ref * w * torch.rsqrt(v_ref + 1e-5), rtol=2e-4, atol=2e-3)
+    assert float(count[0]) == n
+    torch.testing.assert_close(rm, 0.9 * rm_ref + 0.1 * m_ref, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(rv, 0.9 * rv_ref + 0.1 * v_ref * n / (n - 1), rtol=1e-4, atol=1e-4)

@@ -461,3 +461,29 @@ def test_ltor_masks():
     assert pos[0].tolist() == [0, 1, 2, 0, 1]
     assert loss_mask[0].tolist() == [1, 1, 0, 1, 1]
     assert mask[0, 0, 3, 1].item() and not mask[0, 0, 3, 3].item()
+
+
+def _bda_masks(rank, world):
+    """Bias-dropout-add masks across TP ranks: identical without sequence parallelism (replicas hold
+    the same activations), different with it (each rank holds its own sequence shard). Covers both the
+    fused kernel's host seed streams and the PyTorch fallback (forked model-parallel RNG)."""
+    from beforeholiday_amd.models.transformer_lm import bias_dropout_add
+    from beforeholiday_amd.transformer import tensor_parallel
+    from beforeholiday_amd.transformer.tensor_parallel.random import dropout_seed
+
+    _init(world, 1)
+    torch.manual_seed(100 + rank)  # per-rank base seeds (as bench scripts do) must not matter
+    tensor_parallel.model_parallel_cuda_manual_seed(1234)
+    seeds = {mp: torch.tensor([dropout_seed(mp) for _ in range(4)]) for mp in (False, True)}
+    x = torch.ones(64, 2, 32)
+    masks = {mp: (bias_dropout_add(x, None, torch.zeros_like(x), 0.5, True, mp) != 0).float() for mp in (False, True)}
+    for mp in (False, True):
+        for t in (seeds[mp], masks[mp]):
+            g = [torch.empty_like(t) for _ in range(world)]
+            torch.distributed.all_gather(g, t)
+            same = torch.equal(g[0], g[1])
+            assert same == (not mp), (mp, t.dtype)
+
+
+def test_bias_dropout_add_masks_across_tp_ranks():
+    run_distributed(_bda_masks, 2)
