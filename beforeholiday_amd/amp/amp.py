@@ -6,7 +6,7 @@ import itertools
 
 import torch
 
-from . import utils, wrap
+from . import rnn_compat, utils, wrap
 from ._amp_state import _amp_state
 from .handle import AmpHandle, NoOpHandle
 from .lists import functional_overrides, tensor_overrides, torch_overrides
@@ -122,6 +122,10 @@ def init(enabled=True, loss_scale="dynamic", patch_type=torch.float16, enable_ca
         wrap.err_if_arg0_half(tensor_overrides.MODULE, fn, handle, verbose)
     for fn in utils.as_inplace(itertools.chain(getattr(tensor_overrides, low_prec_funcs), tensor_overrides.CASTS)):
         wrap.promote_match_arg0(tensor_overrides.MODULE, fn, handle, verbose)
+
+    # recurrent layers: nn.RNN/GRU/LSTM (+ packed sequences) and the *Cell modules run in the low
+    # precision type through a mutable stand-in for torch.nn.modules.rnn._VF
+    rnn_compat.install(handle, maybe_low, verbose)
 
     for fn, err_msg in functional_overrides.BANNED_FUNCS:
         if allow_banned:

@@ -12,7 +12,8 @@ data parallel (DDP over the DP group). ``--sp`` turns on Megatron sequence paral
 Synthetic token ids, random-init weights. Prints one JSON line (whole-job tokens/s).
 
     python benchmarks/bench_gpt.py --batch 8 --steps 10 --warmup 3
-    python -m torch.distributed.run --nproc-per-node 4 --master-addr 127.0.0.1 benchmarks/bench_gpt.py --tp 4 --sp
+    python benchmarks/bench_gpt.py --gpus 4 --tp 4 --sp          (spawns the 4 ranks itself)
+    python -m torch.distributed.run --nproc-per-node 4 --master-addr 127.0.0.1 benchmarks/bench_gpt.py --gpus 4 --tp 4 --sp
 """
 import argparse
 import json
@@ -23,11 +24,14 @@ import time
 import torch
 import torch.distributed as dist
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=0,
+                    help="ranks; without WORLD_SIZE in the env the script spawns them itself (default: WORLD_SIZE or 1)")
     ap.add_argument("--batch", type=int, default=8, help="sequences per data-parallel rank")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--steps", type=int, default=10)
@@ -41,10 +45,24 @@ def main():
                     help="nccl = RCCL over xGMI; gloo only to rehearse multi-rank TP/SP on one GPU")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        import importlib.util
+
+        spec = importlib.util.spec_from_file_location(
+            "_bh_launch", os.path.join(ROOT, "beforeholiday_amd", "parallel", "launch.py"))
+        launch = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(launch)
+        sys.exit(launch.maybe_spawn(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    local_rank %= max(1, torch.cuda.device_count())
+    if args.gpus and args.gpus != world:
+        sys.exit(f"bench_gpt.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    ndev = torch.cuda.device_count()
+    if args.backend == "gloo":
+        local_rank %= max(1, ndev)  # rehearsal: several ranks may share one GPU
+    elif local_rank >= ndev:
+        sys.exit(f"bench_gpt.py: rank {rank} wants GPU {local_rank} but only {ndev} are visible")
     torch.cuda.set_device(local_rank)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29534")
@@ -54,6 +72,7 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
     tp = args.tp or world
     assert world % tp == 0, f"world {world} not divisible by tp {tp}"
+    assert dist.get_world_size() == world
     dp = world // tp
 
     from beforeholiday_amd import amp
