@@ -1,14 +1,16 @@
 """Legacy FusedAdam with explicit ``grads`` / ``output_params`` / ``scale`` / ``grad_norms``
 (reference: apex/contrib/optimizers/fused_adam.py:6-200, ``fused_adam_cuda``).
 
-Runs the capturable multi-tensor Adam kernel: the combined unscale / clip factor is a device scalar
-and the reduced-precision output copy is written in the same pass (5th tensor list). The
-``eps_inside_sqrt`` variant (update = m / sqrt(v + eps)) is computed with torch ops.
+Runs the deprecated ``fused_adam_cuda`` kernels (kernels/legacy_optim.hip) with the reference's
+update rule: ``step_size = lr*sqrt(1-b2^t)/(1-b1^t)``, ``p -= step_size*(m/denom + wd*p)``,
+``denom = sqrt(v + eps)`` (``eps_inside_sqrt``) or ``sqrt(v) + eps``; the reduced-precision
+``output_params`` copy is written in the same pass. ``use_mt`` launches one multi-tensor kernel per
+group (lists p, m, v, g[, out]).
 """
 import torch
 
 from ...multi_tensor_apply import multi_tensor_applier
-from ...ops import amp_C
+from ...ops import fused_adam_cuda
 from ._legacy import group_lists
 
 
@@ -41,54 +43,43 @@ class FusedAdam(torch.optim.Optimizer):
             o_this = o_this or [None] * len(group["params"])
             combined = float(scale)
             if group["max_grad_norm"] > 0 and gnorm is not None:
+                # the norm is of the scaled gradients
                 clip = ((float(gnorm) / scale) + 1e-6) / group["max_grad_norm"]
                 if clip > 1:
                     combined = clip * scale
             beta1, beta2 = group["betas"]
-            buckets = {}
+            bias_correction = 1 if group["bias_correction"] else 0
+            mt_lists, mt_dev, has_out = [[], [], [], [], []], None, False
             for p, g, o in zip(group["params"], g_this, o_this):
                 if p.grad is None and g is None:
                     continue
                 g = p.grad if g is None else g
                 if g.is_sparse:
-                    raise RuntimeError("FusedAdam does not support sparse gradients")
+                    raise RuntimeError("FusedAdam does not support sparse gradients, please consider SparseAdam instead")
                 st = self.state[p]
                 if len(st) == 0:
                     st["step"] = 0
-                    st["exp_avg"] = torch.zeros_like(p, dtype=torch.float32 if p.dtype != torch.float64 else p.dtype)
-                    st["exp_avg_sq"] = torch.zeros_like(st["exp_avg"])
+                    st["exp_avg"] = torch.zeros_like(p)
+                    st["exp_avg_sq"] = torch.zeros_like(p)
                 st["step"] += 1
-                key = (g.dtype, p.dtype, None if o is None else o.dtype, st["step"])
-                buckets.setdefault(key, [[], [], [], [], []])
-                lists = buckets[key]
-                lists[0].append(g)
-                lists[1].append(p)
-                lists[2].append(st["exp_avg"])
-                lists[3].append(st["exp_avg_sq"])
-                lists[4].append(o)
-            for (gdt, pdt, odt, step), lists in buckets.items():
-                dev = lists[1][0].device
-                if self.eps_mode == 0:
-                    self._eps_inside_sqrt(group, lists, step, combined)
+                if self._use_multi_tensor:
+                    if mt_dev is not None and p.device != mt_dev:
+                        raise RuntimeError("FusedAdam does not support use_mt with tensors on multiple device")
+                    mt_dev = p.device
+                    for lst, t in zip(mt_lists, (p, st["exp_avg"], st["exp_avg_sq"], g, o)):
+                        lst.append(t)
+                    has_out = has_out or o is not None
                     continue
-                use = lists if odt is not None else lists[:4]
-                flag = torch.zeros(1, dtype=torch.int, device=dev)
-                multi_tensor_applier(amp_C.multi_tensor_adam_capturable, flag, use,
-                                     torch.full([1], group["lr"], dtype=torch.float32, device=dev), beta1, beta2,
-                                     group["eps"], torch.full([1], step, dtype=torch.int, device=dev), 0,
-                                     1 if group["bias_correction"] else 0, group["weight_decay"],
-                                     torch.full([1], 1.0 / combined, dtype=torch.float32, device=dev), None)
+                out_p = o if o is not None else torch.empty(0, dtype=torch.float32, device=p.device)
+                fused_adam_cuda.adam(p, out_p, st["exp_avg"], st["exp_avg_sq"], g, group["lr"], beta1, beta2,
+                                     group["eps"], combined, st["step"], self.eps_mode, bias_correction,
+                                     group["weight_decay"])
+            if self._use_multi_tensor and mt_lists[0]:
+                if has_out and any(o is None for o in mt_lists[4]):
+                    raise RuntimeError("FusedAdam use_mt: output_params must be given for all params or none")
+                lists = mt_lists if has_out else mt_lists[:4]
+                flag = torch.zeros(1, dtype=torch.int, device=mt_dev)
+                multi_tensor_applier(fused_adam_cuda.adam_mt, flag, lists, group["lr"], beta1, beta2, group["eps"],
+                                     combined, self.state[mt_lists[0][0]]["step"], self.eps_mode, bias_correction,
+                                     group["weight_decay"])
         return loss
-
-    def _eps_inside_sqrt(self, group, lists, step, combined):
-        beta1, beta2 = group["betas"]
-        bc1 = 1 - beta1 ** step if group["bias_correction"] else 1.0
-        bc2 = 1 - beta2 ** step if group["bias_correction"] else 1.0
-        for g, p, m, v, o in zip(*lists):
-            gf = g.float() / combined + group["weight_decay"] * p.float()
-            m.mul_(beta1).add_(gf, alpha=1 - beta1)
-            v.mul_(beta2).addcmul_(gf, gf, value=1 - beta2)
-            upd = (m / bc1) / torch.sqrt(v / bc2 + group["eps"])
-            p.copy_((p.float() - group["lr"] * upd).to(p.dtype))
-            if o is not None:
-                o.copy_(p.to(o.dtype))

@@ -13,4 +13,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   bhb::register_dense(m);
   bhb::register_contrib(m);
   bhb::register_misc(m);
+  bhb::register_legacy_optim(m);
 }

@@ -148,3 +148,109 @@ def test_legacy_contrib_fused_sgd(device):
         ref(x).pow(2).mean().backward()
         ref_opt.step()
     torch.testing.assert_close(model.weight, ref.weight, rtol=1e-5, atol=1e-6)
+
+
+# ------------------------------------------------------------------------------------------------
+# deprecated fused_adam_cuda ops (reference: apex/contrib/csrc/optimizers/fused_adam_cuda.cpp:79-85)
+# ------------------------------------------------------------------------------------------------
+def _legacy_state(device, n=3000, gdt=torch.float16, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    p = torch.randn(n, generator=g).to(device)
+    m = (torch.randn(n, generator=g) * 0.1).to(device)
+    v = (torch.rand(n, generator=g) * 0.01).to(device)
+    grad = (torch.randn(n, generator=g) * 64).to(device, gdt)
+    return p, m, v, grad
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("copy_dt", [None, torch.float16, torch.uint8])
+def test_fused_adam_cuda_adam_matches_reference(mode, copy_dt):
+    from beforeholiday_amd.ops import fused_adam_cuda as fac
+    args = (1e-3, 0.9, 0.999, 1e-6, 64.0, 3, mode, 1, 0.01)
+    p, m, v, g = _legacy_state("cuda")
+    rp, rm, rv, rg = (t.cpu().clone() for t in (p, m, v, g))
+    pc = torch.empty(0, device="cuda") if copy_dt is None else torch.empty_like(p, dtype=copy_dt)
+    rpc = torch.empty(0) if copy_dt is None else torch.empty_like(rp, dtype=copy_dt)
+    fac.adam(p, pc, m, v, g, *args)
+    fac._ref_adam(rp, rpc, rm, rv, rg, *args)
+    for a, b in ((p, rp), (m, rm), (v, rv)):
+        torch.testing.assert_close(a.cpu(), b, rtol=1e-5, atol=1e-6)
+    if copy_dt is not None:
+        assert torch.equal(pc.cpu(), rpc) if copy_dt == torch.uint8 else torch.allclose(pc.cpu().float(), rpc.float())
+
+
+@pytest.mark.gpu
+def test_fused_adam_cuda_adam_mt_matches_single():
+    from beforeholiday_amd.ops import fused_adam_cuda as fac
+    args = (1e-3, 0.9, 0.999, 1e-8, 1.0, 5, 1, 1, 0.0)
+    sizes = [7, 65536 + 5, 1000]
+    single = [_legacy_state("cuda", n, torch.float32, seed=i) for i, n in enumerate(sizes)]
+    multi = [tuple(t.clone() for t in s) for s in single]
+    outs = [torch.empty_like(s[0], dtype=torch.float16) for s in single]
+    for p, m, v, g in single:
+        fac.adam(p, torch.empty(0, device="cuda"), m, v, g, *args)
+    flag = torch.zeros(1, dtype=torch.int, device="cuda")
+    fac.adam_mt(2048, flag, [[s[0] for s in multi], [s[1] for s in multi], [s[2] for s in multi],
+                             [s[3] for s in multi], outs], *args)
+    for s, t, o in zip(single, multi, outs):
+        for a, b in zip(s[:3], t[:3]):
+            torch.testing.assert_close(a, b, rtol=0, atol=0)
+        torch.testing.assert_close(o.float(), t[0].half().float(), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("device", devices())
+def test_reversible_adam_then_undo_restores_state(device):
+    """reversible_adam skips non-finite grads and flags p_copy[0] = inf; maybe_adam_undo then reverts
+    the step for every other element (reference kernels :571, :657)."""
+    from beforeholiday_amd.ops import fused_adam_cuda as fac
+    args = (1e-2, 0.9, 0.999, 1e-8, 8.0, 1, 1, 1, 0.01)
+    p, m, v, g = _legacy_state(device, 1024, torch.float32, seed=3)
+    g[17] = float("inf")
+    p0, m0, v0 = p.clone(), m.clone(), v.clone()
+    pc = torch.empty_like(p, dtype=torch.float16)
+    fac.reversible_adam(p, pc, m, v, g, *args)
+    assert torch.isinf(pc[0].float())
+    assert p[17] == p0[17] and m[17] == m0[17]
+    assert not torch.equal(p, p0)
+    flag = torch.zeros(1, dtype=torch.int, device=device)
+    fac.strided_check_finite(flag, pc, 1, 1)
+    assert int(flag) == 1
+    fac.maybe_adam_undo(flag, p, m, v, g, *args)
+    torch.testing.assert_close(p, p0, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(m, m0, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(v, v0, rtol=1e-3, atol=1e-7)
+    flag.zero_()
+    p1 = p.clone()
+    fac.maybe_adam_undo(flag, p, m, v, g, *args)  # no overflow -> untouched
+    assert torch.equal(p, p1)
+
+
+@pytest.mark.parametrize("device", devices())
+def test_e5m2_casts(device):
+    from beforeholiday_amd.ops import fused_adam_cuda as fac
+    x = torch.tensor([0.0, 1.0, -1.5, 1.75, 1.8, 3.0e4, -2.0 ** -14, float("inf"), 0.3], device=device)
+    b = torch.empty_like(x, dtype=torch.uint8)
+    fac.maybe_cast(torch.zeros(1, dtype=torch.int, device=device), x, b)
+    back = torch.empty_like(x)
+    fac.maybe_cast(None, b, back)
+    # e5m2: 2 mantissa bits -> representable 1.0, 1.25, 1.5, 1.75, 2.0 ...
+    want = torch.tensor([0.0, 1.0, -1.5, 1.75, 1.75, 28672.0, -2.0 ** -14, float("inf"), 0.3125])
+    torch.testing.assert_close(back.cpu(), want, rtol=0, atol=0)
+    flag = torch.ones(1, dtype=torch.int, device=device)
+    b2 = torch.zeros_like(b)
+    fac.maybe_cast(flag, x, b2)  # overflow set -> skipped
+    assert int(b2.sum()) == 0
+    lists = [[x, x[:3]], [torch.empty_like(x, dtype=torch.float16), torch.empty(3, dtype=torch.float16, device=device)]]
+    fac.maybe_cast_mt(2048, torch.zeros(1, dtype=torch.int, device=device), lists)
+    torch.testing.assert_close(lists[1][0].float(), x.half().float())
+
+
+@pytest.mark.gpu
+def test_e5m2_gpu_matches_cpu_reference():
+    from beforeholiday_amd.ops import fused_adam_cuda as fac
+    x = torch.randn(100000) * torch.exp(torch.randn(100000) * 4)
+    ref = fac.to_e5m2(x)
+    out = torch.empty(100000, dtype=torch.uint8, device="cuda")
+    fac.maybe_cast(None, x.cuda(), out)
+    assert torch.equal(out.cpu(), ref)
