@@ -29,7 +29,7 @@ import torch
 import torch.distributed as dist
 
 from ...multi_tensor_apply import multi_tensor_applier
-from ...ops import amp_C
+from ...ops import amp_C, fused_adam_cuda
 
 
 def _round_up(n, m):
@@ -164,14 +164,29 @@ class DistributedFusedAdam(torch.optim.Optimizer):
                         p.data = b.view(b.param_buffer, i)
                         p.grad = b.view(b.grad_buffer, i) if self.contiguous_grad_buffer else None
                     b.master.copy_(b.param_buffer[b.shard_start:b.shard_start + b.shard_size].to(self.dtype))
-                    b.param_sync_shard.copy_(b.param_buffer[b.shard_start:b.shard_start + b.shard_size])
+                    self._pack_sync(b.param_sync_shard, b.param_buffer[b.shard_start:b.shard_start + b.shard_size])
         # broadcast initial parameters so every rank starts identical (reference: init broadcast)
         for b in self._buckets:
             src = dist.get_global_rank(self.process_group, 0) if self.process_group is not dist.group.WORLD else 0
             dist.broadcast(b.param_buffer, src, group=self.process_group)
             b.master.copy_(b.param_buffer[b.shard_start:b.shard_start + b.shard_size].to(self.dtype))
-            b.param_sync_shard.copy_(b.param_buffer[b.shard_start:b.shard_start + b.shard_size])
+            self._pack_sync(b.param_sync_shard, b.param_buffer[b.shard_start:b.shard_start + b.shard_size])
         self._register_post_backward_hooks()
+
+    @staticmethod
+    def _pack_sync(dst, src):
+        """src (param / master dtype) -> parameter all-gather dtype (uint8 = e5m2 bytes)."""
+        if dst.dtype == torch.uint8:
+            fused_adam_cuda.maybe_cast(None, src.contiguous(), dst)
+        else:
+            dst.copy_(src)
+
+    @staticmethod
+    def _unpack_sync(dst, src):
+        if src.dtype == torch.uint8:
+            fused_adam_cuda.maybe_cast(None, src, dst)
+        else:
+            dst.copy_(src)
 
     def _register_post_backward_hooks(self):
         for g in self.param_groups:
@@ -342,49 +357,101 @@ class DistributedFusedAdam(torch.optim.Optimizer):
             w.wait()
         for b in self._buckets:
             if b.param_sync_full is not b.param_buffer:
-                b.param_buffer.copy_(b.param_sync_full)
+                self._unpack_sync(b.param_buffer, b.param_sync_full)
         self._grad_norm = None
         return loss
 
     # ------------------------------------------------------------------ checkpointing
-    def state_dict(self, gather_on_root=True):
-        """``gather_on_root``: full flat fp32 master / moments per bucket on every rank's dict
-        (rank 0 saves it); otherwise this rank's shards only."""
-        buckets = []
+    def _global_param_index(self):
+        """Global parameter numbering of torch.optim's state_dict (param_groups order)."""
+        idx, out = 0, {}
+        for g in self.param_groups:
+            for p in g["params"]:
+                out[id(p)] = idx
+                idx += 1
+        return out
+
+    def _local_state(self):
+        """This rank's shard as layout-free per-parameter fragments (CPU tensors)."""
+        pidx = self._global_param_index()
+        frags = []
         for b in self._buckets:
-            entry = {"size": b.size, "shard_size": b.shard_size}
-            for name in ("master", "exp_avg", "exp_avg_sq"):
-                t = getattr(b, name)
-                if gather_on_root and self.distributed_size > 1:
-                    full = torch.empty(b.size, dtype=t.dtype, device=t.device)
-                    dist.all_gather_into_tensor(full, t, group=self.distributed_process_group)
-                    entry[name] = full.cpu()
-                else:
-                    entry[name] = t.cpu()
-            buckets.append(entry)
-        return {"state": {"step": self.state["step"], "buckets": buckets, "gathered": gather_on_root,
-                          "distributed_size": self.distributed_size},
-                "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups]}
+            for (i, plo, phi, slo, shi) in b.fragments:
+                frags.append({"param": pidx[id(b.params[i])], "lo": plo, "hi": phi,
+                              "master": b.master[slo:shi].cpu(), "exp_avg": b.exp_avg[slo:shi].cpu(),
+                              "exp_avg_sq": b.exp_avg_sq[slo:shi].cpu()})
+        groups = []
+        for g in self.param_groups:
+            d = {k: v for k, v in g.items() if k != "params"}
+            d["params"] = [pidx[id(p)] for p in g["params"]]
+            groups.append(d)
+        return {"state": {"step": self.state["step"], "fragments": frags, "distributed_size": self.distributed_size,
+                          "distributed_rank": self.distributed_rank},
+                "param_groups": groups}
+
+    def state_dict(self, gather_on_root=True):
+        """Optimizer state in the reference's layout (``distributed_fused_adam.py:1123-1262``).
+
+        ``gather_on_root=True`` (collective): every rank serialises its local state, root returns
+        ``{"gathered_states": [bytes of rank 0, rank 1, ...]}`` and the other ranks ``None``.
+        ``gather_on_root=False``: this rank's local state dict. The local state is a list of
+        per-parameter fragments (global param index, element range, master / exp_avg /
+        exp_avg_sq), so a checkpoint loads back under ANY distributed size or bucket size."""
+        local = self._local_state()
+        if not gather_on_root:
+            return local
+        import io
+
+        buf = io.BytesIO()
+        torch.save(local, buf)
+        blob = buf.getvalue()
+        gathered = [None] * self.distributed_size if self.distributed_rank == 0 else None
+        if self.distributed_size == 1:
+            gathered = [blob]
+        else:
+            root = dist.get_global_rank(self.distributed_process_group, 0) \
+                if self.distributed_process_group is not dist.group.WORLD else 0
+            dist.gather_object(blob, gathered, dst=root, group=self.distributed_process_group)
+        if self.distributed_rank == 0:
+            return {"gathered_states": gathered}
+        return None
 
     def load_state_dict(self, state_dict):
-        st = state_dict["state"]
-        for g, sg in zip(self.param_groups, state_dict["param_groups"]):
-            g.update(sg)
-        self.state["step"] = st["step"]
-        gathered = st.get("gathered", True) or st.get("distributed_size", 1) == 1
-        for b, e in zip(self._buckets, st["buckets"]):
-            for name in ("master", "exp_avg", "exp_avg_sq"):
-                src = e[name]
-                if gathered and src.numel() == b.size:
-                    src = src[b.shard_start:b.shard_start + b.shard_size]
-                getattr(b, name).copy_(src.to(b.master.device))
-            b.param_sync_shard.copy_(b.master)
+        """Load a ``{"gathered_states": [...]}`` checkpoint (any distributed size) or a local dict."""
+        import io
+
+        if "gathered_states" in state_dict:
+            locals_ = [torch.load(io.BytesIO(bytes(blob)), weights_only=True) for blob in state_dict["gathered_states"]]
+        else:
+            locals_ = [state_dict]
+        for g, sg in zip(self.param_groups, locals_[0]["param_groups"]):
+            g.update({k: v for k, v in sg.items() if k != "params"})
+        self.state["step"] = locals_[0]["state"]["step"]
+        # reassemble per-parameter state from every rank's fragments, then take this rank's shards
+        full: Dict[int, Dict[str, torch.Tensor]] = {}
+        pidx = self._global_param_index()
+        numel = {pidx[id(p)]: p.numel() for g in self.param_groups for p in g["params"]}
+        for loc in locals_:
+            for f in loc["state"]["fragments"]:
+                ent = full.setdefault(f["param"], {})
+                for name in ("master", "exp_avg", "exp_avg_sq"):
+                    if name not in ent:
+                        ent[name] = torch.zeros(numel[f["param"]], dtype=f[name].dtype)
+                    ent[name][f["lo"]:f["hi"]] = f[name]
+        for b in self._buckets:
+            for (i, plo, phi, slo, shi) in b.fragments:
+                ent = full.get(pidx[id(b.params[i])])
+                if ent is None:
+                    continue
+                for name in ("master", "exp_avg", "exp_avg_sq"):
+                    getattr(b, name)[slo:shi].copy_(ent[name][plo:phi])
+            self._pack_sync(b.param_sync_shard, b.master)
             if self.distributed_size == 1:
                 b.param_sync_full.copy_(b.param_sync_shard)
             else:
                 dist.all_gather_into_tensor(b.param_sync_full, b.param_sync_shard, group=self.distributed_process_group)
             if b.param_sync_full is not b.param_buffer:
-                b.param_buffer.copy_(b.param_sync_full)
+                self._unpack_sync(b.param_buffer, b.param_sync_full)
 
 
 class _Done:

@@ -133,9 +133,74 @@ void maybe_cast_mt(int64_t chunk_size, at::Tensor overflow_flag, std::vector<std
   bh::maybe_cast_mt(plan.view, flag_ptr(overflow_flag), dt_in, dt_out, stream_for(lists[0][0]));
 }
 
+const float* fptr(const at::Tensor& t, const char* name, int64_t n) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() >= n, name,
+              " must be a contiguous GPU fp32 tensor with >= ", n, " elements");
+  return t.data_ptr<float>();
+}
+
+void lamb_compute_update_term(int64_t chunk_size, at::Tensor noop, std::vector<std::vector<at::Tensor>> lists,
+                              at::Tensor beta1, at::Tensor beta2, at::Tensor beta3, at::Tensor bias_correction,
+                              at::Tensor step, at::Tensor eps, int64_t mode, at::Tensor decay,
+                              at::Tensor global_scale, at::Tensor global_grad_norm, double max_grad_norm) {
+  TORCH_CHECK(lists.size() == 5, "multi_tensor_lamb_compute_update_term: lists g, p, m, v, u");
+  if (lists[0].empty()) return;
+  const int64_t T = lists[0].size();
+  const int dt_g = list_dtype(lists[0], "lamb_update_term");
+  const int dt_p = list_dtype(lists[1], "lamb_update_term");
+  TORCH_CHECK(list_dtype(lists[2], "lamb_update_term") == dt_p && list_dtype(lists[3], "lamb_update_term") == dt_p,
+              "m / v must match p's dtype");
+  TORCH_CHECK(list_dtype(lists[4], "lamb_update_term") == bh::kF32, "update term u must be fp32");
+  TORCH_CHECK(bias_correction.scalar_type() == at::kInt && bias_correction.numel() >= T && step.scalar_type() == at::kInt,
+              "bias_correction / step must be int32 GPU tensors");
+  TORCH_CHECK(noop.is_cuda() && noop.scalar_type() == at::kInt, "noop_flag must be GPU int32");
+  bh::DistLambStage1Args a{};
+  a.beta1 = fptr(beta1, "per_tensor_beta1", T);
+  a.beta2 = fptr(beta2, "per_tensor_beta2", T);
+  a.beta3 = fptr(beta3, "per_tensor_beta3", T);
+  a.eps = fptr(eps, "per_tensor_epsilon", T);
+  a.decay = fptr(decay, "per_tensor_decay", T);
+  a.bias_correction = bias_correction.data_ptr<int>();
+  a.step = step.data_ptr<int>();
+  a.global_scale = fptr(global_scale, "global_scale", 1);
+  a.global_grad_norm = fptr(global_grad_norm, "global_grad_norm", 1);
+  a.max_grad_norm = (float)max_grad_norm;
+  a.mode = (int)mode;
+  const auto& plan = get_plan(lists, chunk_size);
+  bh::distopt_lamb_stage1(plan.view, dt_g, dt_p, a, noop.data_ptr<int>(), stream_for(lists[1][0]));
+}
+
+void lamb_update_weights(int64_t chunk_size, at::Tensor noop, std::vector<std::vector<at::Tensor>> lists,
+                         at::Tensor param_norm, at::Tensor update_norm, at::Tensor update_norm_offset,
+                         at::Tensor learning_rate, at::Tensor decay, at::Tensor global_grad_norm, bool use_nvlamb) {
+  TORCH_CHECK(lists.size() == 2 || lists.size() == 3, "multi_tensor_lamb_update_weights: lists p, u [, p_copy]");
+  (void)global_grad_norm;  // accepted for the reference signature (clipping happened in the update term)
+  if (lists[0].empty()) return;
+  const int64_t T = lists[0].size();
+  const int dt_p = list_dtype(lists[0], "lamb_update_weights");
+  TORCH_CHECK(list_dtype(lists[1], "lamb_update_weights") == bh::kF32, "update term u must be fp32");
+  const int dt_c = lists.size() == 3 ? list_dtype(lists[2], "lamb_update_weights") : -1;
+  TORCH_CHECK(update_norm_offset.scalar_type() == at::kLong && update_norm_offset.numel() >= T && update_norm_offset.is_cuda(),
+              "update_norm_offset must be a GPU int64 tensor");
+  TORCH_CHECK(noop.is_cuda() && noop.scalar_type() == at::kInt, "noop_flag must be GPU int32");
+  bh::DistLambStage2Args a{};
+  a.param_norm = fptr(param_norm, "per_tensor_param_norm", T);
+  a.update_norm = fptr(update_norm, "per_tensor_update_norm", 1);
+  a.update_norm_offset = update_norm_offset.data_ptr<int64_t>();
+  a.lr = fptr(learning_rate, "learning_rate", 1);
+  a.decay = fptr(decay, "per_tensor_decay", T);
+  a.use_nvlamb = use_nvlamb;
+  const auto& plan = get_plan(lists, chunk_size);
+  bh::distopt_lamb_stage2(plan.view, dt_p, dt_c, a, noop.data_ptr<int>(), stream_for(lists[0][0]));
+}
+
 }  // namespace
 
 void register_legacy_optim(pybind11::module_& root) {
+  auto dl = root.def_submodule("distributed_lamb_cuda", "ZeRO LAMB stages with device-resident scalars (gfx950)");
+  dl.def("multi_tensor_lamb_compute_update_term", &lamb_compute_update_term, "Computes update term for LAMB optimizer");
+  dl.def("multi_tensor_lamb_update_weights", &lamb_update_weights, "Applies update term for LAMB optimizer");
   auto m = root.def_submodule("fused_adam_cuda", "deprecated contrib Adam kernels + e5m2 casts (gfx950)");
   m.def("strided_check_finite", &strided_check_finite, "Strided finite check.");
   m.def("adam", &adam, "Adam (legacy update rule).");

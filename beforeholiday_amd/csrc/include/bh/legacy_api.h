@@ -39,3 +39,33 @@ void maybe_cast(int64_t n, const int* overflow, int dt_in, const void* in, int d
 void maybe_cast_mt(const MTAView& view, const int* overflow, int dt_in, int dt_out, hipStream_t s);
 
 }  // namespace bh
+
+namespace bh {
+
+// distributed_lamb_cuda (reference: apex/contrib/csrc/optimizers/multi_tensor_distopt_lamb.cpp):
+// device-resident hyper-parameters, skipped entirely when *noop != 0 (no host synchronisation).
+struct DistLambStage1Args {
+  const float *beta1, *beta2, *beta3, *eps, *decay;  // per tensor
+  const int* bias_correction;                          // per tensor
+  const int* step;                                     // device scalar
+  const float* global_scale;                           // device scalar: gradients are divided by it
+  const float* global_grad_norm;                       // device scalar (norm of the raw gradients)
+  float max_grad_norm;                                 // <= 0: no clipping
+  int mode;                                            // 0: L2, 1: decoupled weight decay
+};
+// lists g, p, m, v, u (u fp32)
+void distopt_lamb_stage1(const MTAView& view, int dt_g, int dt_p, const DistLambStage1Args& a, const int* noop,
+                         hipStream_t s);
+struct DistLambStage2Args {
+  const float* param_norm;    // per tensor
+  const float* update_norm;   // indexed through update_norm_offset
+  const int64_t* update_norm_offset;
+  const float* lr;            // device scalar
+  const float* decay;         // per tensor
+  bool use_nvlamb;
+};
+// lists p, u [, p_copy] (copy fp16 / bf16 / fp32 / u8-e5m2)
+void distopt_lamb_stage2(const MTAView& view, int dt_p, int dt_copy, const DistLambStage2Args& a, const int* noop,
+                         hipStream_t s);
+
+}  // namespace bh

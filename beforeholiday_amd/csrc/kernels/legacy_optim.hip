@@ -193,6 +193,67 @@ __global__ __launch_bounds__(kBlock) void k_cast_mt(MTAView view, const int* ove
   for (int64_t i = threadIdx.x; i < n; i += kBlock) stf<To>(out, i, ldf<Ti>(in, i));
 }
 
+// ---- distributed LAMB stages (device-resident scalars; noop-gated) ----
+template <typename P, typename G>
+__global__ __launch_bounds__(kBlock) void k_distlamb_s1(MTAView view, DistLambStage1Args a, const int* noop) {
+  if (*noop != 0) return;  // overflow: leave every state untouched
+  const int c = blockIdx.x;
+  const int t = view.chunk_tensor[c];
+  const int64_t base = (int64_t)view.chunk_local[c] * view.chunk;
+  const int64_t n = min((int64_t)view.chunk, view.numel[t] - base);
+  const G* g = plan_ptr<const G>(view, 0, t, base);
+  const P* p = plan_ptr<const P>(view, 1, t, base);
+  P* m = plan_ptr<P>(view, 2, t, base);
+  P* v = plan_ptr<P>(view, 3, t, base);
+  float* u = plan_ptr<float>(view, 4, t, base);
+  const float gs = *a.global_scale;
+  float combined = gs;
+  if (a.max_grad_norm > 0.f) {
+    const float clip = a.max_grad_norm / (*a.global_grad_norm / gs + 1e-6f);
+    combined = gs / fminf(1.f, clip);
+  }
+  const float b1 = a.beta1[t], b2 = a.beta2[t], b3 = a.beta3[t], eps = a.eps[t], decay = a.decay[t];
+  float c1 = 1.f, c2 = 1.f;
+  if (a.bias_correction[t] == 1) {
+    c1 = 1.f - powf(b1, (float)*a.step);
+    c2 = 1.f - powf(b2, (float)*a.step);
+  }
+  for (int64_t i = threadIdx.x; i < n; i += kBlock) {
+    float sg = to_f<G>(g[i]) / combined;
+    const float pv = decay != 0.f ? to_f<P>(p[i]) : 0.f;
+    if (a.mode == 0) sg += decay * pv;
+    const float mv = to_f<P>(m[i]) * b1 + b3 * sg;
+    const float vv = to_f<P>(v[i]) * b2 + (1.f - b2) * sg * sg;
+    float upd = (mv / c1) / (sqrtf(vv / c2) + eps);
+    if (a.mode != 0) upd += decay * pv;
+    m[i] = from_f<P>(mv);
+    v[i] = from_f<P>(vv);
+    u[i] = upd;
+  }
+}
+
+template <typename P, typename C>
+__global__ __launch_bounds__(kBlock) void k_distlamb_s2(MTAView view, DistLambStage2Args a, const int* noop) {
+  if (*noop != 0) return;
+  const int c = blockIdx.x;
+  const int t = view.chunk_tensor[c];
+  const int64_t base = (int64_t)view.chunk_local[c] * view.chunk;
+  const int64_t n = min((int64_t)view.chunk, view.numel[t] - base);
+  P* p = plan_ptr<P>(view, 0, t, base);
+  const float* u = plan_ptr<const float>(view, 1, t, base);
+  C* pc = view.depth > 2 ? plan_ptr<C>(view, 2, t, base) : nullptr;
+  float ratio = *a.lr;
+  if (a.use_nvlamb || a.decay[t] != 0.f) {
+    const float pn = a.param_norm[t], un = a.update_norm[a.update_norm_offset[t]];
+    ratio = (un != 0.f && pn != 0.f) ? *a.lr * (pn / un) : *a.lr;
+  }
+  for (int64_t i = threadIdx.x; i < n; i += kBlock) {
+    const float pv = to_f<P>(p[i]) - ratio * u[i];
+    p[i] = from_f<P>(pv);
+    if (pc) stf<C>(pc, i, pv);
+  }
+}
+
 int grid_for(int64_t n, int per_thread) {
   const int64_t b = (n + (int64_t)kBlock * per_thread - 1) / ((int64_t)kBlock * per_thread);
   return (int)std::max<int64_t>(1, std::min<int64_t>(b, 256 * 8));
@@ -294,6 +355,22 @@ void maybe_cast_mt(const MTAView& view, const int* overflow, int dt_in, int dt_o
   LG_CAST(dt_in, Ti, LG_CAST(dt_out, To,
       hipLaunchKernelGGL((k_cast_mt<Ti, To>), dim3(view.C), dim3(kBlock), 0, s, view, overflow)));
   check_launch("fused_adam_cuda.maybe_cast_mt");
+}
+
+void distopt_lamb_stage1(const MTAView& view, int dt_g, int dt_p, const DistLambStage1Args& a, const int* noop,
+                         hipStream_t s) {
+  if (view.C == 0) return;
+  LG_PARAM(dt_p, P, LG_GRAD(dt_g, G,
+      hipLaunchKernelGGL((k_distlamb_s1<P, G>), dim3(view.C), dim3(kBlock), 0, s, view, a, noop)));
+  check_launch("distributed_lamb_cuda.multi_tensor_lamb_compute_update_term");
+}
+
+void distopt_lamb_stage2(const MTAView& view, int dt_p, int dt_copy, const DistLambStage2Args& a, const int* noop,
+                         hipStream_t s) {
+  if (view.C == 0) return;
+  LG_PARAM(dt_p, P, LG_COPY(view.depth > 2 ? dt_copy : -1, C,
+      hipLaunchKernelGGL((k_distlamb_s2<P, C>), dim3(view.C), dim3(kBlock), 0, s, view, a, noop)));
+  check_launch("distributed_lamb_cuda.multi_tensor_lamb_update_weights");
 }
 
 }  // namespace bh

@@ -44,6 +44,11 @@ def _dist_adam(rank, world, bucket_mb, overlap):
     assert torch.isfinite(n).all()
     opt.step()
     sd = opt.state_dict()
+    assert (sd is not None) == (rank == 0)
+    box = [sd]
+    torch.distributed.broadcast_object_list(box, src=0)  # as if every rank torch.load-ed the file
+    sd = box[0]
+    assert set(sd) == {"gathered_states"} and len(sd["gathered_states"]) == world
     before = [p.detach().clone() for p in model.parameters()]
     opt2 = DistributedFusedAdam(_model(1).parameters(), lr=1e-2, bucket_cap_mb=bucket_mb)
     opt2.load_state_dict(sd)
@@ -58,6 +63,45 @@ def _dist_adam(rank, world, bucket_mb, overlap):
 @pytest.mark.parametrize("bucket_mb,overlap", [(100, True), (0.0005, True), (0.0005, False)])
 def test_distributed_fused_adam(bucket_mb, overlap):
     run_distributed(_dist_adam, 2, bucket_mb, overlap)
+
+
+def _dist_adam_resize(rank, world):
+    """Checkpoint written by 2 shards (tiny buckets) loads into 1 shard (one big bucket) and into 2
+    shards again; continuing training matches the uninterrupted optimizer (reference format:
+    distributed_fused_adam.py:1123-1280, whose own loader needs the same distributed size)."""
+    from beforeholiday_amd.contrib.optimizers import DistributedFusedAdam
+    X, Y = _data(1)  # identical data on every rank: the averaged gradient equals the local one
+    model = _model()
+    opt = DistributedFusedAdam(model.parameters(), lr=1e-2, weight_decay=0.1, bucket_cap_mb=0.0005)
+
+    def step(m, o):
+        o.zero_grad()
+        torch.nn.functional.mse_loss(m(X[0]), Y[0]).backward()
+        o.step()
+
+    for _ in range(2):
+        step(model, opt)
+    box = [opt.state_dict()]
+    torch.distributed.broadcast_object_list(box, src=0)
+    sd = box[0]
+    snapshot = [p.detach().clone() for p in model.parameters()]
+    step(model, opt)  # uninterrupted reference
+    single = torch.distributed.new_group([rank])
+    for group, cap in ((single, 100), (None, 0.0003)):
+        m2 = _model(7)
+        with torch.no_grad():
+            for p, s in zip(m2.parameters(), snapshot):
+                p.copy_(s)
+        o2 = DistributedFusedAdam(m2.parameters(), lr=5.0, bucket_cap_mb=cap, process_group=group)
+        o2.load_state_dict(sd)
+        assert o2.param_groups[0]["lr"] == 1e-2 and o2.state["step"] == 2
+        step(m2, o2)
+        for p, q in zip(m2.parameters(), model.parameters()):
+            torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-6, atol=1e-7)
+
+
+def test_distributed_fused_adam_checkpoint_across_sizes():
+    run_distributed(_dist_adam_resize, 2)
 
 
 def _dist_adam_no_sync(rank, world):
@@ -254,3 +298,85 @@ def test_e5m2_gpu_matches_cpu_reference():
     out = torch.empty(100000, dtype=torch.uint8, device="cuda")
     fac.maybe_cast(None, x.cuda(), out)
     assert torch.equal(out.cpu(), ref)
+
+
+def _dist_lamb_e5m2_and_overflow(rank, world):
+    """e5m2 parameter all-gather: the masters follow the uncompressed run exactly after one step and
+    the model parameters are their e5m2 rounding; a non-finite gradient on ONE rank skips the step
+    everywhere through the device noop flag (reference: distributed_fused_lamb.py e5m2_allgather,
+    multi_tensor_distopt_lamb_kernel.cu:109-506)."""
+    from beforeholiday_amd.contrib.optimizers import DistributedFusedLAMB
+    from beforeholiday_amd.ops import fused_adam_cuda as fac
+    X, Y = _data(world)
+    runs = {}
+    for e5 in (False, True):
+        model = _model()
+        opt = DistributedFusedLAMB(model.parameters(), lr=1e-2, weight_decay=0.01, max_grad_norm=1.0,
+                                   bucket_cap_mb=0.0005, e5m2_allgather=e5)
+        opt.zero_grad()
+        torch.nn.functional.mse_loss(model(X[rank]), Y[rank]).backward()
+        opt.step()
+        runs[e5] = (model, opt)
+    for b0, b1 in zip(runs[False][1]._buckets, runs[True][1]._buckets):
+        torch.testing.assert_close(b0.master, b1.master, rtol=0, atol=0)
+    for p0, p1 in zip(runs[False][0].parameters(), runs[True][0].parameters()):
+        torch.testing.assert_close(p1.detach(), fac.from_e5m2(fac.to_e5m2(p0.detach())), rtol=0, atol=0)
+    # overflow on rank 1 only -> both ranks skip
+    model, opt = runs[False]
+    masters = [b.master.clone() for b in opt._buckets]
+    moments = [b.exp_avg.clone() for b in opt._buckets]
+    opt.zero_grad()
+    loss = torch.nn.functional.mse_loss(model(X[rank]), Y[rank])
+    (loss * (float("inf") if rank == 1 else 1.0)).backward()
+    opt.step()
+    assert int(opt.has_overflow) == 1
+    for b, m0, e0 in zip(opt._buckets, masters, moments):
+        assert torch.equal(b.master, m0) and torch.equal(b.exp_avg, e0)
+    assert int(opt._step_t) == 1
+    sd = opt.state_dict()
+    assert rank != 0 or sd is not None
+
+
+def test_distributed_fused_lamb_e5m2_and_overflow_skip():
+    run_distributed(_dist_lamb_e5m2_and_overflow, 2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("copy_dt", [torch.bfloat16, torch.uint8])
+def test_distributed_lamb_cuda_stages_match_reference(mode, copy_dt):
+    from beforeholiday_amd.ops import distributed_lamb_cuda as dl
+    torch.manual_seed(0)
+    sizes = [5, 4099, 70000]
+    T = len(sizes)
+
+    def make(dev):
+        torch.manual_seed(1)
+        g = [torch.randn(n).to(dev, torch.float16) * 8 for n in sizes]
+        p = [torch.randn(n).to(dev) for n in sizes]
+        m = [torch.randn(n).to(dev) * 0.01 for n in sizes]
+        v = [torch.rand(n).to(dev) * 0.01 for n in sizes]
+        u = [torch.zeros(n, device=dev) for n in sizes]
+        c = [torch.empty(n, dtype=copy_dt, device=dev) for n in sizes]
+        vec = lambda x, dt=torch.float32: torch.tensor(x, dtype=dt, device=dev)  # noqa: E731
+        hp = dict(b1=vec([0.9] * T), b2=vec([0.999] * T), b3=vec([0.1] * T), bc=vec([1, 0, 1], torch.int),
+                  step=vec([3], torch.int), eps=vec([1e-6] * T), decay=vec([0.01, 0.0, 0.02]), gs=vec([8.0]),
+                  gn=vec([40.0]), lr=vec([1e-2]), off=vec([0, 1, 2], torch.long))
+        return [g, p, m, v, u, c], hp
+
+    out = {}
+    for dev in ("cuda", "cpu"):
+        (g, p, m, v, u, c), hp = make(dev)
+        noop = torch.zeros(1, dtype=torch.int, device=dev)
+        dl.multi_tensor_lamb_compute_update_term(65536, noop, [g, p, m, v, u], hp["b1"], hp["b2"], hp["b3"], hp["bc"],
+                                                 hp["step"], hp["eps"], mode, hp["decay"], hp["gs"], hp["gn"], 1.0)
+        pn = torch.stack([t.norm() for t in p])
+        un = torch.stack([t.norm() for t in u])
+        dl.multi_tensor_lamb_update_weights(65536, noop, [p, u, c], pn, un, hp["off"], hp["lr"], hp["decay"], hp["gn"],
+                                            False)
+        out[dev] = [t.cpu() for t in p + m + v + u + c]
+    for a, b in zip(out["cuda"], out["cpu"]):
+        if a.dtype == torch.uint8:
+            assert (a.int() - b.int()).abs().max() <= 1
+        else:
+            torch.testing.assert_close(a.float(), b.float(), rtol=2e-5, atol=2e-6)
