@@ -55,11 +55,14 @@ def install_apex_aliases():
             sys.modules.setdefault(f"apex.{sub}", importlib.import_module(f".{sub}", __name__))
         except ImportError:
             pass
-    from .ops import amp_C, apex_C, fused_adam_cuda
+    from .ops import amp_C, apex_C, distributed_adam_cuda, distributed_lamb_cuda, fused_adam_cuda
 
     sys.modules.setdefault("amp_C", amp_C)
     sys.modules.setdefault("apex_C", apex_C)
+    # python modules with CPU reference paths around the native submodules
     sys.modules.setdefault("fused_adam_cuda", fused_adam_cuda)
+    sys.modules.setdefault("distributed_adam_cuda", distributed_adam_cuda)
+    sys.modules.setdefault("distributed_lamb_cuda", distributed_lamb_cuda)
     # the reference's other top-level extension modules map onto submodules of the native _C
     if _native.available():
         for ext in ("syncbn", "fused_layer_norm_cuda", "fused_dense_cuda", "mlp_cuda", "fused_weight_gradient_mlp_cuda",

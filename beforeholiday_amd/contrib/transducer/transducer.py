@@ -149,7 +149,42 @@ class TransducerLoss(torch.nn.Module):
 
 
 # ------------------------------------------------------------------------------------------ joint
+def _joint_native_ok(f, g):
+    return f.is_cuda and g.is_cuda and f.dtype == g.dtype and f.dtype in (torch.float16, torch.bfloat16, torch.float32) \
+        and f.size(-1) % 8 == 0
+
+
+class _TransducerJointNative(torch.autograd.Function):
+    """HIP joint (kernels/transducer.hip): f + g broadcast-add, packing, ReLU and counter-hash dropout
+    in one pass; the backward regenerates the dropout bits and reads the ReLU mask off the output, so
+    neither pass materialises [B, T, U, H] temporaries or a mask tensor."""
+
+    @staticmethod
+    def forward(ctx, f, g, f_len, g_len, pack_output, relu, dropout, batch_offset, packed_batch, dropout_prob,
+                mask_probe):
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())  # host generator: no device sync
+        out, mask = submodule("transducer_joint_cuda").forward(
+            f, g, f_len, g_len, batch_offset, int(packed_batch), bool(pack_output), bool(relu), bool(dropout),
+            float(dropout_prob), seed, mask_probe is not None)
+        if mask_probe is not None:
+            mask_probe.append(mask)
+        ctx.save_for_backward(out if relu else None, f_len, g_len, batch_offset if pack_output else None)
+        ctx.meta = (f.size(1), g.size(1), bool(pack_output), bool(relu), bool(dropout), float(dropout_prob), seed)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        out, f_len, g_len, bo = ctx.saved_tensors
+        T, U, pack, relu, dropout, prob, seed = ctx.meta
+        df, dg = submodule("transducer_joint_cuda").backward(
+            grad, out, f_len, g_len, bo if bo is not None else torch.empty(0, device=grad.device), T, U, pack, relu,
+            dropout, prob, seed)
+        return df, dg, None, None, None, None, None, None, None, None, None
+
+
 class TransducerJointFunc(torch.autograd.Function):
+    """PyTorch reference joint (CPU tensors, or shapes the HIP kernel does not take)."""
+
     @staticmethod
     def forward(ctx, f, g, f_len, g_len, pack_output, relu, dropout, batch_offset, packed_batch, opt, fwd_tile_size,
                 dropout_prob, mask_probe):
@@ -213,5 +248,8 @@ class TransducerJoint(torch.nn.Module):
         if self.pack_output and (batch_offset is None or packed_batch == 0):
             raise Exception("Please specify batch_offset and packed_batch when packing is enabled")
         dropout = self.dropout and self.training
+        if _joint_native_ok(f, g):
+            return _TransducerJointNative.apply(f, g, f_len, g_len, self.pack_output, self.relu, dropout,
+                                                bo.to(f.device), packed_batch, self.dropout_prob, self.mask_probe)
         return TransducerJointFunc.apply(f, g, f_len, g_len, self.pack_output, self.relu, dropout, bo, packed_batch,
                                          self.opt, self.fwd_tile_size, self.dropout_prob, self.mask_probe)

@@ -179,6 +179,90 @@ at::Tensor td_loss_bwd(at::Tensor x, at::Tensor loss_grad, at::Tensor alpha, at:
   return dx;
 }
 
+bh::JointArgs joint_args(int64_t B, int64_t T, int64_t U, int64_t H, const at::Tensor& fl, const at::Tensor& gl,
+                         const at::Tensor& bo, bool pack, int64_t rows, bool relu, bool dropout, double prob,
+                         int64_t seed) {
+  bh::JointArgs a{};
+  a.B = (int)B;
+  a.T = (int)T;
+  a.U = (int)U;
+  a.H = (int)H;
+  a.rows = rows;
+  a.f_len = fl.data_ptr<int>();
+  a.g_len = gl.data_ptr<int>();
+  a.batch_offset = pack ? bo.data_ptr<int64_t>() : nullptr;
+  a.relu = relu;
+  a.dropout = dropout && prob > 0.0;
+  const double keep_thresh = prob * 4294967296.0;
+  a.keep_thresh = (uint32_t)std::min(keep_thresh, 4294967295.0);
+  a.scale = (a.dropout && prob < 1.0) ? (float)(1.0 / (1.0 - prob)) : 1.f;
+  a.seed = (uint32_t)seed;
+  return a;
+}
+
+// returns (out, mask) -- mask (uint8 per output element) only when want_mask
+std::vector<at::Tensor> td_joint_fwd(at::Tensor f, at::Tensor g, at::Tensor f_len, at::Tensor g_len,
+                                     at::Tensor batch_offset, int64_t packed_batch, bool pack_output, bool relu,
+                                     bool dropout, double dropout_prob, int64_t seed, bool want_mask) {
+  check_cuda(f, "f");
+  check_cuda(g, "g");
+  TORCH_CHECK(f.dim() == 3 && g.dim() == 3 && f.size(0) == g.size(0) && f.size(2) == g.size(2),
+              "transducer_joint: f [B, T, H] and g [B, U, H]");
+  TORCH_CHECK(f.scalar_type() == g.scalar_type(), "transducer_joint: f and g must share a dtype");
+  TORCH_CHECK(f.size(2) % 8 == 0, "transducer_joint: hidden size must be a multiple of 8");
+  f = f.contiguous();
+  g = g.contiguous();
+  auto fl = f_len.to(at::kInt).contiguous();
+  auto gl = g_len.to(at::kInt).contiguous();
+  TORCH_CHECK(fl.is_cuda() && gl.is_cuda() && fl.numel() == f.size(0) && gl.numel() == f.size(0),
+              "transducer_joint: f_len / g_len must be GPU tensors of length B");
+  const int64_t B = f.size(0), T = f.size(1), U = g.size(1), H = f.size(2);
+  at::Tensor bo;
+  at::Tensor out;
+  int64_t rows;
+  if (pack_output) {
+    bo = batch_offset.to(at::kLong).contiguous();
+    TORCH_CHECK(bo.is_cuda() && bo.numel() == B, "transducer_joint: batch_offset must be a GPU tensor of length B");
+    rows = packed_batch;
+    out = at::empty({packed_batch, H}, f.options());
+  } else {
+    rows = B * T * U;
+    out = at::empty({B, T, U, H}, f.options());
+  }
+  at::Tensor mask;
+  if (want_mask) mask = at::zeros(out.sizes(), f.options().dtype(at::kByte));
+  auto a = joint_args(B, T, U, H, fl, gl, bo, pack_output, rows, relu, dropout, dropout_prob, seed);
+  bh::transducer_joint_forward(a, dtype_code(f.scalar_type()), f.data_ptr(), g.data_ptr(), out.data_ptr(),
+                               want_mask ? mask.data_ptr<uint8_t>() : nullptr, stream_for(f));
+  return {out, mask};
+}
+
+std::vector<at::Tensor> td_joint_bwd(at::Tensor grad, at::Tensor out, at::Tensor f_len, at::Tensor g_len,
+                                     at::Tensor batch_offset, int64_t T, int64_t U, bool pack_output, bool relu,
+                                     bool dropout, double dropout_prob, int64_t seed) {
+  check_cuda(grad, "grad");
+  grad = grad.contiguous();
+  auto fl = f_len.to(at::kInt).contiguous();
+  auto gl = g_len.to(at::kInt).contiguous();
+  const int64_t B = fl.numel();
+  const int64_t H = grad.size(-1);
+  TORCH_CHECK(H % 8 == 0, "transducer_joint: hidden size must be a multiple of 8");
+  at::Tensor bo;
+  if (pack_output) bo = batch_offset.to(at::kLong).contiguous();
+  const int64_t rows = grad.numel() / H;
+  TORCH_CHECK(pack_output || rows == B * T * U, "transducer_joint backward: grad must be [B, T, U, H]");
+  if (relu) {
+    TORCH_CHECK(out.defined() && out.sizes() == grad.sizes(), "transducer_joint backward: relu needs the output");
+    out = out.contiguous();
+  }
+  auto df = at::empty({B, T, H}, grad.options());
+  auto dg = at::empty({B, U, H}, grad.options());
+  auto a = joint_args(B, T, U, H, fl, gl, bo, pack_output, rows, relu, dropout, dropout_prob, seed);
+  bh::transducer_joint_backward(a, dtype_code(grad.scalar_type()), grad.data_ptr(), relu ? out.data_ptr() : nullptr,
+                                df.data_ptr(), dg.data_ptr(), stream_for(grad));
+  return {df, dg};
+}
+
 void check_perm_matrix(const at::Tensor& m) {
   check_cuda(m, "matrix");
   TORCH_CHECK(m.dim() == 2 && m.scalar_type() == at::kFloat && m.is_contiguous(),
@@ -352,6 +436,9 @@ void register_contrib_impl(pybind11::module_& root) {
   auto tl = root.def_submodule("transducer_loss_cuda", "RNN-T loss");
   tl.def("forward", &td_loss_fwd);
   tl.def("backward", &td_loss_bwd);
+  auto tj = root.def_submodule("transducer_joint_cuda", "RNN-T joint: broadcast add + pack + ReLU + dropout");
+  tj.def("forward", &td_joint_fwd);
+  tj.def("backward", &td_joint_bwd);
   auto ps = root.def_submodule("permutation_search_cuda", "2:4 sparsity channel-permutation search");
   ps.def("sum_after_2_to_4", &perm_sum24, "kept |w| after 2:4 pruning along rows of a [R, C] fp32 matrix");
   ps.def("stripe_pair_gains", &perm_pair_gains, "best re-split gain and split index per stripe pair");

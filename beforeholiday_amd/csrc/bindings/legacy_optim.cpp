@@ -195,9 +195,39 @@ void lamb_update_weights(int64_t chunk_size, at::Tensor noop, std::vector<std::v
   bh::distopt_lamb_stage2(plan.view, dt_p, dt_c, a, noop.data_ptr<int>(), stream_for(lists[0][0]));
 }
 
+void dist_fused_adam(int64_t chunk_size, at::Tensor noop, std::vector<std::vector<at::Tensor>> lists,
+                     at::Tensor beta1, at::Tensor beta2, at::Tensor bias_correction, at::Tensor eps,
+                     at::Tensor weight_decay, double lr, double grad_scale, int64_t step, int64_t mode) {
+  TORCH_CHECK(lists.size() == 4 || lists.size() == 5, "multi_tensor_fused_adam: lists p, m, v, g [, p_copy]");
+  (void)noop;
+  if (lists[0].empty()) return;
+  const int64_t T = lists[0].size();
+  const int dt_p = list_dtype(lists[0], "dist_adam");
+  TORCH_CHECK(list_dtype(lists[1], "dist_adam") == dt_p && list_dtype(lists[2], "dist_adam") == dt_p,
+              "m / v must match p's dtype");
+  const int dt_g = list_dtype(lists[3], "dist_adam");
+  const int dt_c = lists.size() == 5 ? list_dtype(lists[4], "dist_adam") : -1;
+  TORCH_CHECK(bias_correction.is_cuda() && bias_correction.scalar_type() == at::kInt && bias_correction.numel() >= T,
+              "per_tensor_bias_correction must be a GPU int32 tensor");
+  bh::DistAdamArgs a{};
+  a.beta1 = fptr(beta1, "per_tensor_beta1", T);
+  a.beta2 = fptr(beta2, "per_tensor_beta2", T);
+  a.eps = fptr(eps, "per_tensor_eps", T);
+  a.decay = fptr(weight_decay, "per_tensor_weight_decay", T);
+  a.bias_correction = bias_correction.data_ptr<int>();
+  a.lr = (float)lr;
+  a.grad_scale = (float)grad_scale;
+  a.step = (int)step;
+  a.mode = (int)mode;
+  const auto& plan = get_plan(lists, chunk_size);
+  bh::distopt_adam(plan.view, dt_p, dt_g, dt_c, a, stream_for(lists[0][0]));
+}
+
 }  // namespace
 
 void register_legacy_optim(pybind11::module_& root) {
+  auto da = root.def_submodule("distributed_adam_cuda", "per-tensor hyper-parameter multi-tensor Adam (gfx950)");
+  da.def("multi_tensor_fused_adam", &dist_fused_adam, "Multi tensor Adam with per-tensor hyper-parameters.");
   auto dl = root.def_submodule("distributed_lamb_cuda", "ZeRO LAMB stages with device-resident scalars (gfx950)");
   dl.def("multi_tensor_lamb_compute_update_term", &lamb_compute_update_term, "Computes update term for LAMB optimizer");
   dl.def("multi_tensor_lamb_update_weights", &lamb_update_weights, "Applies update term for LAMB optimizer");

@@ -69,3 +69,19 @@ void distopt_lamb_stage2(const MTAView& view, int dt_p, int dt_copy, const DistL
                          hipStream_t s);
 
 }  // namespace bh
+
+namespace bh {
+
+// distributed_adam_cuda.multi_tensor_fused_adam (reference: multi_tensor_distopt_adam_kernel.cu:32-228):
+// lists p, m, v, g [, p_copy]; per-tensor beta1 / beta2 / bias_correction / eps / weight_decay;
+// denom from the bias-corrected v (eps inside the sqrt for mode 0); p -= lr*(m_hat/denom + wd*p).
+struct DistAdamArgs {
+  const float *beta1, *beta2, *eps, *decay;
+  const int* bias_correction;
+  float lr, grad_scale;
+  int step, mode;
+};
+void distopt_adam(const MTAView& view, int dt_p, int dt_g, int dt_copy, const DistAdamArgs& a, hipStream_t s);
+
+}  // namespace bh
+

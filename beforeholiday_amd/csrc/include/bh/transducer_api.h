@@ -17,3 +17,29 @@ void transducer_loss_backward(int dt, const void* x, const float* loss_grad, con
                               bool fuse_softmax, void* dx, hipStream_t st);
 
 }  // namespace bh
+
+namespace bh {
+
+// RNN-T joint: out(b,t,u,:) = f(b,t,:) + g(b,u,:) (+ ReLU) (+ dropout), for t < f_len[b], u < g_len[b].
+// Padded output [B, T, U, H] (invalid rows zero) or packed [rows, H] with row
+// (b ? batch_offset[b-1] : 0) + t*g_len[b] + u. Dropout keep bits come from a keyed counter hash of the
+// (b, t, u, h) index, so the backward regenerates them (no mask tensor); with ReLU the backward mask
+// is (out > 0). mask (optional, uint8 per output element) is only written for the mask probe.
+struct JointArgs {
+  int B, T, U, H;
+  int64_t rows;  // rows of the output / grad tensor (bounds every access)
+  const int* f_len;
+  const int* g_len;
+  const int64_t* batch_offset;  // null: padded output
+  bool relu, dropout;
+  uint32_t keep_thresh;  // keep iff hash >= keep_thresh
+  float scale;           // 1 / (1 - p)
+  uint32_t seed;
+};
+void transducer_joint_forward(const JointArgs& a, int dt, const void* f, const void* g, void* out, uint8_t* mask,
+                              hipStream_t st);
+// df [B, T, H], dg [B, U, H] (both fully written; zeros outside the valid ranges)
+void transducer_joint_backward(const JointArgs& a, int dt, const void* grad, const void* out, void* df, void* dg,
+                               hipStream_t st);
+
+}  // namespace bh

@@ -254,6 +254,38 @@ __global__ __launch_bounds__(kBlock) void k_distlamb_s2(MTAView view, DistLambSt
   }
 }
 
+template <typename P, typename G, typename C>
+__global__ __launch_bounds__(kBlock) void k_distadam(MTAView view, DistAdamArgs a) {
+  const int c = blockIdx.x;
+  const int t = view.chunk_tensor[c];
+  const int64_t base = (int64_t)view.chunk_local[c] * view.chunk;
+  const int64_t n = min((int64_t)view.chunk, view.numel[t] - base);
+  P* p = plan_ptr<P>(view, 0, t, base);
+  P* m = plan_ptr<P>(view, 1, t, base);
+  P* v = plan_ptr<P>(view, 2, t, base);
+  const G* g = plan_ptr<const G>(view, 3, t, base);
+  C* pc = view.depth > 4 ? plan_ptr<C>(view, 4, t, base) : nullptr;
+  const float b1 = a.beta1[t], b2 = a.beta2[t], eps = a.eps[t], decay = a.decay[t];
+  float c1 = 1.f, c2 = 1.f;
+  if (a.bias_correction[t] == 1) {
+    c1 = 1.f - powf(b1, (float)a.step);
+    c2 = 1.f - powf(b2, (float)a.step);
+  }
+  for (int64_t i = threadIdx.x; i < n; i += kBlock) {
+    const float sg = to_f<G>(g[i]) / a.grad_scale;
+    const float pv = to_f<P>(p[i]);
+    const float mv = b1 * to_f<P>(m[i]) + (1.f - b1) * sg;
+    const float vv = b2 * to_f<P>(v[i]) + (1.f - b2) * sg * sg;
+    const float vh = vv / c2;
+    const float denom = a.mode == 0 ? sqrtf(vh + eps) : sqrtf(vh) + eps;
+    const float np = pv - a.lr * ((mv / c1) / denom + decay * pv);
+    m[i] = from_f<P>(mv);
+    v[i] = from_f<P>(vv);
+    p[i] = from_f<P>(np);
+    if (pc) stf<C>(pc, i, np);
+  }
+}
+
 int grid_for(int64_t n, int per_thread) {
   const int64_t b = (n + (int64_t)kBlock * per_thread - 1) / ((int64_t)kBlock * per_thread);
   return (int)std::max<int64_t>(1, std::min<int64_t>(b, 256 * 8));
@@ -355,6 +387,13 @@ void maybe_cast_mt(const MTAView& view, const int* overflow, int dt_in, int dt_o
   LG_CAST(dt_in, Ti, LG_CAST(dt_out, To,
       hipLaunchKernelGGL((k_cast_mt<Ti, To>), dim3(view.C), dim3(kBlock), 0, s, view, overflow)));
   check_launch("fused_adam_cuda.maybe_cast_mt");
+}
+
+void distopt_adam(const MTAView& view, int dt_p, int dt_g, int dt_copy, const DistAdamArgs& a, hipStream_t s) {
+  if (view.C == 0) return;
+  LG_PARAM(dt_p, P, LG_GRAD(dt_g, G, LG_COPY(view.depth > 4 ? dt_copy : -1, C,
+      hipLaunchKernelGGL((k_distadam<P, G, C>), dim3(view.C), dim3(kBlock), 0, s, view, a))));
+  check_launch("distributed_adam_cuda.multi_tensor_fused_adam");
 }
 
 void distopt_lamb_stage1(const MTAView& view, int dt_g, int dt_p, const DistLambStage1Args& a, const int* noop,

@@ -183,3 +183,196 @@ void transducer_loss_backward(int dt, const void* x, const float* loss_grad, con
 }
 
 }  // namespace bh
+
+// ==========================================================================================
+// RNN-T joint (reference: apex/contrib/csrc/transducer/transducer_joint_kernel.cu:177-845)
+//
+// MI355X design: a workgroup owns one (b, t) encoder row and a tile of kJointU prediction rows; each
+// lane keeps its 8-element slice of f in registers and streams g / out in 16-byte vectors, so f is
+// read once per tile and the [B, T, U, H] broadcast is never materialised. ReLU + dropout are fused;
+// dropout bits are a keyed counter hash of the element index (no RNG state, no mask tensor), the
+// backward regenerates them. The two backward reductions (sum over U for df, over T for dg) are
+// separate deterministic passes, one workgroup per output row (no atomics).
+// ==========================================================================================
+#include "bh/transducer_api.h"
+
+namespace bh {
+namespace {
+
+constexpr int kJointU = 4;       // prediction rows per forward workgroup
+constexpr int kJointBlock = 256;
+
+BH_DEVICE uint32_t jmix(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x7feb352du;
+  h ^= h >> 15;
+  h *= 0x846ca68bu;
+  h ^= h >> 16;
+  return h;
+}
+BH_DEVICE uint32_t joint_hash(uint32_t seed, uint64_t i) {
+  const uint32_t k = jmix(seed * 0x9E3779B9u + 0x632BE5ABu);
+  return jmix(jmix((uint32_t)i ^ k) + k * 0x85EBCA6Bu + (uint32_t)(i >> 32) * 0xC2B2AE35u);
+}
+
+BH_DEVICE int64_t joint_row(const JointArgs& a, int b, int t, int u) {
+  if (a.batch_offset) return (b ? a.batch_offset[b - 1] : 0) + (int64_t)t * a.g_len[b] + u;
+  return ((int64_t)b * a.T + t) * a.U + u;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kJointBlock) void k_joint_fwd(JointArgs a, const T* __restrict__ f, const T* __restrict__ g,
+                                                           T* __restrict__ out, uint8_t* __restrict__ mask) {
+  const int bt = blockIdx.x;
+  const int b = bt / a.T, t = bt % a.T;
+  const int u0 = blockIdx.y * kJointU;
+  const int fl = min(a.f_len[b], a.T), gl = min(a.g_len[b], a.U);  // lengths clamped to the tensors
+  const bool packed = a.batch_offset != nullptr;
+  const bool trow = t < fl;
+  if (packed && (!trow || u0 >= gl)) return;  // nothing of this tile exists in the packed output
+  const int H8 = a.H / 8;
+  for (int c = threadIdx.x; c < H8; c += kJointBlock) {
+    float fv[8];
+    if (trow) VecIO<T>::load(f + ((int64_t)b * a.T + t) * a.H + c * 8, fv);
+#pragma unroll
+    for (int j = 0; j < kJointU; ++j) {
+      const int u = u0 + j;
+      if (u >= a.U || (packed && u >= gl)) break;
+      const int64_t row = joint_row(a, b, t, u);
+      if (row < 0 || row >= a.rows) continue;  // inconsistent batch_offset: never write out of bounds
+      float o[8];
+      uint32_t bits = 0u;
+      if (trow && u < gl) {
+        float gv[8];
+        VecIO<T>::load(g + ((int64_t)b * a.U + u) * a.H + c * 8, gv);
+        const uint64_t e0 = (((uint64_t)b * a.T + t) * a.U + u) * (uint64_t)a.H + (uint64_t)c * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float h = fv[k] + gv[k];
+          bool keep = true;
+          if (a.relu && !(h > 0.f)) keep = false;
+          if (a.dropout && joint_hash(a.seed, e0 + k) < a.keep_thresh) keep = false;
+          o[k] = keep ? (a.dropout ? h * a.scale : h) : 0.f;
+          bits |= (uint32_t)keep << k;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = 0.f;  // padded output: invalid rows are zero
+      }
+      VecIO<T>::store(out + row * a.H + c * 8, o);
+      if (mask) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) mask[row * a.H + c * 8 + k] = (uint8_t)((bits >> k) & 1u);
+      }
+    }
+  }
+}
+
+// gradient factor of element (b, t, u, h) given its output value
+template <typename T>
+BH_DEVICE void joint_grad_mask(const JointArgs& a, const T* out, int64_t row, int b, int t, int u, int c,
+                               float (&gr)[8]) {
+  if (a.relu) {
+    float ov[8];
+    VecIO<T>::load(out + row * a.H + c * 8, ov);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (!(ov[k] > 0.f)) gr[k] = 0.f;  // out > 0  <=>  h > 0 and kept
+  } else if (a.dropout) {
+    const uint64_t e0 = (((uint64_t)b * a.T + t) * a.U + u) * (uint64_t)a.H + (uint64_t)c * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (joint_hash(a.seed, e0 + k) < a.keep_thresh) gr[k] = 0.f;
+  }
+  if (a.dropout) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gr[k] *= a.scale;
+  }
+}
+
+// df(b, t, :) = sum_u grad'(b, t, u, :)
+template <typename T>
+__global__ __launch_bounds__(kJointBlock) void k_joint_bwd_f(JointArgs a, const T* __restrict__ grad,
+                                                             const T* __restrict__ out, T* __restrict__ df) {
+  const int bt = blockIdx.x;
+  const int b = bt / a.T, t = bt % a.T;
+  const int fl = min(a.f_len[b], a.T), gl = min(a.g_len[b], a.U);
+  const int H8 = a.H / 8;
+  for (int c = threadIdx.x; c < H8; c += kJointBlock) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (t < fl) {
+      for (int u = 0; u < gl; ++u) {
+        const int64_t row = joint_row(a, b, t, u);
+        if (row < 0 || row >= a.rows) continue;
+        float gr[8];
+        VecIO<T>::load(grad + row * a.H + c * 8, gr);
+        joint_grad_mask(a, out, row, b, t, u, c, gr);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += gr[k];
+      }
+    }
+    VecIO<T>::store(df + ((int64_t)b * a.T + t) * a.H + c * 8, acc);
+  }
+}
+
+// dg(b, u, :) = sum_t grad'(b, t, u, :)
+template <typename T>
+__global__ __launch_bounds__(kJointBlock) void k_joint_bwd_g(JointArgs a, const T* __restrict__ grad,
+                                                             const T* __restrict__ out, T* __restrict__ dg) {
+  const int bu = blockIdx.x;
+  const int b = bu / a.U, u = bu % a.U;
+  const int fl = min(a.f_len[b], a.T), gl = min(a.g_len[b], a.U);
+  const int H8 = a.H / 8;
+  for (int c = threadIdx.x; c < H8; c += kJointBlock) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (u < gl) {
+      for (int t = 0; t < fl; ++t) {
+        const int64_t row = joint_row(a, b, t, u);
+        if (row < 0 || row >= a.rows) continue;
+        float gr[8];
+        VecIO<T>::load(grad + row * a.H + c * 8, gr);
+        joint_grad_mask(a, out, row, b, t, u, c, gr);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += gr[k];
+      }
+    }
+    VecIO<T>::store(dg + ((int64_t)b * a.U + u) * a.H + c * 8, acc);
+  }
+}
+
+#define JOINT_DISPATCH(code, T, ...)                                      \
+  switch (code) {                                                         \
+    case kF32: { using T = float; __VA_ARGS__; } break;                   \
+    case kF16: { using T = f16; __VA_ARGS__; } break;                     \
+    case kBF16: { using T = bf16; __VA_ARGS__; } break;                   \
+    default: throw std::runtime_error("transducer_joint: unsupported dtype " + std::to_string(code)); \
+  }
+
+}  // namespace
+
+void transducer_joint_forward(const JointArgs& a, int dt, const void* f, const void* g, void* out, uint8_t* mask,
+                              hipStream_t st) {
+  if (a.B == 0 || a.T == 0 || a.U == 0 || a.H == 0) return;
+  if (a.H % 8) throw std::runtime_error("transducer_joint: hidden size must be a multiple of 8");
+  const dim3 grid(a.B * a.T, (a.U + kJointU - 1) / kJointU);
+  JOINT_DISPATCH(dt, T,
+      hipLaunchKernelGGL((k_joint_fwd<T>), grid, dim3(kJointBlock), 0, st, a, (const T*)f, (const T*)g, (T*)out, mask));
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("transducer_joint_forward: ") + hipGetErrorString(e));
+}
+
+void transducer_joint_backward(const JointArgs& a, int dt, const void* grad, const void* out, void* df, void* dg,
+                               hipStream_t st) {
+  if (a.B == 0 || a.T == 0 || a.U == 0 || a.H == 0) return;
+  if (a.H % 8) throw std::runtime_error("transducer_joint: hidden size must be a multiple of 8");
+  JOINT_DISPATCH(dt, T, {
+      hipLaunchKernelGGL((k_joint_bwd_f<T>), dim3(a.B * a.T), dim3(kJointBlock), 0, st, a, (const T*)grad,
+                         (const T*)out, (T*)df);
+      hipLaunchKernelGGL((k_joint_bwd_g<T>), dim3(a.B * a.U), dim3(kJointBlock), 0, st, a, (const T*)grad,
+                         (const T*)out, (T*)dg);
+  });
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("transducer_joint_backward: ") + hipGetErrorString(e));
+}
+
+}  // namespace bh

@@ -380,3 +380,26 @@ def test_distributed_lamb_cuda_stages_match_reference(mode, copy_dt):
             assert (a.int() - b.int()).abs().max() <= 1
         else:
             torch.testing.assert_close(a.float(), b.float(), rtol=2e-5, atol=2e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1])
+def test_distributed_adam_cuda_matches_reference(mode):
+    from beforeholiday_amd.ops import distributed_adam_cuda as da
+    sizes = [3, 5000, 65537]
+    T = len(sizes)
+    out = {}
+    for dev in ("cuda", "cpu"):
+        torch.manual_seed(4)
+        p = [torch.randn(n).to(dev) for n in sizes]
+        m = [torch.randn(n).to(dev) * 0.01 for n in sizes]
+        v = [torch.rand(n).to(dev) * 0.01 for n in sizes]
+        g = [(torch.randn(n) * 16).to(dev, torch.float16) for n in sizes]
+        c = [torch.empty(n, dtype=torch.float16, device=dev) for n in sizes]
+        vec = lambda x, dt=torch.float32: torch.tensor(x, dtype=dt, device=dev)  # noqa: E731
+        da.multi_tensor_fused_adam(65536, torch.zeros(1, dtype=torch.int, device=dev), [p, m, v, g, c],
+                                   vec([0.9, 0.8, 0.9]), vec([0.999] * T), vec([1, 1, 0], torch.int),
+                                   vec([1e-8, 1e-6, 1e-8]), vec([0.0, 0.01, 0.1]), 1e-3, 16.0, 4, mode)
+        out[dev] = [t.cpu().float() for t in p + m + v + c]
+    for a, b in zip(out["cuda"], out["cpu"]):
+        torch.testing.assert_close(a, b, rtol=2e-5, atol=2e-6)

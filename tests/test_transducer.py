@@ -116,3 +116,64 @@ def test_transducer_joint(device, pack, relu):
         h.backward(full)
     torch.testing.assert_close(f.grad, fr.grad)
     torch.testing.assert_close(g.grad, gr.grad)
+
+
+@pytest.mark.parametrize("device", devices())
+@pytest.mark.parametrize("pack", [False, True])
+@pytest.mark.parametrize("relu", [False, True])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_transducer_joint_dropout_with_probe(device, pack, relu, dtype):
+    """Fused ReLU + dropout: the probed mask drives an fp32 reference for the output and both input
+    gradients (the HIP backward regenerates the dropout bits from the counter hash)."""
+    from beforeholiday_amd.contrib.transducer import TransducerJoint
+    torch.manual_seed(3)
+    B, T, U, H, p = 3, 7, 9, 64, 0.3
+    f = torch.randn(B, T, H, device=device).to(dtype).requires_grad_()
+    g = torch.randn(B, U, H, device=device).to(dtype).requires_grad_()
+    f_len = torch.tensor([7, 4, 1], device=device)
+    g_len = torch.tensor([9, 5, 2], device=device)
+    bo = torch.cumsum(f_len * g_len, 0)
+    j = TransducerJoint(pack_output=pack, relu=relu, dropout=True, dropout_prob=p, probe_mask=True)
+    j.train()
+    h = j(f, g, f_len, g_len, batch_offset=bo, packed_batch=int(bo[-1]))
+    mask = j.mask_probe[-1].float()
+    assert mask.shape == h.shape
+    hr = f.detach().float().unsqueeze(2) + g.detach().float().unsqueeze(1)
+    rows = [hr[b, :f_len[b], :g_len[b]].reshape(-1, H) for b in range(B)]
+    ref_in = torch.cat(rows)
+    if pack:
+        m_valid = mask
+    else:
+        m_valid = torch.cat([mask[b, :f_len[b], :g_len[b]].reshape(-1, H) for b in range(B)])
+    if relu:
+        assert bool(((ref_in <= 0) & (m_valid > 0)).sum() <= 2)  # relu'd elements are masked (bf16 ties aside)
+    keep_frac = m_valid.mean().item()
+    want = (1 - p) * (0.5 if relu else 1.0)
+    assert abs(keep_frac - want) < 0.05, keep_frac
+    ref_out = ref_in * m_valid / (1 - p)
+    got = h if pack else torch.cat([h[b, :f_len[b], :g_len[b]].reshape(-1, H) for b in range(B)])
+    tol = 1e-5 if dtype == torch.float32 else 3e-2
+    torch.testing.assert_close(got.float(), ref_out, rtol=tol, atol=tol)
+    gh = torch.randn_like(ref_out)
+    if pack:
+        h.backward(gh.to(dtype))
+    else:
+        full = torch.zeros(h.shape, dtype=dtype, device=device)
+        off = 0
+        for b in range(B):
+            n = int(f_len[b] * g_len[b])
+            full[b, :f_len[b], :g_len[b]] = gh[off:off + n].view(int(f_len[b]), int(g_len[b]), H).to(dtype)
+            off += n
+        h.backward(full)
+    gm = gh.to(dtype).float() * m_valid / (1 - p)
+    df = torch.zeros(B, T, H, device=device)
+    dg = torch.zeros(B, U, H, device=device)
+    off = 0
+    for b in range(B):
+        fl, gl = int(f_len[b]), int(g_len[b])
+        blk = gm[off:off + fl * gl].view(fl, gl, H)
+        df[b, :fl] = blk.sum(1)
+        dg[b, :gl] = blk.sum(0)
+        off += fl * gl
+    torch.testing.assert_close(f.grad.float(), df, rtol=tol, atol=tol * 4)
+    torch.testing.assert_close(g.grad.float(), dg, rtol=tol, atol=tol * 4)
