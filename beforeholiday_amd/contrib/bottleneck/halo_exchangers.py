@@ -3,7 +3,8 @@
 ``left_right_halo_exchange(left_output_halo, right_output_halo[, left_input_halo, right_input_halo])``:
 send my boundary rows to the left / right neighbour in ``ranks`` and receive theirs; edge ranks
 receive zeros. Variants: no communication (single rank, wraps), one all-gather over a sub-group,
-and point-to-point (grouped RCCL send/recv — also used for the reference's IPC 'Peer' variant).
+point-to-point (grouped RCCL send/recv on a private communicator, as the reference's nccl_p2p), and
+'Peer' (direct loads / stores into IPC-mapped neighbour memory through peer_memory_cuda).
 """
 import torch
 import torch.distributed as dist
@@ -57,9 +58,20 @@ class HaloExchangerAllGather(HaloExchanger):
 
 
 class HaloExchangerSendRecv(HaloExchanger):
+    """Grouped send/recv on a private communicator (reference: get_unique_nccl_id + broadcast +
+    init_nccl_comm, halo_exchangers.py:69-88); ``group`` overrides it."""
+
     def __init__(self, ranks, rank_in_group, group=None):
         super().__init__(ranks, rank_in_group)
-        self.group = group if group is not None else dist.group.WORLD
+        if group is None:
+            from ..nccl_p2p import get_unique_nccl_id, init_nccl_comm
+
+            uid = get_unique_nccl_id(1)
+            if dist.get_backend() == "nccl":
+                uid = uid.cuda()
+            dist.broadcast(uid, 0)
+            group = init_nccl_comm(uid.cpu(), dist.get_rank(), dist.get_world_size())
+        self.group = group
 
     def left_right_halo_exchange(self, left_output_halo, right_output_halo, left_input_halo=None,
                                  right_input_halo=None):
@@ -72,15 +84,37 @@ class HaloExchangerSendRecv(HaloExchanger):
         right_input_halo.copy_(ri)
 
 
-class HaloExchangerPeer(HaloExchangerSendRecv):
-    """The reference pushes halos through IPC-mapped peer buffers; here the same exchange runs as
-    grouped RCCL send/recv over xGMI (see contrib.peer_memory)."""
+class HaloExchangerPeer(HaloExchanger):
+    """Halos moved through IPC-mapped neighbour memory (peer_memory_cuda.push_pull_halos_1d) when the
+    pool is native; otherwise grouped send/recv over the default group."""
 
     def __init__(self, ranks, rank_in_group, peer_pool, explicit_nhwc, numSM=1):
         super().__init__(ranks, rank_in_group)
         self.peer_pool = peer_pool
         self.explicit_nhwc = explicit_nhwc
         self.numSM = numSM
+        self._peer = None
+        if getattr(peer_pool, "native", False):
+            from ..peer_memory import PeerHaloExchanger1d
+
+            self._peer = PeerHaloExchanger1d(ranks, rank_in_group, peer_pool, 0)
+
+    def left_right_halo_exchange(self, left_output_halo, right_output_halo, left_input_halo=None,
+                                 right_input_halo=None):
+        ret = left_input_halo is None
+        if ret:
+            left_input_halo = torch.empty_like(right_output_halo)
+            right_input_halo = torch.empty_like(left_output_halo)
+        if self._peer is not None and left_output_halo.is_cuda:
+            self._peer.exchange_views(left_output_halo, right_output_halo, left_input_halo, right_input_halo)
+        else:
+            li = torch.empty_like(right_output_halo, memory_format=torch.contiguous_format)
+            ri = torch.empty_like(left_output_halo, memory_format=torch.contiguous_format)
+            _exchange(dist.group.WORLD, self.left_rank, self.right_rank, left_output_halo, right_output_halo, li, ri)
+            left_input_halo.copy_(li)
+            right_input_halo.copy_(ri)
+        if ret:
+            return left_input_halo, right_input_halo
 
 
 class HaloPadder:

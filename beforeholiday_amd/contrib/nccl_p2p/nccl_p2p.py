@@ -1,22 +1,33 @@
-"""Neighbour halo exchange over the process group (reference: apex/contrib/csrc/nccl_p2p/nccl_p2p_cuda.cu,
-``nccl_p2p_cuda``: private NCCL communicator + grouped send/recv).
+"""Neighbour halo exchange on a private communicator (reference: apex/contrib/csrc/nccl_p2p/nccl_p2p_cuda.cu,
+``nccl_p2p_cuda``: ``ncclGetUniqueId`` + ``ncclCommInitRank`` of a second communicator + grouped
+send/recv).
 
-On ROCm the torch.distributed "nccl" backend IS RCCL, so no second communicator is created: a
-"handle" is a process group, and one ``batch_isend_irecv`` group moves both halos (RCCL coalesces
-the sends/receives into one launch on the xGMI links between neighbouring GPUs).
+On ROCm the torch.distributed "nccl" backend IS RCCL: ``init_nccl_comm`` creates a dedicated process
+group over the ranks, i.e. its own RCCL communicator (own streams, never queued behind the default
+group's gradient all-reduces), keyed by the unique id every rank received from rank 0. One
+``batch_isend_irecv`` group then moves both halos (RCCL coalesces the sends / receives into one
+launch on the xGMI links between neighbouring GPUs).
 """
+import os
+
 import torch
 import torch.distributed as dist
 
+_COMMS = {}
+
 
 def get_unique_nccl_id(n):
-    """API shim: RCCL communicators come from torch.distributed; returns a dummy id tensor."""
-    return torch.zeros(n, 128, dtype=torch.uint8)
+    """``n`` random 128-byte communicator ids (uint8 [n, 128]); rank 0's are broadcast by the caller."""
+    return torch.frombuffer(bytearray(os.urandom(128 * n)), dtype=torch.uint8).view(n, 128).clone()
 
 
 def init_nccl_comm(unique_id, my_rank, num_ranks):
-    """Returns the communicator handle (the default process group)."""
-    return dist.group.WORLD
+    """Collective: the private communicator (process group over ranks 0..num_ranks-1) for ``unique_id``."""
+    key = bytes(unique_id.cpu().contiguous().view(-1)[:128].tolist())
+    if key not in _COMMS:
+        assert dist.get_rank() == my_rank, "init_nccl_comm: my_rank must be this process's global rank"
+        _COMMS[key] = dist.new_group(ranks=list(range(num_ranks)))
+    return _COMMS[key]
 
 
 def _exchange(handle, left_rank, right_rank, left_out, right_out, left_in, right_in):
@@ -55,5 +66,6 @@ def left_right_halo_exchange_inplace(handle, left_rank, right_rank, left_output_
 
 
 def add_delay(delay):
-    """Reference debugging hook (spin kernel); a no-op here."""
-    return None
+    """Reference debugging hook: enqueue a ``delay`` ns busy kernel on the current stream (GPU only)."""
+    if torch.cuda.is_available():
+        torch.cuda._sleep(max(1, int(delay * 2.4)))  # ~2.4 GHz shader clock on MI355X

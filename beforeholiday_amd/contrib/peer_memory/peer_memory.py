@@ -1,64 +1,166 @@
 """Peer-memory pool and 1-D halo exchanger (reference: apex/contrib/peer_memory/{peer_memory,
-peer_halo_exchanger_1d}.py, csrc/peer_memory: hipIpc-shared buffers + push/pull kernels with
-flag signalling).
+peer_halo_exchanger_1d}.py, apex/contrib/csrc/peer_memory/peer_memory{.cpp,_cuda.cu}).
 
-MI355X: the host driver here only supports dmabuf IPC, and RCCL already drives the xGMI peer links
-directly, so the pool hands out ordinary device tensors (one per peer slot) and the exchanger moves
-halos with grouped RCCL send/recv between neighbours — the same data movement without IPC
-handles, spin-wait flags or a resident copy kernel.
+MI355X path (GPU tensors, native extension present): :class:`PeerMemoryPool` allocates one raw
+device block per rank, exports it as a HIP IPC handle (dmabuf-backed on this driver), all-gathers
+the handles over the process group and opens every peer's block, so ``allocate_peer_tensors``
+returns the SAME pool offset viewed in every peer's memory (direct loads / stores over xGMI).
+:class:`PeerHaloExchanger1d` runs ``peer_memory_cuda.push_pull_halos_1d``: stage the outgoing
+halos in this rank's transfer slots, publish an epoch flag into each neighbour's memory, wait
+(bounded) for the neighbours' flags and pull their slots straight into the input halos -- one kernel,
+no collective, no host synchronisation (see kernels/peer_memory.hip for the protocol).
+
+Fallback (CPU tensors / no extension, e.g. gloo tests): the pool hands out ordinary tensors and the
+exchanger moves halos with point-to-point send/recv between neighbours.
 """
+from __future__ import annotations
+
+import numpy as np
 import torch
 import torch.distributed as dist
 
+from ... import _native
 from ..nccl_p2p.nccl_p2p import _exchange
+
+_ALIGN = 256
+_VIEW = {torch.float16: "blob_view_half", torch.bfloat16: "blob_view_bfloat16", torch.float32: "blob_view_float",
+         torch.int32: "blob_view_int"}
+
+
+def _pm():
+    return _native.submodule("peer_memory_cuda")
 
 
 class PeerMemoryPool(object):
-    def __init__(self, static_size, dynamic_size, peer_ranks=None):
-        self.peer_ranks = peer_ranks if peer_ranks is not None else list(range(dist.get_world_size()))
-        self.peer_rank = self.peer_ranks.index(dist.get_rank()) if dist.get_rank() in self.peer_ranks else 0
-        self.static_size = static_size
-        self.dynamic_size = dynamic_size
-        self._static = []
-        self._dynamic = []
+    """``static_size`` + ``dynamic_size`` bytes per rank, shared with ``peer_ranks`` (default: the
+    ranks of this node). ``allocate_peer_tensors`` returns one view per peer rank, all at the same offset."""
+
+    def __init__(self, static_size, dynamic_size, peer_ranks=None, group=None):
+        rank = dist.get_rank()
+        world = dist.get_world_size()
+        if peer_ranks is None:
+            from ...parallel.launch import visible_gpu_count
+
+            ngpus = max(1, min(visible_gpu_count() or torch.cuda.device_count(), world))
+            base = (rank // ngpus) * ngpus
+            peer_ranks = list(range(base, base + ngpus))
+        assert rank in peer_ranks, f"rank {rank} is not among peer_ranks {peer_ranks}"
+        self.peer_ranks = list(peer_ranks)
+        self.peer_rank = self.peer_ranks.index(rank)
+        self.alignment = _ALIGN
+        self.static_size = (static_size + _ALIGN - 1) // _ALIGN * _ALIGN
+        self.dynamic_size = (dynamic_size + _ALIGN - 1) // _ALIGN * _ALIGN
+        self.static_offset = 0
+        self.dynamic_offset = 0
+        self.native = torch.cuda.is_available() and _native.available()
+        self.raw = None
+        self.peer_raw = None
+        if self.native:
+            pm = _pm()
+            self.raw = pm.allocate_raw(self.static_size + self.dynamic_size)
+            handle = pm.get_raw_ipc_address(self.raw).numpy().tobytes()
+            handles = [None] * world
+            dist.all_gather_object(handles, handle, group=group)
+            table = torch.from_numpy(np.frombuffer(b"".join(handles[r] for r in self.peer_ranks), dtype=np.uint8)
+                                     .reshape(len(self.peer_ranks), -1).copy())
+            self.peer_raw = pm.get_raw_peers(table, self.peer_rank, self.raw)
+        else:
+            self._host = []
 
     def __del__(self):
-        self._static = self._dynamic = []
+        try:
+            if self.native and self.raw is not None:
+                pm = _pm()
+                pm.close_raw_peers([p for i, p in enumerate(self.peer_raw) if i != self.peer_rank])
+                pm.free_raw(self.raw)
+                self.raw = None
+        except Exception:
+            pass
 
     def reset(self):
-        self._dynamic = []
+        self.dynamic_offset = 0
+
+    def _take(self, nbytes, dynamic):
+        if dynamic:
+            start = (self.dynamic_offset + _ALIGN - 1) // _ALIGN * _ALIGN
+            self.dynamic_offset = start + nbytes
+            assert self.dynamic_offset <= self.dynamic_size, "Dynamic peer memory pool exhausted"
+            return self.static_size + start
+        start = (self.static_offset + _ALIGN - 1) // _ALIGN * _ALIGN
+        self.static_offset = start + nbytes
+        assert self.static_offset <= self.static_size, "Static peer memory pool exhausted"
+        return start
 
     def allocate_peer_tensors(self, shape, dtype, channels_last, dynamic):
+        if dtype not in _VIEW:
+            raise AssertionError("dtype %s not supported" % (str(dtype),))
+        nbytes = int(np.prod(shape)) * torch.empty((), dtype=dtype).element_size()
+        off = self._take(nbytes, dynamic)
+        if self.native:
+            view = getattr(_pm(), _VIEW[dtype])
+            return [view(p + off, list(shape), bool(channels_last)) for p in self.peer_raw]
         fmt = torch.channels_last if channels_last and len(shape) == 4 else torch.contiguous_format
-        dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
-        ts = [torch.zeros(shape, dtype=dtype, device=dev).contiguous(memory_format=fmt) for _ in self.peer_ranks]
-        (self._dynamic if dynamic else self._static).append(ts)
+        ts = [torch.zeros(shape, dtype=dtype).contiguous(memory_format=fmt) for _ in self.peer_ranks]
+        self._host.append(ts)
         return ts
 
 
 class PeerHaloExchanger1d:
-    """In-place halo exchange along H (or W) of a padded activation ``y`` ([N, C, H+2h, W] channels_last
-    or explicit NHWC [N, H+2h, W, C]); first/last ranks get zero halos."""
+    """In-place halo exchange along H (or W) of a padded activation ``y`` ([N, C, H+2h, W], channels_last
+    or not, or explicit NHWC [N, H+2h, W, C]); the first / last rank of the group get zero halos."""
 
-    def __init__(self, ranks, rank_in_group, peer_pool, half_halo):
+    def __init__(self, ranks, rank_in_group, peer_pool, half_halo, max_spins=1 << 22):
         self.peer_group_size = len(ranks)
         self.ranks = ranks
-        self.rank_in_group = rank_in_group
+        self.peer_rank = rank_in_group
+        self.low_neighbor = (rank_in_group + self.peer_group_size - 1) % self.peer_group_size
+        self.high_neighbor = (rank_in_group + 1) % self.peer_group_size
+        self.low_zero = rank_in_group == 0
+        self.high_zero = rank_in_group == self.peer_group_size - 1
         self.peer_pool = peer_pool
         self.half_halo = half_halo
-        self.left_rank = ranks[rank_in_group - 1] if rank_in_group > 0 else -1
-        self.right_rank = ranks[rank_in_group + 1] if rank_in_group < len(ranks) - 1 else -1
+        self.max_spins = max_spins
+        self.epoch = 0
+        self._tx = {}
+        self.native = getattr(peer_pool, "native", False)
+        if self.native:
+            self.signals = peer_pool.allocate_peer_tensors([2, 64], torch.int32, False, False)
+            self.err = torch.zeros(1, dtype=torch.int32, device="cuda")
 
-    def __call__(self, y, H_split=True, explicit_nhwc=False, numSM=0, diagnostics=False):
+    def _slots(self, numel, dtype):
+        key = (numel, dtype)
+        if key not in self._tx:  # same allocation order on every rank -> same pool offsets
+            lo = self.peer_pool.allocate_peer_tensors([2, numel], dtype, False, False)
+            hi = self.peer_pool.allocate_peer_tensors([2, numel], dtype, False, False)
+            self._tx[key] = (lo, hi)
+        return self._tx[key]
+
+    def _views(self, y, H_split, explicit_nhwc):
         h = self.half_halo
         dim = (1 if H_split else 2) if explicit_nhwc else (2 if H_split else 3)
         n = y.size(dim)
-        left_out = y.narrow(dim, h, h)
-        right_out = y.narrow(dim, n - 2 * h, h)
-        left_in = y.narrow(dim, 0, h)
-        right_in = y.narrow(dim, n - h, h)
-        li = torch.empty_like(left_in, memory_format=torch.contiguous_format)
-        ri = torch.empty_like(right_in, memory_format=torch.contiguous_format)
-        _exchange(dist.group.WORLD, self.left_rank, self.right_rank, left_out, right_out, li, ri)
-        left_in.copy_(li)
-        right_in.copy_(ri)
+        return (y.narrow(dim, h, h), y.narrow(dim, n - 2 * h, h), y.narrow(dim, 0, h), y.narrow(dim, n - h, h))
+
+    def __call__(self, y, H_split=True, explicit_nhwc=False, numSM=0, diagnostics=False):
+        out_lo, out_hi, in_lo, in_hi = self._views(y, H_split, explicit_nhwc)
+        if not (self.native and y.is_cuda):
+            left = self.ranks[self.low_neighbor] if not self.low_zero else -1
+            right = self.ranks[self.high_neighbor] if not self.high_zero else -1
+            li = torch.empty_like(in_lo, memory_format=torch.contiguous_format)
+            ri = torch.empty_like(in_hi, memory_format=torch.contiguous_format)
+            _exchange(dist.group.WORLD, left, right, out_lo, out_hi, li, ri)
+            in_lo.copy_(li)
+            in_hi.copy_(ri)
+            return
+        self.exchange_views(out_lo, out_hi, in_lo, in_hi, diagnostics)
+
+    def exchange_views(self, out_lo, out_hi, in_lo, in_hi, diagnostics=False):
+        """Native exchange of explicit 4-D halo views (outgoing low / high, incoming low / high)."""
+        self.epoch += 1
+        lo_tx, hi_tx = self._slots(out_lo.numel(), out_lo.dtype)
+        me, lo_n, hi_n = self.peer_rank, self.low_neighbor, self.high_neighbor
+        _pm().push_pull_halos_1d(out_lo, out_hi, in_lo, in_hi, lo_tx[me], hi_tx[me], hi_tx[lo_n], lo_tx[hi_n],
+                                 self.signals[me], self.signals[lo_n], self.signals[hi_n], self.low_zero,
+                                 self.high_zero, self.epoch, self.err, self.max_spins)
+        if diagnostics and int(self.err.item()) != 0:
+            raise RuntimeError("PeerHaloExchanger1d: a neighbour did not publish its halo in time")

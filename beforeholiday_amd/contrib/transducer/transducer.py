@@ -177,7 +177,7 @@ class _TransducerJointNative(torch.autograd.Function):
         out, f_len, g_len, bo = ctx.saved_tensors
         T, U, pack, relu, dropout, prob, seed = ctx.meta
         df, dg = submodule("transducer_joint_cuda").backward(
-            grad, out, f_len, g_len, bo if bo is not None else torch.empty(0, device=grad.device), T, U, pack, relu,
+            grad, out if out is not None else torch.empty(0, device=grad.device), f_len, g_len, bo if bo is not None else torch.empty(0, device=grad.device), T, U, pack, relu,
             dropout, prob, seed)
         return df, dg, None, None, None, None, None, None, None, None, None
 

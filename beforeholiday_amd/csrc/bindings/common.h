@@ -59,6 +59,7 @@ void register_amp_C(pybind11::module_& m);
 void register_norms(pybind11::module_& m);
 void register_syncbn(pybind11::module_& m);
 void register_legacy_optim(pybind11::module_& m);
+void register_peer_memory(pybind11::module_& m);
 void register_softmax(pybind11::module_& m);
 void register_dense(pybind11::module_& m);
 void register_contrib(pybind11::module_& m);

@@ -110,13 +110,13 @@ void strided_check_finite(at::Tensor overflow_flag, at::Tensor p_copy, int64_t s
                            p_copy.data_ptr(), (int)stride, clear_overflow_first != 0, stream_for(p_copy));
 }
 
-const int* flag_ptr(const at::Tensor& f) {
-  if (!f.defined() || f.numel() == 0) return nullptr;
-  TORCH_CHECK(f.is_cuda() && f.scalar_type() == at::kInt, "overflow_flag must be GPU int32");
-  return f.data_ptr<int>();
+const int* flag_ptr(const c10::optional<at::Tensor>& f) {
+  if (!f.has_value() || !f->defined() || f->numel() == 0) return nullptr;
+  TORCH_CHECK(f->is_cuda() && f->scalar_type() == at::kInt, "overflow_flag must be GPU int32");
+  return f->data_ptr<int>();
 }
 
-void maybe_cast(at::Tensor overflow_flag, at::Tensor p_in, at::Tensor p_out) {
+void maybe_cast(c10::optional<at::Tensor> overflow_flag, at::Tensor p_in, at::Tensor p_out) {
   const int64_t n = p_in.numel();
   check_same(p_in, n, "p_in");
   check_same(p_out, n, "p_out");
@@ -124,7 +124,8 @@ void maybe_cast(at::Tensor overflow_flag, at::Tensor p_in, at::Tensor p_out) {
                  dtype_code(p_out.scalar_type()), p_out.data_ptr(), stream_for(p_in));
 }
 
-void maybe_cast_mt(int64_t chunk_size, at::Tensor overflow_flag, std::vector<std::vector<at::Tensor>> lists) {
+void maybe_cast_mt(int64_t chunk_size, c10::optional<at::Tensor> overflow_flag,
+                   std::vector<std::vector<at::Tensor>> lists) {
   TORCH_CHECK(lists.size() == 2, "maybe_cast_mt: tensor lists p_in, p_out");
   if (lists[0].empty()) return;
   const int dt_in = list_dtype(lists[0], "maybe_cast_mt");

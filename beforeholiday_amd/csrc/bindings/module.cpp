@@ -14,4 +14,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   bhb::register_contrib(m);
   bhb::register_misc(m);
   bhb::register_legacy_optim(m);
+  bhb::register_peer_memory(m);
 }

@@ -5,9 +5,10 @@
     python setup.py build_ext --inplace                 # in-tree build, same as python -m beforeholiday_amd._build
 
 Every native module of the reference (amp_C, syncbn, fused_layer_norm_cuda, fused_dense_cuda, mlp_cuda,
-scaled_*softmax_cuda, fast_multihead_attn, xentropy_cuda, focal_loss_cuda, distributed_{adam,lamb}_cuda,
-transducer_*_cuda, peer_memory_cuda, nccl_p2p_cuda, ...) is a submodule of the ONE extension
-``beforeholiday_amd._C``, so there are no per-extension flags: the reference's flags selected which of its
+scaled_*softmax_cuda, fast_multihead_attn, xentropy_cuda, focal_loss_cuda, fused_index_mul_2d,
+fused_adam_cuda, distributed_{adam,lamb}_cuda, transducer_{joint,loss}_cuda, peer_memory_cuda, ...) is a
+submodule of the ONE extension ``beforeholiday_amd._C`` (nccl_p2p is python over torch.distributed's RCCL
+communicators: ``beforeholiday_amd.contrib.nccl_p2p``), so there are no per-extension flags: the reference's flags selected which of its
 ~25 .so files to compile; here one ninja build compiles all kernels for gfx950 (incremental).
 """
 import os
