@@ -15,49 +15,102 @@ def conv3x3(cin, cout, stride=1):
     return nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
 
 
-class _Conv1x1GemmFn(torch.autograd.Function):
-    """1x1 / stride-1 convolution of a channels_last activation as ONE GEMM on its [N*H*W, C] view
-    (no layout change): forward x2d @ W^T, backward dY @ W and dY^T @ x2d (hipBLASLt)."""
+def _time_ms(fn, reps=3):
+    fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+# per-shape choice of the 1x1 / stride-1 convolution paths: {(N, Cin, H, W, Cout, dtype, dir): "gemm" | "miopen"}
+_CONV1X1_CHOICE = {}
+
+
+def _pick(key, gemm_fn, miopen_fn, mode):
+    """``mode`` "gemm" / "miopen" forces a path; "auto" times both once per shape (first call, e.g. a
+    warmup step) and keeps the faster. Measured on MI355X at ResNet-50 / batch 256 (benchmarks/
+    bench_conv_dirs.py): hipBLASLt wins the forward of every channel-expanding 1x1 conv (64->256:
+    0.13 vs 0.21 ms) and most data gradients; MIOpen wins the small-channel 56x56 layers."""
+    if mode != "auto":
+        return mode
+    choice = _CONV1X1_CHOICE.get(key)
+    if choice is None:
+        t_gemm = _time_ms(gemm_fn)
+        t_miopen = _time_ms(miopen_fn)
+        choice = "gemm" if t_gemm < t_miopen else "miopen"
+        _CONV1X1_CHOICE[key] = choice
+    return choice
+
+
+class _Conv1x1Fn(torch.autograd.Function):
+    """1x1 / stride-1 convolution of a channels_last activation. Forward and data gradient run either
+    as ONE hipBLASLt GEMM on the [N*H*W, C] view (no layout change) or as the MIOpen convolution,
+    chosen per shape; the weight gradient -- a K = N*H*W split reduction that hipBLASLt handles badly
+    (1.0 vs 0.14 ms at 64->256 / 56x56) -- always runs on MIOpen."""
 
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, mode):
         n, c, h, w = x.shape
         x2d = x.permute(0, 2, 3, 1).reshape(-1, c)
         w2d = weight.view(weight.size(0), c)
-        y2d = torch.mm(x2d, w2d.t())
+        key = (n, c, h, w, weight.size(0), x.dtype, "fwd")
+        how = _pick(key, lambda: torch.mm(x2d, w2d.t()), lambda: torch.nn.functional.conv2d(x, weight), mode)
+        if how == "gemm":
+            y = torch.mm(x2d, w2d.t()).view(n, h, w, -1).permute(0, 3, 1, 2)
+        else:
+            y = torch.nn.functional.conv2d(x, weight)
         ctx.save_for_backward(x, weight)
-        return y2d.view(n, h, w, -1).permute(0, 3, 1, 2)
+        ctx.mode = mode
+        return y
 
     @staticmethod
     def backward(ctx, gy):
         x, weight = ctx.saved_tensors
         n, c, h, w = x.shape
-        gy2d = gy.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, weight.size(0))
-        w2d = weight.view(weight.size(0), c)
-        gx = None
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        gx = gw = None
+        conv_bwd = torch.ops.aten.convolution_backward
+        args = ([1, 1], [0, 0], [1, 1], False, [0, 0], 1)
         if ctx.needs_input_grad[0]:
-            gx = torch.mm(gy2d, w2d).view(n, h, w, c).permute(0, 3, 1, 2)
-        gw = torch.mm(gy2d.t(), x.permute(0, 2, 3, 1).reshape(-1, c)).view_as(weight)
-        return gx, gw
+            gy2d = gy.permute(0, 2, 3, 1).reshape(-1, weight.size(0))
+            w2d = weight.view(weight.size(0), c)
+            key = (n, c, h, w, weight.size(0), x.dtype, "dgrad")
+            how = _pick(key, lambda: torch.mm(gy2d, w2d),
+                        lambda: conv_bwd(gy, x, weight, None, *args, [True, False, False]), ctx.mode)
+            if how == "gemm":
+                gx = torch.mm(gy2d, w2d).view(n, h, w, c).permute(0, 3, 1, 2)
+            else:
+                gx = conv_bwd(gy, x, weight, None, *args, [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            gw = conv_bwd(gy, x, weight, None, *args, [False, True, False])[1]
+        return gx, gw, None
 
 
 class Conv1x1(nn.Conv2d):
-    """nn.Conv2d(k=1, bias=False) that runs as a GEMM on channels_last GPU activations (stride 1),
-    and as a regular convolution otherwise."""
+    """nn.Conv2d(k=1, bias=False) whose stride-1 channels_last GPU path picks hipBLASLt or MIOpen per
+    shape and direction (``mode`` "auto" / "gemm" / "miopen"); a regular convolution otherwise."""
+
+    def __init__(self, *args, mode="auto", **kw):
+        super().__init__(*args, **kw)
+        self.mode = mode
 
     def forward(self, x):
-        if (x.is_cuda and self.stride == (1, 1) and self.groups == 1 and x.dim() == 4 and
+        if (x.is_cuda and self.stride == (1, 1) and self.groups == 1 and x.dim() == 4 and self.mode != "miopen" and
                 x.is_contiguous(memory_format=torch.channels_last) and x.dtype == self.weight.dtype):
-            return _Conv1x1GemmFn.apply(x, self.weight)
+            return _Conv1x1Fn.apply(x, self.weight, self.mode)
         return super().forward(x)
 
 
-_GEMM_1X1 = False
+_CONV1X1_MODE = "miopen"  # "miopen" (plain nn.Conv2d), "auto" or "gemm" (Conv1x1)
 
 
 def conv1x1(cin, cout, stride=1):
-    if _GEMM_1X1 and stride == 1:
-        return Conv1x1(cin, cout, 1, stride=stride, bias=False)
+    if _CONV1X1_MODE != "miopen" and stride == 1:
+        return Conv1x1(cin, cout, 1, stride=stride, bias=False, mode=_CONV1X1_MODE)
     return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
 
 
@@ -158,22 +211,26 @@ def resnet50(**kw) -> ResNet:
     return ResNet(Bottleneck, [3, 4, 6, 3], **kw)
 
 
-def resnet50_fused(process_group=None, channel_last=True, gemm_1x1=False, stem_pool_fused=True, **kw) -> ResNet:
+def resnet50_fused(process_group=None, channel_last=True, conv1x1_mode="auto", stem_pool_fused=True,
+                   gemm_1x1=None, **kw) -> ResNet:
     """ResNet-50 whose BatchNorms are fused SyncBatchNorms (BN+ReLU and BN+add+ReLU in one pass),
     synchronised over ``process_group`` -- the 'amp O2 + SyncBatchNorm' benchmark model.
-    ``gemm_1x1``: stride-1 1x1 convolutions run as GEMMs on the channels_last view."""
-    global _GEMM_1X1
+    ``conv1x1_mode``: stride-1 1x1 convolutions as hipBLASLt GEMMs on the channels_last view
+    ("gemm"), MIOpen ("miopen"), or the faster of the two per shape and direction ("auto")."""
+    global _CONV1X1_MODE
+    if gemm_1x1 is not None:  # older keyword
+        conv1x1_mode = "gemm" if gemm_1x1 else "miopen"
     from ..parallel import SyncBatchNorm
 
     def norm(c, fuse_relu=False, fuse_maxpool=None):
         return SyncBatchNorm(c, process_group=process_group, channel_last=channel_last, fuse_relu=fuse_relu,
                              fuse_maxpool=fuse_maxpool)
 
-    old, _GEMM_1X1 = _GEMM_1X1, gemm_1x1
+    old, _CONV1X1_MODE = _CONV1X1_MODE, conv1x1_mode
     try:
         return ResNet(Bottleneck, [3, 4, 6, 3], norm_layer=norm, fused=True, stem_pool_fused=stem_pool_fused, **kw)
     finally:
-        _GEMM_1X1 = old
+        _CONV1X1_MODE = old
 
 
 def resnet18_like(**kw) -> ResNet:

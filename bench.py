@@ -78,8 +78,9 @@ def parse():
                          "never queues behind a DDP gradient bucket on the same RCCL stream")
     ap.add_argument("--stem", default="fused", choices=["fused", "unfused"],
                     help="fused: bn1+ReLU+maxpool in one HIP pass; unfused: SyncBN+ReLU then torch max_pool2d")
-    ap.add_argument("--conv1x1", default="miopen", choices=["miopen", "gemm"],
-                    help="stride-1 1x1 convolutions: MIOpen, or GEMMs on the channels_last view")
+    ap.add_argument("--conv1x1", default="auto", choices=["auto", "miopen", "gemm"],
+                    help="stride-1 1x1 convolution forward / data gradient: hipBLASLt GEMMs on the channels_last "
+                         "view, MIOpen, or the faster per shape (auto, timed in the first warmup step)")
     return ap.parse_args()
 
 
@@ -121,7 +122,7 @@ def main():
     torch.manual_seed(1234 + rank)
     bn_group = dist.new_group(list(range(world))) if (world > 1 and args.bn_group == "separate") else None
     model = (resnet50() if args.no_syncbn else resnet50_fused(process_group=bn_group, channel_last=True,
-                                                                   gemm_1x1=args.conv1x1 == "gemm",
+                                                                   conv1x1_mode=args.conv1x1,
                                                                    stem_pool_fused=args.stem == "fused")).cuda()
     model = model.to(memory_format=torch.channels_last)
     global_batch = args.batch * world

@@ -169,11 +169,12 @@ def test_num_batches_and_cumulative_momentum(device, momentum):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["gemm", "auto", "miopen"])
 @pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
-def test_conv1x1_gemm_matches_conv(dtype):
+def test_conv1x1_gemm_matches_conv(dtype, mode):
     from beforeholiday_amd.models.resnet import Conv1x1
     torch.manual_seed(0)
-    m = Conv1x1(64, 96, 1, bias=False).cuda().to(dtype)
+    m = Conv1x1(64, 96, 1, bias=False, mode=mode).cuda().to(dtype)
     x = torch.randn(4, 64, 14, 14, device="cuda", dtype=dtype).to(memory_format=torch.channels_last)
     x.requires_grad_()
     y = m(x)
