@@ -792,10 +792,10 @@ __global__ __launch_bounds__(kBlock) void k_dgrad_generic(const T* __restrict__ 
 struct NhwcGeom {
   int cvb, R, gx;
 };
-NhwcGeom nhwc_geom(int C) {
+NhwcGeom nhwc_geom(int C, int max_cvb = kBlock) {
   const int cv = (C + 7) / 8;
   NhwcGeom g;
-  g.cvb = std::min(cv, kBlock);
+  g.cvb = std::min(std::min(cv, kBlock), std::max(1, max_cvb));
   int R = kBlock / g.cvb;
   int p = 1;
   while (p * 2 <= R) p *= 2;
@@ -827,13 +827,22 @@ int64_t knob_ew_rows() { static const int64_t v = env_knob("BH_BN_EW_ROWS", 8); 
 int64_t knob_stat_blocks() { static const int64_t v = env_knob("BH_BN_STAT_BLOCKS", 1024); return v; }
 int64_t knob_red_blocks() { static const int64_t v = env_knob("BH_BN_RED_BLOCKS", 256); return v; }
 int64_t knob_red_rows() { static const int64_t v = env_knob("BH_BN_RED_ROWS", 32); return v; }
+// channel vectors (x8 channels) per workgroup of the two reductions (stats, backward reduce): fewer
+// channels per workgroup -> more row lanes merged in LDS, so a layer reaches the workgroup target
+// with fewer split partials (small 7x7 / 14x14 layers were latency-bound with one row lane)
+// (bench_bn.py sweep on MI355X: statistics 1.83 -> 1.66 ms per ResNet-50 step with 16 vectors / 1024
+// workgroups; the two-input backward reduction is best left at 256 vectors / 256 workgroups)
+int64_t knob_red_cvb() { static const int64_t v = env_knob("BH_BN_RED_CVB", 256); return v; }
+int64_t knob_stat_cvb() { static const int64_t v = env_knob("BH_BN_STAT_CVB", 16); return v; }
+NhwcGeom red_geom(int C) { return nhwc_geom(C, (int)knob_red_cvb()); }
+NhwcGeom stat_geom(int C) { return nhwc_geom(C, (int)knob_stat_cvb()); }
 
 // small-layer split boost: measured slower on MI355X (bench_bn.py: 28x28x128 stats 27 -> 35 us, the
 // finalize merges more partials), so off by default; BH_BN_SMALL_ELEMS=<elements> enables it.
 int64_t knob_small_elems() { static const int64_t v = env_knob("BH_BN_SMALL_ELEMS", 0); return v; }
 
-int64_t nhwc_splits(const BNShape& s, int64_t target, int64_t min_iter) {
-  const NhwcGeom g = nhwc_geom(s.C);
+int64_t nhwc_splits(const BNShape& s, int64_t target, int64_t min_iter, int geom = 0) {
+  const NhwcGeom g = geom == 2 ? stat_geom(s.C) : geom == 1 ? red_geom(s.C) : nhwc_geom(s.C);
   int64_t splits = std::max<int64_t>(1, target / g.gx);
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, s.outer / (g.R * min_iter)));
   // Small layers (ResNet stages 2-4 at batch 256: 6-32 M elements) are latency-bound with the
@@ -844,21 +853,22 @@ int64_t nhwc_splits(const BNShape& s, int64_t target, int64_t min_iter) {
   return std::max<int64_t>(1, splits);
 }
 
-static int splits_for(const BNShape& s, int64_t target_blocks) {
-  if (s.channels_last) return (int)nhwc_splits(s, target_blocks, knob_red_rows());
+static int splits_for(const BNShape& s, int64_t target_blocks, int geom) {
+  if (s.channels_last)
+    return (int)nhwc_splits(s, target_blocks, geom == 2 ? env_knob("BH_BN_STAT_ROWS", 16) : knob_red_rows(), geom);
   const int64_t per_c = s.outer * s.inner;
   int64_t splits = std::max<int64_t>(1, 2048 / std::max(1, s.C));
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, per_c / (kBlock * 16)));
   return (int)std::max<int64_t>(1, splits);
 }
 
-int bn_num_splits(const BNShape& s) { return splits_for(s, knob_stat_blocks()); }
-int bn_num_splits_reduce(const BNShape& s) { return splits_for(s, knob_red_blocks()); }
+int bn_num_splits(const BNShape& s) { return splits_for(s, knob_stat_blocks(), 2); }
+int bn_num_splits_reduce(const BNShape& s) { return splits_for(s, knob_red_blocks(), 1); }
 
 void bn_stats(const BNShape& s, int dt_x, const void* x, int splits, float* pmean, float* pm2, float* pn,
               hipStream_t st) {
   if (s.channels_last) {
-    const NhwcGeom g = nhwc_geom(s.C);
+    const NhwcGeom g = stat_geom(s.C);
     const int64_t rows_per_split = (s.outer + splits - 1) / splits;
     const size_t shm = sizeof(float) * (2 * g.R * g.cvb * 8 + g.R);
     BN_DISPATCH(dt_x, T,
@@ -933,7 +943,7 @@ void bn_backward_reduce(const BNShape& s, int dt, const void* dy, const void* x,
                         float* p_dyx, hipStream_t st, const uint8_t* mbits) {
   if (dt_z < 0) dt_z = dt;
   if (s.channels_last && s.C % 8 == 0) {
-    const NhwcGeom g = nhwc_geom(s.C);
+    const NhwcGeom g = red_geom(s.C);
     const int64_t rows_per_split = (s.outer + splits - 1) / splits;
     const size_t shm = sizeof(float) * (2 * g.R * g.cvb * 8);
     BN_DISPATCH(dt, T, BN_DISPATCH(dt_z, Tz,

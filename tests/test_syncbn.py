@@ -380,3 +380,34 @@ def test_multirank_stats_kernels_on_shards(mode, dtype, channels_last):
     assert float(count[0]) == n
     torch.testing.assert_close(rm, 0.9 * rm_ref + 0.1 * m_ref, rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(rv, 0.9 * rv_ref + 0.1 * v_ref * n / (n - 1), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["gemm", "auto"])
+def test_fused_resnet_residual_grad_folded_into_conv1(mode):
+    """Bottleneck backward with the residual-branch gradient summed inside conv1's data-gradient GEMM
+    (beta = 1) equals the plain autograd sum (same model with MIOpen 1x1 convolutions)."""
+    from beforeholiday_amd.models import resnet as R
+    torch.manual_seed(0)
+
+    def build(m):
+        old, R._CONV1X1_MODE = R._CONV1X1_MODE, m
+        try:
+            torch.manual_seed(0)
+            norm = lambda c, fuse_relu=False, fuse_maxpool=None: SyncBatchNorm(  # noqa: E731
+                c, channel_last=True, fuse_relu=fuse_relu, fuse_maxpool=fuse_maxpool)
+            return R.ResNet(R.Bottleneck, [2, 2, 1, 1], num_classes=10, norm_layer=norm, fused=True,
+                            stem_pool_fused=True).cuda().to(memory_format=torch.channels_last)
+        finally:
+            R._CONV1X1_MODE = old
+
+    ref, fold = build("miopen"), build(mode)
+    fold.load_state_dict(ref.state_dict())
+    assert any(isinstance(m, R.Conv1x1) for m in fold.modules())
+    x = torch.randn(4, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
+    xr, xf = x.clone().requires_grad_(), x.clone().requires_grad_()
+    ref(xr).square().sum().backward()
+    fold(xf).square().sum().backward()
+    torch.testing.assert_close(xf.grad, xr.grad, rtol=2e-3, atol=2e-3)
+    for (n, p), q in zip(fold.named_parameters(), ref.parameters()):
+        torch.testing.assert_close(p.grad, q.grad, rtol=2e-3, atol=2e-3, msg=n)
