@@ -45,7 +45,8 @@ inline void check_launch(const char* what) {
 template <typename T> BH_DEVICE float ld(const T* p, int64_t i) { return to_f<T>(p[i]); }
 template <typename T> BH_DEVICE float ld_or(const T* p, int64_t i, float d) { return p ? to_f<T>(p[i]) : d; }
 
-constexpr int kFinLanes = 16;  // split-lanes of the finalize kernels (block = 64 ch x 16 = 1024)
+// finalize kernels: 1024-thread blocks of CPB channels x (1024 / CPB) split-lanes
+inline int fin_cpb(int splits) { return splits >= 128 ? 16 : 64; }
 
 // running-stat factor: momentum, or 1/(num_batches_tracked+1) for momentum=None (cumulative
 // average). The counter is only READ here; it is incremented by the following forward kernel
@@ -223,20 +224,22 @@ __global__ __launch_bounds__(kBlock) void k_stats_nchw(const T* __restrict__ x, 
 
 // merge split partials -> local (mean, biased var, count); optionally also the "merge ranks"
 // work for a single rank (running stats, invstd, scale/shift) to save a launch.
-template <typename Tw>
-__global__ __launch_bounds__(64 * kFinLanes) void k_stats_finalize(int C, int splits, bool per_channel_n,
+template <typename Tw, int CPB>
+__global__ __launch_bounds__(1024) void k_stats_finalize(int C, int splits, bool per_channel_n,
                                                            const float* __restrict__ pmean, const float* __restrict__ pm2,
                                                            const float* __restrict__ pn, float* __restrict__ out_local,
                                                            BNFinal fin, const Tw* w, const Tw* b, Tw* rmean, Tw* rvar,
                                                            const Tw* kref, float* __restrict__ out_sums) {
-  // 64 channels x kFinLanes split-lanes per block. The split partials were written by workgroups on
+  // CPB channels x (1024 / CPB) split-lanes per block (CPB = 16 when there are many splits, so a
+  // lane issues <= splits / 64 loads; 64 otherwise). The split partials were written by workgroups on
   // all 8 XCDs, so every load here is a cross-XCD miss (~1 us): the merge is written as plain sums
   // about a common shift K (split 0's mean) -- S1 = sum n_s (m_s - K), S2 = sum m2_s + n_s (m_s - K)^2
   // -- so a lane keeps 8 splits of loads in flight with no division in the chain (a sequential Chan
   // merge serialised one latency round per 4 splits: 14 us per layer at 1024 splits).
-  __shared__ float sh[3][kFinLanes][64];
-  const int cl = threadIdx.x & 63, lane = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  constexpr int kFinLanes = 1024 / CPB;
+  __shared__ float sh[3][kFinLanes][CPB];
+  const int cl = threadIdx.x % CPB, lane = threadIdx.x / CPB;
+  const int c = blockIdx.x * CPB + cl;
   float N = 0.f, S1 = 0.f, S2 = 0.f, K = 0.f;
   if (c < C) {
     K = pmean[c];
@@ -626,14 +629,15 @@ __global__ __launch_bounds__(kBlock) void k_bwd_reduce_generic(const T* __restri
 }
 
 // sum partials; grad_weight = sum_dy_xmu * invstd, grad_bias = sum_dy (local, pre-all-reduce)
-template <typename Tw>
-__global__ __launch_bounds__(64 * kFinLanes) void k_bwd_reduce_finalize(int C, int splits, const float* __restrict__ p_dy,
+template <typename Tw, int CPB>
+__global__ __launch_bounds__(1024) void k_bwd_reduce_finalize(int C, int splits, const float* __restrict__ p_dy,
                                                                 const float* __restrict__ p_dyx,
                                                                 const float* __restrict__ invstd,
                                                                 float* __restrict__ sums, Tw* gw, Tw* gb) {
-  __shared__ float sh[2][kFinLanes][64];
-  const int cl = threadIdx.x & 63, lane = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  constexpr int kFinLanes = 1024 / CPB;
+  __shared__ float sh[2][kFinLanes][CPB];
+  const int cl = threadIdx.x % CPB, lane = threadIdx.x / CPB;
+  const int c = blockIdx.x * CPB + cl;
   float a = 0.f, b = 0.f;
   if (c < C) {
     int s = lane;
@@ -887,12 +891,18 @@ void bn_stats(const BNShape& s, int dt_x, const void* x, int splits, float* pmea
 void bn_stats_finalize(const BNShape& s, int splits, const float* pmean, const float* pm2, const float* pn,
                        float* out_local, const BNFinal& fin, int dt_w, const void* w, const void* b, void* rmean,
                        void* rvar, hipStream_t st, const void* kref, float* out_sums) {
-  const int grid = (s.C + 63) / 64;
   const bool per_channel_n = !s.channels_last;
-  BN_DISPATCH(dt_w, Tw,
-      hipLaunchKernelGGL((k_stats_finalize<Tw>), dim3(grid), dim3(64 * kFinLanes), 0, st, s.C, splits, per_channel_n, pmean, pm2,
-                         pn, out_local, fin, (const Tw*)w, (const Tw*)b, (Tw*)rmean, (Tw*)rvar, (const Tw*)kref,
-                         out_sums));
+  if (fin_cpb(splits) == 16) {
+    BN_DISPATCH(dt_w, Tw,
+        hipLaunchKernelGGL((k_stats_finalize<Tw, 16>), dim3((s.C + 15) / 16), dim3(1024), 0, st, s.C, splits, per_channel_n,
+                           pmean, pm2, pn, out_local, fin, (const Tw*)w, (const Tw*)b, (Tw*)rmean, (Tw*)rvar,
+                           (const Tw*)kref, out_sums));
+  } else {
+    BN_DISPATCH(dt_w, Tw,
+        hipLaunchKernelGGL((k_stats_finalize<Tw, 64>), dim3((s.C + 63) / 64), dim3(1024), 0, st, s.C, splits, per_channel_n,
+                           pmean, pm2, pn, out_local, fin, (const Tw*)w, (const Tw*)b, (Tw*)rmean, (Tw*)rvar,
+                           (const Tw*)kref, out_sums));
+  }
   check_launch("bn_stats_finalize");
 }
 
@@ -967,10 +977,15 @@ void bn_backward_reduce(const BNShape& s, int dt, const void* dy, const void* x,
 
 void bn_backward_reduce_finalize(int C, int splits, const float* p_dy, const float* p_dyx, const float* invstd,
                                  float* sums, int dt_w, void* gw, void* gb, hipStream_t st) {
-  const int grid = (C + 63) / 64;
-  BN_DISPATCH(dt_w, Tw,
-      hipLaunchKernelGGL((k_bwd_reduce_finalize<Tw>), dim3(grid), dim3(64 * kFinLanes), 0, st, C, splits, p_dy, p_dyx, invstd,
-                         sums, (Tw*)gw, (Tw*)gb));
+  if (fin_cpb(splits) == 16) {
+    BN_DISPATCH(dt_w, Tw,
+        hipLaunchKernelGGL((k_bwd_reduce_finalize<Tw, 16>), dim3((C + 15) / 16), dim3(1024), 0, st, C, splits, p_dy, p_dyx,
+                           invstd, sums, (Tw*)gw, (Tw*)gb));
+  } else {
+    BN_DISPATCH(dt_w, Tw,
+        hipLaunchKernelGGL((k_bwd_reduce_finalize<Tw, 64>), dim3((C + 63) / 64), dim3(1024), 0, st, C, splits, p_dy, p_dyx,
+                           invstd, sums, (Tw*)gw, (Tw*)gb));
+  }
   check_launch("bn_backward_reduce_finalize");
 }
 
