@@ -8,6 +8,11 @@
 // the HIP kernels in kernels/dense.hip.
 #include "common.h"
 
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+
 #include "bh/dense_api.h"
 #include "bh/gemm_api.h"
 
@@ -110,6 +115,60 @@ bool mfma_ok(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c) {
                             b.data_ptr(), c.data_ptr());
 }
 
+// Measured dispatch between the MFMA GEMM with the fused epilogue and hipBLASLt + a separate epilogue
+// pass: per (op, dtype, M, N, K, epilogue) both are timed once on the current stream (first call, e.g.
+// a warmup step) and the faster is kept. The MFMA kernel wins where the fused epilogue saves a pass
+// that matters (K <= 1024: the GPT-2-medium fc1 forward, small MLPs); hipBLASLt's main loop wins the
+// large-K shapes (fc2 forward / fc1 backward at K = 4096: 0.12 vs 0.08 ms,
+// profiles/gemm_mfma_big_tile_vs_hipblaslt.jsonl). BH_DENSE_TUNE=0 uses the static K <= 1024 rule;
+// during HIP-graph capture the cached choice (or the static rule) is used, never a timing run.
+bool tune_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("BH_DENSE_TUNE");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
+template <typename F>
+float time_ms(hipStream_t st, F&& fn) {
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  fn();
+  (void)hipEventRecord(e0, st);
+  for (int i = 0; i < 3; ++i) fn();
+  (void)hipEventRecord(e1, st);
+  (void)hipEventSynchronize(e1);
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return ms;
+}
+
+template <typename FA, typename FB>
+bool prefer_mfma(const char* op, const at::Tensor& a, int64_t M, int64_t N, int64_t K, int variant, FA&& mfma,
+                 FB&& lib) {
+  static std::mutex mu;
+  static auto& cache = *new std::map<std::tuple<std::string, int, int64_t, int64_t, int64_t, int>, bool>();
+  const auto key = std::make_tuple(std::string(op), (int)a.scalar_type(), M, N, K, variant);
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  const bool rule = K <= 1024;
+  hipStream_t st = stream_for(a);
+  if (!tune_enabled() || capturing(st)) return rule;
+  const float tm = time_ms(st, mfma);
+  const float tl = time_ms(st, lib);
+  const bool pick = tm < tl;
+  std::lock_guard<std::mutex> lock(mu);
+  cache[key] = pick;
+  return pick;
+}
+
 // y = act(x . w^T + bias), optionally also the pre-activation. x [M,K], w [N,K].
 std::vector<at::Tensor> linear_act(const at::Tensor& x, const at::Tensor& w, const at::Tensor& bias, int act,
                                    bool want_pre) {
@@ -117,7 +176,7 @@ std::vector<at::Tensor> linear_act(const at::Tensor& x, const at::Tensor& w, con
   at::Tensor pre;
   if (want_pre) pre = at::empty_like(y);
   const bool bias_ok = !bias.defined() || (bias.is_contiguous() && al16(bias) && bias.scalar_type() == x.scalar_type());
-  if (bias_ok && mfma_ok(x, w, y)) {
+  auto run_mfma = [&] {
     bh::GemmEpilogue e;
     e.bias = bias.defined() ? bias.data_ptr() : nullptr;
     e.act = act;
@@ -125,11 +184,19 @@ std::vector<at::Tensor> linear_act(const at::Tensor& x, const at::Tensor& w, con
     e.ld_aux = y.size(1);
     bh::gemm_nt(dtype_code(x.scalar_type()), x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), y.data_ptr(),
                 y.stride(0), x.size(0), w.size(0), x.size(1), e, stream_for(x));
-    return {y, pre};
+  };
+  auto run_lib = [&] {
+    if (bias.defined()) at::addmm_out(y, bias, x, w.t());
+    else at::mm_out(y, x, w.t());
+    if (want_pre) pre.copy_(y);
+    act_inplace(y, at::Tensor(), act);
+  };
+  if (bias_ok && mfma_ok(x, w, y) &&
+      prefer_mfma("linear_act", x, x.size(0), w.size(0), x.size(1), act * 2 + (want_pre ? 1 : 0), run_mfma, run_lib)) {
+    run_mfma();
+  } else {
+    run_lib();
   }
-  y = bias.defined() ? at::addmm(bias, x, w.t()) : at::mm(x, w.t());
-  if (want_pre) pre.copy_(y);
-  act_inplace(y, at::Tensor(), act);
   return {y, pre};
 }
 
@@ -140,7 +207,11 @@ std::vector<at::Tensor> linear_dact(const at::Tensor& dy, const at::Tensor& wt, 
   const bool aux_ok = act == bh::kActNone ||
                       (aux.defined() && aux.dim() == 2 && aux.stride(1) == 1 && aux.stride(0) % 8 == 0 && al16(aux) &&
                        aux.scalar_type() == dy.scalar_type());
-  if (aux_ok && mfma_ok(dy, wt, dx)) {
+  auto run_lib = [&] {
+    at::mm_out(dx, dy, wt.t());
+    return act_backward(dx, aux, dx, act, want_bgrad);
+  };
+  auto run_mfma = [&] {
     at::Tensor part, db;
     bh::GemmEpilogue e;
     e.act = act;
@@ -159,11 +230,14 @@ std::vector<at::Tensor> linear_dact(const at::Tensor& dy, const at::Tensor& wt, 
       bh::gemm_colsum_finalize(dtype_code(dy.scalar_type()), part.data_ptr<float>(), slabs, dx.size(1), db.data_ptr(),
                                stream_for(dy));
     }
-    return {dx, db};
+    return db;
+  };
+  if (aux_ok && mfma_ok(dy, wt, dx) &&
+      prefer_mfma("linear_dact", dy, dy.size(0), wt.size(0), dy.size(1), act * 2 + (want_bgrad ? 1 : 0), run_mfma,
+                  run_lib)) {
+    return {dx, run_mfma()};
   }
-  dx = at::mm(dy, wt.t());
-  auto db = act_backward(dx, aux, dx, act, want_bgrad);
-  return {dx, db};
+  return {dx, run_lib()};
 }
 
 // ------------------------------------------------------------------------------------------------
