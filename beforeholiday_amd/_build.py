@@ -52,6 +52,13 @@ def _sources():
     return hip, cpp
 
 
+# per-source extra hipcc flags. attn.hip: the flash kernels take fmaxf / sums of MFMA results in
+# tight VALU budgets; without NaN semantics hipcc emits bare v_max3_f32 trees (no canonicalising
+# v_max per operand), and without SLP it keeps f32 adds scalar (v_pk_add_f32 co-issues badly with
+# MFMA). No kernel in that file tests for NaN.
+_FILE_FLAGS = {"attn.hip": "-fno-honor-nans -fno-slp-vectorize"}
+
+
 def write_ninja() -> str:
     arch = os.environ.get("BH_ARCH", "gfx950")
     debug = os.environ.get("BH_DEBUG", "0") == "1"
@@ -110,6 +117,9 @@ def write_ninja() -> str:
         obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
         objs.append(obj)
         lines.append(f"build {obj}: hip {src}")
+        extra = _FILE_FLAGS.get(os.path.basename(src))
+        if extra:
+            lines.append(f"  hip_flags = $hip_flags {extra}")
     for src in cpp:
         obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
         objs.append(obj)

@@ -29,6 +29,7 @@
 #include "bh/attn_api.h"
 #include "bh/device.h"
 
+#include <cstdlib>
 #include <stdexcept>
 #include <type_traits>
 #include <string>
@@ -419,24 +420,39 @@ BH_DEVICE void flash_tile(int& tile, int& bh) {
   bh = (slot / nx) * 8 + (id & 7);
 }
 
-// 64 rows x 128 B of a head operand: 2 x 16-byte chunks per thread
+// 64 rows x 128 B of a head operand: 2 x 16-byte chunks per thread. The loads are unconditional
+// (rows past `valid` re-read the last valid row) and the zero fill of those rows happens when the
+// registers are written to LDS: a select right after a load would make the compiler wait for the
+// load there, in front of the block's compute, instead of letting it fly under it.
 struct RowRegs {
   i4v v[2];
+  int valid;
 };
 template <typename T>
 BH_DEVICE void rows_load(RowRegs& r, const T* src, int64_t st, int valid, int tid) {
+  r.valid = valid;
+  if (valid >= 64) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int idx = tid + i * kThreads, row = idx >> 3, ch = idx & 7;
-    const i4v v = *reinterpret_cast<const i4v*>(src + (int64_t)min(row, valid - 1) * st + ch * 8);
-    r.v[i] = row < valid ? v : i4v{0, 0, 0, 0};
+    for (int i = 0; i < 2; ++i) {
+      const int idx = tid + i * kThreads;
+      r.v[i] = *reinterpret_cast<const i4v*>(src + (int64_t)(idx >> 3) * st + (idx & 7) * 8);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = tid + i * kThreads;
+      r.v[i] = *reinterpret_cast<const i4v*>(src + (int64_t)min(idx >> 3, valid - 1) * st + (idx & 7) * 8);
+    }
   }
+}
+BH_DEVICE i4v rows_val(const RowRegs& r, int i, int tid) {
+  return ((tid + i * kThreads) >> 3) < r.valid ? r.v[i] : i4v{0, 0, 0, 0};
 }
 BH_DEVICE void rows_store(char* img, const RowRegs& r, int tid) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int idx = tid + i * kThreads;
-    *reinterpret_cast<i4v*>(img + img_off(idx >> 3, idx & 7, 128)) = r.v[i];
+    *reinterpret_cast<i4v*>(img + img_off(idx >> 3, idx & 7, 128)) = rows_val(r, i, tid);
   }
 }
 
@@ -559,8 +575,13 @@ BH_DEVICE uint32_t row_hash(const AttnArgs& a, int bh, int q) {
                                         ((uint32_t)q * 0x85EBCA77u)));
 }
 // one 32-bit hash per (query, key pair): keys 2i and 2i+1 use its low / high 16 bits, so the
-// query-on-lane kernels (forward, dQ) hash once per two scores; thresh is (1 - p) * 65536
-BH_DEVICE uint32_t pair_hash(uint32_t rowh, int k) { return mix32(rowh ^ ((uint32_t)(k >> 1) * 0xC2B2AE3Du)); }
+// query-on-lane kernels (forward, dQ) hash once per two scores; thresh is (1 - p) * 65536. The row
+// hash is a full avalanche; per pair a Weyl step, a 16-bit fold, ONE 32-bit multiply and a fold
+// (the multiply is a quarter-rate instruction: this is the per-score cost of dropout).
+BH_DEVICE uint32_t fold16(uint32_t x) { return x ^ (x >> 16); }
+BH_DEVICE uint32_t pair_hash(uint32_t rowh, int k) {
+  return fold16(fold16(rowh + (uint32_t)(k >> 1) * 0x9E3779B9u) * 0x7feb352du);
+}
 BH_DEVICE bool keep_elem(uint32_t rowh, int k, uint32_t thresh) {
   const uint32_t h = pair_hash(rowh, k);
   return ((k & 1) ? (h >> 16) : (h & 0xffffu)) < thresh;
@@ -695,6 +716,287 @@ __global__ __launch_bounds__(kThreads) void k_flash_fwd(AttnArgs a) {
 #pragma unroll
     for (int dn = 0; dn < 4; ++dn) store4<T>(out + 16 * dn + 4 * fq, O[dn], inv);
     if (fq == 0) a.lse[(int64_t)bh * a.sq + myq] = l > 0.f ? m + __logf(l) : INFINITY;
+  }
+}
+
+// =============================================================================================
+// Flash forward, 32x32x16 form (mask modes 0 / 5: the GPT / BERT-without-padding shapes).
+// Workgroup = 4 waves x 32 query rows. Each wave computes S^T = K.Q^T of a 64-key block as two
+// 32x32 tiles (key on the register index, query on the lane): every K fragment read from LDS now
+// feeds 32 queries, half the LDS bytes per FLOP of the 16x16x32 kernel above, which ran LDS-bound.
+// Softmax runs in base 2 with the scale folded into one fma per score, the running max is raised
+// only when some row's block max exceeds it by more than 2^8 (a wave-uniform vote; P <= 256 is
+// exact enough in bf16 / f16 since the relative rounding is scale-free) and the row sum is kept
+// per half-wave until the epilogue. P^T feeds O^T = V^T.P^T straight from the accumulators; V^T
+// comes from the row-major V image through ds_read_b64_tr_b16. Causal: blocks past a wave's last
+// query are skipped, only blocks crossing the diagonal are masked, tiles are issued heaviest first.
+// =============================================================================================
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+template <typename T> struct Mfma32;
+template <> struct Mfma32<f16> {
+  static BH_DEVICE f16v run(i4v a, i4v b, f16v c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8v, a), __builtin_bit_cast(h8v, b), c, 0, 0, 0);
+  }
+};
+template <> struct Mfma32<bf16> {
+  static BH_DEVICE f16v run(i4v a, i4v b, f16v c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(b8v, a), __builtin_bit_cast(b8v, b), c, 0, 0,
+                                                   0);
+  }
+};
+
+constexpr int kFQ = 128;  // query rows per workgroup of the 32x32 kernels
+
+// 128-B-row image: chunk ^= ((row>>1)&1)<<2 | ((row>>2)&3). Conflict-free for the 32-row
+// ds_read_b128 row reads (every 16-lane group hits 16 distinct 16-B slots) and for the 4-row
+// ds_read_b64_tr_b16 column reads (rows r, r+2 of a 4-row block land in disjoint chunk halves).
+BH_DEVICE int sw_off(int row, int ch) { return row * 128 + ((ch ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3))) << 4); }
+
+BH_DEVICE void rows_store_sw(char* img, const RowRegs& r, int tid) {
+  if (r.valid >= 64) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = tid + i * kThreads;
+      *reinterpret_cast<i4v*>(img + sw_off(idx >> 3, idx & 7)) = r.v[i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = tid + i * kThreads;
+      *reinterpret_cast<i4v*>(img + sw_off(idx >> 3, idx & 7)) = rows_val(r, i, tid);
+    }
+  }
+}
+// per-thread stream over 64-row blocks of one head operand: the row offsets are computed once, a
+// block costs one scalar multiply (kn * st) plus the two loads; only a partial tail block clamps.
+template <typename T> struct RowStream {
+  const T* base;
+  int64_t st;
+  int64_t off[2];
+  BH_DEVICE RowStream(const T* b, int64_t s, int tid) : base(b), st(s) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = tid + i * kThreads;
+      off[i] = (int64_t)(idx >> 3) * s + (idx & 7) * 8;
+    }
+  }
+  BH_DEVICE void load(RowRegs& r, int kn, int n, int tid) const {
+    const int valid = min(kKB, n - kn);
+    if (valid >= kKB) {
+      r.valid = kKB;
+      const T* src = base + (int64_t)kn * st;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) r.v[i] = *reinterpret_cast<const i4v*>(src + off[i]);
+    } else {
+      rows_load<T>(r, base + (int64_t)kn * st, st, valid, tid);
+    }
+  }
+};
+
+// 32x32x16 A operand = rows 32t.. of the image, k = columns 16s.. (lane: row r32, 8 columns at 8h)
+BH_DEVICE i4v frag32_row(const char* img, int r0, int s, int lane) {
+  return *reinterpret_cast<const i4v*>(img + sw_off(r0 + (lane & 31), 2 * s + (lane >> 5)));
+}
+// 32x32x16 A operand V^T[dims 32dn.., keys] whose k order matches an accumulator tile's register
+// order: element j of half h <-> image row k0 + 4h + (j&3) + 8(j>>2); two transposed reads.
+BH_DEVICE i4v frag32_tr(const char* img, int k0, int dn, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int row = k0 + 4 * (lane >> 5) + q, col = 32 * dn + 16 * (g & 1) + 4 * p;
+  const int cb = (col & 7) << 1;
+  const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(img + sw_off(row, col >> 3) + cb));
+  const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(img + sw_off(row + 8, col >> 3) + cb));
+  typedef int bh_i2v __attribute__((ext_vector_type(2)));
+  const bh_i2v l = __builtin_bit_cast(bh_i2v, lo), hh = __builtin_bit_cast(bh_i2v, hi);
+  return i4v{l[0], l[1], hh[0], hh[1]};
+}
+// registers 8u..8u+7 of an accumulator tile as a 16-bit operand (k = those 8 rows)
+template <typename T> BH_DEVICE i4v pack8(const f16v& x, int u) {
+  T v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = from_f<T>(x[8 * u + j]);
+  return *reinterpret_cast<const i4v*>(v);
+}
+// max / sum of a value over the two half-waves (lanes l and l ^ 32): one v_permlane32_swap
+BH_DEVICE float half_pair(float x, bool sum) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x), __builtin_bit_cast(unsigned, x),
+                                                  false, false);
+  const float a = __builtin_bit_cast(float, (unsigned)r[0]), b = __builtin_bit_cast(float, (unsigned)r[1]);
+  return sum ? a + b : fmaxf(a, b);
+}
+
+// attn.hip is built with -fno-honor-nans (no canonicalising v_max in front of every fmaxf of an
+// MFMA result: the max trees below become pure v_max3_f32) and -fno-slp-vectorize (adjacent f32
+// adds are not packed into v_pk_add_f32, which co-issues badly beside MFMAs); see _build.py.
+BH_DEVICE float vmax3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+BH_DEVICE float vadd(float a, float b) { return a + b; }
+// max of the 32 scores of a lane: 16 v_max3_f32, depth 4
+BH_DEVICE float tree_max(const f16v (&S)[2]) {
+  float r[5];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    r[2 * t] = vmax3(vmax3(S[t][0], S[t][1], S[t][2]), vmax3(S[t][3], S[t][4], S[t][5]),
+                     vmax3(S[t][6], S[t][7], S[t][8]));
+    r[2 * t + 1] = vmax3(vmax3(S[t][9], S[t][10], S[t][11]), vmax3(S[t][12], S[t][13], S[t][14]), S[t][15]);
+  }
+  return vmax3(vmax3(r[0], r[1], r[2]), r[3], r[3]);
+}
+
+// 3 waves per SIMD (<= 168 VGPRs): only the first half of the V^T fragments is read ahead of the
+// softmax, the second half after it (measured: 1.13-1.19x over reading all of them ahead at 2 waves)
+template <typename T, int MODE, bool DROP>
+__global__ __launch_bounds__(kThreads, 3) void k_flash_fwd32(AttnArgs a) {
+  constexpr int kImg = kKB * 128;
+  __shared__ __attribute__((aligned(16))) char smem[4 * kImg];  // {K, V} x 2 buffers
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  int qtile, bh;
+  flash_tile(qtile, bh);
+  if (MODE == 5) qtile = gridDim.x - 1 - qtile;  // longest causal prefix first
+  const int q0w = qtile * kFQ + wave * 32;
+  const int myq = q0w + r32;
+
+  const T* K = reinterpret_cast<const T*>(a.k) + (int64_t)bh * a.k_sbh;
+  const T* V = reinterpret_cast<const T*>(a.v) + (int64_t)bh * a.v_sbh;
+  const T* Q = reinterpret_cast<const T*>(a.q) + (int64_t)bh * a.q_sbh;
+  i4v qf[4];  // B operand of S^T = K.Q^T: Q[myq][16s + 8h + 0..7]
+  {
+    const int qr = min(myq, a.sq - 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const i4v*>(Q + (int64_t)qr * a.q_st + 16 * s + 8 * h);
+  }
+  const float c = a.scale * 1.4426950408889634f;  // scores -> base-2 exponents
+  const float kscale = a.p_drop < 1.f ? 1.f / (1.f - a.p_drop) : 0.f;
+  const uint32_t thresh = keep_thresh(a.p_drop);
+  const uint32_t rowh = DROP ? row_hash(a, bh, myq) : 0u;
+  float m = -INFINITY, l = 0.f;  // running base-2 max (shared by both halves), this half's sum
+  f16v O[2];                      // O^T: dims 32dn + (i&3) + 8(i>>2) + 4h, query myq
+#pragma unroll
+  for (int dn = 0; dn < 2; ++dn)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) O[dn][i] = 0.f;
+  const int q_last = min(q0w + 31, a.sq - 1);
+  const int kend = MODE == 5 ? min(a.sk, min(qtile * kFQ + kFQ, a.sq)) : a.sk;
+  const int nb = (kend + kKB - 1) / kKB;
+
+  RowRegs rk, rv;
+  const RowStream<T> ks(K, a.k_st, tid), vs(V, a.v_st, tid);
+  ks.load(rk, 0, a.sk, tid);
+  vs.load(rv, 0, a.sk, tid);
+  rows_store_sw(smem, rk, tid);
+  rows_store_sw(smem + kImg, rv, tid);
+  __syncthreads();
+  for (int ib = 0; ib < nb; ++ib) {
+    const int kb = ib * kKB;
+    const char* kimg = smem + (ib & 1) * 2 * kImg;
+    const char* vimg = kimg + kImg;
+    if (ib + 1 < nb) {
+      ks.load(rk, kb + kKB, a.sk, tid);
+      vs.load(rv, kb + kKB, a.sk, tid);
+    }
+    if (MODE != 5 || kb <= q_last) {  // wave-uniform: a causal block past every query of the wave is skipped
+      // all LDS reads of the block up front (K row fragments, then V^T fragments): the MFMAs then
+      // wait on the first reads only and the V reads land under QK^T and the softmax
+      i4v kf[2][4], vf[2][2][2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) kf[t][s] = frag32_row(kimg, 32 * t, s, lane);
+#pragma unroll
+      for (int t = 0; t < 1; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int dn = 0; dn < 2; ++dn) vf[t][u][dn] = frag32_tr(vimg, 32 * t + 16 * u, dn, lane);
+      f16v S[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) S[t][i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) S[t] = Mfma32<T>::run(kf[t][s], qf[s], S[t]);
+      }
+      // masks as one compare of the register's key offset against a per-lane limit
+      if (kb + kKB > a.sk) {
+        const int lim = a.sk - kb - 4 * h;  // key offset (32t + (i&3) + 8(i>>2)) must stay below
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (32 * t + (i & 3) + 8 * (i >> 2) >= lim) S[t][i] = -INFINITY;
+      }
+      if (MODE == 5 && kb + kKB - 1 > q0w) {
+        const int lim = myq - kb - 4 * h;  // masked: key offset > lim
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (32 * t + (i & 3) + 8 * (i >> 2) > lim) S[t][i] = -INFINITY;
+      }
+      const float mx = half_pair(tree_max(S), false) * c;
+      if (__any(mx > m + 8.f)) {
+        const float mn = fmaxf(m, mx);
+        const float corr = m == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m - mn);
+        l *= corr;
+#pragma unroll
+        for (int dn = 0; dn < 2; ++dn)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) O[dn][i] *= corr;
+        m = mn;
+      }
+      const float nm = m == -INFINITY ? 0.f : -m;
+      float ls[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+          const float p0 = __builtin_amdgcn_exp2f(fmaf(S[t][i], c, nm));
+          const float p1 = __builtin_amdgcn_exp2f(fmaf(S[t][i + 1], c, nm));
+          const int ch = (i >> 1) & 3;
+          ls[ch] = (t == 0 && i < 8) ? vadd(p0, p1) : vadd(vadd(ls[ch], p0), p1);
+          if (DROP) {
+            bool k0, k1;
+            keep_pair(rowh, kb + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h, thresh, k0, k1);
+            S[t][i] = k0 ? p0 : 0.f;
+            S[t][i + 1] = k1 ? p1 : 0.f;
+          } else {
+            S[t][i] = p0;
+            S[t][i + 1] = p1;
+          }
+        }
+      l = vadd(l, vadd(vadd(ls[0], ls[1]), vadd(ls[2], ls[3])));
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int dn = 0; dn < 2; ++dn) vf[1][u][dn] = frag32_tr(vimg, 32 + 16 * u, dn, lane);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const i4v pb = pack8<T>(S[t], u);
+#pragma unroll
+          for (int dn = 0; dn < 2; ++dn) O[dn] = Mfma32<T>::run(vf[t][u][dn], pb, O[dn]);
+        }
+    }
+    if (ib + 1 < nb) {
+      char* nk = smem + ((ib + 1) & 1) * 2 * kImg;
+      rows_store_sw(nk, rk, tid);
+      rows_store_sw(nk + kImg, rv, tid);
+    }
+    __syncthreads();
+  }
+  l = half_pair(l, true);
+  if (myq < a.sq) {
+    const float inv = l > 0.f ? (DROP ? kscale : 1.f) / l : 0.f;
+    T* out = reinterpret_cast<T*>(a.o) + (int64_t)bh * a.o_sbh + (int64_t)myq * a.o_st;
+#pragma unroll
+    for (int dn = 0; dn < 2; ++dn)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const f4v v4 = f4v{O[dn][4 * gq], O[dn][4 * gq + 1], O[dn][4 * gq + 2], O[dn][4 * gq + 3]};
+        store4<T>(out + 32 * dn + 8 * gq + 4 * h, v4, inv);
+      }
+    if (h == 0) a.lse[(int64_t)bh * a.sq + myq] = l > 0.f ? (m + __log2f(l)) * 0.6931471805599453f : INFINITY;
   }
 }
 
@@ -996,6 +1298,23 @@ void attn_backward(int dt, const AttnArgs& a, hipStream_t st) {
 
 void flash_forward(int dt, const AttnArgs& a, hipStream_t st) {
   if (a.sk < 1 || a.sq < 1 || !a.lse) throw std::runtime_error("flash_forward: bad shape or missing lse");
+  static const bool legacy = [] {
+    const char* e = getenv("BH_FLASH_FWD16");
+    return e && e[0] == '1';
+  }();
+  if (!legacy && (a.mask_mode == 0 || a.mask_mode == 5)) {
+    const dim3 grid((unsigned)((a.sq + kFQ - 1) / kFQ), (unsigned)a.BH);
+    flash_dispatch(dt, a.mask_mode, "flash_forward", [&](auto tt, auto mm) {
+      using T = typename decltype(tt)::type;
+      constexpr int M = decltype(mm)::value;
+      if constexpr (M == 0 || M == 5) {
+        if (a.training && a.p_drop > 0.f) hipLaunchKernelGGL((k_flash_fwd32<T, M, true>), grid, dim3(kThreads), 0, st, a);
+        else hipLaunchKernelGGL((k_flash_fwd32<T, M, false>), grid, dim3(kThreads), 0, st, a);
+      }
+    });
+    check_launch("flash_forward");
+    return;
+  }
   const dim3 grid((unsigned)((a.sq + kQB - 1) / kQB), (unsigned)a.BH);
   flash_dispatch(dt, a.mask_mode, "flash_forward", [&](auto tt, auto mm) {
     using T = typename decltype(tt)::type;

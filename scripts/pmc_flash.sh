@@ -1,5 +1,5 @@
 #!/bin/bash
-# rocprofv3 counter passes over benchmarks/pmc_flash.py (flash attention at the BERT-large shape)
+# rocprofv3 counter passes over benchmarks/pmc_flash.py (flash attention); args go to pmc_flash.py
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmcf
 i=0
@@ -8,7 +8,7 @@ for counters in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_M
   i=$((i+1))
   echo "=== pass $i: $counters"
   timeout -s KILL 90 rocprofv3 --pmc $counters --output-format csv -d gpurun_out/pmcf/p$i -o run -- \
-      python3 benchmarks/pmc_flash.py > gpurun_out/pmcf/p$i.log 2>&1
+      python3 benchmarks/pmc_flash.py "$@" > gpurun_out/pmcf/p$i.log 2>&1
   rc=$?
   tail -2 gpurun_out/pmcf/p$i.log
   if [ $rc -ne 0 ]; then echo "pass $i rc=$rc, stopping"; exit $rc; fi
