@@ -1000,6 +1000,305 @@ __global__ __launch_bounds__(kThreads, 3) void k_flash_fwd32(AttnArgs a) {
   }
 }
 
+// dQ, 32x32x16 form (mask modes 0 / 5). Same layout as k_flash_fwd32 (query on the lane): S^T =
+// K.Q^T and dP^T = V.dO^T from K / V row fragments, P^T rebuilt from the saved LSE in base 2,
+// dS^T = P^T (dP^T - delta) stays in registers and feeds dQ^T = K^T.dS^T (K^T by transposed reads
+// of the same K image); the softmax scale is applied once to dQ in the epilogue.
+template <typename T, int MODE, bool DROP>
+__global__ __launch_bounds__(kThreads, 2) void k_flash_dq32(AttnArgs a) {
+  constexpr int kImg = kKB * 128;
+  __shared__ __attribute__((aligned(16))) char smem[4 * kImg];  // {K, V} x 2 buffers
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  int qtile, bh;
+  flash_tile(qtile, bh);
+  if (MODE == 5) qtile = gridDim.x - 1 - qtile;
+  const int q0w = qtile * kFQ + wave * 32;
+  const int myq = q0w + r32;
+  const T* K = reinterpret_cast<const T*>(a.k) + (int64_t)bh * a.k_sbh;
+  const T* V = reinterpret_cast<const T*>(a.v) + (int64_t)bh * a.v_sbh;
+  const T* Q = reinterpret_cast<const T*>(a.q) + (int64_t)bh * a.q_sbh;
+  const T* dO = reinterpret_cast<const T*>(a.dout) + (int64_t)bh * a.do_sbh;
+  const int qr = min(myq, a.sq - 1);
+  i4v qf[4], df[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = *reinterpret_cast<const i4v*>(Q + (int64_t)qr * a.q_st + 16 * s + 8 * h);
+    df[s] = *reinterpret_cast<const i4v*>(dO + (int64_t)qr * a.do_st + 16 * s + 8 * h);
+  }
+  const float c = a.scale * 1.4426950408889634f;
+  const float lse = a.lse[(int64_t)bh * a.sq + qr];
+  const float dl = a.delta[(int64_t)bh * a.sq + qr];
+  const float nl = (myq < a.sq && lse != INFINITY) ? -lse * 1.4426950408889634f : -INFINITY;  // p = 2^(c*s + nl)
+  const float kscale = a.p_drop < 1.f ? 1.f / (1.f - a.p_drop) : 0.f;
+  const uint32_t thresh = keep_thresh(a.p_drop);
+  const uint32_t rowh = DROP ? row_hash(a, bh, myq) : 0u;
+  f16v acc[2];
+#pragma unroll
+  for (int dn = 0; dn < 2; ++dn)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[dn][i] = 0.f;
+  const int q_last = min(q0w + 31, a.sq - 1);
+  const int kend = MODE == 5 ? min(a.sk, min(qtile * kFQ + kFQ, a.sq)) : a.sk;
+  const int nb = (kend + kKB - 1) / kKB;
+  RowRegs rk, rv;
+  const RowStream<T> ks(K, a.k_st, tid), vs(V, a.v_st, tid);
+  ks.load(rk, 0, a.sk, tid);
+  vs.load(rv, 0, a.sk, tid);
+  rows_store_sw(smem, rk, tid);
+  rows_store_sw(smem + kImg, rv, tid);
+  __syncthreads();
+  for (int ib = 0; ib < nb; ++ib) {
+    const int kb = ib * kKB;
+    const char* kimg = smem + (ib & 1) * 2 * kImg;
+    const char* vimg = kimg + kImg;
+    if (ib + 1 < nb) {
+      ks.load(rk, kb + kKB, a.sk, tid);
+      vs.load(rv, kb + kKB, a.sk, tid);
+    }
+    if (MODE != 5 || kb <= q_last) {
+      f16v S[2], P[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        i4v kf[4], vf[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          kf[s] = frag32_row(kimg, 32 * t, s, lane);
+          vf[s] = frag32_row(vimg, 32 * t, s, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) S[t][i] = P[t][i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          S[t] = Mfma32<T>::run(kf[s], qf[s], S[t]);
+          P[t] = Mfma32<T>::run(vf[s], df[s], P[t]);  // dP^T
+        }
+      }
+      if (kb + kKB > a.sk) {
+        const int lim = a.sk - kb - 4 * h;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (32 * t + (i & 3) + 8 * (i >> 2) >= lim) S[t][i] = -INFINITY;
+      }
+      if (MODE == 5 && kb + kKB - 1 > q0w) {
+        const int lim = myq - kb - 4 * h;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (32 * t + (i & 3) + 8 * (i >> 2) > lim) S[t][i] = -INFINITY;
+      }
+      // dS'^T = P^T (dP^T_dropped - delta), into P (scale applied in the epilogue)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+          const float p0 = __builtin_amdgcn_exp2f(fmaf(S[t][i], c, nl));
+          const float p1 = __builtin_amdgcn_exp2f(fmaf(S[t][i + 1], c, nl));
+          if (DROP) {
+            bool k0, k1;
+            keep_pair(rowh, kb + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h, thresh, k0, k1);
+            P[t][i] = p0 * ((k0 ? P[t][i] * kscale : 0.f) - dl);
+            P[t][i + 1] = p1 * ((k1 ? P[t][i + 1] * kscale : 0.f) - dl);
+          } else {
+            P[t][i] = p0 * (P[t][i] - dl);
+            P[t][i + 1] = p1 * (P[t][i + 1] - dl);
+          }
+        }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const i4v sb = pack8<T>(P[t], u);
+#pragma unroll
+          for (int dn = 0; dn < 2; ++dn)
+            acc[dn] = Mfma32<T>::run(frag32_tr(kimg, 32 * t + 16 * u, dn, lane), sb, acc[dn]);
+        }
+    }
+    if (ib + 1 < nb) {
+      char* nk = smem + ((ib + 1) & 1) * 2 * kImg;
+      rows_store_sw(nk, rk, tid);
+      rows_store_sw(nk + kImg, rv, tid);
+    }
+    __syncthreads();
+  }
+  if (myq < a.sq) {
+    T* dq = reinterpret_cast<T*>(a.dq) + (int64_t)bh * a.dq_sbh + (int64_t)myq * a.dq_st;
+#pragma unroll
+    for (int dn = 0; dn < 2; ++dn)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const f4v v4 = f4v{acc[dn][4 * gq], acc[dn][4 * gq + 1], acc[dn][4 * gq + 2], acc[dn][4 * gq + 3]};
+        store4<T>(dq + 32 * dn + 8 * gq + 4 * h, v4, a.scale);
+      }
+  }
+}
+
+// dK / dV, 32x32x16 form (mask modes 0 / 5). Workgroup = 4 waves x 32 keys, key on the lane: S =
+// Q.K^T and dP = dO.V^T per 32-query tile (A = Q / dO row fragments from LDS, B = K / V fragments
+// held in registers), P from the per-query base-2 LSE row constants, and P_dropped / dS feed dV^T
+// = dO^T.P and dK^T = Q^T.dS straight from the accumulators (dO^T, Q^T by transposed reads of the
+// same images). Per 64-query block the LDS also carries the block's -LSE*log2(e), delta and (with
+// dropout) row hashes, read as float4 broadcasts. Causal: key tiles start at the diagonal block and
+// blocks entirely above a wave's keys are skipped; the heaviest key tiles (lowest keys) go first.
+template <typename T, int MODE, bool DROP>
+__global__ __launch_bounds__(kThreads, 2) void k_flash_dkdv32(AttnArgs a) {
+  constexpr int kImg = kQB * 128;
+  constexpr int kBuf = 2 * kImg + 3 * kQB * 4;  // Q, dO images; -lse2, delta, row hash
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  int ktile, bh;
+  flash_tile(ktile, bh);
+  const int k0w = ktile * kFQ + wave * 32;
+  const int mykey = k0w + r32;
+  const T* K = reinterpret_cast<const T*>(a.k) + (int64_t)bh * a.k_sbh;
+  const T* V = reinterpret_cast<const T*>(a.v) + (int64_t)bh * a.v_sbh;
+  const T* Q = reinterpret_cast<const T*>(a.q) + (int64_t)bh * a.q_sbh;
+  const T* dO = reinterpret_cast<const T*>(a.dout) + (int64_t)bh * a.do_sbh;
+  i4v kf[4], vf[4];  // B operands: K[mykey][16s + 8h ..], V[mykey][16s + 8h ..]
+  {
+    const int kr = min(mykey, a.sk - 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[s] = *reinterpret_cast<const i4v*>(K + (int64_t)kr * a.k_st + 16 * s + 8 * h);
+      vf[s] = *reinterpret_cast<const i4v*>(V + (int64_t)kr * a.v_st + 16 * s + 8 * h);
+    }
+  }
+  const float c = a.scale * 1.4426950408889634f;
+  const float kscale = a.p_drop < 1.f ? 1.f / (1.f - a.p_drop) : 0.f;
+  const uint32_t thresh = keep_thresh(a.p_drop);
+  f16v dK[2], dV[2];  // dims 32dn + (i&3) + 8(i>>2) + 4h, key mykey
+#pragma unroll
+  for (int dn = 0; dn < 2; ++dn)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dK[dn][i] = dV[dn][i] = 0.f;
+  const int qstart = MODE == 5 ? (ktile * kFQ / kQB) * kQB : 0;
+  const int nqb = a.sq > qstart ? (a.sq - qstart + kQB - 1) / kQB : 0;
+  const int k_last = min(k0w + 31, a.sk - 1);
+  const float* lseg = a.lse + (int64_t)bh * a.sq;
+  const float* dlg = a.delta + (int64_t)bh * a.sq;
+  RowRegs rq, rd;
+  const RowStream<T> qs(Q, a.q_st, tid), ds(dO, a.do_st, tid);
+  float rl = 0.f;
+  auto load_blk = [&](int q0) {
+    qs.load(rq, q0, a.sq, tid);
+    ds.load(rd, q0, a.sq, tid);
+    if (tid < 3 * kQB) {  // tid / 64: 0 -> -lse*log2(e), 1 -> delta, 2 -> row hash
+      const int q = q0 + (tid & (kQB - 1)), w = tid >> 6;
+      const int qc = min(q, a.sq - 1);
+      if (w == 0) {
+        const float l = lseg[qc];
+        rl = (q < a.sq && l != INFINITY) ? -l * 1.4426950408889634f : -INFINITY;
+      } else if (w == 1) {
+        rl = q < a.sq ? dlg[qc] : 0.f;
+      } else {
+        rl = DROP ? __builtin_bit_cast(float, row_hash(a, bh, q)) : 0.f;
+      }
+    }
+  };
+  auto store_blk = [&](char* buf) {
+    rows_store_sw(buf, rq, tid);
+    rows_store_sw(buf + kImg, rd, tid);
+    if (tid < 3 * kQB) reinterpret_cast<float*>(buf + 2 * kImg)[tid] = rl;
+  };
+  if (nqb > 0) {
+    load_blk(qstart);
+    store_blk(smem);
+  }
+  __syncthreads();
+  for (int iq = 0; iq < nqb; ++iq) {
+    const int q0 = qstart + iq * kQB;
+    const char* qimg = smem + (iq & 1) * kBuf;
+    const char* dimg = qimg + kImg;
+    const float* nlp = reinterpret_cast<const float*>(dimg + kImg);
+    const float* dlp = nlp + kQB;
+    const uint32_t* rhp = reinterpret_cast<const uint32_t*>(dlp + kQB);
+    if (iq + 1 < nqb) load_blk(q0 + kQB);
+    if (MODE != 5 || q0 + kQB - 1 >= k0w) {  // wave-uniform: some query of the block sees a key of the wave
+      f16v S[2], P[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        i4v qa[4], da[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          qa[s] = frag32_row(qimg, 32 * t, s, lane);
+          da[s] = frag32_row(dimg, 32 * t, s, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) S[t][i] = P[t][i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          S[t] = Mfma32<T>::run(qa[s], kf[s], S[t]);
+          P[t] = Mfma32<T>::run(da[s], vf[s], P[t]);  // dP
+        }
+      }
+      if (MODE == 5 && q0 < k0w + 31) {  // diagonal: masked where key > query
+        const int lim = mykey - q0 - 4 * h;  // masked: query offset (32t + (i&3) + 8(i>>2)) < lim
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (32 * t + (i & 3) + 8 * (i >> 2) < lim) S[t][i] = -INFINITY;
+      }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int ql = 32 * t + 8 * g + 4 * h;  // queries ql .. ql+3 in registers 4g .. 4g+3
+          const f4v n4 = *reinterpret_cast<const f4v*>(nlp + ql);
+          const f4v d4 = *reinterpret_cast<const f4v*>(dlp + ql);
+          i4v r4 = i4v{0, 0, 0, 0};
+          if (DROP) r4 = *reinterpret_cast<const i4v*>(rhp + ql);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int i = 4 * g + j;
+            const float p = __builtin_amdgcn_exp2f(fmaf(S[t][i], c, n4[j]));
+            if (DROP) {
+              const bool kp = keep_elem((uint32_t)r4[j], mykey, thresh);
+              const float kk = kp ? kscale : 0.f;
+              S[t][i] = p * kk;                     // P dropped
+              P[t][i] = p * (P[t][i] * kk - d4[j]);  // dS'
+            } else {
+              S[t][i] = p;
+              P[t][i] = p * (P[t][i] - d4[j]);
+            }
+          }
+        }
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const i4v pb = pack8<T>(S[t], u);
+          const i4v sb = pack8<T>(P[t], u);
+#pragma unroll
+          for (int dn = 0; dn < 2; ++dn) {
+            dV[dn] = Mfma32<T>::run(frag32_tr(dimg, 32 * t + 16 * u, dn, lane), pb, dV[dn]);
+            dK[dn] = Mfma32<T>::run(frag32_tr(qimg, 32 * t + 16 * u, dn, lane), sb, dK[dn]);
+          }
+        }
+    }
+    if (iq + 1 < nqb) store_blk(smem + ((iq + 1) & 1) * kBuf);
+    __syncthreads();
+  }
+  (void)k_last;
+  if (mykey < a.sk) {
+    T* dk = reinterpret_cast<T*>(a.dk) + (int64_t)bh * a.dk_sbh + (int64_t)mykey * a.dk_st;
+    T* dv = reinterpret_cast<T*>(a.dv) + (int64_t)bh * a.dv_sbh + (int64_t)mykey * a.dv_st;
+#pragma unroll
+    for (int dn = 0; dn < 2; ++dn)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const f4v k4 = f4v{dK[dn][4 * gq], dK[dn][4 * gq + 1], dK[dn][4 * gq + 2], dK[dn][4 * gq + 3]};
+        const f4v v4 = f4v{dV[dn][4 * gq], dV[dn][4 * gq + 1], dV[dn][4 * gq + 2], dV[dn][4 * gq + 3]};
+        store4<T>(dk + 32 * dn + 8 * gq + 4 * h, k4, a.scale);
+        store4<T>(dv + 32 * dn + 8 * gq + 4 * h, v4, 1.f);
+      }
+  }
+}
+
 // delta[bh, q] = sum_d dO[q, bh, d] * O[q, bh, d]; one 16-lane group per row
 template <typename T>
 __global__ __launch_bounds__(256) void k_flash_delta(AttnArgs a, float* __restrict__ delta) {
@@ -1336,6 +1635,30 @@ void flash_delta(int dt, const AttnArgs& a, float* delta, hipStream_t st) {
 
 void flash_backward(int dt, const AttnArgs& a, hipStream_t st) {
   if (a.sk < 1 || a.sq < 1 || !a.lse || !a.delta) throw std::runtime_error("flash_backward: bad args");
+  static const bool legacy = [] {
+    const char* e = getenv("BH_FLASH_BWD16");
+    return e && e[0] == '1';
+  }();
+  if (!legacy && (a.mask_mode == 0 || a.mask_mode == 5)) {
+    const dim3 gq((unsigned)((a.sq + kFQ - 1) / kFQ), (unsigned)a.BH);
+    const dim3 gk((unsigned)((a.sk + kFQ - 1) / kFQ), (unsigned)a.BH);
+    const bool dr = a.training && a.p_drop > 0.f;
+    flash_dispatch(dt, a.mask_mode, "flash_backward", [&](auto tt, auto mm) {
+      using T = typename decltype(tt)::type;
+      constexpr int M = decltype(mm)::value;
+      if constexpr (M == 0 || M == 5) {
+        if (dr) {
+          hipLaunchKernelGGL((k_flash_dkdv32<T, M, true>), gk, dim3(kThreads), 0, st, a);
+          hipLaunchKernelGGL((k_flash_dq32<T, M, true>), gq, dim3(kThreads), 0, st, a);
+        } else {
+          hipLaunchKernelGGL((k_flash_dkdv32<T, M, false>), gk, dim3(kThreads), 0, st, a);
+          hipLaunchKernelGGL((k_flash_dq32<T, M, false>), gq, dim3(kThreads), 0, st, a);
+        }
+      }
+    });
+    check_launch("flash_backward");
+    return;
+  }
   const dim3 gq((unsigned)((a.sq + kQB - 1) / kQB), (unsigned)a.BH);
   const dim3 gk((unsigned)((a.sk + kKB - 1) / kKB), (unsigned)a.BH);
   flash_dispatch(dt, a.mask_mode, "flash_backward", [&](auto tt, auto mm) {
