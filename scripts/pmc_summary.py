@@ -19,9 +19,9 @@ def main():
                     name = "gemm_nt<" + ("256x256" if big else "128x128") + ">"
                 elif "k_flash_fwd" in name:
                     name = "flash_fwd"
-                elif "k_flash_bwd_dq" in name:
+                elif "k_flash_bwd_dq" in name or "k_flash_dq32" in name:
                     name = "flash_bwd_dq"
-                elif "k_flash_bwd_dkdv" in name:
+                elif "k_flash_bwd_dkdv" in name or "k_flash_dkdv32" in name:
                     name = "flash_bwd_dkdv"
                 elif "attn_fwd" in name:
                     name = "attn_fwd"
