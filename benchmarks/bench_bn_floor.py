@@ -30,7 +30,10 @@ def timeit(fn, iters=50):
 
 
 def main():
+    only = os.environ.get("BN_SHAPE")  # e.g. "14x256": one shape (for rocprofv3 kernel traces)
     for H, C in SHAPES:
+        if only and only != f"{H}x{C}":
+            continue
         x = torch.randn(256, C, H, H, device="cuda", dtype=torch.float16).contiguous(memory_format=torch.channels_last)
         dy = torch.randn_like(x)
         w = torch.rand(C, device="cuda") + 0.5
