@@ -1,0 +1,53 @@
+// `conv_cuda`: direct 3x3 / stride 1 / pad 1 NHWC convolution (kernels/conv.hip), used by the fused
+// ResNet bottleneck for its middle conv (forward, and data gradient through flipped weights).
+#include "common.h"
+
+#include "bh/conv_api.h"
+
+namespace bhb {
+namespace {
+
+bh::Conv3x3Args conv_args(const at::Tensor& x, const at::Tensor& w, const at::Tensor& y) {
+  bh::Conv3x3Args a;
+  a.x = x.data_ptr();
+  a.w = w.data_ptr();
+  a.y = y.data_ptr();
+  a.N = (int)x.size(0);
+  a.C = (int)x.size(1);
+  a.H = (int)x.size(2);
+  a.W = (int)x.size(3);
+  a.K = (int)w.size(0);
+  return a;
+}
+
+bool shapes_ok(const at::Tensor& x, const at::Tensor& w) {
+  return x.is_cuda() && w.is_cuda() && x.dim() == 4 && w.dim() == 4 && w.size(1) == x.size(1) && w.size(2) == 3 &&
+         w.size(3) == 3 && x.scalar_type() == w.scalar_type() &&
+         (x.scalar_type() == at::kHalf || x.scalar_type() == at::kBFloat16) &&
+         x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.size(1) % 64 == 0 && w.size(0) % 64 == 0;
+}
+
+// True when conv3x3_forward covers (x, w): channels_last fp16 / bf16, C and K multiples of 64.
+bool supported(const at::Tensor& x, const at::Tensor& w) { return shapes_ok(x, w); }
+
+// y = conv2d(x, w, stride 1, padding 1) for channels_last x [N, C, H, W], w [K, C, 3, 3]; y channels_last
+at::Tensor conv3x3_forward(const at::Tensor& x, const at::Tensor& w) {
+  TORCH_CHECK(shapes_ok(x, w), "conv3x3_forward: needs channels_last fp16/bf16 x, w [K, C, 3, 3], C and K % 64 == 0");
+  const at::Tensor wc = w.contiguous(at::MemoryFormat::ChannelsLast);  // [K][3][3][C] in memory
+  auto y = at::empty({x.size(0), w.size(0), x.size(2), x.size(3)}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const auto a = conv_args(x, wc, y);
+  TORCH_CHECK(bh::conv3x3_supported(a), "conv3x3_forward: unaligned tensors");
+  bh::conv3x3_forward(dtype_code(x.scalar_type()), a, stream_for(x));
+  return y;
+}
+
+}  // namespace
+
+void register_conv(pybind11::module_& root) {
+  auto m = root.def_submodule("conv_cuda", "direct 3x3 stride-1 NHWC convolution (MFMA implicit GEMM)");
+  m.def("conv3x3_forward", &conv3x3_forward, py::arg("x"), py::arg("weight"),
+        "conv2d(x, weight, stride=1, padding=1) for channels_last fp16 / bf16, C and K multiples of 64");
+  m.def("supported", &supported, py::arg("x"), py::arg("weight"));
+}
+
+}  // namespace bhb

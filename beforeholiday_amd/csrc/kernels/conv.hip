@@ -1,0 +1,223 @@
+// Direct 3x3 / stride 1 / pad 1 NHWC convolution on MFMA 32x32x16 (gfx950): see bh/conv_api.h.
+//
+// Implicit GEMM with the output channel on the MFMA row and the output pixel on the lane:
+//   acc[k_out, pixel] += W[k_out, r, s, c] * X[pixel + (r-1, s-1), c]
+// Workgroup = 4 waves = an 8-row x 32-lane window of output pixels x 64 output channels; wave w owns
+// window rows 2w, 2w+1 (two 32x32 accumulator tiles per 32 output channels). The 32 lanes of a row
+// are 32 consecutive columns of one image (W >= 32: W / 32 column tiles), or G = 2 / 4 images side
+// by side with 16 / 8 lanes each (W <= 16 / 8), so a 14x14 or 7x7 layer still fills the lanes.
+// Per 64-channel input chunk the window's halo (10 rows x (lanes + 2 per image) pixels, zero outside
+// the image) is staged in LDS once -- 144-byte pixel slots keep the 32-pixel fragment reads bank-
+// conflict free -- and read at all nine (r, s) offsets (each input pixel leaves HBM / L2 ~1.3 times
+// instead of 9); the 64x64 weight slice of each (r, s) streams through a double buffer (register
+// prefetch, one barrier per offset), and the next chunk's halo is prefetched into registers while
+// the current chunk computes. Loads are issued unconditionally on clamped addresses and zeroed when
+// written to LDS, so no select waits on a load in front of the MFMAs.
+#include "bh/api.h"
+#include "bh/conv_api.h"
+#include "bh/device.h"
+
+#include <stdexcept>
+#include <string>
+
+namespace bh {
+namespace {
+
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef __bf16 b8v __attribute__((ext_vector_type(8)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef int i4v __attribute__((ext_vector_type(4)));
+
+template <typename T> struct Mfma32;
+template <> struct Mfma32<f16> {
+  static BH_DEVICE f16v run(i4v a, i4v b, f16v c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8v, a), __builtin_bit_cast(h8v, b), c, 0, 0, 0);
+  }
+};
+template <> struct Mfma32<bf16> {
+  static BH_DEVICE f16v run(i4v a, i4v b, f16v c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(b8v, a), __builtin_bit_cast(b8v, b), c, 0, 0,
+                                                   0);
+  }
+};
+
+constexpr int kThreads = 256;
+constexpr int kTH = 8;      // output rows per window (2 per wave)
+constexpr int kBN = 64;     // output channels per workgroup
+constexpr int kCK = 64;     // input channels per chunk
+constexpr int kPix = 144;   // LDS bytes per halo pixel: 128 data + 16 pad
+constexpr int kMaxHC = 40;  // halo columns G * (lanes per image + 2) <= 40
+constexpr int kHaloBytes = (kTH + 2) * kMaxHC * kPix;
+constexpr int kWBytes = kBN * 128;
+constexpr int kHaloPer = ((kTH + 2) * kMaxHC * 8 + kThreads - 1) / kThreads;  // 16-byte pieces per thread
+
+struct Geo {
+  int G, gw, HC, XT, YT;
+};
+
+// 64 x 128-byte weight image, swizzled for the 32-row fragment reads
+BH_DEVICE int wsw(int row, int ch) { return row * 128 + ((ch ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3))) << 4); }
+
+template <typename T>
+__global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
+  __shared__ __attribute__((aligned(16))) char smem[kHaloBytes + 2 * kWBytes];
+  char* halo = smem;
+  char* wb = smem + kHaloBytes;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  int tt = blockIdx.x;
+  const int xt = tt % g.XT;
+  tt /= g.XT;
+  const int yt = tt % g.YT;
+  const int n0 = (tt / g.YT) * g.G, y0 = yt * kTH, x0 = xt * 32;
+  const int k0 = blockIdx.y * kBN;
+  const T* X = reinterpret_cast<const T*>(a.x);
+  const T* Wt = reinterpret_cast<const T*>(a.w);
+  const int C = a.C, H = a.H, W = a.W, N = a.N;
+  const int nch = C / kCK, steps = nch * 9;
+  const int npieces = (kTH + 2) * g.HC * 8;
+
+  // ---- halo staging: registers (prefetch) -> LDS ----
+  i4v hreg[kHaloPer];
+  uint32_t hmask = 0;
+  auto halo_load = [&](int c0) {
+    hmask = 0;
+#pragma unroll
+    for (int i = 0; i < kHaloPer; ++i) {
+      const int q = tid + i * kThreads, pix = q >> 3, ch = q & 7;
+      const int hr = pix / g.HC, hc = pix - hr * g.HC;
+      const int gi = hc / (g.gw + 2), jj = hc - gi * (g.gw + 2);
+      const int n = n0 + gi, y = y0 - 1 + hr, x = x0 - 1 + jj;
+      const bool ok = q < npieces && n < N && y >= 0 && y < H && x >= 0 && x < W;
+      const int64_t off = ok ? (((int64_t)n * H + y) * W + x) * C + c0 + ch * 8 : 0;
+      hreg[i] = *reinterpret_cast<const i4v*>(X + off);
+      hmask |= (ok ? 1u : 0u) << i;
+    }
+  };
+  auto halo_store = [&]() {
+#pragma unroll
+    for (int i = 0; i < kHaloPer; ++i) {
+      const int q = tid + i * kThreads;
+      if (q < npieces)
+        *reinterpret_cast<i4v*>(halo + (q >> 3) * kPix + (q & 7) * 16) =
+            ((hmask >> i) & 1u) ? hreg[i] : i4v{0, 0, 0, 0};
+    }
+  };
+  // ---- weight slice of step t = chunk * 9 + (r * 3 + s): W[k0 .. k0+63][r][s][c0 .. c0+63] ----
+  i4v wreg[2];
+  auto w_load = [&](int step) {
+    const int chunk = step / 9, rs = step - chunk * 9;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int p = tid + i * kThreads, row = p >> 3, ch = p & 7;
+      wreg[i] = *reinterpret_cast<const i4v*>(Wt + ((int64_t)(k0 + row) * 9 + rs) * C + chunk * kCK + ch * 8);
+    }
+  };
+  auto w_store = [&](char* buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int p = tid + i * kThreads;
+      *reinterpret_cast<i4v*>(buf + wsw(p >> 3, p & 7)) = wreg[i];
+    }
+  };
+
+  f16v acc[2][2];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int pb = 0; pb < 2; ++pb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[kb][pb][i] = 0.f;
+  const int gi = r32 / g.gw, jl = r32 - gi * g.gw;
+  const int hcol = gi * (g.gw + 2) + jl;  // this lane's halo column at s = 0
+
+  halo_load(0);
+  w_load(0);
+  halo_store();
+  w_store(wb);
+  __syncthreads();
+  for (int t = 0; t < steps; ++t) {
+    const int chunk = t / 9, rs = t - chunk * 9;
+    if (t + 1 < steps) w_load(t + 1);
+    if (rs == 0 && chunk + 1 < nch) halo_load((chunk + 1) * kCK);
+    const char* wcur = wb + (t & 1) * kWBytes;
+    const int r = rs / 3, s = rs - r * 3;
+    const char* hb0 = halo + ((2 * wave + r) * g.HC + hcol + s) * kPix;  // window row 2w, offset (r, s)
+    const char* hb1 = hb0 + g.HC * kPix;                                  // window row 2w + 1
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int ch = 2 * kk + h;
+      const i4v a0 = *reinterpret_cast<const i4v*>(wcur + wsw(r32, ch));
+      const i4v a1 = *reinterpret_cast<const i4v*>(wcur + wsw(32 + r32, ch));
+      const i4v b0 = *reinterpret_cast<const i4v*>(hb0 + ch * 16);
+      const i4v b1 = *reinterpret_cast<const i4v*>(hb1 + ch * 16);
+      acc[0][0] = Mfma32<T>::run(a0, b0, acc[0][0]);
+      acc[0][1] = Mfma32<T>::run(a0, b1, acc[0][1]);
+      acc[1][0] = Mfma32<T>::run(a1, b0, acc[1][0]);
+      acc[1][1] = Mfma32<T>::run(a1, b1, acc[1][1]);
+    }
+    if (t + 1 < steps) w_store(wb + ((t + 1) & 1) * kWBytes);
+    if (rs == 8 && chunk + 1 < nch) {
+      __syncthreads();  // every wave is done with this chunk's halo
+      halo_store();
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane = pixel, registers = 4 consecutive output channels per group ----
+  const int n = n0 + gi, x = x0 + jl;
+  if (n >= N || x >= W || jl >= g.gw) return;
+  T* Y = reinterpret_cast<T*>(a.y);
+#pragma unroll
+  for (int pb = 0; pb < 2; ++pb) {
+    const int y = y0 + 2 * wave + pb;
+    if (y >= H) continue;
+    T* out = Y + (((int64_t)n * H + y) * W + x) * a.K + k0;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        T o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = from_f<T>(acc[kb][pb][4 * gq + j]);
+        *reinterpret_cast<uint2*>(out + 32 * kb + 8 * gq + 4 * h) = *reinterpret_cast<const uint2*>(o);
+      }
+  }
+}
+
+Geo make_geo(int H, int W) {
+  Geo g;
+  g.G = 1;
+  while (g.G < 4 && 32 / (2 * g.G) >= W) g.G *= 2;  // pack up to 4 narrow images side by side
+  g.gw = 32 / g.G;
+  g.HC = g.G * (g.gw + 2);
+  g.XT = g.G == 1 ? (W + 31) / 32 : 1;
+  g.YT = (H + kTH - 1) / kTH;
+  return g;
+}
+
+}  // namespace
+
+bool conv3x3_supported(const Conv3x3Args& a) {
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  return a.N > 0 && a.H > 0 && a.W > 0 && a.C > 0 && a.K > 0 && a.C % kCK == 0 && a.K % kBN == 0 && al(a.x) &&
+         al(a.w) && al(a.y);
+}
+
+void conv3x3_forward(int dt, const Conv3x3Args& a, hipStream_t st) {
+  if (!conv3x3_supported(a)) throw std::runtime_error("conv3x3_forward: needs C % 64 == 0, K % 64 == 0, aligned tensors");
+  const Geo g = make_geo(a.H, a.W);
+  if (g.HC > kMaxHC) throw std::runtime_error("conv3x3_forward: halo geometry out of range");
+  const int64_t tiles = (int64_t)g.XT * g.YT * ((a.N + g.G - 1) / g.G);
+  const dim3 grid((unsigned)tiles, (unsigned)(a.K / kBN));
+  switch (dt) {
+    case kF16: hipLaunchKernelGGL((k_conv3x3<f16>), grid, dim3(kThreads), 0, st, a, g); break;
+    case kBF16: hipLaunchKernelGGL((k_conv3x3<bf16>), grid, dim3(kThreads), 0, st, a, g); break;
+    default: throw std::runtime_error("conv3x3_forward: fp16 / bf16 only");
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("conv3x3_forward: ") + hipGetErrorString(e));
+}
+
+}  // namespace bh

@@ -12,6 +12,8 @@ import torch.nn as nn
 
 
 def conv3x3(cin, cout, stride=1):
+    if _CONV3X3_MODE != "miopen" and stride == 1:
+        return Conv3x3(cin, cout, 3, stride=1, padding=1, bias=False, mode=_CONV3X3_MODE)
     return nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
 
 
@@ -146,6 +148,72 @@ class Conv1x1(nn.Conv2d):
 
 
 _CONV1X1_MODE = "miopen"  # "miopen" (plain nn.Conv2d), "auto" or "gemm" (Conv1x1)
+_CONV3X3_MODE = "miopen"  # "miopen" (plain nn.Conv2d), "auto" or "direct" (Conv3x3)
+
+
+class _Conv3x3Fn(torch.autograd.Function):
+    """3x3 / stride-1 / pad-1 convolution of a channels_last activation: forward and data gradient
+    on the direct MFMA kernel (kernels/conv.hip; the data gradient is the same kernel on dY with the
+    flipped, transposed weights) or on MIOpen, chosen per shape and direction ("auto" times both once);
+    the weight gradient runs on MIOpen. Measured at ResNet-50 / batch 256 (benchmarks/
+    bench_conv3x3.py): forward 1.45 vs 1.96 ms, data gradient 1.59 vs 1.84 ms per step."""
+
+    @staticmethod
+    def forward(ctx, x, weight, mode):
+        from ..ops import conv as bhconv
+
+        n, c, h, w = x.shape
+        conv = torch.nn.functional.conv2d
+        how = _pick((n, c, h, w, weight.size(0), x.dtype, "fwd3"), lambda: bhconv.conv3x3(x, weight),
+                    lambda: conv(x, weight, padding=1), "gemm" if mode == "direct" else mode)
+        y = bhconv.conv3x3(x, weight) if how == "gemm" else conv(x, weight, padding=1)
+        ctx.save_for_backward(x, weight)
+        ctx.mode = mode
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from ..ops import conv as bhconv
+
+        x, weight = ctx.saved_tensors
+        n, c, h, w = x.shape
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        conv_bwd = torch.ops.aten.convolution_backward
+        args = ([1, 1], [1, 1], [1, 1], False, [0, 0], 1)
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            how = _pick((n, c, h, w, weight.size(0), x.dtype, "dgrad3"), lambda: bhconv.conv3x3_dgrad(gy, weight),
+                        lambda: conv_bwd(gy, x, weight, None, *args, [True, False, False]),
+                        "gemm" if ctx.mode == "direct" else ctx.mode)
+            if how == "gemm":
+                gx = bhconv.conv3x3_dgrad(gy, weight)
+            else:
+                gx = conv_bwd(gy, x, weight, None, *args, [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            gw = conv_bwd(gy, x, weight, None, *args, [False, True, False])[1]
+        return gx, gw, None
+
+
+class Conv3x3(nn.Conv2d):
+    """nn.Conv2d(k=3, stride=1, padding=1, bias=False) whose channels_last fp16 / bf16 GPU path picks
+    the direct MFMA kernel or MIOpen per shape (``mode`` "auto" / "direct" / "miopen")."""
+
+    def __init__(self, *args, mode="auto", **kw):
+        super().__init__(*args, **kw)
+        self.mode = mode
+
+    def fast_path(self, x):
+        if not (self.mode != "miopen" and x.is_cuda and x.dim() == 4 and x.dtype == self.weight.dtype
+                and self.stride == (1, 1) and self.padding == (1, 1) and self.dilation == (1, 1) and self.groups == 1):
+            return False
+        from ..ops import conv as bhconv
+
+        return bhconv.supported(x, self.weight)
+
+    def forward(self, x):
+        if self.fast_path(x):
+            return _Conv3x3Fn.apply(x, self.weight, self.mode)
+        return super().forward(x)
 
 
 def conv1x1(cin, cout, stride=1):
@@ -259,12 +327,13 @@ def resnet50(**kw) -> ResNet:
 
 
 def resnet50_fused(process_group=None, channel_last=True, conv1x1_mode="auto", stem_pool_fused=True,
-                   gemm_1x1=None, **kw) -> ResNet:
+                   gemm_1x1=None, conv3x3_mode="auto", **kw) -> ResNet:
     """ResNet-50 whose BatchNorms are fused SyncBatchNorms (BN+ReLU and BN+add+ReLU in one pass),
     synchronised over ``process_group`` -- the 'amp O2 + SyncBatchNorm' benchmark model.
     ``conv1x1_mode``: stride-1 1x1 convolutions as hipBLASLt GEMMs on the channels_last view
-    ("gemm"), MIOpen ("miopen"), or the faster of the two per shape and direction ("auto")."""
-    global _CONV1X1_MODE
+    ("gemm"), MIOpen ("miopen"), or the faster of the two per shape and direction ("auto").
+    ``conv3x3_mode``: stride-1 3x3 convolutions on the direct MFMA kernel ("direct"), MIOpen, or "auto"."""
+    global _CONV1X1_MODE, _CONV3X3_MODE
     if gemm_1x1 is not None:  # older keyword
         conv1x1_mode = "gemm" if gemm_1x1 else "miopen"
     from ..parallel import SyncBatchNorm
@@ -274,10 +343,12 @@ def resnet50_fused(process_group=None, channel_last=True, conv1x1_mode="auto", s
                              fuse_maxpool=fuse_maxpool)
 
     old, _CONV1X1_MODE = _CONV1X1_MODE, conv1x1_mode
+    old3, _CONV3X3_MODE = _CONV3X3_MODE, conv3x3_mode
     try:
         return ResNet(Bottleneck, [3, 4, 6, 3], norm_layer=norm, fused=True, stem_pool_fused=stem_pool_fused, **kw)
     finally:
         _CONV1X1_MODE = old
+        _CONV3X3_MODE = old3
 
 
 def resnet18_like(**kw) -> ResNet:

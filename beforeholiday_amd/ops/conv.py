@@ -1,0 +1,32 @@
+"""Direct 3x3 / stride 1 / pad 1 NHWC convolution on MFMA (kernels/conv.hip, ``_C.conv_cuda``).
+
+``conv3x3(x, w)`` runs the HIP kernel for channels_last fp16 / bf16 CUDA tensors with C and K
+multiples of 64 and falls back to ``F.conv2d`` otherwise. ``conv3x3_dgrad(dy, w)`` is the data
+gradient of that conv: the same kernel applied to dy with the spatially flipped, in/out-swapped
+weights (``dgrad_weight``), since for stride 1 / pad 1 dX = conv(dY, flip(W)^T).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .._native import available, submodule
+
+
+def supported(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return x.is_cuda and available() and submodule("conv_cuda").supported(x, w)
+
+
+def conv3x3(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    if supported(x, w):
+        return submodule("conv_cuda").conv3x3_forward(x, w)
+    return F.conv2d(x, w, stride=1, padding=1)
+
+
+def dgrad_weight(w: torch.Tensor) -> torch.Tensor:
+    """[K, C, 3, 3] -> [C, K, 3, 3] with W'[c, k, r, s] = W[k, c, 2-r, 2-s], channels_last."""
+    return w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+
+
+def conv3x3_dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    return conv3x3(dy, dgrad_weight(w))

@@ -81,6 +81,9 @@ def parse():
     ap.add_argument("--conv1x1", default="auto", choices=["auto", "miopen", "gemm"],
                     help="stride-1 1x1 convolution forward / data gradient: hipBLASLt GEMMs on the channels_last "
                          "view, MIOpen, or the faster per shape (auto, timed in the first warmup step)")
+    ap.add_argument("--conv3x3", default="auto", choices=["auto", "miopen", "direct"],
+                    help="stride-1 3x3 convolution forward / data gradient: the direct MFMA kernel "
+                         "(kernels/conv.hip), MIOpen, or the faster per shape (auto)")
     return ap.parse_args()
 
 
@@ -122,7 +125,7 @@ def main():
     torch.manual_seed(1234 + rank)
     bn_group = dist.new_group(list(range(world))) if (world > 1 and args.bn_group == "separate") else None
     model = (resnet50() if args.no_syncbn else resnet50_fused(process_group=bn_group, channel_last=True,
-                                                                   conv1x1_mode=args.conv1x1,
+                                                                   conv1x1_mode=args.conv1x1, conv3x3_mode=args.conv3x3,
                                                                    stem_pool_fused=args.stem == "fused")).cuda()
     model = model.to(memory_format=torch.channels_last)
     global_batch = args.batch * world

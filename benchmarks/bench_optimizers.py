@@ -12,6 +12,7 @@ Prints one JSON line per (model, optimizer, implementation) and writes them to -
 """
 import argparse
 import json
+import time
 import os
 import sys
 
@@ -88,11 +89,13 @@ def time_opt(opt, iters, warmup):
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
+    t0 = time.perf_counter()
     for _ in range(iters):
         opt.step()
+    host = (time.perf_counter() - t0) / iters * 1e3  # issue time: ~= ms_per_step when host-bound
     e.record()
     e.synchronize()
-    return s.elapsed_time(e) / iters
+    return s.elapsed_time(e) / iters, host
 
 
 def main():
@@ -126,14 +129,14 @@ def main():
             for impl, ctor in impls:
                 ps = make(sh, dev)
                 try:
-                    ms = time_opt(ctor(ps), args.iters, args.warmup)
+                    ms, host_ms = time_opt(ctor(ps), args.iters, args.warmup)
                 except Exception as e:  # noqa: BLE001 - report unsupported baselines, keep going
                     print(json.dumps({"model": model, "optimizer": opt_name, "impl": impl, "error": str(e)[:200]}))
                     continue
                 # bytes touched per step by an ideal fused kernel: read p,g,m,v + write p,m,v (fp32)
                 ideal_gb = nparam * 4 * (7 if opt_name != "sgd" else 5) / 1e9
                 row = {"model": model, "params_M": round(nparam / 1e6, 2), "tensors": len(sh), "optimizer": opt_name,
-                       "impl": impl, "ms_per_step": round(ms, 4), "effective_GBps": round(ideal_gb / ms * 1e3, 1)}
+                       "impl": impl, "ms_per_step": round(ms, 4), "host_issue_ms": round(host_ms, 4), "effective_GBps": round(ideal_gb / ms * 1e3, 1)}
                 if base is None:
                     base = ms
                 else:
