@@ -41,12 +41,38 @@ at::Tensor conv3x3_forward(const at::Tensor& x, const at::Tensor& w) {
   return y;
 }
 
+// dX of y = conv2d(x, w, stride 1, padding 1) from dY (channels_last) and the forward's w
+at::Tensor conv3x3_dgrad(const at::Tensor& dy, const at::Tensor& w) {
+  TORCH_CHECK(dy.is_cuda() && w.is_cuda() && dy.dim() == 4 && w.dim() == 4 && w.size(0) == dy.size(1) &&
+                  w.size(2) == 3 && w.size(3) == 3 && dy.scalar_type() == w.scalar_type() &&
+                  (dy.scalar_type() == at::kHalf || dy.scalar_type() == at::kBFloat16) &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast) && w.size(0) % 64 == 0 && w.size(1) % 64 == 0,
+              "conv3x3_dgrad: needs channels_last fp16/bf16 dy, w [K, C, 3, 3], C and K % 64 == 0");
+  const at::Tensor wc = w.contiguous(at::MemoryFormat::ChannelsLast);
+  auto dx = at::empty({dy.size(0), w.size(1), dy.size(2), dy.size(3)},
+                      dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  bh::Conv3x3Args a;
+  a.x = dy.data_ptr();
+  a.w = wc.data_ptr();
+  a.y = dx.data_ptr();
+  a.N = (int)dy.size(0);
+  a.C = (int)dy.size(1);
+  a.H = (int)dy.size(2);
+  a.W = (int)dy.size(3);
+  a.K = (int)w.size(1);
+  TORCH_CHECK(bh::conv3x3_supported(a), "conv3x3_dgrad: unaligned tensors");
+  bh::conv3x3_dgrad(dtype_code(dy.scalar_type()), a, stream_for(dy));
+  return dx;
+}
+
 }  // namespace
 
 void register_conv(pybind11::module_& root) {
   auto m = root.def_submodule("conv_cuda", "direct 3x3 stride-1 NHWC convolution (MFMA implicit GEMM)");
   m.def("conv3x3_forward", &conv3x3_forward, py::arg("x"), py::arg("weight"),
         "conv2d(x, weight, stride=1, padding=1) for channels_last fp16 / bf16, C and K multiples of 64");
+  m.def("conv3x3_dgrad", &conv3x3_dgrad, py::arg("grad_out"), py::arg("weight"),
+        "grad of conv2d(x, weight, stride=1, padding=1) w.r.t. x, straight from the forward weight");
   m.def("supported", &supported, py::arg("x"), py::arg("weight"));
 }
 

@@ -17,6 +17,7 @@
 #include "bh/conv_api.h"
 #include "bh/device.h"
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -28,6 +29,8 @@ typedef __bf16 b8v __attribute__((ext_vector_type(8)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 typedef int i4v __attribute__((ext_vector_type(4)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4v* lds_s4_ptr;
 
 template <typename T> struct Mfma32;
 template <> struct Mfma32<f16> {
@@ -53,35 +56,61 @@ constexpr int kWBytes = kBN * 128;
 constexpr int kHaloPer = ((kTH + 2) * kMaxHC * 8 + kThreads - 1) / kThreads;  // 16-byte pieces per thread
 
 struct Geo {
-  int G, gw, HC, XT, YT;
+  int G, gw, HC, XT, YT, tiles, tpw;  // tpw: consecutive windows per workgroup
 };
 
-// 64 x 128-byte weight image, swizzled for the 32-row fragment reads
+// 64 x 128-byte weight image, swizzled for the 32-row fragment reads (ds_read_b128) and for the
+// 4-row column reads (ds_read_b64_tr_b16) alike
 BH_DEVICE int wsw(int row, int ch) { return row * 128 + ((ch ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3))) << 4); }
 
-template <typename T>
+// A operand from a [k rows][m columns] image: lane (m = m0 + (lane & 31), half h) gets image rows
+// r0 .. r0 + 7 of its column (r0 already includes 8h), two transposed 4-row reads
+BH_DEVICE i4v frag_tr(const char* img, int r0, int m0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int col = m0 + 16 * (g & 1) + 4 * p;
+  const int cb = (col & 7) << 1;
+  const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(img + wsw(r0 + q, col >> 3) + cb));
+  const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(img + wsw(r0 + 4 + q, col >> 3) + cb));
+  typedef int i2v __attribute__((ext_vector_type(2)));
+  const i2v l = __builtin_bit_cast(i2v, lo), hh = __builtin_bit_cast(i2v, hi);
+  return i4v{l[0], l[1], hh[0], hh[1]};
+}
+
+// FLIP: the data gradient of conv(x, w): input dY [N, H, W, K_w], weights given as the forward's
+// w [K_w][3][3][C_w], computing conv with W'[c][r][s][k] = w[k][2-r][2-s][c]. The slice of each
+// step is then a [k_w rows][c_w contiguous] block of w, staged as it lies and read as the MFMA A
+// operand through ds_read_b64_tr_b16 -- no transposed weight copy is ever materialised.
+template <typename T, bool FLIP>
 __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
   __shared__ __attribute__((aligned(16))) char smem[kHaloBytes + 2 * kWBytes];
   char* halo = smem;
   char* wb = smem + kHaloBytes;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r32 = lane & 31, h = lane >> 5;
-  int tt = blockIdx.x;
-  const int xt = tt % g.XT;
-  tt /= g.XT;
-  const int yt = tt % g.YT;
-  const int n0 = (tt / g.YT) * g.G, y0 = yt * kTH, x0 = xt * 32;
+  const int tile0 = blockIdx.x * g.tpw;
+  const int ntile = min(g.tpw, g.tiles - tile0);
   const int k0 = blockIdx.y * kBN;
   const T* X = reinterpret_cast<const T*>(a.x);
   const T* Wt = reinterpret_cast<const T*>(a.w);
   const int C = a.C, H = a.H, W = a.W, N = a.N;
-  const int nch = C / kCK, steps = nch * 9;
+  const int nch = C / kCK, per_tile = nch * 9, steps = ntile * per_tile;
   const int npieces = (kTH + 2) * g.HC * 8;
+  // window origin of tile id t: x-tile fastest, then row window, then image group
+  auto origin = [&](int t, int& n0, int& y0, int& x0) {
+    const int xt = t % g.XT;
+    t /= g.XT;
+    const int yt = t % g.YT;
+    n0 = (t / g.YT) * g.G;
+    y0 = yt * kTH;
+    x0 = xt * 32;
+  };
 
   // ---- halo staging: registers (prefetch) -> LDS ----
   i4v hreg[kHaloPer];
   uint32_t hmask = 0;
-  auto halo_load = [&](int c0) {
+  auto halo_load = [&](int t, int c0) {
+    int n0, y0, x0;
+    origin(t, n0, y0, x0);
     hmask = 0;
 #pragma unroll
     for (int i = 0; i < kHaloPer; ++i) {
@@ -104,14 +133,17 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
             ((hmask >> i) & 1u) ? hreg[i] : i4v{0, 0, 0, 0};
     }
   };
-  // ---- weight slice of step t = chunk * 9 + (r * 3 + s): W[k0 .. k0+63][r][s][c0 .. c0+63] ----
+  // ---- weight slice of step (chunk, r * 3 + s): W[k0 .. k0+63][r][s][c0 .. c0+63] ----
   i4v wreg[2];
   auto w_load = [&](int step) {
-    const int chunk = step / 9, rs = step - chunk * 9;
+    const int within = step % per_tile, chunk = within / 9, rs = within - chunk * 9;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int p = tid + i * kThreads, row = p >> 3, ch = p & 7;
-      wreg[i] = *reinterpret_cast<const i4v*>(Wt + ((int64_t)(k0 + row) * 9 + rs) * C + chunk * kCK + ch * 8);
+      if (FLIP)  // image row = input channel c (= w's output channel), 64 contiguous k
+        wreg[i] = *reinterpret_cast<const i4v*>(Wt + ((int64_t)(chunk * kCK + row) * 9 + (8 - rs)) * a.K + k0 + ch * 8);
+      else
+        wreg[i] = *reinterpret_cast<const i4v*>(Wt + ((int64_t)(k0 + row) * 9 + rs) * C + chunk * kCK + ch * 8);
     }
   };
   auto w_store = [&](char* buf) {
@@ -123,24 +155,57 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
   };
 
   f16v acc[2][2];
+  auto zero_acc = [&]() {
 #pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
+    for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-    for (int pb = 0; pb < 2; ++pb)
+      for (int pb = 0; pb < 2; ++pb)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[kb][pb][i] = 0.f;
+        for (int i = 0; i < 16; ++i) acc[kb][pb][i] = 0.f;
+  };
   const int gi = r32 / g.gw, jl = r32 - gi * g.gw;
   const int hcol = gi * (g.gw + 2) + jl;  // this lane's halo column at s = 0
+  T* Y = reinterpret_cast<T*>(a.y);
+  // lane = pixel, registers = 4 consecutive output channels per group
+  auto epilogue = [&](int t) {
+    int n0, y0, x0;
+    origin(t, n0, y0, x0);
+    const int n = n0 + gi, x = x0 + jl;
+    if (n >= N || x >= W) return;
+#pragma unroll
+    for (int pb = 0; pb < 2; ++pb) {
+      const int y = y0 + 2 * wave + pb;
+      if (y >= H) continue;
+      T* out = Y + (((int64_t)n * H + y) * W + x) * a.K + k0;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          T o[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = from_f<T>(acc[kb][pb][4 * gq + j]);
+          *reinterpret_cast<uint2*>(out + 32 * kb + 8 * gq + 4 * h) = *reinterpret_cast<const uint2*>(o);
+        }
+    }
+  };
 
-  halo_load(0);
+  zero_acc();
+  halo_load(tile0, 0);
   w_load(0);
   halo_store();
   w_store(wb);
   __syncthreads();
   for (int t = 0; t < steps; ++t) {
-    const int chunk = t / 9, rs = t - chunk * 9;
+    const int it = t / per_tile, within = t - it * per_tile;
+    const int chunk = within / 9, rs = within - chunk * 9;
+    const bool last_rs = rs == 8;
+    // the next (window, chunk) whose halo is prefetched during this chunk
+    const bool more = chunk + 1 < nch || it + 1 < ntile;
     if (t + 1 < steps) w_load(t + 1);
-    if (rs == 0 && chunk + 1 < nch) halo_load((chunk + 1) * kCK);
+    if (rs == 0 && more) {
+      if (chunk + 1 < nch) halo_load(tile0 + it, (chunk + 1) * kCK);
+      else halo_load(tile0 + it + 1, 0);
+    }
     const char* wcur = wb + (t & 1) * kWBytes;
     const int r = rs / 3, s = rs - r * 3;
     const char* hb0 = halo + ((2 * wave + r) * g.HC + hcol + s) * kPix;  // window row 2w, offset (r, s)
@@ -148,8 +213,14 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int ch = 2 * kk + h;
-      const i4v a0 = *reinterpret_cast<const i4v*>(wcur + wsw(r32, ch));
-      const i4v a1 = *reinterpret_cast<const i4v*>(wcur + wsw(32 + r32, ch));
+      i4v a0, a1;
+      if (FLIP) {
+        a0 = frag_tr(wcur, 16 * kk + 8 * h, 0, lane);
+        a1 = frag_tr(wcur, 16 * kk + 8 * h, 32, lane);
+      } else {
+        a0 = *reinterpret_cast<const i4v*>(wcur + wsw(r32, ch));
+        a1 = *reinterpret_cast<const i4v*>(wcur + wsw(32 + r32, ch));
+      }
       const i4v b0 = *reinterpret_cast<const i4v*>(hb0 + ch * 16);
       const i4v b1 = *reinterpret_cast<const i4v*>(hb1 + ch * 16);
       acc[0][0] = Mfma32<T>::run(a0, b0, acc[0][0]);
@@ -158,31 +229,15 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
       acc[1][1] = Mfma32<T>::run(a1, b1, acc[1][1]);
     }
     if (t + 1 < steps) w_store(wb + ((t + 1) & 1) * kWBytes);
-    if (rs == 8 && chunk + 1 < nch) {
+    if (last_rs && chunk + 1 == nch) {  // window done: results out, accumulators reset
+      epilogue(tile0 + it);
+      zero_acc();
+    }
+    if (last_rs && more) {
       __syncthreads();  // every wave is done with this chunk's halo
       halo_store();
     }
     __syncthreads();
-  }
-
-  // ---- epilogue: lane = pixel, registers = 4 consecutive output channels per group ----
-  const int n = n0 + gi, x = x0 + jl;
-  if (n >= N || x >= W || jl >= g.gw) return;
-  T* Y = reinterpret_cast<T*>(a.y);
-#pragma unroll
-  for (int pb = 0; pb < 2; ++pb) {
-    const int y = y0 + 2 * wave + pb;
-    if (y >= H) continue;
-    T* out = Y + (((int64_t)n * H + y) * W + x) * a.K + k0;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        T o[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = from_f<T>(acc[kb][pb][4 * gq + j]);
-        *reinterpret_cast<uint2*>(out + 32 * kb + 8 * gq + 4 * h) = *reinterpret_cast<const uint2*>(o);
-      }
   }
 }
 
@@ -194,6 +249,8 @@ Geo make_geo(int H, int W) {
   g.HC = g.G * (g.gw + 2);
   g.XT = g.G == 1 ? (W + 31) / 32 : 1;
   g.YT = (H + kTH - 1) / kTH;
+  g.tiles = 0;
+  g.tpw = 1;
   return g;
 }
 
@@ -205,19 +262,34 @@ bool conv3x3_supported(const Conv3x3Args& a) {
          al(a.w) && al(a.y);
 }
 
-void conv3x3_forward(int dt, const Conv3x3Args& a, hipStream_t st) {
+void conv3x3_run(int dt, const Conv3x3Args& a, bool flip, hipStream_t st) {
   if (!conv3x3_supported(a)) throw std::runtime_error("conv3x3_forward: needs C % 64 == 0, K % 64 == 0, aligned tensors");
   const Geo g = make_geo(a.H, a.W);
   if (g.HC > kMaxHC) throw std::runtime_error("conv3x3_forward: halo geometry out of range");
+  Geo g2 = g;
   const int64_t tiles = (int64_t)g.XT * g.YT * ((a.N + g.G - 1) / g.G);
-  const dim3 grid((unsigned)tiles, (unsigned)(a.K / kBN));
+  g2.tiles = (int)tiles;
+  // about two resident workgroups per CU over the whole grid: each walks tpw consecutive windows and
+  // prefetches the next window's halo while computing the current one
+  const int64_t ktiles = a.K / kBN;
+  g2.tpw = (int)std::max<int64_t>(1, (tiles * ktiles + 511) / 512);
+  const dim3 grid((unsigned)((tiles + g2.tpw - 1) / g2.tpw), (unsigned)ktiles);
   switch (dt) {
-    case kF16: hipLaunchKernelGGL((k_conv3x3<f16>), grid, dim3(kThreads), 0, st, a, g); break;
-    case kBF16: hipLaunchKernelGGL((k_conv3x3<bf16>), grid, dim3(kThreads), 0, st, a, g); break;
+    case kF16:
+      if (flip) hipLaunchKernelGGL((k_conv3x3<f16, true>), grid, dim3(kThreads), 0, st, a, g2);
+      else hipLaunchKernelGGL((k_conv3x3<f16, false>), grid, dim3(kThreads), 0, st, a, g2);
+      break;
+    case kBF16:
+      if (flip) hipLaunchKernelGGL((k_conv3x3<bf16, true>), grid, dim3(kThreads), 0, st, a, g2);
+      else hipLaunchKernelGGL((k_conv3x3<bf16, false>), grid, dim3(kThreads), 0, st, a, g2);
+      break;
     default: throw std::runtime_error("conv3x3_forward: fp16 / bf16 only");
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("conv3x3_forward: ") + hipGetErrorString(e));
 }
+
+void conv3x3_forward(int dt, const Conv3x3Args& a, hipStream_t st) { conv3x3_run(dt, a, false, st); }
+void conv3x3_dgrad(int dt, const Conv3x3Args& a, hipStream_t st) { conv3x3_run(dt, a, true, st); }
 
 }  // namespace bh

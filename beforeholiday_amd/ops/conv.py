@@ -3,7 +3,7 @@
 ``conv3x3(x, w)`` runs the HIP kernel for channels_last fp16 / bf16 CUDA tensors with C and K
 multiples of 64 and falls back to ``F.conv2d`` otherwise. ``conv3x3_dgrad(dy, w)`` is the data
 gradient of that conv: the same kernel applied to dy with the spatially flipped, in/out-swapped
-weights (``dgrad_weight``), since for stride 1 / pad 1 dX = conv(dY, flip(W)^T).
+weights (for stride 1 / pad 1 dX = conv(dY, flip(W)^T)), read in place from ``w``.
 """
 from __future__ import annotations
 
@@ -29,4 +29,8 @@ def dgrad_weight(w: torch.Tensor) -> torch.Tensor:
 
 
 def conv3x3_dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    return conv3x3(dy, dgrad_weight(w))
+    """dX of conv3x3(x, w) from dY: the kernel reads w in place (transposed LDS reads of the
+    flipped slices); reference path conv(dY, dgrad_weight(w))."""
+    if dy.is_cuda and available() and supported(dy, w.transpose(0, 1)):
+        return submodule("conv_cuda").conv3x3_dgrad(dy, w)
+    return F.conv2d(dy, dgrad_weight(w), stride=1, padding=1)
