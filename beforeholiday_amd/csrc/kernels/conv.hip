@@ -18,6 +18,7 @@
 #include "bh/device.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <stdexcept>
 #include <string>
 
@@ -80,8 +81,10 @@ BH_DEVICE i4v frag_tr(const char* img, int r0, int m0, int lane) {
 // w [K_w][3][3][C_w], computing conv with W'[c][r][s][k] = w[k][2-r][2-s][c]. The slice of each
 // step is then a [k_w rows][c_w contiguous] block of w, staged as it lies and read as the MFMA A
 // operand through ds_read_b64_tr_b16 -- no transposed weight copy is ever materialised.
-template <typename T, bool FLIP>
+template <typename T, bool FLIP, int G>
 __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
+  // window geometry as compile-time constants (the halo address math divides by them)
+  constexpr int GW = 32 / G, HC = G * (GW + 2);
   __shared__ __attribute__((aligned(16))) char smem[kHaloBytes + 2 * kWBytes];
   char* halo = smem;
   char* wb = smem + kHaloBytes;
@@ -94,13 +97,13 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
   const T* Wt = reinterpret_cast<const T*>(a.w);
   const int C = a.C, H = a.H, W = a.W, N = a.N;
   const int nch = C / kCK, per_tile = nch * 9, steps = ntile * per_tile;
-  const int npieces = (kTH + 2) * g.HC * 8;
+  constexpr int npieces = (kTH + 2) * HC * 8;
   // window origin of tile id t: x-tile fastest, then row window, then image group
   auto origin = [&](int t, int& n0, int& y0, int& x0) {
     const int xt = t % g.XT;
     t /= g.XT;
     const int yt = t % g.YT;
-    n0 = (t / g.YT) * g.G;
+    n0 = (t / g.YT) * G;
     y0 = yt * kTH;
     x0 = xt * 32;
   };
@@ -115,11 +118,11 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
 #pragma unroll
     for (int i = 0; i < kHaloPer; ++i) {
       const int q = tid + i * kThreads, pix = q >> 3, ch = q & 7;
-      const int hr = pix / g.HC, hc = pix - hr * g.HC;
-      const int gi = hc / (g.gw + 2), jj = hc - gi * (g.gw + 2);
+      const int hr = pix / HC, hc = pix - hr * HC;
+      const int gi = hc / (GW + 2), jj = hc - gi * (GW + 2);
       const int n = n0 + gi, y = y0 - 1 + hr, x = x0 - 1 + jj;
       const bool ok = q < npieces && n < N && y >= 0 && y < H && x >= 0 && x < W;
-      const int64_t off = ok ? (((int64_t)n * H + y) * W + x) * C + c0 + ch * 8 : 0;
+      const int off = ok ? ((n * H + y) * W + x) * C + c0 + ch * 8 : 0;  // < 2^31 (host check)
       hreg[i] = *reinterpret_cast<const i4v*>(X + off);
       hmask |= (ok ? 1u : 0u) << i;
     }
@@ -141,9 +144,9 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
     for (int i = 0; i < 2; ++i) {
       const int p = tid + i * kThreads, row = p >> 3, ch = p & 7;
       if (FLIP)  // image row = input channel c (= w's output channel), 64 contiguous k
-        wreg[i] = *reinterpret_cast<const i4v*>(Wt + ((int64_t)(chunk * kCK + row) * 9 + (8 - rs)) * a.K + k0 + ch * 8);
+        wreg[i] = *reinterpret_cast<const i4v*>(Wt + ((chunk * kCK + row) * 9 + (8 - rs)) * a.K + k0 + ch * 8);
       else
-        wreg[i] = *reinterpret_cast<const i4v*>(Wt + ((int64_t)(k0 + row) * 9 + rs) * C + chunk * kCK + ch * 8);
+        wreg[i] = *reinterpret_cast<const i4v*>(Wt + ((k0 + row) * 9 + rs) * C + chunk * kCK + ch * 8);
     }
   };
   auto w_store = [&](char* buf) {
@@ -163,8 +166,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[kb][pb][i] = 0.f;
   };
-  const int gi = r32 / g.gw, jl = r32 - gi * g.gw;
-  const int hcol = gi * (g.gw + 2) + jl;  // this lane's halo column at s = 0
+  const int gi = r32 / GW, jl = r32 - gi * GW;
+  const int hcol = gi * (GW + 2) + jl;  // this lane's halo column at s = 0
   T* Y = reinterpret_cast<T*>(a.y);
   // lane = pixel, registers = 4 consecutive output channels per group
   auto epilogue = [&](int t) {
@@ -176,7 +179,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
     for (int pb = 0; pb < 2; ++pb) {
       const int y = y0 + 2 * wave + pb;
       if (y >= H) continue;
-      T* out = Y + (((int64_t)n * H + y) * W + x) * a.K + k0;
+      T* out = Y + ((n * H + y) * W + x) * a.K + k0;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -208,25 +211,35 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
     }
     const char* wcur = wb + (t & 1) * kWBytes;
     const int r = rs / 3, s = rs - r * 3;
-    const char* hb0 = halo + ((2 * wave + r) * g.HC + hcol + s) * kPix;  // window row 2w, offset (r, s)
-    const char* hb1 = hb0 + g.HC * kPix;                                  // window row 2w + 1
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
+    const char* hb0 = halo + ((2 * wave + r) * HC + hcol + s) * kPix;  // window row 2w, offset (r, s)
+    const char* hb1 = hb0 + HC * kPix;                                    // window row 2w + 1
+    // fragments of k-step kk + 1 are read while the MFMAs of kk run (two register sets)
+    auto frags = [&](int kk, i4v (&f)[4]) {
       const int ch = 2 * kk + h;
-      i4v a0, a1;
       if (FLIP) {
-        a0 = frag_tr(wcur, 16 * kk + 8 * h, 0, lane);
-        a1 = frag_tr(wcur, 16 * kk + 8 * h, 32, lane);
+        f[0] = frag_tr(wcur, 16 * kk + 8 * h, 0, lane);
+        f[1] = frag_tr(wcur, 16 * kk + 8 * h, 32, lane);
       } else {
-        a0 = *reinterpret_cast<const i4v*>(wcur + wsw(r32, ch));
-        a1 = *reinterpret_cast<const i4v*>(wcur + wsw(32 + r32, ch));
+        f[0] = *reinterpret_cast<const i4v*>(wcur + wsw(r32, ch));
+        f[1] = *reinterpret_cast<const i4v*>(wcur + wsw(32 + r32, ch));
       }
-      const i4v b0 = *reinterpret_cast<const i4v*>(hb0 + ch * 16);
-      const i4v b1 = *reinterpret_cast<const i4v*>(hb1 + ch * 16);
-      acc[0][0] = Mfma32<T>::run(a0, b0, acc[0][0]);
-      acc[0][1] = Mfma32<T>::run(a0, b1, acc[0][1]);
-      acc[1][0] = Mfma32<T>::run(a1, b0, acc[1][0]);
-      acc[1][1] = Mfma32<T>::run(a1, b1, acc[1][1]);
+      f[2] = *reinterpret_cast<const i4v*>(hb0 + ch * 16);
+      f[3] = *reinterpret_cast<const i4v*>(hb1 + ch * 16);
+    };
+    i4v fa[4], fb[4];
+    frags(0, fa);
+#pragma unroll
+    for (int kk = 0; kk < 4; kk += 2) {
+      frags(kk + 1, fb);
+      acc[0][0] = Mfma32<T>::run(fa[0], fa[2], acc[0][0]);
+      acc[0][1] = Mfma32<T>::run(fa[0], fa[3], acc[0][1]);
+      acc[1][0] = Mfma32<T>::run(fa[1], fa[2], acc[1][0]);
+      acc[1][1] = Mfma32<T>::run(fa[1], fa[3], acc[1][1]);
+      if (kk + 2 < 4) frags(kk + 2, fa);
+      acc[0][0] = Mfma32<T>::run(fb[0], fb[2], acc[0][0]);
+      acc[0][1] = Mfma32<T>::run(fb[0], fb[3], acc[0][1]);
+      acc[1][0] = Mfma32<T>::run(fb[1], fb[2], acc[1][0]);
+      acc[1][1] = Mfma32<T>::run(fb[1], fb[3], acc[1][1]);
     }
     if (t + 1 < steps) w_store(wb + ((t + 1) & 1) * kWBytes);
     if (last_rs && chunk + 1 == nch) {  // window done: results out, accumulators reset
@@ -240,6 +253,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
     __syncthreads();
   }
 }
+
+template <typename T> struct Tag { using type = T; };
 
 Geo make_geo(int H, int W) {
   Geo g;
@@ -258,8 +273,9 @@ Geo make_geo(int H, int W) {
 
 bool conv3x3_supported(const Conv3x3Args& a) {
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const int64_t pix = (int64_t)a.N * a.H * a.W;
   return a.N > 0 && a.H > 0 && a.W > 0 && a.C > 0 && a.K > 0 && a.C % kCK == 0 && a.K % kBN == 0 && al(a.x) &&
-         al(a.w) && al(a.y);
+         al(a.w) && al(a.y) && pix * a.C < (1ll << 31) && pix * a.K < (1ll << 31);  // 32-bit offsets
 }
 
 void conv3x3_run(int dt, const Conv3x3Args& a, bool flip, hipStream_t st) {
@@ -274,15 +290,22 @@ void conv3x3_run(int dt, const Conv3x3Args& a, bool flip, hipStream_t st) {
   const int64_t ktiles = a.K / kBN;
   g2.tpw = (int)std::max<int64_t>(1, (tiles * ktiles + 511) / 512);
   const dim3 grid((unsigned)((tiles + g2.tpw - 1) / g2.tpw), (unsigned)ktiles);
+  auto launch = [&](auto tt, auto gg) {
+    using T = typename decltype(tt)::type;
+    constexpr int GG = decltype(gg)::value;
+    if (flip) hipLaunchKernelGGL((k_conv3x3<T, true, GG>), grid, dim3(kThreads), 0, st, a, g2);
+    else hipLaunchKernelGGL((k_conv3x3<T, false, GG>), grid, dim3(kThreads), 0, st, a, g2);
+  };
+  auto by_g = [&](auto tt) {
+    switch (g.G) {
+      case 1: launch(tt, std::integral_constant<int, 1>{}); break;
+      case 2: launch(tt, std::integral_constant<int, 2>{}); break;
+      default: launch(tt, std::integral_constant<int, 4>{}); break;
+    }
+  };
   switch (dt) {
-    case kF16:
-      if (flip) hipLaunchKernelGGL((k_conv3x3<f16, true>), grid, dim3(kThreads), 0, st, a, g2);
-      else hipLaunchKernelGGL((k_conv3x3<f16, false>), grid, dim3(kThreads), 0, st, a, g2);
-      break;
-    case kBF16:
-      if (flip) hipLaunchKernelGGL((k_conv3x3<bf16, true>), grid, dim3(kThreads), 0, st, a, g2);
-      else hipLaunchKernelGGL((k_conv3x3<bf16, false>), grid, dim3(kThreads), 0, st, a, g2);
-      break;
+    case kF16: by_g(Tag<f16>{}); break;
+    case kBF16: by_g(Tag<bf16>{}); break;
     default: throw std::runtime_error("conv3x3_forward: fp16 / bf16 only");
   }
   hipError_t e = hipGetLastError();
