@@ -18,6 +18,7 @@
 #include "bh/device.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 #include <stdexcept>
 #include <string>
@@ -285,9 +286,11 @@ void conv3x3_run(int dt, const Conv3x3Args& a, bool flip, hipStream_t st) {
   Geo g2 = g;
   const int64_t tiles = (int64_t)g.XT * g.YT * ((a.N + g.G - 1) / g.G);
   g2.tiles = (int)tiles;
-  // about two resident workgroups per CU over the whole grid: each walks tpw consecutive windows and
-  // prefetches the next window's halo while computing the current one
   const int64_t ktiles = a.K / kBN;
+  // about two resident workgroups per CU over the whole grid: each walks tpw consecutive windows and
+  // prefetches the next window's halo while computing the current one. (A one-workgroup-per-CU
+  // variant holding all nine weight slices of a chunk in LDS measured 1.2x slower: profiles/
+  // conv3x3_direct_vs_miopen.jsonl.)
   g2.tpw = (int)std::max<int64_t>(1, (tiles * ktiles + 511) / 512);
   const dim3 grid((unsigned)((tiles + g2.tpw - 1) / g2.tpw), (unsigned)ktiles);
   auto launch = [&](auto tt, auto gg) {
