@@ -147,11 +147,15 @@ float time_ms(hipStream_t st, F&& fn) {
   return ms;
 }
 
+// tests / benchmarks pin the MFMA kernel so the measured dispatch cannot route around it
+bool g_force_mfma = false;
+
 template <typename FA, typename FB>
 bool prefer_mfma(const char* op, const at::Tensor& a, int64_t M, int64_t N, int64_t K, int variant, FA&& mfma,
                  FB&& lib) {
   static std::mutex mu;
   static auto& cache = *new std::map<std::tuple<std::string, int, int64_t, int64_t, int64_t, int>, bool>();
+  if (g_force_mfma) return true;
   const auto key = std::make_tuple(std::string(op), (int)a.scalar_type(), M, N, K, variant);
   {
     std::lock_guard<std::mutex> lock(mu);
@@ -415,6 +419,10 @@ void register_dense(pybind11::module_& root) {
     return linear_dact(dy, wt, aux.has_value() ? *aux : at::Tensor(), act, want_bgrad);
   }, py::arg("dy"), py::arg("wt"), py::arg("aux"), py::arg("act"), py::arg("want_bgrad"));
   gm.def("mfma_enabled", &mfma_enabled);
+  gm.def("set_tile_mode", &bh::gemm_set_tile_mode, "0 auto, 1 128x128, 2 256x256, 3 256x128, 4 ping-pong 256x256");
+  gm.def("tile_mode", &bh::gemm_tile_mode);
+  gm.def("set_force_mfma", [](bool on) { g_force_mfma = on; },
+         "route every supported linear_act / linear_dact call to the MFMA kernel (no measured dispatch)");
   auto wg = root.def_submodule("fused_weight_gradient_mlp_cuda", "weight-gradient GEMM accumulated into main_grad");
   wg.def("wgrad_gemm_accum_fp32", &wgrad_gemm_accum_fp32);
   wg.def("wgrad_gemm_accum_fp16", &wgrad_gemm_accum_fp16);

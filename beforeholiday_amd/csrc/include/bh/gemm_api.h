@@ -33,6 +33,10 @@ bool gemm_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, i
 int64_t gemm_bgrad_slabs(int64_t M);
 void gemm_nt(int dt, const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M,
              int64_t N, int64_t K, const GemmEpilogue& epi, hipStream_t st);
+// kernel choice: 0 auto (ping-pong 256x256 on large grids), 1 128x128, 2 256x256 one-barrier,
+// 3 256x128 three-stage, 4 ping-pong forced (K % 64 == 0 only); default from BH_GEMM_TILE
+int gemm_tile_mode();
+void gemm_set_tile_mode(int mode);
 // out[N] (dtype dt) = sum_r part[r][N]
 void gemm_colsum_finalize(int dt, const float* part, int64_t slabs, int64_t N, void* out, hipStream_t st);
 

@@ -28,6 +28,7 @@
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 
 namespace bh {
 namespace {
@@ -104,6 +105,21 @@ struct Args {
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// 4 consecutive 16-bit elements <-> fp32 (one 8-byte access)
+template <typename T> BH_DEVICE void load4(const T* p, float (&r)[4]) {
+  typedef T t4 __attribute__((ext_vector_type(4)));
+  const t4 v = *reinterpret_cast<const t4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = static_cast<float>(v[i]);
+}
+template <typename T> BH_DEVICE void store4(T* p, const float (&r)[4]) {
+  typedef T t4 __attribute__((ext_vector_type(4)));
+  t4 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = static_cast<T>(r[i]);
+  *reinterpret_cast<t4*>(p) = v;
+}
 
 // One K-step of A and B via LDS-DMA (global_load_lds, 16 B per lane): each wave-instruction fills
 // one 1-KiB piece = 8 rows of 128 B. The LDS destination is lane-linear, so the XOR swizzle is
@@ -341,6 +357,281 @@ __global__ __launch_bounds__(C::kThreads, 1) void k_gemm_nt(Args p) {
   }
 }
 
+// ---- 256x256 ping-pong kernel (large grids, K % 64 == 0) ----------------------------------------
+//
+// 8 waves as 2 (rows) x 4 (cols), each owning 128x64 outputs (acc[8][4] of 16x16 tiles). A K-step
+// of 64 is split into four phases, one per 64x32 quadrant of the wave tile (16 MFMAs each), and
+// every phase is two barrier-delimited segments: R (ds_read the quadrant's fragments, issue one
+// 8-KiB unit of the NEXT K-step's LDS-DMA, counted vmcnt) and M (the 16 MFMAs). The wave group
+// wr == 1 executes one extra barrier up front, so on every SIMD - which holds one wave of each
+// group - one wave runs its MFMA segment while the other reads LDS and issues loads: the matrix
+// core never waits on LDS latency and the DMA of a unit has ~5 segments to land.
+//
+// Units (64 rows x 128 B) of a K-step, issued by group g in phase j: j0 A rows g*128+[0,64),
+// j1 / j2 the ni = 0 / 1 column halves of B rows g*128+[0,128), j3 A rows g*128+[64,128). The
+// `vmcnt(4)` in each R segment retires every unit issued two own-R-segments earlier, which is
+// before the barrier ahead of its first reader (A halves are read only by their own group; a B
+// unit of group h is first read one phase after it is retired, by either group). Reads of step t
+// finish before step t+1's loads overwrite that buffer (two LDS buffers, 128 KiB).
+//
+// Loads are buffer_load ... lds through a per-workgroup buffer resource whose range ends at the
+// last valid row, so rows past M / N land as zeros without clamped per-lane pointers; the per-lane
+// VGPR offset carries the row (range-checked), the K offset rides in the scalar offset.
+constexpr int kPPThreads = 512;
+constexpr int kPPTile = 256;
+constexpr int kPPBuf = 65536;  // A 32 KiB + B 32 KiB per K-step
+constexpr int kPPSmem = 2 * kPPBuf;
+constexpr unsigned kRsrcWord3 = 0x00020000u;
+
+BH_DEVICE __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, int64_t rows_left, int64_t ld) {
+  const int64_t bytes = rows_left * ld * 2;
+  const int nrec = bytes >= 0xFFFFFFFFll ? (int)0xFFFFFFFFu : (int)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nrec, (int)kRsrcWord3);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kPPThreads, 1) void k_gemm_pp(Args p) {
+  __shared__ __attribute__((aligned(16))) char smem[kPPSmem];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int nwg = p.tiles_m * p.tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int per_group = kGroupM * p.tiles_n;
+  const int first_m = (wgid / per_group) * kGroupM;
+  const int gsize = min(p.tiles_m - first_m, kGroupM);
+  const int tm = first_m + (wgid % per_group) % gsize, tn = (wgid % per_group) / gsize;
+  const int brow = tm * kPPTile, bcol = tn * kPPTile;
+
+  const __amdgpu_buffer_rsrc_t rsA =
+      tile_rsrc(reinterpret_cast<const T*>(p.A) + (int64_t)brow * p.lda, p.M - brow, p.lda);
+  const __amdgpu_buffer_rsrc_t rsB =
+      tile_rsrc(reinterpret_cast<const T*>(p.B) + (int64_t)bcol * p.ldb, p.N - bcol, p.ldb);
+  const int lda2 = (int)p.lda * 2, ldb2 = (int)p.ldb * 2;
+  // per-lane part of a 1-KiB piece (8 rows x 8 chunks): row prow, physical chunk pch holding
+  // logical chunk pch ^ ((row >> 1) & 7); a piece's first row is a multiple of 8 whose parity of
+  // row / 8 is the piece parity i, so the XOR is ((i << 2) | (prow >> 1)).
+  const int prow = lane >> 3, pch = lane & 7;
+  int voffA[2], voffB[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int ch = pch ^ ((i << 2) | (prow >> 1));
+    voffA[i] = prow * lda2 + ch * 16;
+    voffB[i] = prow * ldb2 + ch * 16;
+  }
+
+  f4v acc[8][4];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  // unit j of group wr for the K-step at byte offset kb, into buffer dst; wave wc takes pieces
+  // 2wc, 2wc+1 of the unit's eight
+  auto issue = [&](auto jc, char* dst, int kb) {
+    constexpr int j = decltype(jc)::value;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if constexpr (j == 0 || j == 3) {
+        const int rb = wr * 128 + (j == 3 ? 64 : 0) + (2 * wc + i) * 8;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_ptr_t)(dst + rb * 128), 16, voffA[i] + rb * lda2, kb, 0,
+                                                 0);
+      } else {
+        const int rb = (2 * wr + (wc >> 1)) * 64 + (j == 2 ? 32 : 0) + (2 * (wc & 1) + i) * 8;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, (lds_ptr_t)(dst + 32768 + rb * 128), 16, voffB[i] + rb * ldb2,
+                                                 kb, 0, 0);
+      }
+    }
+  };
+
+  const int fr = lane & 15, fq = lane >> 4;
+  i4v af[2][4], b0[2][2], b1[2][2];
+  auto read_a = [&](const char* sa, int mi) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+        af[s][m] = *reinterpret_cast<const i4v*>(sa + swz(wr * 128 + mi * 64 + m * 16 + fr, s * 4 + fq));
+  };
+  auto read_b = [&](const char* sb, int ni, i4v (&bf)[2][2]) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        bf[s][n] = *reinterpret_cast<const i4v*>(sb + swz(wc * 64 + ni * 32 + n * 16 + fr, s * 4 + fq));
+  };
+  auto mfma_q = [&](int mi, int ni, const i4v (&bf)[2][2]) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+          acc[mi * 4 + m][ni * 2 + n] = Mfma<T>::run(bf[s][n], af[s][m], acc[mi * 4 + m][ni * 2 + n]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // one K-step from buffer cur; unless LAST, stage K-step byte offset kb into nxt
+  auto step = [&](auto last, const char* cur, char* nxt, int kb) {
+    constexpr bool LAST = decltype(last)::value;
+    const char* sa = cur;
+    const char* sb = cur + 32768;
+    // phase 0: quadrant (0, 0)
+    read_a(sa, 0);
+    read_b(sb, 0, b0);
+    if constexpr (!LAST) issue(std::integral_constant<int, 0>{}, nxt, kb);
+    if constexpr (LAST) wait_vmcnt<2>(); else wait_vmcnt<4>();
+    raw_barrier();
+    mfma_q(0, 0, b0);
+    raw_barrier();
+    // phase 1: quadrant (0, 1)
+    read_b(sb, 1, b1);
+    if constexpr (!LAST) issue(std::integral_constant<int, 1>{}, nxt, kb);
+    if constexpr (LAST) wait_vmcnt<0>(); else wait_vmcnt<4>();
+    raw_barrier();
+    mfma_q(0, 1, b1);
+    raw_barrier();
+    // phase 2: quadrant (1, 1)
+    read_a(sa, 1);
+    if constexpr (!LAST) issue(std::integral_constant<int, 2>{}, nxt, kb);
+    if constexpr (!LAST) wait_vmcnt<4>();
+    raw_barrier();
+    mfma_q(1, 1, b1);
+    raw_barrier();
+    // phase 3: quadrant (1, 0), fragments already in registers
+    if constexpr (!LAST) issue(std::integral_constant<int, 3>{}, nxt, kb);
+    if constexpr (!LAST) wait_vmcnt<4>();
+    raw_barrier();
+    mfma_q(1, 0, b0);
+    raw_barrier();
+  };
+
+  // prologue: the whole first K-step, then stagger the groups
+  issue(std::integral_constant<int, 0>{}, smem, 0);
+  issue(std::integral_constant<int, 1>{}, smem, 0);
+  issue(std::integral_constant<int, 2>{}, smem, 0);
+  issue(std::integral_constant<int, 3>{}, smem, 0);
+  wait_vmcnt<0>();
+  raw_barrier();
+  if (wr == 1) raw_barrier();
+  const int nk = p.K / BK;
+  for (int kt = 0; kt + 1 < nk; ++kt)
+    step(std::false_type{}, smem + (kt & 1) * kPPBuf, smem + ((kt + 1) & 1) * kPPBuf, (kt + 1) * BK * 2);
+  step(std::true_type{}, smem + ((nk - 1) & 1) * kPPBuf, nullptr, 0);
+  if (wr == 0) raw_barrier();
+
+  // ---- epilogue straight from the accumulators. The MFMAs ran with B as the first operand, so
+  // acc[mt][nt][j] = C[row fr of 16-row tile mt][column 4 * fq + j of 16-column tile nt]: every lane
+  // holds 4 consecutive columns, and bias, activation, aux and stores work on 8-byte vectors
+  // without an LDS transpose.
+  const GemmEpilogue& e = p.epi;
+  T* __restrict__ Cp = reinterpret_cast<T*>(p.C);
+  const int row_l = brow + wr * 128 + fr;
+  const int col_l = bcol + wc * 64 + fq * 4;
+  auto body = [&](auto actc) {
+    constexpr int ACT = decltype(actc)::value;
+    if (!e.bwd_act) {
+      float bias[4][4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int col = col_l + nt * 16;
+        if (e.bias && col < p.N) load4<T>(reinterpret_cast<const T*>(e.bias) + col, bias[nt]);
+        else bias[nt][0] = bias[nt][1] = bias[nt][2] = bias[nt][3] = 0.f;
+      }
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) {
+        const int row = row_l + mt * 16;
+        if (row >= p.M) break;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const int col = col_l + nt * 16;
+          if (col < p.N) {
+            float v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = acc[mt][nt][j] + bias[nt][j];
+            if (e.pre_out) store4<T>(reinterpret_cast<T*>(e.pre_out) + (int64_t)row * e.ld_aux + col, v);
+            if constexpr (ACT != kActNone) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[j] = act_f(v[j], ACT);
+            }
+            store4<T>(Cp + (int64_t)row * p.ldc + col, v);
+          }
+        }
+      }
+    } else {
+      float cs[4][4] = {};
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) {
+        const int row = row_l + mt * 16;
+        if (row >= p.M) break;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const int col = col_l + nt * 16;
+          if (col < p.N) {
+            float v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = acc[mt][nt][j];
+            if constexpr (ACT != kActNone) {
+              float a[4];
+              load4<T>(reinterpret_cast<const T*>(e.aux_in) + (int64_t)row * e.ld_aux + col, a);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[j] *= act_d(a[j], ACT);
+            }
+            // bias grad of the value actually stored (rounded like the reference's separate pass)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              v[j] = to_f<T>(from_f<T>(v[j]));
+              cs[nt][j] += v[j];
+            }
+            store4<T>(Cp + (int64_t)row * p.ldc + col, v);
+          }
+        }
+      }
+      if (e.bgrad_part) {
+        // sum over the 16 row lanes; the wave's 128 rows go to its first 64-row slab, the second
+        // slab (if it exists) gets zeros so the fixed-order finalize still sees every slab written
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float t = cs[nt][j];
+            t += __shfl_xor(t, 1);
+            t += __shfl_xor(t, 2);
+            t += __shfl_xor(t, 4);
+            t += __shfl_xor(t, 8);
+            cs[nt][j] = t;
+          }
+        const int row0 = brow + wr * 128;
+        if (fr == 0 && row0 < p.M) {
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            const int col = col_l + nt * 16;
+            if (col < p.N) {
+              float* dst = e.bgrad_part + (int64_t)(row0 / 64) * p.N + col;
+              *reinterpret_cast<float4*>(dst) = make_float4(cs[nt][0], cs[nt][1], cs[nt][2], cs[nt][3]);
+              if (row0 + 64 < p.M) *reinterpret_cast<float4*>(dst + p.N) = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+          }
+        }
+      }
+    }
+  };
+  switch (e.act) {
+    case kActRelu: body(std::integral_constant<int, kActRelu>{}); break;
+    case kActSigmoid: body(std::integral_constant<int, kActSigmoid>{}); break;
+    case kActGelu: body(std::integral_constant<int, kActGelu>{}); break;
+    case kActGeluTanh: body(std::integral_constant<int, kActGeluTanh>{}); break;
+    default: body(std::integral_constant<int, kActNone>{}); break;
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(64 * kColsumLanes) void k_colsum(const float* __restrict__ part, int64_t slabs, int64_t N,
                                                                T* __restrict__ out) {
@@ -367,6 +658,16 @@ bool gemm_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, i
 int64_t gemm_bgrad_slabs(int64_t M) { return (M + 63) / 64; }
 
 namespace {
+template <typename T>
+void launch_pp(const Args& a0, hipStream_t st) {
+  Args a = a0;
+  a.tiles_m = (a.M + kPPTile - 1) / kPPTile;
+  a.tiles_n = (a.N + kPPTile - 1) / kPPTile;
+  const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
+  if (nwg >= (1ll << 31)) throw std::runtime_error("gemm_nt: grid too large");
+  hipLaunchKernelGGL((k_gemm_pp<T>), dim3((unsigned)nwg), dim3(kPPThreads), 0, st, a);
+}
+
 template <typename C, typename T>
 void launch(const Args& a0, bool glds, hipStream_t st) {
   Args a = a0;
@@ -384,6 +685,15 @@ int env_mode(const char* name, int dflt) {
 }
 }  // namespace
 
+namespace {
+int g_tile_mode = -1;
+}
+int gemm_tile_mode() {
+  if (g_tile_mode < 0) g_tile_mode = env_mode("BH_GEMM_TILE", 0);
+  return g_tile_mode;
+}
+void gemm_set_tile_mode(int mode) { g_tile_mode = mode; }
+
 void gemm_nt(int dt, const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int64_t M,
              int64_t N, int64_t K, const GemmEpilogue& epi, hipStream_t st) {
   if (!gemm_supported(M, N, K, lda, ldb, ldc, A, B, C))
@@ -395,21 +705,27 @@ void gemm_nt(int dt, const void* A, int64_t lda, const void* B, int64_t ldb, voi
   a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.M = (int)M; a.N = (int)N; a.K = (int)K;
   a.epi = epi;
-  // BH_GEMM_GLDS=0 forces register staging; BH_GEMM_TILE=1 small / 2 big / 3 mid / 0 auto
+  // BH_GEMM_GLDS=0 forces register staging; tile mode (BH_GEMM_TILE / gemm_set_tile_mode):
+  // 1 small / 2 big / 3 mid / 4 ping-pong / 0 auto
   static const bool glds_on = env_mode("BH_GEMM_GLDS", 1) != 0;
-  static const int tile_mode = env_mode("BH_GEMM_TILE", 0);
+  const int tile_mode = gemm_tile_mode();
   const bool glds = glds_on && (K % BK) == 0;
   const int64_t big_wgs = ((M + CfgBig::BM - 1) / CfgBig::BM) * ((N + CfgBig::BN - 1) / CfgBig::BN);
-  const bool big = glds && (tile_mode == 2 || (tile_mode == 0 && big_wgs >= 256));
+  // the ping-pong kernel keeps row offsets of a 256-row tile in 32 bits
+  const bool pp_ok = glds && lda < (1 << 22) && ldb < (1 << 22);
+  const bool pp = pp_ok && (tile_mode == 4 || (tile_mode == 0 && big_wgs >= 256));
+  const bool big = glds && !pp && (tile_mode == 2 || (tile_mode == 0 && big_wgs >= 256));
   const bool mid = glds && tile_mode == 3;
   switch (dt) {
     case kF16:
-      if (mid) launch<CfgMid, f16>(a, true, st);
+      if (pp) launch_pp<f16>(a, st);
+      else if (mid) launch<CfgMid, f16>(a, true, st);
       else if (big) launch<CfgBig, f16>(a, true, st);
       else launch<CfgSmall, f16>(a, glds, st);
       break;
     case kBF16:
-      if (mid) launch<CfgMid, bf16>(a, true, st);
+      if (pp) launch_pp<bf16>(a, st);
+      else if (mid) launch<CfgMid, bf16>(a, true, st);
       else if (big) launch<CfgBig, bf16>(a, true, st);
       else launch<CfgSmall, bf16>(a, glds, st);
       break;

@@ -42,7 +42,24 @@ def main():
 
     require_native("bench_gemm")
     gm, fd = submodule("gemm"), submodule("fused_dense_cuda")
+    gm.set_force_mfma(True)  # time the kernels themselves, not the measured dispatch
     out = []
+    # plain C = A.B^T per tile kernel (uniform [-1, 1) operands) vs hipBLASLt
+    for dtype in (torch.bfloat16,):
+        for M, N, K in [(4096, 4096, 4096), (8192, 8192, 8192), (8192, 4096, 1024), (8192, 1024, 4096),
+                        (16384, 1024, 1024)]:
+            a = torch.rand(M, K, device="cuda", dtype=dtype) * 2 - 1
+            bm = torch.rand(N, K, device="cuda", dtype=dtype) * 2 - 1
+            flops = 2.0 * M * N * K
+            r = {"kind": "plain", "dtype": str(dtype).split(".")[1], "M": M, "N": N, "K": K}
+            iters = 20 if M * N * K >= 2 ** 38 else 50
+            r["blaslt_tflops"] = round(flops / timeit(lambda: torch.mm(a, bm.t()), iters) / 1e9, 1)
+            for mode, name in ((1, "t128"), (2, "t256"), (4, "pingpong")):
+                gm.set_tile_mode(mode)
+                r[name + "_tflops"] = round(flops / timeit(lambda: gm.linear_act(a, bm, None, 0, False), iters) / 1e9, 1)
+            gm.set_tile_mode(0)
+            out.append(r)
+            print(json.dumps(r), flush=True)
     for dtype in (torch.bfloat16, torch.float16):
         for M, N, K in SHAPES:
             x = torch.randn(M, K, device="cuda", dtype=dtype)

@@ -36,6 +36,44 @@ def _dact(pre_or_out, act):
 
 
 SHAPES = [(128, 128, 64), (300, 264, 72), (1, 8, 8), (257, 136, 520), (1536, 3072, 1024), (77, 1000, 16)]
+# tile-boundary shapes for the 256x256 kernels (K % 64 == 0: LDS-DMA paths)
+BIG_SHAPES = [(256, 256, 64), (520, 776, 192), (1000, 264, 1024), (2048, 2056, 128), (4096, 4096, 512)]
+MODES = [0, 1, 2, 3, 4]
+
+
+@pytest.fixture(autouse=True)
+def _pin_mfma():
+    gm = _gm()
+    gm.set_force_mfma(True)
+    yield
+    gm.set_force_mfma(False)
+    gm.set_tile_mode(0)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("shape", BIG_SHAPES)
+@pytest.mark.parametrize("mode", MODES)
+def test_tile_kernels(dtype, shape, mode):
+    """every tile configuration (auto, 128x128, 256x256, 256x128 three-stage, 256x256 ping-pong)
+    on edge shapes, forward with bias + GELU + aux and backward with dGELU + bias-grad partials"""
+    M, N, K = shape
+    _gm().set_tile_mode(mode)
+    torch.manual_seed(M + N + K + mode)
+    x = torch.randn(M, K, device="cuda", dtype=dtype)
+    w = torch.randn(N, K, device="cuda", dtype=dtype) / K ** 0.5
+    b = torch.randn(N, device="cuda", dtype=dtype)
+    y, pre = _gm().linear_act(x, w, b, 3, True)
+    ref_pre = x.float() @ w.float().t() + b.float()
+    tol = 2e-2 if dtype == torch.float16 else 6e-2
+    torch.testing.assert_close(pre.float(), ref_pre, rtol=tol, atol=tol)
+    torch.testing.assert_close(y.float(), F.gelu(ref_pre), rtol=tol, atol=tol)
+    dy = torch.randn(M, K, device="cuda", dtype=dtype)
+    wt = torch.randn(N, K, device="cuda", dtype=dtype) / K ** 0.5  # W^T of a [K, N] weight
+    aux = torch.randn(M, N, device="cuda", dtype=dtype)
+    dx, db = _gm().linear_dact(dy, wt, aux, 3, True)
+    ref = (dy.float() @ wt.float().t()) * _dact(aux, 3)
+    torch.testing.assert_close(dx.float(), ref, rtol=tol, atol=tol)
+    torch.testing.assert_close(db.float(), ref.sum(0), rtol=tol, atol=tol * max(1.0, M ** 0.5))
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
