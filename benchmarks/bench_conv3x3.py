@@ -39,7 +39,7 @@ def main():
 
     torch.backends.cudnn.benchmark = False
     dt = torch.float16 if args.dtype == "fp16" else torch.bfloat16
-    tot = {"ours_fwd": 0.0, "miopen_fwd": 0.0, "ours_dgrad": 0.0, "miopen_dgrad": 0.0}
+    tot = {"ours_fwd": 0.0, "miopen_fwd": 0.0, "ours_dgrad": 0.0, "miopen_dgrad": 0.0, "miopen_wgrad": 0.0}
     for C, H, cnt in SHAPES:
         N = args.batch
         x = torch.randn(N, C, H, H, device="cuda", dtype=dt).contiguous(memory_format=torch.channels_last)
@@ -52,9 +52,14 @@ def main():
         r["ours_dgrad"] = timeit(lambda: bhconv.conv3x3_dgrad(dy, w))
         r["miopen_dgrad"] = timeit(lambda: torch.ops.aten.convolution_backward(
             dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False]))
+        r["miopen_wgrad"] = timeit(lambda: torch.ops.aten.convolution_backward(
+            dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False]))
+        if hasattr(bhconv, "conv3x3_wgrad"):
+            r["ours_wgrad"] = timeit(lambda: bhconv.conv3x3_wgrad(dy, x))
+            tot.setdefault("ours_wgrad", 0.0)
         for k in tot:
             tot[k] += r[k] * cnt
-            r[k.replace("_fwd", "_fwd_tflops").replace("_dgrad", "_dgrad_tflops")] = round(flops / r[k] / 1e9, 1)
+            r[k + "_tflops"] = round(flops / r[k] / 1e9, 1)
             r[k] = round(r[k], 4)
         print(json.dumps(r), flush=True)
     print(json.dumps({"resnet50_weighted_ms": {k: round(v, 3) for k, v in tot.items()}}), flush=True)

@@ -16,12 +16,23 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--only", choices=["all", "gemm_plain"], default="all",
+                    help="gemm_plain: only C = A.B^T at 4096^3 bf16 on the ping-pong kernel (uniform [-1, 1) data)")
     args = ap.parse_args()
     from beforeholiday_amd._native import require_native, submodule
 
     require_native("pmc_kernels")
     gm, fa = submodule("gemm"), submodule("fused_attention")
+    gm.set_force_mfma(True)
     dt = torch.bfloat16
+    if args.only == "gemm_plain":
+        gm.set_tile_mode(4)
+        a = torch.rand(4096, 4096, device="cuda", dtype=dt) * 2 - 1
+        bm = torch.rand(4096, 4096, device="cuda", dtype=dt) * 2 - 1
+        for _ in range(args.iters):
+            gm.linear_act(a, bm, None, 0, False)
+        torch.cuda.synchronize()
+        return
     x = torch.randn(4096, 4096, device="cuda", dtype=dt)
     w = torch.randn(4096, 4096, device="cuda", dtype=dt) / 64
     b = torch.randn(4096, device="cuda", dtype=dt)

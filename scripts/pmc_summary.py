@@ -14,7 +14,9 @@ def main():
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 name = r.get("Kernel_Name", "?")
-                if "gemm_nt" in name:
+                if "k_gemm_pp" in name:
+                    name = "gemm_pp<256x256>"
+                elif "gemm_nt" in name:
                     big = "Li8ELi4E" in name or "Cfg<2, 4, 8, 4, 2>" in name
                     name = "gemm_nt<" + ("256x256" if big else "128x128") + ">"
                 elif "k_flash_fwd" in name:
@@ -39,6 +41,10 @@ def main():
             print(f"| {k} | {c} | {m[c]:.4g} |")
         if "SQ_VALU_MFMA_BUSY_CYCLES" in m and "SQ_BUSY_CYCLES" in m and m["SQ_BUSY_CYCLES"]:
             print(f"| {k} | MFMA busy / SQ busy | {m['SQ_VALU_MFMA_BUSY_CYCLES'] / m['SQ_BUSY_CYCLES']:.3f} |")
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in m and m.get("GRBM_GUI_ACTIVE"):
+            # per-SIMD share of the GPU-active cycles (GRBM_GUI_ACTIVE summed over 8 XCDs, 1024 SIMDs)
+            util = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["GRBM_GUI_ACTIVE"] / 8 * 1024)
+            print(f"| {k} | MFMA utilisation (busy / (GUI_ACTIVE/8 x 1024 SIMDs)) | {util:.3f} |")
         if "SQ_LDS_BANK_CONFLICT" in m and m.get("SQ_LDS_IDX_ACTIVE"):
             print(f"| {k} | LDS bank-conflict cycles / LDS active | {m['SQ_LDS_BANK_CONFLICT'] / m['SQ_LDS_IDX_ACTIVE']:.3f} |")
         if "TCC_HIT_sum" in m and (m["TCC_HIT_sum"] + m.get("TCC_MISS_sum", 0)):
