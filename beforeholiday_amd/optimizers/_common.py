@@ -49,3 +49,52 @@ def zero_grad(opt, set_grad_none: bool, set_to_none=None):
                 grads.append(p.grad)
     if grads:
         torch._foreach_zero_(grads)
+
+
+class ParamTableMixin:
+    """Host fast path of the fused optimizers: the parameters and their state tensors are registered
+    once in a native ``amp_C.ParamTable`` and a step is ONE call that reads the gradients in C++
+    (see csrc/bindings/mta.cpp). The table is rebuilt when the param groups change, after
+    ``load_state_dict`` / ``add_param_group``, and when a parameter gets its first gradient (the step
+    returns False before launching anything, the optimizer creates that state and retries)."""
+
+    _table = None
+    _table_sig = None
+    native_table = True  # False: always the per-step tensor-list path (kept for A/B tests)
+
+    def _table_signature(self):
+        return tuple((id(g["params"]), len(g["params"])) for g in self.param_groups)
+
+    def _native_table(self, state_keys, master=None):
+        sig = self._table_signature()
+        if self._table is not None and self._table_sig == sig:
+            return self._table
+        from .._native import submodule
+
+        table = submodule("amp_C").ParamTable()
+        for g in self.param_groups:
+            sts = [self.state.get(p) or {} for p in g["params"]]
+            s0 = [st.get(state_keys[0]) for st in sts]
+            s1 = [st.get(state_keys[1]) for st in sts]
+            m = [st.get(master) for st in sts] if master else []
+            table.add_group(list(g["params"]), s0, s1, m)
+        self._table, self._table_sig = table, sig
+        return table
+
+    def _fast_path_ok(self):
+        if not self.native_table:
+            return False
+        buf = getattr(self, "_dummy_overflow_buf", None)
+        if buf is None or not buf.is_cuda:
+            return False
+        from .._native import available
+
+        return available()
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._table = None
+
+    def add_param_group(self, param_group):
+        super().add_param_group(param_group)
+        self._table = None

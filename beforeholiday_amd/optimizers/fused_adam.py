@@ -14,10 +14,10 @@ import torch
 
 from ..multi_tensor_apply import multi_tensor_applier
 from ..ops import amp_C
-from ._common import first_device, grad_like_param, noop_buffer, zero_grad
+from ._common import ParamTableMixin, first_device, grad_like_param, noop_buffer, zero_grad
 
 
-class FusedAdam(torch.optim.Optimizer):
+class FusedAdam(ParamTableMixin, torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, bias_correction=True, betas=(0.9, 0.999), eps=1e-8,
                  adam_w_mode=True, weight_decay=0.0, amsgrad=False, set_grad_none=True,
                  capturable=False, master_weights=False):
@@ -47,6 +47,38 @@ class FusedAdam(torch.optim.Optimizer):
             st["master_param"] = p.detach().float().clone()
         return st["master_param"]
 
+    def _init_state(self, p):
+        state = self.state[p]
+        use_master = self.master_weights and p.dtype in (torch.float16, torch.bfloat16)
+        target = self._master(p) if use_master else p
+        if "exp_avg" not in state:
+            # 16-bit params keep fp32 moments: an fp16 exp_avg_sq underflows to 0 for
+            # |g| < 8e-3 and the update then blows up to inf (the reference stores them in
+            # the param dtype); the kernel reads/writes fp32 state natively.
+            sdt = torch.float32 if target.dtype in (torch.float16, torch.bfloat16) else target.dtype
+            state["exp_avg"] = torch.zeros_like(target, dtype=sdt)
+            state["exp_avg_sq"] = torch.zeros_like(target, dtype=sdt)
+        return state, use_master, target
+
+    def _native_step(self):
+        """GPU step through the native parameter table (one host call for every group's launches)."""
+        hyper = []
+        for group in self.param_groups:
+            group["step"] = group.get("step", 0) + 1
+            beta1, beta2 = group["betas"]
+            hyper.append([float(group["lr"]), beta1, beta2, group["eps"], group["step"],
+                          1 if group["bias_correction"] else 0, group["weight_decay"]])
+        master = "master_param" if self.master_weights else None
+        args = (self._dummy_overflow_buf, hyper, self.adam_w_mode)
+        if not self._native_table(("exp_avg", "exp_avg_sq"), master).adam_step(*args):
+            for group in self.param_groups:
+                for p in group["params"]:
+                    if p.grad is not None:
+                        self._init_state(p)
+            self._table = None
+            if not self._native_table(("exp_avg", "exp_avg_sq"), master).adam_step(*args):
+                raise RuntimeError("FusedAdam: optimizer state missing after initialisation")
+
     @torch.no_grad()
     def step(self, closure=None, grads=None, output_params=None, scale=None, grad_norms=None,
              grad_scaler=None):
@@ -57,6 +89,9 @@ class FusedAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        if not self.capturable and grad_scaler is None and self._fast_path_ok():
+            self._native_step()
+            return loss
         inv_scale = found_inf = None
         if grad_scaler is not None:
             if not self.capturable:
@@ -84,16 +119,7 @@ class FusedAdam(torch.optim.Optimizer):
                     raise RuntimeError("FusedAdam does not support sparse gradients, please consider SparseAdam instead")
                 if p.dtype not in (torch.float16, torch.bfloat16, torch.float32, torch.float64):
                     raise RuntimeError("FusedAdam only support fp16, bfloat16, fp32 and fp64.")
-                state = self.state[p]
-                use_master = self.master_weights and p.dtype in (torch.float16, torch.bfloat16)
-                target = self._master(p) if use_master else p
-                if "exp_avg" not in state:
-                    # 16-bit params keep fp32 moments: an fp16 exp_avg_sq underflows to 0 for
-                    # |g| < 8e-3 and the update then blows up to inf (the reference stores them in
-                    # the param dtype); the kernel reads/writes fp32 state natively.
-                    sdt = torch.float32 if target.dtype in (torch.float16, torch.bfloat16) else target.dtype
-                    state["exp_avg"] = torch.zeros_like(target, dtype=sdt)
-                    state["exp_avg_sq"] = torch.zeros_like(target, dtype=sdt)
+                state, use_master, target = self._init_state(p)
                 g = grad_like_param(p)
                 key = (target.dtype, state["exp_avg"].dtype, use_master)
                 lists = buckets.setdefault(key, [[], [], [], [], []])

@@ -11,10 +11,10 @@ import torch
 
 from ..multi_tensor_apply import multi_tensor_applier, multi_tensor_applier_l2norm
 from ..ops import amp_C
-from ._common import first_device, grad_like_param, noop_buffer, zero_grad
+from ._common import ParamTableMixin, first_device, grad_like_param, noop_buffer, zero_grad
 
 
-class FusedLAMB(torch.optim.Optimizer):
+class FusedLAMB(ParamTableMixin, torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, bias_correction=True, betas=(0.9, 0.999), eps=1e-6,
                  weight_decay=0.01, amsgrad=False, adam_w_mode=True, grad_averaging=True,
                  set_grad_none=True, max_grad_norm=1.0, use_nvlamb=False):
@@ -51,12 +51,36 @@ class FusedLAMB(torch.optim.Optimizer):
             return norms[0]
         return multi_tensor_applier_l2norm(self.multi_tensor_l2norm, self._dummy_overflow_buf, [norms], False)[0]
 
+    def _native_step(self):
+        """GPU step through the native parameter table: one host call for the global norm and every
+        group's LAMB launches (same kernels and semantics as the list path below)."""
+        hyper = []
+        for group in self.param_groups:
+            group["step"] = group.get("step", 0) + 1
+            beta1, beta2 = group["betas"]
+            hyper.append([float(group["lr"]), beta1, beta2, group["eps"], group["step"],
+                          1 if group["bias_correction"] else 0, group["weight_decay"],
+                          1 if group["grad_averaging"] else 0])
+        args = (self._dummy_overflow_buf, hyper, self.adam_w_mode, self.defaults["max_grad_norm"], self.use_nvlamb)
+        if not self._native_table(("exp_avg", "exp_avg_sq")).lamb_step(*args):
+            for group in self.param_groups:
+                for p in group["params"]:
+                    if p.grad is not None and "exp_avg" not in self.state[p]:
+                        self.state[p]["exp_avg"] = torch.zeros_like(p)
+                        self.state[p]["exp_avg_sq"] = torch.zeros_like(p)
+            self._table = None
+            if not self._native_table(("exp_avg", "exp_avg_sq")).lamb_step(*args):
+                raise RuntimeError("FusedLAMB: optimizer state missing after initialisation")
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        if self._fast_path_ok():
+            self._native_step()
+            return loss
         device = first_device(self.param_groups)
         global_grad_norm = self._global_grad_norm(device)
         max_grad_norm = self.defaults["max_grad_norm"]
