@@ -1,3 +1,3 @@
-from .peer_memory import PeerHaloExchanger1d, PeerMemoryPool
+from .peer_memory import PeerAllReduce, PeerHaloExchanger1d, PeerMemoryPool
 
-__all__ = ["PeerMemoryPool", "PeerHaloExchanger1d"]
+__all__ = ["PeerMemoryPool", "PeerHaloExchanger1d", "PeerAllReduce"]

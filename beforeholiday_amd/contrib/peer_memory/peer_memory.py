@@ -164,3 +164,46 @@ class PeerHaloExchanger1d:
                                  self.high_zero, self.epoch, self.err, self.max_spins)
         if diagnostics and int(self.err.item()) != 0:
             raise RuntimeError("PeerHaloExchanger1d: a neighbour did not publish its halo in time")
+
+
+class PeerAllReduce:
+    """SUM all-reduce of small fp32 vectors among the ranks of a :class:`PeerMemoryPool` through
+    IPC-mapped peer memory: one single-workgroup kernel pushes the payload into every peer's slot row,
+    publishes an epoch flag and sums the rows in rank order once every peer's flag arrived (bounded
+    wait; ``err`` is set on a timeout) -- no collective launch, no host synchronisation. This is the
+    statistics exchange of group batch norm (reference: apex/contrib/csrc/groupbn/ipc.cu:22-129 and
+    the peer-buffer exchange of nhwc_batch_norm_kernel.h). Every rank must issue the same sequence of
+    calls with the same payload sizes, like any collective. Without a native pool (CPU / gloo) it
+    falls back to ``dist.all_reduce``."""
+
+    def __init__(self, peer_pool, capacity=1 << 14, group=None, max_spins=1 << 22):
+        self.pool = peer_pool
+        self.group = group
+        self.G = len(peer_pool.peer_ranks)
+        self.me = peer_pool.peer_rank
+        self.capacity = int(capacity)
+        self.max_spins = max_spins
+        self.epoch = 0
+        self.native = getattr(peer_pool, "native", False)
+        if self.native:
+            assert self.G <= 8, "PeerAllReduce: at most 8 ranks per pool"
+            self.slots = peer_pool.allocate_peer_tensors([2, self.G, self.capacity], torch.float32, False, False)
+            self.flags = peer_pool.allocate_peer_tensors([self.G], torch.int32, False, False)
+            self._slot_ptrs = [t.data_ptr() for t in self.slots]
+            self._flag_ptrs = [t.data_ptr() for t in self.flags]
+            self.err = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+    @property
+    def size(self):
+        return self.G
+
+    def all_reduce_(self, t):
+        """In-place SUM over the pool's ranks of a contiguous fp32 GPU tensor (numel <= capacity)."""
+        if not (self.native and t.is_cuda):
+            dist.all_reduce(t, group=self.group)
+            return t
+        assert t.dtype == torch.float32 and t.is_contiguous(), "PeerAllReduce: contiguous fp32 tensors only"
+        self.epoch += 1
+        _pm().peer_allreduce(t, t, self._slot_ptrs, self._flag_ptrs, self.capacity, self.me, self.epoch, self.err,
+                             self.max_spins)
+        return t

@@ -144,6 +144,35 @@ void push_pull_halos_1d(at::Tensor out_lo, at::Tensor out_hi, at::Tensor in_lo, 
   bh::push_pull_halos_1d(a, stream_for(out_lo));
 }
 
+// SUM all-reduce of the fp32 vector `in` (into `out`, may alias) over the pool's ranks: slots[q] /
+// flags[q] are the device addresses of rank q's [2, G, capacity] slot array and int32 [G] flags.
+void peer_allreduce(at::Tensor in, at::Tensor out, std::vector<int64_t> slots, std::vector<int64_t> flags,
+                    int64_t capacity, int64_t me, int64_t epoch, at::Tensor err, int64_t max_spins) {
+  TORCH_CHECK(in.is_cuda() && in.scalar_type() == at::kFloat && in.is_contiguous(), "in must be contiguous fp32 GPU");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() == in.numel(),
+              "out must match in");
+  TORCH_CHECK(slots.size() == flags.size() && !slots.empty() && slots.size() <= (size_t)bh::kPeerMaxRanks,
+              "peer_allreduce: 1..8 ranks");
+  TORCH_CHECK(in.numel() <= capacity, "peer_allreduce: payload of ", in.numel(), " floats exceeds the slot capacity ",
+              capacity);
+  TORCH_CHECK(err.is_cuda() && err.scalar_type() == at::kInt, "err must be a GPU int32 tensor");
+  TORCH_CHECK(epoch > 0 && epoch < (1ll << 30), "epoch must be in [1, 2^30)");
+  bh::PeerReduceArgs a{};
+  a.in = in.data_ptr<float>();
+  a.out = out.data_ptr<float>();
+  a.G = (int)slots.size();
+  for (int q = 0; q < a.G; ++q) {
+    a.slots[q] = reinterpret_cast<float*>(slots[q]);
+    a.flags[q] = reinterpret_cast<int*>(flags[q]);
+  }
+  a.me = (int)me;
+  a.L = (int)in.numel();
+  a.epoch = (int)epoch;
+  a.max_spins = (int)max_spins;
+  a.err = err.data_ptr<int>();
+  bh::peer_allreduce(a, stream_for(in));
+}
+
 }  // namespace
 
 void register_peer_memory(pybind11::module_& root) {
@@ -159,6 +188,7 @@ void register_peer_memory(pybind11::module_& root) {
   m.def("blob_view_float", [](int64_t raw, std::vector<int64_t> shape, bool cl) { return blob_view(raw, shape, cl, at::kFloat); });
   m.def("blob_view_int", [](int64_t raw, std::vector<int64_t> shape, bool cl) { return blob_view(raw, shape, cl, at::kInt); });
   m.def("push_pull_halos_1d", &push_pull_halos_1d);
+  m.def("peer_allreduce", &peer_allreduce, "one-shot IPC SUM all-reduce of a small fp32 vector (group BN statistics)");
 }
 
 }  // namespace bhb

@@ -41,4 +41,22 @@ struct HaloArgs {
 };
 void push_pull_halos_1d(const HaloArgs& a, hipStream_t st);
 
+// One-shot SUM all-reduce of a small fp32 vector over the G ranks of a peer-memory pool (the IPC path
+// of group batch norm; reference: apex/contrib/csrc/groupbn/ipc.cu:22-129 + the peer exchange inside
+// nhwc_batch_norm_kernel.h). Every rank pushes its payload into row `me` of every peer's slot array
+// (parity epoch % 2: [2][G][L] floats in each rank's pool), publishes `epoch` in each peer's flag
+// array (flags[me], release, system scope), waits (bounded) until all G-1 peers published the same
+// epoch in its own flags, then sums its G local rows in rank order -- the same order on every rank,
+// so all ranks get bitwise-identical results. out may alias in.
+constexpr int kPeerMaxRanks = 8;
+struct PeerReduceArgs {
+  const float* in;
+  float* out;
+  float* slots[kPeerMaxRanks];  // slot array of each rank (peer pointers; own at index me)
+  int* flags[kPeerMaxRanks];    // int32 [G] flag array of each rank
+  int G, me, L, epoch, max_spins;
+  int* err;
+};
+void peer_allreduce(const PeerReduceArgs& a, hipStream_t st);
+
 }  // namespace bh

@@ -94,7 +94,56 @@ __global__ __launch_bounds__(kBlock) void k_halo_1d(HaloArgs a) {
   }
 }
 
+constexpr int kReduceBlock = 512;
+
+__global__ __launch_bounds__(kReduceBlock) void k_peer_allreduce(PeerReduceArgs a) {
+  const int parity = a.epoch & 1;
+  // 1. push: my payload into row `me` of every rank's slot array (vector stores over xGMI)
+  for (int q = 0; q < a.G; ++q) {
+    float* dst = a.slots[q] + ((int64_t)parity * a.G + a.me) * a.L;
+    for (int i = threadIdx.x; i < a.L; i += kReduceBlock) dst[i] = a.in[i];
+  }
+  __syncthreads();
+  // 2. publish: the rows are visible system-wide before any flag is
+  if (threadIdx.x == 0) {
+    __atomic_thread_fence(__ATOMIC_RELEASE);
+    for (int q = 0; q < a.G; ++q)
+      if (q != a.me) __hip_atomic_store(a.flags[q] + a.me, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // 3. one lane per peer waits (bounded) for that peer's rows of this epoch
+  __shared__ int ok;
+  if (threadIdx.x == 0) ok = 1;
+  __syncthreads();
+  const int q = threadIdx.x;
+  if (q < a.G && q != a.me && !wait_epoch(a.flags[a.me] + q, a.epoch, a.max_spins)) {
+    ok = 0;
+    __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  // 4. sum the G rows in rank order (identical on every rank); a timed-out exchange keeps the input
+  const float* rows = a.slots[a.me] + (int64_t)parity * a.G * a.L;
+  for (int i = threadIdx.x; i < a.L; i += kReduceBlock) {
+    float s = 0.f;
+    if (ok) {
+      for (int r = 0; r < a.G; ++r) s += rows[(int64_t)r * a.L + i];
+    } else {
+      s = a.in[i];
+    }
+    a.out[i] = s;
+  }
+}
+
 }  // namespace
+
+void peer_allreduce(const PeerReduceArgs& a, hipStream_t st) {
+  if (a.L <= 0) return;
+  if (a.G < 1 || a.G > kPeerMaxRanks || a.me < 0 || a.me >= a.G)
+    throw std::runtime_error("peer_allreduce: bad group geometry");
+  hipLaunchKernelGGL(k_peer_allreduce, dim3(1), dim3(kReduceBlock), 0, st, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("peer_allreduce: ") + hipGetErrorString(e));
+}
 
 void push_pull_halos_1d(const HaloArgs& a, hipStream_t st) {
   if (a.numel == 0) return;

@@ -39,9 +39,18 @@ def set_stats_mode(mode: str) -> None:
 
 
 def _world(pg):
+    if hasattr(pg, "all_reduce_"):  # a reducer object, e.g. contrib.peer_memory.PeerAllReduce (IPC)
+        return pg.size
     if not (dist.is_available() and dist.is_initialized()):
         return 1
     return dist.get_world_size(pg)
+
+
+def _all_reduce(t, pg):
+    if hasattr(pg, "all_reduce_"):
+        pg.all_reduce_(t)
+    else:
+        dist.all_reduce(t, group=pg)
 
 
 class SyncBatchnormFunction(torch.autograd.Function):
@@ -50,11 +59,11 @@ class SyncBatchnormFunction(torch.autograd.Function):
                 channel_last, fuse_relu, num_batches=None, pool=None):
         input = input.contiguous(memory_format=torch.channels_last) if (channel_last and input.dim() == 4) else input
         world = _world(process_group)
-        if world > 1 and stats_mode() == "allreduce":
+        if world > 1 and (stats_mode() == "allreduce" or hasattr(process_group, "all_reduce_")):
             # one fixed-size [2C+1] SUM all-reduce of shifted sums (K = running mean, shared by all ranks)
             sums = syncbn.stats_local_sums(input, running_mean)
             with comm_stats.timed("syncbn_fwd", sums):
-                dist.all_reduce(sums, group=process_group)
+                _all_reduce(sums, process_group)
             mean, invstd, scale, shift, count = syncbn.merge_sums(sums, weight, bias, running_mean, running_var,
                                                                   momentum, eps, num_batches)
         elif world > 1:
@@ -100,7 +109,7 @@ class SyncBatchnormFunction(torch.autograd.Function):
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             if ctx.world > 1:
                 with comm_stats.timed("syncbn_bwd", sums):
-                    dist.all_reduce(sums, group=ctx.process_group)
+                    _all_reduce(sums, ctx.process_group)
             grad_input, grad_z = syncbn.backward_dgrad(grad_output, input, z, mean, invstd, weight, sums, count,
                                                        scale, shift, ctx.fuse_relu,
                                                        ctx.has_z and ctx.needs_input_grad[1], mask)

@@ -65,3 +65,77 @@ def test_peer_halo_exchange_cpu(world):
 @pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
 def test_peer_halo_exchange_ipc_two_processes_one_gpu(dtype):
     run_distributed(_halo, 2, "cuda", dtype)
+
+
+def _allreduce(rank, world, device):
+    from beforeholiday_amd.contrib.peer_memory import PeerAllReduce, PeerMemoryPool
+    if device == "cuda":
+        torch.cuda.set_device(0)
+    pool = PeerMemoryPool(1 << 20, 0, peer_ranks=list(range(world)))
+    red = PeerAllReduce(pool, capacity=4096)
+    for step, n in enumerate([1, 257, 4096, 33, 4096, 1000]):
+        rows = [torch.randn(n, generator=torch.Generator().manual_seed(10 * step + r)) for r in range(world)]
+        expect = torch.zeros(n)
+        for r in range(world):  # rank order, fp32: the kernel's summation order
+            expect = expect + rows[r]
+        t = rows[rank].to(device)
+        red.all_reduce_(t)
+        torch.testing.assert_close(t.cpu(), expect, rtol=0, atol=0 if device == "cuda" else 1e-6)
+    if device == "cuda":
+        torch.cuda.synchronize()
+        assert int(red.err.item()) == 0
+    dist.barrier()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_peer_allreduce_ipc_processes_one_gpu(world):
+    run_distributed(_allreduce, world, "cuda")
+
+
+def test_peer_allreduce_cpu_fallback():
+    run_distributed(_allreduce, 2, "cpu")
+
+
+def _groupbn(rank, world, device, fuse_relu):
+    from beforeholiday_amd.contrib import groupbn
+    if device == "cuda":
+        torch.cuda.set_device(0)
+    N, H, W, C = 4, 5, 6, 24
+    g = torch.Generator().manual_seed(0)
+    xs = torch.randn(world * N, H, W, C, generator=g) * 2 + 0.5
+    dys = torch.randn(world * N, H, W, C, generator=g)
+    bn = groupbn.BatchNorm2d_NHWC(C, fuse_relu=fuse_relu, bn_group=world).to(device)
+    with torch.no_grad():
+        bn.weight.copy_(torch.linspace(0.5, 1.5, C))
+        bn.bias.copy_(torch.linspace(-0.2, 0.2, C))
+    x = xs[rank * N:(rank + 1) * N].to(device).requires_grad_(True)
+    for _ in range(3):  # several exchanges (epochs / slot parities)
+        y = bn(x)
+        y.backward(dys[rank * N:(rank + 1) * N].to(device))
+    # fp32 full-batch reference
+    xr = xs.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    w = torch.linspace(0.5, 1.5, C).requires_grad_(True)
+    b = torch.linspace(-0.2, 0.2, C).requires_grad_(True)
+    yr = torch.nn.functional.batch_norm(xr, None, None, w, b, True, 0.1, 1e-5)
+    if fuse_relu:
+        yr = torch.relu(yr)
+    yr.backward(dys.permute(0, 3, 1, 2))
+    torch.testing.assert_close(y.detach().cpu(), yr.detach().permute(0, 2, 3, 1)[rank * N:(rank + 1) * N],
+                               rtol=1e-4, atol=1e-4)
+    gx = x.grad.cpu() / 3  # three identical backward passes accumulated
+    torch.testing.assert_close(gx, xr.grad.permute(0, 2, 3, 1)[rank * N:(rank + 1) * N], rtol=1e-4, atol=1e-4)
+    if device == "cuda":
+        assert groupbn.batch_norm._IPC[world].epoch == 6  # 3 forward + 3 backward exchanges went over IPC
+        torch.cuda.synchronize()
+    dist.barrier()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fuse_relu", [False, True])
+def test_groupbn_ipc_two_processes_one_gpu(fuse_relu):
+    run_distributed(_groupbn, 2, "cuda", fuse_relu)
+
+
+def test_groupbn_group_cpu():
+    run_distributed(_groupbn, 2, "cpu", False)
