@@ -73,9 +73,10 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo only to rehearse the "
                          "multi-rank code path, e.g. several ranks sharing one GPU)")
-    ap.add_argument("--bn-group", default="separate", choices=["separate", "world"],
+    ap.add_argument("--bn-group", default="separate", choices=["separate", "world", "ipc"],
                     help="separate: SyncBN stats use their own communicator (all ranks), so a BN all_reduce "
-                         "never queues behind a DDP gradient bucket on the same RCCL stream")
+                         "never queues behind a DDP gradient bucket on the same RCCL stream; ipc: SyncBN stats "
+                         "through HIP-IPC peer memory (PeerAllReduce, single node), no RCCL launch per BN layer")
     ap.add_argument("--stem", default="fused", choices=["fused", "unfused"],
                     help="fused: bn1+ReLU+maxpool in one HIP pass; unfused: SyncBN+ReLU then torch max_pool2d")
     ap.add_argument("--conv1x1", default="auto", choices=["auto", "miopen", "gemm"],
@@ -124,6 +125,12 @@ def main():
     set_stats_mode(args.syncbn_stats)
     torch.manual_seed(1234 + rank)
     bn_group = dist.new_group(list(range(world))) if (world > 1 and args.bn_group == "separate") else None
+    if world > 1 and args.bn_group == "ipc":
+        # SyncBN statistics through HIP-IPC peer memory (one-shot push + flag kernel, no RCCL launch)
+        from beforeholiday_amd.contrib.peer_memory import PeerAllReduce, PeerMemoryPool
+
+        bn_group = PeerAllReduce(PeerMemoryPool(2 * world * (1 << 13) * 4 + 4096, 0, peer_ranks=list(range(world))),
+                                 capacity=1 << 13)
     model = (resnet50() if args.no_syncbn else resnet50_fused(process_group=bn_group, channel_last=True,
                                                                    conv1x1_mode=args.conv1x1, conv3x3_mode=args.conv3x3,
                                                                    stem_pool_fused=args.stem == "fused")).cuda()
