@@ -26,4 +26,21 @@ void conv3x3_forward(int dt, const Conv3x3Args& a, hipStream_t st);
 // a.y = dX [N, H, W, C_w]; a.C = K_w (channels read), a.K = C_w (channels written)
 void conv3x3_dgrad(int dt, const Conv3x3Args& a, hipStream_t st);
 
+// Weight gradient of a stride-1 "same" R x R convolution (R = 1 or 3, pad (R-1)/2), kernels/conv_wgrad.hip:
+// out[k][r][s][c] = sum over pixels of dy[n, y, x, k] * x[n, y + r - P, x + s - P, c].
+struct ConvWgradArgs {
+  const void* x = nullptr;   // [N, H, W, C]
+  const void* dy = nullptr;  // [N, H, W, K]
+  void* out = nullptr;       // [K, R, R, C]
+  int N = 0, H = 0, W = 0, C = 0, K = 0, R = 3;
+};
+struct ConvWgradGeo {
+  int G4 = 0, TH = 0, ksteps = 0, wpi = 0, nwin = 0, ctiles = 0, tiles = 0, wpw = 0, splits = 0, grid = 0;
+};
+// false when the kernel does not cover the shape (C, K % 64, 16-byte alignment, window fits in LDS)
+bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo);
+// fp32 elements of split partials the launch needs (0: the kernel writes `out` directly)
+int64_t conv_wgrad_workspace(const ConvWgradGeo& g, const ConvWgradArgs& a);
+void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws, hipStream_t st);
+
 }  // namespace bh

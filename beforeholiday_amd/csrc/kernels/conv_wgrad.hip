@@ -1,0 +1,359 @@
+// Weight gradient of a stride-1 "same" NHWC convolution (R x R, R = 1 or 3) on MFMA 32x32x16 (gfx950):
+//   dW[k][r][s][c] = sum over pixels p of dY[p][k] * X[p + (r - P, s - P)][c],   P = (R - 1) / 2
+// see bh/conv_api.h.
+//
+// The reduction runs over pixels, which sit on the strided (row) axis of both NHWC operands, so both
+// MFMA operands are read from LDS with ds_read_b64_tr_b16 (the 16-lane hardware transpose: each lane
+// names 4 contiguous channels of one pixel row, and gets one channel of 4 pixels). The k-dimension is
+// a list of 4-pixel groups along image rows, so a 14- or 7-wide image wastes at most one group column
+// instead of padding rows to 32.
+//
+// Workgroup = 4 waves = a 64 (k) x 64 (c) tile of all R*R offsets: wave (kw, cw) owns one 32x32
+// accumulator per offset (144 fp32 AGPRs at R = 3), one workgroup per CU. A window is TH whole image
+// rows: its dY (TH x 4*G4 pixels, zero past the image) and the X halo ((TH + 2P) x (4*G4 + 2P)
+// pixels, zero outside the image) land in LDS by LDS-DMA (buffer loads through whole-tensor
+// resources: an out-of-image pixel gets an out-of-range offset and arrives as zeros), double
+// buffered (138 KiB: 192-byte pixel slots, see kSlot). Every k-step reads one dY
+// fragment and reuses it for the R*R shifted X fragments; the next k-step's fragments are read
+// behind the current MFMAs. Each workgroup walks a contiguous run of windows and writes an fp32
+// partial tile; a second kernel sums the splits in a fixed order into the 16-bit weight gradient
+// (deterministic, no atomics, no zero-fill). Workgroups that share windows sit on one XCD (shared L2).
+#include "bh/api.h"
+#include "bh/conv_api.h"
+#include "bh/device.h"
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+
+namespace bh {
+namespace {
+
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef __bf16 b8v __attribute__((ext_vector_type(8)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef int i4v __attribute__((ext_vector_type(4)));
+typedef int i2v __attribute__((ext_vector_type(2)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4v* lds_s4_ptr;
+
+template <typename T> struct MfmaW;
+template <> struct MfmaW<f16> {
+  static BH_DEVICE f16v run(i4v a, i4v b, f16v c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8v, a), __builtin_bit_cast(h8v, b), c, 0, 0, 0);
+  }
+};
+template <> struct MfmaW<bf16> {
+  static BH_DEVICE f16v run(i4v a, i4v b, f16v c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(b8v, a), __builtin_bit_cast(b8v, b), c, 0, 0, 0);
+  }
+};
+
+constexpr int kThreads = 256;
+constexpr int kTile = 64;        // k and c per workgroup
+// LDS bytes per pixel slot: 64 channels x 2 B + 64 B pad. At a 48-dword stride any four consecutive
+// slots start in four distinct 16-dword bank quarters, so the transposed reads (4 pixels x 64 B per
+// 32-lane half) are conflict free, and a slot's address is LINEAR in the slot index: the R*R
+// shifted X fragments are one base register plus immediate offsets (no per-read swizzle math).
+constexpr int kSlot = 192;
+constexpr int kMaxHalo = 240;    // X slots per window
+constexpr int kMaxD = 128;       // dY slots per window (k-steps x 16)
+constexpr int kBufX = kMaxHalo * kSlot;
+constexpr int kBuf = (kMaxHalo + kMaxD) * kSlot;  // one window buffer (two: 138 KiB)
+constexpr unsigned kRsrcWord3 = 0x00020000u;
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// One LDS-DMA instruction (16 B per lane, lane-linear at LDS byte address `lds`) through buffer
+// resource `rs`, as inline asm: issued through the builtin, the compiler cannot tell the DMA's LDS
+// writes from the fragment reads of the OTHER window buffer and puts an s_waitcnt vmcnt(0) in front
+// of every following ds_read -- which serialises the prefetch with the compute. Here the kernel
+// orders them itself (wait_vmcnt + barrier at the window boundary).
+BH_DEVICE void dma16(i4v rs, int voff, unsigned lds) {
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %0, %2, 0 offen lds" ::"v"(voff),
+      "s"(lds), "s"(rs)
+      : "memory", "m0");
+}
+BH_DEVICE i4v make_rsrc(const void* base, int64_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  return i4v{(int)(uint32_t)a, (int)((a >> 32) & 0xffff), (int)(uint32_t)bytes, (int)kRsrcWord3};
+}
+BH_DEVICE unsigned lds_addr(const void* p) {
+  typedef const __attribute__((address_space(3))) char* lds_cptr;
+  return (unsigned)(uintptr_t)((lds_cptr)p);
+}
+
+template <int N> BH_DEVICE void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// workgroup barrier the compiler may not move LDS accesses across (LDS-DMA writes are invisible to it)
+BH_DEVICE void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// operand fragment: two transposed 4-pixel reads at byte offsets lo / hi (+ a compile-time shift)
+BH_DEVICE i4v frag2(const char* img, int lo, int hi) {
+  const s4v a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(img + lo));
+  const s4v b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(img + hi));
+  const i2v l = __builtin_bit_cast(i2v, a), hh = __builtin_bit_cast(i2v, b);
+  return i4v{l[0], l[1], hh[0], hh[1]};
+}
+
+// window geometry (G4 four-pixel groups per row, TH rows) as compile-time constants: the staging
+// address math divides by them
+template <typename T, int R, int G4, int TH>
+__global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, ConvWgradGeo g, float* __restrict__ ws,
+                                                           T* __restrict__ out) {
+  constexpr int P = (R - 1) / 2, RR = R * R;
+  constexpr int HC = 4 * G4 + 2 * P, KSTEPS = (TH * G4 + 3) / 4;
+  constexpr int XS = (TH + 2 * P) * HC, DS = KSTEPS * 16;  // X halo / dY pixel slots per window
+  constexpr int XP = (XS * kSlot + 1023) / 1024, DP = (DS * kSlot + 1023) / 1024;  // 1-KiB LDS-DMA pieces
+  constexpr int XPW = (XP + 3) / 4, DPW = (DP + 3) / 4;  // pieces per wave
+  static_assert(XS <= kMaxHalo && DS <= kMaxD, "window does not fit");
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
+  // XCD-aware placement: hardware deals workgroup ids round-robin over the 8 XCDs; consecutive
+  // logical ids (same window run, different tiles) land on one XCD so the run is read from one L2
+  const int b = blockIdx.x;
+  const int L = (b & 7) * (g.grid / 8) + (b >> 3);
+  if (L >= g.tiles * g.splits) return;  // grid padding (before any barrier)
+  const int tile = L % g.tiles, split = L / g.tiles;
+  const int k0 = (tile / g.ctiles) * kTile, c0 = (tile % g.ctiles) * kTile;
+  const int w_begin = split * g.wpw, w_end = min(g.nwin, w_begin + g.wpw);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kw = wave >> 1, cw = wave & 1;
+  const int C = a.C, K = a.K, H = a.H, W = a.W;
+  // whole-tensor buffer resources: a pixel outside the image (or a pad chunk) gets an offset past
+  // the range and lands in LDS as zeros (no clamped pointers, no select)
+  const i4v rsX = make_rsrc(a.x, (int64_t)a.N * H * W * C * 2);
+  const i4v rsD = make_rsrc(a.dy, (int64_t)a.N * H * W * K * 2);
+  constexpr int kOut = 0x7ff00000;  // any offset past both ranges
+  // LDS-DMA is lane-linear: lane l of piece j fills bytes [1024 j + 16 l, +16) = one 16-byte chunk
+  // of a pixel slot. The per-lane part of every piece's source offset is fixed for the kernel (the
+  // window only moves the image row): rel = byte offset from the window origin, hrow = the pixel's
+  // row in the window (kBad: pad chunk / past the slots / outside the image columns).
+  constexpr int NPW = XPW + DPW;  // this wave's pieces: X pieces first, then dY pieces
+  constexpr int kBad = -4096;
+  int rel[NPW], hrow[NPW];
+#pragma unroll
+  for (int i = 0; i < NPW; ++i) {
+    const bool isx = i < XPW;
+    const int piece = wave + 4 * (isx ? i : i - XPW);
+    const int byte = piece * 1024 + lane * 16, slot = byte / kSlot, ch = (byte - slot * kSlot) >> 4;
+    if (isx) {
+      const int hr = slot / HC, x = slot - hr * HC - P;
+      const bool ok = piece < XP && ch < 8 && slot < XS && x >= 0 && x < W;
+      rel[i] = (((hr - P) * W + x) * C + c0 + ch * 8) * 2;
+      hrow[i] = ok ? hr - P : kBad;
+    } else {
+      const int grp = slot >> 2, row = grp / G4, x = 4 * (grp - row * G4) + (slot & 3);
+      const bool ok = piece < DP && ch < 8 && slot < DS && row < TH && x < W;
+      rel[i] = ((row * W + x) * K + k0 + ch * 8) * 2;
+      hrow[i] = ok ? row : kBad;
+    }
+  }
+  // piece i of window (n, y0) into buffer buf (wave-uniform guard: waves own different piece counts)
+  auto issue_piece = [&](int i, int n, int y0, char* buf) {
+    const bool isx = i < XPW;
+    const int piece = wave + 4 * (isx ? i : i - XPW);
+    if (piece >= (isx ? XP : DP)) return;
+    const int y = y0 + hrow[i];
+    const bool ok = hrow[i] != kBad && y >= 0 && y < H;
+    const int off = ok ? (n * H + y0) * W * (isx ? C : K) * 2 + rel[i] : kOut;
+    if (isx) dma16(rsX, off, __builtin_amdgcn_readfirstlane(lds_addr(buf + piece * 1024)));
+    else dma16(rsD, off, __builtin_amdgcn_readfirstlane(lds_addr(buf + kBufX + piece * 1024)));
+  };
+  auto win_origin = [&](int win, int& n, int& y0) {
+    n = win / g.wpi;
+    y0 = (win - n * g.wpi) * TH;
+  };
+
+  // per-lane fragment addresses, fixed for the whole kernel. Transposed read: lane 4q + p of each
+  // 16-lane group names pixel q, columns 4p .. 4p+3 of its group's 16-column band; half h takes the
+  // k-step's pixel groups 2h, 2h + 1 (the MFMA's k = 8h .. 8h + 7).
+  const int g16 = lane >> 4, q = (lane & 15) >> 2, pc = lane & 3, h = lane >> 5;
+  const int colb = 2 * (16 * (g16 & 1) + 4 * pc);
+  const int a_off = (8 * h + q) * kSlot + 2 * 32 * kw + colb;  // dY: slot 16 ks + 8h + q (+4 for hi)
+  constexpr int ng = TH * G4;  // real groups; padded groups read zero dY (and clamped X)
+  int x_off[KSTEPS][2];        // X: slot of pixel q of groups 4 ks + 2h + j at shift (0, 0)
+#pragma unroll
+  for (int ks = 0; ks < KSTEPS; ++ks)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int grp = min(4 * ks + 2 * h + j, ng - 1), row = grp / G4;
+      x_off[ks][j] = (row * HC + 4 * (grp - row * G4) + q) * kSlot + 2 * 32 * cw + colb;
+    }
+
+  f16v acc[RR];
+#pragma unroll
+  for (int j = 0; j < RR; ++j)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+
+  if (w_begin < w_end) {
+    int n, y0;
+    win_origin(w_begin, n, y0);
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) issue_piece(i, n, y0, smem);
+  }
+  // fragments of k-step ks + 1 are read while the R*R MFMAs of ks run (two register sets, one read
+  // pair behind each MFMA, order pinned by sched_barrier): with one wave per SIMD this pipelining, not
+  // other waves, hides the LDS latency
+  i4v fa[2], fb[2][RR];
+  for (int win = w_begin; win < w_end; ++win) {
+    const char* xs = smem + ((win - w_begin) & 1) * kBuf;
+    const char* ds = xs + kBufX;
+    wait_vmcnt<0>();  // this wave's pieces of window `win` have landed ...
+    raw_barrier();    // ... and everyone's; everyone is also done reading the other buffer
+    // the next window's pieces are issued one behind each of the first MFMAs (their address math
+    // co-issues with the matrix cores instead of stalling in front of them)
+    const bool pre = win + 1 < w_end;
+    int nn = 0, ny0 = 0;
+    if (pre) win_origin(win + 1, nn, ny0);
+    char* nbuf = smem + ((win + 1 - w_begin) & 1) * kBuf;
+    auto read_a = [&](int ks, int buf) {
+      fa[buf] = frag2(ds + 16 * ks * kSlot, a_off, a_off + 4 * kSlot);
+    };
+    auto read_b = [&](int ks, int buf, int r, int s) {
+      const char* base = xs + (r * HC + s) * kSlot;
+      fb[buf][r * R + s] = frag2(base, x_off[ks][0], x_off[ks][1]);
+    };
+    read_a(0, 0);
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int s = 0; s < R; ++s) read_b(0, 0, r, s);
+#pragma unroll
+    for (int ks = 0; ks < KSTEPS; ++ks) {
+      const int cur = ks & 1, nxt = cur ^ 1;
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int s = 0; s < R; ++s) {
+          acc[r * R + s] = MfmaW<T>::run(fa[cur], fb[cur][r * R + s], acc[r * R + s]);
+          if (const int t = ks * RR + r * R + s; t < NPW && pre) issue_piece(t, nn, ny0, nbuf);
+          if (ks + 1 < KSTEPS) {
+            if (r == 0 && s == 0) read_a(ks + 1, nxt);
+            read_b(ks + 1, nxt, r, s);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+#pragma unroll
+    for (int t = KSTEPS * RR; t < NPW; ++t)  // pieces left over when a window has few MFMAs (R = 1)
+      if (pre) issue_piece(t, nn, ny0, nbuf);
+  }
+
+  // lane holds column c = c0 + 32 cw + (lane & 31) and rows k = k0 + 32 kw + 8 j + 4 h + i (acc[4 j + i])
+  const int c = c0 + 32 * cw + (lane & 31);
+#pragma unroll
+  for (int rs = 0; rs < RR; ++rs)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = k0 + 32 * kw + 8 * j + 4 * h + i;
+        const int64_t o = ((int64_t)k * RR + rs) * C + c;
+        if (g.splits == 1) out[o] = from_f<T>(acc[rs][4 * j + i]);
+        else ws[(int64_t)split * K * RR * C + o] = acc[rs][4 * j + i];
+      }
+}
+
+// out[i] = sum over splits of ws[s][i] (fixed order), 4 elements per thread
+template <typename T>
+__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ ws, T* __restrict__ out, int64_t n,
+                                                      int splits) {
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= n) return;
+  float4 s = *reinterpret_cast<const float4*>(ws + i);
+  for (int j = 1; j < splits; ++j) {
+    const float4 v = *reinterpret_cast<const float4*>(ws + (int64_t)j * n + i);
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  }
+  T o[4] = {from_f<T>(s.x), from_f<T>(s.y), from_f<T>(s.z), from_f<T>(s.w)};
+  *reinterpret_cast<uint2*>(out + i) = *reinterpret_cast<const uint2*>(o);
+}
+
+}  // namespace
+
+bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo) {
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (!(a.R == 1 || a.R == 3) || a.N <= 0 || a.H <= 0 || a.W <= 0 || a.C % kTile || a.K % kTile || !al(a.x) ||
+      !al(a.dy) || !al(a.out))
+    return false;
+  // 32-bit buffer offsets (the out-of-image offset sits past both tensors)
+  if (2 * (int64_t)a.N * a.H * a.W * std::max(a.C, a.K) >= 0x7ff00000ll) return false;
+  ConvWgradGeo g;
+  if (a.R == 1) {
+    // no halo: the N*H*W pixels are one flat list, 112-pixel windows (one row of 28 groups)
+    if (((int64_t)a.N * a.H * a.W) % 112) return false;
+    g.G4 = 28;
+    g.TH = 1;
+    g.wpi = 1;
+    g.nwin = (int)((int64_t)a.N * a.H * a.W / 112);
+  } else {
+    // ~112 pixels per window: 2 rows at W = 56, 4 at 28, 7 at 14 / 7 (the instantiated geometries)
+    g.G4 = (a.W + 3) / 4;
+    if (g.G4 == 14) g.TH = 2;
+    else if (g.G4 == 7) g.TH = 4;
+    else if (g.G4 == 4 || g.G4 == 2) g.TH = 7;
+    else return false;
+    g.wpi = (a.H + g.TH - 1) / g.TH;
+    g.nwin = a.N * g.wpi;
+  }
+  g.ksteps = (g.TH * g.G4 + 3) / 4;
+  g.ctiles = a.C / kTile;
+  g.tiles = (a.K / kTile) * g.ctiles;
+  // one round of workgroups (one per CU), split over the windows
+  int splits = std::max(1, 256 / g.tiles);
+  splits = std::min(splits, g.nwin);
+  g.wpw = (g.nwin + splits - 1) / splits;
+  g.splits = (g.nwin + g.wpw - 1) / g.wpw;
+  g.grid = (g.tiles * g.splits + 7) / 8 * 8;
+  *geo = g;
+  return true;
+}
+
+int64_t conv_wgrad_workspace(const ConvWgradGeo& g, const ConvWgradArgs& a) {
+  return g.splits > 1 ? (int64_t)g.splits * a.K * a.C * a.R * a.R : 0;
+}
+
+void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws, hipStream_t st) {
+  const int64_t n = (int64_t)a.K * a.C * a.R * a.R;
+  ConvWgradArgs b = a;
+  if (a.R == 1) {  // flat pixel list: windows are the rows of an [nwin, 1, 112] image
+    b.N = g.nwin;
+    b.H = 1;
+    b.W = 112;
+  }
+  auto run = [&](auto tt) {
+    using T = typename decltype(tt)::type;
+    T* out = reinterpret_cast<T*>(a.out);
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(g.grid), dim3(kThreads), 0, st, b, g, ws, out); };
+    if (a.R == 1) go(k_conv_wgrad<T, 1, 28, 1>);
+    else if (g.G4 == 14) go(k_conv_wgrad<T, 3, 14, 2>);
+    else if (g.G4 == 7) go(k_conv_wgrad<T, 3, 7, 4>);
+    else if (g.G4 == 4) go(k_conv_wgrad<T, 3, 4, 7>);
+    else go(k_conv_wgrad<T, 3, 2, 7>);
+    if (g.splits > 1)
+      hipLaunchKernelGGL(k_wgrad_reduce<T>, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, ws, out, n,
+                         g.splits);
+  };
+  switch (dt) {
+    case kF16: run(std::common_type<f16>{}); break;
+    case kBF16: run(std::common_type<bf16>{}); break;
+    default: throw std::runtime_error("conv_wgrad: fp16 / bf16 only");
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("conv_wgrad: ") + hipGetErrorString(e));
+}
+
+}  // namespace bh

@@ -48,6 +48,24 @@ def _pick(key, gemm_fn, miopen_fn, mode):
     return choice
 
 
+def _wgrad(x, gy, weight, r, mode, miopen_fn):
+    """Weight gradient of a stride-1 r x r conv: the MFMA kernel of kernels/conv_wgrad.hip or MIOpen,
+    per shape ("auto" times both once). Measured at ResNet-50 / batch 256: see
+    profiles/conv_wgrad_vs_miopen.jsonl."""
+    from ..ops import conv as bhconv
+
+    if mode == "miopen" or not bhconv.wgrad_supported(x, gy, r):
+        return miopen_fn()
+    n, c, h, w = x.shape
+    how = _pick((n, c, h, w, gy.size(1), x.dtype, f"wgrad{r}"), lambda: bhconv.conv_wgrad(x, gy, r), miopen_fn, mode)
+    if how != "gemm":
+        return miopen_fn()
+    gw = bhconv.conv_wgrad(x, gy, r)
+    return gw if gw.stride() == weight.stride() else gw.contiguous(memory_format=torch.channels_last
+                                                                    if weight.is_contiguous(memory_format=torch.channels_last)
+                                                                    else torch.contiguous_format)
+
+
 class _GradStash(torch.autograd.Function):
     """Identity in forward. In backward, the gradient arriving through this (second) use of a tensor
     is parked in ``box`` for the block's first 1x1 convolution, whose data-gradient GEMM then adds it
@@ -74,7 +92,7 @@ class _Conv1x1Fn(torch.autograd.Function):
     """1x1 / stride-1 convolution of a channels_last activation. Forward and data gradient run either
     as ONE hipBLASLt GEMM on the [N*H*W, C] view (no layout change) or as the MIOpen convolution,
     chosen per shape; the weight gradient -- a K = N*H*W split reduction that hipBLASLt handles badly
-    (1.0 vs 0.14 ms at 64->256 / 56x56) -- always runs on MIOpen."""
+    (1.0 vs 0.14 ms at 64->256 / 56x56) -- runs on the MFMA wgrad kernel or MIOpen (``_wgrad``)."""
 
     @staticmethod
     def forward(ctx, x, weight, mode, box=None):
@@ -125,7 +143,9 @@ class _Conv1x1Fn(torch.autograd.Function):
         if box is not None:
             box["conv_done"] = True
         if ctx.needs_input_grad[1]:
-            gw = conv_bwd(gy, x, weight, None, *args, [False, True, False])[1]
+            # 1x1: the MFMA wgrad kernel only through the timed per-shape choice (MIOpen wins most shapes)
+            gw = _wgrad(x, gy, weight, 1, "auto" if ctx.mode == "auto" else "miopen",
+                        lambda: conv_bwd(gy, x, weight, None, *args, [False, True, False])[1])
         return gx, gw, None, None
 
 
@@ -155,7 +175,7 @@ class _Conv3x3Fn(torch.autograd.Function):
     """3x3 / stride-1 / pad-1 convolution of a channels_last activation: forward and data gradient
     on the direct MFMA kernel (kernels/conv.hip; the data gradient is the same kernel on dY with the
     flipped, transposed weights) or on MIOpen, chosen per shape and direction ("auto" times both once);
-    the weight gradient runs on MIOpen. Measured at ResNet-50 / batch 256 (benchmarks/
+    the weight gradient likewise on the MFMA wgrad kernel (kernels/conv_wgrad.hip) or MIOpen. Measured at ResNet-50 / batch 256 (benchmarks/
     bench_conv3x3.py): forward 1.45 vs 1.96 ms, data gradient 1.59 vs 1.84 ms per step."""
 
     @staticmethod
@@ -190,7 +210,8 @@ class _Conv3x3Fn(torch.autograd.Function):
             else:
                 gx = conv_bwd(gy, x, weight, None, *args, [True, False, False])[0]
         if ctx.needs_input_grad[1]:
-            gw = conv_bwd(gy, x, weight, None, *args, [False, True, False])[1]
+            gw = _wgrad(x, gy, weight, 3, "gemm" if ctx.mode == "direct" else ctx.mode,
+                        lambda: conv_bwd(gy, x, weight, None, *args, [False, True, False])[1])
         return gx, gw, None
 
 

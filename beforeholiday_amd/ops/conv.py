@@ -34,3 +34,20 @@ def conv3x3_dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     if dy.is_cuda and available() and supported(dy, w.transpose(0, 1)):
         return submodule("conv_cuda").conv3x3_dgrad(dy, w)
     return F.conv2d(dy, dgrad_weight(w), stride=1, padding=1)
+
+
+def wgrad_supported(x: torch.Tensor, dy: torch.Tensor, r: int) -> bool:
+    return x.is_cuda and available() and submodule("conv_cuda").wgrad_supported(x, dy, r)
+
+
+def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, r: int) -> torch.Tensor:
+    """Weight gradient of ``conv2d(x, w, stride=1, padding=(r-1)//2)`` for r in {1, 3}: the MFMA
+    kernel of kernels/conv_wgrad.hip (both operands read through LDS transposes, fp32 split partials
+    summed in a fixed order) for channels_last fp16 / bf16 with C, K multiples of 64; otherwise
+    ``torch.ops.aten.convolution_backward``. Returns [K, C, r, r] (channels_last on the kernel path)."""
+    if wgrad_supported(x, dy, r):
+        return submodule("conv_cuda").conv_wgrad(x, dy, r)
+    w_shape = [dy.size(1), x.size(1), r, r]
+    p = (r - 1) // 2
+    return torch.ops.aten.convolution_backward(dy, x, torch.empty(w_shape, device=x.device, dtype=x.dtype), None,
+                                               [1, 1], [p, p], [1, 1], False, [0, 0], 1, [False, True, False])[1]

@@ -29,6 +29,10 @@ def main():
                     name = "attn_fwd"
                 elif "attn_bwd" in name:
                     name = "attn_bwd"
+                elif "k_conv_wgrad" in name:
+                    geo = {"Li14ELi2E": "56x56", "Li7ELi4E": "28x28", "Li4ELi7E": "14x14", "Li2ELi7E": "7x7",
+                           "Li28ELi1E": "1x1"}
+                    name = "conv_wgrad<" + next((v for k, v in geo.items() if k in name), "?") + ">"
                 else:
                     continue
                 vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))

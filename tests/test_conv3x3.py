@@ -70,6 +70,52 @@ def test_conv3x3_module_grads_match_miopen(mode):
     yb.backward(g)
     torch.testing.assert_close(ya.float(), yb.float(), rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(xa.grad.float(), xb.grad.float(), rtol=2e-2, atol=2e-2)
-    # both weight gradients are MIOpen's (fp16 split-K accumulation, order not fixed): compare to scale
+    # the weight gradient is the MFMA wgrad kernel ("direct") or the faster of it and MIOpen ("auto"); MIOpen
+    # accumulates split-K partials in an unfixed order: compare to scale
     wr = ref.weight.grad.float()
     torch.testing.assert_close(m.weight.grad.float(), wr, rtol=5e-2, atol=1e-2 * wr.abs().max().item())
+
+
+WGRAD_SHAPES = [  # N, C, K, H, W, R
+    (2, 64, 64, 56, 56, 3), (3, 128, 128, 28, 28, 3), (5, 256, 64, 14, 14, 3), (7, 64, 128, 7, 7, 3),
+    (9, 64, 64, 16, 16, 3), (3, 64, 192, 13, 13, 3), (4, 128, 64, 5, 5, 3),
+    (2, 64, 256, 56, 56, 1), (4, 256, 128, 14, 14, 1), (1, 64, 64, 7, 16, 1),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("shape", WGRAD_SHAPES)
+def test_conv_wgrad_kernel(dtype, shape):
+    """kernels/conv_wgrad.hip vs fp32 torch.nn.grad.conv2d_weight: 56/28/14/7-wide windows, ragged
+    widths (13, 5), partial row windows, single-split (direct store) and multi-split (reduce) launches."""
+    N, C, K, H, W, R = shape
+    g = torch.Generator(device="cuda").manual_seed(N * 100 + C + K + H + R)
+    x = torch.randn(N, C, H, W, device="cuda", dtype=dtype, generator=g).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(N, K, H, W, device="cuda", dtype=dtype, generator=g).contiguous(memory_format=torch.channels_last)
+    assert bhconv.wgrad_supported(x, dy, R)
+    gw = bhconv.conv_wgrad(x, dy, R)
+    assert gw.shape == (K, C, R, R) and gw.dtype == dtype
+    ref = torch.nn.grad.conv2d_weight(x.float(), (K, C, R, R), dy.float(), stride=1, padding=(R - 1) // 2)
+    scale = ref.abs().max().item()
+    tol = 1e-2 if dtype == torch.float16 else 2e-2
+    torch.testing.assert_close(gw.float(), ref, rtol=tol, atol=tol * scale)
+    # bitwise reproducible (fixed-order split reduction)
+    assert torch.equal(gw, bhconv.conv_wgrad(x, dy, R))
+
+
+@pytest.mark.gpu
+def test_conv_wgrad_fallback_shapes():
+    """Widths without an instantiated window geometry (W = 20 -> 5 groups) and 1x1 pixel counts that
+    are not a multiple of 112 report unsupported and take the convolution_backward path."""
+    x = torch.randn(2, 64, 9, 20, device="cuda", dtype=torch.half).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(2, 64, 9, 20, device="cuda", dtype=torch.half).contiguous(memory_format=torch.channels_last)
+    assert not bhconv.wgrad_supported(x, dy, 3)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (64, 64, 3, 3), dy.float(), stride=1, padding=1)
+    torch.testing.assert_close(bhconv.conv_wgrad(x, dy, 3).float(), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item())
+    x1 = x[:, :, :5, :5].contiguous(memory_format=torch.channels_last)
+    dy1 = dy[:, :, :5, :5].contiguous(memory_format=torch.channels_last)
+    assert not bhconv.wgrad_supported(x1, dy1, 1)
+    ref1 = torch.nn.grad.conv2d_weight(x1.float(), (64, 64, 1, 1), dy1.float())
+    torch.testing.assert_close(bhconv.conv_wgrad(x1, dy1, 1).float(), ref1, rtol=2e-2,
+                               atol=2e-2 * ref1.abs().max().item())
