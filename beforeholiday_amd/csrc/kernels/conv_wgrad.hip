@@ -8,12 +8,13 @@
 // a list of 4-pixel groups along image rows, so a 14- or 7-wide image wastes at most one group column
 // instead of padding rows to 32.
 //
-// Workgroup = 4 waves = a 64 (k) x 64 (c) tile of all R*R offsets: wave (kw, cw) owns one 32x32
-// accumulator per offset (144 fp32 AGPRs at R = 3), one workgroup per CU. A window is TH whole image
+// Workgroup = 8 waves = a 64 (k) x 64 (c) tile of all R*R offsets, one workgroup per CU: the two
+// waves of a SIMD share a 32x32 (k, c) quadrant and split its R*R offsets (5 + 4 accumulators at
+// R = 3), so each SIMD runs two waves that cover each other's waits. A window is TH whole image
 // rows: its dY (TH x 4*G4 pixels, zero past the image) and the X halo ((TH + 2P) x (4*G4 + 2P)
 // pixels, zero outside the image) land in LDS by LDS-DMA (buffer loads through whole-tensor
 // resources: an out-of-image pixel gets an out-of-range offset and arrives as zeros), double
-// buffered (138 KiB: 192-byte pixel slots, see kSlot). Every k-step reads one dY
+// buffered (up to 141 KiB: padded pixel slots, see kSlot). Every k-step reads one dY
 // fragment and reuses it for the R*R shifted X fragments; the next k-step's fragments are read
 // behind the current MFMAs. Each workgroup walks a contiguous run of windows and writes an fp32
 // partial tile; a second kernel sums the splits in a fixed order into the 16-bit weight gradient
@@ -50,7 +51,7 @@ template <> struct MfmaW<bf16> {
   }
 };
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 512;   // 8 waves: two per SIMD
 constexpr int kTile = 64;        // k and c per workgroup
 // LDS bytes per pixel slot: 64 channels x 2 B + 64 B pad. At a 48-dword stride any four consecutive
 // slots start in four distinct 16-dword bank quarters, so the transposed reads (4 pixels x 64 B per
@@ -59,8 +60,9 @@ constexpr int kTile = 64;        // k and c per workgroup
 constexpr int kSlot = 192;
 constexpr int kMaxHalo = 240;    // X slots per window
 constexpr int kMaxD = 128;       // dY slots per window (k-steps x 16)
-constexpr int kBufX = kMaxHalo * kSlot;
-constexpr int kBuf = (kMaxHalo + kMaxD) * kSlot;  // one window buffer (two: 138 KiB)
+// dY slots hold 64 * KT channels: 128 + 64 B (KT = 1) or 256 + 64 B (KT = 2, again four distinct
+// bank quarters for four consecutive slots)
+template <int KT> constexpr int dslot() { return KT == 1 ? 192 : 320; }
 constexpr unsigned kRsrcWord3 = 0x00020000u;
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -105,28 +107,33 @@ BH_DEVICE i4v frag2(const char* img, int lo, int hi) {
 
 // window geometry (G4 four-pixel groups per row, TH rows) as compile-time constants: the staging
 // address math divides by them
-template <typename T, int R, int G4, int TH>
+template <typename T, int R, int G4, int TH, int KT>
 __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, ConvWgradGeo g, float* __restrict__ ws,
                                                            T* __restrict__ out) {
   constexpr int P = (R - 1) / 2, RR = R * R;
   constexpr int HC = 4 * G4 + 2 * P, KSTEPS = (TH * G4 + 3) / 4;
   constexpr int XS = (TH + 2 * P) * HC, DS = KSTEPS * 16;  // X halo / dY pixel slots per window
-  constexpr int XP = (XS * kSlot + 1023) / 1024, DP = (DS * kSlot + 1023) / 1024;  // 1-KiB LDS-DMA pieces
-  constexpr int XPW = (XP + 3) / 4, DPW = (DP + 3) / 4;  // pieces per wave
+  constexpr int DSL = dslot<KT>(), TK = kTile * KT;  // dY slot bytes, output channels per workgroup
+  constexpr int BUFX = (XS * kSlot + 1023) / 1024 * 1024, BUF = BUFX + (DS * DSL + 1023) / 1024 * 1024;
+  constexpr int XP = BUFX / 1024, DP = (BUF - BUFX) / 1024;  // 1-KiB LDS-DMA pieces
+  constexpr int XPW = (XP + 7) / 8, DPW = (DP + 7) / 8;  // pieces per wave
+  constexpr int NOFF = (RR + 1) / 2;  // offsets per wave: the two waves of a SIMD split the R*R offsets
   static_assert(XS <= kMaxHalo && DS <= kMaxD, "window does not fit");
-  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
+  static_assert(2 * BUF <= 160 * 1024, "two window buffers must fit in LDS");
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
   // XCD-aware placement: hardware deals workgroup ids round-robin over the 8 XCDs; consecutive
   // logical ids (same window run, different tiles) land on one XCD so the run is read from one L2
   const int b = blockIdx.x;
   const int L = (b & 7) * (g.grid / 8) + (b >> 3);
   if (L >= g.tiles * g.splits) return;  // grid padding (before any barrier)
   const int tile = L % g.tiles, split = L / g.tiles;
-  const int k0 = (tile / g.ctiles) * kTile, c0 = (tile % g.ctiles) * kTile;
+  const int k0 = (tile / g.ctiles) * TK, c0 = (tile % g.ctiles) * kTile;
   const int w_begin = split * g.wpw, w_end = min(g.nwin, w_begin + g.wpw);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int kw = wave >> 1, cw = wave & 1;
+  const int kw = (wave >> 1) & 1, cw = wave & 1, half = wave >> 2;
+  const int rs0 = half * NOFF, noff = min(NOFF, RR - rs0);  // this wave's offsets rs0 .. rs0 + noff - 1
   const int C = a.C, K = a.K, H = a.H, W = a.W;
   // whole-tensor buffer resources: a pixel outside the image (or a pad chunk) gets an offset past
   // the range and lands in LDS as zeros (no clamped pointers, no select)
@@ -143,7 +150,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
 #pragma unroll
   for (int i = 0; i < NPW; ++i) {
     const bool isx = i < XPW;
-    const int piece = wave + 4 * (isx ? i : i - XPW);
+    const int piece = wave + 8 * (isx ? i : i - XPW);
     const int byte = piece * 1024 + lane * 16, slot = byte / kSlot, ch = (byte - slot * kSlot) >> 4;
     if (isx) {
       const int hr = slot / HC, x = slot - hr * HC - P;
@@ -151,22 +158,23 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
       rel[i] = (((hr - P) * W + x) * C + c0 + ch * 8) * 2;
       hrow[i] = ok ? hr - P : kBad;
     } else {
-      const int grp = slot >> 2, row = grp / G4, x = 4 * (grp - row * G4) + (slot & 3);
-      const bool ok = piece < DP && ch < 8 && slot < DS && row < TH && x < W;
-      rel[i] = ((row * W + x) * K + k0 + ch * 8) * 2;
+      const int dbyte = byte, dsl = dbyte / DSL, dch = (dbyte - dsl * DSL) >> 4;
+      const int grp = dsl >> 2, row = grp / G4, x = 4 * (grp - row * G4) + (dsl & 3);
+      const bool ok = piece < DP && dch < 8 * KT && dsl < DS && row < TH && x < W;
+      rel[i] = ((row * W + x) * K + k0 + dch * 8) * 2;
       hrow[i] = ok ? row : kBad;
     }
   }
   // piece i of window (n, y0) into buffer buf (wave-uniform guard: waves own different piece counts)
   auto issue_piece = [&](int i, int n, int y0, char* buf) {
     const bool isx = i < XPW;
-    const int piece = wave + 4 * (isx ? i : i - XPW);
+    const int piece = wave + 8 * (isx ? i : i - XPW);
     if (piece >= (isx ? XP : DP)) return;
     const int y = y0 + hrow[i];
     const bool ok = hrow[i] != kBad && y >= 0 && y < H;
     const int off = ok ? (n * H + y0) * W * (isx ? C : K) * 2 + rel[i] : kOut;
     if (isx) dma16(rsX, off, __builtin_amdgcn_readfirstlane(lds_addr(buf + piece * 1024)));
-    else dma16(rsD, off, __builtin_amdgcn_readfirstlane(lds_addr(buf + kBufX + piece * 1024)));
+    else dma16(rsD, off, __builtin_amdgcn_readfirstlane(lds_addr(buf + BUFX + piece * 1024)));
   };
   auto win_origin = [&](int win, int& n, int& y0) {
     n = win / g.wpi;
@@ -178,7 +186,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
   // k-step's pixel groups 2h, 2h + 1 (the MFMA's k = 8h .. 8h + 7).
   const int g16 = lane >> 4, q = (lane & 15) >> 2, pc = lane & 3, h = lane >> 5;
   const int colb = 2 * (16 * (g16 & 1) + 4 * pc);
-  const int a_off = (8 * h + q) * kSlot + 2 * 32 * kw + colb;  // dY: slot 16 ks + 8h + q (+4 for hi)
+  const int a_off = (8 * h + q) * DSL + 2 * 32 * KT * kw + colb;  // dY: slot 16 ks + 8h + q (+4 for hi)
   constexpr int ng = TH * G4;  // real groups; padded groups read zero dY (and clamped X)
   int x_off[KSTEPS][2];        // X: slot of pixel q of groups 4 ks + 2h + j at shift (0, 0)
 #pragma unroll
@@ -189,11 +197,13 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
       x_off[ks][j] = (row * HC + 4 * (grp - row * G4) + q) * kSlot + 2 * 32 * cw + colb;
     }
 
-  f16v acc[RR];
+  f16v acc[NOFF][KT];
 #pragma unroll
-  for (int j = 0; j < RR; ++j)
+  for (int j = 0; j < NOFF; ++j)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[j][i] = 0.f;
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[j][t][i] = 0.f;
 
   if (w_begin < w_end) {
     int n, y0;
@@ -201,13 +211,12 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
 #pragma unroll
     for (int i = 0; i < NPW; ++i) issue_piece(i, n, y0, smem);
   }
-  // fragments of k-step ks + 1 are read while the R*R MFMAs of ks run (two register sets, one read
-  // pair behind each MFMA, order pinned by sched_barrier): with one wave per SIMD this pipelining, not
-  // other waves, hides the LDS latency
-  i4v fa[2], fb[2][RR];
+  // fragments of k-step ks + 1 are read while the MFMAs of ks run (two register sets, one read pair
+  // behind each MFMA, order pinned by sched_barrier)
+  i4v fa[2][KT], fb[2][NOFF];
   for (int win = w_begin; win < w_end; ++win) {
-    const char* xs = smem + ((win - w_begin) & 1) * kBuf;
-    const char* ds = xs + kBufX;
+    const char* xs = smem + ((win - w_begin) & 1) * BUF;
+    const char* ds = xs + BUFX;
     wait_vmcnt<0>();  // this wave's pieces of window `win` have landed ...
     raw_barrier();    // ... and everyone's; everyone is also done reading the other buffer
     // the next window's pieces are issued one behind each of the first MFMAs (their address math
@@ -215,71 +224,95 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
     const bool pre = win + 1 < w_end;
     int nn = 0, ny0 = 0;
     if (pre) win_origin(win + 1, nn, ny0);
-    char* nbuf = smem + ((win + 1 - w_begin) & 1) * kBuf;
+    char* nbuf = smem + ((win + 1 - w_begin) & 1) * BUF;
     auto read_a = [&](int ks, int buf) {
-      fa[buf] = frag2(ds + 16 * ks * kSlot, a_off, a_off + 4 * kSlot);
+#pragma unroll
+      for (int t = 0; t < KT; ++t) fa[buf][t] = frag2(ds + 16 * ks * DSL + 64 * t, a_off, a_off + 4 * DSL);
     };
-    auto read_b = [&](int ks, int buf, int r, int s) {
+    // offset j of this wave: rs = rs0 + j = r * R + s, LDS shift (r * HC + s) slots (wave-uniform
+    // branch: the half-1 waves of an odd R*R own one offset fewer)
+    auto read_b = [&](int ks, int buf, int j) {
+      const int rs = rs0 + j, r = rs / R, s = rs - r * R;
       const char* base = xs + (r * HC + s) * kSlot;
-      fb[buf][r * R + s] = frag2(base, x_off[ks][0], x_off[ks][1]);
+      fb[buf][j] = frag2(base, x_off[ks][0], x_off[ks][1]);
     };
     read_a(0, 0);
 #pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-      for (int s = 0; s < R; ++s) read_b(0, 0, r, s);
+    for (int j = 0; j < NOFF; ++j)
+      if (j < noff) read_b(0, 0, j);
 #pragma unroll
     for (int ks = 0; ks < KSTEPS; ++ks) {
       const int cur = ks & 1, nxt = cur ^ 1;
 #pragma unroll
-      for (int r = 0; r < R; ++r)
+      for (int j = 0; j < NOFF; ++j) {
+        if (j < noff)
 #pragma unroll
-        for (int s = 0; s < R; ++s) {
-          acc[r * R + s] = MfmaW<T>::run(fa[cur], fb[cur][r * R + s], acc[r * R + s]);
-          if (const int t = ks * RR + r * R + s; t < NPW && pre) issue_piece(t, nn, ny0, nbuf);
-          if (ks + 1 < KSTEPS) {
-            if (r == 0 && s == 0) read_a(ks + 1, nxt);
-            read_b(ks + 1, nxt, r, s);
-          }
-          __builtin_amdgcn_sched_barrier(0);
+          for (int t = 0; t < KT; ++t) acc[j][t] = MfmaW<T>::run(fa[cur][t], fb[cur][j], acc[j][t]);
+        if (const int t = ks * NOFF + j; t < NPW && pre) issue_piece(t, nn, ny0, nbuf);
+        if (ks + 1 < KSTEPS) {
+          if (j == 0) read_a(ks + 1, nxt);
+          if (j < noff) read_b(ks + 1, nxt, j);
         }
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
 #pragma unroll
-    for (int t = KSTEPS * RR; t < NPW; ++t)  // pieces left over when a window has few MFMAs (R = 1)
+    for (int t = KSTEPS * NOFF; t < NPW; ++t)  // pieces left over when a window has few MFMAs (R = 1)
       if (pre) issue_piece(t, nn, ny0, nbuf);
   }
 
   // lane holds column c = c0 + 32 cw + (lane & 31) and rows k = k0 + 32 kw + 8 j + 4 h + i (acc[4 j + i])
   const int c = c0 + 32 * cw + (lane & 31);
 #pragma unroll
-  for (int rs = 0; rs < RR; ++rs)
+  for (int jo = 0; jo < NOFF; ++jo) {
+    if (jo >= noff) break;
+    const int rs = rs0 + jo;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int t = 0; t < KT; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int k = k0 + 32 * kw + 8 * j + 4 * h + i;
-        const int64_t o = ((int64_t)k * RR + rs) * C + c;
-        if (g.splits == 1) out[o] = from_f<T>(acc[rs][4 * j + i]);
-        else ws[(int64_t)split * K * RR * C + o] = acc[rs][4 * j + i];
-      }
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = k0 + 32 * KT * kw + 32 * t + 8 * j + 4 * h + i;
+          const int64_t o = ((int64_t)k * RR + rs) * C + c;
+          if (g.splits == 1) out[o] = from_f<T>(acc[jo][t][4 * j + i]);
+          else ws[(int64_t)split * K * RR * C + o] = acc[jo][t][4 * j + i];
+        }
+  }
 }
 
-// out[i] = sum over splits of ws[s][i] (fixed order), 4 elements per thread
+// out[i] = sum over splits of ws[s][i] in a fixed order: a block owns 64 elements (16 float4 quads)
+// x 16 split groups; group g sums splits g, g + 16, ... and the groups are added in order through
+// LDS (deterministic, and 16x the workgroups of a one-thread-per-quad loop over 256 splits)
 template <typename T>
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ ws, T* __restrict__ out, int64_t n,
                                                       int splits) {
-  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-  if (i >= n) return;
-  float4 s = *reinterpret_cast<const float4*>(ws + i);
-  for (int j = 1; j < splits; ++j) {
-    const float4 v = *reinterpret_cast<const float4*>(ws + (int64_t)j * n + i);
-    s.x += v.x;
-    s.y += v.y;
-    s.z += v.z;
-    s.w += v.w;
+  __shared__ float4 part[16][16];
+  const int tq = threadIdx.x & 15, sg = threadIdx.x >> 4;
+  const int64_t i = ((int64_t)blockIdx.x * 16 + tq) * 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n)
+    for (int j = sg; j < splits; j += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(ws + (int64_t)j * n + i);
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+  part[sg][tq] = acc;
+  __syncthreads();
+  if (sg == 0 && i < n) {
+    float4 t = part[0][tq];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) {
+      t.x += part[k][tq].x;
+      t.y += part[k][tq].y;
+      t.z += part[k][tq].z;
+      t.w += part[k][tq].w;
+    }
+    T o[4] = {from_f<T>(t.x), from_f<T>(t.y), from_f<T>(t.z), from_f<T>(t.w)};
+    *reinterpret_cast<uint2*>(out + i) = *reinterpret_cast<const uint2*>(o);
   }
-  T o[4] = {from_f<T>(s.x), from_f<T>(s.y), from_f<T>(s.z), from_f<T>(s.w)};
-  *reinterpret_cast<uint2*>(out + i) = *reinterpret_cast<const uint2*>(o);
 }
 
 }  // namespace
@@ -310,8 +343,11 @@ bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo) {
     g.nwin = a.N * g.wpi;
   }
   g.ksteps = (g.TH * g.G4 + 3) / 4;
+  // 128 output channels per workgroup (each wave two k sub-tiles sharing its X fragments) for the
+  // 14- / 7-wide windows (measured 1.1x there; the 28-wide instantiation spills and is slower)
+  g.kt = (a.K % 128 == 0 && a.R == 3 && (g.G4 == 4 || g.G4 == 2)) ? 2 : 1;
   g.ctiles = a.C / kTile;
-  g.tiles = (a.K / kTile) * g.ctiles;
+  g.tiles = (a.K / (kTile * g.kt)) * g.ctiles;
   // one round of workgroups (one per CU), split over the windows
   int splits = std::max(1, 256 / g.tiles);
   splits = std::min(splits, g.nwin);
@@ -338,14 +374,13 @@ void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws
     using T = typename decltype(tt)::type;
     T* out = reinterpret_cast<T*>(a.out);
     auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(g.grid), dim3(kThreads), 0, st, b, g, ws, out); };
-    if (a.R == 1) go(k_conv_wgrad<T, 1, 28, 1>);
-    else if (g.G4 == 14) go(k_conv_wgrad<T, 3, 14, 2>);
-    else if (g.G4 == 7) go(k_conv_wgrad<T, 3, 7, 4>);
-    else if (g.G4 == 4) go(k_conv_wgrad<T, 3, 4, 7>);
-    else go(k_conv_wgrad<T, 3, 2, 7>);
+    if (a.R == 1) go(k_conv_wgrad<T, 1, 28, 1, 1>);
+    else if (g.G4 == 14) go(k_conv_wgrad<T, 3, 14, 2, 1>);
+    else if (g.G4 == 7) go(k_conv_wgrad<T, 3, 7, 4, 1>);
+    else if (g.G4 == 4) g.kt == 2 ? go(k_conv_wgrad<T, 3, 4, 7, 2>) : go(k_conv_wgrad<T, 3, 4, 7, 1>);
+    else g.kt == 2 ? go(k_conv_wgrad<T, 3, 2, 7, 2>) : go(k_conv_wgrad<T, 3, 2, 7, 1>);
     if (g.splits > 1)
-      hipLaunchKernelGGL(k_wgrad_reduce<T>, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, ws, out, n,
-                         g.splits);
+      hipLaunchKernelGGL(k_wgrad_reduce<T>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, ws, out, n, g.splits);
   };
   switch (dt) {
     case kF16: run(std::common_type<f16>{}); break;

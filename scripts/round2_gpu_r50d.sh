@@ -1,0 +1,6 @@
+# wgrad numerics + bench table, headline bench, ResNet-50 kernel summary with the MFMA wgrad
+bash scripts/gpu_steps.sh \
+ "twgrad:240:python -u -m pytest tests/test_conv3x3.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider" \
+ "bwgrad:240:python benchmarks/bench_conv_wgrad.py" \
+ "bench:400:python bench.py --steps 20 --warmup 5" \
+ "prof:300:cd /tmp && export TMPDIR=/tmp && cd \$GRAFT_REPO_ROOT && rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r50 -o run -- python bench.py --steps 8 --warmup 5 && python scripts/prof_summary.py gpurun_out/prof_r50 k_lamb2 3 gpurun_out/r50_summary.md && rm -rf gpurun_out/prof_r50"
