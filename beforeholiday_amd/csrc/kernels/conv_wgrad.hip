@@ -133,7 +133,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kw = (wave >> 1) & 1, cw = wave & 1, half = wave >> 2;
-  const int rs0 = half * NOFF, noff = min(NOFF, RR - rs0);  // this wave's offsets rs0 .. rs0 + noff - 1
+  // R = 3: the two waves of a SIMD split the offsets (rs0 .. rs0 + noff - 1); R = 1 (one offset):
+  // they split the k-steps instead (half h takes ks = h, h + 2, ...) and write separate partials
+  const int rs0 = R == 1 ? 0 : half * NOFF, noff = R == 1 ? 1 : min(NOFF, RR - rs0);
   const int C = a.C, K = a.K, H = a.H, W = a.W;
   // whole-tensor buffer resources: a pixel outside the image (or a pad chunk) gets an offset past
   // the range and lands in LDS as zeros (no clamped pointers, no select)
@@ -236,6 +238,31 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
       const char* base = xs + (r * HC + s) * kSlot;
       fb[buf][j] = frag2(base, x_off[ks][0], x_off[ks][1]);
     };
+    if constexpr (R == 1) {
+      // k-step ks = 2u + half; the X slots of a flat 1x1 window are linear in ks
+      constexpr int KL = (KSTEPS + 1) / 2;
+      auto rd = [&](int u, int buf) {
+        const int ks = 2 * u + half;
+#pragma unroll
+        for (int t = 0; t < KT; ++t) fa[buf][t] = frag2(ds + 16 * ks * DSL + 64 * t, a_off, a_off + 4 * DSL);
+        fb[buf][0] = frag2(xs + 16 * ks * kSlot, x_off[0][0], x_off[0][1]);
+      };
+#pragma unroll
+      for (int t = 0; t < NPW; ++t)  // the next window's pieces first: they have the whole window to land
+        if (pre) issue_piece(t, nn, ny0, nbuf);
+      rd(0, 0);
+#pragma unroll
+      for (int u = 0; u < KL; ++u) {
+        const int cur = u & 1;
+        if (2 * u + half < KSTEPS) {
+#pragma unroll
+          for (int t = 0; t < KT; ++t) acc[0][t] = MfmaW<T>::run(fa[cur][t], fb[cur][0], acc[0][t]);
+        }
+        if (u + 1 < KL && 2 * (u + 1) + half < KSTEPS) rd(u + 1, cur ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      continue;
+    }
     read_a(0, 0);
 #pragma unroll
     for (int j = 0; j < NOFF; ++j)
@@ -275,8 +302,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
         for (int i = 0; i < 4; ++i) {
           const int k = k0 + 32 * KT * kw + 32 * t + 8 * j + 4 * h + i;
           const int64_t o = ((int64_t)k * RR + rs) * C + c;
-          if (g.splits == 1) out[o] = from_f<T>(acc[jo][t][4 * j + i]);
-          else ws[(int64_t)split * K * RR * C + o] = acc[jo][t][4 * j + i];
+          if (g.parts == 1) out[o] = from_f<T>(acc[jo][t][4 * j + i]);
+          else ws[(int64_t)(R == 1 ? 2 * split + half : split) * K * RR * C + o] = acc[jo][t][4 * j + i];
         }
   }
 }
@@ -345,7 +372,7 @@ bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo) {
   g.ksteps = (g.TH * g.G4 + 3) / 4;
   // 128 output channels per workgroup (each wave two k sub-tiles sharing its X fragments) for the
   // 14- / 7-wide windows (measured 1.1x there; the 28-wide instantiation spills and is slower)
-  g.kt = (a.K % 128 == 0 && a.R == 3 && (g.G4 == 4 || g.G4 == 2)) ? 2 : 1;
+  g.kt = (a.K % 128 == 0 && (a.R == 1 || g.G4 == 4 || g.G4 == 2)) ? 2 : 1;
   g.ctiles = a.C / kTile;
   g.tiles = (a.K / (kTile * g.kt)) * g.ctiles;
   // one round of workgroups (one per CU), split over the windows
@@ -353,13 +380,14 @@ bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo) {
   splits = std::min(splits, g.nwin);
   g.wpw = (g.nwin + splits - 1) / splits;
   g.splits = (g.nwin + g.wpw - 1) / g.wpw;
+  g.parts = g.splits * (a.R == 1 ? 2 : 1);
   g.grid = (g.tiles * g.splits + 7) / 8 * 8;
   *geo = g;
   return true;
 }
 
 int64_t conv_wgrad_workspace(const ConvWgradGeo& g, const ConvWgradArgs& a) {
-  return g.splits > 1 ? (int64_t)g.splits * a.K * a.C * a.R * a.R : 0;
+  return g.parts > 1 ? (int64_t)g.parts * a.K * a.C * a.R * a.R : 0;
 }
 
 void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws, hipStream_t st) {
@@ -374,13 +402,13 @@ void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws
     using T = typename decltype(tt)::type;
     T* out = reinterpret_cast<T*>(a.out);
     auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(g.grid), dim3(kThreads), 0, st, b, g, ws, out); };
-    if (a.R == 1) go(k_conv_wgrad<T, 1, 28, 1, 1>);
+    if (a.R == 1) g.kt == 2 ? go(k_conv_wgrad<T, 1, 28, 1, 2>) : go(k_conv_wgrad<T, 1, 28, 1, 1>);
     else if (g.G4 == 14) go(k_conv_wgrad<T, 3, 14, 2, 1>);
     else if (g.G4 == 7) go(k_conv_wgrad<T, 3, 7, 4, 1>);
     else if (g.G4 == 4) g.kt == 2 ? go(k_conv_wgrad<T, 3, 4, 7, 2>) : go(k_conv_wgrad<T, 3, 4, 7, 1>);
     else g.kt == 2 ? go(k_conv_wgrad<T, 3, 2, 7, 2>) : go(k_conv_wgrad<T, 3, 2, 7, 1>);
-    if (g.splits > 1)
-      hipLaunchKernelGGL(k_wgrad_reduce<T>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, ws, out, n, g.splits);
+    if (g.parts > 1)
+      hipLaunchKernelGGL(k_wgrad_reduce<T>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, ws, out, n, g.parts);
   };
   switch (dt) {
     case kF16: run(std::common_type<f16>{}); break;
