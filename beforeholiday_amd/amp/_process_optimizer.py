@@ -78,6 +78,22 @@ def lazy_init_with_master_weights(self):
 
 
 def post_backward_models_are_masters(scaler, params, stashed_grads, scale_override=None):
+    if getattr(scaler, "device_mode", False) and scale_override is None:
+        # device-resident scale (LossScaler.enable_device_mode): plain unscale without reading it
+        need_unscale, keep = [], False
+        for i, (param, stashed_grad) in enumerate(zip(params, stashed_grads)):
+            if param.grad is None and stashed_grad is not None:
+                param.grad = stashed_grad
+            elif param.grad is not None and stashed_grad is None:
+                need_unscale.append(param.grad)
+            elif param.grad is not None and stashed_grad is not None:
+                keep = True  # accumulation into stashed grads: the host-scale path below
+        if not keep:
+            if need_unscale:
+                scaler.unscale(need_unscale, need_unscale, None, models_are_masters=True)
+            for i in range(len(stashed_grads)):
+                stashed_grads[i] = None
+            return
     grads_have_scale, stashed_have_scale, out_scale = scaler.loss_scale(), 1.0, 1.0
     # not much to do if scale == 1.0 and static scaling
     if scaler.loss_scale() == 1.0 and not scaler.dynamic:
@@ -131,7 +147,7 @@ def post_backward_with_master_weights(self, scaler):
             fp16_unscale_stash.append(fp16_param.grad)
             preexisting.append(fp32_param.grad)
     if fp16_unscale:
-        scaler.unscale(fp16_unscale, new_fp32, scaler.loss_scale(), models_are_masters=False)
+        scaler.unscale(fp16_unscale, new_fp32, None, models_are_masters=False)
     if fp16_unscale_stash:
         scaler.unscale_with_stashed(fp16_unscale_stash, preexisting, preexisting)
     post_backward_models_are_masters(scaler, stash.all_fp32_from_fp32_params, stash.all_fp32_from_fp32_grad_stash)

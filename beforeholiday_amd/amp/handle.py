@@ -9,6 +9,20 @@ from ._amp_state import _amp_state, maybe_print
 from .scaler import LossScaler
 
 
+def _device_scaler_wanted(loss_scaler, optimizers):
+    """BH_AMP_DEVICE_SCALER=1, dynamic scaling, the fused unscale kernel, a CUDA loss, and only fused
+    optimizers whose kernels return early on a set noop flag (``_dummy_overflow_buf``): FusedLAMB
+    (both stages) and FusedSGD."""
+    import os
+
+    from ..optimizers import FusedLAMB, FusedSGD
+
+    return (os.environ.get("BH_AMP_DEVICE_SCALER", "0") == "1" and loss_scaler.dynamic
+            and LossScaler.has_fused_kernel and torch.cuda.is_available()
+            and all(isinstance(o, (FusedLAMB, FusedSGD)) and hasattr(o, "_dummy_overflow_buf")
+                    for o in optimizers))
+
+
 @contextlib.contextmanager
 def scale_loss(loss, optimizers, loss_id=0, model=None, delay_unscale=False, delay_overflow_check=False):
     """Yields ``loss.float() * loss_scale``; on exit unscales gradients (fp16 -> fp32 master grads
@@ -23,9 +37,15 @@ def scale_loss(loss, optimizers, loss_id=0, model=None, delay_unscale=False, del
     if isinstance(optimizers, (torch.optim.Optimizer, LARC)):
         optimizers = [optimizers]
     loss_scaler = _amp_state.loss_scalers[loss_id]
-    loss_scale = loss_scaler.loss_scale()
+    if not loss_scaler.device_mode and _device_scaler_wanted(loss_scaler, optimizers):
+        loss_scaler.enable_device_mode(loss.device)
+    if loss_scaler.device_mode:
+        for optimizer in optimizers:  # an overflowing step: the fused kernels see the flag and no-op
+            optimizer._dummy_overflow_buf = loss_scaler._overflow_buf
+    loss_scale = loss_scaler.scale_for_loss()
 
-    if (not _amp_state.opt_properties.master_weights) and (not loss_scaler.dynamic) and loss_scale == 1.0:
+    if (not _amp_state.opt_properties.master_weights) and (not loss_scaler.dynamic) and \
+            not loss_scaler.device_mode and loss_scale == 1.0:
         yield loss.float()
         if _amp_state.opt_properties.patch_torch_functions and _amp_state.handle is not None:
             _amp_state.handle._clear_cache()

@@ -48,7 +48,29 @@ class LossScaler(object):
         LossScaler.multi_tensor_scale_cuda = amp_C.multi_tensor_scale
         LossScaler.multi_tensor_axpby_cuda = amp_C.multi_tensor_axpby
 
+    # ---- device-resident dynamic scaling (no host sync per step) ----
+    # The scale and the clean-step counter live in device tensors; the overflow flag of the unscale
+    # kernels is handed to the fused optimizers as their noop flag, so an overflowing step is skipped
+    # ON THE DEVICE (its kernels return early) and the scale update runs as tiny device ops. The host
+    # never waits for the backward to finish. Differences from the host path: the optimizer's step
+    # counter also advances on a skipped step, and the skip is not printed. Enabled by
+    # BH_AMP_DEVICE_SCALER=1 (bench.py) for dynamic scaling with fused optimizers only.
+    device_mode = False
+
+    def enable_device_mode(self, device):
+        self._scale_dev = torch.full((1,), float(self._loss_scale), dtype=torch.float32, device=device)
+        self._inv_dev = torch.empty_like(self._scale_dev)
+        self._unskipped_dev = torch.zeros((1,), dtype=torch.int32, device=device)
+        self._overflow_buf = torch.zeros(1, dtype=torch.int, device=device)
+        self.device_mode = True
+
+    def scale_for_loss(self):
+        """The factor scale_loss multiplies the loss by: a device scalar in device mode."""
+        return self._scale_dev if self.device_mode else self._loss_scale
+
     def loss_scale(self):
+        if self.device_mode:
+            return float(self._scale_dev.item())  # an explicit read: synchronises
         return self._loss_scale
 
     def _flag_for(self, tensors):
@@ -68,10 +90,24 @@ class LossScaler(object):
     def unscale(self, model_grads, master_grads, unused_scale, models_are_masters=False, scale_override=None):
         if self._has_overflow:
             return
-        scale = self._loss_scale if scale_override is None else scale_override
-        if scale == 1.0 and models_are_masters and not self.dynamic:
-            return
         if not model_grads:
+            return
+        if self.device_mode and scale_override is None:
+            self._warn_non_fp32(master_grads)
+            torch.reciprocal(self._scale_dev, out=self._inv_dev)
+            flag = self._overflow_buf
+            groups = {}
+            for m, s in zip(model_grads, master_grads):
+                groups.setdefault((m.dtype, s.dtype), ([], []))
+                groups[(m.dtype, s.dtype)][0].append(m)
+                groups[(m.dtype, s.dtype)][1].append(s)
+            for ins, outs in groups.values():
+                multi_tensor_applier(amp_C.multi_tensor_scale, flag, [ins, outs], self._inv_dev)
+            return
+        scale = self._loss_scale if scale_override is None else scale_override
+        if self.device_mode:
+            scale = float(scale)
+        if scale == 1.0 and models_are_masters and not self.dynamic:
             return
         self._warn_non_fp32(master_grads)
         if not LossScaler.has_fused_kernel:
@@ -129,6 +165,19 @@ class LossScaler(object):
         self._overflow_buf.zero_()
 
     def update_scale(self):
+        if self.device_mode:
+            # on the device: overflow -> scale / factor (>= min), counter 0; else counter + 1 and
+            # scale * factor (<= max) when it reaches the window. Never skips on the host.
+            ov = self._overflow_buf > 0
+            down = self._scale_dev / self._scale_factor
+            if self._min_loss_scale:
+                down = torch.clamp(down, min=self._min_loss_scale)
+            cnt = torch.where(ov, torch.zeros_like(self._unskipped_dev), self._unskipped_dev + 1)
+            grow = cnt >= self._scale_seq_len
+            up = torch.clamp(self._scale_dev * self._scale_factor, max=self._max_loss_scale)
+            self._scale_dev.copy_(torch.where(ov, down, torch.where(grow, up, self._scale_dev)))
+            self._unskipped_dev.copy_(torch.where(grow, torch.zeros_like(cnt), cnt))
+            return False
         if self.dynamic and not self._has_overflow and LossScaler.has_fused_kernel:
             self._has_overflow = bool(self._overflow_buf.item())
         if self._has_overflow and self.dynamic:

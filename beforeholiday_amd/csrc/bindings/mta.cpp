@@ -358,6 +358,7 @@ void multi_tensor_lamb(int64_t chunk, at::Tensor noop, Lists lists, double lr, d
   TORCH_CHECK(global_grad_norm.is_cuda() && global_grad_norm.scalar_type() == at::kFloat,
               "global_grad_norm must be a GPU fp32 tensor");
   a.grad_norm = global_grad_norm.data_ptr<float>();
+  a.noop = noop.data_ptr<int>();
   lamb_run(lists, chunk, noop, a);
 }
 
@@ -544,6 +545,7 @@ class ParamTable {
         auto a = lamb_args(h[0], h[1], h[2], h[3], (int64_t)h[4], (int64_t)h[5], h[6], (int64_t)h[7], mode,
                            max_grad_norm, nvlamb);
         a.grad_norm = gnorm.data_ptr<float>();
+        a.noop = noop.data_ptr<int>();  // a set flag (amp's device-resident overflow) skips the step
         lamb_run(kv.second, kElemChunk, noop, a);
       }
     }

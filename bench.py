@@ -82,6 +82,9 @@ def parse():
     ap.add_argument("--conv1x1", default="auto", choices=["auto", "miopen", "gemm"],
                     help="stride-1 1x1 convolution forward / data gradient: hipBLASLt GEMMs on the channels_last "
                          "view, MIOpen, or the faster per shape (auto, timed in the first warmup step)")
+    ap.add_argument("--host-scaler", action="store_true",
+                    help="dynamic loss scale read on the host every step (the reference's .item() per step); "
+                         "default: device-resident scale, overflow skipped by the fused optimizer's noop flag")
     ap.add_argument("--conv3x3", default="auto", choices=["auto", "miopen", "direct"],
                     help="stride-1 3x3 convolution forward / data gradient: the direct MFMA kernel "
                          "(kernels/conv.hip), MIOpen, or the faster per shape (auto)")
@@ -122,6 +125,8 @@ def main():
     from beforeholiday_amd.parallel.optimized_sync_batchnorm import set_stats_mode
 
     require_native("bench")
+    if not args.host_scaler:
+        os.environ["BH_AMP_DEVICE_SCALER"] = "1"  # amp/scaler.py enable_device_mode: no host sync per step
     set_stats_mode(args.syncbn_stats)
     torch.manual_seed(1234 + rank)
     bn_group = dist.new_group(list(range(world))) if (world > 1 and args.bn_group == "separate") else None
@@ -234,6 +239,7 @@ def main():
             "backend": (args.backend if world > 1 else "none"),
             "ddp_bucket_mb": buckets,
             "syncbn_stats": args.syncbn_stats,
+            "loss_scaler": "host" if args.host_scaler else "device",
             "comm_ms_per_step": comm,
         }), flush=True)
     if world > 1:

@@ -53,6 +53,21 @@ def main():
     lines.append(f"# kernel time per step (last {n} steps, marker {marker.pattern!r})\n")
     lines.append(f"wall span/step: {span / n / 1e6:.3f} ms; GPU busy/step (sum of kernel times): "
                  f"{busy / n / 1e6:.3f} ms; kernels/step: {len(seg) / n:.0f}\n")
+    # idle gaps (GPU waiting on the host) in the last step: where they are tells a host sync at the
+    # step boundary from host-issue-bound stretches of small kernels
+    last = rows[marks[-2] + 1:marks[-1] + 1] if len(marks) >= 2 else seg
+    gaps, end = [], None
+    for s_, e_, name in last:
+        if end is not None and s_ > end:
+            gaps.append((s_ - end, prev, name))
+        end = e_ if end is None else max(end, e_)
+        prev = name
+    short = lambda n_: re.sub(r"\(.*", "", n_.replace("(anonymous namespace)::", ""))[:60]
+    tot_gap = sum(g[0] for g in gaps)
+    lines.append(f"idle in the last step: {tot_gap / 1e6:.3f} ms in {len(gaps)} gaps; largest:\n")
+    for g_, a_, b_ in sorted(gaps, reverse=True)[:8]:
+        lines.append(f"* {g_ / 1e3:.1f} us after `{short(a_)}` before `{short(b_)}`")
+    lines.append("")
     lines.append("| kernel | ms/step | share | launches/step |")
     lines.append("|---|---|---|---|")
     for k, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:60]:

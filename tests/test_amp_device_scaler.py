@@ -1,0 +1,66 @@
+"""Device-resident dynamic loss scaling (BH_AMP_DEVICE_SCALER=1, amp/scaler.py ``enable_device_mode``):
+no host sync per step, the overflow flag is the fused optimizer's noop flag.
+
+Checked on the GPU against the host scaler (the reference's behaviour, apex/amp/scaler.py:197-226):
+matching parameter trajectories and identical loss scales while no step overflows (including a scale
+growth after ``scale_window`` clean steps), and on an injected overflow: parameters unchanged by
+the skipped step and the scale halved."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+
+def _run(device_mode, steps, inf_at=None, monkeypatch=None, window=3, init_scale=256.0):
+    from beforeholiday_amd import amp
+    from beforeholiday_amd.amp._amp_state import _amp_state
+    from beforeholiday_amd.optimizers import FusedLAMB
+
+    monkeypatch.setenv("BH_AMP_DEVICE_SCALER", "1" if device_mode else "0")
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.BatchNorm1d(64), torch.nn.ReLU(),
+                                torch.nn.Linear(64, 8)).cuda()
+    opt = FusedLAMB(model.parameters(), lr=1e-2, weight_decay=0.01)
+    model, opt = amp.initialize(model, opt, opt_level="O2", keep_batchnorm_fp32=True, verbosity=0,
+                                loss_scale="dynamic")
+    _amp_state.loss_scalers[0]._scale_seq_len = window
+    _amp_state.loss_scalers[0]._loss_scale = init_scale  # before the first scale_loss (device mode copies it)
+    x = torch.randn(16, 32, device="cuda", dtype=torch.half)
+    y = torch.randint(0, 8, (16,), device="cuda")
+    scales, snaps = [], []
+    for i in range(steps):
+        loss = F.cross_entropy(model(x).float(), y)
+        with amp.scale_loss(loss, opt) as scaled:
+            scaled.backward()
+            if inf_at == i:
+                next(model.parameters()).grad.view(-1)[0] = float("inf")
+        opt.step()
+        opt.zero_grad()
+        scales.append(_amp_state.loss_scalers[0].loss_scale())
+        snaps.append([p.detach().float().clone() for p in model.parameters()])
+    device_used = _amp_state.loss_scalers[0].device_mode
+    amp.deactivate() if hasattr(amp, "deactivate") else None
+    return scales, snaps, device_used
+
+
+@pytest.mark.gpu
+def test_device_scaler_matches_host_without_overflow(monkeypatch):
+    s_host, p_host, dev0 = _run(False, 5, monkeypatch=monkeypatch)
+    s_dev, p_dev, dev1 = _run(True, 5, monkeypatch=monkeypatch)
+    assert not dev0 and dev1
+    assert s_host == s_dev and s_host[-1] > s_host[0]  # grew after the window, identically
+    # same arithmetic, bitwise (5 steps from scale 256 with one growth: no step overflows. On a
+    # skipped step the device mode still advances the optimizer's step counter -- the one documented
+    # difference -- so trajectories with overflows differ in the bias correction)
+    for a, b in zip(p_host, p_dev):
+        for u, v in zip(a, b):
+            assert torch.equal(u, v)
+
+
+@pytest.mark.gpu
+def test_device_scaler_overflow_skips_on_device(monkeypatch):
+    s_dev, p_dev, used = _run(True, 4, inf_at=2, monkeypatch=monkeypatch, window=100)
+    assert used
+    assert s_dev[2] == s_dev[1] / 2  # halved on the overflowing step
+    for u, v in zip(p_dev[1], p_dev[2]):  # the skipped step left every parameter unchanged
+        assert torch.equal(u, v)
+    assert any(not torch.equal(u, v) for u, v in zip(p_dev[2], p_dev[3]))  # and training goes on
