@@ -45,6 +45,8 @@ def main():
     from beforeholiday_amd._native import require_native
     from beforeholiday_amd.models import BertModel, TransformerConfig
     from beforeholiday_amd.optimizers import FusedLAMB
+
+    os.environ.setdefault("BH_AMP_DEVICE_SCALER", "1")  # device-resident loss scale (amp/scaler.py), as bench.py
     from beforeholiday_amd.parallel import DistributedDataParallel
     from beforeholiday_amd.transformer import parallel_state, tensor_parallel
 
