@@ -29,6 +29,10 @@ def main():
                     name = "attn_fwd"
                 elif "attn_bwd" in name:
                     name = "attn_bwd"
+                elif "k_conv3x3" in name:
+                    kind = "dgrad" if "Lb1E" in name else "fwd"
+                    g = "G4" if "Li4E" in name else ("G2" if "Li2E" in name else "G1")
+                    name = f"conv3x3_{kind}<{g}>"
                 elif "k_conv_wgrad" in name:
                     geo = {"Li14ELi2E": "56x56", "Li7ELi4E": "28x28", "Li4ELi7E": "14x14", "Li2ELi7E": "7x7",
                            "Li28ELi1E": "1x1"}
