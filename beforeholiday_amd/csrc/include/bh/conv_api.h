@@ -35,7 +35,7 @@ struct ConvWgradArgs {
   int N = 0, H = 0, W = 0, C = 0, K = 0, R = 3;
 };
 struct ConvWgradGeo {
-  int G4 = 0, TH = 0, ksteps = 0, wpi = 0, nwin = 0, ctiles = 0, tiles = 0, wpw = 0, splits = 0, grid = 0, kt = 1, parts = 0;
+  int G4 = 0, TH = 0, ksteps = 0, wpi = 0, nwin = 0, ctiles = 0, tiles = 0, wpw = 0, splits = 0, grid = 0, kt = 1, ct = 1, parts = 0;
 };
 // false when the kernel does not cover the shape (C, K % 64, 16-byte alignment, window fits in LDS)
 bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo);

@@ -107,17 +107,20 @@ BH_DEVICE i4v frag2(const char* img, int lo, int hi) {
 
 // window geometry (G4 four-pixel groups per row, TH rows) as compile-time constants: the staging
 // address math divides by them
-template <typename T, int R, int G4, int TH, int KT>
+template <typename T, int R, int G4, int TH, int KT, int CT = 1>
 __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, ConvWgradGeo g, float* __restrict__ ws,
                                                            T* __restrict__ out) {
   constexpr int P = (R - 1) / 2, RR = R * R;
   constexpr int HC = 4 * G4 + 2 * P, KSTEPS = (TH * G4 + 3) / 4;
   constexpr int XS = (TH + 2 * P) * HC, DS = KSTEPS * 16;  // X halo / dY pixel slots per window
   constexpr int DSL = dslot<KT>(), TK = kTile * KT;  // dY slot bytes, output channels per workgroup
-  constexpr int BUFX = (XS * kSlot + 1023) / 1024 * 1024, BUF = BUFX + (DS * DSL + 1023) / 1024 * 1024;
+  constexpr int XSL = dslot<CT>(), TC = kTile * CT;  // X slot bytes, input channels per workgroup
+  constexpr int BUFX = (XS * XSL + 1023) / 1024 * 1024, BUF = BUFX + (DS * DSL + 1023) / 1024 * 1024;
   constexpr int XP = BUFX / 1024, DP = (BUF - BUFX) / 1024;  // 1-KiB LDS-DMA pieces
   constexpr int XPW = (XP + 7) / 8, DPW = (DP + 7) / 8;  // pieces per wave
-  constexpr int NOFF = (RR + 1) / 2;  // offsets per wave: the two waves of a SIMD split the R*R offsets
+  // offsets per wave: the two waves of a SIMD split the R*R offsets; at R = 1 the slot is the wave's
+  // 32-column sub-tile of its 32 * CT input channels instead
+  constexpr int NOFF = R == 1 ? CT : (RR + 1) / 2;
   static_assert(XS <= kMaxHalo && DS <= kMaxD, "window does not fit");
   static_assert(2 * BUF <= 160 * 1024, "two window buffers must fit in LDS");
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
@@ -127,7 +130,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
   const int L = (b & 7) * (g.grid / 8) + (b >> 3);
   if (L >= g.tiles * g.splits) return;  // grid padding (before any barrier)
   const int tile = L % g.tiles, split = L / g.tiles;
-  const int k0 = (tile / g.ctiles) * TK, c0 = (tile % g.ctiles) * kTile;
+  const int k0 = (tile / g.ctiles) * TK, c0 = (tile % g.ctiles) * TC;
   const int w_begin = split * g.wpw, w_end = min(g.nwin, w_begin + g.wpw);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -135,7 +138,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
   const int kw = (wave >> 1) & 1, cw = wave & 1, half = wave >> 2;
   // R = 3: the two waves of a SIMD split the offsets (rs0 .. rs0 + noff - 1); R = 1 (one offset):
   // they split the k-steps instead (half h takes ks = h, h + 2, ...) and write separate partials
-  const int rs0 = R == 1 ? 0 : half * NOFF, noff = R == 1 ? 1 : min(NOFF, RR - rs0);
+  const int rs0 = R == 1 ? 0 : half * NOFF, noff = R == 1 ? NOFF : min(NOFF, RR - rs0);
   const int C = a.C, K = a.K, H = a.H, W = a.W;
   // whole-tensor buffer resources: a pixel outside the image (or a pad chunk) gets an offset past
   // the range and lands in LDS as zeros (no clamped pointers, no select)
@@ -153,10 +156,10 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
   for (int i = 0; i < NPW; ++i) {
     const bool isx = i < XPW;
     const int piece = wave + 8 * (isx ? i : i - XPW);
-    const int byte = piece * 1024 + lane * 16, slot = byte / kSlot, ch = (byte - slot * kSlot) >> 4;
+    const int byte = piece * 1024 + lane * 16, slot = byte / XSL, ch = (byte - slot * XSL) >> 4;
     if (isx) {
       const int hr = slot / HC, x = slot - hr * HC - P;
-      const bool ok = piece < XP && ch < 8 && slot < XS && x >= 0 && x < W;
+      const bool ok = piece < XP && ch < 8 * CT && slot < XS && x >= 0 && x < W;
       rel[i] = (((hr - P) * W + x) * C + c0 + ch * 8) * 2;
       hrow[i] = ok ? hr - P : kBad;
     } else {
@@ -196,7 +199,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int grp = min(4 * ks + 2 * h + j, ng - 1), row = grp / G4;
-      x_off[ks][j] = (row * HC + 4 * (grp - row * G4) + q) * kSlot + 2 * 32 * cw + colb;
+      x_off[ks][j] = (row * HC + 4 * (grp - row * G4) + q) * XSL + 2 * 32 * CT * cw + colb;
     }
 
   f16v acc[NOFF][KT];
@@ -235,7 +238,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
     // branch: the half-1 waves of an odd R*R own one offset fewer)
     auto read_b = [&](int ks, int buf, int j) {
       const int rs = rs0 + j, r = rs / R, s = rs - r * R;
-      const char* base = xs + (r * HC + s) * kSlot;
+      const char* base = xs + (r * HC + s) * XSL;
       fb[buf][j] = frag2(base, x_off[ks][0], x_off[ks][1]);
     };
     if constexpr (R == 1) {
@@ -245,7 +248,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
         const int ks = 2 * u + half;
 #pragma unroll
         for (int t = 0; t < KT; ++t) fa[buf][t] = frag2(ds + 16 * ks * DSL + 64 * t, a_off, a_off + 4 * DSL);
-        fb[buf][0] = frag2(xs + 16 * ks * kSlot, x_off[0][0], x_off[0][1]);
+#pragma unroll
+        for (int j = 0; j < NOFF; ++j) fb[buf][j] = frag2(xs + 16 * ks * XSL + 64 * j, x_off[0][0], x_off[0][1]);
       };
 #pragma unroll
       for (int t = 0; t < NPW; ++t)  // the next window's pieces first: they have the whole window to land
@@ -256,7 +260,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
         const int cur = u & 1;
         if (2 * u + half < KSTEPS) {
 #pragma unroll
-          for (int t = 0; t < KT; ++t) acc[0][t] = MfmaW<T>::run(fa[cur][t], fb[cur][0], acc[0][t]);
+          for (int j = 0; j < NOFF; ++j)
+#pragma unroll
+            for (int t = 0; t < KT; ++t) acc[j][t] = MfmaW<T>::run(fa[cur][t], fb[cur][j], acc[j][t]);
         }
         if (u + 1 < KL && 2 * (u + 1) + half < KSTEPS) rd(u + 1, cur ^ 1);
         __builtin_amdgcn_sched_barrier(0);
@@ -288,12 +294,13 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
       if (pre) issue_piece(t, nn, ny0, nbuf);
   }
 
-  // lane holds column c = c0 + 32 cw + (lane & 31) and rows k = k0 + 32 kw + 8 j + 4 h + i (acc[4 j + i])
-  const int c = c0 + 32 * cw + (lane & 31);
+  // lane holds column c = c0 + 32 CT cw (+ 32 jo at R = 1) + (lane & 31) and rows
+  // k = k0 + 32 KT kw + 32 t + 8 j + 4 h + i (acc[4 j + i])
 #pragma unroll
   for (int jo = 0; jo < NOFF; ++jo) {
     if (jo >= noff) break;
-    const int rs = rs0 + jo;
+    const int rs = R == 1 ? 0 : rs0 + jo;
+    const int c = c0 + 32 * CT * cw + (R == 1 ? 32 * jo : 0) + (lane & 31);
 #pragma unroll
     for (int t = 0; t < KT; ++t)
 #pragma unroll
@@ -373,7 +380,8 @@ bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo) {
   // 128 output channels per workgroup (each wave two k sub-tiles sharing its X fragments) for the
   // 14- / 7-wide windows (measured 1.1x there; the 28-wide instantiation spills and is slower)
   g.kt = (a.K % 128 == 0 && (a.R == 1 || g.G4 == 4 || g.G4 == 2)) ? 2 : 1;
-  g.ctiles = a.C / kTile;
+  g.ct = (a.R == 1 && a.C % 128 == 0) ? 2 : 1;  // 1x1: 128 input channels per workgroup where C allows
+  g.ctiles = a.C / (kTile * g.ct);
   g.tiles = (a.K / (kTile * g.kt)) * g.ctiles;
   // one round of workgroups (one per CU), split over the windows
   int splits = std::max(1, 256 / g.tiles);
@@ -402,7 +410,10 @@ void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws
     using T = typename decltype(tt)::type;
     T* out = reinterpret_cast<T*>(a.out);
     auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(g.grid), dim3(kThreads), 0, st, b, g, ws, out); };
-    if (a.R == 1) g.kt == 2 ? go(k_conv_wgrad<T, 1, 28, 1, 2>) : go(k_conv_wgrad<T, 1, 28, 1, 1>);
+    if (a.R == 1) {
+      if (g.ct == 2) g.kt == 2 ? go(k_conv_wgrad<T, 1, 28, 1, 2, 2>) : go(k_conv_wgrad<T, 1, 28, 1, 1, 2>);
+      else g.kt == 2 ? go(k_conv_wgrad<T, 1, 28, 1, 2, 1>) : go(k_conv_wgrad<T, 1, 28, 1, 1, 1>);
+    }
     else if (g.G4 == 14) go(k_conv_wgrad<T, 3, 14, 2, 1>);
     else if (g.G4 == 7) go(k_conv_wgrad<T, 3, 7, 4, 1>);
     else if (g.G4 == 4) g.kt == 2 ? go(k_conv_wgrad<T, 3, 4, 7, 2>) : go(k_conv_wgrad<T, 3, 4, 7, 1>);

@@ -79,7 +79,7 @@ def test_conv3x3_module_grads_match_miopen(mode):
 WGRAD_SHAPES = [  # N, C, K, H, W, R
     (2, 64, 64, 56, 56, 3), (3, 128, 128, 28, 28, 3), (5, 256, 64, 14, 14, 3), (7, 64, 128, 7, 7, 3),
     (9, 64, 64, 16, 16, 3), (3, 64, 192, 13, 13, 3), (4, 128, 64, 5, 5, 3), (2, 64, 256, 14, 14, 3),
-    (2, 64, 256, 56, 56, 1), (4, 256, 128, 14, 14, 1), (1, 64, 64, 7, 16, 1),
+    (2, 64, 256, 56, 56, 1), (4, 256, 128, 14, 14, 1), (1, 64, 64, 7, 16, 1), (2, 128, 64, 28, 28, 1),
 ]
 
 
