@@ -294,6 +294,30 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
       if (pre) issue_piece(t, nn, ny0, nbuf);
   }
 
+  if constexpr (R == 1) {
+    // the two waves of a SIMD hold partial sums of the same tile (even / odd k-steps): the odd
+    // half hands its accumulators to the even half through LDS, so one partial slab per split
+    float* red = reinterpret_cast<float*>(smem);  // NOFF * KT * 16 floats per lane, 4 waves
+    constexpr int NA = NOFF * KT * 16;
+    raw_barrier();  // every wave is done with the window buffers
+    if (half == 1) {
+#pragma unroll
+      for (int jo = 0; jo < NOFF; ++jo)
+#pragma unroll
+        for (int t = 0; t < KT; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) red[((jo * KT + t) * 16 + i) * 256 + (wave & 3) * 64 + lane] = acc[jo][t][i];
+    }
+    __syncthreads();
+    if (half == 1) return;
+#pragma unroll
+    for (int jo = 0; jo < NOFF; ++jo)
+#pragma unroll
+      for (int t = 0; t < KT; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[jo][t][i] += red[((jo * KT + t) * 16 + i) * 256 + (wave & 3) * 64 + lane];
+    static_assert(NA * 256 * 4 <= 2 * BUF, "reduction staging fits in the window buffers");
+  }
   // lane holds column c = c0 + 32 CT cw (+ 32 jo at R = 1) + (lane & 31) and rows
   // k = k0 + 32 KT kw + 32 t + 8 j + 4 h + i (acc[4 j + i])
 #pragma unroll
@@ -310,7 +334,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
           const int k = k0 + 32 * KT * kw + 32 * t + 8 * j + 4 * h + i;
           const int64_t o = ((int64_t)k * RR + rs) * C + c;
           if (g.parts == 1) out[o] = from_f<T>(acc[jo][t][4 * j + i]);
-          else ws[(int64_t)(R == 1 ? 2 * split + half : split) * K * RR * C + o] = acc[jo][t][4 * j + i];
+          else ws[(int64_t)split * K * RR * C + o] = acc[jo][t][4 * j + i];
         }
   }
 }
@@ -388,7 +412,7 @@ bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo) {
   splits = std::min(splits, g.nwin);
   g.wpw = (g.nwin + splits - 1) / splits;
   g.splits = (g.nwin + g.wpw - 1) / g.wpw;
-  g.parts = g.splits * (a.R == 1 ? 2 : 1);
+  g.parts = g.splits;
   g.grid = (g.tiles * g.splits + 7) / 8 * 8;
   *geo = g;
   return true;
