@@ -243,9 +243,80 @@ class Conv3x3(nn.Conv2d):
         return super().forward(x)
 
 
+class _Conv1x1S2Fn(torch.autograd.Function):
+    """1x1 / stride-2 convolution of a channels_last activation (the ResNet downsample branch).
+    Every output pixel reads input pixel (2y, 2x), so the layer is a 1x1 convolution of the
+    gathered quarter-resolution input ``xg``. The forward gathers ``xg`` once (a strided copy of
+    a quarter of the input) and runs the GEMM on it, or it runs MIOpen, whichever is faster per
+    shape. ``xg`` is saved instead of the full-resolution input, and the weight gradient is the MFMA
+    1x1 wgrad kernel on (xg, dY). The data gradient is one GEMM scattered into a zeroed
+    full-resolution tensor, the same work MIOpen's stride-2 backward-data does."""
+
+    @staticmethod
+    def forward(ctx, x, weight, mode):
+        n, c, h, w = x.shape
+        w2d = weight.view(weight.size(0), c)
+        conv = torch.nn.functional.conv2d
+
+        def gemm():
+            xg = x[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last)
+            return xg, torch.mm(xg.permute(0, 2, 3, 1).reshape(-1, c), w2d.t())
+
+        how = _pick((n, c, h, w, weight.size(0), x.dtype, "fwd_s2"), lambda: gemm(), lambda: conv(x, weight, stride=2),
+                    mode)
+        ho, wo = (h + 1) // 2, (w + 1) // 2
+        if how == "gemm":
+            xg, y2d = gemm()
+            y = y2d.view(n, ho, wo, -1).permute(0, 3, 1, 2)
+        else:
+            y = conv(x, weight, stride=2)
+            xg = x[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last)
+        ctx.save_for_backward(xg, weight)
+        ctx.in_hw = (h, w)
+        ctx.mode = mode
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        xg, weight = ctx.saved_tensors
+        n, c, ho, wo = xg.shape
+        h, w = ctx.in_hw
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            dxg = torch.mm(gy.permute(0, 2, 3, 1).reshape(-1, weight.size(0)), weight.view(weight.size(0), c))
+            gx = torch.zeros((n, c, h, w), dtype=gy.dtype, device=gy.device).contiguous(memory_format=torch.channels_last)
+            gx[:, :, ::2, ::2] = dxg.view(n, ho, wo, c).permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1]:
+            conv_bwd = torch.ops.aten.convolution_backward
+            args = ([1, 1], [0, 0], [1, 1], False, [0, 0], 1)
+            gw = _wgrad(xg, gy, weight, 1, "auto" if ctx.mode == "auto" else "miopen",
+                        lambda: conv_bwd(gy, xg, weight, None, *args, [False, True, False])[1])
+        return gx, gw, None
+
+
+class Conv1x1S2(nn.Conv2d):
+    """nn.Conv2d(k=1, stride=2, bias=False) with the gathered-input GPU path (``_Conv1x1S2Fn``)."""
+
+    def __init__(self, *args, mode="auto", **kw):
+        super().__init__(*args, **kw)
+        self.mode = mode
+
+    def forward(self, x):
+        if (x.is_cuda and self.mode != "miopen" and x.dim() == 4 and x.dtype == self.weight.dtype
+                and x.is_contiguous(memory_format=torch.channels_last) and x.size(2) % 2 == 0 and x.size(3) % 2 == 0):
+            return _Conv1x1S2Fn.apply(x, self.weight, self.mode)
+        return super().forward(x)
+
+
 def conv1x1(cin, cout, stride=1):
     if _CONV1X1_MODE != "miopen" and stride == 1:
         return Conv1x1(cin, cout, 1, stride=stride, bias=False, mode=_CONV1X1_MODE)
+    # opt-in (BH_CONV1X1_S2=1): measured 27.7 vs 26.4 ms per ResNet-50 step on the same box, the
+    # strided gather / zero-fill + scatter cost more than MIOpen's stride-2 kernels
+    # (profiles/resnet50_conv1x1_s2_ab.txt)
+    if _CONV1X1_MODE != "miopen" and stride == 2 and os.environ.get("BH_CONV1X1_S2", "0") == "1":
+        return Conv1x1S2(cin, cout, 1, stride=2, bias=False, mode=_CONV1X1_MODE)
     return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
 
 

@@ -119,3 +119,28 @@ def test_conv_wgrad_fallback_shapes():
     ref1 = torch.nn.grad.conv2d_weight(x1.float(), (64, 64, 1, 1), dy1.float())
     torch.testing.assert_close(bhconv.conv_wgrad(x1, dy1, 1).float(), ref1, rtol=2e-2,
                                atol=2e-2 * ref1.abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["gemm", "auto"])
+def test_conv1x1_stride2_module_matches_conv2d(mode):
+    """ResNet downsample 1x1 / stride 2 (models/resnet.py Conv1x1S2, opt-in BH_CONV1X1_S2=1: gathered
+    quarter-resolution input, GEMM forward, GEMM + scatter data gradient, MFMA wgrad kernel) vs
+    nn.Conv2d(stride=2)."""
+    from beforeholiday_amd.models.resnet import Conv1x1S2
+    torch.manual_seed(0)
+    ref = torch.nn.Conv2d(256, 512, 1, stride=2, bias=False).cuda().half().to(memory_format=torch.channels_last)
+    m = Conv1x1S2(256, 512, 1, stride=2, bias=False, mode=mode).cuda().half().to(memory_format=torch.channels_last)
+    m.weight.data.copy_(ref.weight.data)
+    x = torch.randn(16, 256, 28, 28, device="cuda", dtype=torch.half).contiguous(memory_format=torch.channels_last)
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    ya, yb = m(xa), ref(xb)
+    assert ya.shape == yb.shape == (16, 512, 14, 14)
+    g = torch.randn_like(ya)
+    ya.backward(g)
+    yb.backward(g)
+    torch.testing.assert_close(ya.float(), yb.float(), rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(xa.grad.float(), xb.grad.float(), rtol=2e-2, atol=2e-2)
+    assert torch.count_nonzero(xa.grad[:, :, 1::2, :]) == 0  # odd rows / columns get no gradient
+    wr = ref.weight.grad.float()
+    torch.testing.assert_close(m.weight.grad.float(), wr, rtol=2e-2, atol=1e-2 * wr.abs().max().item())
