@@ -42,6 +42,7 @@ def scale_loss(loss, optimizers, loss_id=0, model=None, delay_unscale=False, del
     if loss_scaler.device_mode:
         for optimizer in optimizers:  # an overflowing step: the fused kernels see the flag and no-op
             optimizer._dummy_overflow_buf = loss_scaler._overflow_buf
+            optimizer._device_step = True  # FusedLAMB: step counters advance on the device, unless skipped
     loss_scale = loss_scaler.scale_for_loss()
 
     if (not _amp_state.opt_properties.master_weights) and (not loss_scaler.dynamic) and \

@@ -52,9 +52,10 @@ class LossScaler(object):
     # The scale and the clean-step counter live in device tensors; the overflow flag of the unscale
     # kernels is handed to the fused optimizers as their noop flag, so an overflowing step is skipped
     # ON THE DEVICE (its kernels return early) and the scale update runs as tiny device ops. The host
-    # never waits for the backward to finish. Differences from the host path: the optimizer's step
-    # counter also advances on a skipped step, and the skip is not printed. Enabled by
-    # BH_AMP_DEVICE_SCALER=1 (bench.py) for dynamic scaling with fused optimizers only.
+    # never waits for the backward to finish. FusedLAMB keeps device step counters that advance only
+    # on steps the flag did not skip, so trajectories match the host path (to the rounding of fp32
+    # bias corrections); the skip is not
+    # printed. Enabled by BH_AMP_DEVICE_SCALER=1 (bench.py) for dynamic scaling with fused optimizers.
     device_mode = False
 
     def enable_device_mode(self, device):

@@ -512,8 +512,10 @@ class ParamTable {
   size_t num_groups() const { return groups_.size(); }
 
   // hyper[g] = {lr, beta1, beta2, eps, step, bias_correction, weight_decay, grad_averaging}
+  // steps (optional): int32 [groups] device step counters (amp's device-resident loss scale): the
+  // bias corrections use them, so a step skipped on the device does not advance them
   bool lamb_step(at::Tensor noop, std::vector<std::vector<double>> hyper, int64_t mode, double max_grad_norm,
-                 bool nvlamb) {
+                 bool nvlamb, c10::optional<at::Tensor> steps) {
     TORCH_CHECK(hyper.size() == groups_.size(), "ParamTable.lamb_step: one hyper-parameter row per group");
     std::vector<std::map<std::pair<int, int>, Lists>> buckets(groups_.size());
     std::map<int, std::vector<at::Tensor>> by_gdt;
@@ -534,6 +536,9 @@ class ParamTable {
     }
     if (by_gdt.empty()) return true;
     check_noop(noop);
+    if (steps.has_value())
+      TORCH_CHECK(steps->is_cuda() && steps->scalar_type() == at::kInt && steps->numel() >= (int64_t)groups_.size(),
+                  "ParamTable.lamb_step: steps must be a CUDA int32 tensor with one counter per group");
     // global gradient norm: one deterministic norm per gradient dtype, blended on the device
     std::vector<at::Tensor> norms;
     for (auto& kv : by_gdt) norms.push_back(std::get<0>(norm_impl(kNormChunk, noop, {kv.second}, false, 2, false, 1.0, false)));
@@ -546,6 +551,7 @@ class ParamTable {
                            max_grad_norm, nvlamb);
         a.grad_norm = gnorm.data_ptr<float>();
         a.noop = noop.data_ptr<int>();  // a set flag (amp's device-resident overflow) skips the step
+        if (steps.has_value()) a.step_ptr = steps->data_ptr<int>() + gi;
         lamb_run(kv.second, kElemChunk, noop, a);
       }
     }
@@ -654,7 +660,7 @@ void register_amp_C(pybind11::module_& root) {
            py::arg("master") = std::vector<c10::optional<at::Tensor>>())
       .def("num_groups", &ParamTable::num_groups)
       .def("lamb_step", &ParamTable::lamb_step, py::arg("noop_flag"), py::arg("hyper"), py::arg("mode"),
-           py::arg("max_grad_norm"), py::arg("use_nvlamb"))
+           py::arg("max_grad_norm"), py::arg("use_nvlamb"), py::arg("steps") = py::none())
       .def("adam_step", &ParamTable::adam_step, py::arg("noop_flag"), py::arg("hyper"), py::arg("mode"));
   m.def("plan_cache_clear", &plan_cache_clear);
 }

@@ -61,7 +61,17 @@ class FusedLAMB(ParamTableMixin, torch.optim.Optimizer):
             hyper.append([float(group["lr"]), beta1, beta2, group["eps"], group["step"],
                           1 if group["bias_correction"] else 0, group["weight_decay"],
                           1 if group["grad_averaging"] else 0])
-        args = (self._dummy_overflow_buf, hyper, self.adam_w_mode, self.defaults["max_grad_norm"], self.use_nvlamb)
+        steps = None
+        if getattr(self, "_device_step", False):
+            # amp's device-resident loss scale: the noop flag may skip this step on the device, so the
+            # step counters the bias corrections use advance on the device only when it does not
+            if getattr(self, "_device_steps", None) is None or self._device_steps.numel() != len(self.param_groups):
+                self._device_steps = torch.tensor([g["step"] - 1 for g in self.param_groups], dtype=torch.int32,
+                                                  device=self._dummy_overflow_buf.device)
+            self._device_steps.add_((self._dummy_overflow_buf == 0).to(torch.int32))
+            steps = self._device_steps
+        args = (self._dummy_overflow_buf, hyper, self.adam_w_mode, self.defaults["max_grad_norm"], self.use_nvlamb,
+                steps)
         if not self._native_table(("exp_avg", "exp_avg_sq")).lamb_step(*args):
             for group in self.param_groups:
                 for p in group["params"]:
@@ -71,6 +81,17 @@ class FusedLAMB(ParamTableMixin, torch.optim.Optimizer):
             self._table = None
             if not self._native_table(("exp_avg", "exp_avg_sq")).lamb_step(*args):
                 raise RuntimeError("FusedLAMB: optimizer state missing after initialisation")
+
+    def state_dict(self):
+        steps = getattr(self, "_device_steps", None)
+        if steps is not None:  # the device counters are the real step counts (skipped steps excluded)
+            for g, st in zip(self.param_groups, steps.tolist()):
+                g["step"] = int(st)
+        return super().state_dict()
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._device_steps = None  # re-seeded from the loaded host counters
 
     @torch.no_grad()
     def step(self, closure=None):
