@@ -31,22 +31,24 @@ inline void check_launch(const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-template <typename T>
+// I: index type -- uint32_t when every element offset of the launch fits (the ResNet stem: 205 M
+// elements), which turns the per-thread 64-bit divisions of the pixel decomposition into 32-bit ones
+template <typename T, typename I>
 __global__ __launch_bounds__(kBlock) void k_maxpool_fwd_nhwc(PoolArgs a, const T* __restrict__ x,
                                                              const float* __restrict__ scale,
                                                              const float* __restrict__ shift, T* __restrict__ y,
                                                              uint8_t* __restrict__ idx, int64_t* counter) {
   if (counter && blockIdx.x == 0 && threadIdx.x == 0) *counter += 1;
-  const int cv = a.C / 8;
-  const int64_t total = (int64_t)a.N * a.OH * a.OW * cv;
-  const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const I cv = (I)(a.C / 8);
+  const I total = (I)a.N * a.OH * a.OW * cv;
+  const I t = (I)blockIdx.x * kBlock + threadIdx.x;
   if (t >= total) return;
   const int c0 = (int)(t % cv) * 8;
-  int64_t p = t / cv;
-  const int ow = (int)(p % a.OW);
-  p /= a.OW;
-  const int oh = (int)(p % a.OH);
-  const int n = (int)(p / a.OH);
+  I p = t / cv;
+  const int ow = (int)(p % (I)a.OW);
+  p /= (I)a.OW;
+  const int oh = (int)(p % (I)a.OH);
+  const int n = (int)(p / (I)a.OH);
   float sc[8], sh[8];
   const bool bn = scale != nullptr;
   if (bn) {
@@ -68,7 +70,7 @@ __global__ __launch_bounds__(kBlock) void k_maxpool_fwd_nhwc(PoolArgs a, const T
       const int iw = ws + kw;
       if (iw < 0 || iw >= a.W) continue;
       float v[8];
-      VecIO<T>::load(x + (((int64_t)n * a.H + ih) * a.W + iw) * a.C + c0, v);
+      VecIO<T>::load(x + (((I)n * a.H + ih) * a.W + iw) * a.C + c0, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float u = v[j];
@@ -81,7 +83,7 @@ __global__ __launch_bounds__(kBlock) void k_maxpool_fwd_nhwc(PoolArgs a, const T
       }
     }
   }
-  const int64_t o = (((int64_t)n * a.OH + oh) * a.OW + ow) * a.C + c0;
+  const I o = (((I)n * a.OH + oh) * a.OW + ow) * a.C + c0;
   VecIO<T>::store(y + o, best);
   if (idx) {
     uint32_t lo = 0, hi = 0;
@@ -94,19 +96,19 @@ __global__ __launch_bounds__(kBlock) void k_maxpool_fwd_nhwc(PoolArgs a, const T
   }
 }
 
-template <typename T>
+template <typename T, typename I>
 __global__ __launch_bounds__(kBlock) void k_maxpool_bwd_nhwc(PoolArgs a, const T* __restrict__ gy,
                                                              const uint8_t* __restrict__ idx, T* __restrict__ gx) {
-  const int cv = a.C / 8;
-  const int64_t total = (int64_t)a.N * a.H * a.W * cv;
-  const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const I cv = (I)(a.C / 8);
+  const I total = (I)a.N * a.H * a.W * cv;
+  const I t = (I)blockIdx.x * kBlock + threadIdx.x;
   if (t >= total) return;
   const int c0 = (int)(t % cv) * 8;
-  int64_t p = t / cv;
-  const int iw = (int)(p % a.W);
-  p /= a.W;
-  const int ih = (int)(p % a.H);
-  const int n = (int)(p / a.H);
+  I p = t / cv;
+  const int iw = (int)(p % (I)a.W);
+  p /= (I)a.W;
+  const int ih = (int)(p % (I)a.H);
+  const int n = (int)(p / (I)a.H);
   // windows containing ih: oh*s - pad <= ih <= oh*s - pad + k - 1
   const int oh0 = max(0, (ih + a.pad - a.k + a.stride) / a.stride);
   const int oh1 = min(a.OH - 1, (ih + a.pad) / a.stride);
@@ -119,7 +121,7 @@ __global__ __launch_bounds__(kBlock) void k_maxpool_bwd_nhwc(PoolArgs a, const T
     const int kh = ih - (oh * a.stride - a.pad);
     for (int ow = ow0; ow <= ow1; ++ow) {
       const int want = kh * a.k + iw - (ow * a.stride - a.pad);
-      const int64_t o = (((int64_t)n * a.OH + oh) * a.OW + ow) * a.C + c0;
+      const I o = (((I)n * a.OH + oh) * a.OW + ow) * a.C + c0;
       const uint2 id = *reinterpret_cast<const uint2*>(idx + o);
       float g[8];
       VecIO<T>::load(gy + o, g);
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(kBlock) void k_maxpool_bwd_nhwc(PoolArgs a, const T
       }
     }
   }
-  VecIO<T>::store(gx + (((int64_t)n * a.H + ih) * a.W + iw) * a.C + c0, acc);
+  VecIO<T>::store(gx + (((I)n * a.H + ih) * a.W + iw) * a.C + c0, acc);
 }
 
 #define POOL_DISPATCH(code, T, ...)                                        \
@@ -150,9 +152,12 @@ void maxpool_forward_nhwc(const PoolArgs& a, int dt, const void* x, const float*
   if (a.C % 8 != 0 || a.k * a.k > 255) throw std::runtime_error("maxpool_forward_nhwc: needs C % 8 == 0, k*k <= 255");
   const int64_t total = (int64_t)a.N * a.OH * a.OW * (a.C / 8);
   if (total == 0) return;
+  const bool i32 = (int64_t)a.N * a.H * a.W * a.C < (1ll << 31);  // input is the larger tensor
   POOL_DISPATCH(dt, T,
-      hipLaunchKernelGGL((k_maxpool_fwd_nhwc<T>), dim3(blocks_for(total)), dim3(kBlock), 0, st, a, (const T*)x, scale,
-                         shift, (T*)y, idx, counter));
+      if (i32) hipLaunchKernelGGL((k_maxpool_fwd_nhwc<T, uint32_t>), dim3(blocks_for(total)), dim3(kBlock), 0, st, a,
+                                  (const T*)x, scale, shift, (T*)y, idx, counter);
+      else hipLaunchKernelGGL((k_maxpool_fwd_nhwc<T, int64_t>), dim3(blocks_for(total)), dim3(kBlock), 0, st, a,
+                              (const T*)x, scale, shift, (T*)y, idx, counter));
   check_launch("maxpool_forward_nhwc");
 }
 
@@ -160,9 +165,12 @@ void maxpool_backward_nhwc(const PoolArgs& a, int dt, const void* gy, const uint
   if (a.C % 8 != 0) throw std::runtime_error("maxpool_backward_nhwc: needs C % 8 == 0");
   const int64_t total = (int64_t)a.N * a.H * a.W * (a.C / 8);
   if (total == 0) return;
+  const bool i32 = (int64_t)a.N * a.H * a.W * a.C < (1ll << 31);
   POOL_DISPATCH(dt, T,
-      hipLaunchKernelGGL((k_maxpool_bwd_nhwc<T>), dim3(blocks_for(total)), dim3(kBlock), 0, st, a, (const T*)gy, idx,
-                         (T*)gx));
+      if (i32) hipLaunchKernelGGL((k_maxpool_bwd_nhwc<T, uint32_t>), dim3(blocks_for(total)), dim3(kBlock), 0, st, a,
+                                  (const T*)gy, idx, (T*)gx);
+      else hipLaunchKernelGGL((k_maxpool_bwd_nhwc<T, int64_t>), dim3(blocks_for(total)), dim3(kBlock), 0, st, a,
+                              (const T*)gy, idx, (T*)gx));
   check_launch("maxpool_backward_nhwc");
 }
 
