@@ -66,10 +66,10 @@ def _wgrad(x, gy, weight, r, mode, miopen_fn):
     how = _pick((n, c, h, w, gy.size(1), x.dtype, f"wgrad{r}"), lambda: bhconv.conv_wgrad(x, gy, r), miopen_fn, mode)
     if how != "gemm":
         return miopen_fn()
-    gw = bhconv.conv_wgrad(x, gy, r)
-    return gw if gw.stride() == weight.stride() else gw.contiguous(memory_format=torch.channels_last
-                                                                    if weight.is_contiguous(memory_format=torch.channels_last)
-                                                                    else torch.contiguous_format)
+    gw = bhconv.conv_wgrad(x, gy, r)  # channels_last [K, C, r, r]
+    if gw.stride() != weight.stride():  # match the parameter's layout (a contiguous-format weight)
+        gw = gw.contiguous()
+    return gw
 
 
 class _GradStash(torch.autograd.Function):
