@@ -34,8 +34,8 @@ def main():
                     g = "G4" if "Li4E" in name else ("G2" if "Li2E" in name else "G1")
                     name = f"conv3x3_{kind}<{g}>"
                 elif "k_conv_wgrad" in name:
-                    geo = {"Li14ELi2E": "56x56", "Li7ELi4E": "28x28", "Li4ELi7E": "14x14", "Li2ELi7E": "7x7",
-                           "Li28ELi1E": "1x1"}
+                    geo = {"Li3ELi14ELi2E": "3x3 56x56", "Li3ELi7ELi4E": "3x3 28x28", "Li3ELi4ELi7E": "3x3 14x14",
+                           "Li3ELi2ELi7E": "3x3 7x7", "Li1ELi28ELi1E": "1x1"}
                     name = "conv_wgrad<" + next((v for k, v in geo.items() if k in name), "?") + ">"
                 else:
                     continue

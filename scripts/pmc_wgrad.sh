@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 counter passes over the 3x3 conv weight-gradient kernel (benchmarks/bench_conv_wgrad.py, ONLY_R=3)
-export TMPDIR=/tmp ONLY_R=3
+export TMPDIR=/tmp
 mkdir -p gpurun_out/pmcw
 i=0
 for counters in "SQ_WAVES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" \
