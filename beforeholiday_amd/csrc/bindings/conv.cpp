@@ -112,6 +112,24 @@ at::Tensor conv_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t R) {
   return out;
 }
 
+bool stem_ok(const at::Tensor& x, const at::Tensor& w) {
+  return x.is_cuda() && w.is_cuda() && x.dim() == 4 && w.dim() == 4 && x.scalar_type() == w.scalar_type() &&
+         (x.scalar_type() == at::kHalf || x.scalar_type() == at::kBFloat16) &&
+         x.is_contiguous(at::MemoryFormat::ChannelsLast) && w.size(1) == 3 && w.size(2) == 7 && w.size(3) == 7 &&
+         bh::conv_stem_supported((int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), (int)w.size(0)) &&
+         (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0;
+}
+
+// conv2d(x, w, stride 2, padding 3) of the ResNet stem (x [N, 3, 224, 224] channels_last, w [64, 3, 7, 7])
+at::Tensor stem_forward(const at::Tensor& x, const at::Tensor& w) {
+  TORCH_CHECK(stem_ok(x, w), "stem_forward: needs channels_last fp16/bf16 x [N, 3, 224, 224], w [64, 3, 7, 7]");
+  const at::Tensor wc = w.contiguous(at::MemoryFormat::ChannelsLast);  // [64][7][7][3]
+  auto y = at::empty({x.size(0), 64, 112, 112}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  bh::conv_stem_forward(dtype_code(x.scalar_type()), x.data_ptr(), wc.data_ptr(), y.data_ptr(), (int)x.size(0),
+                        stream_for(x));
+  return y;
+}
+
 }  // namespace
 
 void register_conv(pybind11::module_& root) {
@@ -124,6 +142,9 @@ void register_conv(pybind11::module_& root) {
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("grad_out"), py::arg("R"),
         "weight gradient of conv2d(x, w, stride=1, padding=(R-1)//2), R in {1, 3}: [K, C, R, R] channels_last");
   m.def("wgrad_supported", &wgrad_supported, py::arg("x"), py::arg("grad_out"), py::arg("R"));
+  m.def("stem_forward", &stem_forward, py::arg("x"), py::arg("weight"),
+        "ResNet stem conv2d(x, w, stride=2, padding=3), 3 -> 64 channels at 224x224, channels_last fp16 / bf16");
+  m.def("stem_supported", &stem_ok, py::arg("x"), py::arg("weight"));
 }
 
 }  // namespace bhb

@@ -43,4 +43,9 @@ bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo);
 int64_t conv_wgrad_workspace(const ConvWgradGeo& g, const ConvWgradArgs& a);
 void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws, hipStream_t st);
 
+// ResNet stem forward (kernels/conv_stem.hip): 7x7 / stride 2 / pad 3, C = 3 -> K = 64, 224x224 NHWC
+// x [N, 224, 224, 3], w [64, 7, 7, 3], y [N, 112, 112, 64]
+bool conv_stem_supported(int N, int C, int H, int W, int K);
+void conv_stem_forward(int dt, const void* x, const void* w, void* y, int N, hipStream_t st);
+
 }  // namespace bh

@@ -295,6 +295,49 @@ class _Conv1x1S2Fn(torch.autograd.Function):
         return gx, gw, None
 
 
+class _StemConvFn(torch.autograd.Function):
+    """ResNet stem 7x7 / stride 2 / pad 3 convolution: forward on the MFMA stem kernel
+    (kernels/conv_stem.hip) or MIOpen, whichever is faster for the shape (timed once); the
+    weight (and, if needed, input) gradient on MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x, weight, mode):
+        from ..ops import conv as bhconv
+
+        n, c, h, w = x.shape
+        conv = torch.nn.functional.conv2d
+        how = _pick((n, c, h, w, weight.size(0), x.dtype, "stem"), lambda: bhconv.stem_conv(x, weight),
+                    lambda: conv(x, weight, stride=2, padding=3), mode)
+        y = bhconv.stem_conv(x, weight) if how == "gemm" else conv(x, weight, stride=2, padding=3)
+        ctx.save_for_backward(x, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        gx, gw, _ = torch.ops.aten.convolution_backward(gy, x, weight, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
+                                                        [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False])
+        return gx, gw, None
+
+
+class StemConv(nn.Conv2d):
+    """nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False) with the MFMA stem forward (``mode``
+    "auto" times it against MIOpen once, "gemm" forces it, "miopen" is plain nn.Conv2d)."""
+
+    def __init__(self, *args, mode="auto", **kw):
+        super().__init__(*args, **kw)
+        self.mode = mode
+
+    def forward(self, x):
+        if self.mode != "miopen" and x.is_cuda and x.dtype == self.weight.dtype:
+            from ..ops import conv as bhconv
+
+            if bhconv.stem_supported(x, self.weight):
+                return _StemConvFn.apply(x, self.weight, self.mode)
+        return super().forward(x)
+
+
 class Conv1x1S2(nn.Conv2d):
     """nn.Conv2d(k=1, stride=2, bias=False) with the gathered-input GPU path (``_Conv1x1S2Fn``)."""
 
@@ -373,7 +416,11 @@ class ResNet(nn.Module):
         # activation is never materialised); same parameters / state_dict as the unfused stem
         self.stem_pool_fused = fused and stem_pool_fused
         self.inplanes = 64
-        self.conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
+        if _CONV3X3_MODE != "miopen":  # the fused model: MFMA stem forward, timed against MIOpen
+            self.conv1 = StemConv(3, 64, kernel_size=7, stride=2, padding=3, bias=False,
+                                  mode="gemm" if _CONV3X3_MODE == "direct" else _CONV3X3_MODE)
+        else:
+            self.conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
         if self.stem_pool_fused:
             self.bn1 = norm_layer(64, fuse_relu=True, fuse_maxpool=(3, 2, 1))
         else:

@@ -51,3 +51,15 @@ def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, r: int) -> torch.Tensor:
     p = (r - 1) // 2
     return torch.ops.aten.convolution_backward(dy, x, torch.empty(w_shape, device=x.device, dtype=x.dtype), None,
                                                [1, 1], [p, p], [1, 1], False, [0, 0], 1, [False, True, False])[1]
+
+
+def stem_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return x.is_cuda and available() and submodule("conv_cuda").stem_supported(x, w)
+
+
+def stem_conv(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """ResNet stem ``conv2d(x, w, stride=2, padding=3)`` (3 -> 64 channels, 224x224): the MFMA kernel of
+    kernels/conv_stem.hip for channels_last fp16 / bf16, ``F.conv2d`` otherwise."""
+    if stem_supported(x, w):
+        return submodule("conv_cuda").stem_forward(x, w)
+    return F.conv2d(x, w, stride=2, padding=3)

@@ -144,3 +144,38 @@ def test_conv1x1_stride2_module_matches_conv2d(mode):
     assert torch.count_nonzero(xa.grad[:, :, 1::2, :]) == 0  # odd rows / columns get no gradient
     wr = ref.weight.grad.float()
     torch.testing.assert_close(m.weight.grad.float(), wr, rtol=2e-2, atol=1e-2 * wr.abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_stem_conv_kernel(dtype):
+    """kernels/conv_stem.hip (7x7 / stride 2 / pad 3, 3 -> 64 at 224x224) vs fp32 F.conv2d: image
+    borders (zero padding) and every output row block."""
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randn(3, 3, 224, 224, device="cuda", dtype=dtype, generator=g).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(64, 3, 7, 7, device="cuda", dtype=dtype, generator=g) * 0.1).contiguous(
+        memory_format=torch.channels_last)
+    assert bhconv.stem_supported(x, w)
+    y = bhconv.stem_conv(x, w)
+    assert y.shape == (3, 64, 112, 112) and y.is_contiguous(memory_format=torch.channels_last)
+    ref = F.conv2d(x.float(), w.float(), stride=2, padding=3)
+    tol = 2e-2 if dtype == torch.float16 else 6e-2
+    torch.testing.assert_close(y.float(), ref, rtol=tol, atol=tol)
+
+
+@pytest.mark.gpu
+def test_stem_conv_module_grads():
+    from beforeholiday_amd.models.resnet import StemConv
+    torch.manual_seed(0)
+    ref = torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).cuda().half().to(memory_format=torch.channels_last)
+    m = StemConv(3, 64, 7, stride=2, padding=3, bias=False, mode="gemm").cuda().half().to(
+        memory_format=torch.channels_last)
+    m.weight.data.copy_(ref.weight.data)
+    x = torch.randn(2, 3, 224, 224, device="cuda", dtype=torch.half).contiguous(memory_format=torch.channels_last)
+    ya, yb = m(x), ref(x)
+    torch.testing.assert_close(ya.float(), yb.float(), rtol=2e-2, atol=2e-2)
+    g = torch.randn_like(ya)
+    ya.backward(g)
+    yb.backward(g)
+    wr = ref.weight.grad.float()
+    torch.testing.assert_close(m.weight.grad.float(), wr, rtol=5e-2, atol=1e-2 * wr.abs().max().item())
