@@ -6,7 +6,7 @@
 // output pixel p the 21 values j = 0 .. 20 are CONTIGUOUS in the staged input row (input columns
 // 2p - 3 .. 2p + 3, three channels each). One k-step of 32 = one kernel row, padded 21 -> 32 with
 // zero weights, so a B fragment (8 consecutive j of one pixel) is 8 contiguous halves of an LDS row.
-// The weights (64 x 7 x 32 halves) stay in registers for the whole workgroup; each wave computes the
+// The weights (64 x 7 x 32 halves, staged once per persistent workgroup) stay in registers; each wave computes the
 // transposed tile C^T[channel][pixel] (weights as the first operand) for 16 pixels x 64 channels per
 // item, and writes it through an LDS transpose so every pixel's 64 channels leave as one 128-byte row.
 // A workgroup owns four output rows of one image: 13 staged input rows (zero outside the image),
@@ -51,89 +51,97 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const T* __restrict__ x, const
                                                   int N) {
   __shared__ __attribute__((aligned(16))) uint16_t rows[kRowsIn * kRowHalves];
   __shared__ __attribute__((aligned(16))) uint16_t tile[4][16 * kTileStride];
+  __shared__ __attribute__((aligned(16))) uint16_t wl[kK * kR * 32];  // [channel][r][j], j >= 21 zero
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int blk = blockIdx.x;                       // (n, row block)
-  const int n = blk / (kOH / kRowsOut), yb = blk - n * (kOH / kRowsOut);
-  const int iy0 = 2 * kRowsOut * yb - 3;            // input row of staged row 0
   const uint16_t* xs = reinterpret_cast<const uint16_t*>(x);
 
-  // ---- weights -> registers: A fragment (m-tile mt, kernel row r) = 8 halves of j for channel
-  // 16 mt + (lane & 15), j = 8 (lane >> 4) .. + 7 (zero past j = 20) ----
-  i4v wa[4][kR];
+  // ---- weights, once per (persistent) workgroup: coalesced 16-byte loads of the [64][147] tensor,
+  // scattered into the padded [64][7][32] LDS image, then every lane's 28 A fragments (8 halves of j
+  // for channel 16 mt + (lane & 15), j = 8 (lane >> 4) ..) read into registers ----
+  for (int i = tid; i < kK * kR * 32 / 8; i += 256) reinterpret_cast<i4v*>(wl)[i] = i4v{0, 0, 0, 0};
+  __syncthreads();
   {
     const uint16_t* ws = reinterpret_cast<const uint16_t*>(w);
-    const int j0 = 8 * (lane >> 4);
+    for (int i = tid; i < kK * kR * 21 / 8; i += 256) {  // 9408 halves = 1176 chunks
+      const i4v v = reinterpret_cast<const i4v*>(ws)[i];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const int ch = 16 * mt + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < kR; ++r) {
-        uint16_t v[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = (j0 + e < 21) ? ws[(ch * kR + r) * 21 + j0 + e] : (uint16_t)0;
-        wa[mt][r] = i4v{(int)(v[0] | (v[1] << 16)), (int)(v[2] | (v[3] << 16)), (int)(v[4] | (v[5] << 16)),
-                        (int)(v[6] | (v[7] << 16))};
+      for (int e = 0; e < 8; ++e) {
+        const int f = i * 8 + e, cr = f / 21, j = f - cr * 21;  // cr = channel * 7 + r
+        wl[cr * 32 + j] = (uint16_t)((uint32_t)v[e >> 1] >> (16 * (e & 1)));
       }
     }
   }
-
-  // ---- stage 13 input rows: 672 data halves per row (16-byte global loads), zero elsewhere ----
-  for (int i = tid; i < kRowsIn * kRowHalves / 8; i += 256) {
-    const int row = i / (kRowHalves / 8), c8 = i - row * (kRowHalves / 8);
-    reinterpret_cast<i4v*>(rows + row * kRowHalves)[c8] = i4v{0, 0, 0, 0};
-  }
   __syncthreads();
-  for (int i = tid; i < kRowsIn * 84; i += 256) {  // 84 chunks of 8 halves per image row
-    const int row = i / 84, c8 = i - row * 84, iy = iy0 + row;
-    if (iy < 0 || iy >= kH) continue;
-    const i4v v = *reinterpret_cast<const i4v*>(xs + ((int64_t)n * kH + iy) * (kW * 3) + c8 * 8);
-    uint16_t* dst = rows + row * kRowHalves + kLead + c8 * 8;
+  i4v wa[4][kR];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      dst[2 * e] = (uint16_t)(v[e] & 0xffff);
-      dst[2 * e + 1] = (uint16_t)((uint32_t)v[e] >> 16);
-    }
-  }
-  __syncthreads();
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int r = 0; r < kR; ++r)
+      wa[mt][r] = *reinterpret_cast<const i4v*>(wl + ((16 * mt + (lane & 15)) * kR + r) * 32 + 8 * (lane >> 4));
 
-  // ---- 28 items (output row yl, pixel tile pt) over 4 waves ----
+  // the 9 leading and 39 trailing halves of every staged row stay zero (image padding)
+  for (int i = tid; i < kRowsIn * (kRowHalves - 672); i += 256) {
+    const int row = i / (kRowHalves - 672), e = i - row * (kRowHalves - 672);
+    rows[row * kRowHalves + (e < kLead ? e : e + 672)] = 0;
+  }
   uint16_t* tw = tile[wave];
-  for (int item = wave; item < kRowsOut * 7; item += 4) {
-    const int yl = item / 7, pt = item - yl * 7;
-    const int p = pt * 16 + (lane & 15);
-    const int j0 = 8 * (lane >> 4);
-    f4v acc[4];
+  const int nblk = N * (kOH / kRowsOut);
+  for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const int n = blk / (kOH / kRowsOut), yb = blk - n * (kOH / kRowsOut);
+    const int iy0 = 2 * kRowsOut * yb - 3;  // input row of staged row 0
+    // ---- stage 13 input rows: 672 data halves per row (16-byte global loads), zero elsewhere ----
+    __syncthreads();  // the previous block's items are done with `rows`
+    for (int i = tid; i < kRowsIn * 84; i += 256) {  // 84 chunks of 8 halves per image row
+      const int row = i / 84, c8 = i - row * 84, iy = iy0 + row;
+      const i4v v = (iy >= 0 && iy < kH)
+                        ? *reinterpret_cast<const i4v*>(xs + ((int64_t)n * kH + iy) * (kW * 3) + c8 * 8)
+                        : i4v{0, 0, 0, 0};
+      uint16_t* dst = rows + row * kRowHalves + kLead + c8 * 8;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) acc[mt] = f4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < kR; ++r) {
-      // B fragment: halves 6 p + j0 .. + 7 of staged row 2 yl + r (4-byte aligned: four 32-bit reads)
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(rows + (2 * yl + r) * kRowHalves + 6 * p + j0);
-      const i4v b = i4v{(int)src[0], (int)src[1], (int)src[2], (int)src[3]};
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) acc[mt] = Mfma16<T>::run(wa[mt][r], b, acc[mt]);
+      for (int e = 0; e < 4; ++e) {
+        dst[2 * e] = (uint16_t)(v[e] & 0xffff);
+        dst[2 * e + 1] = (uint16_t)((uint32_t)v[e] >> 16);
+      }
     }
-    // lane holds channels 16 mt + 4 (lane >> 4) + i of pixel p: transpose through LDS, then each
-    // pixel's 64 channels leave as one 128-byte row
+    __syncthreads();
+
+    // ---- 28 items (output row yl, pixel tile pt) over 4 waves ----
+    for (int item = wave; item < kRowsOut * 7; item += 4) {
+      const int yl = item / 7, pt = item - yl * 7;
+      const int p = pt * 16 + (lane & 15);
+      const int j0 = 8 * (lane >> 4);
+      f4v acc[4];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      T o[4];
+      for (int mt = 0; mt < 4; ++mt) acc[mt] = f4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) o[i] = from_f<T>(acc[mt][i]);
-      *reinterpret_cast<uint2*>(tw + (lane & 15) * kTileStride + 16 * mt + 4 * (lane >> 4)) =
-          *reinterpret_cast<const uint2*>(o);
+      for (int r = 0; r < kR; ++r) {
+        // B fragment: halves 6 p + j0 .. + 7 of staged row 2 yl + r (4-byte aligned: four 32-bit reads)
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(rows + (2 * yl + r) * kRowHalves + 6 * p + j0);
+        const i4v b = i4v{(int)src[0], (int)src[1], (int)src[2], (int)src[3]};
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[mt] = Mfma16<T>::run(wa[mt][r], b, acc[mt]);
+      }
+      // lane holds channels 16 mt + 4 (lane >> 4) + i of pixel p: transpose through LDS, then each
+      // pixel's 64 channels leave as one 128-byte row
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        T o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = from_f<T>(acc[mt][i]);
+        *reinterpret_cast<uint2*>(tw + (lane & 15) * kTileStride + 16 * mt + 4 * (lane >> 4)) =
+            *reinterpret_cast<const uint2*>(o);
+      }
+      __builtin_amdgcn_wave_barrier();
+      const int oy = kRowsOut * yb + yl;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int q = lane + 64 * h, px = q >> 3, c8 = q & 7;
+        const i4v v = *reinterpret_cast<const i4v*>(tw + px * kTileStride + c8 * 8);
+        *reinterpret_cast<i4v*>(reinterpret_cast<uint16_t*>(y) +
+                                (((int64_t)n * kOH + oy) * kOW + pt * 16 + px) * kK + c8 * 8) = v;
+      }
+      __builtin_amdgcn_wave_barrier();
     }
-    __builtin_amdgcn_wave_barrier();
-    const int oy = kRowsOut * yb + yl;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int q = lane + 64 * h, px = q >> 3, c8 = q & 7;
-      const int op = pt * 16 + px;
-      const i4v v = *reinterpret_cast<const i4v*>(tw + px * kTileStride + c8 * 8);
-      if (op < kOW)
-        *reinterpret_cast<i4v*>(reinterpret_cast<uint16_t*>(y) + (((int64_t)n * kOH + oy) * kOW + op) * kK + c8 * 8) = v;
-    }
-    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -144,7 +152,9 @@ bool conv_stem_supported(int N, int C, int H, int W, int K) {
 }
 
 void conv_stem_forward(int dt, const void* x, const void* w, void* y, int N, hipStream_t st) {
-  const dim3 grid((unsigned)(N * (kOH / kRowsOut)));
+  // persistent: two workgroups per CU (57 KB of LDS each), each walks row blocks blockIdx.x + k * grid
+  const int nblk = N * (kOH / kRowsOut);
+  const dim3 grid((unsigned)(nblk < 512 ? nblk : 512));
   switch (dt) {
     case kF16:
       hipLaunchKernelGGL(k_stem_fwd<f16>, grid, dim3(256), 0, st, (const f16*)x, (const f16*)w, (f16*)y, N);
