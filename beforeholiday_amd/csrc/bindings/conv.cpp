@@ -130,6 +130,23 @@ at::Tensor stem_forward(const at::Tensor& x, const at::Tensor& w) {
   return y;
 }
 
+// weight gradient of stem_forward: [64, 3, 7, 7] channels_last from x and dy [N, 64, 112, 112] channels_last
+at::Tensor stem_wgrad(const at::Tensor& x, const at::Tensor& dy) {
+  TORCH_CHECK(x.is_cuda() && dy.is_cuda() && x.dim() == 4 && dy.dim() == 4 && x.scalar_type() == dy.scalar_type() &&
+                  (x.scalar_type() == at::kHalf || x.scalar_type() == at::kBFloat16) &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  bh::conv_stem_supported((int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), 64) &&
+                  dy.size(0) == x.size(0) && dy.size(1) == 64 && dy.size(2) == 112 && dy.size(3) == 112 &&
+                  (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(dy.data_ptr()) & 15) == 0,
+              "stem_wgrad: needs channels_last fp16/bf16 x [N, 3, 224, 224], dy [N, 64, 112, 112]");
+  auto out = at::empty({64, 3, 7, 7}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto ws = at::empty({(int64_t)bh::conv_stem_wgrad_parts((int)x.size(0)) * 64 * 7 * 21}, x.options().dtype(at::kFloat));
+  bh::conv_stem_wgrad(dtype_code(x.scalar_type()), x.data_ptr(), dy.data_ptr(), out.data_ptr(), ws.data_ptr<float>(),
+                      (int)x.size(0), stream_for(x));
+  return out;
+}
+
 }  // namespace
 
 void register_conv(pybind11::module_& root) {
@@ -145,6 +162,8 @@ void register_conv(pybind11::module_& root) {
   m.def("stem_forward", &stem_forward, py::arg("x"), py::arg("weight"),
         "ResNet stem conv2d(x, w, stride=2, padding=3), 3 -> 64 channels at 224x224, channels_last fp16 / bf16");
   m.def("stem_supported", &stem_ok, py::arg("x"), py::arg("weight"));
+  m.def("stem_wgrad", &stem_wgrad, py::arg("x"), py::arg("grad_out"),
+        "weight gradient of the ResNet stem conv (7x7 / 2, 3 -> 64 at 224x224): [64, 3, 7, 7] channels_last");
 }
 
 }  // namespace bhb

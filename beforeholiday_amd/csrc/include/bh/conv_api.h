@@ -47,5 +47,9 @@ void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws
 // x [N, 224, 224, 3], w [64, 7, 7, 3], y [N, 112, 112, 64]
 bool conv_stem_supported(int N, int C, int H, int W, int K);
 void conv_stem_forward(int dt, const void* x, const void* w, void* y, int N, hipStream_t st);
+// its weight gradient: out [64, 7, 7, 3] from x and dy [N, 112, 112, 64]; ws holds
+// conv_stem_wgrad_parts(N) * 9408 fp32 partials
+int conv_stem_wgrad_parts(int N);
+void conv_stem_wgrad(int dt, const void* x, const void* dy, void* out, float* ws, int N, hipStream_t st);
 
 }  // namespace bh

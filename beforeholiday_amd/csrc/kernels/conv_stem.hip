@@ -145,6 +145,188 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const T* __restrict__ x, const
   }
 }
 
+// ---- weight gradient: dW[k][r][j] = sum over output pixels p of dY[p][k] * X_r[p][j] ----
+// MFMA 32x32x16 with the output channel on the row (A = dY^T) and j on the column (B = X^T), the
+// reduction over 16 pixels per k-step. Both operands come from LDS through ds_read_b64_tr_b16: dY rows
+// (one 128-byte pixel each, 192-byte stride: conflict free) and the staged input rows, where pixel p's
+// 21 values start at half 6p. A transposed read needs 8-byte-aligned rows, which 12p bytes is only for
+// even p, so every input row is staged twice: as is, and shifted by two halves for the odd pixels.
+// j = 21 .. 31 read the next pixels' values (finite) and are dropped. Persistent workgroups walk output
+// rows; wave (mt = wave & 1) owns 32 channels and the kernel rows r = (wave >> 1) + 2 i; each
+// workgroup writes one fp32 partial [64][7][21], summed in a fixed order by k_stem_wgrad_reduce.
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef int i2v __attribute__((ext_vector_type(2)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) s4v* lds_s4_ptr;
+
+template <typename T> struct Mfma32s;
+template <> struct Mfma32s<f16> {
+  static BH_DEVICE f16v run(i4v a, i4v b, f16v c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8v, a), __builtin_bit_cast(h8v, b), c, 0, 0, 0);
+  }
+};
+template <> struct Mfma32s<bf16> {
+  static BH_DEVICE f16v run(i4v a, i4v b, f16v c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(b8v, a), __builtin_bit_cast(b8v, b), c, 0, 0, 0);
+  }
+};
+
+constexpr int kDyStride = 96;      // halves per staged dY pixel (64 + 32 pad: 48-dword stride)
+constexpr int kXRow = 736;         // halves per staged input-row copy (720 + 16)
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_stem_wgrad(const T* __restrict__ x, const T* __restrict__ dy,
+                                                    float* __restrict__ part, int N) {
+  __shared__ __attribute__((aligned(16))) uint16_t dys[kOW * kDyStride];
+  __shared__ __attribute__((aligned(16))) uint16_t xr[kR][2][kXRow];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int mt = wave & 1, rbase = wave >> 1;
+  const uint16_t* xs = reinterpret_cast<const uint16_t*>(x);
+  const uint16_t* ds = reinterpret_cast<const uint16_t*>(dy);
+  // zero padding of the input-row copies (never overwritten: data goes to [kLead, kLead + 672))
+  for (int i = tid; i < kR * 2 * kXRow; i += 256) (&xr[0][0][0])[i] = 0;
+
+  f16v acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+
+  // transposed-read lane roles (16-lane groups): lane 4q + pc names row q, columns 4pc .. 4pc + 3
+  const int g16 = lane >> 4, q = (lane & 15) >> 2, pc = lane & 3, h = lane >> 5;
+  const int nrows = N * kOH;
+  // the next row's dY (896 chunks of 16 B) and input rows (588 chunks) are prefetched into registers
+  // while the current row computes, and stored to LDS after the barrier
+  constexpr int kDC = kOW * 8, kXC = kR * 84;
+  i4v pd[(kDC + 255) / 256], px[(kXC + 255) / 256];
+  auto load_row = [&](int row) {
+    const int n = row / kOH, oy = row - n * kOH;
+#pragma unroll
+    for (int i = 0; i < (kDC + 255) / 256; ++i) {
+      const int c = tid + 256 * i, pxl = c >> 3, c8 = c & 7;
+      if (c < kDC) pd[i] = *reinterpret_cast<const i4v*>(ds + (((int64_t)n * kOH + oy) * kOW + pxl) * kK + c8 * 8);
+    }
+#pragma unroll
+    for (int i = 0; i < (kXC + 255) / 256; ++i) {
+      const int c = tid + 256 * i, r = c / 84, c8 = c - r * 84, iy = 2 * oy - 3 + r;
+      px[i] = (c < kXC && iy >= 0 && iy < kH)
+                  ? *reinterpret_cast<const i4v*>(xs + ((int64_t)n * kH + iy) * (kW * 3) + c8 * 8)
+                  : i4v{0, 0, 0, 0};
+    }
+  };
+  auto store_row = [&]() {
+#pragma unroll
+    for (int i = 0; i < (kDC + 255) / 256; ++i) {
+      const int c = tid + 256 * i;
+      if (c < kDC) *reinterpret_cast<i4v*>(dys + (c >> 3) * kDyStride + (c & 7) * 8) = pd[i];
+    }
+#pragma unroll
+    for (int i = 0; i < (kXC + 255) / 256; ++i) {
+      const int c = tid + 256 * i;
+      if (c >= kXC) continue;
+      const int r = c / 84, c8 = c - r * 84;
+      uint16_t* d0 = &xr[r][0][kLead + c8 * 8];
+      uint16_t* d1 = &xr[r][1][kLead + c8 * 8 + 2];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint16_t lo = (uint16_t)(px[i][e] & 0xffff), hi = (uint16_t)((uint32_t)px[i][e] >> 16);
+        d0[2 * e] = lo;
+        d0[2 * e + 1] = hi;
+        d1[2 * e] = lo;
+        d1[2 * e + 1] = hi;
+      }
+    }
+  };
+  if (blockIdx.x < nrows) load_row(blockIdx.x);
+  __syncthreads();  // zero padding written
+  store_row();
+  __syncthreads();
+  for (int row = blockIdx.x; row < nrows; row += gridDim.x) {
+    const int next = row + gridDim.x;
+    if (next < nrows) load_row(next);
+#pragma unroll
+    for (int ks = 0; ks < kOW / 16; ++ks) {
+      // A = dY^T: lane (channel 32 mt + (lane & 31), half h) gets pixels 16 ks + 8 h .. + 7
+      const int col = 32 * mt + 16 * (g16 & 1) + 4 * pc;
+      const int pA = 16 * ks + 8 * h + q;
+      const s4v a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(dys + pA * kDyStride + col));
+      const s4v a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)(dys + (pA + 4) * kDyStride + col));
+      const i2v la = __builtin_bit_cast(i2v, a0), ha = __builtin_bit_cast(i2v, a1);
+      const i4v fa = i4v{la[0], la[1], ha[0], ha[1]};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int r = rbase + 2 * t;
+        if (r >= kR) break;  // wave-uniform
+        // B = X_r^T: lane (j = (lane & 31), half h) gets pixels 16 ks + 8 h .. + 7; row p starts at
+        // half 6p of copy 0 (even p) or at half 6p + 2 of copy 1 (odd p)
+        const int j = 16 * (g16 & 1) + 4 * pc;
+        auto xaddr = [&](int p) {
+          return (p & 1) ? &xr[r][1][6 * p + 2 + j] : &xr[r][0][6 * p + j];
+        };
+        const s4v b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)xaddr(pA));
+        const s4v b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_ptr)xaddr(pA + 4));
+        const i2v lb = __builtin_bit_cast(i2v, b0), hb = __builtin_bit_cast(i2v, b1);
+        acc[t] = Mfma32s<T>::run(fa, i4v{lb[0], lb[1], hb[0], hb[1]}, acc[t]);
+      }
+    }
+    __syncthreads();  // everyone is done with this row's tiles
+    if (next < nrows) {
+      store_row();
+      __syncthreads();
+    }
+  }
+  // lane holds j = lane & 31 and channels 32 mt + 8 i + 4 h + e (acc[t][4 i + e]) of kernel row r
+  const int jj = lane & 31;
+  if (jj < 21) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int r = rbase + 2 * t;
+      if (r >= kR) break;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int ch = 32 * mt + 8 * i + 4 * h + e;
+          part[(int64_t)blockIdx.x * (kK * kR * 21) + (ch * kR + r) * 21 + jj] = acc[t][4 * i + e];
+        }
+    }
+  }
+}
+
+// out[i] = sum over the workgroups' partials in a fixed order: a block owns 64 outputs (16 float4
+// quads) x 16 partial groups (group g sums partials g, g + 16, ...), the groups added in order in LDS
+template <typename T>
+__global__ __launch_bounds__(256) void k_stem_wgrad_reduce(const float* __restrict__ part, int parts, T* __restrict__ out) {
+  constexpr int kN = kK * kR * 21;  // 9408 = 147 blocks x 64
+  __shared__ float4 red[16][16];
+  const int tq = threadIdx.x & 15, sg = threadIdx.x >> 4;
+  const int i = (blockIdx.x * 16 + tq) * 4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int b = sg; b < parts; b += 16) {
+    const float4 v = *reinterpret_cast<const float4*>(part + (int64_t)b * kN + i);
+    acc.x += v.x;
+    acc.y += v.y;
+    acc.z += v.z;
+    acc.w += v.w;
+  }
+  red[sg][tq] = acc;
+  __syncthreads();
+  if (sg == 0) {
+    float4 t = red[0][tq];
+#pragma unroll
+    for (int k = 1; k < 16; ++k) {
+      t.x += red[k][tq].x;
+      t.y += red[k][tq].y;
+      t.z += red[k][tq].z;
+      t.w += red[k][tq].w;
+    }
+    out[i] = from_f<T>(t.x);
+    out[i + 1] = from_f<T>(t.y);
+    out[i + 2] = from_f<T>(t.z);
+    out[i + 3] = from_f<T>(t.w);
+  }
+}
+
 }  // namespace
 
 bool conv_stem_supported(int N, int C, int H, int W, int K) {
@@ -168,4 +350,24 @@ void conv_stem_forward(int dt, const void* x, const void* w, void* y, int N, hip
   if (e != hipSuccess) throw std::runtime_error(std::string("conv_stem_forward: ") + hipGetErrorString(e));
 }
 
+}  // namespace bh
+
+namespace bh {
+int conv_stem_wgrad_parts(int N) { return N * kOH < 512 ? N * kOH : 512; }
+
+void conv_stem_wgrad(int dt, const void* x, const void* dy, void* out, float* ws, int N, hipStream_t st) {
+  const int parts = conv_stem_wgrad_parts(N);
+  auto run = [&](auto tt) {
+    using T = typename decltype(tt)::type;
+    hipLaunchKernelGGL(k_stem_wgrad<T>, dim3(parts), dim3(256), 0, st, (const T*)x, (const T*)dy, ws, N);
+    hipLaunchKernelGGL(k_stem_wgrad_reduce<T>, dim3(kK * kR * 21 / 64), dim3(256), 0, st, ws, parts, (T*)out);
+  };
+  switch (dt) {
+    case kF16: run(std::common_type<f16>{}); break;
+    case kBF16: run(std::common_type<bf16>{}); break;
+    default: throw std::runtime_error("conv_stem_wgrad: fp16 / bf16 only");
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("conv_stem_wgrad: ") + hipGetErrorString(e));
+}
 }  // namespace bh

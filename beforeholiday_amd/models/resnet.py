@@ -296,9 +296,9 @@ class _Conv1x1S2Fn(torch.autograd.Function):
 
 
 class _StemConvFn(torch.autograd.Function):
-    """ResNet stem 7x7 / stride 2 / pad 3 convolution: forward on the MFMA stem kernel
-    (kernels/conv_stem.hip) or MIOpen, whichever is faster for the shape (timed once); the
-    weight (and, if needed, input) gradient on MIOpen."""
+    """ResNet stem 7x7 / stride 2 / pad 3 convolution: forward and weight gradient on the MFMA stem
+    kernels (kernels/conv_stem.hip) or MIOpen, whichever is faster for the shape (timed once); the
+    input gradient (not needed for the image input) on MIOpen."""
 
     @staticmethod
     def forward(ctx, x, weight, mode):
@@ -310,14 +310,28 @@ class _StemConvFn(torch.autograd.Function):
                     lambda: conv(x, weight, stride=2, padding=3), mode)
         y = bhconv.stem_conv(x, weight) if how == "gemm" else conv(x, weight, stride=2, padding=3)
         ctx.save_for_backward(x, weight)
+        ctx.mode = mode
         return y
 
     @staticmethod
     def backward(ctx, gy):
+        from ..ops import conv as bhconv
+
         x, weight = ctx.saved_tensors
         gy = gy.contiguous(memory_format=torch.channels_last)
-        gx, gw, _ = torch.ops.aten.convolution_backward(gy, x, weight, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
-                                                        [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False])
+        conv_bwd = torch.ops.aten.convolution_backward
+        args = ([2, 2], [3, 3], [1, 1], False, [0, 0], 1)
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            gx = conv_bwd(gy, x, weight, None, *args, [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            n, c, h, w = x.shape
+            miopen = lambda: conv_bwd(gy, x, weight, None, *args, [False, True, False])[1]  # noqa: E731
+            how = _pick((n, c, h, w, weight.size(0), x.dtype, "stem_wgrad"), lambda: bhconv.stem_wgrad(x, gy), miopen,
+                        ctx.mode)
+            gw = bhconv.stem_wgrad(x, gy) if how == "gemm" else miopen()
+            if gw.stride() != weight.stride():
+                gw = gw.contiguous()
         return gx, gw, None
 
 

@@ -63,3 +63,13 @@ def stem_conv(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     if stem_supported(x, w):
         return submodule("conv_cuda").stem_forward(x, w)
     return F.conv2d(x, w, stride=2, padding=3)
+
+
+def stem_wgrad(x: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
+    """Weight gradient of :func:`stem_conv` (kernels/conv_stem.hip, MFMA over transposed LDS reads of
+    dY and of the staged input rows); ``convolution_backward`` otherwise."""
+    w = torch.empty(dy.size(1), x.size(1), 7, 7, device=x.device, dtype=x.dtype)
+    if stem_supported(x, w) and dy.is_contiguous(memory_format=torch.channels_last):
+        return submodule("conv_cuda").stem_wgrad(x, dy)
+    return torch.ops.aten.convolution_backward(dy, x, w, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
+                                               [False, True, False])[1]

@@ -41,8 +41,13 @@ def main():
             if bhconv.stem_supported(x, w):
                 t = t_ms(lambda: bhconv.stem_conv(x, w))
                 err = ((bhconv.stem_conv(x, w).float() - y.float()).abs().max() / y.float().abs().max()).item()
+                tw = t_ms(lambda: bhconv.stem_wgrad(x, gy))
+                ref_w = torch.ops.aten.convolution_backward(gy, x, w, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
+                                                            [False, True, False])[1].float()
+                werr = ((bhconv.stem_wgrad(x, gy).float() - ref_w).abs().max() / ref_w.abs().max()).item()
                 rec.update(mfma_stem_fwd_ms=round(t, 4), mfma_stem_tflops=round(2 * 256 * 112 * 112 * 64 * 147 / t / 1e9, 1),
-                           rel_err_vs_miopen=round(err, 5))
+                           rel_err_vs_miopen=round(err, 5), mfma_stem_wgrad_ms=round(tw, 4),
+                           wgrad_rel_err_vs_miopen=round(werr, 5))
         print(json.dumps(rec), flush=True)
 
 

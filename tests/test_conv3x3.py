@@ -179,3 +179,20 @@ def test_stem_conv_module_grads():
     yb.backward(g)
     wr = ref.weight.grad.float()
     torch.testing.assert_close(m.weight.grad.float(), wr, rtol=5e-2, atol=1e-2 * wr.abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_stem_wgrad_kernel(dtype):
+    """kernels/conv_stem.hip weight gradient vs fp32 torch.nn.grad.conv2d_weight (image borders,
+    several persistent row walks: 3 images x 112 rows over at most 512 workgroups)."""
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.randn(5, 3, 224, 224, device="cuda", dtype=dtype, generator=g).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(5, 64, 112, 112, device="cuda", dtype=dtype, generator=g).contiguous(
+        memory_format=torch.channels_last)
+    gw = bhconv.stem_wgrad(x, dy)
+    assert gw.shape == (64, 3, 7, 7) and gw.dtype == dtype
+    ref = torch.nn.grad.conv2d_weight(x.float(), (64, 3, 7, 7), dy.float(), stride=2, padding=3)
+    tol = 1e-2 if dtype == torch.float16 else 2e-2
+    torch.testing.assert_close(gw.float(), ref, rtol=tol, atol=tol * ref.abs().max().item())
+    assert torch.equal(gw, bhconv.stem_wgrad(x, dy))  # fixed-order reduction
