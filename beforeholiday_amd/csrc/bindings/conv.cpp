@@ -67,41 +67,43 @@ at::Tensor conv3x3_dgrad(const at::Tensor& dy, const at::Tensor& w) {
 
 // dW of y = conv2d(x, w, stride 1, padding (R-1)/2) for channels_last x [N, C, H, W], dy [N, K, H, W];
 // returns [K, C, R, R] channels_last (memory [K][R][R][C])
-bool wgrad_ok(const at::Tensor& x, const at::Tensor& dy, int64_t R) {
+bool wgrad_ok(const at::Tensor& x, const at::Tensor& dy, int64_t R, int64_t stride = 1) {
   return x.is_cuda() && dy.is_cuda() && x.dim() == 4 && dy.dim() == 4 && x.size(0) == dy.size(0) &&
-         x.size(2) == dy.size(2) && x.size(3) == dy.size(3) && x.scalar_type() == dy.scalar_type() &&
+         (stride == 1 || (stride == 2 && R == 1)) && x.size(2) == stride * dy.size(2) &&
+         x.size(3) == stride * dy.size(3) && x.scalar_type() == dy.scalar_type() &&
          (x.scalar_type() == at::kHalf || x.scalar_type() == at::kBFloat16) &&
          x.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
          (R == 1 || R == 3) && x.size(1) % 64 == 0 && dy.size(1) % 64 == 0 &&
          x.numel() < (int64_t(1) << 40);
 }
 
-bh::ConvWgradArgs wgrad_args(const at::Tensor& x, const at::Tensor& dy, int64_t R) {
+bh::ConvWgradArgs wgrad_args(const at::Tensor& x, const at::Tensor& dy, int64_t R, int64_t stride) {
   bh::ConvWgradArgs a;
   a.x = x.data_ptr();
   a.dy = dy.data_ptr();
   a.N = (int)x.size(0);
   a.C = (int)x.size(1);
-  a.H = (int)x.size(2);
-  a.W = (int)x.size(3);
+  a.H = (int)dy.size(2);  // output (dY) geometry; x is stride x larger
+  a.W = (int)dy.size(3);
   a.K = (int)dy.size(1);
   a.R = (int)R;
+  a.stride = (int)stride;
   return a;
 }
 
-bool wgrad_supported(const at::Tensor& x, const at::Tensor& dy, int64_t R) {
-  if (!wgrad_ok(x, dy, R)) return false;
+bool wgrad_supported(const at::Tensor& x, const at::Tensor& dy, int64_t R, int64_t stride) {
+  if (!wgrad_ok(x, dy, R, stride)) return false;
   bh::ConvWgradGeo g;
-  auto a = wgrad_args(x, dy, R);
+  auto a = wgrad_args(x, dy, R, stride);
   a.out = x.data_ptr();  // alignment probe only
   return bh::conv_wgrad_plan(a, &g);
 }
 
-at::Tensor conv_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t R) {
-  TORCH_CHECK(wgrad_ok(x, dy, R), "conv_wgrad: needs channels_last fp16/bf16 x [N, C, H, W], dy [N, K, H, W], "
-                                  "C and K % 64 == 0, R in {1, 3}");
+at::Tensor conv_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t R, int64_t stride) {
+  TORCH_CHECK(wgrad_ok(x, dy, R, stride), "conv_wgrad: needs channels_last fp16/bf16 x [N, C, sH, sW], "
+                                          "dy [N, K, H, W], C and K % 64 == 0, R in {1, 3}, stride 2 only for R = 1");
   auto out = at::empty({dy.size(1), x.size(1), R, R}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  auto a = wgrad_args(x, dy, R);
+  auto a = wgrad_args(x, dy, R, stride);
   a.out = out.data_ptr();
   bh::ConvWgradGeo g;
   TORCH_CHECK(bh::conv_wgrad_plan(a, &g), "conv_wgrad: shape not covered (window does not fit in LDS / unaligned)");
@@ -156,9 +158,10 @@ void register_conv(pybind11::module_& root) {
   m.def("conv3x3_dgrad", &conv3x3_dgrad, py::arg("grad_out"), py::arg("weight"),
         "grad of conv2d(x, weight, stride=1, padding=1) w.r.t. x, straight from the forward weight");
   m.def("supported", &supported, py::arg("x"), py::arg("weight"));
-  m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("grad_out"), py::arg("R"),
-        "weight gradient of conv2d(x, w, stride=1, padding=(R-1)//2), R in {1, 3}: [K, C, R, R] channels_last");
-  m.def("wgrad_supported", &wgrad_supported, py::arg("x"), py::arg("grad_out"), py::arg("R"));
+  m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("grad_out"), py::arg("R"), py::arg("stride") = 1,
+        "weight gradient of conv2d(x, w, stride, padding=(R-1)//2), R in {1, 3} (stride 2: R = 1): [K, C, R, R] "
+        "channels_last");
+  m.def("wgrad_supported", &wgrad_supported, py::arg("x"), py::arg("grad_out"), py::arg("R"), py::arg("stride") = 1);
   m.def("stem_forward", &stem_forward, py::arg("x"), py::arg("weight"),
         "ResNet stem conv2d(x, w, stride=2, padding=3), 3 -> 64 channels at 224x224, channels_last fp16 / bf16");
   m.def("stem_supported", &stem_ok, py::arg("x"), py::arg("weight"));

@@ -29,10 +29,12 @@ void conv3x3_dgrad(int dt, const Conv3x3Args& a, hipStream_t st);
 // Weight gradient of a stride-1 "same" R x R convolution (R = 1 or 3, pad (R-1)/2), kernels/conv_wgrad.hip:
 // out[k][r][s][c] = sum over pixels of dy[n, y, x, k] * x[n, y + r - P, x + s - P, c].
 struct ConvWgradArgs {
-  const void* x = nullptr;   // [N, H, W, C]
+  const void* x = nullptr;   // [N, stride H, stride W, C]
   const void* dy = nullptr;  // [N, H, W, K]
   void* out = nullptr;       // [K, R, R, C]
   int N = 0, H = 0, W = 0, C = 0, K = 0, R = 3;
+  int stride = 1;            // 2: 1x1 / stride-2 convolution (R = 1; dY pixel (y, x) reads x pixel (2y, 2x))
+  int wout = 0;              // set by the launcher: the real output width of a flattened 1x1 problem
 };
 struct ConvWgradGeo {
   int G4 = 0, TH = 0, ksteps = 0, wpi = 0, nwin = 0, ctiles = 0, tiles = 0, wpw = 0, splits = 0, grid = 0, kt = 1, ct = 1, parts = 0;

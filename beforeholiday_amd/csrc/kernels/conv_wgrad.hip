@@ -142,7 +142,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
   const int C = a.C, K = a.K, H = a.H, W = a.W;
   // whole-tensor buffer resources: a pixel outside the image (or a pad chunk) gets an offset past
   // the range and lands in LDS as zeros (no clamped pointers, no select)
-  const i4v rsX = make_rsrc(a.x, (int64_t)a.N * H * W * C * 2);
+  const int sx = a.stride * a.stride;  // x pixels per dY pixel
+  const i4v rsX = make_rsrc(a.x, (int64_t)a.N * H * W * C * 2 * sx);
   const i4v rsD = make_rsrc(a.dy, (int64_t)a.N * H * W * K * 2);
   constexpr int kOut = 0x7ff00000;  // any offset past both ranges
   // LDS-DMA is lane-linear: lane l of piece j fills bytes [1024 j + 16 l, +16) = one 16-byte chunk
@@ -160,7 +161,11 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
     if (isx) {
       const int hr = slot / HC, x = slot - hr * HC - P;
       const bool ok = piece < XP && ch < 8 * CT && slot < XS && x >= 0 && x < W;
-      rel[i] = (((hr - P) * W + x) * C + c0 + ch * 8) * 2;
+      // 1x1 / stride 2 (flat windows of whole output rows): dY pixel x of the window reads x pixel
+      // 2 x + 2 wout (x / wout) from the window's x origin (input rows are twice as long, and every
+      // other one is skipped)
+      const int xin = a.stride == 2 ? 2 * x + 2 * a.wout * (x / a.wout) : x;
+      rel[i] = (((hr - P) * W + xin) * C + c0 + ch * 8) * 2;
       hrow[i] = ok ? hr - P : kBad;
     } else {
       const int dbyte = byte, dsl = dbyte / DSL, dch = (dbyte - dsl * DSL) >> 4;
@@ -177,7 +182,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
     if (piece >= (isx ? XP : DP)) return;
     const int y = y0 + hrow[i];
     const bool ok = hrow[i] != kBad && y >= 0 && y < H;
-    const int off = ok ? (n * H + y0) * W * (isx ? C : K) * 2 + rel[i] : kOut;
+    const int off = ok ? (n * H + y0) * W * (isx ? C * sx : K) * 2 + rel[i] : kOut;
     if (isx) dma16(rsX, off, __builtin_amdgcn_readfirstlane(lds_addr(buf + piece * 1024)));
     else dma16(rsD, off, __builtin_amdgcn_readfirstlane(lds_addr(buf + BUFX + piece * 1024)));
   };
@@ -380,8 +385,10 @@ bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo) {
   if (!(a.R == 1 || a.R == 3) || a.N <= 0 || a.H <= 0 || a.W <= 0 || a.C % kTile || a.K % kTile || !al(a.x) ||
       !al(a.dy) || !al(a.out))
     return false;
+  // stride 2: 1x1 only, windows of whole output rows (W divides 112)
+  if (!(a.stride == 1 || (a.stride == 2 && a.R == 1 && 112 % a.W == 0))) return false;
   // 32-bit buffer offsets (the out-of-image offset sits past both tensors)
-  if (2 * (int64_t)a.N * a.H * a.W * std::max(a.C, a.K) >= 0x7ff00000ll) return false;
+  if (2 * (int64_t)a.N * a.H * a.W * std::max(a.C * a.stride * a.stride, a.K) >= 0x7ff00000ll) return false;
   ConvWgradGeo g;
   if (a.R == 1) {
     // no halo: the N*H*W pixels are one flat list, 112-pixel windows (one row of 28 groups)
@@ -426,6 +433,7 @@ void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws
   const int64_t n = (int64_t)a.K * a.C * a.R * a.R;
   ConvWgradArgs b = a;
   if (a.R == 1) {  // flat pixel list: windows are the rows of an [nwin, 1, 112] image
+    b.wout = a.W;
     b.N = g.nwin;
     b.H = 1;
     b.W = 112;

@@ -295,6 +295,42 @@ class _Conv1x1S2Fn(torch.autograd.Function):
         return gx, gw, None
 
 
+class _Conv1x1S2WFn(torch.autograd.Function):
+    """1x1 / stride-2 convolution: forward and data gradient on MIOpen, the weight gradient on the
+    MFMA wgrad kernel reading the even input pixels in place (``conv_wgrad(..., stride=2)``, no
+    gathered copy) or MIOpen, whichever is faster for the shape (timed once)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, mode):
+        ctx.save_for_backward(x, weight)
+        ctx.mode = mode
+        return torch.nn.functional.conv2d(x, weight, stride=2)
+
+    @staticmethod
+    def backward(ctx, gy):
+        from ..ops import conv as bhconv
+
+        x, weight = ctx.saved_tensors
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        conv_bwd = torch.ops.aten.convolution_backward
+        args = ([2, 2], [0, 0], [1, 1], False, [0, 0], 1)
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            gx = conv_bwd(gy, x, weight, None, *args, [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            miopen = lambda: conv_bwd(gy, x, weight, None, *args, [False, True, False])[1]  # noqa: E731
+            mode = "miopen" if os.environ.get("BH_CONV_WGRAD") == "miopen" else ctx.mode
+            if mode == "miopen" or not bhconv.wgrad_supported(x, gy, 1, 2):
+                return gx, miopen(), None
+            n, c, h, w = x.shape
+            how = _pick((n, c, h, w, weight.size(0), x.dtype, "wgrad1s2"), lambda: bhconv.conv_wgrad_s2(x, gy), miopen,
+                        mode)
+            gw = bhconv.conv_wgrad_s2(x, gy) if how == "gemm" else miopen()
+            if gw.stride() != weight.stride():
+                gw = gw.contiguous()
+        return gx, gw, None
+
+
 class _StemConvFn(torch.autograd.Function):
     """ResNet stem 7x7 / stride 2 / pad 3 convolution: forward and weight gradient on the MFMA stem
     kernels (kernels/conv_stem.hip) or MIOpen, whichever is faster for the shape (timed once); the
@@ -353,27 +389,32 @@ class StemConv(nn.Conv2d):
 
 
 class Conv1x1S2(nn.Conv2d):
-    """nn.Conv2d(k=1, stride=2, bias=False) with the gathered-input GPU path (``_Conv1x1S2Fn``)."""
+    """nn.Conv2d(k=1, stride=2, bias=False): MIOpen forward / data gradient with the in-place
+    stride-2 MFMA weight gradient (``_Conv1x1S2WFn``), or with ``gather=True`` the gathered-input
+    GEMM path (``_Conv1x1S2Fn``)."""
 
-    def __init__(self, *args, mode="auto", **kw):
+    def __init__(self, *args, mode="auto", gather=False, **kw):
         super().__init__(*args, **kw)
         self.mode = mode
+        self.gather = gather
 
     def forward(self, x):
         if (x.is_cuda and self.mode != "miopen" and x.dim() == 4 and x.dtype == self.weight.dtype
                 and x.is_contiguous(memory_format=torch.channels_last) and x.size(2) % 2 == 0 and x.size(3) % 2 == 0):
-            return _Conv1x1S2Fn.apply(x, self.weight, self.mode)
+            fn = _Conv1x1S2Fn if self.gather else _Conv1x1S2WFn
+            return fn.apply(x, self.weight, self.mode)
         return super().forward(x)
 
 
 def conv1x1(cin, cout, stride=1):
     if _CONV1X1_MODE != "miopen" and stride == 1:
         return Conv1x1(cin, cout, 1, stride=stride, bias=False, mode=_CONV1X1_MODE)
-    # opt-in (BH_CONV1X1_S2=1): measured 27.7 vs 26.4 ms per ResNet-50 step on the same box, the
-    # strided gather / zero-fill + scatter cost more than MIOpen's stride-2 kernels
-    # (profiles/resnet50_conv1x1_s2_ab.txt)
-    if _CONV1X1_MODE != "miopen" and stride == 2 and os.environ.get("BH_CONV1X1_S2", "0") == "1":
-        return Conv1x1S2(cin, cout, 1, stride=2, bias=False, mode=_CONV1X1_MODE)
+    # the gathered-input path is opt-in (BH_CONV1X1_S2=gather): measured 27.7 vs 26.4 ms per
+    # ResNet-50 step on the same box, the strided gather / zero-fill + scatter cost more than
+    # MIOpen's stride-2 kernels (profiles/resnet50_conv1x1_s2_ab.txt); BH_CONV1X1_S2=0 is plain MIOpen
+    s2 = os.environ.get("BH_CONV1X1_S2", "wgrad")
+    if _CONV1X1_MODE != "miopen" and stride == 2 and s2 in ("wgrad", "gather"):
+        return Conv1x1S2(cin, cout, 1, stride=2, bias=False, mode=_CONV1X1_MODE, gather=s2 == "gather")
     return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
 
 

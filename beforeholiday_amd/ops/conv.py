@@ -36,8 +36,18 @@ def conv3x3_dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return F.conv2d(dy, dgrad_weight(w), stride=1, padding=1)
 
 
-def wgrad_supported(x: torch.Tensor, dy: torch.Tensor, r: int) -> bool:
-    return x.is_cuda and available() and submodule("conv_cuda").wgrad_supported(x, dy, r)
+def wgrad_supported(x: torch.Tensor, dy: torch.Tensor, r: int, stride: int = 1) -> bool:
+    return x.is_cuda and available() and submodule("conv_cuda").wgrad_supported(x, dy, r, stride)
+
+
+def conv_wgrad_s2(x: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
+    """Weight gradient of a 1x1 / stride-2 convolution (the ResNet downsample) on the MFMA wgrad
+    kernel, reading x at the even pixels straight from memory (no gathered copy)."""
+    if wgrad_supported(x, dy, 1, 2):
+        return submodule("conv_cuda").conv_wgrad(x, dy, 1, 2)
+    w = torch.empty(dy.size(1), x.size(1), 1, 1, device=x.device, dtype=x.dtype)
+    return torch.ops.aten.convolution_backward(dy, x, w, None, [2, 2], [0, 0], [1, 1], False, [0, 0], 1,
+                                               [False, True, False])[1]
 
 
 def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, r: int) -> torch.Tensor:

@@ -121,16 +121,45 @@ def test_conv_wgrad_fallback_shapes():
                                atol=2e-2 * ref1.abs().max().item())
 
 
+S2_SHAPES = [  # N, C, K, H_in, W_in: the ResNet-50 downsample layers (output pixel counts a multiple of 112)
+    (4, 256, 512, 56, 56), (4, 512, 1024, 28, 28), (16, 1024, 2048, 14, 14), (16, 64, 128, 14, 14),
+]
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("shape", S2_SHAPES)
+def test_conv_wgrad_stride2_kernel(dtype, shape):
+    """1x1 / stride-2 weight gradient on the MFMA wgrad kernel (x read at the even pixels in place)
+    vs fp32 torch.nn.grad.conv2d_weight(stride=2)."""
+    N, C, K, H, W = shape
+    g = torch.Generator(device="cuda").manual_seed(N * 10 + C + K + H)
+    x = torch.randn(N, C, H, W, device="cuda", dtype=dtype, generator=g).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(N, K, H // 2, W // 2, device="cuda", dtype=dtype, generator=g).contiguous(
+        memory_format=torch.channels_last)
+    assert bhconv.wgrad_supported(x, dy, 1, 2)
+    assert not bhconv.wgrad_supported(x, dy, 1)  # shape mismatch at stride 1
+    gw = bhconv.conv_wgrad_s2(x, dy)
+    assert gw.shape == (K, C, 1, 1) and gw.dtype == dtype
+    ref = torch.nn.grad.conv2d_weight(x.float(), (K, C, 1, 1), dy.float(), stride=2)
+    tol = 1e-2 if dtype == torch.float16 else 2e-2
+    torch.testing.assert_close(gw.float(), ref, rtol=tol, atol=tol * ref.abs().max().item())
+    assert torch.equal(gw, bhconv.conv_wgrad_s2(x, dy))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gather", [False, True])
 @pytest.mark.parametrize("mode", ["gemm", "auto"])
-def test_conv1x1_stride2_module_matches_conv2d(mode):
-    """ResNet downsample 1x1 / stride 2 (models/resnet.py Conv1x1S2, opt-in BH_CONV1X1_S2=1: gathered
-    quarter-resolution input, GEMM forward, GEMM + scatter data gradient, MFMA wgrad kernel) vs
-    nn.Conv2d(stride=2)."""
+def test_conv1x1_stride2_module_matches_conv2d(mode, gather):
+    """ResNet downsample 1x1 / stride 2 (models/resnet.py Conv1x1S2) vs nn.Conv2d(stride=2): the
+    default path (MIOpen forward / data gradient, in-place stride-2 MFMA wgrad) and the gathered
+    path (BH_CONV1X1_S2=gather: quarter-resolution input, GEMM forward, GEMM + scatter data
+    gradient, MFMA wgrad kernel)."""
     from beforeholiday_amd.models.resnet import Conv1x1S2
     torch.manual_seed(0)
     ref = torch.nn.Conv2d(256, 512, 1, stride=2, bias=False).cuda().half().to(memory_format=torch.channels_last)
-    m = Conv1x1S2(256, 512, 1, stride=2, bias=False, mode=mode).cuda().half().to(memory_format=torch.channels_last)
+    m = Conv1x1S2(256, 512, 1, stride=2, bias=False, mode=mode, gather=gather).cuda().half().to(
+        memory_format=torch.channels_last)
     m.weight.data.copy_(ref.weight.data)
     x = torch.randn(16, 256, 28, 28, device="cuda", dtype=torch.half).contiguous(memory_format=torch.channels_last)
     xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
