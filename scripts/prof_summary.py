@@ -82,6 +82,18 @@ def main():
         if t / n / 1e6 < 0.5:
             break
         lines.append(f"* `{k[:60]}`: {per[k]}")
+    # neighbours of library helper kernels (fills, copies) in the last step: which op launched them
+    helpers = re.compile(os.environ.get("PROF_NEIGHBOURS", r"SubTensorOp|copyBuffer|fillBuffer"))
+    pairs = collections.Counter()
+    for i, (s_, e_, name) in enumerate(last):
+        if helpers.search(name):
+            before = short(last[i - 1][2]) if i > 0 else "-"
+            after = short(last[i + 1][2]) if i + 1 < len(last) else "-"
+            pairs[(short(name), before, after)] += 1
+    if pairs:
+        lines.append("\n## helper kernels in the last step: (kernel, launched after, launched before) x count\n")
+        for (k, b_, a_), c in pairs.most_common(20):
+            lines.append(f"* {c} x `{k}` after `{b_}` before `{a_}`")
     text = "\n".join(lines) + "\n"
     with open(out, "w") as fh:
         fh.write(text)
