@@ -3,6 +3,7 @@
 #include "common.h"
 
 #include "bh/conv_api.h"
+#include "bh/dense_api.h"
 
 namespace bhb {
 namespace {
@@ -132,6 +133,28 @@ at::Tensor stem_forward(const at::Tensor& x, const at::Tensor& w) {
   return y;
 }
 
+bool gemm_n64_ok(const at::Tensor& a, const at::Tensor& b) {
+  auto al = [](const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0; };
+  return a.is_cuda() && b.is_cuda() && a.dim() == 2 && b.dim() == 2 && a.scalar_type() == b.scalar_type() &&
+         (a.scalar_type() == at::kHalf || a.scalar_type() == at::kBFloat16) && a.is_contiguous() && b.is_contiguous() &&
+         a.size(1) == b.size(1) && al(a) && al(b) && bh::gemm_n64_supported(a.size(0), (int)a.size(1), (int)b.size(0));
+}
+
+at::Tensor gemm_n64(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& resid) {
+  TORCH_CHECK(gemm_n64_ok(a, b), "gemm_n64: contiguous aligned fp16/bf16 a [M, K], b [64, K], K in {64, 128, 256}, "
+                                 "M % 32 == 0");
+  auto c = at::empty({a.size(0), 64}, a.options());
+  const void* r = nullptr;
+  if (resid.has_value()) {
+    TORCH_CHECK(resid->sizes() == c.sizes() && resid->is_contiguous() && resid->scalar_type() == a.scalar_type(),
+                "gemm_n64: resid must be a contiguous [M, 64] tensor of a's dtype");
+    r = resid->data_ptr();
+  }
+  bh::gemm_n64(dtype_code(a.scalar_type()), a.data_ptr(), b.data_ptr(), r, c.data_ptr(), a.size(0), (int)a.size(1),
+               stream_for(a));
+  return c;
+}
+
 // weight gradient of stem_forward: [64, 3, 7, 7] channels_last from x and dy [N, 64, 112, 112] channels_last
 at::Tensor stem_wgrad(const at::Tensor& x, const at::Tensor& dy) {
   TORCH_CHECK(x.is_cuda() && dy.is_cuda() && x.dim() == 4 && dy.dim() == 4 && x.scalar_type() == dy.scalar_type() &&
@@ -162,6 +185,9 @@ void register_conv(pybind11::module_& root) {
         "weight gradient of conv2d(x, w, stride, padding=(R-1)//2), R in {1, 3} (stride 2: R = 1): [K, C, R, R] "
         "channels_last");
   m.def("wgrad_supported", &wgrad_supported, py::arg("x"), py::arg("grad_out"), py::arg("R"), py::arg("stride") = 1);
+  m.def("gemm_n64", &gemm_n64, py::arg("a"), py::arg("b"), py::arg("resid") = c10::nullopt,
+        "a [M, K] . b[64, K]^T (+ resid [M, 64]), K in {64, 128, 256}, M % 32 == 0 (kernels/gemm_n64.hip)");
+  m.def("gemm_n64_supported", &gemm_n64_ok, py::arg("a"), py::arg("b"));
   m.def("stem_forward", &stem_forward, py::arg("x"), py::arg("weight"),
         "ResNet stem conv2d(x, w, stride=2, padding=3), 3 -> 64 channels at 224x224, channels_last fp16 / bf16");
   m.def("stem_supported", &stem_ok, py::arg("x"), py::arg("weight"));

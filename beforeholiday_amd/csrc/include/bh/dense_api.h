@@ -26,4 +26,9 @@ void dense_bias_dropout_add(int dt, const void* x, const void* bias, const void*
 void dense_dropout_backward(int dt, const void* dy, const uint8_t* keep, float keep_scale, void* dx, void* bgrad,
                             float* part, int splits, int64_t M, int N, hipStream_t st);
 
+// C[M, 64] = A[M, K] . B[64, K]^T (+ resid[M, 64] if non-null), K in {64, 128, 256}, M % 32 == 0,
+// 16-byte aligned row-major operands (kernels/gemm_n64.hip)
+bool gemm_n64_supported(int64_t M, int K, int N);
+void gemm_n64(int dt, const void* a, const void* b, const void* resid, void* c, int64_t M, int K, hipStream_t st);
+
 }  // namespace bh

@@ -94,6 +94,17 @@ class _GradStash(torch.autograd.Function):
         return None, None
 
 
+def _mm64(a2d, b):
+    """``a2d @ b.t()`` for a 64-row ``b`` on the streaming MFMA kernel (kernels/gemm_n64.hip: the
+    64-channel side of the 56x56 1x1 convolutions, HBM bound), torch.mm (hipBLASLt) otherwise.
+    ``BH_GEMM_N64=0`` keeps hipBLASLt (A/B switch)."""
+    from ..ops import conv as bhconv
+
+    if b.size(0) == 64 and os.environ.get("BH_GEMM_N64", "1") != "0" and bhconv.gemm_n64_supported(a2d, b):
+        return bhconv.gemm_n64(a2d, b)
+    return torch.mm(a2d, b.t())
+
+
 class _Conv1x1Fn(torch.autograd.Function):
     """1x1 / stride-1 convolution of a channels_last activation. Forward and data gradient run either
     as ONE hipBLASLt GEMM on the [N*H*W, C] view (no layout change) or as the MIOpen convolution,
@@ -106,9 +117,9 @@ class _Conv1x1Fn(torch.autograd.Function):
         x2d = x.permute(0, 2, 3, 1).reshape(-1, c)
         w2d = weight.view(weight.size(0), c)
         key = (n, c, h, w, weight.size(0), x.dtype, "fwd")
-        how = _pick(key, lambda: torch.mm(x2d, w2d.t()), lambda: torch.nn.functional.conv2d(x, weight), mode)
+        how = _pick(key, lambda: _mm64(x2d, w2d), lambda: torch.nn.functional.conv2d(x, weight), mode)
         if how == "gemm":
-            y = torch.mm(x2d, w2d.t()).view(n, h, w, -1).permute(0, 3, 1, 2)
+            y = _mm64(x2d, w2d).view(n, h, w, -1).permute(0, 3, 1, 2)
         else:
             y = torch.nn.functional.conv2d(x, weight)
         ctx.save_for_backward(x, weight)
@@ -136,12 +147,14 @@ class _Conv1x1Fn(torch.autograd.Function):
             acc = None
         elif ctx.needs_input_grad[0]:
             gy2d = gy.permute(0, 2, 3, 1).reshape(-1, weight.size(0))
-            w2d = weight.view(weight.size(0), c)
+            wt = weight.view(weight.size(0), c).t()  # [c, k]: dX = dY @ W = dY . wt^T
+            if c == 64:
+                wt = wt.contiguous()
             key = (n, c, h, w, weight.size(0), x.dtype, "dgrad")
-            how = _pick(key, lambda: torch.mm(gy2d, w2d),
+            how = _pick(key, lambda: _mm64(gy2d, wt),
                         lambda: conv_bwd(gy, x, weight, None, *args, [True, False, False]), ctx.mode)
             if how == "gemm":
-                gx = torch.mm(gy2d, w2d).view(n, h, w, c).permute(0, 3, 1, 2)
+                gx = _mm64(gy2d, wt).view(n, h, w, c).permute(0, 3, 1, 2)
             else:
                 gx = conv_bwd(gy, x, weight, None, *args, [True, False, False])[0]
         if acc is not None:

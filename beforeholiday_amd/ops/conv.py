@@ -83,3 +83,16 @@ def stem_wgrad(x: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
         return submodule("conv_cuda").stem_wgrad(x, dy)
     return torch.ops.aten.convolution_backward(dy, x, w, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
                                                [False, True, False])[1]
+
+
+def gemm_n64_supported(a: torch.Tensor, b: torch.Tensor) -> bool:
+    return a.is_cuda and available() and submodule("conv_cuda").gemm_n64_supported(a, b)
+
+
+def gemm_n64(a: torch.Tensor, b: torch.Tensor, resid: torch.Tensor = None) -> torch.Tensor:
+    """``a @ b.t() (+ resid)`` for ``b`` of 64 rows: the streaming MFMA kernel of kernels/gemm_n64.hip
+    (the 64-channel side of the 56x56 1x1 convolutions), torch.mm elsewhere."""
+    if gemm_n64_supported(a, b):
+        return submodule("conv_cuda").gemm_n64(a, b, resid)
+    out = torch.mm(a, b.t())
+    return out if resid is None else out.add_(resid)

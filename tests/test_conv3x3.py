@@ -225,3 +225,26 @@ def test_stem_wgrad_kernel(dtype):
     tol = 1e-2 if dtype == torch.float16 else 2e-2
     torch.testing.assert_close(gw.float(), ref, rtol=tol, atol=tol * ref.abs().max().item())
     assert torch.equal(gw, bhconv.stem_wgrad(x, dy))  # fixed-order reduction
+
+
+N64_SHAPES = [(802816, 256), (200704, 64), (4096, 128), (96, 256), (32, 64)]  # M, K
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("shape", N64_SHAPES)
+@pytest.mark.parametrize("resid", [False, True])
+def test_gemm_n64_kernel(dtype, shape, resid):
+    """kernels/gemm_n64.hip (a [M, K] . b [64, K]^T (+ resid)) vs an fp32 torch.mm, including grids
+    with fewer strips than waves and the persistent loop at ResNet-50 56x56 sizes."""
+    M, K = shape
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    a = torch.randn(M, K, device="cuda", dtype=dtype, generator=g)
+    b = torch.randn(64, K, device="cuda", dtype=dtype, generator=g) * K ** -0.5
+    r = torch.randn(M, 64, device="cuda", dtype=dtype, generator=g) if resid else None
+    assert bhconv.gemm_n64_supported(a, b)
+    c = bhconv.gemm_n64(a, b, r)
+    ref = a.float() @ b.float().t() + (r.float() if resid else 0)
+    tol = 1e-2 if dtype == torch.float16 else 3e-2
+    torch.testing.assert_close(c.float(), ref, rtol=tol, atol=tol)
+    assert not bhconv.gemm_n64_supported(a[:M - 1] if M > 32 else a[:, :K - 8].contiguous(), b)
