@@ -142,8 +142,15 @@ class _Conv1x1Fn(torch.autograd.Function):
             # residual branch gradient already here: dX = acc + dY @ W in one GEMM (beta = 1)
             gy2d = gy.permute(0, 2, 3, 1).reshape(-1, weight.size(0))
             acc2d = acc.permute(0, 2, 3, 1).reshape(-1, c)
-            torch.addmm(acc2d, gy2d, weight.view(weight.size(0), c), out=acc2d)
-            gx = acc
+            wt = weight.view(weight.size(0), c).t().contiguous() if c == 64 else None
+            from ..ops import conv as bhconv
+
+            if wt is not None and os.environ.get("BH_GEMM_N64", "1") != "0" and bhconv.gemm_n64_supported(gy2d, wt):
+                # 64-channel input (layer1's first block): the streaming kernel adds the stash in its epilogue
+                gx = bhconv.gemm_n64(gy2d, wt, acc2d).view(n, h, w, c).permute(0, 3, 1, 2)
+            else:
+                torch.addmm(acc2d, gy2d, weight.view(weight.size(0), c), out=acc2d)
+                gx = acc
             acc = None
         elif ctx.needs_input_grad[0]:
             gy2d = gy.permute(0, 2, 3, 1).reshape(-1, weight.size(0))
