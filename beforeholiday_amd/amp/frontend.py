@@ -174,7 +174,7 @@ def state_dict(destination=None):
     for idx, loss_scaler in enumerate(_amp_state.loss_scalers):
         destination["loss_scaler%d" % idx] = {
             "loss_scale": loss_scaler.loss_scale(),
-            "unskipped": loss_scaler._unskipped,
+            "unskipped": loss_scaler.unskipped(),
         }
     return destination
 
@@ -195,8 +195,7 @@ def load_state_dict(state_dict):
             if idx > (nb_loss_scalers - 1):
                 print("Skipping loss_scaler[{}], since num_losses was set to {}".format(idx, nb_loss_scalers))
                 break
-            _amp_state.loss_scalers[idx]._loss_scale = state_dict[key]["loss_scale"]
-            _amp_state.loss_scalers[idx]._unskipped = state_dict[key]["unskipped"]
+            _amp_state.loss_scalers[idx].load_scale_state(state_dict[key]["loss_scale"], state_dict[key]["unskipped"])
             idx += 1
     if len(unexpected_keys) > 0:
         raise RuntimeError("Error(s) in loading state_dict. Unexpected key(s) in state_dict: {}. ".format(

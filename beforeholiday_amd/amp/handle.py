@@ -23,76 +23,100 @@ def _device_scaler_wanted(loss_scaler, optimizers):
                     for o in optimizers))
 
 
+class _StepGate(object):
+    """Installed once per optimizer as ``optimizer.step`` by :func:`scale_loss` (reference behaviour:
+    apex/amp/handle.py:128-154, which re-patches ``step`` on every overflow instead).
+
+    * host-scaled: an overflowing backward sets ``pending_skip`` (the message to print); the next call
+      then drops the step -- fp32 master grads are released and FusedSGD's scale bookkeeping reset --
+      and clears the mark;
+    * device-scaled: the step always runs (its fused kernels read the step-level overflow flag and
+      return early on their own), then that flag is cleared for the next accumulation window.
+    """
+
+    def __init__(self, optimizer, inner):
+        self.optimizer = optimizer
+        self.inner = inner
+        self.pending_skip = None
+        self.device_flag = None
+
+    def __call__(self, closure=None):
+        if closure is not None:
+            raise RuntimeError("Currently, Amp does not support closure use with optimizers.")
+        if self.pending_skip is not None:
+            maybe_print(self.pending_skip)
+            self.pending_skip = None
+            opt = self.optimizer
+            for p in getattr(opt._amp_stash, "all_fp32_from_fp16_params", ()):
+                p.grad = None
+            if hasattr(opt, "most_recent_scale"):
+                opt.most_recent_scale = 1.0
+                opt.scale_set_by_backward = False
+            return None
+        out = self.inner()
+        if self.device_flag is not None:
+            self.device_flag.zero_()
+        return out
+
+
+def _gate(optimizer):
+    stash = optimizer._amp_stash
+    gate = getattr(stash, "step_gate", None)
+    if gate is None:
+        gate = stash.step_gate = _StepGate(optimizer, optimizer.step)
+        optimizer.step = gate
+    return gate
+
+
 @contextlib.contextmanager
 def scale_loss(loss, optimizers, loss_id=0, model=None, delay_unscale=False, delay_overflow_check=False):
     """Yields ``loss.float() * loss_scale``; on exit unscales gradients (fp16 -> fp32 master grads
-    under master weights), checks for Inf/NaN and, on overflow, reduces the scale and arms a
-    one-shot skip of ``optimizer.step()``."""
+    under master weights), checks for Inf/NaN and, on overflow, lowers the scale and makes the next
+    ``optimizer.step()`` a no-op (host scale: skipped by the step gate; device scale: the fused
+    kernels see the step-level flag)."""
     from ..parallel.LARC import LARC
 
-    if not hasattr(_amp_state, "opt_properties") or _amp_state.opt_properties is None or \
-            not _amp_state.opt_properties.enabled:
+    props = getattr(_amp_state, "opt_properties", None)
+    if props is None or not props.enabled:
         yield loss
         return
     if isinstance(optimizers, (torch.optim.Optimizer, LARC)):
         optimizers = [optimizers]
-    loss_scaler = _amp_state.loss_scalers[loss_id]
-    if not loss_scaler.device_mode and _device_scaler_wanted(loss_scaler, optimizers):
-        loss_scaler.enable_device_mode(loss.device)
-    if loss_scaler.device_mode:
-        for optimizer in optimizers:  # an overflowing step: the fused kernels see the flag and no-op
-            optimizer._dummy_overflow_buf = loss_scaler._overflow_buf
-            optimizer._device_step = True  # FusedLAMB: step counters advance on the device, unless skipped
-    loss_scale = loss_scaler.scale_for_loss()
+    scaler = _amp_state.loss_scalers[loss_id]
+    if not scaler.device_mode and _device_scaler_wanted(scaler, optimizers):
+        scaler.enable_device_mode(loss.device)
+    if scaler.device_mode:
+        for opt in optimizers:
+            opt._dummy_overflow_buf = scaler._step_flag
+            opt._device_step = True  # FusedLAMB: step counters advance on the device, unless skipped
+            _gate(opt).device_flag = scaler._step_flag
+    factor = scaler.scale_for_loss()
 
-    if (not _amp_state.opt_properties.master_weights) and (not loss_scaler.dynamic) and \
-            not loss_scaler.device_mode and loss_scale == 1.0:
-        yield loss.float()
-        if _amp_state.opt_properties.patch_torch_functions and _amp_state.handle is not None:
-            _amp_state.handle._clear_cache()
-        return
+    trivial = not props.master_weights and not scaler.dynamic and not scaler.device_mode and factor == 1.0
+    if not trivial and not delay_unscale:
+        for opt in optimizers:
+            if not opt._amp_stash.params_have_scaled_gradients:
+                opt._prepare_amp_backward()
 
-    if not delay_unscale:
-        for optimizer in optimizers:
-            if not optimizer._amp_stash.params_have_scaled_gradients:
-                optimizer._prepare_amp_backward()
+    yield loss.float() if trivial else loss.float() * factor
 
-    yield loss.float() * loss_scale
-
-    if delay_unscale:
-        for optimizer in optimizers:
-            optimizer._amp_stash.params_have_scaled_gradients = True
-    else:
-        loss_scaler.clear_overflow_state()
-        for optimizer in optimizers:
-            optimizer._post_amp_backward(loss_scaler)
-            optimizer._amp_stash.params_have_scaled_gradients = False
-        should_skip = False if delay_overflow_check else loss_scaler.update_scale()
-        if should_skip:
-            for optimizer in optimizers:
-                if not optimizer._amp_stash.already_patched:
-                    def patch_step(opt, loss_scaler, loss_id):
-                        opt_step = opt.step
-
-                        def skip_step(closure=None):
-                            if closure is not None:
-                                raise RuntimeError("Currently, Amp does not support closure use with optimizers.")
-                            maybe_print(("Gradient overflow.  Skipping step, loss scaler {} reducing loss scale to {}")
-                                        .format(loss_id, loss_scaler.loss_scale()))
-                            if hasattr(opt._amp_stash, "all_fp32_from_fp16_params"):
-                                for param in opt._amp_stash.all_fp32_from_fp16_params:
-                                    param.grad = None
-                            if hasattr(opt, "most_recent_scale"):
-                                opt.most_recent_scale = 1.0
-                                opt.scale_set_by_backward = False
-                            opt.step = opt_step
-                            opt._amp_stash.already_patched = False
-                        return skip_step
-
-                    optimizer.step = patch_step(optimizer, loss_scaler, loss_id)
-                    optimizer._amp_stash.already_patched = True
-
-    if _amp_state.opt_properties.patch_torch_functions and _amp_state.handle is not None:
+    if not trivial:
+        if delay_unscale:
+            for opt in optimizers:
+                opt._amp_stash.params_have_scaled_gradients = True
+        else:
+            scaler.clear_overflow_state()  # this pass's flag only
+            for opt in optimizers:
+                opt._post_amp_backward(scaler)
+                opt._amp_stash.params_have_scaled_gradients = False
+            if scaler.device_mode:
+                scaler.fold_pass_into_step()
+            if not delay_overflow_check and scaler.update_scale():
+                msg = "Gradient overflow.  Skipping step, loss scaler {} reducing loss scale to {}".format(
+                    loss_id, scaler.loss_scale())
+                for opt in optimizers:
+                    _gate(opt).pending_skip = msg
+    if props.patch_torch_functions and _amp_state.handle is not None:
         _amp_state.handle._clear_cache()
 
 

@@ -61,9 +61,28 @@ class LossScaler(object):
     def enable_device_mode(self, device):
         self._scale_dev = torch.full((1,), float(self._loss_scale), dtype=torch.float32, device=device)
         self._inv_dev = torch.empty_like(self._scale_dev)
-        self._unskipped_dev = torch.zeros((1,), dtype=torch.int32, device=device)
+        # seeded from the host counter, so a checkpoint loaded before the first step carries over
+        self._unskipped_dev = torch.full((1,), int(self._unskipped), dtype=torch.int32, device=device)
+        # two flags: ``_overflow_buf`` is one backward pass's (it drives the scale update of that pass),
+        # ``_step_flag`` ORs every pass since the last optimizer step and is the fused optimizers' no-op
+        # flag -- an overflow in an early micro-batch of an accumulated step still skips the step
         self._overflow_buf = torch.zeros(1, dtype=torch.int, device=device)
+        self._step_flag = torch.zeros(1, dtype=torch.int, device=device)
         self.device_mode = True
+
+    def fold_pass_into_step(self):
+        """Device mode: OR this pass's overflow flag into the step-level flag (one tiny kernel)."""
+        torch.maximum(self._step_flag, self._overflow_buf, out=self._step_flag)
+
+    def unskipped(self):
+        return int(self._unskipped_dev.item()) if self.device_mode else self._unskipped
+
+    def load_scale_state(self, loss_scale, unskipped):
+        self._loss_scale = loss_scale
+        self._unskipped = unskipped
+        if self.device_mode:
+            self._scale_dev.fill_(float(loss_scale))
+            self._unskipped_dev.fill_(int(unskipped))
 
     def scale_for_loss(self):
         """The factor scale_loss multiplies the loss by: a device scalar in device mode."""
@@ -142,6 +161,16 @@ class LossScaler(object):
         if not model_grads:
             return
         self._warn_non_fp32(master_grads)
+        if self.device_mode and scale_override is None:
+            # the scale lives on the device: out = model_grad / scale + stashed, with the unscale
+            # (and its overflow check) on the device reciprocal -- never the stale host value
+            torch.reciprocal(self._scale_dev, out=self._inv_dev)
+            flag = self._overflow_buf
+            for m, st, out in zip(model_grads, stashed_master_grads, master_grads):
+                tmp = torch.empty_like(out)
+                multi_tensor_applier(amp_C.multi_tensor_scale, flag, [[m], [tmp]], self._inv_dev)
+                torch.add(tmp, st, out=out)
+            return
         if not LossScaler.has_fused_kernel:
             a, b = out_scale / grads_have_scale, out_scale / stashed_have_scale
             for m, st, out in zip(model_grads, stashed_master_grads, master_grads):

@@ -105,6 +105,33 @@ class PeerMemoryPool(object):
         return ts
 
 
+class PeerTimeoutError(RuntimeError):
+    """A peer did not publish its data within the bounded wait of an IPC exchange kernel."""
+
+
+class _ErrorWatch:
+    """Host view of a kernel's sticky device ``err`` word without a synchronisation per call: after
+    every launch the word is copied (async) into pinned memory, and the next call checks the copy a
+    previous, completed call left there -- a timeout raises at most one call late. ``check(sync=True)``
+    (a step boundary) waits for the stream first. The kernels also write NaN where data is missing,
+    so even the late call's output is visibly invalid, never silently rank-local."""
+
+    def __init__(self, err, what):
+        self.err = err
+        self.what = what
+        self.host = torch.zeros(1, dtype=torch.int32, pin_memory=torch.cuda.is_available())
+
+    def after_launch(self):
+        self.host.copy_(self.err, non_blocking=True)
+
+    def check(self, sync=False):
+        if sync:
+            torch.cuda.current_stream(self.err.device).synchronize()
+            self.host.copy_(self.err)
+        if int(self.host[0]) != 0:
+            raise PeerTimeoutError(f"{self.what}: a peer did not publish its data in time (outputs were NaN-poisoned)")
+
+
 class PeerHaloExchanger1d:
     """In-place halo exchange along H (or W) of a padded activation ``y`` ([N, C, H+2h, W], channels_last
     or not, or explicit NHWC [N, H+2h, W, C]); the first / last rank of the group get zero halos."""
@@ -126,6 +153,7 @@ class PeerHaloExchanger1d:
         if self.native:
             self.signals = peer_pool.allocate_peer_tensors([2, 64], torch.int32, False, False)
             self.err = torch.zeros(1, dtype=torch.int32, device="cuda")
+            self._watch = _ErrorWatch(self.err, "PeerHaloExchanger1d")
 
     def _slots(self, numel, dtype):
         key = (numel, dtype)
@@ -162,8 +190,13 @@ class PeerHaloExchanger1d:
         _pm().push_pull_halos_1d(out_lo, out_hi, in_lo, in_hi, lo_tx[me], hi_tx[me], hi_tx[lo_n], lo_tx[hi_n],
                                  self.signals[me], self.signals[lo_n], self.signals[hi_n], self.low_zero,
                                  self.high_zero, self.epoch, self.err, self.max_spins)
-        if diagnostics and int(self.err.item()) != 0:
-            raise RuntimeError("PeerHaloExchanger1d: a neighbour did not publish its halo in time")
+        self._watch.after_launch()
+        self._watch.check(sync=diagnostics)
+
+    def check(self):
+        """Raise :class:`PeerTimeoutError` if any exchange so far timed out (synchronises)."""
+        if getattr(self, "_watch", None) is not None:
+            self._watch.check(sync=True)
 
 
 class PeerAllReduce:
@@ -192,6 +225,7 @@ class PeerAllReduce:
             self._slot_ptrs = [t.data_ptr() for t in self.slots]
             self._flag_ptrs = [t.data_ptr() for t in self.flags]
             self.err = torch.zeros(1, dtype=torch.int32, device="cuda")
+            self._watch = _ErrorWatch(self.err, "PeerAllReduce")
 
     @property
     def size(self):
@@ -204,6 +238,14 @@ class PeerAllReduce:
             return t
         assert t.dtype == torch.float32 and t.is_contiguous(), "PeerAllReduce: contiguous fp32 tensors only"
         self.epoch += 1
+        self._watch.check()  # an earlier exchange timed out: raise before adding to the damage
         _pm().peer_allreduce(t, t, self._slot_ptrs, self._flag_ptrs, self.capacity, self.me, self.epoch, self.err,
                              self.max_spins)
+        self._watch.after_launch()
         return t
+
+    def check(self):
+        """Raise :class:`PeerTimeoutError` if any exchange so far timed out (synchronises; call it at
+        a step boundary, e.g. next to the loss read)."""
+        if self.native:
+            self._watch.check(sync=True)

@@ -135,7 +135,7 @@ at::Tensor stem_forward(const at::Tensor& x, const at::Tensor& w) {
 
 bool gemm_n64_ok(const at::Tensor& a, const at::Tensor& b) {
   auto al = [](const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0; };
-  return a.is_cuda() && b.is_cuda() && a.dim() == 2 && b.dim() == 2 && a.scalar_type() == b.scalar_type() &&
+  return a.is_cuda() && b.is_cuda() && a.device() == b.device() && a.dim() == 2 && b.dim() == 2 && a.scalar_type() == b.scalar_type() &&
          (a.scalar_type() == at::kHalf || a.scalar_type() == at::kBFloat16) && a.is_contiguous() && b.is_contiguous() &&
          a.size(1) == b.size(1) && al(a) && al(b) && bh::gemm_n64_supported(a.size(0), (int)a.size(1), (int)b.size(0));
 }
@@ -146,8 +146,10 @@ at::Tensor gemm_n64(const at::Tensor& a, const at::Tensor& b, const c10::optiona
   auto c = at::empty({a.size(0), 64}, a.options());
   const void* r = nullptr;
   if (resid.has_value()) {
-    TORCH_CHECK(resid->sizes() == c.sizes() && resid->is_contiguous() && resid->scalar_type() == a.scalar_type(),
-                "gemm_n64: resid must be a contiguous [M, 64] tensor of a's dtype");
+    TORCH_CHECK(resid->is_cuda() && resid->device() == a.device() && resid->sizes() == c.sizes() &&
+                    resid->is_contiguous() && resid->scalar_type() == a.scalar_type() &&
+                    (reinterpret_cast<uintptr_t>(resid->data_ptr()) & 15) == 0,
+                "gemm_n64: resid must be a contiguous aligned [M, 64] tensor of a's dtype on a's device");
     r = resid->data_ptr();
   }
   bh::gemm_n64(dtype_code(a.scalar_type()), a.data_ptr(), b.data_ptr(), r, c.data_ptr(), a.size(0), (int)a.size(1),

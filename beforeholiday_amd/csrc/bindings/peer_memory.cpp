@@ -95,15 +95,40 @@ at::Tensor blob_view(int64_t raw, std::vector<int64_t> shape, bool channels_last
   return at::from_blob(reinterpret_cast<void*>(raw), shape, strides, [](void*) {}, opts);
 }
 
+// 4-D view with mergeable dimensions collapsed (row-major order kept): [N, 1, W, C] rows of an NHWC
+// tensor become [1, 1, N, W*C], so the kernel's offset math mostly sees size-1 dimensions
 bh::HaloView halo_view(const at::Tensor& t) {
   TORCH_CHECK(t.is_cuda() && t.dim() == 4, "halo tensors must be 4-D GPU tensors");
+  int64_t sz[4], st[4];
+  int n = 0;
+  for (int d = 0; d < 4; ++d) {
+    if (t.size(d) == 1) continue;
+    if (n > 0 && st[n - 1] == t.size(d) * t.stride(d)) {
+      sz[n - 1] *= t.size(d);
+      st[n - 1] = t.stride(d);
+    } else {
+      sz[n] = t.size(d);
+      st[n] = t.stride(d);
+      ++n;
+    }
+  }
   bh::HaloView v{};
   v.ptr = t.data_ptr();
   for (int d = 0; d < 4; ++d) {
-    v.size[d] = t.size(d);
-    v.stride[d] = t.stride(d);
+    const int k = d - (4 - n);  // right-aligned, leading size-1 dimensions
+    v.size[d] = k >= 0 ? sz[k] : 1;
+    v.stride[d] = k >= 0 ? st[k] : 0;
   }
   return v;
+}
+
+bool view_vec16(const bh::HaloView& v, int eb) {
+  const int64_t V = 16 / eb;
+  if ((reinterpret_cast<uintptr_t>(v.ptr) & 15) != 0 || v.size[3] % V != 0 || (v.size[3] > 1 && v.stride[3] != 1))
+    return false;
+  for (int d = 0; d < 3; ++d)
+    if (v.size[d] > 1 && v.stride[d] % V != 0) return false;
+  return true;
 }
 
 // Halo exchange step (see bh/peer_api.h). tx_* are [2, numel] transfer-slot tensors in the pool;
@@ -141,6 +166,10 @@ void push_pull_halos_1d(at::Tensor out_lo, at::Tensor out_hi, at::Tensor in_lo, 
   a.elem_bytes = eb;
   a.max_spins = (int)max_spins;
   a.err = err.data_ptr<int>();
+  a.vec16 = view_vec16(a.out_lo, eb) && view_vec16(a.out_hi, eb) && view_vec16(a.in_lo, eb) &&
+            view_vec16(a.in_hi, eb);
+  for (const at::Tensor* t : {&tx_lo_self, &tx_hi_self, &tx_peer_lo, &tx_peer_hi})
+    a.vec16 = a.vec16 && (reinterpret_cast<uintptr_t>(t->data_ptr()) & 15) == 0;
   bh::push_pull_halos_1d(a, stream_for(out_lo));
 }
 

@@ -37,6 +37,7 @@ struct HaloArgs {
   int64_t numel;           // elements of one halo
   int elem_bytes;          // 2 or 4
   int max_spins;
+  bool vec16;              // every view copies in 16-byte pieces (set by the host, see k_halo_1d)
   int* err;
 };
 void push_pull_halos_1d(const HaloArgs& a, hipStream_t st);

@@ -27,22 +27,48 @@ namespace {
 constexpr int kBlock = 256;
 
 BH_DEVICE int64_t view_offset(const HaloView& v, int64_t i) {
+  // views arrive with mergeable dimensions collapsed on the host (an NHWC row halo is [1, 1, N, W*C]),
+  // so the leading divisions usually see size-1 dimensions
   const int64_t i3 = i % v.size[3];
   int64_t r = i / v.size[3];
-  const int64_t i2 = r % v.size[2];
-  r /= v.size[2];
-  const int64_t i1 = r % v.size[1];
-  const int64_t i0 = r / v.size[1];
-  return i0 * v.stride[0] + i1 * v.stride[1] + i2 * v.stride[2] + i3 * v.stride[3];
+  int64_t o = i3 * v.stride[3];
+  if (v.size[2] > 1) {
+    o += (r % v.size[2]) * v.stride[2];
+    r /= v.size[2];
+  }
+  if (v.size[1] > 1) {
+    o += (r % v.size[1]) * v.stride[1];
+    r /= v.size[1];
+  }
+  return o + r * v.stride[0];
 }
 
+// copy elements [lo, hi) of a halo; with a.vec16 every view is innermost-contiguous, its innermost
+// size and all strides are multiples of 16 bytes and the range bounds are too, so whole 16-byte
+// pieces move (one offset computation per 8 fp16 elements instead of per element)
 template <typename E>
-BH_DEVICE void copy_range(E* dst, const HaloView* dview, const E* src, const HaloView* sview, int64_t lo, int64_t hi) {
+BH_DEVICE void copy_range(E* dst, const HaloView* dview, const E* src, const HaloView* sview, int64_t lo, int64_t hi,
+                          bool vec16) {
+  if (vec16) {
+    constexpr int V = 16 / sizeof(E);
+    for (int64_t i = lo + (int64_t)threadIdx.x * V; i < hi; i += (int64_t)kBlock * V) {
+      const uint4 x = *reinterpret_cast<const uint4*>(sview ? src + view_offset(*sview, i) : src + i);
+      *reinterpret_cast<uint4*>(dview ? dst + view_offset(*dview, i) : dst + i) = x;
+    }
+    return;
+  }
   for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) {
     const E x = sview ? src[view_offset(*sview, i)] : src[i];
     if (dview) dst[view_offset(*dview, i)] = x;
     else dst[i] = x;
   }
+}
+
+// a timed-out pull leaves NaN (all bits set: NaN in fp16, bf16 and fp32) instead of stale data, so a
+// missing neighbour poisons the result visibly (the device loss scaler then skips the step)
+template <typename E>
+BH_DEVICE void poison_range(E* dst, const HaloView& v, int64_t lo, int64_t hi) {
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) dst[view_offset(v, i)] = static_cast<E>(~E(0));
 }
 
 BH_DEVICE bool wait_epoch(int* flag, int epoch, int max_spins) {
@@ -56,14 +82,16 @@ BH_DEVICE bool wait_epoch(int* flag, int epoch, int max_spins) {
 template <typename E>
 __global__ __launch_bounds__(kBlock) void k_halo_1d(HaloArgs a) {
   const int b = blockIdx.x;
-  const int64_t per = (a.numel + gridDim.x - 1) / gridDim.x;
+  // per-workgroup ranges are multiples of 16 bytes when the vector path is on
+  const int64_t gran = a.vec16 ? 16 / sizeof(E) : 1;
+  const int64_t per = ((a.numel + gridDim.x - 1) / gridDim.x + gran - 1) / gran * gran;
   const int64_t lo = min(a.numel, (int64_t)b * per), hi = min(a.numel, lo + per);
   const int slot = a.epoch & 1;
   E* tx_lo = reinterpret_cast<E*>(a.tx_lo_self) + slot * a.numel;
   E* tx_hi = reinterpret_cast<E*>(a.tx_hi_self) + slot * a.numel;
   // 1. stage the outgoing halos in this rank's transfer slots (local memory)
-  if (!a.lo_zero) copy_range<E>(tx_lo, nullptr, reinterpret_cast<const E*>(a.out_lo.ptr), &a.out_lo, lo, hi);
-  if (!a.hi_zero) copy_range<E>(tx_hi, nullptr, reinterpret_cast<const E*>(a.out_hi.ptr), &a.out_hi, lo, hi);
+  if (!a.lo_zero) copy_range<E>(tx_lo, nullptr, reinterpret_cast<const E*>(a.out_lo.ptr), &a.out_lo, lo, hi, a.vec16);
+  if (!a.hi_zero) copy_range<E>(tx_hi, nullptr, reinterpret_cast<const E*>(a.out_hi.ptr), &a.out_hi, lo, hi, a.vec16);
   __syncthreads();
   // 2. publish: my low halo is what the low neighbour pulls as its HIGH input (its flag row 1)
   if (threadIdx.x == 0) {
@@ -85,12 +113,16 @@ __global__ __launch_bounds__(kBlock) void k_halo_1d(HaloArgs a) {
   if (a.lo_zero) {
     for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) in_lo[view_offset(a.in_lo, i)] = E(0);
   } else if (ok[0]) {
-    copy_range<E>(in_lo, &a.in_lo, reinterpret_cast<const E*>(a.tx_peer_lo) + slot * a.numel, nullptr, lo, hi);
+    copy_range<E>(in_lo, &a.in_lo, reinterpret_cast<const E*>(a.tx_peer_lo) + slot * a.numel, nullptr, lo, hi, a.vec16);
+  } else {
+    poison_range<E>(in_lo, a.in_lo, lo, hi);
   }
   if (a.hi_zero) {
     for (int64_t i = lo + threadIdx.x; i < hi; i += kBlock) in_hi[view_offset(a.in_hi, i)] = E(0);
   } else if (ok[1]) {
-    copy_range<E>(in_hi, &a.in_hi, reinterpret_cast<const E*>(a.tx_peer_hi) + slot * a.numel, nullptr, lo, hi);
+    copy_range<E>(in_hi, &a.in_hi, reinterpret_cast<const E*>(a.tx_peer_hi) + slot * a.numel, nullptr, lo, hi, a.vec16);
+  } else {
+    poison_range<E>(in_hi, a.in_hi, lo, hi);
   }
 }
 
@@ -121,14 +153,14 @@ __global__ __launch_bounds__(kReduceBlock) void k_peer_allreduce(PeerReduceArgs 
   }
   __syncthreads();
   __atomic_thread_fence(__ATOMIC_ACQUIRE);
-  // 4. sum the G rows in rank order (identical on every rank); a timed-out exchange keeps the input
+  // 4. sum the G rows in rank order (identical on every rank). A timed-out exchange writes NaN: never
+  //    rank-local statistics that silently differ between ranks (the host also raises on *err)
   const float* rows = a.slots[a.me] + (int64_t)parity * a.G * a.L;
   for (int i = threadIdx.x; i < a.L; i += kReduceBlock) {
-    float s = 0.f;
+    float s = __builtin_nanf("");
     if (ok) {
+      s = 0.f;
       for (int r = 0; r < a.G; ++r) s += rows[(int64_t)r * a.L + i];
-    } else {
-      s = a.in[i];
     }
     a.out[i] = s;
   }

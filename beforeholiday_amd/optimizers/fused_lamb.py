@@ -102,6 +102,10 @@ class FusedLAMB(ParamTableMixin, torch.optim.Optimizer):
         if self._fast_path_ok():
             self._native_step()
             return loss
+        if getattr(self, "_device_step", False) and bool(self._dummy_overflow_buf.item()):
+            # device-scaled amp on the list path (no parameter table): the kernels would no-op on the
+            # flag, but the host step counters below must not advance for a skipped step either
+            return loss
         device = first_device(self.param_groups)
         global_grad_norm = self._global_grad_norm(device)
         max_grad_norm = self.defaults["max_grad_norm"]

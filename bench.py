@@ -67,6 +67,7 @@ def parse():
     ap.add_argument("--diag-steps", type=int, default=3,
                     help="untimed steps AFTER the timed region with collective timing events (comm_ms_per_step)")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--trace-warmup", default="", help="write a cProfile table of warmup step 1 to this file")
     ap.add_argument("--autotune", action="store_true",
                     help="MIOpen find (cudnn.benchmark): minutes of first-step tuning on a fresh box and measured "
                          "slower (35.1 ms/step) than the immediate-mode solvers (33.1 ms/step) at batch 256")
@@ -175,7 +176,21 @@ def main():
 
     for i in range(args.warmup):
         tw = time.perf_counter()
-        step()
+        if i == 0 and args.trace_warmup:
+            # where the first step's host time goes (MIOpen find / kernel JIT, hipBLASLt heuristics,
+            # per-shape A/B timing): cumulative-time table of the slowest calls
+            import cProfile
+            import pstats
+
+            prof = cProfile.Profile()
+            prof.enable()
+            step()
+            torch.cuda.synchronize()
+            prof.disable()
+            with open(args.trace_warmup, "w") as f:
+                pstats.Stats(prof, stream=f).sort_stats("cumulative").print_stats(60)
+        else:
+            step()
         torch.cuda.synchronize()
         if rank == 0:
             print(f"[bench] warmup {i + 1}/{args.warmup}: {(time.perf_counter() - tw) * 1e3:.1f} ms",

@@ -10,7 +10,7 @@ import torch
 import torch.nn.functional as F
 
 
-def _run(device_mode, steps, inf_at=None, monkeypatch=None, window=3, init_scale=256.0):
+def _run(device_mode, steps, inf_at=None, monkeypatch=None, window=3, init_scale=256.0, micro=1, state=None):
     from beforeholiday_amd import amp
     from beforeholiday_amd.amp._amp_state import _amp_state
     from beforeholiday_amd.optimizers import FusedLAMB
@@ -28,11 +28,14 @@ def _run(device_mode, steps, inf_at=None, monkeypatch=None, window=3, init_scale
     y = torch.randint(0, 8, (16,), device="cuda")
     scales, snaps = [], []
     for i in range(steps):
-        loss = F.cross_entropy(model(x).float(), y)
-        with amp.scale_loss(loss, opt) as scaled:
-            scaled.backward()
-            if inf_at == i:
-                next(model.parameters()).grad.view(-1)[0] = float("inf")
+        for m in range(micro):  # gradient accumulation: one scale_loss per micro-batch
+            loss = F.cross_entropy(model(x[m::micro]).float(), y[m::micro])
+            with amp.scale_loss(loss, opt) as scaled:
+                scaled.backward()
+                if inf_at == i and m == 0:
+                    next(model.parameters()).grad.view(-1)[0] = float("inf")
+        if state is not None and i == 1:
+            state.append(amp.state_dict())
         opt.step()
         opt.zero_grad()
         scales.append(_amp_state.loss_scalers[0].loss_scale())
@@ -75,3 +78,45 @@ def test_device_scaler_matches_host_with_overflow(monkeypatch):
     for a, b in zip(p_host, p_dev):
         for u, v in zip(a, b):
             torch.testing.assert_close(u, v, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_device_scaler_accumulation_overflow_in_first_micro_batch(monkeypatch):
+    """Two micro-batches per step, an Inf in the FIRST one: the device path must still skip the whole
+    step (the per-pass flag is cleared by the second pass, the step-level flag is not) and unscale the
+    accumulated grads with the device scale -- same trajectory and scales as the host reference."""
+    s_host, p_host, _ = _run(False, 5, inf_at=2, monkeypatch=monkeypatch, window=100, micro=2)
+    s_dev, p_dev, used = _run(True, 5, inf_at=2, monkeypatch=monkeypatch, window=100, micro=2)
+    assert used and s_host == s_dev
+    for u, v in zip(p_dev[1], p_dev[2]):
+        assert torch.equal(u, v)  # skipped
+    for a, b in zip(p_host, p_dev):
+        for u, v in zip(a, b):
+            torch.testing.assert_close(u, v, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_device_scaler_accumulation_after_scale_change(monkeypatch):
+    """Accumulated grads after the device scale has grown: unscaled by the device value (the host
+    ``_loss_scale`` is stale in device mode)."""
+    s_host, p_host, _ = _run(False, 6, monkeypatch=monkeypatch, window=2, micro=2)
+    s_dev, p_dev, used = _run(True, 6, monkeypatch=monkeypatch, window=2, micro=2)
+    assert used and s_host == s_dev and s_host[-1] > s_host[0]
+    for a, b in zip(p_host, p_dev):
+        for u, v in zip(a, b):
+            torch.testing.assert_close(u, v, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_device_scaler_state_dict_roundtrip(monkeypatch):
+    from beforeholiday_amd import amp
+    from beforeholiday_amd.amp._amp_state import _amp_state
+
+    st_host, st_dev = [], []
+    _run(False, 3, monkeypatch=monkeypatch, window=100, state=st_host)
+    _run(True, 3, monkeypatch=monkeypatch, window=100, state=st_dev)
+    assert st_host[0] == st_dev[0]  # the device counter, not the never-updated host one
+    sd = {"loss_scaler0": {"loss_scale": 1024.0, "unskipped": 7}}
+    amp.load_state_dict(sd)
+    sc = _amp_state.loss_scalers[0]
+    assert sc.device_mode and sc.loss_scale() == 1024.0 and sc.unskipped() == 7

@@ -139,3 +139,54 @@ def test_groupbn_ipc_two_processes_one_gpu(fuse_relu):
 
 def test_groupbn_group_cpu():
     run_distributed(_groupbn, 2, "cpu", False)
+
+
+def _allreduce_timeout(rank, world, device):
+    """Rank 1 withholds its contribution: rank 0's bounded wait times out, its output is NaN (never
+    its rank-local input) and check() raises; a following call raises before launching."""
+    from beforeholiday_amd.contrib.peer_memory import PeerAllReduce, PeerMemoryPool
+    from beforeholiday_amd.contrib.peer_memory.peer_memory import PeerTimeoutError
+    torch.cuda.set_device(0)
+    pool = PeerMemoryPool(1 << 20, 0, peer_ranks=list(range(world)))
+    red = PeerAllReduce(pool, capacity=1024)
+    t = torch.ones(100, device="cuda")
+    red.all_reduce_(t)  # both ranks: a healthy exchange first
+    torch.cuda.synchronize()
+    assert float(t[0]) == world
+    dist.barrier()
+    red.max_spins = 1 << 12  # a short bounded wait for the withheld exchange
+    if rank == 0:
+        t = torch.ones(100, device="cuda")
+        red.all_reduce_(t)
+        torch.cuda.synchronize()
+        assert torch.isnan(t.cpu()).all()
+        with pytest.raises(PeerTimeoutError):
+            red.check()
+        with pytest.raises(PeerTimeoutError):
+            red.all_reduce_(torch.ones(4, device="cuda"))
+    dist.barrier()
+
+
+@pytest.mark.gpu
+def test_peer_allreduce_timeout_poisons_and_raises():
+    run_distributed(_allreduce_timeout, 2, "cuda")
+
+
+def _halo_timeout(rank, world, device):
+    from beforeholiday_amd.contrib.peer_memory import PeerHaloExchanger1d, PeerMemoryPool
+    from beforeholiday_amd.contrib.peer_memory.peer_memory import PeerTimeoutError
+    torch.cuda.set_device(0)
+    pool = PeerMemoryPool(1 << 20, 1 << 20, peer_ranks=list(range(world)))
+    ex = PeerHaloExchanger1d(list(range(world)), rank, pool, 1, max_spins=1 << 12)
+    dist.barrier()
+    if rank == 0:  # rank 1 never publishes: rank 0's incoming high halo is NaN, and it raises
+        y = torch.zeros(2, 8, 6, 16, device="cuda", dtype=torch.float16)
+        with pytest.raises(PeerTimeoutError):
+            ex(y, H_split=True, explicit_nhwc=True, diagnostics=True)
+        assert torch.isnan(y[:, -1].float().cpu()).all() and not torch.isnan(y[:, :-1].float().cpu()).any()
+    dist.barrier()
+
+
+@pytest.mark.gpu
+def test_peer_halo_timeout_poisons_and_raises():
+    run_distributed(_halo_timeout, 2, "cuda")
