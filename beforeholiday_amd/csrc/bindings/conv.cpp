@@ -66,6 +66,77 @@ at::Tensor conv3x3_dgrad(const at::Tensor& dy, const at::Tensor& w) {
   return dx;
 }
 
+const float* f32_or_null(const c10::optional<at::Tensor>& t, int64_t n, const char* what) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == n, what,
+              " must be a contiguous fp32 GPU tensor of ", n, " elements");
+  return t->data_ptr<float>();
+}
+
+// conv3x3_forward with the BatchNorm folding: x is the producing layer's RAW output when pro_scale /
+// pro_shift are given (relu(x * scale + shift) is convolved); stats=True also returns the per-workgroup
+// partial sums [2, G, K] of (y - kshift) and (y - kshift)^2 (conv_bn.sum_parts reduces them)
+std::vector<at::Tensor> conv3x3_bn_forward(const at::Tensor& x, const at::Tensor& w,
+                                           const c10::optional<at::Tensor>& pro_scale,
+                                           const c10::optional<at::Tensor>& pro_shift, bool stats,
+                                           const c10::optional<at::Tensor>& kshift) {
+  TORCH_CHECK(shapes_ok(x, w), "conv3x3_bn_forward: needs channels_last fp16/bf16 x, w [K, C, 3, 3], C and K % 64 == 0");
+  const at::Tensor wc = w.contiguous(at::MemoryFormat::ChannelsLast);
+  auto y = at::empty({x.size(0), w.size(0), x.size(2), x.size(3)}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto a = conv_args(x, wc, y);
+  a.pro_scale = f32_or_null(pro_scale, a.C, "pro_scale");
+  a.pro_shift = f32_or_null(pro_shift, a.C, "pro_shift");
+  at::Tensor part = at::empty({0}, x.options().dtype(at::kFloat));
+  if (stats) {
+    a.epi = bh::kConvEpiStats;
+    a.kshift = f32_or_null(kshift, a.K, "kshift");
+    part = at::empty({2, (int64_t)bh::conv3x3_parts(a), (int64_t)a.K}, x.options().dtype(at::kFloat));
+    a.part = part.data_ptr<float>();
+  }
+  TORCH_CHECK(bh::conv3x3_supported(a), "conv3x3_bn_forward: unsupported arguments (C <= 512 with a prologue)");
+  bh::conv3x3_forward(dtype_code(x.scalar_type()), a, stream_for(x));
+  return {y, part};
+}
+
+// conv3x3_dgrad whose epilogue also reduces the PREVIOUS BatchNorm's backward sums: by is that
+// BatchNorm's raw input (same shape as dx), dz = dx * (by * bscale + bshift > 0) (brelu): partials
+// [2, G, C] of dz and dz * (by - bmean)
+std::vector<at::Tensor> conv3x3_bn_dgrad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& by,
+                                         const at::Tensor& bscale, const at::Tensor& bshift, const at::Tensor& bmean,
+                                         bool brelu) {
+  TORCH_CHECK(dy.is_cuda() && w.is_cuda() && dy.dim() == 4 && w.dim() == 4 && w.size(0) == dy.size(1) &&
+                  w.size(2) == 3 && w.size(3) == 3 && dy.scalar_type() == w.scalar_type() &&
+                  (dy.scalar_type() == at::kHalf || dy.scalar_type() == at::kBFloat16) &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast) && w.size(0) % 64 == 0 && w.size(1) % 64 == 0,
+              "conv3x3_bn_dgrad: needs channels_last fp16/bf16 dy, w [K, C, 3, 3], C and K % 64 == 0");
+  const at::Tensor wc = w.contiguous(at::MemoryFormat::ChannelsLast);
+  auto dx = at::empty({dy.size(0), w.size(1), dy.size(2), dy.size(3)},
+                      dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  TORCH_CHECK(by.is_cuda() && by.device() == dy.device() && by.scalar_type() == dy.scalar_type() &&
+                  by.sizes() == dx.sizes() && by.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3_bn_dgrad: by must be a channels_last tensor shaped like dx");
+  bh::Conv3x3Args a;
+  a.x = dy.data_ptr();
+  a.w = wc.data_ptr();
+  a.y = dx.data_ptr();
+  a.N = (int)dy.size(0);
+  a.C = (int)dy.size(1);
+  a.H = (int)dy.size(2);
+  a.W = (int)dy.size(3);
+  a.K = (int)w.size(1);
+  a.epi = bh::kConvEpiBwd;
+  a.by = by.data_ptr();
+  a.bscale = f32_or_null(bscale, a.K, "bscale");
+  a.bshift = f32_or_null(bshift, a.K, "bshift");
+  a.bmean = f32_or_null(bmean, a.K, "bmean");
+  a.brelu = brelu;
+  auto part = at::empty({2, (int64_t)bh::conv3x3_parts(a), (int64_t)a.K}, dy.options().dtype(at::kFloat));
+  a.part = part.data_ptr<float>();
+  TORCH_CHECK(bh::conv3x3_supported(a), "conv3x3_bn_dgrad: unaligned tensors");
+  bh::conv3x3_dgrad(dtype_code(dy.scalar_type()), a, stream_for(dy));
+  return {dx, part};
+}
+
 // dW of y = conv2d(x, w, stride 1, padding (R-1)/2) for channels_last x [N, C, H, W], dy [N, K, H, W];
 // returns [K, C, R, R] channels_last (memory [K][R][R][C])
 bool wgrad_ok(const at::Tensor& x, const at::Tensor& dy, int64_t R, int64_t stride = 1) {
@@ -183,6 +254,10 @@ void register_conv(pybind11::module_& root) {
   m.def("conv3x3_dgrad", &conv3x3_dgrad, py::arg("grad_out"), py::arg("weight"),
         "grad of conv2d(x, weight, stride=1, padding=1) w.r.t. x, straight from the forward weight");
   m.def("supported", &supported, py::arg("x"), py::arg("weight"));
+  m.def("conv3x3_bn_forward", &conv3x3_bn_forward, py::arg("x"), py::arg("weight"), py::arg("pro_scale") = py::none(),
+        py::arg("pro_shift") = py::none(), py::arg("stats") = false, py::arg("kshift") = py::none());
+  m.def("conv3x3_bn_dgrad", &conv3x3_bn_dgrad, py::arg("grad_out"), py::arg("weight"), py::arg("by"),
+        py::arg("bscale"), py::arg("bshift"), py::arg("bmean"), py::arg("brelu") = true);
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("grad_out"), py::arg("R"), py::arg("stride") = 1,
         "weight gradient of conv2d(x, w, stride, padding=(R-1)//2), R in {1, 3} (stride 2: R = 1): [K, C, R, R] "
         "channels_last");

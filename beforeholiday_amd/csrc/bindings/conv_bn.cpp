@@ -1,0 +1,189 @@
+// `conv_bn`: 1x1 convolution GEMMs with BatchNorm prologue / statistics epilogues
+// (kernels/conv_bn.hip, bh/conv_bn_api.h) on [pixels, channels] views of NHWC activations.
+#include "common.h"
+
+#include "bh/conv_bn_api.h"
+#include "bh/gemm_api.h"
+
+namespace bhb {
+namespace {
+
+const float* fptr(const c10::optional<at::Tensor>& t, int64_t n, const char* what) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == n, what,
+              " must be a contiguous fp32 GPU tensor of ", n, " elements");
+  return t->data_ptr<float>();
+}
+
+bh::C1x1Args make_args(const at::Tensor& a, const at::Tensor& b, bool b_trans, int64_t M,
+                       const c10::optional<at::Tensor>& pro_scale,
+                       const c10::optional<at::Tensor>& pro_shift, const c10::optional<at::Tensor>& resid,
+                       int64_t s2_h, int64_t s2_w, int64_t epi, const c10::optional<at::Tensor>& kshift,
+                       const c10::optional<at::Tensor>& by, const c10::optional<at::Tensor>& bscale,
+                       const c10::optional<at::Tensor>& bshift, const c10::optional<at::Tensor>& bmean, bool brelu) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.device() == b.device() && a.dim() == 2 && b.dim() == 2 &&
+                  a.is_contiguous() && b.is_contiguous() && a.scalar_type() == b.scalar_type() &&
+                  a.size(1) == b.size(b_trans ? 0 : 1),
+              "conv_bn.c1x1: a [rows, K] and b [N, K] ([K, N] with b_trans) contiguous GPU tensors of one dtype");
+  bh::C1x1Args p;
+  p.A = a.data_ptr();
+  p.B = b.data_ptr();
+  p.b_trans = b_trans;
+  p.M = M;
+  p.K = (int)a.size(1);
+  p.N = (int)b.size(b_trans ? 1 : 0);
+  p.pro_scale = fptr(pro_scale, p.K, "pro_scale");
+  p.pro_shift = fptr(pro_shift, p.K, "pro_shift");
+  TORCH_CHECK((p.pro_scale == nullptr) == (p.pro_shift == nullptr), "conv_bn.c1x1: pro_scale and pro_shift together");
+  if (resid.has_value() && resid->defined()) {
+    TORCH_CHECK(resid->is_cuda() && resid->device() == a.device() && resid->scalar_type() == a.scalar_type() &&
+                    resid->is_contiguous() && resid->numel() == M * p.N,
+                "conv_bn.c1x1: resid must be a contiguous [M, N] tensor of a's dtype on a's device");
+    p.R = resid->data_ptr();
+  }
+  p.s2_H = (int)s2_h;
+  p.s2_W = (int)s2_w;
+  if (s2_h > 0) {
+    TORCH_CHECK(a.size(0) * (s2_h / 2) * (s2_w / 2) == M * s2_h * s2_w, "conv_bn.c1x1: stride-2 rows");
+  } else {
+    TORCH_CHECK(a.size(0) == M, "conv_bn.c1x1: a has M rows");
+  }
+  p.epi = (int)epi;
+  p.kshift = fptr(kshift, p.N, "kshift");
+  if (epi == bh::kC1x1Bwd) {
+    TORCH_CHECK(by.has_value() && by->defined() && by->is_cuda() && by->device() == a.device() &&
+                    by->scalar_type() == a.scalar_type() && by->is_contiguous() && by->numel() == M * p.N,
+                "conv_bn.c1x1: by must be a contiguous [M, N] tensor of a's dtype");
+    p.by = by->data_ptr();
+    p.bscale = fptr(bscale, p.N, "bscale");
+    p.bshift = fptr(bshift, p.N, "bshift");
+    p.bmean = fptr(bmean, p.N, "bmean");
+    p.brelu = brelu;
+  }
+  return p;
+}
+
+// returns (C [M, N], partials [2, G, N] fp32 or an empty tensor for the plain epilogue)
+std::vector<at::Tensor> c1x1(const at::Tensor& a, const at::Tensor& b, bool b_trans, int64_t M,
+                             const c10::optional<at::Tensor>& pro_scale, const c10::optional<at::Tensor>& pro_shift,
+                             const c10::optional<at::Tensor>& resid, int64_t s2_h, int64_t s2_w, int64_t epi,
+                             const c10::optional<at::Tensor>& kshift, const c10::optional<at::Tensor>& by,
+                             const c10::optional<at::Tensor>& bscale, const c10::optional<at::Tensor>& bshift,
+                             const c10::optional<at::Tensor>& bmean, bool brelu) {
+  bh::C1x1Args p = make_args(a, b, b_trans, M, pro_scale, pro_shift, resid, s2_h, s2_w, epi, kshift, by, bscale, bshift, bmean,
+                             brelu);
+  auto c = at::empty({M, (int64_t)p.N}, a.options());
+  p.C = c.data_ptr();
+  at::Tensor part;
+  if (epi != bh::kC1x1Plain) {
+    const int G = bh::c1x1_parts(p);
+    TORCH_CHECK(G > 0, "conv_bn.c1x1: unsupported shape");
+    part = at::empty({2, (int64_t)G, (int64_t)p.N}, a.options().dtype(at::kFloat));
+    p.part = part.data_ptr<float>();
+  } else {
+    part = at::empty({0}, a.options().dtype(at::kFloat));
+  }
+  TORCH_CHECK(bh::c1x1_supported(p), "conv_bn.c1x1: unsupported shape / alignment / argument combination (M=", M,
+              ", K=", p.K, ", N=", p.N, ")");
+  bh::c1x1_run(dtype_code(a.scalar_type()), p, stream_for(a));
+  return {c, part};
+}
+
+bool c1x1_supported(const at::Tensor& a, const at::Tensor& b, bool b_trans, int64_t M, bool pro, bool resid,
+                    int64_t s2_h, int64_t s2_w, int64_t epi) {
+  if (!(a.is_cuda() && b.is_cuda() && a.dim() == 2 && b.dim() == 2 && a.is_contiguous() && b.is_contiguous() &&
+        a.scalar_type() == b.scalar_type() && a.size(1) == b.size(b_trans ? 0 : 1) &&
+        (a.scalar_type() == at::kHalf || a.scalar_type() == at::kBFloat16)))
+    return false;
+  static float dummy[1];
+  bh::C1x1Args p;
+  p.A = a.data_ptr();
+  p.B = b.data_ptr();
+  p.C = a.data_ptr();  // alignment of the future output: at::empty is 16-byte aligned
+  p.b_trans = b_trans;
+  p.M = M;
+  p.K = (int)a.size(1);
+  p.N = (int)b.size(b_trans ? 1 : 0);
+  p.pro_scale = pro ? dummy : nullptr;
+  p.pro_shift = pro ? dummy : nullptr;
+  p.R = resid ? a.data_ptr() : nullptr;
+  p.s2_H = (int)s2_h;
+  p.s2_W = (int)s2_w;
+  p.epi = (int)epi;
+  p.part = dummy;
+  if (epi == bh::kC1x1Bwd) {
+    p.by = a.data_ptr();
+    p.bscale = p.bshift = p.bmean = dummy;
+  }
+  return bh::c1x1_supported(p);
+}
+
+// [2N+1] (count >= 0) or [2N] sums over the G partial rows of c1x1's statistics
+at::Tensor sum_parts(const at::Tensor& part, double count) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.dim() == 3 && part.size(0) == 2 &&
+                  part.is_contiguous(),
+              "conv_bn.sum_parts: part must be a contiguous fp32 [2, G, N] GPU tensor");
+  const int64_t G = part.size(1), N = part.size(2);
+  auto out = at::empty({2 * N + (count >= 0 ? 1 : 0)}, part.options());
+  bh::c1x1_sum_parts((int)G, (int)N, part.data_ptr<float>(), out.data_ptr<float>(), (float)count, stream_for(part));
+  return out;
+}
+
+// C = A . B^T on the tiled MFMA GEMM (kernels/gemm.hip) with a BatchNorm statistics epilogue (epi 1:
+// forward statistics centred on kshift; epi 2: the previous BatchNorm's backward sums with by / bscale
+// / bshift / bmean) -- the compute-bound 1x1 layers. Returns (C [M, N], partials [2, slabs, N]).
+std::vector<at::Tensor> gemm_bn(const at::Tensor& a, const at::Tensor& b, int64_t epi,
+                                const c10::optional<at::Tensor>& kshift, const c10::optional<at::Tensor>& by,
+                                const c10::optional<at::Tensor>& bscale, const c10::optional<at::Tensor>& bshift,
+                                const c10::optional<at::Tensor>& bmean, bool brelu) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.device() == b.device() && a.dim() == 2 && b.dim() == 2 &&
+                  a.is_contiguous() && b.is_contiguous() && a.scalar_type() == b.scalar_type() &&
+                  (a.scalar_type() == at::kHalf || a.scalar_type() == at::kBFloat16) && a.size(1) == b.size(1),
+              "conv_bn.gemm_bn: a [M, K] and b [N, K] contiguous fp16/bf16 GPU tensors");
+  TORCH_CHECK(epi == 1 || epi == 2, "conv_bn.gemm_bn: epi must be 1 (statistics) or 2 (backward sums)");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  auto c = at::empty({M, N}, a.options());
+  TORCH_CHECK(bh::gemm_supported(M, N, K, K, K, N, a.data_ptr(), b.data_ptr(), c.data_ptr()) && N % 64 == 0,
+              "conv_bn.gemm_bn: unsupported shape");
+  const int64_t slabs = bh::gemm_bgrad_slabs(M);
+  auto part = at::empty({2, slabs, N}, a.options().dtype(at::kFloat));
+  bh::GemmEpilogue e;
+  e.bn_stats = (int)epi;
+  e.stat_part = part.data_ptr<float>();
+  e.kshift = fptr(kshift, N, "kshift");
+  if (epi == 2) {
+    TORCH_CHECK(by.has_value() && by->defined() && by->is_cuda() && by->scalar_type() == a.scalar_type() &&
+                    by->is_contiguous() && by->numel() == M * N,
+                "conv_bn.gemm_bn: by must be a contiguous [M, N] tensor of a's dtype");
+    e.bn_y = by->data_ptr();
+    e.bn_scale = fptr(bscale, N, "bscale");
+    e.bn_shift = fptr(bshift, N, "bshift");
+    e.bn_mean = fptr(bmean, N, "bmean");
+    TORCH_CHECK(e.bn_scale && e.bn_shift && e.bn_mean, "conv_bn.gemm_bn: bscale / bshift / bmean required");
+    e.bn_relu = brelu;
+  }
+  bh::gemm_nt(dtype_code(a.scalar_type()), a.data_ptr(), K, b.data_ptr(), K, c.data_ptr(), N, M, N, K, e,
+              stream_for(a));
+  return {c, part};
+}
+
+}  // namespace
+
+void register_conv_bn(pybind11::module_& root) {
+  auto m = root.def_submodule("conv_bn", "1x1 convolution GEMMs with BatchNorm prologue / statistics epilogues");
+  m.attr("EPI_PLAIN") = (int)bh::kC1x1Plain;
+  m.attr("EPI_STATS") = (int)bh::kC1x1Stats;
+  m.attr("EPI_BWD") = (int)bh::kC1x1Bwd;
+  m.def("c1x1", &c1x1, py::arg("a"), py::arg("b"), py::arg("b_trans"), py::arg("M"), py::arg("pro_scale") = py::none(),
+        py::arg("pro_shift") = py::none(), py::arg("resid") = py::none(), py::arg("s2_h") = 0, py::arg("s2_w") = 0,
+        py::arg("epi") = 0, py::arg("kshift") = py::none(), py::arg("by") = py::none(), py::arg("bscale") = py::none(),
+        py::arg("bshift") = py::none(), py::arg("bmean") = py::none(), py::arg("brelu") = true);
+  m.def("c1x1_supported", &c1x1_supported, py::arg("a"), py::arg("b"), py::arg("b_trans"), py::arg("M"), py::arg("pro") = false,
+        py::arg("resid") = false, py::arg("s2_h") = 0, py::arg("s2_w") = 0, py::arg("epi") = 0);
+  m.def("sum_parts", &sum_parts, py::arg("part"), py::arg("count") = -1.0);
+  m.def("gemm_bn", &gemm_bn, py::arg("a"), py::arg("b"), py::arg("epi"), py::arg("kshift") = py::none(),
+        py::arg("by") = py::none(), py::arg("bscale") = py::none(), py::arg("bshift") = py::none(),
+        py::arg("bmean") = py::none(), py::arg("brelu") = true);
+}
+
+}  // namespace bhb

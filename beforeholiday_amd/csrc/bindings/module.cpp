@@ -16,4 +16,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   bhb::register_legacy_optim(m);
   bhb::register_peer_memory(m);
   bhb::register_conv(m);
+  bhb::register_conv_bn(m);
 }

@@ -12,11 +12,28 @@
 
 namespace bh {
 
+enum ConvEpi { kConvEpiPlain = 0, kConvEpiStats = 1, kConvEpiBwd = 2 };
+
 struct Conv3x3Args {
   const void* x = nullptr;  // [N, H, W, C]
   const void* w = nullptr;  // [K, 3, 3, C]
   void* y = nullptr;        // [N, H, W, K]
   int N = 0, H = 0, W = 0, C = 0, K = 0;
+  // forward only: BatchNorm + ReLU of the producing layer applied to x as it is staged (C <= 512)
+  const float* pro_scale = nullptr;
+  const float* pro_shift = nullptr;
+  // per-workgroup partial statistics per output channel, part [2][G][K], G = conv3x3_parts():
+  //   kConvEpiStats (forward): sums of (y - kshift) and (y - kshift)^2 of y as stored;
+  //   kConvEpiBwd (data gradient): with yb = by (the previous BatchNorm's raw input, [N, H, W, K]),
+  //     dz = y * (yb * bscale + bshift > 0): sums of dz and dz * (yb - bmean)
+  int epi = kConvEpiPlain;
+  float* part = nullptr;
+  const float* kshift = nullptr;
+  const void* by = nullptr;
+  const float* bscale = nullptr;
+  const float* bshift = nullptr;
+  const float* bmean = nullptr;
+  bool brelu = true;
 };
 
 // true when the kernel covers the shape (C % 64 == 0, K % 64 == 0, 16-byte aligned tensors)
@@ -25,6 +42,8 @@ void conv3x3_forward(int dt, const Conv3x3Args& a, hipStream_t st);
 // data gradient: a.x = dY [N, H, W, K_w], a.w = the forward weights [K_w, 3, 3, C_w] as they are,
 // a.y = dX [N, H, W, C_w]; a.C = K_w (channels read), a.K = C_w (channels written)
 void conv3x3_dgrad(int dt, const Conv3x3Args& a, hipStream_t st);
+// partial rows G of the statistics epilogues for this shape
+int conv3x3_parts(const Conv3x3Args& a);
 
 // Weight gradient of a stride-1 "same" R x R convolution (R = 1 or 3, pad (R-1)/2), kernels/conv_wgrad.hip:
 // out[k][r][s][c] = sum over pixels of dy[n, y, x, k] * x[n, y + r - P, x + s - P, c].

@@ -1,0 +1,57 @@
+// 1x1 convolution GEMMs with BatchNorm folded into their prologue / epilogue (kernels/conv_bn.hip).
+//
+// C[M, N] = f(A)[M, K] . B[N, K]^T on NHWC activations viewed as [pixels, channels], fp32 accumulation:
+//   * prologue (pro_scale != null): f(a) = relu(a * pro_scale[k] + pro_shift[k]) -- the BatchNorm(+ReLU)
+//     of the producing layer applied while the operand is loaded, so the normalised activation is never
+//     written to HBM;
+//   * stride-2 gather (s2_H > 0): output row (n, y, x) reads input row (n, 2y, 2x) of an [N, s2_H, s2_W, K]
+//     tensor (the ResNet downsample branch), no gathered copy;
+//   * epilogue, optional residual R[M, N] added before rounding;
+//   * epilogue statistics, per output column over the rows (deterministic per-workgroup partials,
+//     part[g][n] and part[G + g][n], g < G = c1x1_parts()):
+//       kStats: sums of (c - kshift[n]) and (c - kshift[n])^2 of the ROUNDED stored value c -- the
+//               BatchNorm statistics of this conv's output, centred on the running mean;
+//       kBwd:   with y = by[m, n] (the raw input of the previous BatchNorm), mask = (y * bscale[n] +
+//               bshift[n] > 0) when brelu: sums of dz = c * mask and dz * (y - bmean[n]) -- that
+//               BatchNorm's backward reduction, computed on the data gradient as it is produced.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bh {
+
+enum C1x1Epi { kC1x1Plain = 0, kC1x1Stats = 1, kC1x1Bwd = 2 };
+
+struct C1x1Args {
+  const void* A = nullptr;  // [rows, K] (rows = M, or N * s2_H * s2_W with the stride-2 gather)
+  const void* B = nullptr;  // [N, K], or [K, N] with b_trans
+  bool b_trans = false;
+  void* C = nullptr;        // [M, N]
+  const void* R = nullptr;  // optional residual [M, N]
+  int64_t M = 0;
+  int K = 0, N = 0;
+  const float* pro_scale = nullptr;  // [K] prologue BatchNorm (with ReLU)
+  const float* pro_shift = nullptr;
+  int s2_H = 0, s2_W = 0;  // > 0: stride-2 gather from an [.., s2_H, s2_W, K] input; output is [.., s2_H/2, s2_W/2, N]
+  int epi = kC1x1Plain;
+  float* part = nullptr;            // [2][G][N] fp32 partials (kStats / kBwd)
+  const float* kshift = nullptr;    // kStats centre per column (may be null = 0)
+  const void* by = nullptr;         // kBwd: [M, N] raw input of the previous BatchNorm
+  const float* bscale = nullptr;    // kBwd: its scale / shift (ReLU mask) and batch mean
+  const float* bshift = nullptr;
+  const float* bmean = nullptr;
+  bool brelu = true;
+};
+
+// whether the kernel covers the shape (K % 64, N % 64, M % 32, LDS budget, 16-byte alignment)
+bool c1x1_supported(const C1x1Args& a);
+// number of partial rows G per statistic for this shape (part holds 2 * G * N floats)
+int c1x1_parts(const C1x1Args& a);
+void c1x1_run(int dt, const C1x1Args& a, hipStream_t st);
+
+// sums[n] = sum_g part[g][n], sums[N + n] = sum_g part[G + g][n], sums[2N] = count (if count >= 0):
+// the [2N+1] layout of syncbn.stats_local_sums (forward) or [2N] (sum_dy, sum_dy_xmu) (backward)
+void c1x1_sum_parts(int G, int N, const float* part, float* sums, float count, hipStream_t st);
+
+}  // namespace bh

@@ -24,6 +24,19 @@ struct GemmEpilogue {
   const void* aux_in = nullptr;   // [M, ld_aux] backward
   int64_t ld_aux = 0;
   float* bgrad_part = nullptr;    // [gemm_bgrad_slabs(M), N]
+  // BatchNorm statistics of the output, per 64-row slab into stat_part [2][slabs][N] (no activation /
+  // bias with these; the 128x128 / 256x128 / 256x256 kernels, never the ping-pong one):
+  //   1: sums of (c - kshift[n]) and its square, c the stored value (the next BatchNorm's statistics);
+  //   2: with y = bn_y[m, n] (ld = ldc): dz = c * (y * bn_scale + bn_shift > 0 | !bn_relu), sums of dz
+  //      and dz * (y - bn_mean[n]) (the previous BatchNorm's backward reduction)
+  int bn_stats = 0;
+  float* stat_part = nullptr;
+  const float* kshift = nullptr;
+  const void* bn_y = nullptr;
+  const float* bn_scale = nullptr;
+  const float* bn_shift = nullptr;
+  const float* bn_mean = nullptr;
+  bool bn_relu = true;
 };
 
 // Shape / layout requirements of the MFMA path (else the caller must fall back):

@@ -56,6 +56,8 @@ constexpr int kMaxHC = 40;  // halo columns G * (lanes per image + 2) <= 40
 constexpr int kHaloBytes = (kTH + 2) * kMaxHC * kPix;
 constexpr int kWBytes = kBN * 128;
 constexpr int kHaloPer = ((kTH + 2) * kMaxHC * 8 + kThreads - 1) / kThreads;  // 16-byte pieces per thread
+constexpr int kMaxProC = 512;                 // input channels the BatchNorm prologue covers
+constexpr int kProBytes = 2 * kMaxProC * 4;   // its scale / shift in LDS
 
 struct Geo {
   int G, gw, HC, XT, YT, tiles, tpw;  // tpw: consecutive windows per workgroup
@@ -82,13 +84,14 @@ BH_DEVICE i4v frag_tr(const char* img, int r0, int m0, int lane) {
 // w [K_w][3][3][C_w], computing conv with W'[c][r][s][k] = w[k][2-r][2-s][c]. The slice of each
 // step is then a [k_w rows][c_w contiguous] block of w, staged as it lies and read as the MFMA A
 // operand through ds_read_b64_tr_b16 -- no transposed weight copy is ever materialised.
-template <typename T, bool FLIP, int G>
+template <typename T, bool FLIP, int G, bool PRO, int EPI>
 __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
   // window geometry as compile-time constants (the halo address math divides by them)
   constexpr int GW = 32 / G, HC = G * (GW + 2);
-  __shared__ __attribute__((aligned(16))) char smem[kHaloBytes + 2 * kWBytes];
+  __shared__ __attribute__((aligned(16))) char smem[kHaloBytes + 2 * kWBytes + (PRO ? kProBytes : 0)];
   char* halo = smem;
   char* wb = smem + kHaloBytes;
+  float* ss = reinterpret_cast<float*>(smem + kHaloBytes + 2 * kWBytes);  // PRO: scale[C], shift[C]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r32 = lane & 31, h = lane >> 5;
   const int tile0 = blockIdx.x * g.tpw;
@@ -99,6 +102,13 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
   const int C = a.C, H = a.H, W = a.W, N = a.N;
   const int nch = C / kCK, per_tile = nch * 9, steps = ntile * per_tile;
   constexpr int npieces = (kTH + 2) * HC * 8;
+  if constexpr (PRO) {
+    for (int c = tid; c < C; c += kThreads) {
+      ss[c] = a.pro_scale[c];
+      ss[kMaxProC + c] = a.pro_shift[c];
+    }
+    // visible to the first halo_store through the __syncthreads below it
+  }
   // window origin of tile id t: x-tile fastest, then row window, then image group
   auto origin = [&](int t, int& n0, int& y0, int& x0) {
     const int xt = t % g.XT;
@@ -112,10 +122,12 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
   // ---- halo staging: registers (prefetch) -> LDS ----
   i4v hreg[kHaloPer];
   uint32_t hmask = 0;
+  int hc0 = 0;  // first input channel of the staged chunk (the prologue's scale / shift)
   auto halo_load = [&](int t, int c0) {
     int n0, y0, x0;
     origin(t, n0, y0, x0);
     hmask = 0;
+    hc0 = c0;
 #pragma unroll
     for (int i = 0; i < kHaloPer; ++i) {
       const int q = tid + i * kThreads, pix = q >> 3, ch = q & 7;
@@ -129,12 +141,32 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
     }
   };
   auto halo_store = [&]() {
+    float sc[8], sh[8];
+    if constexpr (PRO) {
+      // BatchNorm + ReLU of the producing layer on the staged input; this thread's pieces all hold
+      // channels hc0 + 8 (tid & 7) .. + 7 (kThreads is a multiple of 8). Padding stays zero: it pads
+      // the normalised activation, not the raw input.
+      const int cb = hc0 + 8 * (tid & 7);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sc[j] = ss[cb + j];
+        sh[j] = ss[kMaxProC + cb + j];
+      }
+    }
 #pragma unroll
     for (int i = 0; i < kHaloPer; ++i) {
       const int q = tid + i * kThreads;
-      if (q < npieces)
-        *reinterpret_cast<i4v*>(halo + (q >> 3) * kPix + (q & 7) * 16) =
-            ((hmask >> i) & 1u) ? hreg[i] : i4v{0, 0, 0, 0};
+      if (q < npieces) {
+        i4v v = hreg[i];
+        if constexpr (PRO) {
+          typedef T t8 __attribute__((ext_vector_type(8)));
+          t8 e = __builtin_bit_cast(t8, v);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) e[j] = from_f<T>(fmaxf(fmaf(to_f<T>(e[j]), sc[j], sh[j]), 0.f));
+          v = __builtin_bit_cast(i4v, e);
+        }
+        *reinterpret_cast<i4v*>(halo + (q >> 3) * kPix + (q & 7) * 16) = ((hmask >> i) & 1u) ? v : i4v{0, 0, 0, 0};
+      }
     }
   };
   // ---- weight slice of step (chunk, r * 3 + s): W[k0 .. k0+63][r][s][c0 .. c0+63] ----
@@ -170,26 +202,53 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
   const int gi = r32 / GW, jl = r32 - gi * GW;
   const int hcol = gi * (GW + 2) + jl;  // this lane's halo column at s = 0
   T* Y = reinterpret_cast<T*>(a.y);
-  // lane = pixel, registers = 4 consecutive output channels per group
+  const T* BY = reinterpret_cast<const T*>(a.by);
+  // Output tile of the wave, D[pixel][channel] (the MFMA's A operand is the halo, B the weights):
+  // lane (r32, h) holds channel k0 + 32 kb + r32 of pixels 8 (v >> 2) + 4 h + (v & 3) of window row
+  // 2 wave + pb in acc[kb][pb][v]. Stores are 64-byte channel runs of one pixel; the per-channel
+  // statistics stay in 2 x 2 registers per lane for the whole workgroup.
+  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f}, e0[2] = {0.f, 0.f}, e1[2] = {0.f, 0.f}, e2[2] = {0.f, 0.f};
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    const int ch = k0 + 32 * kb + r32;
+    if constexpr (EPI == kConvEpiStats) {
+      e0[kb] = a.kshift ? a.kshift[ch] : 0.f;
+    } else if constexpr (EPI == kConvEpiBwd) {
+      e0[kb] = a.bscale[ch];
+      e1[kb] = a.bshift[ch];
+      e2[kb] = a.bmean[ch];
+    }
+  }
   auto epilogue = [&](int t) {
     int n0, y0, x0;
     origin(t, n0, y0, x0);
-    const int n = n0 + gi, x = x0 + jl;
-    if (n >= N || x >= W) return;
 #pragma unroll
     for (int pb = 0; pb < 2; ++pb) {
       const int y = y0 + 2 * wave + pb;
-      if (y >= H) continue;
-      T* out = Y + ((n * H + y) * W + x) * a.K + k0;
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int v = 0; v < 16; ++v) {
+        const int pp = 8 * (v >> 2) + 4 * h + (v & 3);
+        const int gp = pp / GW, xp = pp - gp * GW;
+        const int n = n0 + gp, x = x0 + xp;
+        if (y >= H || n >= N || x >= W) continue;
+        const int off = ((n * H + y) * W + x) * a.K + k0 + r32;
 #pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          T o[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = from_f<T>(acc[kb][pb][4 * gq + j]);
-          *reinterpret_cast<uint2*>(out + 32 * kb + 8 * gq + 4 * h) = *reinterpret_cast<const uint2*>(o);
+        for (int kb = 0; kb < 2; ++kb) {
+          const T o = from_f<T>(acc[kb][pb][v]);
+          Y[off + 32 * kb] = o;
+          const float f = to_f<T>(o);  // statistics of the value as stored
+          if constexpr (EPI == kConvEpiStats) {
+            const float d = f - e0[kb];
+            s1[kb] += d;
+            s2[kb] = fmaf(d, d, s2[kb]);
+          } else if constexpr (EPI == kConvEpiBwd) {
+            const float yv = to_f<T>(BY[off + 32 * kb]);
+            const float dz = (!a.brelu || fmaf(yv, e0[kb], e1[kb]) > 0.f) ? f : 0.f;
+            s1[kb] += dz;
+            s2[kb] = fmaf(dz, yv - e2[kb], s2[kb]);
+          }
         }
+      }
     }
   };
 
@@ -232,15 +291,15 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
 #pragma unroll
     for (int kk = 0; kk < 4; kk += 2) {
       frags(kk + 1, fb);
-      acc[0][0] = Mfma32<T>::run(fa[0], fa[2], acc[0][0]);
-      acc[0][1] = Mfma32<T>::run(fa[0], fa[3], acc[0][1]);
-      acc[1][0] = Mfma32<T>::run(fa[1], fa[2], acc[1][0]);
-      acc[1][1] = Mfma32<T>::run(fa[1], fa[3], acc[1][1]);
+      acc[0][0] = Mfma32<T>::run(fa[2], fa[0], acc[0][0]);
+      acc[0][1] = Mfma32<T>::run(fa[3], fa[0], acc[0][1]);
+      acc[1][0] = Mfma32<T>::run(fa[2], fa[1], acc[1][0]);
+      acc[1][1] = Mfma32<T>::run(fa[3], fa[1], acc[1][1]);
       if (kk + 2 < 4) frags(kk + 2, fa);
-      acc[0][0] = Mfma32<T>::run(fb[0], fb[2], acc[0][0]);
-      acc[0][1] = Mfma32<T>::run(fb[0], fb[3], acc[0][1]);
-      acc[1][0] = Mfma32<T>::run(fb[1], fb[2], acc[1][0]);
-      acc[1][1] = Mfma32<T>::run(fb[1], fb[3], acc[1][1]);
+      acc[0][0] = Mfma32<T>::run(fb[2], fb[0], acc[0][0]);
+      acc[0][1] = Mfma32<T>::run(fb[3], fb[0], acc[0][1]);
+      acc[1][0] = Mfma32<T>::run(fb[2], fb[1], acc[1][0]);
+      acc[1][1] = Mfma32<T>::run(fb[3], fb[1], acc[1][1]);
     }
     if (t + 1 < steps) w_store(wb + ((t + 1) & 1) * kWBytes);
     if (last_rs && chunk + 1 == nch) {  // window done: results out, accumulators reset
@@ -252,6 +311,27 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
       halo_store();
     }
     __syncthreads();
+  }
+  if constexpr (EPI != kConvEpiPlain) {
+    // per-workgroup partial of each statistic: lane halves, then the 4 waves (LDS, the halo is free)
+    float* red = reinterpret_cast<float*>(smem);  // [waves][2][64]
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      s1[kb] += __shfl_xor(s1[kb], 32);
+      s2[kb] += __shfl_xor(s2[kb], 32);
+      if (h == 0) {
+        red[(wave * 2) * 64 + 32 * kb + r32] = s1[kb];
+        red[(wave * 2 + 1) * 64 + 32 * kb + r32] = s2[kb];
+      }
+    }
+    __syncthreads();
+    if (tid < 128) {
+      const int stat = tid >> 6, c = tid & 63;
+      float u = 0.f;
+#pragma unroll
+      for (int q = 0; q < kThreads / 64; ++q) u += red[(q * 2 + stat) * 64 + c];
+      a.part[((int64_t)stat * gridDim.x + blockIdx.x) * a.K + k0 + c] = u;
+    }
   }
 }
 
@@ -275,32 +355,64 @@ Geo make_geo(int H, int W) {
 bool conv3x3_supported(const Conv3x3Args& a) {
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   const int64_t pix = (int64_t)a.N * a.H * a.W;
+  if (a.pro_scale && (!a.pro_shift || a.C > kMaxProC)) return false;
+  if (a.epi != kConvEpiPlain && !a.part) return false;
+  if (a.epi == kConvEpiBwd && (!a.by || !al(a.by) || !a.bscale || !a.bshift || !a.bmean)) return false;
   return a.N > 0 && a.H > 0 && a.W > 0 && a.C > 0 && a.K > 0 && a.C % kCK == 0 && a.K % kBN == 0 && al(a.x) &&
          al(a.w) && al(a.y) && pix * a.C < (1ll << 31) && pix * a.K < (1ll << 31);  // 32-bit offsets
 }
 
-void conv3x3_run(int dt, const Conv3x3Args& a, bool flip, hipStream_t st) {
-  if (!conv3x3_supported(a)) throw std::runtime_error("conv3x3_forward: needs C % 64 == 0, K % 64 == 0, aligned tensors");
+namespace {
+
+struct Launch {
+  Geo g;
+  dim3 grid;
+};
+
+Launch plan(const Conv3x3Args& a) {
   const Geo g = make_geo(a.H, a.W);
-  if (g.HC > kMaxHC) throw std::runtime_error("conv3x3_forward: halo geometry out of range");
-  Geo g2 = g;
+  if (g.HC > kMaxHC) throw std::runtime_error("conv3x3: halo geometry out of range");
+  Launch l;
+  l.g = g;
   const int64_t tiles = (int64_t)g.XT * g.YT * ((a.N + g.G - 1) / g.G);
-  g2.tiles = (int)tiles;
+  l.g.tiles = (int)tiles;
   const int64_t ktiles = a.K / kBN;
   // about two resident workgroups per CU over the whole grid: each walks tpw consecutive windows and
   // prefetches the next window's halo while computing the current one. (A one-workgroup-per-CU
   // variant holding all nine weight slices of a chunk in LDS measured 1.2x slower: profiles/
   // conv3x3_direct_vs_miopen.jsonl.)
-  g2.tpw = (int)std::max<int64_t>(1, (tiles * ktiles + 511) / 512);
-  const dim3 grid((unsigned)((tiles + g2.tpw - 1) / g2.tpw), (unsigned)ktiles);
+  l.g.tpw = (int)std::max<int64_t>(1, (tiles * ktiles + 511) / 512);
+  l.grid = dim3((unsigned)((tiles + l.g.tpw - 1) / l.g.tpw), (unsigned)ktiles);
+  return l;
+}
+
+}  // namespace
+
+int conv3x3_parts(const Conv3x3Args& a) { return (int)plan(a).grid.x; }
+
+void conv3x3_run(int dt, const Conv3x3Args& a, bool flip, hipStream_t st) {
+  if (!conv3x3_supported(a)) throw std::runtime_error("conv3x3: needs C % 64 == 0, K % 64 == 0, aligned tensors");
+  // instantiated: forward (prologue and / or statistics epilogue), data gradient (backward epilogue)
+  if (flip && (a.pro_scale || a.epi == kConvEpiStats)) throw std::runtime_error("conv3x3_dgrad: no prologue / stats");
+  if (!flip && a.epi == kConvEpiBwd) throw std::runtime_error("conv3x3_forward: no backward epilogue");
+  const Launch l = plan(a);
   auto launch = [&](auto tt, auto gg) {
     using T = typename decltype(tt)::type;
     constexpr int GG = decltype(gg)::value;
-    if (flip) hipLaunchKernelGGL((k_conv3x3<T, true, GG>), grid, dim3(kThreads), 0, st, a, g2);
-    else hipLaunchKernelGGL((k_conv3x3<T, false, GG>), grid, dim3(kThreads), 0, st, a, g2);
+    auto L = [&](auto kern) { hipLaunchKernelGGL(kern, l.grid, dim3(kThreads), 0, st, a, l.g); };
+    if (flip) {
+      if (a.epi == kConvEpiBwd) L(k_conv3x3<T, true, GG, false, kConvEpiBwd>);
+      else L(k_conv3x3<T, true, GG, false, kConvEpiPlain>);
+    } else if (a.pro_scale) {
+      if (a.epi == kConvEpiStats) L(k_conv3x3<T, false, GG, true, kConvEpiStats>);
+      else L(k_conv3x3<T, false, GG, true, kConvEpiPlain>);
+    } else {
+      if (a.epi == kConvEpiStats) L(k_conv3x3<T, false, GG, false, kConvEpiStats>);
+      else L(k_conv3x3<T, false, GG, false, kConvEpiPlain>);
+    }
   };
   auto by_g = [&](auto tt) {
-    switch (g.G) {
+    switch (l.g.G) {
       case 1: launch(tt, std::integral_constant<int, 1>{}); break;
       case 2: launch(tt, std::integral_constant<int, 2>{}); break;
       default: launch(tt, std::integral_constant<int, 4>{}); break;
@@ -309,10 +421,10 @@ void conv3x3_run(int dt, const Conv3x3Args& a, bool flip, hipStream_t st) {
   switch (dt) {
     case kF16: by_g(Tag<f16>{}); break;
     case kBF16: by_g(Tag<bf16>{}); break;
-    default: throw std::runtime_error("conv3x3_forward: fp16 / bf16 only");
+    default: throw std::runtime_error("conv3x3: fp16 / bf16 only");
   }
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess) throw std::runtime_error(std::string("conv3x3_forward: ") + hipGetErrorString(e));
+  if (e != hipSuccess) throw std::runtime_error(std::string("conv3x3: ") + hipGetErrorString(e));
 }
 
 void conv3x3_forward(int dt, const Conv3x3Args& a, hipStream_t st) { conv3x3_run(dt, a, false, st); }

@@ -1,0 +1,435 @@
+// 1x1 convolution GEMMs with the neighbouring BatchNorms folded in (see bh/conv_bn_api.h): the
+// ResNet-50 bottleneck's 1x1 convolutions, which are HBM bound at batch 256 (K, N <= 512 against
+// M = 50k - 800k pixels), so every separate BatchNorm pass over their inputs or outputs costs as much
+// as the convolution itself.
+//
+// Layout (MFMA v_mfma_f32_32x32x16): a wave owns whole 32-row strips of the output with NC columns
+// (a column slice of N). Lane (r, h) = (lane & 31, lane >> 5) loads row r of the strip, channels
+// 16 s + 8 h .. + 7 of k-step s straight from global memory into its A fragment (16-byte loads), so
+// the BatchNorm prologue is a register transform on the fragment (scale / shift held in LDS). The
+// column slice of the weights stays in LDS for the life of the persistent workgroup (rows padded by 16
+// bytes: the 16-lane phases of a ds_read_b128 hit distinct banks), one B-fragment read per MFMA. The
+// next strip's rows are loaded while the current strip's epilogue runs.
+//
+// Epilogue: lane holds C[8 j + 4 h + i][32 t + r] in acc[t][4 j + i], i.e. ONE column per 32-column
+// tile, 16 rows of it. Each store writes two 64-byte row segments. The per-column statistics are
+// accumulated per lane across all strips the wave processes (2 floats per tile), then reduced over the
+// lane halves, the 4 waves (LDS) and written as one partial row per workgroup: deterministic, no
+// atomics, and the statistics of an 800k-row output cost one extra read of nothing.
+#include "bh/api.h"
+#include "bh/conv_bn_api.h"
+#include "bh/device.h"
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+
+namespace bh {
+namespace {
+
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef __bf16 b8v __attribute__((ext_vector_type(8)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef int i4v __attribute__((ext_vector_type(4)));
+
+template <typename T> struct Mf;
+template <> struct Mf<f16> {
+  typedef h8v v8;
+  static BH_DEVICE f16v run(i4v a, i4v b, f16v c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8v, a), __builtin_bit_cast(h8v, b), c, 0, 0, 0);
+  }
+};
+template <> struct Mf<bf16> {
+  typedef b8v v8;
+  static BH_DEVICE f16v run(i4v a, i4v b, f16v c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(b8v, a), __builtin_bit_cast(b8v, b), c, 0, 0, 0);
+  }
+};
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+
+struct Geo {
+  int nslices;  // column slices of NC
+  int G;        // workgroups per slice (multiple of 8)
+  int strips;   // M / 32
+  int ss_off;   // LDS byte offset of the prologue scale / shift
+  int red_off;  // LDS byte offset of the cross-wave reduction buffer
+};
+
+template <typename T, int KC, int NC, int EPI, bool PRO, bool S2, bool RES>
+__global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NT = NC / 32;  // 32-column tiles per wave
+  constexpr int KS = KC / 16;  // k-steps per register chunk
+  using V8 = typename Mf<T>::v8;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  // workgroup -> (column slice, strip group), XCD-aware: consecutive ids land on different XCDs
+  // (id % 8), so the slices of one strip group are given the same id % 8 and share that XCD's L2
+  const int xcd = blockIdx.x & 7, idx = blockIdx.x >> 3;
+  const int slice = idx % g.nslices;
+  const int grp = (idx / g.nslices) * 8 + xcd;
+  const int K = p.K, N = p.N;
+  const int nch = K / KC;
+  const int col0 = slice * NC;
+  const int RS = 2 * K + 16;
+  char* bl = smem;
+  float* ss = reinterpret_cast<float*>(smem + g.ss_off);
+  {
+    if (!p.b_trans) {
+      const T* Bp = reinterpret_cast<const T*>(p.B) + (int64_t)col0 * K;
+      const int per_row = K >> 3;
+      for (int c = threadIdx.x; c < NC * per_row; c += kThreads) {
+        const int row = c / per_row, c8 = c - row * per_row;
+        *reinterpret_cast<i4v*>(bl + row * RS + c8 * 16) =
+            *reinterpret_cast<const i4v*>(Bp + (int64_t)row * K + c8 * 8);
+      }
+    } else {
+      // B given as [K, N] (a forward weight read as its transpose, the data-gradient case): each thread
+      // reads 8 consecutive n of one k (16 bytes) and scatters them down 8 LDS rows
+      const T* Bp = reinterpret_cast<const T*>(p.B) + col0;
+      constexpr int per_k = NC / 8;
+      for (int c = threadIdx.x; c < K * per_k; c += kThreads) {
+        const int k = c / per_k, n8 = c - k * per_k;
+        typedef T t8 __attribute__((ext_vector_type(8)));
+        const t8 v = *reinterpret_cast<const t8*>(Bp + (int64_t)k * N + n8 * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) *reinterpret_cast<T*>(bl + (n8 * 8 + j) * RS + 2 * k) = v[j];
+      }
+    }
+    if constexpr (PRO) {
+      for (int c = threadIdx.x; c < K; c += kThreads) {
+        ss[c] = p.pro_scale[c];
+        ss[K + c] = p.pro_shift[c];
+      }
+    }
+    if constexpr (EPI == kC1x1Bwd) {  // the previous BatchNorm's per-column constants, read per tile
+      for (int c = threadIdx.x; c < NC; c += kThreads) {
+        ss[c] = p.bscale[col0 + c];
+        ss[NC + c] = p.bshift[col0 + c];
+        ss[2 * NC + c] = p.bmean[col0 + c];
+      }
+    }
+  }
+  __syncthreads();
+
+  // per-lane statistics of column col0 + 32 t + r
+  float s1[NT], s2[NT], e0[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    s1[t] = s2[t] = 0.f;
+    e0[t] = 0.f;
+    if constexpr (EPI == kC1x1Stats) e0[t] = p.kshift ? p.kshift[col0 + 32 * t + r] : 0.f;
+  }
+
+  const T* __restrict__ A = reinterpret_cast<const T*>(p.A);
+  T* __restrict__ Cp = reinterpret_cast<T*>(p.C);
+  const T* __restrict__ Rp = reinterpret_cast<const T*>(p.R);
+  const T* __restrict__ Yp = reinterpret_cast<const T*>(p.by);
+  auto arow = [&](int sp) -> int64_t {
+    const int64_t m = (int64_t)sp * 32 + r;
+    if constexpr (S2) {
+      const int Wo = p.s2_W >> 1, HWo = (p.s2_H >> 1) * Wo;
+      const int64_t n = m / HWo;
+      const int rem = (int)(m - n * HWo), yo = rem / Wo, xo = rem - yo * Wo;
+      return (n * p.s2_H + 2 * yo) * p.s2_W + 2 * xo;
+    } else {
+      return m;
+    }
+  };
+  // The wave's work is a flat sequence of (strip, chunk) steps; A fragments are double-buffered in
+  // registers so that the loads of step i + 1 are in flight during step i's MFMAs (and epilogue).
+  const int stride = g.G * kWaves;
+  const int first = grp * kWaves + wave;
+  const int total = (first < g.strips ? (g.strips - first + stride - 1) / stride : 0) * nch;
+  i4v a0[KS], a1[KS];
+  auto load = [&](int i, i4v(&a)[KS]) {
+    const int q = i / nch, c = i - q * nch;
+    const T* src = A + arow(first + q * stride) * K + c * KC + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) a[s] = __builtin_nontemporal_load(reinterpret_cast<const i4v*>(src + 16 * s));
+  };
+  f16v acc[NT];
+  auto process = [&](int i, i4v(&a)[KS]) {
+    const int q = i / nch, c = i - q * nch;
+    const int strip = first + q * stride;
+    if (c == 0) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[t][v] = 0.f;
+    }
+    if constexpr (PRO) {
+      // BatchNorm + ReLU of the producing layer, on the fragment (channels 16 s + 8 h .. + 7)
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int kb = c * KC + 16 * s + 8 * h;
+        const float4 c0 = *reinterpret_cast<const float4*>(ss + kb);
+        const float4 c1 = *reinterpret_cast<const float4*>(ss + kb + 4);
+        const float4 d0 = *reinterpret_cast<const float4*>(ss + K + kb);
+        const float4 d1 = *reinterpret_cast<const float4*>(ss + K + kb + 4);
+        const float sc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        const float sh[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+        V8 v = __builtin_bit_cast(V8, a[s]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = from_f<T>(fmaxf(fmaf(to_f<T>(v[j]), sc[j], sh[j]), 0.f));
+        a[s] = __builtin_bit_cast(i4v, v);
+      }
+    }
+    int boff = r * RS + 16 * h + c * KC * 2;
+    asm volatile("" : "+v"(boff));  // opaque: keeps the B fragment reads in the loop, not in VGPRs
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const i4v bf = *reinterpret_cast<const i4v*>(bl + boff + t * 32 * RS + 32 * s);
+        acc[t] = Mf<T>::run(a[s], bf, acc[t]);
+      }
+    if (c + 1 < nch) return;
+    // ---- epilogue ----
+    const int64_t row0 = (int64_t)strip * 32 + 4 * h;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = col0 + 32 * t + r;
+      float xr[16];
+      if constexpr (RES || EPI == kC1x1Bwd) {
+        const T* src = RES ? Rp : Yp;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) xr[4 * j + i] = to_f<T>(src[(row0 + 8 * j + i) * N + col]);
+      }
+      float bsc = 0.f, bsh = 0.f, bmn = 0.f;
+      if constexpr (EPI == kC1x1Bwd) {
+        bsc = ss[32 * t + r];
+        bsh = ss[NC + 32 * t + r];
+        bmn = ss[2 * NC + 32 * t + r];
+      }
+      float yv[16];
+      if constexpr (RES && EPI == kC1x1Bwd) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) yv[4 * j + i] = to_f<T>(Yp[(row0 + 8 * j + i) * N + col]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int v = 4 * j + i;
+          float x = acc[t][v];
+          if constexpr (RES) x += xr[v];
+          const T o = from_f<T>(x);
+          Cp[(row0 + 8 * j + i) * N + col] = o;
+          const float f = to_f<T>(o);  // statistics of the value as stored
+          if constexpr (EPI == kC1x1Stats) {
+            const float d = f - e0[t];
+            s1[t] += d;
+            s2[t] = fmaf(d, d, s2[t]);
+          } else if constexpr (EPI == kC1x1Bwd) {
+            const float y = RES ? yv[v] : xr[v];
+            const float dz = (!p.brelu || fmaf(y, bsc, bsh) > 0.f) ? f : 0.f;
+            s1[t] += dz;
+            s2[t] = fmaf(dz, y - bmn, s2[t]);
+          }
+        }
+      // one tile's residual / input loads at a time: hoisting every tile's 16-32 loads to the top
+      // of the epilogue spills at NC >= 128
+      if constexpr (RES || EPI == kC1x1Bwd) __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  if (total > 0) load(0, a0);
+  for (int i = 0; i < total; i += 2) {
+    if (i + 1 < total) load(i + 1, a1);
+    process(i, a0);
+    if (i + 1 < total) {
+      if (i + 2 < total) load(i + 2, a0);
+      process(i + 1, a1);
+    }
+  }
+
+  if constexpr (EPI != kC1x1Plain) {
+    float* red = reinterpret_cast<float*>(smem + g.red_off);  // [waves][2][NC]
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      s1[t] += __shfl_xor(s1[t], 32);
+      s2[t] += __shfl_xor(s2[t], 32);
+      if (h == 0) {
+        red[(wave * 2) * NC + 32 * t + r] = s1[t];
+        red[(wave * 2 + 1) * NC + 32 * t + r] = s2[t];
+      }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < NC; c += kThreads) {
+      float u = 0.f, w = 0.f;
+#pragma unroll
+      for (int q = 0; q < kWaves; ++q) {
+        u += red[(q * 2) * NC + c];
+        w += red[(q * 2 + 1) * NC + c];
+      }
+      p.part[(int64_t)grp * N + col0 + c] = u;
+      p.part[((int64_t)g.G + grp) * N + col0 + c] = w;
+    }
+  }
+}
+
+constexpr int kSumRows = 16;  // partial rows summed in parallel per column
+
+__global__ __launch_bounds__(64 * kSumRows) void k_sum_parts(int G, int N, const float* __restrict__ part,
+                                                             float* __restrict__ sums, float count) {
+  // block = 64 columns x kSumRows row groups of one statistic (blockIdx.y); coalesced 256-byte rows,
+  // a fixed order (strided per group, then the groups in order): deterministic
+  __shared__ float sh[kSumRows][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl, which = blockIdx.y;
+  float acc = 0.f;
+  if (c < N) {
+    const float* src = part + (int64_t)which * G * N + c;
+    for (int g = rg; g < G; g += kSumRows) acc += src[(int64_t)g * N];
+  }
+  sh[rg][cl] = acc;
+  __syncthreads();
+  if (rg == 0 && c < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < kSumRows; ++q) t += sh[q][cl];
+    sums[(int64_t)which * N + c] = t;
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && count >= 0.f) sums[2 * N] = count;
+}
+
+// ---------------------------------------------------------------------------- host side
+struct Plan {
+  int NC, KC, lds, occ;
+  Geo g;
+};
+
+int ss_bytes(int NC, int K, bool pro, bool bwd) { return pro ? 8 * K : (bwd ? 12 * NC : 0); }
+
+int lds_bytes(int NC, int K, bool pro, bool bwd, bool stats) {
+  int b = NC * (2 * K + 16) + ss_bytes(NC, K, pro, bwd);
+  if (stats) b += kWaves * 2 * NC * 4;
+  return b;
+}
+
+bool make_plan(const C1x1Args& a, Plan* pl) {
+  if (a.K <= 0 || a.N <= 0 || a.M <= 0 || a.K % 64 != 0 || a.N % 64 != 0 || a.M % 32 != 0) return false;
+  if (a.M / 32 >= (1ll << 31)) return false;
+  const bool pro = a.pro_scale != nullptr, stats = a.epi != kC1x1Plain, bwd = a.epi == kC1x1Bwd;
+  // register budget: the backward epilogue (input loads + statistics) fits 4 column tiles per wave
+  const int max_nc = bwd ? (a.R ? 64 : 128) : 256;
+  int NC = 0, occ = 0;
+  // the widest column slice (A read once per slice) that still leaves two workgroups per CU; else one
+  for (int want_occ = 2; want_occ >= 1 && !NC; --want_occ)
+    for (int nc : {256, 128, 64})
+      if (nc <= max_nc && a.N % nc == 0 && lds_bytes(nc, a.K, pro, bwd, stats) <= 160 * 1024 / want_occ) {
+        NC = nc;
+        occ = want_occ;
+        break;
+      }
+  if (!NC) return false;
+  // registers: two A chunks of KC / 4 VGPRs each next to NC / 2 accumulators
+  const int KC = (NC <= 128 && a.K % 128 == 0 && !(bwd && NC == 128)) ? 128 : 64;
+  Geo g{};
+  g.nslices = a.N / NC;
+  g.strips = (int)(a.M / 32);
+  const int want = (g.strips + kWaves - 1) / kWaves;         // one strip per wave
+  const int cap = std::max(1, occ * 256 / g.nslices);        // resident workgroups per slice
+  g.G = (std::min(want, cap) + 7) / 8 * 8;
+  g.ss_off = NC * (2 * a.K + 16);
+  g.red_off = g.ss_off + ss_bytes(NC, a.K, pro, bwd);
+  pl->NC = NC;
+  pl->KC = KC;
+  pl->lds = lds_bytes(NC, a.K, pro, bwd, stats);
+  pl->occ = occ;
+  pl->g = g;
+  return true;
+}
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+template <typename T> struct Tag { using type = T; };
+
+}  // namespace
+
+bool c1x1_supported(const C1x1Args& a) {
+  Plan pl;
+  if (!make_plan(a, &pl)) return false;
+  if (!al16(a.A) || !al16(a.B) || !al16(a.C) || (a.R && !al16(a.R))) return false;
+  if (a.epi == kC1x1Bwd && (!a.by || !a.bscale || !a.bshift || !a.bmean)) return false;
+  if (a.epi != kC1x1Plain && !a.part) return false;
+  if (a.s2_H > 0) {
+    if (a.s2_H % 2 || a.s2_W % 2 || a.M % ((int64_t)(a.s2_H / 2) * (a.s2_W / 2))) return false;
+    if (a.pro_scale || a.R || a.epi == kC1x1Bwd) return false;  // combinations not instantiated
+  }
+  if (a.pro_scale && (a.R || a.epi != kC1x1Stats)) return false;
+  return true;
+}
+
+int c1x1_parts(const C1x1Args& a) {
+  Plan pl;
+  return make_plan(a, &pl) ? pl.g.G : 0;
+}
+
+void c1x1_run(int dt, const C1x1Args& a, hipStream_t st) {
+  if (!c1x1_supported(a)) throw std::runtime_error("c1x1: unsupported shape / arguments");
+  Plan pl;
+  make_plan(a, &pl);
+  const dim3 grid(pl.g.nslices * pl.g.G), block(kThreads);
+  const bool pro = a.pro_scale != nullptr, s2 = a.s2_H > 0, res = a.R != nullptr;
+  // instantiated flag combinations: (epi, pro, s2, res)
+  auto go = [&](auto tt, auto kc, auto nc) {
+    using T = typename decltype(tt)::type;
+    constexpr int KC = decltype(kc)::value, NC = decltype(nc)::value;
+    auto L = [&](auto kern) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, pl.lds);
+      hipLaunchKernelGGL(kern, grid, block, pl.lds, st, a, pl.g);
+    };
+    if (a.epi == kC1x1Stats) {
+      if (pro) L(k_c1x1<T, KC, NC, kC1x1Stats, true, false, false>);
+      else if (s2) L(k_c1x1<T, KC, NC, kC1x1Stats, false, true, false>);
+      else L(k_c1x1<T, KC, NC, kC1x1Stats, false, false, false>);
+    } else if (a.epi == kC1x1Bwd) {
+      if constexpr (NC <= 64) {
+        if (res) L(k_c1x1<T, KC, NC, kC1x1Bwd, false, false, true>);
+      }
+      if constexpr (NC <= 128) {
+        if (!res) L(k_c1x1<T, KC, NC, kC1x1Bwd, false, false, false>);
+      }
+    } else {
+      if (s2) L(k_c1x1<T, KC, NC, kC1x1Plain, false, true, false>);
+      else if (res) L(k_c1x1<T, KC, NC, kC1x1Plain, false, false, true>);
+      else L(k_c1x1<T, KC, NC, kC1x1Plain, false, false, false>);
+    }
+  };
+  auto by_nc = [&](auto tt, auto kc) {
+    switch (pl.NC) {
+      case 64: go(tt, kc, std::integral_constant<int, 64>{}); break;
+      case 128: go(tt, kc, std::integral_constant<int, 128>{}); break;
+      default:
+        if constexpr (decltype(kc)::value == 64) go(tt, kc, std::integral_constant<int, 256>{});
+        else throw std::runtime_error("c1x1: KC 128 with NC 256 is not instantiated");
+    }
+  };
+  auto by_kc = [&](auto tt) {
+    if (pl.KC == 64) by_nc(tt, std::integral_constant<int, 64>{});
+    else by_nc(tt, std::integral_constant<int, 128>{});
+  };
+  switch (dt) {
+    case kF16: by_kc(Tag<f16>{}); break;
+    case kBF16: by_kc(Tag<bf16>{}); break;
+    default: throw std::runtime_error("c1x1: fp16 / bf16 only");
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("c1x1: ") + hipGetErrorString(e));
+}
+
+void c1x1_sum_parts(int G, int N, const float* part, float* sums, float count, hipStream_t st) {
+  hipLaunchKernelGGL(k_sum_parts, dim3((N + 63) / 64, 2), dim3(64 * kSumRows), 0, st, G, N, part, sums, count);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("c1x1_sum_parts: ") + hipGetErrorString(e));
+}
+
+}  // namespace bh

@@ -291,6 +291,20 @@ __global__ __launch_bounds__(C::kThreads, 1) void k_gemm_nt(Args p) {
     for (int c = 0; c < 8; ++c) bias[c] = 0.f;
   }
   T* __restrict__ Cp = reinterpret_cast<T*>(p.C);
+  // BatchNorm statistics epilogue (e.bn_stats, see bh/gemm_api.h): per-column constants of this
+  // lane's 8 columns, loaded once
+  float bk[8], bsc[8], bsh[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) bk[c] = bsc[c] = bsh[c] = 0.f;
+  if (e.bn_stats && col_ok) {
+    if (e.bn_stats == 1) {
+      if (e.kshift) VecIO<float>::load(e.kshift + gcol, bk);
+    } else {
+      VecIO<float>::load(e.bn_scale + gcol, bsc);
+      VecIO<float>::load(e.bn_shift + gcol, bsh);
+      VecIO<float>::load(e.bn_mean + gcol, bk);
+    }
+  }
 #pragma unroll
   for (int chunk = 0; chunk < C::TM / 4; ++chunk) {
 #pragma unroll
@@ -302,6 +316,7 @@ __global__ __launch_bounds__(C::kThreads, 1) void k_gemm_nt(Args p) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // image is wave-private: in-order LDS suffices
     const int row0 = brow + wr * C::WTM + chunk * 64;
     float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float csq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 2
     for (int i = 0; i < 8; ++i) {
       const int lr = (lane >> 3) + 8 * i;
@@ -335,9 +350,48 @@ __global__ __launch_bounds__(C::kThreads, 1) void k_gemm_nt(Args p) {
           }
         }
         VecIO<T>::store(Cp + (int64_t)grow * p.ldc + gcol, v);
+        if (e.bn_stats == 1) {  // statistics of the stored value, centred on kshift
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            const float d = to_f<T>(from_f<T>(v[c])) - bk[c];
+            csum[c] += d;
+            csq[c] = fmaf(d, d, csq[c]);
+          }
+        } else if (e.bn_stats == 2) {  // the previous BatchNorm's backward sums
+          float y[8];
+          VecIO<T>::load(reinterpret_cast<const T*>(e.bn_y) + (int64_t)grow * p.ldc + gcol, y);
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            const float g = to_f<T>(from_f<T>(v[c]));
+            const float dz = (!e.bn_relu || fmaf(y[c], bsc[c], bsh[c]) > 0.f) ? g : 0.f;
+            csum[c] += dz;
+            csq[c] = fmaf(dz, y[c] - bk[c], csq[c]);
+          }
+        }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // image reads done before the next chunk
+    if (e.bn_stats) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        float a = csum[c], b = csq[c];
+        a += __shfl_xor(a, 8);
+        b += __shfl_xor(b, 8);
+        a += __shfl_xor(a, 16);
+        b += __shfl_xor(b, 16);
+        a += __shfl_xor(a, 32);
+        b += __shfl_xor(b, 32);
+        csum[c] = a;
+        csq[c] = b;
+      }
+      const int64_t slab = row0 / 64, slabs = ((int64_t)p.M + 63) / 64;
+      if (lane < 8 && col_ok && row0 < p.M) {
+        float* d1 = e.stat_part + slab * p.N + gcol;
+        float* d2 = e.stat_part + (slabs + slab) * p.N + gcol;
+        VecIO<float>::store(d1, csum);
+        VecIO<float>::store(d2, csq);
+      }
+    }
     if (e.bgrad_part) {
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
@@ -713,7 +767,7 @@ void gemm_nt(int dt, const void* A, int64_t lda, const void* B, int64_t ldb, voi
   const int64_t big_wgs = ((M + CfgBig::BM - 1) / CfgBig::BM) * ((N + CfgBig::BN - 1) / CfgBig::BN);
   // the ping-pong kernel keeps row offsets of a 256-row tile in 32 bits
   const bool pp_ok = glds && lda < (1 << 22) && ldb < (1 << 22);
-  const bool pp = pp_ok && (tile_mode == 4 || (tile_mode == 0 && big_wgs >= 256));
+  const bool pp = pp_ok && !epi.bn_stats && (tile_mode == 4 || (tile_mode == 0 && big_wgs >= 256));
   const bool big = glds && !pp && (tile_mode == 2 || (tile_mode == 0 && big_wgs >= 256));
   const bool mid = glds && tile_mode == 3;
   switch (dt) {

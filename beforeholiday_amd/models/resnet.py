@@ -438,6 +438,168 @@ def conv1x1(cin, cout, stride=1):
     return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
 
 
+# ------------------------------------------------------------------------------------------------
+# BatchNorm folded into the convolutions (BH_FOLD_BN=1, default for the fused model): each conv's
+# epilogue produces the statistics partials of the BatchNorm that follows it (no statistics pass),
+# and the data gradient of each conv whose input came out of a BatchNorm(+ReLU) reduces that
+# BatchNorm's backward sums in its epilogue (no backward-reduce pass). See kernels/conv_bn.hip and
+# kernels/conv.hip (the 3x3 kernel's EPI variants).
+
+
+def _kshift(bn):
+    """The statistics centre shared by the conv epilogue and syncbn.merge_sums: the running mean."""
+    rm = getattr(bn, "running_mean", None)
+    return rm if rm is not None and rm.dtype == torch.float32 else None
+
+
+def _part_from_tensor(y, kshift):
+    """Fallback statistics partials ([2, 1, C]) from a statistics pass over y."""
+    from ..ops import syncbn
+
+    C = y.size(1)
+    return syncbn.stats_local_sums(y, kshift)[:2 * C].view(2, 1, C)
+
+
+def _link_ok(link, c):
+    return link is not None and link.y is not None and link.y.size(1) == c
+
+
+class _Conv1x1BNFn(torch.autograd.Function):
+    """1x1 convolution (stride 1, or stride 2 read in place) of a channels_last activation whose
+    epilogue emits the next BatchNorm's statistics partials; backward: data gradient with the
+    previous BatchNorm's backward sums (``link_in``) and the parked residual gradient (``box``) in its
+    epilogue, weight gradient on the MFMA wgrad kernel (or MIOpen, per shape)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, kshift, link_in, box, s2):
+        from ..ops import conv_bn
+
+        n, c, h, w = x.shape
+        k = weight.size(0)
+        a2d = x.permute(0, 2, 3, 1).reshape(-1, c)
+        w2d = weight.view(k, c)
+        ho, wo = (h // 2, w // 2) if s2 else (h, w)
+        hw = (h, w) if s2 else None
+        if conv_bn.preferred(c, k, n * ho * wo, s2) and conv_bn.supported(a2d, w2d, s2=hw, epi="stats"):
+            y2d, part = conv_bn.c1x1(a2d, w2d, s2=hw, epi="stats", kshift=kshift)
+            y = y2d.view(n, ho, wo, k).permute(0, 3, 1, 2)
+        else:  # hipBLASLt on the [pixels, channels] view (MIOpen for stride 2) + a statistics pass
+            if s2:
+                y = torch.nn.functional.conv2d(x, weight, stride=2)
+            else:
+                y = torch.mm(a2d, w2d.t()).view(n, h, w, k).permute(0, 3, 1, 2)
+            part = _part_from_tensor(y, kshift)
+        ctx.save_for_backward(x, weight)
+        ctx.link_in, ctx.box, ctx.s2 = link_in, box, s2
+        ctx.mark_non_differentiable(part)
+        ctx.set_materialize_grads(False)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, gy, _gpart):
+        from ..ops import conv as bhconv
+        from ..ops import conv_bn
+
+        x, weight = ctx.saved_tensors
+        n, c, h, w = x.shape
+        k = weight.size(0)
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        conv_bwd = torch.ops.aten.convolution_backward
+        st = 2 if ctx.s2 else 1
+        args = ([st, st], [0, 0], [1, 1], False, [0, 0], 1)
+        box = ctx.box
+        acc = box.pop("g", None) if box is not None else None
+        if acc is not None and not (acc.is_contiguous(memory_format=torch.channels_last) and acc.dtype == gy.dtype
+                                    and acc.shape == x.shape):
+            acc = acc.contiguous(memory_format=torch.channels_last).to(gy.dtype)
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            if ctx.s2:
+                gx = conv_bwd(gy, x, weight, None, *args, [True, False, False])[0]
+                if acc is not None:
+                    gx = gx + acc
+            else:
+                gy2d = gy.permute(0, 2, 3, 1).reshape(-1, k)
+                w2d = weight.view(k, c)  # dX = dY . W: the strip kernel reads W as the [K, N] operand
+                r2d = acc.permute(0, 2, 3, 1).reshape(-1, c) if acc is not None else None
+                link = ctx.link_in
+                fast = conv_bn.preferred(k, c, gy2d.size(0))
+                if fast and _link_ok(link, c) and conv_bn.supported(gy2d, w2d, resid=r2d is not None, epi="bwd",
+                                                                    b_trans=True):
+                    y2d = link.y.permute(0, 2, 3, 1).reshape(-1, c)
+                    gx2d, part = conv_bn.c1x1(gy2d, w2d, resid=r2d, epi="bwd", by=y2d, bscale=link.scale,
+                                              bshift=link.shift, bmean=link.mean, brelu=link.relu, b_trans=True)
+                    link.sums = conv_bn.sum_parts(part)
+                elif fast and conv_bn.supported(gy2d, w2d, resid=r2d is not None, b_trans=True):
+                    gx2d, _ = conv_bn.c1x1(gy2d, w2d, resid=r2d, b_trans=True)
+                elif r2d is not None:  # beta = 1 into the parked residual gradient (no output copy)
+                    gx2d = torch.addmm(r2d, gy2d, w2d, out=r2d)
+                else:
+                    gx2d = torch.mm(gy2d, w2d)
+                gx = gx2d.view(n, h, w, c).permute(0, 3, 1, 2)
+            acc = None
+        if box is not None:
+            box["conv_done"] = True
+        if ctx.needs_input_grad[1]:
+            if ctx.s2:
+                gw = bhconv.conv_wgrad_s2(x, gy) if bhconv.wgrad_supported(x, gy, 1, 2) else \
+                    conv_bwd(gy, x, weight, None, *args, [False, True, False])[1]
+                if gw.stride() != weight.stride():
+                    gw = gw.contiguous()
+            else:
+                gw = _wgrad(x, gy, weight, 1, "auto", lambda: conv_bwd(gy, x, weight, None, *args,
+                                                                       [False, True, False])[1])
+        return gx, gw, None, None, None, None
+
+
+class _Conv3x3BNFn(torch.autograd.Function):
+    """3x3 / stride-1 convolution on the direct MFMA kernel with the next BatchNorm's statistics in
+    its epilogue; backward: data gradient (flipped-weight kernel) with the previous BatchNorm's
+    backward sums in its epilogue, weight gradient on the MFMA wgrad kernel."""
+
+    @staticmethod
+    def forward(ctx, x, weight, kshift, link_in):
+        from .._native import submodule
+
+        y, part = submodule("conv_cuda").conv3x3_bn_forward(x, weight, None, None, True, kshift)
+        ctx.save_for_backward(x, weight)
+        ctx.link_in = link_in
+        ctx.mark_non_differentiable(part)
+        ctx.set_materialize_grads(False)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, gy, _gpart):
+        from .._native import submodule
+        from ..ops import conv as bhconv
+        from ..ops import conv_bn
+
+        x, weight = ctx.saved_tensors
+        c = x.size(1)
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        conv_bwd = torch.ops.aten.convolution_backward
+        args = ([1, 1], [1, 1], [1, 1], False, [0, 0], 1)
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            link = ctx.link_in
+            # the 3x3 data gradient's BatchNorm-sums epilogue reads the previous BatchNorm's input 2 bytes
+            # per lane; measured slower than the separate reduce pass at 56x56 (170 vs 104 + 50 us), so
+            # it is opt-in (BH_FOLD_3X3_BWD=1)
+            if _FOLD_3X3_BWD and _link_ok(link, c) and link.y.is_contiguous(memory_format=torch.channels_last):
+                gx, part = submodule("conv_cuda").conv3x3_bn_dgrad(gy, weight, link.y, link.scale, link.shift,
+                                                                   link.mean, link.relu)
+                link.sums = conv_bn.sum_parts(part)
+            else:
+                gx = bhconv.conv3x3_dgrad(gy, weight)
+        if ctx.needs_input_grad[1]:
+            gw = _wgrad(x, gy, weight, 3, "gemm", lambda: conv_bwd(gy, x, weight, None, *args, [False, True, False])[1])
+        return gx, gw, None, None
+
+
+_FOLD_BN = os.environ.get("BH_FOLD_BN", "1") != "0"
+_FOLD_3X3_BWD = os.environ.get("BH_FOLD_3X3_BWD", "0") == "1"
+
+
 class Bottleneck(nn.Module):
     expansion = 4
 
@@ -456,8 +618,45 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
         self.stride = stride
 
+    def _fold_ok(self, x):
+        from ..parallel import SyncBatchNorm
+
+        bns = [self.bn1, self.bn2, self.bn3] + ([self.downsample[1]] if self.downsample is not None else [])
+        return (_FOLD_BN and self.training and x.is_cuda and x.dim() == 4 and x.dtype in (torch.float16, torch.bfloat16)
+                and x.is_contiguous(memory_format=torch.channels_last) and self.conv1.weight.dtype == x.dtype
+                and all(isinstance(b, SyncBatchNorm) and b.track_running_stats and b.channel_last
+                        and b.running_mean is not None and b.running_mean.dtype == torch.float32 for b in bns)
+                and (self.downsample is None or len(self.downsample) == 2))
+
+    def _forward_folded(self, x):
+        from ..ops import conv as bhconv
+        from ..parallel.optimized_sync_batchnorm import BNLink
+
+        box = {} if (torch.is_grad_enabled() and x.requires_grad) else None
+        y1, p1 = _Conv1x1BNFn.apply(x, self.conv1.weight, _kshift(self.bn1), None, box, False)
+        l1 = BNLink()
+        a1 = self.bn1.forward_from_stats(y1, p1, link=l1)
+        l2 = None
+        if self.stride == 1 and bhconv.supported(a1, self.conv2.weight):
+            y2, p2 = _Conv3x3BNFn.apply(a1, self.conv2.weight, _kshift(self.bn2), l1)
+            l2 = BNLink()
+            a2 = self.bn2.forward_from_stats(y2, p2, link=l2)
+        else:  # stride-2 3x3 (MIOpen): its BatchNorm computes its own statistics
+            a2 = self.bn2(self.conv2(a1))
+        y3, p3 = _Conv1x1BNFn.apply(a2, self.conv3.weight, _kshift(self.bn3), l2, None, False)
+        xs = _GradStash.apply(x, box) if box is not None else x
+        if self.downsample is not None:
+            conv_d, bn_d = self.downsample[0], self.downsample[1]
+            yd, pd = _Conv1x1BNFn.apply(xs, conv_d.weight, _kshift(bn_d), None, None, self.stride == 2)
+            identity = bn_d.forward_from_stats(yd, pd)
+        else:
+            identity = xs
+        return self.bn3.forward_from_stats(y3, p3, z=identity)
+
     def forward(self, x):
         identity = x
+        if self.fused and self._fold_ok(x):
+            return self._forward_folded(x)
         if self.fused:
             # BN+ReLU and BN+residual-add+ReLU run as single fused passes (SyncBatchNorm fuse_relu)
             box = None
@@ -547,7 +746,7 @@ def resnet50(**kw) -> ResNet:
 
 
 def resnet50_fused(process_group=None, channel_last=True, conv1x1_mode="auto", stem_pool_fused=True,
-                   gemm_1x1=None, conv3x3_mode="auto", **kw) -> ResNet:
+                   gemm_1x1=None, conv3x3_mode="auto", layers=(3, 4, 6, 3), **kw) -> ResNet:
     """ResNet-50 whose BatchNorms are fused SyncBatchNorms (BN+ReLU and BN+add+ReLU in one pass),
     synchronised over ``process_group`` -- the 'amp O2 + SyncBatchNorm' benchmark model.
     ``conv1x1_mode``: stride-1 1x1 convolutions as hipBLASLt GEMMs on the channels_last view
@@ -565,7 +764,7 @@ def resnet50_fused(process_group=None, channel_last=True, conv1x1_mode="auto", s
     old, _CONV1X1_MODE = _CONV1X1_MODE, conv1x1_mode
     old3, _CONV3X3_MODE = _CONV3X3_MODE, conv3x3_mode
     try:
-        return ResNet(Bottleneck, [3, 4, 6, 3], norm_layer=norm, fused=True, stem_pool_fused=stem_pool_fused, **kw)
+        return ResNet(Bottleneck, list(layers), norm_layer=norm, fused=True, stem_pool_fused=stem_pool_fused, **kw)
     finally:
         _CONV1X1_MODE = old
         _CONV3X3_MODE = old3

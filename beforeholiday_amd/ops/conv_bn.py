@@ -1,0 +1,114 @@
+"""1x1 convolution GEMMs with BatchNorm folded in (kernels/conv_bn.hip, ``_C.conv_bn``).
+
+All tensors are ``[pixels, channels]`` views of NHWC activations. ``c1x1`` returns ``(C, part)``:
+
+* ``C = f(A) @ B.T`` (+ ``resid``) rounded to A's dtype, with ``f(a) = relu(a * pro_scale + pro_shift)``
+  per input channel when a prologue is given (the producing layer's BatchNorm + ReLU, never written);
+* ``s2=(H, W)``: output row (n, y, x) reads input row (n, 2y, 2x) of an ``[N, H, W, K]`` input
+  (1x1 / stride-2 convolution);
+* ``epi="stats"``: ``part [2, G, N]`` holds per-workgroup sums of ``C - kshift`` and ``(C - kshift)^2``
+  (C as stored) -- :func:`sum_parts` turns them into the ``[2N+1]`` payload of
+  ``syncbn.stats_local_sums``;
+* ``epi="bwd"``: with ``by`` (the raw input of the previous BatchNorm, same shape as C), ``dz = C *
+  (by * bscale + bshift > 0)``: sums of ``dz`` and ``dz * (by - bmean)`` -- that BatchNorm's backward
+  reduction (``syncbn.backward_reduce``'s sums), computed as the data gradient is produced.
+
+GPU tensors run the HIP kernel (no silent fallback: unsupported shapes raise); CPU tensors run the
+fp32 reference below, which is also what the GPU tests compare against.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from .._native import available, submodule
+
+_EPI = {"plain": 0, "stats": 1, "bwd": 2}
+
+
+def _gather_s2(a: torch.Tensor, s2) -> torch.Tensor:
+    H, W = s2
+    K = a.size(1)
+    return a.view(-1, H, W, K)[:, ::2, ::2, :].reshape(-1, K)
+
+
+def _reference(a, b, pro_scale, pro_shift, resid, s2, epi, kshift, by, bscale, bshift, bmean, brelu):
+    if s2 is not None:
+        a = _gather_s2(a, s2)
+    af = a.float()
+    if pro_scale is not None:
+        af = torch.relu(af * pro_scale + pro_shift).to(a.dtype).float()
+    c = af @ b.float().t()
+    if resid is not None:
+        c = c + resid.float()
+    c = c.to(a.dtype)
+    cf = c.float()
+    N = b.size(0)
+    if epi == "stats":
+        d = cf - (kshift if kshift is not None else 0.0)
+        part = torch.stack([d.sum(0), (d * d).sum(0)]).view(2, 1, N)
+    elif epi == "bwd":
+        y = by.float()
+        dz = cf * ((y * bscale + bshift) > 0).float() if brelu else cf
+        part = torch.stack([dz.sum(0), (dz * (y - bmean)).sum(0)]).view(2, 1, N)
+    else:
+        part = torch.empty(0)
+    return c, part
+
+
+def c1x1(a: torch.Tensor, b: torch.Tensor, pro_scale: Optional[torch.Tensor] = None,
+         pro_shift: Optional[torch.Tensor] = None, resid: Optional[torch.Tensor] = None, s2=None,
+         epi: str = "plain", kshift: Optional[torch.Tensor] = None, by: Optional[torch.Tensor] = None,
+         bscale: Optional[torch.Tensor] = None, bshift: Optional[torch.Tensor] = None,
+         bmean: Optional[torch.Tensor] = None, brelu: bool = True,
+         b_trans: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``b_trans``: ``b`` is given as ``[K, N]`` (e.g. a forward weight for the data gradient)."""
+    rows = a.size(0)
+    M = rows // 4 if s2 is not None else rows
+    if not a.is_cuda:
+        return _reference(a, b.t() if b_trans else b, pro_scale, pro_shift, resid, s2, epi, kshift, by, bscale,
+                          bshift, bmean, brelu)
+    H, W = s2 if s2 is not None else (0, 0)
+    return submodule("conv_bn").c1x1(a, b, b_trans, M, pro_scale, pro_shift, resid, H, W, _EPI[epi], kshift, by,
+                                     bscale, bshift, bmean, brelu)
+
+
+def supported(a: torch.Tensor, b: torch.Tensor, pro: bool = False, resid: bool = False, s2=None,
+              epi: str = "plain", b_trans: bool = False) -> bool:
+    if not (a.is_cuda and available()):
+        return False
+    H, W = s2 if s2 is not None else (0, 0)
+    M = a.size(0) // 4 if s2 is not None else a.size(0)
+    return submodule("conv_bn").c1x1_supported(a, b, b_trans, M, pro, resid, H, W, _EPI[epi])
+
+
+def preferred(K: int, N: int, M: int, s2: bool = False) -> bool:
+    """Whether the strip kernel beats hipBLASLt + a separate BatchNorm pass for a ``[M, K] x [K, N]``
+    layer (microbenchmark: profiles/conv_bn_vs_unfused.jsonl). It wins the HBM-bound shapes -- both
+    channel counts <= 256 on 56x56 / 28x28 pixels, and the stride-2 gather from 256 channels -- and
+    loses the MFMA-bound ones (a K >= 512 layer keeps its whole weight slice in LDS, so the column
+    slices get narrow and the activation is re-read per slice)."""
+    if s2:  # against MIOpen's stride-2 kernel (or a strided gather + GEMM) plus the statistics pass
+        return K <= 256
+    return K <= 256 and N <= 256 and M >= 100000
+
+
+def sum_parts(part: torch.Tensor, count: float = -1.0) -> torch.Tensor:
+    """``[2N+1]`` = (sum over partial rows of both statistics, count) when ``count >= 0``, else ``[2N]``."""
+    if part.is_cuda:
+        return submodule("conv_bn").sum_parts(part, float(count))
+    out = part.sum(1).reshape(-1)
+    if count >= 0:
+        out = torch.cat([out, torch.tensor([float(count)], dtype=out.dtype)])
+    return out
+
+
+def gemm_bn(a: torch.Tensor, b: torch.Tensor, epi: str = "stats", kshift=None, by=None, bscale=None, bshift=None,
+            bmean=None, brelu: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``C = a @ b.T`` on the tiled MFMA GEMM (kernels/gemm.hip, 128x128 / 256x128 / 256x256 tiles) with the
+    same BatchNorm epilogues as :func:`c1x1` (``epi`` "stats" or "bwd"; partials per 64-row slab):
+    the compute-bound 1x1 layers (K or N >= 512) that the strip kernel runs at low MFMA rates."""
+    if not a.is_cuda:
+        return _reference(a, b, None, None, None, None, epi, kshift, by, bscale, bshift, bmean, brelu)
+    return submodule("conv_bn").gemm_bn(a, b, _EPI[epi], kshift, by, bscale, bshift, bmean, brelu)

@@ -18,8 +18,13 @@ MI355X / RCCL design:
   reference's element count, sized per xGMI peer (:func:`xgmi_bucket_mb`).
 * averaging uses ``ReduceOp.AVG`` inside the collective when the backend supports it (RCCL), so no
   extra scaling kernel runs per bucket.
-* each bucket owns a persistent flat buffer: the gather is one ``torch.cat(out=)`` and the scatter
-  back one fused ``_foreach_copy_`` launch (fixed pointers, no allocator churn).
+* gradients live IN the buckets (gradient-as-bucket-view): once the bucket structure is known each
+  parameter gets a slot view of its bucket's persistent flat buffer (``param._bh_grad_slot``,
+  same strides as the parameter). A gradient that arrives elsewhere is copied into its slot by the
+  per-parameter hook -- as it arrives, overlapped with the rest of backward -- and ``param.grad``
+  becomes the slot view; the all-reduce runs on the flat buffer in place, and nothing is copied
+  back. A backward that writes its weight gradient straight into the slot (the MFMA conv wgrad
+  kernels do, models/resnet.py) makes the hook a no-op.
 * device-agnostic: the same code runs on CPU tensors over gloo (the reference hard-codes CUDA).
 * a single-process world skips every collective.
 """
@@ -61,6 +66,16 @@ def _raw(t: torch.Tensor) -> torch.Tensor:
         except RuntimeError:
             pass
     raise RuntimeError("DistributedDataParallel: gradients must be dense (contiguous or channels_last)")
+
+
+def _fmt(t: torch.Tensor):
+    for fmt in (torch.channels_last, torch.channels_last_3d):
+        try:
+            if t.dim() >= 4 and t.is_contiguous(memory_format=fmt):
+                return fmt
+        except RuntimeError:
+            pass
+    return torch.contiguous_format
 
 
 def flatten(bucket):
@@ -161,8 +176,16 @@ def _supports_avg(pg) -> bool:
         return False
 
 
+def _slot_view(flat: torch.Tensor, off: int, p: torch.Tensor) -> torch.Tensor:
+    """View of ``flat[off:off+numel]`` with ``p``'s shape and (dense) strides."""
+    n = p.numel()
+    if p.is_contiguous():
+        return flat[off:off + n].view(p.shape)
+    return flat[off:off + n].as_strided(p.size(), p.stride())
+
+
 class _Bucket:
-    __slots__ = ("params", "numel", "dtype", "flat", "work", "launched", "ready", "outputs")
+    __slots__ = ("params", "numel", "dtype", "flat", "work", "launched", "ready", "outputs", "slots")
 
     def __init__(self, params, dtype):
         self.params = params  # list of param indices
@@ -173,6 +196,7 @@ class _Bucket:
         self.launched = False
         self.ready = 0
         self.outputs = None
+        self.slots = None  # per-parameter views of flat
 
 
 class DistributedDataParallel(Module):
@@ -262,6 +286,9 @@ class DistributedDataParallel(Module):
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        for p in getattr(self, "active_params", []):
+            if hasattr(p, "_bh_grad_slot"):
+                del p._bh_grad_slot
         self.active_params = [p for p in self.module.parameters() if p.requires_grad]
         self._param_ids = [id(p) for p in self.active_params]
         self.needs_refresh = True
@@ -329,6 +356,7 @@ class DistributedDataParallel(Module):
                 b_idx = self._param_to_bucket.get(idx)
                 if b_idx is not None:
                     b = self._buckets[b_idx]
+                    self._to_slot(b, idx)
                     b.ready += 1
                     if b.ready == len(b.params):
                         self._launch_ready_in_order()
@@ -405,27 +433,46 @@ class DistributedDataParallel(Module):
             out.append(b)
         return out
 
+    def _alloc_slots(self, b: _Bucket):
+        """Persistent flat buffer of a bucket and one slot view per parameter (gradient-as-bucket-view)."""
+        p0 = self.active_params[b.params[0]]
+        if b.flat is None or b.flat.numel() != b.numel or b.flat.device != p0.device or b.flat.dtype != p0.dtype:
+            b.flat = torch.empty(b.numel, dtype=p0.dtype, device=p0.device)
+        b.slots, off = {}, 0
+        for i in b.params:
+            p = self.active_params[i]
+            b.slots[i] = _slot_view(b.flat, off, p)
+            p._bh_grad_slot = b.slots[i]
+            off += p.numel()
+
+    def _to_slot(self, b: _Bucket, i: int):
+        """Make ``param.grad`` the bucket slot view, copying the gradient in unless it is already there."""
+        if b.slots is None:
+            self._alloc_slots(b)
+        p, slot = self.active_params[i], b.slots[i]
+        g = p.grad
+        if g is None:
+            slot.zero_()
+        elif g.data_ptr() != slot.data_ptr() or g.stride() != slot.stride():
+            _raw(slot).copy_(_raw(g if g.stride() == slot.stride() else g.contiguous(memory_format=_fmt(slot))))
+        else:
+            return
+        p.grad = slot
+
     def _launch(self, b_idx):
         b = self._buckets[b_idx]
         if b.launched:
             return
-        grads = []
-        for i in b.params:
-            p = self.active_params[i]
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
-            grads.append(p.grad)
-        views = [_raw(g) for g in grads]
-        if self.retain_allreduce_buffers or b.flat is None or b.flat.device != views[0].device \
-                or b.flat.numel() != b.numel or b.flat.dtype != views[0].dtype:
-            b.flat = torch.empty(b.numel, dtype=views[0].dtype, device=views[0].device)
-        torch.cat(views, out=b.flat)
+        if b.slots is None:
+            self._alloc_slots(b)
+        for i in b.params:  # parameters the hooks have not placed yet (first / delayed / unused)
+            self._to_slot(b, i)
         tensor = b.flat.float() if self.allreduce_always_fp32 and b.flat.dtype != torch.float32 else b.flat
         if self.gradient_predivide_factor != 1.0:
             tensor.mul_(1.0 / self.gradient_predivide_factor)
         op = dist.ReduceOp.AVG if self._use_avg else dist.ReduceOp.SUM
         b.work = dist.all_reduce(tensor, op=op, group=self._pg_for(b_idx), async_op=True)
-        b.outputs = (tensor, grads)
+        b.outputs = tensor
         b.launched = True
 
     def _finish(self, b_idx):
@@ -434,27 +481,13 @@ class DistributedDataParallel(Module):
             with comm_stats.timed("ddp_wait", b.flat):
                 b.work.wait()
             b.work = None
-        tensor, grads = b.outputs
+        tensor = b.outputs
         if self.gradient_average and not self._use_avg:
             tensor.mul_(self.gradient_predivide_factor / self.world_size)
         if tensor is not b.flat:
             b.flat.copy_(tensor)
         if self.retain_allreduce_buffers:
             self.allreduce_buffers[b_idx] = b.flat
-            off = 0
-            for i, g in zip(b.params, grads):
-                p = self.active_params[i]
-                n = g.numel()
-                p.grad = b.flat[off:off + n].view_as(g) if g.is_contiguous() else \
-                    b.flat[off:off + n].as_strided(g.size(), g.stride())
-                off += n
-        else:
-            outs, off = [], 0
-            for g in grads:
-                n = g.numel()
-                outs.append(b.flat[off:off + n])
-                off += n
-            torch._foreach_copy_([_raw(g) for g in grads], outs)
         b.outputs = None
 
     def _end_of_backward(self):

@@ -19,6 +19,7 @@ import torch.distributed as dist
 from torch.nn import functional as F
 from torch.nn.modules.batchnorm import _BatchNorm
 
+from ..ops import conv_bn as conv_bn_ops
 from ..ops import syncbn
 from . import comm_stats
 
@@ -117,6 +118,82 @@ class SyncBatchnormFunction(torch.autograd.Function):
             None, None, None, None
 
 
+class BNLink(object):
+    """One BatchNorm -> convolution boundary of the conv-folded ResNet path (models/resnet.py).
+
+    The BatchNorm's forward records its raw input ``y`` and per-channel ``scale / shift / mean``; the
+    consuming convolution's backward reads them to reduce the BatchNorm's backward sums inside its
+    data-gradient epilogue and leaves them in ``sums`` (``[sum_dz, sum_dz*(y-mean)]``, local to this
+    rank); the BatchNorm's backward then skips its own reduction pass over ``dA`` and ``y``."""
+
+    __slots__ = ("y", "scale", "shift", "mean", "relu", "sums")
+
+    def __init__(self):
+        self.y = self.scale = self.shift = self.mean = self.sums = None
+        self.relu = True
+
+
+class SyncBatchnormFromStats(torch.autograd.Function):
+    """Training-mode SyncBatchNorm whose local statistics arrive as the producing convolution's
+    epilogue partials (``part [2, G, C]``: sums of ``x - running_mean`` and its square, see
+    ops/conv_bn.py) instead of a statistics pass over ``input``: partials -> ``[2C+1]`` sums -> (one
+    all-reduce across ranks) -> merge / running-stat update -> the fused normalise (+z)(ReLU) pass.
+    With ``link``, the backward reduction may already have been done by the consuming convolution."""
+
+    @staticmethod
+    def forward(ctx, input, part, z, weight, bias, running_mean, running_var, eps, momentum, process_group,
+                fuse_relu, num_batches, link):
+        world = _world(process_group)
+        C = input.size(1)
+        count = float(input.numel() // C)
+        sums = conv_bn_ops.sum_parts(part, count)
+        if world > 1:
+            with comm_stats.timed("syncbn_fwd", sums):
+                _all_reduce(sums, process_group)
+        mean, invstd, scale, shift, count_t = syncbn.merge_sums(sums, weight, bias, running_mean, running_var,
+                                                                momentum, eps, num_batches)
+        mask = None
+        if fuse_relu and syncbn.mask_ok(input, z):
+            out, mask = syncbn.forward_mask(input, z, scale, shift, num_batches)
+        else:
+            out = syncbn.forward(input, z, scale, shift, fuse_relu, None, num_batches)
+        if link is not None:
+            link.y, link.scale, link.shift, link.mean, link.relu = input, scale, shift, mean, fuse_relu
+            link.sums = None
+        ctx.save_for_backward(input, None if mask is not None else z, weight, mean, invstd, scale, shift, count_t, mask)
+        ctx.process_group = process_group
+        ctx.world = world
+        ctx.fuse_relu = fuse_relu
+        ctx.has_z = z is not None
+        ctx.link = link
+        ctx.mark_non_differentiable(part)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        input, z, weight, mean, invstd, scale, shift, count, mask = ctx.saved_tensors
+        link = ctx.link
+        need_w = weight is not None and (ctx.needs_input_grad[3] or ctx.needs_input_grad[4])
+        if link is not None and link.sums is not None:
+            sums = link.sums  # reduced by the consuming convolution's data-gradient epilogue
+            link.sums = None
+            C = input.size(1)
+            gw = (sums[C:] * invstd).to(weight.dtype) if need_w else None
+            gb = sums[:C].to(weight.dtype) if need_w else None
+        else:
+            sums, gw, gb = syncbn.backward_reduce(grad_output, input, z, mean, invstd, scale, shift, ctx.fuse_relu,
+                                                  weight, need_w, mask)
+        if link is not None:
+            link.y = None  # release the saved activation reference
+        if ctx.world > 1:
+            with comm_stats.timed("syncbn_bwd", sums):
+                _all_reduce(sums, ctx.process_group)
+        grad_input, grad_z = syncbn.backward_dgrad(grad_output, input, z, mean, invstd, weight, sums, count, scale,
+                                                   shift, ctx.fuse_relu, ctx.has_z and ctx.needs_input_grad[2], mask)
+        return grad_input, None, grad_z, (gw if need_w else None), (gb if need_w else None), None, None, None, None, \
+            None, None, None, None
+
+
 class SyncBatchNorm(_BatchNorm):
     """Synchronized batch norm over ``process_group`` (default: WORLD).
 
@@ -156,6 +233,14 @@ class SyncBatchNorm(_BatchNorm):
         if self.fuse_maxpool is not None and not self._pool_ok(input, z):
             return F.max_pool2d(self._bn(input, z, None), *self.fuse_maxpool)
         return self._bn(input, z, self.fuse_maxpool)
+
+    def forward_from_stats(self, input, part, z=None, link=None):
+        """Training forward from the producing convolution's statistics partials (see
+        :class:`SyncBatchnormFromStats`); ``part`` must be centred on ``self.running_mean``."""
+        exp_avg = self.momentum if self.momentum is not None else -1.0
+        return SyncBatchnormFromStats.apply(input, part, z, self.weight, self.bias, self.running_mean, self.running_var,
+                                            self.eps, exp_avg, self.process_group, self.fuse_relu,
+                                            self.num_batches_tracked, link)
 
     def _bn(self, input, z, pool):
         if not self.training and self.track_running_stats:

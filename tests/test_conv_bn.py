@@ -1,0 +1,227 @@
+"""1x1 convolution GEMMs with BatchNorm prologue / epilogues (kernels/conv_bn.hip) against fp32 PyTorch.
+
+Shapes are the ResNet-50 bottleneck's 1x1 layers (channels) on small pixel counts. Each GPU case
+compares the HIP kernel with the fp32 reference of ``ops.conv_bn`` (``F.linear`` on the fp32 upcast,
+BatchNorm prologue applied in fp32 and rounded like the kernel): the output to fp16 / bf16 rounding,
+the statistics partial sums to fp32 summation-order tolerance.
+"""
+import pytest
+import torch
+
+from beforeholiday_amd.ops import conv_bn
+
+SHAPES = [  # (K, N): forward and data-gradient directions of the bottleneck 1x1 convs
+    (64, 64), (64, 256), (256, 64), (128, 512), (512, 128), (256, 1024), (1024, 256), (512, 2048), (128, 128),
+]
+
+
+def _tol(dt):
+    return dict(rtol=2e-2, atol=2e-2) if dt == torch.bfloat16 else dict(rtol=5e-3, atol=5e-3)
+
+
+def _data(M, K, N, dt, dev, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    a = (torch.randn(M, K, generator=g)).to(dt).to(dev)
+    b = (torch.randn(N, K, generator=g) / K ** 0.5).to(dt).to(dev)
+    return a, b
+
+
+def _stats_close(got, ref, rows):
+    # partial sums over rows: fp32 accumulation in different orders
+    torch.testing.assert_close(got.float().cpu(), ref.float().cpu(), rtol=2e-3, atol=2e-3 * rows ** 0.5)
+
+
+def test_reference_cpu_matches_definition():
+    a, b = _data(64, 64, 64, torch.float32, "cpu")
+    sc, sh = torch.rand(64) + 0.5, torch.randn(64)
+    c, part = conv_bn.c1x1(a, b, sc, sh, epi="stats")
+    ref = torch.relu(a * sc + sh) @ b.t()
+    torch.testing.assert_close(c, ref, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(conv_bn.sum_parts(part, 64)[:64], ref.sum(0), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("KN", SHAPES)
+def test_c1x1_plain_and_stats(KN, dt):
+    K, N = KN
+    M = 2048
+    a, b = _data(M, K, N, dt, "cuda")
+    assert conv_bn.supported(a, b, epi="stats")
+    kshift = torch.randn(N, device="cuda") * 0.1
+    c, part = conv_bn.c1x1(a, b, epi="stats", kshift=kshift)
+    rc, rpart = conv_bn.c1x1(a.cpu(), b.cpu(), epi="stats", kshift=kshift.cpu())
+    torch.testing.assert_close(c.float().cpu(), rc.float(), **_tol(dt))
+    # statistics of the stored output: compare against the reference statistics of OUR output
+    cf = c.float().cpu() - kshift.cpu()
+    _stats_close(conv_bn.sum_parts(part, M)[:2 * N], torch.cat([cf.sum(0), (cf * cf).sum(0)]), M)
+    assert float(conv_bn.sum_parts(part, M)[-1]) == M
+    c2, p2 = conv_bn.c1x1(a, b)
+    torch.testing.assert_close(c2, c, rtol=0, atol=0)
+    assert p2.numel() == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("KN", [(64, 256), (128, 512), (256, 1024), (512, 2048), (64, 64)])
+def test_c1x1_bn_prologue(KN, dt):
+    """conv3 of the bottleneck: input = relu(BN2(y2)) applied on the fly."""
+    K, N = KN
+    M = 1024
+    a, b = _data(M, K, N, dt, "cuda", seed=1)
+    sc = (torch.rand(K) + 0.5).cuda()
+    sh = torch.randn(K).cuda() * 0.5
+    c, part = conv_bn.c1x1(a, b, sc, sh, epi="stats")
+    rc, _ = conv_bn.c1x1(a.cpu(), b.cpu(), sc.cpu(), sh.cpu(), epi="stats")
+    torch.testing.assert_close(c.float().cpu(), rc.float(), **_tol(dt))
+    cf = c.float().cpu()
+    _stats_close(conv_bn.sum_parts(part)[:N], cf.sum(0), M)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("KNHW", [(64, 256, 8, 8), (256, 512, 12, 8), (512, 1024, 4, 16)])
+def test_c1x1_stride2_gather(KNHW, dt):
+    K, N, H, W = KNHW
+    n = 4
+    a, b = _data(n * H * W, K, N, dt, "cuda", seed=2)
+    assert conv_bn.supported(a, b, s2=(H, W), epi="stats")
+    c, part = conv_bn.c1x1(a, b, s2=(H, W), epi="stats")
+    ref = torch.nn.functional.conv2d(a.float().cpu().view(n, H, W, K).permute(0, 3, 1, 2),
+                                     b.float().cpu().view(N, K, 1, 1), stride=2)
+    ref = ref.permute(0, 2, 3, 1).reshape(-1, N)
+    torch.testing.assert_close(c.float().cpu(), ref, **_tol(dt))
+    _stats_close(conv_bn.sum_parts(part)[:N], c.float().cpu().sum(0), ref.size(0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("KN", [(64, 256), (256, 64), (128, 512), (64, 64)])
+def test_c1x1_residual(KN, dt):
+    K, N = KN
+    M = 1024
+    a, b = _data(M, K, N, dt, "cuda", seed=3)
+    r = torch.randn(M, N, device="cuda").to(dt)
+    c, _ = conv_bn.c1x1(a, b, resid=r)
+    ref = (a.float() @ b.float().t() + r.float())
+    torch.testing.assert_close(c.float(), ref, **_tol(dt))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("KN", [(256, 64), (512, 128), (1024, 256), (64, 64), (128, 256)])
+@pytest.mark.parametrize("resid", [False, True])
+def test_c1x1_bn_backward_epilogue(KN, dt, resid):
+    """Data gradient dA = dY . W with the previous BatchNorm's backward sums in the epilogue:
+    sum(dz), sum(dz * (y - mean)), dz = dA * (y*scale + shift > 0) -- syncbn.backward_reduce."""
+    from beforeholiday_amd.ops import syncbn
+
+    K, N = KN
+    M = 1024
+    a, b = _data(M, K, N, dt, "cuda", seed=4)
+    y = (torch.randn(M, N) * 2 + 0.3).to(dt).cuda()
+    sc = (torch.rand(N) + 0.5).cuda()
+    sh = torch.randn(N).cuda() * 0.3
+    mean = torch.randn(N).cuda() * 0.1
+    r = torch.randn(M, N, device="cuda").to(dt) if resid else None
+    if not conv_bn.supported(a, b, resid=resid, epi="bwd"):
+        pytest.skip("shape outside the backward-epilogue kernel")
+    c, part = conv_bn.c1x1(a, b, resid=r, epi="bwd", by=y, bscale=sc, bshift=sh, bmean=mean)
+    ref = a.float() @ b.float().t() + (r.float() if resid else 0)
+    torch.testing.assert_close(c.float(), ref, **_tol(dt))
+    # the sums must equal syncbn.backward_reduce of (dA as stored, y) -- the unfused path
+    x4 = y.view(1, 1, M, N).permute(0, 3, 1, 2)
+    dy4 = c.view(1, 1, M, N).permute(0, 3, 1, 2)
+    sums, _, _ = syncbn.backward_reduce(dy4.cpu().float(), x4.cpu().float(), None, mean.cpu(), None, sc.cpu(),
+                                        sh.cpu(), True, None, False)
+    _stats_close(conv_bn.sum_parts(part), sums, M)
+
+
+@pytest.mark.gpu
+def test_c1x1_rejects_unsupported():
+    a = torch.randn(100, 64, device="cuda", dtype=torch.float16)  # M % 32 != 0
+    b = torch.randn(64, 64, device="cuda", dtype=torch.float16)
+    assert not conv_bn.supported(a, b)
+    with pytest.raises(RuntimeError):
+        conv_bn.c1x1(a, b)
+
+
+# ---------------------------------------------------------------- 3x3 kernel with BatchNorm folding
+def _conv3x3_ref(x, w, sc=None, sh=None):
+    xf = x.float()
+    if sc is not None:
+        xf = torch.relu(xf * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1)).to(x.dtype).float()
+    return torch.nn.functional.conv2d(xf, w.float(), padding=1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(4, 64, 56, 56), (4, 128, 28, 28), (8, 256, 14, 14), (8, 512, 7, 7), (3, 64, 9, 13)])
+@pytest.mark.parametrize("pro", [False, True])
+def test_conv3x3_bn_forward(shape, dt, pro):
+    from beforeholiday_amd._native import submodule
+
+    n, c, h, w_ = shape
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(n, c, h, w_, generator=g).to(dt).cuda().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(c, c, 3, 3, generator=g) / (9 * c) ** 0.5).to(dt).cuda().contiguous(memory_format=torch.channels_last)
+    sc = (torch.rand(c, generator=g) + 0.5).cuda() if pro else None
+    sh = (torch.randn(c, generator=g) * 0.5).cuda() if pro else None
+    kshift = torch.randn(c, generator=g).cuda() * 0.1
+    y, part = submodule("conv_cuda").conv3x3_bn_forward(x, w, sc, sh, True, kshift)
+    ref = _conv3x3_ref(x, w, sc, sh)
+    torch.testing.assert_close(y.float(), ref, **_tol(dt))
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, c).cpu() - kshift.cpu()
+    _stats_close(conv_bn.sum_parts(part)[:2 * c], torch.cat([yf.sum(0), (yf * yf).sum(0)]), yf.size(0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(4, 64, 56, 56), (8, 256, 14, 14), (8, 512, 7, 7)])
+def test_conv3x3_bn_dgrad_epilogue(shape, dt):
+    from beforeholiday_amd._native import submodule
+    from beforeholiday_amd.ops import syncbn
+
+    n, c, h, w_ = shape
+    g = torch.Generator().manual_seed(6)
+    dy = torch.randn(n, c, h, w_, generator=g).to(dt).cuda().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(c, c, 3, 3, generator=g) / (9 * c) ** 0.5).to(dt).cuda().contiguous(memory_format=torch.channels_last)
+    y1 = (torch.randn(n, c, h, w_, generator=g) * 2 + 0.2).to(dt).cuda().contiguous(memory_format=torch.channels_last)
+    sc, sh = (torch.rand(c, generator=g) + 0.5).cuda(), (torch.randn(c, generator=g) * 0.3).cuda()
+    mean = (torch.randn(c, generator=g) * 0.1).cuda()
+    dx, part = submodule("conv_cuda").conv3x3_bn_dgrad(dy, w, y1, sc, sh, mean, True)
+    ref = torch.nn.grad.conv2d_input(dy.shape, w.float(), dy.float(), padding=1)
+    torch.testing.assert_close(dx.float(), ref, **_tol(dt))
+    sums, _, _ = syncbn.backward_reduce(dx.float().cpu(), y1.float().cpu(), None, mean.cpu(), None, sc.cpu(),
+                                        sh.cpu(), True, None, False)
+    _stats_close(conv_bn.sum_parts(part), sums, n * h * w_)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("KN", [(512, 128), (1024, 256), (256, 1024), (512, 2048), (128, 512)])
+@pytest.mark.parametrize("epi", ["stats", "bwd"])
+def test_gemm_bn_epilogues(KN, dt, epi):
+    """Tiled MFMA GEMM (kernels/gemm.hip) with the BatchNorm statistics / backward-sum epilogues."""
+    from beforeholiday_amd.ops import syncbn
+
+    K, N = KN
+    M = 1000  # not a multiple of the tile: the last slab is partial
+    a, b = _data(M, K, N, dt, "cuda", seed=7)
+    kshift = torch.randn(N, device="cuda") * 0.1
+    y = (torch.randn(M, N) * 2 + 0.3).to(dt).cuda()
+    sc, sh = (torch.rand(N) + 0.5).cuda(), torch.randn(N).cuda() * 0.3
+    mean = torch.randn(N).cuda() * 0.1
+    if epi == "stats":
+        c, part = conv_bn.gemm_bn(a, b, "stats", kshift=kshift)
+    else:
+        c, part = conv_bn.gemm_bn(a, b, "bwd", by=y, bscale=sc, bshift=sh, bmean=mean)
+    torch.testing.assert_close(c.float(), a.float() @ b.float().t(), **_tol(dt))
+    cf = c.float().cpu()
+    if epi == "stats":
+        d = cf - kshift.cpu()
+        ref = torch.cat([d.sum(0), (d * d).sum(0)])
+    else:
+        ref, _, _ = syncbn.backward_reduce(cf.t().reshape(1, N, M, 1), y.float().cpu().t().reshape(1, N, M, 1), None,
+                                           mean.cpu(), None, sc.cpu(), sh.cpu(), True, None, False)
+    _stats_close(conv_bn.sum_parts(part), ref, M)

@@ -165,3 +165,32 @@ def _amp_master_params(rank, world, opt_level):
 @pytest.mark.parametrize("opt_level", ["O2", "O5"])
 def test_amp_master_params_ddp_gloo(opt_level):
     run_distributed(_amp_master_params, 2, opt_level)
+
+
+def _bucket_view(rank, world):
+    """Gradient-as-bucket-view: after the first backward every gradient IS a view of its bucket's flat
+    buffer (no gather copy before, no scatter copy after the all-reduce), and stays correct."""
+    torch.manual_seed(100 + rank)
+    model = MLP()
+    ddp = DDP(model, message_size=1000)
+    for it in range(3):
+        torch.manual_seed(it)
+        x = torch.randn(8 * world, 32)
+        xs = x[rank * 8:(rank + 1) * 8]
+        ddp.zero_grad(set_to_none=True)
+        ddp(xs).square().sum().backward()
+        flats = {id(b): b.flat for b in ddp._buckets}
+        for p in model.parameters():
+            assert hasattr(p, "_bh_grad_slot") and p.grad.data_ptr() == p._bh_grad_slot.data_ptr()
+            assert any(f.data_ptr() <= p.grad.data_ptr() < f.data_ptr() + f.numel() * f.element_size()
+                       for f in flats.values())
+        # all ranks hold the same (averaged) gradient
+        g = torch.cat([p.grad.reshape(-1) for p in model.parameters()])
+        gs = [torch.empty_like(g) for _ in range(world)]
+        dist.all_gather(gs, g)
+        for other in gs:
+            torch.testing.assert_close(other, g)
+
+
+def test_ddp_gradient_as_bucket_view():
+    run_distributed(_bucket_view, 2)

@@ -1,0 +1,89 @@
+"""Bottleneck blocks with the BatchNorms folded into the convolutions (models/resnet.py
+``_forward_folded``: statistics from the conv epilogues, backward sums from the data-gradient
+epilogues) against a plain fp32 PyTorch Bottleneck (nn.Conv2d + nn.BatchNorm2d) with the same
+weights: output, input gradient, every parameter gradient, running statistics. A single block is
+well conditioned, so fp16 / bf16 rounding stays at the 1e-2 level (a whole fp16 network at batch 8 on
+64x64 images amplifies rounding through 16 BatchNorm backwards to ~30% in either implementation)."""
+import pytest
+import torch
+
+
+def _rel(a, b):
+    a, b = a.detach().float(), b.detach().float()
+    return float((a - b).norm() / b.norm().clamp_min(1e-12))
+
+
+def _block(inplanes, planes, stride, dt):
+    from beforeholiday_amd.models import resnet as R
+    from beforeholiday_amd.parallel import SyncBatchNorm
+
+    torch.manual_seed(0)
+    ds_ref = ds = None
+    if stride != 1 or inplanes != planes * 4:
+        ds_ref = torch.nn.Sequential(torch.nn.Conv2d(inplanes, planes * 4, 1, stride=stride, bias=False),
+                                     torch.nn.BatchNorm2d(planes * 4))
+    ref = R.Bottleneck(inplanes, planes, stride, ds_ref).cuda()
+
+    def norm(c, fuse_relu=False):
+        return SyncBatchNorm(c, channel_last=True, fuse_relu=fuse_relu)
+
+    if ds_ref is not None:
+        ds = torch.nn.Sequential(torch.nn.Conv2d(inplanes, planes * 4, 1, stride=stride, bias=False), norm(planes * 4))
+    blk = R.Bottleneck(inplanes, planes, stride, ds, norm_layer=norm, fused=True).cuda()
+    blk.load_state_dict(ref.state_dict())
+    blk = blk.to(memory_format=torch.channels_last).to(dt)
+    for m in blk.modules():
+        if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+            m.float()
+    return R, ref, blk
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("cfg", [(256, 64, 1, 56), (64, 64, 1, 56), (256, 128, 2, 56), (512, 128, 1, 28),
+                                 (1024, 256, 1, 14)])
+def test_folded_bottleneck_matches_fp32(cfg, dt):
+    inplanes, planes, stride, hw = cfg
+    R, ref, blk = _block(inplanes, planes, stride, dt)
+    x = torch.randn(8, inplanes, hw, hw, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+    assert blk._fold_ok(x)
+    xr = x.float().clone().requires_grad_()
+    xf = x.clone().requires_grad_()
+    out_r, out_f = ref(xr), blk(xf)
+    tol = 1e-2 if dt == torch.float16 else 4e-2
+    assert _rel(out_f, out_r) < tol
+    g = torch.randn_like(out_r)
+    out_r.backward(g)
+    out_f.backward(g.to(dt))
+    assert _rel(xf.grad, xr.grad) < 2 * tol
+    for (n, p), q in zip(blk.named_parameters(), ref.parameters()):
+        assert _rel(p.grad, q.grad) < 2 * tol, n
+    for (n, b), q in zip(blk.named_buffers(), ref.buffers()):
+        if "running" in n:
+            assert _rel(b, q) < tol, n
+        elif "num_batches" in n:
+            assert int(b) == int(q), n
+
+
+@pytest.mark.gpu
+def test_folded_and_unfolded_paths_agree():
+    """Same fp16 block through the folded and the unfolded fused paths: identical math up to rounding."""
+    R, _, blk = _block(256, 64, 1, torch.float16)
+    x = torch.randn(8, 256, 56, 56, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    old = R._FOLD_BN
+    try:
+        outs = []
+        for fold in (True, False):
+            R._FOLD_BN = fold
+            xx = x.clone().requires_grad_()
+            o = blk(xx)
+            o.float().square().sum().backward()
+            outs.append((o.detach(), xx.grad, [p.grad.clone() for p in blk.parameters()]))
+            for p in blk.parameters():
+                p.grad = None
+    finally:
+        R._FOLD_BN = old
+    assert _rel(outs[0][0], outs[1][0]) < 5e-3
+    assert _rel(outs[0][1], outs[1][1]) < 2e-2
+    for a, b in zip(outs[0][2], outs[1][2]):
+        assert _rel(a, b) < 2e-2
