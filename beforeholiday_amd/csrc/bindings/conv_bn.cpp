@@ -69,10 +69,28 @@ std::vector<at::Tensor> c1x1(const at::Tensor& a, const at::Tensor& b, bool b_tr
                              const c10::optional<at::Tensor>& resid, int64_t s2_h, int64_t s2_w, int64_t epi,
                              const c10::optional<at::Tensor>& kshift, const c10::optional<at::Tensor>& by,
                              const c10::optional<at::Tensor>& bscale, const c10::optional<at::Tensor>& bshift,
-                             const c10::optional<at::Tensor>& bmean, bool brelu) {
-  bh::C1x1Args p = make_args(a, b, b_trans, M, pro_scale, pro_shift, resid, s2_h, s2_w, epi, kshift, by, bscale, bshift, bmean,
+                             const c10::optional<at::Tensor>& bmean, bool brelu, bool s2_scatter) {
+  at::Tensor c;
+  if (s2_scatter) {
+    // accumulate into the full-resolution tensor `resid` in place: a is [M, K], resid [4M, N]
+    TORCH_CHECK(s2_h > 0 && resid.has_value() && resid->defined() && resid->is_cuda() &&
+                    resid->device() == a.device() && resid->scalar_type() == a.scalar_type() &&
+                    resid->is_contiguous() && resid->dim() == 2 && resid->size(0) == 4 * M &&
+                    a.size(0) == M,
+                "conv_bn.c1x1: the stride-2 scatter accumulates into a contiguous [4M, N] resid");
+    c = *resid;
+  }
+  bh::C1x1Args p = make_args(a, b, b_trans, M, pro_scale, pro_shift, s2_scatter ? c10::optional<at::Tensor>() : resid,
+                             s2_scatter ? 0 : s2_h, s2_scatter ? 0 : s2_w, epi, kshift, by, bscale, bshift, bmean,
                              brelu);
-  auto c = at::empty({M, (int64_t)p.N}, a.options());
+  if (s2_scatter) {
+    p.s2_H = (int)s2_h;
+    p.s2_W = (int)s2_w;
+    p.s2_scatter = true;
+    p.R = c.data_ptr();
+  } else {
+    c = at::empty({M, (int64_t)p.N}, a.options());
+  }
   p.C = c.data_ptr();
   at::Tensor part;
   if (epi != bh::kC1x1Plain) {
@@ -90,7 +108,7 @@ std::vector<at::Tensor> c1x1(const at::Tensor& a, const at::Tensor& b, bool b_tr
 }
 
 bool c1x1_supported(const at::Tensor& a, const at::Tensor& b, bool b_trans, int64_t M, bool pro, bool resid,
-                    int64_t s2_h, int64_t s2_w, int64_t epi) {
+                    int64_t s2_h, int64_t s2_w, int64_t epi, bool s2_scatter) {
   if (!(a.is_cuda() && b.is_cuda() && a.dim() == 2 && b.dim() == 2 && a.is_contiguous() && b.is_contiguous() &&
         a.scalar_type() == b.scalar_type() && a.size(1) == b.size(b_trans ? 0 : 1) &&
         (a.scalar_type() == at::kHalf || a.scalar_type() == at::kBFloat16)))
@@ -107,6 +125,8 @@ bool c1x1_supported(const at::Tensor& a, const at::Tensor& b, bool b_trans, int6
   p.pro_scale = pro ? dummy : nullptr;
   p.pro_shift = pro ? dummy : nullptr;
   p.R = resid ? a.data_ptr() : nullptr;
+  if (s2_scatter) p.R = p.C;
+  p.s2_scatter = s2_scatter;
   p.s2_H = (int)s2_h;
   p.s2_W = (int)s2_w;
   p.epi = (int)epi;
@@ -177,9 +197,11 @@ void register_conv_bn(pybind11::module_& root) {
   m.def("c1x1", &c1x1, py::arg("a"), py::arg("b"), py::arg("b_trans"), py::arg("M"), py::arg("pro_scale") = py::none(),
         py::arg("pro_shift") = py::none(), py::arg("resid") = py::none(), py::arg("s2_h") = 0, py::arg("s2_w") = 0,
         py::arg("epi") = 0, py::arg("kshift") = py::none(), py::arg("by") = py::none(), py::arg("bscale") = py::none(),
-        py::arg("bshift") = py::none(), py::arg("bmean") = py::none(), py::arg("brelu") = true);
+        py::arg("bshift") = py::none(), py::arg("bmean") = py::none(), py::arg("brelu") = true,
+        py::arg("s2_scatter") = false);
   m.def("c1x1_supported", &c1x1_supported, py::arg("a"), py::arg("b"), py::arg("b_trans"), py::arg("M"), py::arg("pro") = false,
-        py::arg("resid") = false, py::arg("s2_h") = 0, py::arg("s2_w") = 0, py::arg("epi") = 0);
+        py::arg("resid") = false, py::arg("s2_h") = 0, py::arg("s2_w") = 0, py::arg("epi") = 0,
+        py::arg("s2_scatter") = false);
   m.def("sum_parts", &sum_parts, py::arg("part"), py::arg("count") = -1.0);
   m.def("gemm_bn", &gemm_bn, py::arg("a"), py::arg("b"), py::arg("epi"), py::arg("kshift") = py::none(),
         py::arg("by") = py::none(), py::arg("bscale") = py::none(), py::arg("bshift") = py::none(),

@@ -34,6 +34,10 @@ struct C1x1Args {
   const float* pro_scale = nullptr;  // [K] prologue BatchNorm (with ReLU)
   const float* pro_shift = nullptr;
   int s2_H = 0, s2_W = 0;  // > 0: stride-2 gather from an [.., s2_H, s2_W, K] input; output is [.., s2_H/2, s2_W/2, N]
+  // with s2_H > 0: scatter instead -- row (n, y, x) of the [M, N] result is ADDED into row (n, 2y, 2x) of
+  // the full-resolution C [.., s2_H, s2_W, N] (R must equal C): the data gradient of a 1x1 / stride-2
+  // convolution accumulated onto the other branch's gradient of the same input
+  bool s2_scatter = false;
   int epi = kC1x1Plain;
   float* part = nullptr;            // [2][G][N] fp32 partials (kStats / kBwd)
   const float* kshift = nullptr;    // kStats centre per column (may be null = 0)

@@ -58,7 +58,9 @@ struct Geo {
   int red_off;  // LDS byte offset of the cross-wave reduction buffer
 };
 
-template <typename T, int KC, int NC, int EPI, bool PRO, bool S2, bool RES>
+// S2: 0 none, 1 stride-2 gather of the A rows, 2 stride-2 scatter of the C rows (output row (n, y, x)
+// of the quarter-resolution problem lands in row (n, 2y, 2x) of the full-resolution C)
+template <typename T, int KC, int NC, int EPI, bool PRO, int S2, bool RES>
 __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = NC / 32;  // 32-column tiles per wave
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
   const T* __restrict__ Yp = reinterpret_cast<const T*>(p.by);
   auto arow = [&](int sp) -> int64_t {
     const int64_t m = (int64_t)sp * 32 + r;
-    if constexpr (S2) {
+    if constexpr (S2 == 1) {
       const int Wo = p.s2_W >> 1, HWo = (p.s2_H >> 1) * Wo;
       const int64_t n = m / HWo;
       const int rem = (int)(m - n * HWo), yo = rem / Wo, xo = rem - yo * Wo;
@@ -190,6 +192,20 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
     if (c + 1 < nch) return;
     // ---- epilogue ----
     const int64_t row0 = (int64_t)strip * 32 + 4 * h;
+    // output rows of this lane (the scatter maps them once per strip, shared by every column tile)
+    int64_t orow[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int64_t m = row0 + 8 * (v >> 2) + (v & 3);
+      if constexpr (S2 == 2) {
+        const int Wo = p.s2_W >> 1, HWo = (p.s2_H >> 1) * Wo;
+        const int64_t n = m / HWo;
+        const int rem = (int)(m - n * HWo), yo = rem / Wo, xo = rem - yo * Wo;
+        orow[v] = (n * p.s2_H + 2 * yo) * p.s2_W + 2 * xo;
+      } else {
+        orow[v] = m;
+      }
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int col = col0 + 32 * t + r;
@@ -199,7 +215,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) xr[4 * j + i] = to_f<T>(src[(row0 + 8 * j + i) * N + col]);
+          for (int i = 0; i < 4; ++i) xr[4 * j + i] = to_f<T>(src[orow[4 * j + i] * N + col]);
       }
       float bsc = 0.f, bsh = 0.f, bmn = 0.f;
       if constexpr (EPI == kC1x1Bwd) {
@@ -212,7 +228,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) yv[4 * j + i] = to_f<T>(Yp[(row0 + 8 * j + i) * N + col]);
+          for (int i = 0; i < 4; ++i) yv[4 * j + i] = to_f<T>(Yp[orow[4 * j + i] * N + col]);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -222,7 +238,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
           float x = acc[t][v];
           if constexpr (RES) x += xr[v];
           const T o = from_f<T>(x);
-          Cp[(row0 + 8 * j + i) * N + col] = o;
+          Cp[orow[v] * N + col] = o;
           const float f = to_f<T>(o);  // statistics of the value as stored
           if constexpr (EPI == kC1x1Stats) {
             const float d = f - e0[t];
@@ -362,7 +378,11 @@ bool c1x1_supported(const C1x1Args& a) {
   if (a.epi != kC1x1Plain && !a.part) return false;
   if (a.s2_H > 0) {
     if (a.s2_H % 2 || a.s2_W % 2 || a.M % ((int64_t)(a.s2_H / 2) * (a.s2_W / 2))) return false;
-    if (a.pro_scale || a.R || a.epi == kC1x1Bwd) return false;  // combinations not instantiated
+    if (a.pro_scale || a.epi == kC1x1Bwd) return false;  // combinations not instantiated
+    // gather: no residual; scatter: plain epilogue accumulating into the full-resolution C (R == C)
+    if (a.s2_scatter ? (a.epi != kC1x1Plain || a.R != a.C) : a.R != nullptr) return false;
+  } else if (a.s2_scatter) {
+    return false;
   }
   if (a.pro_scale && (a.R || a.epi != kC1x1Stats)) return false;
   return true;
@@ -388,20 +408,21 @@ void c1x1_run(int dt, const C1x1Args& a, hipStream_t st) {
       hipLaunchKernelGGL(kern, grid, block, pl.lds, st, a, pl.g);
     };
     if (a.epi == kC1x1Stats) {
-      if (pro) L(k_c1x1<T, KC, NC, kC1x1Stats, true, false, false>);
-      else if (s2) L(k_c1x1<T, KC, NC, kC1x1Stats, false, true, false>);
-      else L(k_c1x1<T, KC, NC, kC1x1Stats, false, false, false>);
+      if (pro) L(k_c1x1<T, KC, NC, kC1x1Stats, true, 0, false>);
+      else if (s2) L(k_c1x1<T, KC, NC, kC1x1Stats, false, 1, false>);
+      else L(k_c1x1<T, KC, NC, kC1x1Stats, false, 0, false>);
     } else if (a.epi == kC1x1Bwd) {
       if constexpr (NC <= 64) {
-        if (res) L(k_c1x1<T, KC, NC, kC1x1Bwd, false, false, true>);
+        if (res) L(k_c1x1<T, KC, NC, kC1x1Bwd, false, 0, true>);
       }
       if constexpr (NC <= 128) {
-        if (!res) L(k_c1x1<T, KC, NC, kC1x1Bwd, false, false, false>);
+        if (!res) L(k_c1x1<T, KC, NC, kC1x1Bwd, false, 0, false>);
       }
     } else {
-      if (s2) L(k_c1x1<T, KC, NC, kC1x1Plain, false, true, false>);
-      else if (res) L(k_c1x1<T, KC, NC, kC1x1Plain, false, false, true>);
-      else L(k_c1x1<T, KC, NC, kC1x1Plain, false, false, false>);
+      if (s2 && a.s2_scatter) L(k_c1x1<T, KC, NC, kC1x1Plain, false, 2, true>);
+      else if (s2) L(k_c1x1<T, KC, NC, kC1x1Plain, false, 1, false>);
+      else if (res) L(k_c1x1<T, KC, NC, kC1x1Plain, false, 0, true>);
+      else L(k_c1x1<T, KC, NC, kC1x1Plain, false, 0, false>);
     }
   };
   auto by_nc = [&](auto tt, auto kc) {

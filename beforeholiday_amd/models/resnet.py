@@ -472,23 +472,7 @@ class _Conv1x1BNFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, kshift, link_in, box, s2):
-        from ..ops import conv_bn
-
-        n, c, h, w = x.shape
-        k = weight.size(0)
-        a2d = x.permute(0, 2, 3, 1).reshape(-1, c)
-        w2d = weight.view(k, c)
-        ho, wo = (h // 2, w // 2) if s2 else (h, w)
-        hw = (h, w) if s2 else None
-        if conv_bn.preferred(c, k, n * ho * wo, s2) and conv_bn.supported(a2d, w2d, s2=hw, epi="stats"):
-            y2d, part = conv_bn.c1x1(a2d, w2d, s2=hw, epi="stats", kshift=kshift)
-            y = y2d.view(n, ho, wo, k).permute(0, 3, 1, 2)
-        else:  # hipBLASLt on the [pixels, channels] view (MIOpen for stride 2) + a statistics pass
-            if s2:
-                y = torch.nn.functional.conv2d(x, weight, stride=2)
-            else:
-                y = torch.mm(a2d, w2d.t()).view(n, h, w, k).permute(0, 3, 1, 2)
-            part = _part_from_tensor(y, kshift)
+        y, part = _c1x1_forward_stats(x, weight, kshift, s2)
         ctx.save_for_backward(x, weight)
         ctx.link_in, ctx.box, ctx.s2 = link_in, box, s2
         ctx.mark_non_differentiable(part)
@@ -547,9 +531,96 @@ class _Conv1x1BNFn(torch.autograd.Function):
                 if gw.stride() != weight.stride():
                     gw = gw.contiguous()
             else:
-                gw = _wgrad(x, gy, weight, 1, "auto", lambda: conv_bwd(gy, x, weight, None, *args,
+                # the MFMA wgrad kernel wins every ResNet-50 1x1 shape (profiles/conv_wgrad_vs_miopen.jsonl):
+                # no per-shape timing (it would JIT-compile MIOpen's solver on the first step)
+                gw = _wgrad(x, gy, weight, 1, "gemm", lambda: conv_bwd(gy, x, weight, None, *args,
                                                                        [False, True, False])[1])
         return gx, gw, None, None, None, None
+
+
+def _c1x1_forward_stats(x, weight, kshift, s2):
+    """Raw 1x1 conv output (channels_last) + its BatchNorm statistics partials: the strip kernel where
+    it wins, else hipBLASLt on the [pixels, channels] view (a gathered quarter of x for stride 2) +
+    a statistics pass. Never MIOpen (whose first call JIT-compiles its kernels)."""
+    from ..ops import conv_bn
+
+    n, c, h, w = x.shape
+    k = weight.size(0)
+    a2d = x.permute(0, 2, 3, 1).reshape(-1, c)
+    w2d = weight.view(k, c)
+    ho, wo = (h // 2, w // 2) if s2 else (h, w)
+    hw = (h, w) if s2 else None
+    if conv_bn.preferred(c, k, n * ho * wo, s2) and conv_bn.supported(a2d, w2d, s2=hw, epi="stats"):
+        y2d, part = conv_bn.c1x1(a2d, w2d, s2=hw, epi="stats", kshift=kshift)
+        return y2d.view(n, ho, wo, k).permute(0, 3, 1, 2), part
+    if s2:
+        a2d = x[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, c)
+    y = torch.mm(a2d, w2d.t()).view(n, ho, wo, k).permute(0, 3, 1, 2)
+    return y, _part_from_tensor(y, kshift)
+
+
+class _Conv1DsFn(torch.autograd.Function):
+    """The first 1x1 convolution of a bottleneck and its downsample 1x1 (stride 1 or 2), both reading
+    the block input x, as ONE autograd node: each emits the statistics partials of its BatchNorm, and
+    the backward produces dX = dY1 . W1 and then ADDS the downsample's data gradient into it in place
+    -- at the even pixels only for stride 2 (scatter-accumulate epilogue) -- instead of materialising a
+    zero-filled full-resolution gradient and summing the two branches (MIOpen's stride-2 backward-data
+    plus an add). Weight gradients on the MFMA wgrad kernels."""
+
+    @staticmethod
+    def forward(ctx, x, w1, wd, k1, kd, s2):
+        y1, p1 = _c1x1_forward_stats(x, w1, k1, False)
+        yd, pd = _c1x1_forward_stats(x, wd, kd, s2)
+        ctx.save_for_backward(x, w1, wd)
+        ctx.s2 = s2
+        ctx.mark_non_differentiable(p1, pd)
+        ctx.set_materialize_grads(False)
+        return y1, p1, yd, pd
+
+    @staticmethod
+    def backward(ctx, gy1, _g1, gyd, _gd):
+        from ..ops import conv as bhconv
+        from ..ops import conv_bn
+
+        x, w1, wd = ctx.saved_tensors
+        n, c, h, w = x.shape
+        k1, kd = w1.size(0), wd.size(0)
+        gy1 = gy1.contiguous(memory_format=torch.channels_last)
+        gyd = gyd.contiguous(memory_format=torch.channels_last)
+        g1 = gy1.permute(0, 2, 3, 1).reshape(-1, k1)
+        gd = gyd.permute(0, 2, 3, 1).reshape(-1, kd)
+        w1_2d, wd_2d = w1.view(k1, c), wd.view(kd, c)
+        gx = gw1 = gwd = None
+        if ctx.needs_input_grad[0]:
+            if conv_bn.preferred(k1, c, g1.size(0)) and conv_bn.supported(g1, w1_2d, b_trans=True):
+                gx2d, _ = conv_bn.c1x1(g1, w1_2d, b_trans=True)
+            else:
+                gx2d = torch.mm(g1, w1_2d)
+            if ctx.s2:
+                if conv_bn.supported(gd, wd_2d, b_trans=True, s2=(h, w), s2_scatter=True):
+                    conv_bn.c1x1(gd, wd_2d, b_trans=True, s2=(h, w), s2_scatter=True, resid=gx2d)
+                else:
+                    gx2d.view(n, h, w, c)[:, ::2, ::2, :] += torch.mm(gd, wd_2d).view(n, h // 2, w // 2, c)
+            elif conv_bn.preferred(kd, c, gd.size(0)) and conv_bn.supported(gd, wd_2d, resid=True, b_trans=True):
+                gx2d, _ = conv_bn.c1x1(gd, wd_2d, resid=gx2d, b_trans=True)
+            else:
+                torch.addmm(gx2d, gd, wd_2d, out=gx2d)
+            gx = gx2d.view(n, h, w, c).permute(0, 3, 1, 2)
+        conv_bwd = torch.ops.aten.convolution_backward
+        if ctx.needs_input_grad[1]:
+            args = ([1, 1], [0, 0], [1, 1], False, [0, 0], 1)
+            gw1 = _wgrad(x, gy1, w1, 1, "gemm", lambda: conv_bwd(gy1, x, w1, None, *args, [False, True, False])[1])
+        if ctx.needs_input_grad[2]:
+            if ctx.s2:
+                args = ([2, 2], [0, 0], [1, 1], False, [0, 0], 1)
+                gwd = bhconv.conv_wgrad_s2(x, gyd) if bhconv.wgrad_supported(x, gyd, 1, 2) else \
+                    conv_bwd(gyd, x, wd, None, *args, [False, True, False])[1]
+                if gwd.stride() != wd.stride():
+                    gwd = gwd.contiguous()
+            else:
+                args = ([1, 1], [0, 0], [1, 1], False, [0, 0], 1)
+                gwd = _wgrad(x, gyd, wd, 1, "gemm", lambda: conv_bwd(gyd, x, wd, None, *args, [False, True, False])[1])
+        return gx, gw1, gwd, None, None, None
 
 
 class _Conv3x3BNFn(torch.autograd.Function):
@@ -632,8 +703,14 @@ class Bottleneck(nn.Module):
         from ..ops import conv as bhconv
         from ..parallel.optimized_sync_batchnorm import BNLink
 
-        box = {} if (torch.is_grad_enabled() and x.requires_grad) else None
-        y1, p1 = _Conv1x1BNFn.apply(x, self.conv1.weight, _kshift(self.bn1), None, box, False)
+        ds = self.downsample
+        if ds is not None:  # conv1 and the downsample conv as one node (no residual stash needed)
+            y1, p1, yd, pd = _Conv1DsFn.apply(x, self.conv1.weight, ds[0].weight, _kshift(self.bn1), _kshift(ds[1]),
+                                              self.stride == 2)
+            box = None
+        else:
+            box = {} if (torch.is_grad_enabled() and x.requires_grad) else None
+            y1, p1 = _Conv1x1BNFn.apply(x, self.conv1.weight, _kshift(self.bn1), None, box, False)
         l1 = BNLink()
         a1 = self.bn1.forward_from_stats(y1, p1, link=l1)
         l2 = None
@@ -644,13 +721,10 @@ class Bottleneck(nn.Module):
         else:  # stride-2 3x3 (MIOpen): its BatchNorm computes its own statistics
             a2 = self.bn2(self.conv2(a1))
         y3, p3 = _Conv1x1BNFn.apply(a2, self.conv3.weight, _kshift(self.bn3), l2, None, False)
-        xs = _GradStash.apply(x, box) if box is not None else x
-        if self.downsample is not None:
-            conv_d, bn_d = self.downsample[0], self.downsample[1]
-            yd, pd = _Conv1x1BNFn.apply(xs, conv_d.weight, _kshift(bn_d), None, None, self.stride == 2)
-            identity = bn_d.forward_from_stats(yd, pd)
+        if ds is not None:
+            identity = ds[1].forward_from_stats(yd, pd)
         else:
-            identity = xs
+            identity = _GradStash.apply(x, box) if box is not None else x
         return self.bn3.forward_from_stats(y3, p3, z=identity)
 
     def forward(self, x):
@@ -690,9 +764,9 @@ class ResNet(nn.Module):
         # activation is never materialised); same parameters / state_dict as the unfused stem
         self.stem_pool_fused = fused and stem_pool_fused
         self.inplanes = 64
-        if _CONV3X3_MODE != "miopen":  # the fused model: MFMA stem forward, timed against MIOpen
-            self.conv1 = StemConv(3, 64, kernel_size=7, stride=2, padding=3, bias=False,
-                                  mode="gemm" if _CONV3X3_MODE == "direct" else _CONV3X3_MODE)
+        if _CONV3X3_MODE != "miopen":  # the fused model: MFMA stem forward and weight gradient
+            # (0.15 / 0.27 ms vs MIOpen's 0.48 / 0.39, profiles/resnet50_stem_mfma_vs_miopen.jsonl)
+            self.conv1 = StemConv(3, 64, kernel_size=7, stride=2, padding=3, bias=False, mode="gemm")
         else:
             self.conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
         if self.stem_pool_fused:

@@ -62,25 +62,34 @@ def c1x1(a: torch.Tensor, b: torch.Tensor, pro_scale: Optional[torch.Tensor] = N
          epi: str = "plain", kshift: Optional[torch.Tensor] = None, by: Optional[torch.Tensor] = None,
          bscale: Optional[torch.Tensor] = None, bshift: Optional[torch.Tensor] = None,
          bmean: Optional[torch.Tensor] = None, brelu: bool = True,
-         b_trans: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
-    """``b_trans``: ``b`` is given as ``[K, N]`` (e.g. a forward weight for the data gradient)."""
+         b_trans: bool = False, s2_scatter: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``b_trans``: ``b`` is given as ``[K, N]`` (e.g. a forward weight for the data gradient).
+    ``s2_scatter`` (with ``s2=(H, W)`` and ``resid`` the full-resolution ``[N*H*W, N]`` tensor): row
+    (n, y, x) of ``a @ b.T`` is ADDED in place into row (n, 2y, 2x) of ``resid``, which is returned --
+    the 1x1 / stride-2 data gradient accumulated onto the other branch's gradient."""
     rows = a.size(0)
-    M = rows // 4 if s2 is not None else rows
+    M = rows // 4 if (s2 is not None and not s2_scatter) else rows
     if not a.is_cuda:
-        return _reference(a, b.t() if b_trans else b, pro_scale, pro_shift, resid, s2, epi, kshift, by, bscale,
-                          bshift, bmean, brelu)
+        bb = b.t() if b_trans else b
+        if s2_scatter:
+            H, W = s2
+            add = a.float() @ bb.float().t()
+            view = resid.view(-1, H, W, resid.size(1))[:, ::2, ::2, :]
+            view.copy_((view.float() + add.view(view.shape)).to(resid.dtype))
+            return resid, torch.empty(0)
+        return _reference(a, bb, pro_scale, pro_shift, resid, s2, epi, kshift, by, bscale, bshift, bmean, brelu)
     H, W = s2 if s2 is not None else (0, 0)
     return submodule("conv_bn").c1x1(a, b, b_trans, M, pro_scale, pro_shift, resid, H, W, _EPI[epi], kshift, by,
-                                     bscale, bshift, bmean, brelu)
+                                     bscale, bshift, bmean, brelu, s2_scatter)
 
 
 def supported(a: torch.Tensor, b: torch.Tensor, pro: bool = False, resid: bool = False, s2=None,
-              epi: str = "plain", b_trans: bool = False) -> bool:
+              epi: str = "plain", b_trans: bool = False, s2_scatter: bool = False) -> bool:
     if not (a.is_cuda and available()):
         return False
     H, W = s2 if s2 is not None else (0, 0)
-    M = a.size(0) // 4 if s2 is not None else a.size(0)
-    return submodule("conv_bn").c1x1_supported(a, b, b_trans, M, pro, resid, H, W, _EPI[epi])
+    M = a.size(0) // 4 if (s2 is not None and not s2_scatter) else a.size(0)
+    return submodule("conv_bn").c1x1_supported(a, b, b_trans, M, pro, resid, H, W, _EPI[epi], s2_scatter)
 
 
 def preferred(K: int, N: int, M: int, s2: bool = False) -> bool:

@@ -1,0 +1,22 @@
+#!/bin/bash
+# Parametrised GPU driver: bash scripts/gpu_suite.sh <preset> [<preset> ...]
+# Each preset expands to named steps run by gpu_steps.sh (own time limit each, stop at the first crash).
+#   tests   : pytest -m gpu (whole suite, one process)
+#   fold    : BN-folded conv kernels + block numerics
+#   micro   : conv_bn microbenchmark (strip / tiled GEMM vs hipBLASLt + BatchNorm passes)
+#   bench   : bench.py 1 GPU (20 steps), with a cProfile of warmup step 1
+#   prof    : rocprofv3 kernel trace of the bench + per-kernel summary (gpurun_out/r50_summary.md)
+#   nofold  : bench.py with BH_FOLD_BN=0 (A/B)
+steps=()
+for preset in "$@"; do
+  case "$preset" in
+    tests) steps+=("tests:900:python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu") ;;
+    fold) steps+=("fold:400:python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_conv_bn.py tests/test_resnet_fold.py tests/test_ddp.py -m gpu") ;;
+    micro) steps+=("micro:300:python benchmarks/bench_conv_bn.py --out gpurun_out/conv_bn_vs_unfused.jsonl") ;;
+    bench) steps+=("bench:400:python bench.py --steps 20 --warmup 5 --trace-warmup gpurun_out/warmup1_cprofile.txt") ;;
+    nofold) steps+=("nofold:400:BH_FOLD_BN=0 python bench.py --steps 20 --warmup 5") ;;
+    prof) steps+=("prof:300:cd /tmp && export TMPDIR=/tmp && cd \$GRAFT_REPO_ROOT && rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r50 -o run -- python bench.py --steps 8 --warmup 5 && python scripts/prof_summary.py gpurun_out/prof_r50 k_lamb2 3 gpurun_out/r50_summary.md && rm -rf gpurun_out/prof_r50") ;;
+    *) echo "unknown preset $preset"; exit 2 ;;
+  esac
+done
+bash scripts/gpu_steps.sh "${steps[@]}"

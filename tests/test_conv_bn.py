@@ -225,3 +225,31 @@ def test_gemm_bn_epilogues(KN, dt, epi):
         ref, _, _ = syncbn.backward_reduce(cf.t().reshape(1, N, M, 1), y.float().cpu().t().reshape(1, N, M, 1), None,
                                            mean.cpu(), None, sc.cpu(), sh.cpu(), True, None, False)
     _stats_close(conv_bn.sum_parts(part), ref, M)
+
+
+def test_c1x1_scatter_reference_cpu():
+    a = torch.randn(2 * 3 * 4, 8)
+    b = torch.randn(16, 8)
+    base = torch.randn(2 * 6 * 8, 16)
+    out, _ = conv_bn.c1x1(a, b, s2=(6, 8), s2_scatter=True, resid=base.clone())
+    ref = base.clone().view(2, 6, 8, 16)
+    ref[:, ::2, ::2, :] += (a @ b.t()).view(2, 3, 4, 16)
+    torch.testing.assert_close(out.view(2, 6, 8, 16), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("KNHW", [(512, 256, 8, 8), (1024, 512, 12, 8), (256, 64, 4, 16)])
+def test_c1x1_stride2_scatter_accumulate(KNHW, dt):
+    """dX += scatter(dY_ds . W_ds): the downsample data gradient added at the even pixels in place."""
+    K, N, H, W = KNHW
+    n = 4
+    a, _ = _data(n * (H // 2) * (W // 2), K, N, dt, "cuda", seed=8)
+    w = (torch.randn(K, N) / K ** 0.5).to(dt).cuda()  # forward weight [Cout=K, Cin=N]: b_trans
+    base = torch.randn(n * H * W, N, device="cuda").to(dt)
+    assert conv_bn.supported(a, w, b_trans=True, s2=(H, W), s2_scatter=True)
+    ref = base.float().clone().view(n, H, W, N)
+    ref[:, ::2, ::2, :] += (a.float() @ w.float()).view(n, H // 2, W // 2, N)
+    out, _ = conv_bn.c1x1(a, w, b_trans=True, s2=(H, W), s2_scatter=True, resid=base)
+    assert out.data_ptr() == base.data_ptr()
+    torch.testing.assert_close(out.float().view(n, H, W, N), ref, **_tol(dt))
