@@ -12,7 +12,8 @@ import torch.distributed as dist
 from torch import nn
 
 from ...ops import syncbn as _bn
-from ..conv_bias_relu.conv_bias_relu import ConvFrozenScaleBiasReLU
+from ..conv_bias_relu.conv_bias_relu import (ConvFrozenScaleBias, ConvFrozenScaleBiasAddReLU,
+                                             ConvFrozenScaleBiasReLU)
 from .halo_exchangers import HaloExchangerSendRecv
 
 
@@ -116,17 +117,19 @@ class Bottleneck(nn.Module):
         return ConvFrozenScaleBiasReLU(out, self.conv2.weight, s2, b2, 1, 1)
 
     def forward(self, x):
+        # every conv + frozen BN (+ residual) + ReLU is ONE kernel (conv_bias_relu's affine epilogues on the
+        # MFMA 1x1 / 3x3 convolutions) where the shape is covered, MIOpen + one epilogue pass otherwise
         x = self._to_nchw(x)
         s1, b1 = self.bn1.get_scale_bias()
         out = ConvFrozenScaleBiasReLU(x, self.conv1.weight, s1, b1, 0, self.stride)
         out = self._conv2(out)
-        c3 = nn.functional.conv2d(out, self.conv3.weight)
         if self.downsample is not None:
-            identity = self.downsample(x)
+            sd, bd = self.downsample[1].get_scale_bias()
+            identity = ConvFrozenScaleBias(x, self.downsample[0].weight, sd, bd, 0, self.stride)
         else:
             identity = x
         s3, b3 = self.bn3.get_scale_bias()
-        y = _ScaleBiasAddReLU.apply(c3, s3, b3, identity.to(c3.dtype))
+        y = ConvFrozenScaleBiasAddReLU(out, self.conv3.weight, s3, b3, identity.to(out.dtype), 0, 1)
         return self._from_nchw(y)
 
 

@@ -98,6 +98,30 @@ std::vector<at::Tensor> conv3x3_bn_forward(const at::Tensor& x, const at::Tensor
   return {y, part};
 }
 
+// y = relu?(conv3x3(x, w) * scale + shift (+ r)) (* r when r_mul): conv + bias / frozen BatchNorm
+// (+ residual) (+ ReLU) (x mask) in one kernel
+at::Tensor conv3x3_affine(const at::Tensor& x, const at::Tensor& w, const at::Tensor& scale, const at::Tensor& shift,
+                          bool relu, const c10::optional<at::Tensor>& r, bool r_mul) {
+  TORCH_CHECK(shapes_ok(x, w), "conv3x3_affine: needs channels_last fp16/bf16 x, w [K, C, 3, 3], C and K % 64 == 0");
+  const at::Tensor wc = w.contiguous(at::MemoryFormat::ChannelsLast);
+  auto y = at::empty({x.size(0), w.size(0), x.size(2), x.size(3)}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto a = conv_args(x, wc, y);
+  a.epi = bh::kConvEpiAffine;
+  a.a_scale = f32_or_null(scale, a.K, "scale");
+  a.a_shift = f32_or_null(shift, a.K, "shift");
+  a.relu = relu;
+  a.r_mul = r_mul;
+  if (r.has_value() && r->defined()) {
+    TORCH_CHECK(r->is_cuda() && r->device() == x.device() && r->scalar_type() == x.scalar_type() &&
+                    r->sizes() == y.sizes() && r->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv3x3_affine: r must be a channels_last tensor shaped like the output");
+    a.r = r->data_ptr();
+  }
+  TORCH_CHECK(bh::conv3x3_supported(a), "conv3x3_affine: unsupported arguments");
+  bh::conv3x3_forward(dtype_code(x.scalar_type()), a, stream_for(x));
+  return y;
+}
+
 // conv3x3_dgrad whose epilogue also reduces the PREVIOUS BatchNorm's backward sums: by is that
 // BatchNorm's raw input (same shape as dx), dz = dx * (by * bscale + bshift > 0) (brelu): partials
 // [2, G, C] of dz and dz * (by - bmean)
@@ -256,6 +280,8 @@ void register_conv(pybind11::module_& root) {
   m.def("supported", &supported, py::arg("x"), py::arg("weight"));
   m.def("conv3x3_bn_forward", &conv3x3_bn_forward, py::arg("x"), py::arg("weight"), py::arg("pro_scale") = py::none(),
         py::arg("pro_shift") = py::none(), py::arg("stats") = false, py::arg("kshift") = py::none());
+  m.def("conv3x3_affine", &conv3x3_affine, py::arg("x"), py::arg("weight"), py::arg("scale"), py::arg("shift"),
+        py::arg("relu") = true, py::arg("r") = py::none(), py::arg("r_mul") = false);
   m.def("conv3x3_bn_dgrad", &conv3x3_bn_dgrad, py::arg("grad_out"), py::arg("weight"), py::arg("by"),
         py::arg("bscale"), py::arg("bshift"), py::arg("bmean"), py::arg("brelu") = true);
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("grad_out"), py::arg("R"), py::arg("stride") = 1,

@@ -69,7 +69,9 @@ std::vector<at::Tensor> c1x1(const at::Tensor& a, const at::Tensor& b, bool b_tr
                              const c10::optional<at::Tensor>& resid, int64_t s2_h, int64_t s2_w, int64_t epi,
                              const c10::optional<at::Tensor>& kshift, const c10::optional<at::Tensor>& by,
                              const c10::optional<at::Tensor>& bscale, const c10::optional<at::Tensor>& bshift,
-                             const c10::optional<at::Tensor>& bmean, bool brelu, bool s2_scatter) {
+                             const c10::optional<at::Tensor>& bmean, bool brelu, bool s2_scatter,
+                             const c10::optional<at::Tensor>& a_scale, const c10::optional<at::Tensor>& a_shift,
+                             bool relu, bool r_mul) {
   at::Tensor c;
   if (s2_scatter) {
     // accumulate into the full-resolution tensor `resid` in place: a is [M, K], resid [4M, N]
@@ -92,8 +94,14 @@ std::vector<at::Tensor> c1x1(const at::Tensor& a, const at::Tensor& b, bool b_tr
     c = at::empty({M, (int64_t)p.N}, a.options());
   }
   p.C = c.data_ptr();
+  if (epi == bh::kC1x1Affine) {
+    p.a_scale = fptr(a_scale, p.N, "a_scale");
+    p.a_shift = fptr(a_shift, p.N, "a_shift");
+    p.relu = relu;
+    p.r_mul = r_mul;
+  }
   at::Tensor part;
-  if (epi != bh::kC1x1Plain) {
+  if (epi == bh::kC1x1Stats || epi == bh::kC1x1Bwd) {
     const int G = bh::c1x1_parts(p);
     TORCH_CHECK(G > 0, "conv_bn.c1x1: unsupported shape");
     part = at::empty({2, (int64_t)G, (int64_t)p.N}, a.options().dtype(at::kFloat));
@@ -131,6 +139,7 @@ bool c1x1_supported(const at::Tensor& a, const at::Tensor& b, bool b_trans, int6
   p.s2_W = (int)s2_w;
   p.epi = (int)epi;
   p.part = dummy;
+  if (epi == bh::kC1x1Affine) p.a_scale = p.a_shift = dummy;
   if (epi == bh::kC1x1Bwd) {
     p.by = a.data_ptr();
     p.bscale = p.bshift = p.bmean = dummy;
@@ -198,7 +207,9 @@ void register_conv_bn(pybind11::module_& root) {
         py::arg("pro_shift") = py::none(), py::arg("resid") = py::none(), py::arg("s2_h") = 0, py::arg("s2_w") = 0,
         py::arg("epi") = 0, py::arg("kshift") = py::none(), py::arg("by") = py::none(), py::arg("bscale") = py::none(),
         py::arg("bshift") = py::none(), py::arg("bmean") = py::none(), py::arg("brelu") = true,
-        py::arg("s2_scatter") = false);
+        py::arg("s2_scatter") = false, py::arg("a_scale") = py::none(), py::arg("a_shift") = py::none(),
+        py::arg("relu") = false, py::arg("r_mul") = false);
+  m.attr("EPI_AFFINE") = (int)bh::kC1x1Affine;
   m.def("c1x1_supported", &c1x1_supported, py::arg("a"), py::arg("b"), py::arg("b_trans"), py::arg("M"), py::arg("pro") = false,
         py::arg("resid") = false, py::arg("s2_h") = 0, py::arg("s2_w") = 0, py::arg("epi") = 0,
         py::arg("s2_scatter") = false);

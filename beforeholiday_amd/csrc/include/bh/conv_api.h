@@ -12,7 +12,7 @@
 
 namespace bh {
 
-enum ConvEpi { kConvEpiPlain = 0, kConvEpiStats = 1, kConvEpiBwd = 2 };
+enum ConvEpi { kConvEpiPlain = 0, kConvEpiStats = 1, kConvEpiBwd = 2, kConvEpiAffine = 3 };
 
 struct Conv3x3Args {
   const void* x = nullptr;  // [N, H, W, C]
@@ -34,6 +34,12 @@ struct Conv3x3Args {
   const float* bshift = nullptr;
   const float* bmean = nullptr;
   bool brelu = true;
+  // forward kConvEpiAffine: y = relu?(acc * a_scale[k] + a_shift[k] (+ r)) (* r when r_mul), r [N, H, W, K]
+  const float* a_scale = nullptr;
+  const float* a_shift = nullptr;
+  const void* r = nullptr;
+  bool relu = false;
+  bool r_mul = false;
 };
 
 // true when the kernel covers the shape (C % 64 == 0, K % 64 == 0, 16-byte aligned tensors)

@@ -21,7 +21,7 @@
 
 namespace bh {
 
-enum C1x1Epi { kC1x1Plain = 0, kC1x1Stats = 1, kC1x1Bwd = 2 };
+enum C1x1Epi { kC1x1Plain = 0, kC1x1Stats = 1, kC1x1Bwd = 2, kC1x1Affine = 3 };
 
 struct C1x1Args {
   const void* A = nullptr;  // [rows, K] (rows = M, or N * s2_H * s2_W with the stride-2 gather)
@@ -46,6 +46,12 @@ struct C1x1Args {
   const float* bshift = nullptr;
   const float* bmean = nullptr;
   bool brelu = true;
+  // kC1x1Affine: c = relu?(acc * a_scale[n] + a_shift[n] (+ R)) (* R when r_mul) -- conv + bias / frozen
+  // BatchNorm (+ residual) (+ ReLU) (x mask) in one pass (contrib conv_bias_relu / bottleneck)
+  const float* a_scale = nullptr;
+  const float* a_shift = nullptr;
+  bool relu = false;
+  bool r_mul = false;
 };
 
 // whether the kernel covers the shape (K % 64, N % 64, M % 32, LDS budget, 16-byte alignment)

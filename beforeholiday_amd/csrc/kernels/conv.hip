@@ -110,7 +110,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
     // visible to the first halo_store through the __syncthreads below it
   }
   // window origin of tile id t: x-tile fastest, then row window, then image group
-  auto origin = [&](int t, int& n0, int& y0, int& x0) {
+  auto origin = [&](int t, int& n0, int& y0, int& x0) __attribute__((always_inline)) {
     const int xt = t % g.XT;
     t /= g.XT;
     const int yt = t % g.YT;
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
   i4v hreg[kHaloPer];
   uint32_t hmask = 0;
   int hc0 = 0;  // first input channel of the staged chunk (the prologue's scale / shift)
-  auto halo_load = [&](int t, int c0) {
+  auto halo_load = [&](int t, int c0) __attribute__((always_inline)) {
     int n0, y0, x0;
     origin(t, n0, y0, x0);
     hmask = 0;
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
       hmask |= (ok ? 1u : 0u) << i;
     }
   };
-  auto halo_store = [&]() {
+  auto halo_store = [&]() __attribute__((always_inline)) {
     float sc[8], sh[8];
     if constexpr (PRO) {
       // BatchNorm + ReLU of the producing layer on the staged input; this thread's pieces all hold
@@ -170,8 +170,12 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
     }
   };
   // ---- weight slice of step (chunk, r * 3 + s): W[k0 .. k0+63][r][s][c0 .. c0+63] ----
-  i4v wreg[2];
-  auto w_load = [&](int step) {
+  // Two register slots, two steps of lookahead: the slice of step t + 2 is requested at the start of
+  // step t and written to LDS at the end of step t + 1, so an L2 round trip (longer than one step's
+  // 16 MFMAs per wave) never sits between the barrier of one step and the MFMAs of the next. The step
+  // loop is unrolled by two so the slots stay statically named.
+  i4v wr0[2], wr1[2];
+  auto w_load = [&](int step, i4v(&wreg)[2]) {
     const int within = step % per_tile, chunk = within / 9, rs = within - chunk * 9;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -182,7 +186,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
         wreg[i] = *reinterpret_cast<const i4v*>(Wt + ((k0 + row) * 9 + rs) * C + chunk * kCK + ch * 8);
     }
   };
-  auto w_store = [&](char* buf) {
+  auto w_store = [&](char* buf, const i4v(&wreg)[2]) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int p = tid + i * kThreads;
@@ -191,7 +195,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
   };
 
   f16v acc[2][2];
-  auto zero_acc = [&]() {
+  auto zero_acc = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -213,13 +217,16 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
     const int ch = k0 + 32 * kb + r32;
     if constexpr (EPI == kConvEpiStats) {
       e0[kb] = a.kshift ? a.kshift[ch] : 0.f;
+    } else if constexpr (EPI == kConvEpiAffine) {
+      e0[kb] = a.a_scale[ch];
+      e1[kb] = a.a_shift[ch];
     } else if constexpr (EPI == kConvEpiBwd) {
       e0[kb] = a.bscale[ch];
       e1[kb] = a.bshift[ch];
       e2[kb] = a.bmean[ch];
     }
   }
-  auto epilogue = [&](int t) {
+  auto epilogue = [&](int t) __attribute__((always_inline)) {
     int n0, y0, x0;
     origin(t, n0, y0, x0);
 #pragma unroll
@@ -234,7 +241,16 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
         const int off = ((n * H + y) * W + x) * a.K + k0 + r32;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
-          const T o = from_f<T>(acc[kb][pb][v]);
+          float xv = acc[kb][pb][v];
+          if constexpr (EPI == kConvEpiAffine) {
+            // conv + bias / frozen BatchNorm (+ residual) (+ ReLU) (x mask) in the epilogue
+            xv = fmaf(xv, e0[kb], e1[kb]);
+            const float rv = a.r ? to_f<T>(reinterpret_cast<const T*>(a.r)[off + 32 * kb]) : 0.f;
+            if (a.r && !a.r_mul) xv += rv;
+            if (a.relu) xv = fmaxf(xv, 0.f);
+            if (a.r && a.r_mul) xv *= rv;
+          }
+          const T o = from_f<T>(xv);
           Y[off + 32 * kb] = o;
           const float f = to_f<T>(o);  // statistics of the value as stored
           if constexpr (EPI == kConvEpiStats) {
@@ -254,17 +270,20 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
 
   zero_acc();
   halo_load(tile0, 0);
-  w_load(0);
+  w_load(0, wr0);
   halo_store();
-  w_store(wb);
+  w_store(wb, wr0);
+  if (steps > 1) w_load(1, wr1);
   __syncthreads();
-  for (int t = 0; t < steps; ++t) {
+  // step t: request slice t + 2 into `nxt2` (free: its slice t went to LDS at the end of step t - 1),
+  // compute from LDS buffer t & 1, write slice t + 1 (`nxt`, requested a step ago) to buffer (t + 1) & 1
+  auto step_body = [&](int t, i4v(&nxt2)[2], const i4v(&nxt)[2]) __attribute__((always_inline)) {
     const int it = t / per_tile, within = t - it * per_tile;
     const int chunk = within / 9, rs = within - chunk * 9;
     const bool last_rs = rs == 8;
     // the next (window, chunk) whose halo is prefetched during this chunk
     const bool more = chunk + 1 < nch || it + 1 < ntile;
-    if (t + 1 < steps) w_load(t + 1);
+    if (t + 2 < steps) w_load(t + 2, nxt2);
     if (rs == 0 && more) {
       if (chunk + 1 < nch) halo_load(tile0 + it, (chunk + 1) * kCK);
       else halo_load(tile0 + it + 1, 0);
@@ -301,7 +320,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
       acc[1][0] = Mfma32<T>::run(fb[2], fb[1], acc[1][0]);
       acc[1][1] = Mfma32<T>::run(fb[3], fb[1], acc[1][1]);
     }
-    if (t + 1 < steps) w_store(wb + ((t + 1) & 1) * kWBytes);
+    if (t + 1 < steps) w_store(wb + ((t + 1) & 1) * kWBytes, nxt);
     if (last_rs && chunk + 1 == nch) {  // window done: results out, accumulators reset
       epilogue(tile0 + it);
       zero_acc();
@@ -311,8 +330,12 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
       halo_store();
     }
     __syncthreads();
+  };
+  for (int t = 0; t < steps; t += 2) {
+    step_body(t, wr0, wr1);
+    if (t + 1 < steps) step_body(t + 1, wr1, wr0);
   }
-  if constexpr (EPI != kConvEpiPlain) {
+  if constexpr (EPI == kConvEpiStats || EPI == kConvEpiBwd) {
     // per-workgroup partial of each statistic: lane halves, then the 4 waves (LDS, the halo is free)
     float* red = reinterpret_cast<float*>(smem);  // [waves][2][64]
 #pragma unroll
@@ -356,8 +379,9 @@ bool conv3x3_supported(const Conv3x3Args& a) {
   auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   const int64_t pix = (int64_t)a.N * a.H * a.W;
   if (a.pro_scale && (!a.pro_shift || a.C > kMaxProC)) return false;
-  if (a.epi != kConvEpiPlain && !a.part) return false;
+  if ((a.epi == kConvEpiStats || a.epi == kConvEpiBwd) && !a.part) return false;
   if (a.epi == kConvEpiBwd && (!a.by || !al(a.by) || !a.bscale || !a.bshift || !a.bmean)) return false;
+  if (a.epi == kConvEpiAffine && (!a.a_scale || !a.a_shift || a.pro_scale)) return false;
   return a.N > 0 && a.H > 0 && a.W > 0 && a.C > 0 && a.K > 0 && a.C % kCK == 0 && a.K % kBN == 0 && al(a.x) &&
          al(a.w) && al(a.y) && pix * a.C < (1ll << 31) && pix * a.K < (1ll << 31);  // 32-bit offsets
 }
@@ -395,6 +419,7 @@ void conv3x3_run(int dt, const Conv3x3Args& a, bool flip, hipStream_t st) {
   // instantiated: forward (prologue and / or statistics epilogue), data gradient (backward epilogue)
   if (flip && (a.pro_scale || a.epi == kConvEpiStats)) throw std::runtime_error("conv3x3_dgrad: no prologue / stats");
   if (!flip && a.epi == kConvEpiBwd) throw std::runtime_error("conv3x3_forward: no backward epilogue");
+  if (flip && a.epi == kConvEpiAffine) throw std::runtime_error("conv3x3_dgrad: no affine epilogue");
   const Launch l = plan(a);
   auto launch = [&](auto tt, auto gg) {
     using T = typename decltype(tt)::type;
@@ -408,6 +433,7 @@ void conv3x3_run(int dt, const Conv3x3Args& a, bool flip, hipStream_t st) {
       else L(k_conv3x3<T, false, GG, true, kConvEpiPlain>);
     } else {
       if (a.epi == kConvEpiStats) L(k_conv3x3<T, false, GG, false, kConvEpiStats>);
+      else if (a.epi == kConvEpiAffine) L(k_conv3x3<T, false, GG, false, kConvEpiAffine>);
       else L(k_conv3x3<T, false, GG, false, kConvEpiPlain>);
     }
   };

@@ -107,6 +107,12 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
         ss[K + c] = p.pro_shift[c];
       }
     }
+    if constexpr (EPI == kC1x1Affine) {  // frozen per-column scale / shift of the epilogue
+      for (int c = threadIdx.x; c < NC; c += kThreads) {
+        ss[c] = p.a_scale[col0 + c];
+        ss[NC + c] = p.a_shift[col0 + c];
+      }
+    }
     if constexpr (EPI == kC1x1Bwd) {  // the previous BatchNorm's per-column constants, read per tile
       for (int c = threadIdx.x; c < NC; c += kThreads) {
         ss[c] = p.bscale[col0 + c];
@@ -218,11 +224,11 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
           for (int i = 0; i < 4; ++i) xr[4 * j + i] = to_f<T>(src[orow[4 * j + i] * N + col]);
       }
       float bsc = 0.f, bsh = 0.f, bmn = 0.f;
-      if constexpr (EPI == kC1x1Bwd) {
+      if constexpr (EPI == kC1x1Bwd || EPI == kC1x1Affine) {
         bsc = ss[32 * t + r];
         bsh = ss[NC + 32 * t + r];
-        bmn = ss[2 * NC + 32 * t + r];
       }
+      if constexpr (EPI == kC1x1Bwd) bmn = ss[2 * NC + 32 * t + r];
       float yv[16];
       if constexpr (RES && EPI == kC1x1Bwd) {
 #pragma unroll
@@ -236,7 +242,19 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
         for (int i = 0; i < 4; ++i) {
           const int v = 4 * j + i;
           float x = acc[t][v];
-          if constexpr (RES) x += xr[v];
+          if constexpr (EPI == kC1x1Affine) {
+            // conv + bias / frozen BatchNorm (+ residual) (+ ReLU) (x mask): one pass
+            x = fmaf(x, bsc, bsh);
+            if constexpr (RES) {
+              if (!p.r_mul) x += xr[v];
+            }
+            if (p.relu) x = fmaxf(x, 0.f);
+            if constexpr (RES) {
+              if (p.r_mul) x *= xr[v];
+            }
+          } else if constexpr (RES) {
+            x += xr[v];
+          }
           const T o = from_f<T>(x);
           Cp[orow[v] * N + col] = o;
           const float f = to_f<T>(o);  // statistics of the value as stored
@@ -266,7 +284,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
     }
   }
 
-  if constexpr (EPI != kC1x1Plain) {
+  if constexpr (EPI == kC1x1Stats || EPI == kC1x1Bwd) {
     float* red = reinterpret_cast<float*>(smem + g.red_off);  // [waves][2][NC]
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -322,10 +340,10 @@ struct Plan {
   Geo g;
 };
 
-int ss_bytes(int NC, int K, bool pro, bool bwd) { return pro ? 8 * K : (bwd ? 12 * NC : 0); }
+int ss_bytes(int NC, int K, bool pro, bool bwd, bool aff) { return pro ? 8 * K : (bwd ? 12 * NC : (aff ? 8 * NC : 0)); }
 
-int lds_bytes(int NC, int K, bool pro, bool bwd, bool stats) {
-  int b = NC * (2 * K + 16) + ss_bytes(NC, K, pro, bwd);
+int lds_bytes(int NC, int K, bool pro, bool bwd, bool aff, bool stats) {
+  int b = NC * (2 * K + 16) + ss_bytes(NC, K, pro, bwd, aff);
   if (stats) b += kWaves * 2 * NC * 4;
   return b;
 }
@@ -333,14 +351,15 @@ int lds_bytes(int NC, int K, bool pro, bool bwd, bool stats) {
 bool make_plan(const C1x1Args& a, Plan* pl) {
   if (a.K <= 0 || a.N <= 0 || a.M <= 0 || a.K % 64 != 0 || a.N % 64 != 0 || a.M % 32 != 0) return false;
   if (a.M / 32 >= (1ll << 31)) return false;
-  const bool pro = a.pro_scale != nullptr, stats = a.epi != kC1x1Plain, bwd = a.epi == kC1x1Bwd;
+  const bool pro = a.pro_scale != nullptr, stats = a.epi == kC1x1Stats || a.epi == kC1x1Bwd,
+             bwd = a.epi == kC1x1Bwd, aff = a.epi == kC1x1Affine;
   // register budget: the backward epilogue (input loads + statistics) fits 4 column tiles per wave
   const int max_nc = bwd ? (a.R ? 64 : 128) : 256;
   int NC = 0, occ = 0;
   // the widest column slice (A read once per slice) that still leaves two workgroups per CU; else one
   for (int want_occ = 2; want_occ >= 1 && !NC; --want_occ)
     for (int nc : {256, 128, 64})
-      if (nc <= max_nc && a.N % nc == 0 && lds_bytes(nc, a.K, pro, bwd, stats) <= 160 * 1024 / want_occ) {
+      if (nc <= max_nc && a.N % nc == 0 && lds_bytes(nc, a.K, pro, bwd, aff, stats) <= 160 * 1024 / want_occ) {
         NC = nc;
         occ = want_occ;
         break;
@@ -355,10 +374,10 @@ bool make_plan(const C1x1Args& a, Plan* pl) {
   const int cap = std::max(1, occ * 256 / g.nslices);        // resident workgroups per slice
   g.G = (std::min(want, cap) + 7) / 8 * 8;
   g.ss_off = NC * (2 * a.K + 16);
-  g.red_off = g.ss_off + ss_bytes(NC, a.K, pro, bwd);
+  g.red_off = g.ss_off + ss_bytes(NC, a.K, pro, bwd, aff);
   pl->NC = NC;
   pl->KC = KC;
-  pl->lds = lds_bytes(NC, a.K, pro, bwd, stats);
+  pl->lds = lds_bytes(NC, a.K, pro, bwd, aff, stats);
   pl->occ = occ;
   pl->g = g;
   return true;
@@ -375,12 +394,14 @@ bool c1x1_supported(const C1x1Args& a) {
   if (!make_plan(a, &pl)) return false;
   if (!al16(a.A) || !al16(a.B) || !al16(a.C) || (a.R && !al16(a.R))) return false;
   if (a.epi == kC1x1Bwd && (!a.by || !a.bscale || !a.bshift || !a.bmean)) return false;
-  if (a.epi != kC1x1Plain && !a.part) return false;
+  if (a.epi == kC1x1Affine && (!a.a_scale || !a.a_shift || a.pro_scale || a.s2_scatter)) return false;
+  if ((a.epi == kC1x1Stats || a.epi == kC1x1Bwd) && !a.part) return false;
   if (a.s2_H > 0) {
     if (a.s2_H % 2 || a.s2_W % 2 || a.M % ((int64_t)(a.s2_H / 2) * (a.s2_W / 2))) return false;
     if (a.pro_scale || a.epi == kC1x1Bwd) return false;  // combinations not instantiated
-    // gather: no residual; scatter: plain epilogue accumulating into the full-resolution C (R == C)
-    if (a.s2_scatter ? (a.epi != kC1x1Plain || a.R != a.C) : a.R != nullptr) return false;
+    // gather: no residual (the affine epilogue excepted); scatter: plain epilogue accumulating into the
+    // full-resolution C (R == C)
+    if (a.s2_scatter ? (a.epi != kC1x1Plain || a.R != a.C) : (a.R != nullptr && a.epi != kC1x1Affine)) return false;
   } else if (a.s2_scatter) {
     return false;
   }
@@ -417,6 +438,14 @@ void c1x1_run(int dt, const C1x1Args& a, hipStream_t st) {
       }
       if constexpr (NC <= 128) {
         if (!res) L(k_c1x1<T, KC, NC, kC1x1Bwd, false, 0, false>);
+      }
+    } else if (a.epi == kC1x1Affine) {
+      if (s2) {
+        if (res) L(k_c1x1<T, KC, NC, kC1x1Affine, false, 1, true>);
+        else L(k_c1x1<T, KC, NC, kC1x1Affine, false, 1, false>);
+      } else {
+        if (res) L(k_c1x1<T, KC, NC, kC1x1Affine, false, 0, true>);
+        else L(k_c1x1<T, KC, NC, kC1x1Affine, false, 0, false>);
       }
     } else {
       if (s2 && a.s2_scatter) L(k_c1x1<T, KC, NC, kC1x1Plain, false, 2, true>);

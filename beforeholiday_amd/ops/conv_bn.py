@@ -24,7 +24,7 @@ import torch
 
 from .._native import available, submodule
 
-_EPI = {"plain": 0, "stats": 1, "bwd": 2}
+_EPI = {"plain": 0, "stats": 1, "bwd": 2, "affine": 3}
 
 
 def _gather_s2(a: torch.Tensor, s2) -> torch.Tensor:
@@ -81,6 +81,26 @@ def c1x1(a: torch.Tensor, b: torch.Tensor, pro_scale: Optional[torch.Tensor] = N
     H, W = s2 if s2 is not None else (0, 0)
     return submodule("conv_bn").c1x1(a, b, b_trans, M, pro_scale, pro_shift, resid, H, W, _EPI[epi], kshift, by,
                                      bscale, bshift, bmean, brelu, s2_scatter)
+
+
+def c1x1_affine(a: torch.Tensor, b: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, relu: bool = True,
+                r: Optional[torch.Tensor] = None, r_mul: bool = False, s2=None) -> torch.Tensor:
+    """``relu?(a @ b.T * scale + shift (+ r)) (* r if r_mul)`` in one kernel (1x1 conv + bias / frozen
+    BatchNorm (+ residual) (+ ReLU) (x mask)); ``s2=(H, W)`` reads the stride-2 pixels of ``a``."""
+    if not a.is_cuda:
+        aa = _gather_s2(a, s2) if s2 is not None else a
+        y = (aa.float() @ b.float().t()) * scale + shift
+        if r is not None and not r_mul:
+            y = y + r.float()
+        if relu:
+            y = torch.relu(y)
+        if r is not None and r_mul:
+            y = y * r.float()
+        return y.to(a.dtype)
+    M = a.size(0) // 4 if s2 is not None else a.size(0)
+    H, W = s2 if s2 is not None else (0, 0)
+    return submodule("conv_bn").c1x1(a, b, False, M, None, None, r, H, W, _EPI["affine"], None, None, None, None,
+                                     None, True, False, scale, shift, relu, r_mul)[0]
 
 
 def supported(a: torch.Tensor, b: torch.Tensor, pro: bool = False, resid: bool = False, s2=None,
