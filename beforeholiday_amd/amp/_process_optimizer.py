@@ -1,9 +1,21 @@
-"""Optimizer patching for amp (reference: apex/amp/_process_optimizer.py:28-489).
+"""How ``amp.initialize`` rewires an optimizer (behaviour: apex/amp/_process_optimizer.py:28-489).
 
-Master weights (O2/O5): 16-bit params are replaced in the optimizer by fp32 masters; after
-backward the 16-bit grads are unscaled into fp32 master grads with one multi-tensor launch per
-dtype pair, and after ``step`` the masters are copied back into the 16-bit model params (again one
-launch). Gradient stashing supports accumulation across several ``scale_loss`` contexts.
+The optimizer gets an ``_amp_stash`` (the state the rest of amp and the fused optimizers read:
+``fp16_groups`` / ``fp32_from_fp16_groups`` / ``all_fp32_from_fp16_params`` / ``params_have_scaled_gradients``)
+and a :class:`_GradPlan` that implements the three moments of a mixed-precision step:
+
+* ``prepare`` (entering ``scale_loss``): gradients already sitting on the parameters are moved aside
+  (stashed) so this backward writes fresh, scaled ones;
+* ``finish`` (leaving ``scale_loss``): the fresh gradients are unscaled -- 16-bit model gradients
+  straight into the fp32 master gradients, one multi-tensor launch per dtype pair -- and added to
+  the stashed ones where a previous micro-batch left some (gradient accumulation);
+* after ``optimizer.step()`` the fp32 masters are copied back into the 16-bit model parameters (one
+  launch per dtype; FusedSGD writes them inside its own kernel).
+
+Three plans: :class:`_MasterPlan` (O2 / O5: fp32 master copies replace the 16-bit parameters inside
+the optimizer), :class:`_FusedSGDMasterPlan` (FusedSGD folds the unscale into its kernel unless
+``materialize_master_grads``) and :class:`_ModelPlan` (O1 / O4 / O0: the model parameters are the
+masters).
 """
 from __future__ import annotations
 
@@ -28,200 +40,250 @@ def _check_param_type(param):
                     .format(param.type()))
 
 
-def _master_params_to_model_params(self):
-    stash = self._amp_stash
-    if len(stash.all_fp16_params) == 0:
-        return
-    groups = {}
-    for master, model in zip(stash.all_fp32_from_fp16_params, stash.all_fp16_params):
-        groups.setdefault(model.dtype, ([], []))
-        groups[model.dtype][0].append(master.data)
-        groups[model.dtype][1].append(model.data)
-    for masters, models in groups.values():
-        multi_tensor_applier(stash.multi_tensor_scale, stash.dummy_overflow_buf, [masters, models], 1.0)
+def _by_dtype(pairs):
+    """{(dtype_a, dtype_b): ([a...], [b...])} so every multi-tensor launch sees one dtype per list."""
+    out = {}
+    for a, b in pairs:
+        lists = out.setdefault((a.dtype, b.dtype), ([], []))
+        lists[0].append(a)
+        lists[1].append(b)
+    return out
 
 
-def lazy_init_with_master_weights(self):
-    stash = self._amp_stash
-    stash.fp16_groups, stash.fp32_from_fp16_groups, stash.fp32_from_fp32_groups = [], [], []
-    for param_group in self.param_groups:
-        fp16_this, fp32_this, fp32_from_fp16_this = [], [], []
-        for i, param in enumerate(param_group["params"]):
-            if not param.requires_grad:
-                continue
-            _check_param_type(param)
-            if param.dtype in _LOW:
-                fp16_this.append(param)
-                master = param.detach().clone().float()
-                master.requires_grad = True
-                param_group["params"][i] = master
-                fp32_from_fp16_this.append(master)
-                if param in self.state:
-                    self.state[master] = self.state.pop(param)
-            else:
-                fp32_this.append(param)
-                param_group["params"][i] = param
-        stash.fp16_groups.append(fp16_this)
-        stash.fp32_from_fp16_groups.append(fp32_from_fp16_this)
-        stash.fp32_from_fp32_groups.append(fp32_this)
-    stash.all_fp16_params = [p for g in stash.fp16_groups for p in g]
-    stash.all_fp32_from_fp16_params = [p for g in stash.fp32_from_fp16_groups for p in g]
-    stash.all_fp32_from_fp32_params = [p for g in stash.fp32_from_fp32_groups for p in g]
-    stash.all_fp16_grad_stash = [None for _ in stash.all_fp16_params]
-    stash.all_fp32_from_fp32_grad_stash = [None for _ in stash.all_fp32_from_fp32_params]
-    for param in stash.all_fp32_from_fp16_params:
-        param.grad = None
-    for param in stash.all_fp32_from_fp32_params:
-        param.grad = None
-    # re-create optimizer state (e.g. torch.optim momentum) against the new master params
-    self.load_state_dict(self.state_dict())
-
-
-def post_backward_models_are_masters(scaler, params, stashed_grads, scale_override=None):
+def _unscale_into_models(scaler, params, stash, scale_override=None):
+    """Unscale the gradients of ``params`` in place (the parameters are their own masters) and fold
+    in the stashed gradients of an earlier micro-batch; clears ``stash``."""
+    fresh, accum, old = [], [], []
+    for i, p in enumerate(params):
+        s = stash[i]
+        if p.grad is None:
+            if s is not None:
+                p.grad = s  # no new gradient this pass: keep the accumulated one
+        elif s is None:
+            fresh.append(p.grad)
+        else:
+            accum.append(p.grad)
+            old.append(s)
+        stash[i] = None
     if getattr(scaler, "device_mode", False) and scale_override is None:
-        # device-resident scale (LossScaler.enable_device_mode): plain unscale without reading it
-        need_unscale, keep = [], False
-        for i, (param, stashed_grad) in enumerate(zip(params, stashed_grads)):
-            if param.grad is None and stashed_grad is not None:
-                param.grad = stashed_grad
-            elif param.grad is not None and stashed_grad is None:
-                need_unscale.append(param.grad)
-            elif param.grad is not None and stashed_grad is not None:
-                keep = True  # accumulation into stashed grads: the host-scale path below
-        if not keep:
-            if need_unscale:
-                scaler.unscale(need_unscale, need_unscale, None, models_are_masters=True)
-            for i in range(len(stashed_grads)):
-                stashed_grads[i] = None
-            return
-    grads_have_scale, stashed_have_scale, out_scale = scaler.loss_scale(), 1.0, 1.0
-    # not much to do if scale == 1.0 and static scaling
-    if scaler.loss_scale() == 1.0 and not scaler.dynamic:
-        for i in range(len(stashed_grads)):
-            stashed_grads[i] = None
+        # device-resident scale: unscale and accumulate on the device reciprocal (no host read)
+        if fresh:
+            scaler.unscale(fresh, fresh, None, models_are_masters=True)
+        if accum:
+            scaler.unscale_with_stashed(accum, old, accum)
         return
-    if scale_override is not None:
-        grads_have_scale, stashed_have_scale, out_scale = scale_override
-    need_unscale, need_stash, stashed = [], [], []
-    for param, stashed_grad in zip(params, stashed_grads):
-        if param.grad is None and stashed_grad is not None:
-            param.grad = stashed_grad
-        elif param.grad is not None and stashed_grad is None:
-            need_unscale.append(param.grad)
-        elif param.grad is not None and stashed_grad is not None:
-            need_stash.append(param.grad)
-            stashed.append(stashed_grad)
-    if need_unscale:
-        scaler.unscale(need_unscale, need_unscale, None, models_are_masters=True,
-                       scale_override=grads_have_scale / out_scale)
-    if need_stash:
-        scaler.unscale_with_stashed(need_stash, stashed, need_stash,
-                                    scale_override=(grads_have_scale, stashed_have_scale, out_scale))
-    for i in range(len(stashed_grads)):
-        stashed_grads[i] = None
-
-
-def prepare_backward_with_master_weights(self):
-    stash = self._amp_stash
-    self._amp_lazy_init()
-    for param in stash.all_fp16_params:
-        # fp16 grads never need stashing: they are folded into the fp32 master grads
-        param.grad = None
-    for i, param in enumerate(stash.all_fp32_from_fp32_params):
-        stash.all_fp32_from_fp32_grad_stash[i] = param.grad
-        param.grad = None
-
-
-def post_backward_with_master_weights(self, scaler):
-    stash = self._amp_stash
-    self._amp_lazy_init()
-    fp16_unscale, new_fp32, fp16_unscale_stash, preexisting = [], [], [], []
-    for fp16_param, fp32_param in zip(stash.all_fp16_params, stash.all_fp32_from_fp16_params):
-        if fp16_param.grad is None and fp32_param.grad is not None:
-            continue
-        elif fp16_param.grad is not None and fp32_param.grad is None:
-            fp32_param.grad = torch.empty_like(fp32_param)
-            fp16_unscale.append(fp16_param.grad)
-            new_fp32.append(fp32_param.grad)
-        elif fp16_param.grad is not None and fp32_param.grad is not None:
-            fp16_unscale_stash.append(fp16_param.grad)
-            preexisting.append(fp32_param.grad)
-    if fp16_unscale:
-        scaler.unscale(fp16_unscale, new_fp32, None, models_are_masters=False)
-    if fp16_unscale_stash:
-        scaler.unscale_with_stashed(fp16_unscale_stash, preexisting, preexisting)
-    post_backward_models_are_masters(scaler, stash.all_fp32_from_fp32_params, stash.all_fp32_from_fp32_grad_stash)
-
-
-def lazy_init_no_master_weights(self):
-    stash = self._amp_stash
-    stash.all_fp16_params, stash.all_fp32_params = [], []
-    for param_group in self.param_groups:
-        for param in param_group["params"]:
-            _check_param_type(param)
-            (stash.all_fp16_params if param.dtype in _LOW else stash.all_fp32_params).append(param)
-    stash.all_fp16_grad_stash = [None for _ in stash.all_fp16_params]
-    stash.all_fp32_grad_stash = [None for _ in stash.all_fp32_params]
-
-
-def prepare_backward_no_master_weights(self):
-    stash = self._amp_stash
-    self._amp_lazy_init()
-    for i, param in enumerate(stash.all_fp16_params):
-        stash.all_fp16_grad_stash[i] = param.grad
-        param.grad = None
-    for i, param in enumerate(stash.all_fp32_params):
-        stash.all_fp32_grad_stash[i] = param.grad
-        param.grad = None
-
-
-def post_backward_no_master_weights(self, scaler):
-    stash = self._amp_stash
-    self._amp_lazy_init()
-    for params, stashed in ((stash.all_fp16_params, stash.all_fp16_grad_stash),
-                            (stash.all_fp32_params, stash.all_fp32_grad_stash)):
-        post_backward_models_are_masters(scaler, params, stashed)
-
-
-# FusedSGD can fold the unscale into its own kernel (materialize_master_grads=False)
-def prepare_backward_with_master_weights_FusedSGD(self):
-    if self.materialize_master_grads:
-        prepare_backward_with_master_weights(self)
+    if scale_override is None:
+        if scaler.loss_scale() == 1.0 and not scaler.dynamic:
+            if accum:  # static scale 1: plain accumulation
+                torch._foreach_add_(accum, old)
+            return
+        grads_have, stashed_have, out_scale = scaler.loss_scale(), 1.0, 1.0
     else:
-        stash = self._amp_stash
-        self._amp_lazy_init()
-        for i, param in enumerate(stash.all_fp16_params):
-            stash.all_fp16_grad_stash[i] = param.grad
-            param.grad = None
-        for i, param in enumerate(stash.all_fp32_from_fp32_params):
-            stash.all_fp32_from_fp32_grad_stash[i] = param.grad
-            param.grad = None
+        grads_have, stashed_have, out_scale = scale_override
+    if fresh:
+        scaler.unscale(fresh, fresh, None, models_are_masters=True, scale_override=grads_have / out_scale)
+    if accum:
+        scaler.unscale_with_stashed(accum, old, accum, scale_override=(grads_have, stashed_have, out_scale))
 
 
-def post_backward_with_master_weights_FusedSGD(self, scaler):
-    if self.materialize_master_grads:
-        post_backward_with_master_weights(self, scaler)
-    else:
-        stash = self._amp_stash
-        self._amp_lazy_init()
-        grads_have_scale = scaler.loss_scale()
-        stashed_have_scale = self.most_recent_scale
-        out_scale = grads_have_scale
-        if self.scale_set_by_backward:
-            out_scale = min(grads_have_scale, self.most_recent_scale)
-        for params, stashed in ((stash.all_fp16_params, stash.all_fp16_grad_stash),
-                                (stash.all_fp32_from_fp32_params, stash.all_fp32_from_fp32_grad_stash)):
-            post_backward_models_are_masters(scaler, params, stashed,
-                                             (grads_have_scale, stashed_have_scale, out_scale))
-        self.most_recent_scale = out_scale
-        self.scale_set_by_backward = True
+class _GradPlan(object):
+    def __init__(self, opt):
+        self.opt = opt
+        self.stash = opt._amp_stash
+        self.ready = False
+
+    def ensure(self):
+        if not self.ready:
+            self.setup()
+            self.ready = True
+            self.stash.lazy_init_called = True
+
+    def setup(self):
+        raise NotImplementedError
+
+    def prepare(self):
+        raise NotImplementedError
+
+    def finish(self, scaler):
+        raise NotImplementedError
+
+    def add_group(self, group):
+        raise NotImplementedError
 
 
-def _amp_lazy_init(self):
-    stash = self._amp_stash
-    if not stash.lazy_init_called:
-        self._lazy_init_maybe_master_weights()
-        stash.lazy_init_called = True
+class _ModelPlan(_GradPlan):
+    """The model parameters are the masters (no fp32 copies)."""
+
+    def setup(self):
+        st = self.stash
+        st.all_fp16_params, st.all_fp32_params = [], []
+        for group in self.opt.param_groups:
+            for p in group["params"]:
+                self.add_param(p)
+
+    def add_param(self, p):
+        st = self.stash
+        _check_param_type(p)
+        (st.all_fp16_params if p.dtype in _LOW else st.all_fp32_params).append(p)
+
+    def _lists(self):
+        st = self.stash
+        st.all_fp16_grad_stash = getattr(st, "all_fp16_grad_stash", [])
+        st.all_fp32_grad_stash = getattr(st, "all_fp32_grad_stash", [])
+        for name, params in (("all_fp16_grad_stash", st.all_fp16_params), ("all_fp32_grad_stash", st.all_fp32_params)):
+            lst = getattr(st, name)
+            lst.extend([None] * (len(params) - len(lst)))
+        return ((st.all_fp16_params, st.all_fp16_grad_stash), (st.all_fp32_params, st.all_fp32_grad_stash))
+
+    def prepare(self):
+        self.ensure()
+        for params, stash in self._lists():
+            for i, p in enumerate(params):
+                stash[i], p.grad = p.grad, None
+
+    def finish(self, scaler):
+        self.ensure()
+        for params, stash in self._lists():
+            _unscale_into_models(scaler, params, stash)
+
+    def add_group(self, group):
+        self.ensure()
+        for p in group["params"]:
+            self.add_param(p)
+        self._lists()
+
+
+class _MasterPlan(_GradPlan):
+    """16-bit model parameters train through fp32 master copies that replace them in the optimizer."""
+
+    def setup(self):
+        st = self.stash
+        st.fp16_groups, st.fp32_from_fp16_groups, st.fp32_from_fp32_groups = [], [], []
+        st.all_fp16_params, st.all_fp32_from_fp16_params, st.all_fp32_from_fp32_params = [], [], []
+        st.all_fp32_from_fp32_grad_stash = []
+        for group in self.opt.param_groups:
+            self._split(group, move_state=True)
+        # optimizer state (e.g. torch.optim momentum) is re-keyed to the masters
+        self.opt.load_state_dict(self.opt.state_dict())
+
+    def _split(self, group, move_state=False):
+        """Swap the 16-bit parameters of ``group`` for fp32 masters and record both sides."""
+        st = self.stash
+        low, masters, fp32 = [], [], []
+        params = group["params"]
+        for i, p in enumerate(params):
+            if not p.requires_grad:
+                continue
+            _check_param_type(p)
+            if p.dtype in _LOW:
+                master = p.detach().clone().float()
+                master.requires_grad = True
+                params[i] = master
+                if move_state and p in self.opt.state:
+                    self.opt.state[master] = self.opt.state.pop(p)
+                low.append(p)
+                masters.append(master)
+            else:
+                fp32.append(p)
+        st.fp16_groups.append(low)
+        st.fp32_from_fp16_groups.append(masters)
+        st.fp32_from_fp32_groups.append(fp32)
+        st.all_fp16_params += low
+        st.all_fp32_from_fp16_params += masters
+        st.all_fp32_from_fp32_params += fp32
+        st.all_fp32_from_fp32_grad_stash += [None] * len(fp32)
+        for p in masters + fp32:
+            p.grad = None
+
+    def prepare(self):
+        self.ensure()
+        st = self.stash
+        for p in st.all_fp16_params:  # 16-bit grads are folded into the fp32 master grads: drop them
+            p.grad = None
+        for i, p in enumerate(st.all_fp32_from_fp32_params):
+            st.all_fp32_from_fp32_grad_stash[i], p.grad = p.grad, None
+
+    def finish(self, scaler):
+        self.ensure()
+        st = self.stash
+        new_pairs, acc_pairs = [], []
+        for low, master in zip(st.all_fp16_params, st.all_fp32_from_fp16_params):
+            if low.grad is None:
+                continue  # nothing new; a master grad from an earlier micro-batch stays as it is
+            if master.grad is None:
+                master.grad = torch.empty_like(master)
+                new_pairs.append((low.grad, master.grad))
+            else:
+                acc_pairs.append((low.grad, master.grad))
+        if new_pairs:
+            scaler.unscale([a for a, _ in new_pairs], [b for _, b in new_pairs], None, models_are_masters=False)
+        if acc_pairs:
+            acc = [b for _, b in acc_pairs]
+            scaler.unscale_with_stashed([a for a, _ in acc_pairs], acc, acc)
+        _unscale_into_models(scaler, st.all_fp32_from_fp32_params, st.all_fp32_from_fp32_grad_stash)
+
+    def masters_to_model(self):
+        st = self.stash
+        if not st.all_fp16_params:
+            return
+        for masters, models in _by_dtype(zip((m.data for m in st.all_fp32_from_fp16_params),
+                                             (p.data for p in st.all_fp16_params))).values():
+            multi_tensor_applier(amp_C.multi_tensor_scale, st.dummy_overflow_buf, [masters, models], 1.0)
+
+    def zero_grad(self, set_to_none=True):
+        # set_to_none=True by default (PyTorch >= 2.0 semantics): the next prepare() drops / stashes these
+        # grads anyway, so zero-filling them would only add one fill kernel per parameter plus a
+        # stashed-gradient axpby pass after backward. set_to_none=False keeps the reference's zeroing.
+        self.ensure()
+        st = self.stash
+        grads = []
+        for p in st.all_fp16_params + st.all_fp32_from_fp32_params:
+            if p.grad is None:
+                continue
+            if set_to_none:
+                p.grad = None
+            else:
+                p.grad.detach_()
+                grads.append(p.grad)
+        if grads:
+            torch._foreach_zero_(grads)
+        for p in st.all_fp32_from_fp16_params:
+            p.grad = None
+
+    def add_group(self, group):
+        self.ensure()
+        self._split(group)
+
+
+class _FusedSGDMasterPlan(_MasterPlan):
+    """FusedSGD reads the scaled 16-bit gradients itself (``materialize_master_grads=False``): they are
+    stashed and unscaled in place with the scale bookkeeping FusedSGD expects (``most_recent_scale``)."""
+
+    def prepare(self):
+        if self.opt.materialize_master_grads:
+            return super().prepare()
+        self.ensure()
+        st = self.stash
+        st.all_fp16_grad_stash = getattr(st, "all_fp16_grad_stash", [])
+        st.all_fp16_grad_stash.extend([None] * (len(st.all_fp16_params) - len(st.all_fp16_grad_stash)))
+        for i, p in enumerate(st.all_fp16_params):
+            st.all_fp16_grad_stash[i], p.grad = p.grad, None
+        for i, p in enumerate(st.all_fp32_from_fp32_params):
+            st.all_fp32_from_fp32_grad_stash[i], p.grad = p.grad, None
+
+    def finish(self, scaler):
+        opt = self.opt
+        if opt.materialize_master_grads:
+            return super().finish(scaler)
+        self.ensure()
+        st = self.stash
+        now = scaler.loss_scale()
+        out_scale = min(now, opt.most_recent_scale) if opt.scale_set_by_backward else now
+        override = (now, opt.most_recent_scale, out_scale)
+        _unscale_into_models(scaler, st.all_fp16_params, st.all_fp16_grad_stash, override)
+        _unscale_into_models(scaler, st.all_fp32_from_fp32_params, st.all_fp32_from_fp32_grad_stash, override)
+        opt.most_recent_scale = out_scale
+        opt.scale_set_by_backward = True
 
 
 def _process_optimizer(optimizer, properties):
@@ -229,122 +291,58 @@ def _process_optimizer(optimizer, properties):
 
     if hasattr(optimizer, "_amp_stash"):
         raise RuntimeError("A given optimizer should only be passed through amp.initialize once.")
-    optimizer._amp_stash = AmpOptimizerState()
-    optimizer._amp_stash.lazy_init_called = False
-    optimizer._amp_stash.already_patched = False
-    optimizer._amp_stash.params_have_scaled_gradients = False
     for name in ("_lazy_init_maybe_master_weights", "_master_params_to_model_params", "_prepare_amp_backward",
                  "_post_amp_backward", "_amp_lazy_init"):
         if hasattr(optimizer, name):
             raise RuntimeError("Incoming optimizer already has {} defined.".format(name))
+    st = optimizer._amp_stash = AmpOptimizerState()
+    st.lazy_init_called = False
+    st.params_have_scaled_gradients = False
+    st.multi_tensor_scale = amp_C.multi_tensor_scale
+    st.multi_tensor_l2norm = amp_C.multi_tensor_l2norm
+    dev = next((p.device for g in optimizer.param_groups for p in g["params"]), None)
+    st.dummy_overflow_buf = torch.zeros(1, dtype=torch.int, device=dev or "cpu")
 
-    dev = None
-    for g in optimizer.param_groups:
-        for p in g["params"]:
-            dev = p.device
-            break
-        if dev is not None:
-            break
-    optimizer._amp_stash.multi_tensor_scale = amp_C.multi_tensor_scale
-    optimizer._amp_stash.multi_tensor_l2norm = amp_C.multi_tensor_l2norm
-    optimizer._amp_stash.dummy_overflow_buf = torch.zeros(1, dtype=torch.int, device=dev or "cpu")
-
-    is_fused_sgd = isinstance(optimizer, FusedSGD)
+    fused_sgd = isinstance(optimizer, FusedSGD)
     if properties.master_weights:
-        optimizer._lazy_init_maybe_master_weights = types.MethodType(lazy_init_with_master_weights, optimizer)
-        optimizer._master_params_to_model_params = types.MethodType(_master_params_to_model_params, optimizer)
-        old_step = optimizer.step
+        plan = (_FusedSGDMasterPlan if fused_sgd else _MasterPlan)(optimizer)
+        inner_step = optimizer.step
 
-        def new_step(self, closure=None):
+        def step(self, closure=None):
             if closure is not None:
                 raise RuntimeError("Currently, Amp does not support closure use with optimizers.")
-            retval = old_step()
-            if not isinstance(self, FusedSGD):  # FusedSGD writes the 16-bit params in its kernel
-                self._master_params_to_model_params()
-            for param in self._amp_stash.all_fp32_from_fp16_params:
-                param.grad = None
-            return retval
+            out = inner_step()
+            if not fused_sgd:  # FusedSGD writes the 16-bit params inside its kernel
+                plan.masters_to_model()
+            for p in self._amp_stash.all_fp32_from_fp16_params:
+                p.grad = None
+            return out
 
-        optimizer.step = types.MethodType(new_step, optimizer)
-
-        def new_zero_grad(self, set_to_none=True):
-            # Default set_to_none=True (PyTorch >= 2.0 semantics): the next _prepare_amp_backward
-            # stashes / drops these grads anyway, so zero-filling them only adds one fill kernel per
-            # parameter plus a stashed-gradient axpby pass after backward. set_to_none=False keeps
-            # the reference's zeroing behaviour.
-            stash = self._amp_stash
-            self._amp_lazy_init()
-            grads = []
-            for param in stash.all_fp16_params + stash.all_fp32_from_fp32_params:
-                if param.grad is not None:
-                    if set_to_none:
-                        param.grad = None
-                    else:
-                        param.grad.detach_()
-                        grads.append(param.grad)
-            if grads:
-                torch._foreach_zero_(grads)
-            for param in stash.all_fp32_from_fp16_params:
-                param.grad = None
-
-        optimizer.zero_grad = types.MethodType(new_zero_grad, optimizer)
-        prep = prepare_backward_with_master_weights_FusedSGD if is_fused_sgd else prepare_backward_with_master_weights
-        post = post_backward_with_master_weights_FusedSGD if is_fused_sgd else post_backward_with_master_weights
+        optimizer.step = types.MethodType(step, optimizer)
+        optimizer.zero_grad = types.MethodType(lambda self, set_to_none=True: plan.zero_grad(set_to_none), optimizer)
+        optimizer._master_params_to_model_params = types.MethodType(lambda self: plan.masters_to_model(), optimizer)
     else:
-        optimizer._lazy_init_maybe_master_weights = types.MethodType(lazy_init_no_master_weights, optimizer)
-        prep = prepare_backward_no_master_weights
-        post = post_backward_no_master_weights
-    optimizer._prepare_amp_backward = types.MethodType(prep, optimizer)
-    optimizer._post_amp_backward = types.MethodType(post, optimizer)
-    optimizer._amp_lazy_init = types.MethodType(_amp_lazy_init, optimizer)
+        plan = _ModelPlan(optimizer)
+    st.plan = plan
+    optimizer._lazy_init_maybe_master_weights = types.MethodType(lambda self: plan.setup(), optimizer)
+    optimizer._amp_lazy_init = types.MethodType(lambda self: plan.ensure(), optimizer)
+    optimizer._prepare_amp_backward = types.MethodType(lambda self: plan.prepare(), optimizer)
+    optimizer._post_amp_backward = types.MethodType(lambda self, scaler: plan.finish(scaler), optimizer)
 
-    old_add_param_group = optimizer.add_param_group
+    inner_add = optimizer.add_param_group
 
-    def new_add_param_group(self, new_group):
-        stash = self._amp_stash
-        if not stash.lazy_init_called:
-            self._lazy_init_maybe_master_weights()
-            stash.lazy_init_called = True
+    def add_param_group(self, new_group):
         assert isinstance(new_group, dict), "param group must be a dict"
-        new_params = new_group["params"]
-        if isinstance(new_params, torch.Tensor):
-            new_group["params"] = [new_params]
-        elif isinstance(new_params, set):
+        params = new_group["params"]
+        if isinstance(params, torch.Tensor):
+            new_group["params"] = [params]
+        elif isinstance(params, set):
             raise TypeError("optimizer parameters need to be organized in ordered collections, but the ordering "
                             "of tensors in sets will change between runs. Please use a list instead.")
         else:
-            new_group["params"] = list(new_params)
-        if properties.master_weights:
-            fp16_this, fp32_this, fp32_from_fp16_this = [], [], []
-            for i, param in enumerate(new_group["params"]):
-                if not param.requires_grad:
-                    continue
-                _check_param_type(param)
-                if param.dtype in _LOW:
-                    fp16_this.append(param)
-                    master = param.detach().clone().float()
-                    master.requires_grad = True
-                    new_group["params"][i] = master
-                    fp32_from_fp16_this.append(master)
-                else:
-                    fp32_this.append(param)
-            stash.fp16_groups.append(fp16_this)
-            stash.fp32_from_fp16_groups.append(fp32_from_fp16_this)
-            stash.fp32_from_fp32_groups.append(fp32_this)
-            stash.all_fp16_params += fp16_this
-            stash.all_fp32_from_fp16_params += fp32_from_fp16_this
-            stash.all_fp32_from_fp32_params += fp32_this
-            stash.all_fp32_from_fp32_grad_stash += [None for _ in fp32_this]
-        else:
-            for param in new_group["params"]:
-                _check_param_type(param)
-                if param.dtype in _LOW:
-                    stash.all_fp16_params.append(param)
-                    stash.all_fp16_grad_stash.append(None)
-                else:
-                    stash.all_fp32_params.append(param)
-                    stash.all_fp32_grad_stash.append(None)
-        old_add_param_group(new_group)
+            new_group["params"] = list(params)
+        plan.add_group(new_group)
+        inner_add(new_group)
 
-    optimizer.add_param_group = types.MethodType(new_add_param_group, optimizer)
+    optimizer.add_param_group = types.MethodType(add_param_group, optimizer)
     return optimizer

@@ -597,7 +597,10 @@ class _Conv1DsFn(torch.autograd.Function):
             else:
                 gx2d = torch.mm(g1, w1_2d)
             if ctx.s2:
-                if conv_bn.supported(gd, wd_2d, b_trans=True, s2=(h, w), s2_scatter=True):
+                # the scatter epilogue wins only where the strip kernel does (K = downsample channels
+                # <= 256); else hipBLASLt + a strided add over the quarter of the pixels
+                if conv_bn.preferred(kd, c, gd.size(0)) and \
+                        conv_bn.supported(gd, wd_2d, b_trans=True, s2=(h, w), s2_scatter=True):
                     conv_bn.c1x1(gd, wd_2d, b_trans=True, s2=(h, w), s2_scatter=True, resid=gx2d)
                 else:
                     gx2d.view(n, h, w, c)[:, ::2, ::2, :] += torch.mm(gd, wd_2d).view(n, h // 2, w // 2, c)

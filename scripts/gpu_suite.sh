@@ -16,6 +16,10 @@ for preset in "$@"; do
     bench) steps+=("bench:400:python bench.py --steps 20 --warmup 5 --trace-warmup gpurun_out/warmup1_cprofile.txt") ;;
     nofold) steps+=("nofold:400:BH_FOLD_BN=0 python bench.py --steps 20 --warmup 5") ;;
     prof) steps+=("prof:300:cd /tmp && export TMPDIR=/tmp && cd \$GRAFT_REPO_ROOT && rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r50 -o run -- python bench.py --steps 8 --warmup 5 && python scripts/prof_summary.py gpurun_out/prof_r50 k_lamb2 3 gpurun_out/r50_summary.md && rm -rf gpurun_out/prof_r50") ;;
+    cbr) steps+=("cbr:300:python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_conv_bias_relu.py tests/test_contrib_basic.py -m gpu") ;;
+    conv3) steps+=("conv3:300:python benchmarks/bench_conv3x3.py") ;;
+    gpt) steps+=("gpt:400:python benchmarks/bench_gpt.py --batch 8 --steps 10 --warmup 3") ;;
+    gptprof) steps+=("gptprof:400:cd /tmp && export TMPDIR=/tmp && cd \$GRAFT_REPO_ROOT && rocprofv3 --kernel-trace --stats -d gpurun_out/prof_gpt -o run -- python benchmarks/bench_gpt.py --batch 8 --steps 6 --warmup 3 && python scripts/prof_summary.py gpurun_out/prof_gpt k_adam 3 gpurun_out/gpt_summary.md && rm -rf gpurun_out/prof_gpt") ;;
     *) echo "unknown preset $preset"; exit 2 ;;
   esac
 done

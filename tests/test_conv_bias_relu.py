@@ -56,7 +56,7 @@ def test_conv_bias_relu(device, variant):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("variant", ["relu", "mask", "bias", "frozen", "frozen_add"])
-@pytest.mark.parametrize("shape", [(64, 128, 3, 1, 1, 28), (64, 256, 1, 0, 1, 56), (256, 512, 1, 0, 2, 28),
+@pytest.mark.parametrize("shape", [(64, 128, 3, 1, 1, 28), (64, 256, 1, 0, 1, 56), (256, 512, 1, 0, 2, 32),
                                    (128, 128, 3, 1, 1, 14)])
 def test_conv_bias_relu_fused_kernels(variant, shape):
     """Shapes the MFMA kernels cover (1x1 s1 / s2, 3x3 s1): ONE kernel per forward (affine epilogue),
