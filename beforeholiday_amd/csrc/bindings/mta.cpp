@@ -76,7 +76,11 @@ const MTAPlan& get_plan(const std::vector<std::vector<at::Tensor>>& lists, int64
   if (it != g_plans.end()) return it->second;
 
   hipStream_t stream = stream_for(lists[0][0]);
-  if (g_plans.size() >= kMaxPlans && !capturing(stream)) g_plans.clear();
+  // a plan recorded into a HIP graph must outlive the graph: once anything was captured the cache
+  // only grows (a captured training step creates no new plans when replayed)
+  static bool captured = false;
+  captured = captured || capturing(stream);
+  if (g_plans.size() >= kMaxPlans && !captured) g_plans.clear();
 
   // chunk schedule
   std::vector<int> chunk0(T + 1, 0);
@@ -96,7 +100,10 @@ const MTAPlan& get_plan(const std::vector<std::vector<at::Tensor>>& lists, int64
   const size_t o_cl = align_up(o_ct + sizeof(int) * C, 16);
   const size_t bytes = align_up(o_cl + sizeof(int) * C, 16) + 16;
 
-  at::Tensor host = at::empty({(int64_t)bytes}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  const bool in_capture = capturing(stream);
+  // pinned staging + async copy normally; while capturing (pinned allocation is not allowed then) a
+  // pageable table uploaded through kernel arguments
+  at::Tensor host = at::empty({(int64_t)bytes}, at::TensorOptions().dtype(at::kByte).pinned_memory(!in_capture));
   uint8_t* h = host.data_ptr<uint8_t>();
   auto* hp = reinterpret_cast<uint64_t*>(h + o_ptrs);
   auto* hn = reinterpret_cast<int64_t*>(h + o_numel);
@@ -122,7 +129,8 @@ const MTAPlan& get_plan(const std::vector<std::vector<at::Tensor>>& lists, int64
     }
 
   at::Tensor devbuf = at::empty({(int64_t)bytes}, lists[0][0].options().dtype(at::kByte));
-  devbuf.copy_(host, /*non_blocking=*/true);
+  if (in_capture) bh::upload_bytes(devbuf.data_ptr(), host.data_ptr(), bytes, stream);
+  else devbuf.copy_(host, /*non_blocking=*/true);
 
   MTAPlan plan;
   plan.dev = devbuf;

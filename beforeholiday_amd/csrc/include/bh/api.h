@@ -40,6 +40,9 @@ struct MTAView {
 };
 
 // scale_dev (optional): device fp32 scalar used instead of `scale`
+// copy a small host table (multiple of 16 bytes) to the device as kernel arguments: legal while the
+// stream is being captured into a HIP graph (no staging buffer, no memcpy node)
+void upload_bytes(void* dst, const void* src, size_t bytes, hipStream_t s);
 void mta_scale(const MTAView& v, int dt_in, int dt_out, float scale, int* noop, hipStream_t s,
                const float* scale_dev = nullptr);
 void mta_axpby(const MTAView& v, int dt_x, int dt_y, int dt_out, float a, float b, int arg_to_check,

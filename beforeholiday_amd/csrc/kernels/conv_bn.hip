@@ -12,7 +12,10 @@
 // next strip's rows are loaded while the current strip's epilogue runs.
 //
 // Epilogue: lane holds C[8 j + 4 h + i][32 t + r] in acc[t][4 j + i], i.e. ONE column per 32-column
-// tile, 16 rows of it. Each store writes two 64-byte row segments. The per-column statistics are
+// tile, 16 rows of it. The rounded values go through a wave-private 16 x 64 LDS tile (adjacent lanes
+// swap one value so each writes 32-bit words) and leave as 128-byte row segments: NC / 16 stores per strip, so
+// the vmcnt wait for the next strip's A rows does not have to drain the stores (vmcnt counts both on
+// gfx9; 2-byte column stores were NC * 2 per strip, past vmcnt's range). The per-column statistics are
 // accumulated per lane across all strips the wave processes (2 floats per tile), then reduced over the
 // lane halves, the 4 waves (LDS) and written as one partial row per workgroup: deterministic, no
 // atomics, and the statistics of an 800k-row output cost one extra read of nothing.
@@ -49,6 +52,7 @@ template <> struct Mf<bf16> {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
+constexpr int kStageBytes = 16 * 128;  // per wave: 16 rows x 64 fp16 columns of output
 
 struct Geo {
   int nslices;  // column slices of NC
@@ -56,6 +60,7 @@ struct Geo {
   int strips;   // M / 32
   int ss_off;   // LDS byte offset of the prologue scale / shift
   int red_off;  // LDS byte offset of the cross-wave reduction buffer
+  int stage_off;  // LDS byte offset of the output staging tiles (kStageBytes per wave)
 };
 
 // S2: 0 none, 1 stride-2 gather of the A rows, 2 stride-2 scatter of the C rows (output row (n, y, x)
@@ -159,6 +164,38 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
 #pragma unroll
     for (int s = 0; s < KS; ++s) a[s] = __builtin_nontemporal_load(reinterpret_cast<const i4v*>(src + 16 * s));
   };
+  // Output staging (all but the scatter variant): the lane-per-column MFMA result leaves as 128-byte
+  // row segments (whole cache lines: 64-byte half lines measured ~20% slower on the HBM-bound shapes)
+  // through a wave-private [16 rows][64 columns] LDS tile. A pair of 32-column tiles fills it twice --
+  // rows 0-15 (j < 2 of both tiles), then rows 16-31; the even tile's upper rows wait in 4 registers
+  // until the odd tile is done with its lower ones. A strip of 32 x NC outputs leaves in NC / 16
+  // dwordx4 stores instead of NC * 2 2-byte ones: few enough that the next strip's loads are waited
+  // for precisely (vmcnt counts stores too on gfx9) instead of draining every store of the strip.
+  // Rows 4 apart (the two lane halves) are XOR-swizzled by half a row: conflict-free 32-bit writes.
+  char* stage = smem + g.stage_off + wave * kStageBytes;
+  auto put = [&](int row, int half_col, unsigned int word) __attribute__((always_inline)) {
+    const int rr = row & 15, wd = half_col * 16 + (r >> 1);
+    *reinterpret_cast<unsigned int*>(stage + rr * 128 + 4 * (wd ^ (((rr >> 2) & 1) << 4))) = word;
+  };
+  auto flush = [&](int strip, int pair, int half) __attribute__((always_inline)) {
+    const int ch = lane & 7;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int rr = 8 * q + (lane >> 3);
+      const i4v v = *reinterpret_cast<const i4v*>(stage + rr * 128 + 16 * (ch ^ (((rr >> 2) & 1) << 2)));
+      *reinterpret_cast<i4v*>(Cp + ((int64_t)strip * 32 + 16 * half + rr) * N + col0 + 64 * pair + ch * 8) = v;
+    }
+  };
+  // the lane pair (r, r ^ 1) swaps one value of rows v - 1, v (v odd) so that each lane holds one
+  // 32-bit word of two adjacent columns: the even lane row v - 1's, the odd lane row v's
+  auto pair_word = [&](int v, unsigned int o_even, unsigned int o_odd, int* row) __attribute__((always_inline)) {
+    const bool odd = r & 1;
+    const unsigned int keep = odd ? o_odd : o_even, send = odd ? o_even : o_odd;
+    const unsigned int got = (unsigned int)__builtin_amdgcn_mov_dpp((int)send, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    const int vv = odd ? v : v - 1;
+    *row = 8 * (vv >> 2) + 4 * h + (vv & 3);
+    return odd ? (got | (keep << 16)) : (keep | (got << 16));
+  };
   f16v acc[NT];
   auto process = [&](int i, i4v(&a)[KS]) {
     const int q = i / nch, c = i - q * nch;
@@ -198,30 +235,34 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
     if (c + 1 < nch) return;
     // ---- epilogue ----
     const int64_t row0 = (int64_t)strip * 32 + 4 * h;
-    // output rows of this lane (the scatter maps them once per strip, shared by every column tile)
-    int64_t orow[16];
+    // output rows of this lane: the scatter maps them once per strip (shared by every column tile);
+    // otherwise row v is row0 + 8 (v >> 2) + (v & 3)
+    int64_t orow[S2 == 2 ? 16 : 1];
+    auto out_row = [&](int v) -> int64_t {
+      if constexpr (S2 == 2) return orow[v];
+      else return row0 + 8 * (v >> 2) + (v & 3);
+    };
 #pragma unroll
-    for (int v = 0; v < 16; ++v) {
+    for (int v = 0; v < (S2 == 2 ? 16 : 0); ++v) {
       const int64_t m = row0 + 8 * (v >> 2) + (v & 3);
-      if constexpr (S2 == 2) {
-        const int Wo = p.s2_W >> 1, HWo = (p.s2_H >> 1) * Wo;
-        const int64_t n = m / HWo;
-        const int rem = (int)(m - n * HWo), yo = rem / Wo, xo = rem - yo * Wo;
-        orow[v] = (n * p.s2_H + 2 * yo) * p.s2_W + 2 * xo;
-      } else {
-        orow[v] = m;
-      }
+      const int Wo = p.s2_W >> 1, HWo = (p.s2_H >> 1) * Wo;
+      const int64_t n = m / HWo;
+      const int rem = (int)(m - n * HWo), yo = rem / Wo, xo = rem - yo * Wo;
+      orow[v] = (n * p.s2_H + 2 * yo) * p.s2_W + 2 * xo;
     }
+    unsigned int held[4];  // the even tile's rows 16-31 (see the staging note above)
+    int held_row[4];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int col = col0 + 32 * t + r;
+      unsigned int o_prev = 0;
       float xr[16];
       if constexpr (RES || EPI == kC1x1Bwd) {
         const T* src = RES ? Rp : Yp;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) xr[4 * j + i] = to_f<T>(src[orow[4 * j + i] * N + col]);
+          for (int i = 0; i < 4; ++i) xr[4 * j + i] = to_f<T>(src[out_row(4 * j + i) * N + col]);
       }
       float bsc = 0.f, bsh = 0.f, bmn = 0.f;
       if constexpr (EPI == kC1x1Bwd || EPI == kC1x1Affine) {
@@ -234,7 +275,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) yv[4 * j + i] = to_f<T>(Yp[orow[4 * j + i] * N + col]);
+          for (int i = 0; i < 4; ++i) yv[4 * j + i] = to_f<T>(Yp[out_row(4 * j + i) * N + col]);
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -256,7 +297,31 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
             x += xr[v];
           }
           const T o = from_f<T>(x);
-          Cp[orow[v] * N + col] = o;
+          if constexpr (S2 == 2) {
+            Cp[out_row(v) * N + col] = o;
+          } else {
+            const unsigned int ou = __builtin_bit_cast(unsigned short, o);
+            if (v & 1) {
+              int row;
+              const unsigned int w = pair_word(v, o_prev, ou, &row);
+              if (v < 8) {
+                put(row, t & 1, w);
+              } else if (!(t & 1)) {
+                held[(v - 8) >> 1] = w;
+                held_row[(v - 8) >> 1] = row;
+              } else {
+                put(row, 1, w);
+              }
+              if ((t & 1) && v == 7) {  // rows 0-15 of the pair complete: out, then the held rows in
+                flush(strip, t >> 1, 0);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) put(held_row[k], 0, held[k]);
+              }
+              if ((t & 1) && v == 15) flush(strip, t >> 1, 1);
+            } else {
+              o_prev = ou;
+            }
+          }
           const float f = to_f<T>(o);  // statistics of the value as stored
           if constexpr (EPI == kC1x1Stats) {
             const float d = f - e0[t];
@@ -285,7 +350,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
   }
 
   if constexpr (EPI == kC1x1Stats || EPI == kC1x1Bwd) {
-    float* red = reinterpret_cast<float*>(smem + g.red_off);  // [waves][2][NC]
+    float* red = reinterpret_cast<float*>(smem + g.red_off);  // [waves][2][NC], aliases the staging tiles
+    __syncthreads();
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       s1[t] += __shfl_xor(s1[t], 32);
@@ -342,24 +408,25 @@ struct Plan {
 
 int ss_bytes(int NC, int K, bool pro, bool bwd, bool aff) { return pro ? 8 * K : (bwd ? 12 * NC : (aff ? 8 * NC : 0)); }
 
-int lds_bytes(int NC, int K, bool pro, bool bwd, bool aff, bool stats) {
-  int b = NC * (2 * K + 16) + ss_bytes(NC, K, pro, bwd, aff);
-  if (stats) b += kWaves * 2 * NC * 4;
-  return b;
+int lds_bytes(int NC, int K, bool pro, bool bwd, bool aff, bool stats, bool scatter) {
+  // the statistics reduction buffer (used after the strip loop) aliases the output staging tiles
+  return NC * (2 * K + 16) + ss_bytes(NC, K, pro, bwd, aff) +
+         std::max(stats ? kWaves * 2 * NC * 4 : 0, scatter ? 0 : kWaves * kStageBytes);
 }
 
 bool make_plan(const C1x1Args& a, Plan* pl) {
   if (a.K <= 0 || a.N <= 0 || a.M <= 0 || a.K % 64 != 0 || a.N % 64 != 0 || a.M % 32 != 0) return false;
   if (a.M / 32 >= (1ll << 31)) return false;
   const bool pro = a.pro_scale != nullptr, stats = a.epi == kC1x1Stats || a.epi == kC1x1Bwd,
-             bwd = a.epi == kC1x1Bwd, aff = a.epi == kC1x1Affine;
+             bwd = a.epi == kC1x1Bwd, aff = a.epi == kC1x1Affine, scatter = a.s2_H > 0 && a.s2_scatter;
   // register budget: the backward epilogue (input loads + statistics) fits 4 column tiles per wave
   const int max_nc = bwd ? (a.R ? 64 : 128) : 256;
   int NC = 0, occ = 0;
   // the widest column slice (A read once per slice) that still leaves two workgroups per CU; else one
   for (int want_occ = 2; want_occ >= 1 && !NC; --want_occ)
     for (int nc : {256, 128, 64})
-      if (nc <= max_nc && a.N % nc == 0 && lds_bytes(nc, a.K, pro, bwd, aff, stats) <= 160 * 1024 / want_occ) {
+      if (nc <= max_nc && a.N % nc == 0 &&
+          lds_bytes(nc, a.K, pro, bwd, aff, stats, scatter) <= 160 * 1024 / want_occ) {
         NC = nc;
         occ = want_occ;
         break;
@@ -375,9 +442,10 @@ bool make_plan(const C1x1Args& a, Plan* pl) {
   g.G = (std::min(want, cap) + 7) / 8 * 8;
   g.ss_off = NC * (2 * a.K + 16);
   g.red_off = g.ss_off + ss_bytes(NC, a.K, pro, bwd, aff);
+  g.stage_off = g.red_off;
   pl->NC = NC;
   pl->KC = KC;
-  pl->lds = lds_bytes(NC, a.K, pro, bwd, aff, stats);
+  pl->lds = lds_bytes(NC, a.K, pro, bwd, aff, stats, scatter);
   pl->occ = occ;
   pl->g = g;
   return true;

@@ -17,6 +17,7 @@
 #include "bh/api.h"
 #include "bh/device.h"
 
+#include <algorithm>
 #include <cmath>
 #include <stdexcept>
 #include <string>
@@ -670,6 +671,36 @@ void mta_lamb_stage2_standalone(const MTAView& v, int dt_p, int dt_u, const floa
       hipLaunchKernelGGL((k_lamb_s2<Tp, Tu>), dim3(v.C), dim3(kBlock), 0, s, v, pnorm, unorm, lr, decay,
                          use_nvlamb)));
   check_launch("multi_tensor_lamb_stage2_cuda");
+}
+
+// ---- graph-capture-safe upload of a small host table ---------------------------------------------
+// While a stream is being captured, a pinned staging buffer + async copy is not allowed; the bytes
+// travel instead as kernel arguments (captured by value into the graph node), up to 3.5 KiB per launch.
+namespace {
+constexpr int kUploadVecs = 224;
+struct UploadPayload {
+  uint4 d[kUploadVecs];
+};
+__global__ __launch_bounds__(256) void k_upload(uint4* __restrict__ dst, UploadPayload p, int n) {
+  const int i = threadIdx.x;
+  if (i < n) dst[i] = p.d[i];
+}
+}  // namespace
+
+void upload_bytes(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (bytes % 16 != 0 || reinterpret_cast<uintptr_t>(dst) % 16 != 0)
+    throw std::runtime_error("upload_bytes: 16-byte multiples / alignment only");
+  const uint4* in = reinterpret_cast<const uint4*>(src);
+  uint4* out = reinterpret_cast<uint4*>(dst);
+  const size_t nvec = bytes / 16;
+  for (size_t off = 0; off < nvec; off += kUploadVecs) {
+    UploadPayload p;
+    const int n = (int)std::min<size_t>(kUploadVecs, nvec - off);
+    for (int i = 0; i < n; ++i) p.d[i] = in[off + i];
+    hipLaunchKernelGGL(k_upload, dim3(1), dim3(256), 0, s, out + off, p, n);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("upload_bytes: ") + hipGetErrorString(e));
 }
 
 }  // namespace bh

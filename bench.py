@@ -86,6 +86,8 @@ def parse():
     ap.add_argument("--host-scaler", action="store_true",
                     help="dynamic loss scale read on the host every step (the reference's .item() per step); "
                          "default: device-resident scale, overflow skipped by the fused optimizer's noop flag")
+    ap.add_argument("--graph", default="off", choices=["off", "on"],
+                    help="replay the whole training step as one captured HIP graph (utils/graphs.py)")
     ap.add_argument("--conv3x3", default="auto", choices=["auto", "miopen", "direct"],
                     help="stride-1 3x3 convolution forward / data gradient: the direct MFMA kernel "
                          "(kernels/conv.hip), MIOpen, or the faster per shape (auto)")
@@ -195,12 +197,22 @@ def main():
         if rank == 0:
             print(f"[bench] warmup {i + 1}/{args.warmup}: {(time.perf_counter() - tw) * 1e3:.1f} ms",
                   file=sys.stderr, flush=True)
+    run = step
+    capture_ms = None
+    if args.graph == "on":
+        from beforeholiday_amd.utils import GraphedStep
+
+        run = GraphedStep(step, warmup=2).capture()
+        capture_ms = round(run.capture_ms, 1)
+        if rank == 0:
+            print(f"[bench] captured the step as a HIP graph in {capture_ms} ms", file=sys.stderr, flush=True)
+        run()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step()
+        loss = run()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -255,6 +267,7 @@ def main():
             "ddp_bucket_mb": buckets,
             "syncbn_stats": args.syncbn_stats,
             "loss_scaler": "host" if args.host_scaler else "device",
+            "hip_graph": args.graph == "on",
             "comm_ms_per_step": comm,
         }), flush=True)
     if world > 1:

@@ -4,6 +4,7 @@
   fwd   : hipBLASLt mm + the separate BatchNorm statistics pass  vs  c1x1 with the statistics epilogue
   pro   : BatchNorm-apply pass + hipBLASLt mm + statistics pass    vs  c1x1 with prologue + statistics
   dgrad : hipBLASLt mm + BatchNorm backward-reduce pass           vs  c1x1 with the backward epilogue
+          (weights read transposed, as in the data gradient)
   s2    : strided gather + mm + statistics                        vs  c1x1 stride-2 gather + statistics
 
 One JSON line per (shape, mode) with ms of both sides and the kernel's effective HBM TB/s
@@ -26,7 +27,10 @@ SHAPES = [
     (256, 128, 56, 56, "fwd"), (512, 128, 28, 28, "fwd"), (128, 512, 28, 28, "pro"),
     (512, 256, 28, 28, "fwd"), (1024, 256, 14, 14, "fwd"), (256, 1024, 14, 14, "pro"),
     (1024, 512, 14, 14, "fwd"), (512, 2048, 7, 7, "pro"),
+    (128, 512, 28, 28, "fwd"), (256, 1024, 14, 14, "fwd"), (512, 2048, 7, 7, "fwd"),
     (256, 64, 56, 56, "dgrad"), (512, 128, 28, 28, "dgrad"), (1024, 256, 14, 14, "dgrad"),
+    (64, 64, 56, 56, "dgrad"), (64, 256, 56, 56, "dgrad"), (128, 512, 28, 28, "dgrad"), (256, 1024, 14, 14, "dgrad"),
+    (512, 2048, 7, 7, "dgrad"), (2048, 512, 7, 7, "dgrad"),
     (64, 256, 56, 56, "plain"), (128, 512, 28, 28, "plain"), (256, 1024, 14, 14, "plain"), (512, 2048, 7, 7, "plain"),
     (256, 512, 56, 56, "s2"), (512, 1024, 28, 28, "s2"), (1024, 2048, 14, 14, "s2"),
 ]
@@ -90,14 +94,18 @@ def main():
                 return syncbn.backward_reduce(c.view(-1, H, W, N).permute(0, 3, 1, 2), x4, None, mn, mn, scn, shn,
                                               True, None, False)
 
-            ours = lambda: conv_bn.sum_parts(conv_bn.c1x1(a, b, epi="bwd", by=y, bscale=scn, bshift=shn,  # noqa: E731
-                                                          bmean=mn)[1])
+            bt = b.t().contiguous()  # the data gradient reads the forward weight [K, N] transposed
+
+            def ours():
+                return conv_bn.sum_parts(conv_bn.c1x1(a, bt, epi="bwd", by=y, bscale=scn, bshift=shn, bmean=mn,
+                                                      b_trans=True)[1])
             extra = M * N * 2
         else:  # s2
             ours = lambda: conv_bn.sum_parts(conv_bn.c1x1(a, b, s2=(H, W), epi="stats", kshift=rm)[1], M)  # noqa: E731
             base = lambda: stats(torch.mm(a.view(-1, H, W, K)[:, ::2, ::2].reshape(-1, K), b.t()))  # noqa: E731
             extra = 0
-        if not conv_bn.supported(a, b, pro=mode == "pro", s2=(H, W) if mode == "s2" else None,
+        if not conv_bn.supported(a, bt if mode == "dgrad" else b, pro=mode == "pro", s2=(H, W) if mode == "s2" else None,
+                                 b_trans=mode == "dgrad",
                                  epi={"fwd": "stats", "fwd_n64": "stats", "pro": "stats", "plain": "plain",
                                       "dgrad": "bwd", "s2": "stats"}[mode]):
             lines.append({"K": K, "N": N, "HW": H, "mode": mode, "supported": False})

@@ -7,6 +7,7 @@
 #   bench   : bench.py 1 GPU (20 steps), with a cProfile of warmup step 1
 #   prof    : rocprofv3 kernel trace of the bench + per-kernel summary (gpurun_out/r50_summary.md)
 #   nofold  : bench.py with BH_FOLD_BN=0 (A/B)
+#   graph   : bench.py with the whole step replayed as a HIP graph
 steps=()
 for preset in "$@"; do
   case "$preset" in
@@ -14,6 +15,9 @@ for preset in "$@"; do
     fold) steps+=("fold:400:python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_conv_bn.py tests/test_resnet_fold.py tests/test_ddp.py -m gpu") ;;
     micro) steps+=("micro:300:python benchmarks/bench_conv_bn.py --out gpurun_out/conv_bn_vs_unfused.jsonl") ;;
     bench) steps+=("bench:400:python bench.py --steps 20 --warmup 5 --trace-warmup gpurun_out/warmup1_cprofile.txt") ;;
+    graphtest) steps+=("graphtest:300:python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_graphs.py -m gpu") ;;
+    graphdiff) steps+=("graphdiff:300:python scripts/diag/graph_diff.py") ;;
+    graph) steps+=("graph:400:python bench.py --steps 20 --warmup 5 --graph on") ;;
     nofold) steps+=("nofold:400:BH_FOLD_BN=0 python bench.py --steps 20 --warmup 5") ;;
     prof) steps+=("prof:300:cd /tmp && export TMPDIR=/tmp && cd \$GRAFT_REPO_ROOT && rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r50 -o run -- python bench.py --steps 8 --warmup 5 && python scripts/prof_summary.py gpurun_out/prof_r50 k_lamb2 3 gpurun_out/r50_summary.md && rm -rf gpurun_out/prof_r50") ;;
     cbr) steps+=("cbr:300:python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_conv_bias_relu.py tests/test_contrib_basic.py -m gpu") ;;
