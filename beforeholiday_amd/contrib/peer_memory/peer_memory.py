@@ -35,7 +35,10 @@ class PeerMemoryPool(object):
     """``static_size`` + ``dynamic_size`` bytes per rank, shared with ``peer_ranks`` (default: the
     ranks of this node). ``allocate_peer_tensors`` returns one view per peer rank, all at the same offset."""
 
-    def __init__(self, static_size, dynamic_size, peer_ranks=None, group=None):
+    def __init__(self, static_size, dynamic_size, peer_ranks=None, group=None, consensus=False):
+        """``consensus=True``: a rank whose allocation / export / peer mapping fails does not raise
+        alone (which would leave its peers waiting in the handle exchange): every rank of ``group``
+        learns the outcome and all of them raise :class:`PeerSetupError` together."""
         rank = dist.get_rank()
         world = dist.get_world_size()
         if peer_ranks is None:
@@ -57,23 +60,49 @@ class PeerMemoryPool(object):
         self.peer_raw = None
         if self.native:
             pm = _pm()
-            self.raw = pm.allocate_raw(self.static_size + self.dynamic_size)
-            handle = pm.get_raw_ipc_address(self.raw).numpy().tobytes()
+            handle, failure = b"", ""
+            try:
+                self.raw = pm.allocate_raw(self.static_size + self.dynamic_size)
+                handle = pm.get_raw_ipc_address(self.raw).numpy().tobytes()
+            except Exception as e:  # noqa: BLE001 - reported to every rank below
+                if not consensus:
+                    raise
+                failure = repr(e)
             handles = [None] * world
             dist.all_gather_object(handles, handle, group=group)
+            bad = [r for r in self.peer_ranks if not handles[r]]
+            if bad:  # every rank sees the same gathered list: all of them raise here
+                self._release()
+                raise PeerSetupError(f"PeerMemoryPool: ranks {bad} could not export an IPC block"
+                                     + (f" ({failure})" if rank in bad else ""))
             table = torch.from_numpy(np.frombuffer(b"".join(handles[r] for r in self.peer_ranks), dtype=np.uint8)
                                      .reshape(len(self.peer_ranks), -1).copy())
-            self.peer_raw = pm.get_raw_peers(table, self.peer_rank, self.raw)
+            ok = True
+            try:
+                self.peer_raw = pm.get_raw_peers(table, self.peer_rank, self.raw)
+            except Exception:
+                if not consensus:
+                    raise
+                ok = False
+            if consensus and not agree(ok, group):
+                self._release()
+                raise PeerSetupError("PeerMemoryPool: a rank could not map its peers' IPC blocks")
         else:
             self._host = []
 
+    def _release(self):
+        pm = _pm()
+        if self.peer_raw is not None:
+            pm.close_raw_peers([p for i, p in enumerate(self.peer_raw) if i != self.peer_rank])
+            self.peer_raw = None
+        if self.raw is not None:
+            pm.free_raw(self.raw)
+            self.raw = None
+
     def __del__(self):
         try:
-            if self.native and self.raw is not None:
-                pm = _pm()
-                pm.close_raw_peers([p for i, p in enumerate(self.peer_raw) if i != self.peer_rank])
-                pm.free_raw(self.raw)
-                self.raw = None
+            if self.native:
+                self._release()
         except Exception:
             pass
 
@@ -107,6 +136,20 @@ class PeerMemoryPool(object):
 
 class PeerTimeoutError(RuntimeError):
     """A peer did not publish its data within the bounded wait of an IPC exchange kernel."""
+
+
+class PeerSetupError(RuntimeError):
+    """IPC peer memory could not be set up on every rank of a group (raised on all of them)."""
+
+
+def agree(ok: bool, group=None) -> bool:
+    """True on every rank iff ``ok`` is True on every rank of ``group`` (a MIN all-reduce)."""
+    dev = "cpu"
+    if dist.get_backend(group) == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device())
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
 
 
 class _ErrorWatch:
@@ -249,3 +292,37 @@ class PeerAllReduce:
         a step boundary, e.g. next to the loss read)."""
         if self.native:
             self._watch.check(sync=True)
+
+
+def build_peer_allreduce(capacity=1 << 13, max_spins=1 << 26, group=None):
+    """A :class:`PeerAllReduce` over all ranks of ``group`` (default WORLD) when every rank can map
+    every peer's IPC block AND a probe exchange returns the exact sum on every rank; otherwise
+    ``None`` -- on every rank alike, so a caller can fall back to an RCCL communicator without the ranks
+    diverging. Meant for single-node groups (HIP IPC does not cross nodes). ``max_spins`` bounds the
+    wait for a peer's flag (2^26 spins is minutes: a rank that is merely slow, e.g. still compiling its
+    first step, is waited for; a dead one NaN-poisons the output and raises)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if not (torch.cuda.is_available() and _native.available()) or world > 8:
+        agree(False, group)
+        return None
+    ranks = list(range(world)) if group is None else dist.get_process_group_ranks(group)
+    size = 2 * world * capacity * 4 + 4096
+    try:
+        pool = PeerMemoryPool(size, 0, peer_ranks=ranks, group=group, consensus=True)
+    except PeerSetupError:
+        return None
+    ok = True
+    red = None
+    try:
+        red = PeerAllReduce(pool, capacity=capacity, group=group, max_spins=max_spins)
+        t = torch.full((capacity,), float(rank + 1), dtype=torch.float32, device="cuda")
+        red.all_reduce_(t)
+        red.check()
+        ok = bool(torch.all(t == float(world * (world + 1) // 2)).item())
+        red.epoch_after_probe = red.epoch
+    except Exception:  # noqa: BLE001 - every rank learns of it through agree()
+        ok = False
+    if not agree(ok, group):
+        return None
+    return red

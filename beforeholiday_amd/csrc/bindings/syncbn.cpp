@@ -212,6 +212,27 @@ std::vector<at::Tensor> merge_sums(at::Tensor sums, c10::optional<at::Tensor> w,
   return r;
 }
 
+// single rank: finalize straight from conv-epilogue partials [2, G, C] (no [2C+1] sums tensor)
+std::vector<at::Tensor> merge_parts(at::Tensor part, double count, c10::optional<at::Tensor> w,
+                                    c10::optional<at::Tensor> b, c10::optional<at::Tensor> rmean,
+                                    c10::optional<at::Tensor> rvar, double momentum, double eps,
+                                    c10::optional<at::Tensor> num_batches) {
+  check_cuda(part, "part");
+  TORCH_CHECK(part.dim() == 3 && part.size(0) == 2 && part.scalar_type() == at::kFloat && part.is_contiguous(),
+              "part must be a contiguous fp32 [2, G, C] tensor");
+  check_running(rmean, rvar, w);
+  const int G = (int)part.size(1), C = (int)part.size(2);
+  auto r = final_outputs(part, C);
+  auto fin = fin_of(r, eps, momentum);
+  fin.num_batches = counter_ptr(num_batches);
+  const bool has_run = rmean.has_value() && rmean->defined();
+  int dtw = wcode(w);
+  if (!(w.has_value() && w->defined()) && has_run) dtw = dtype_code(rmean->scalar_type());
+  bh::bn_merge_parts(G, C, part.data_ptr<float>(), (float)count, fin, dtw, wptr(w), wptr(b),
+                     has_run ? rmean->data_ptr() : nullptr, has_run ? rvar->data_ptr() : nullptr, stream_for(part));
+  return r;
+}
+
 at::Tensor forward(at::Tensor x_in, c10::optional<at::Tensor> z, at::Tensor scale, at::Tensor shift, bool relu,
                    c10::optional<at::ScalarType> out_dtype, c10::optional<at::Tensor> num_batches) {
   check_cuda(x_in, "input");
@@ -385,6 +406,9 @@ void register_syncbn(pybind11::module_& root) {
         py::arg("num_batches") = py::none());
   m.def("stats_local_sums", &stats_local_sums, py::arg("x"), py::arg("running_mean") = py::none(),
         "local [sum(x-K), sum((x-K)^2), count] about K = running_mean (all_reduce SUM payload)");
+  m.def("merge_parts", &merge_parts, py::arg("part"), py::arg("count"), py::arg("weight"), py::arg("bias"),
+        py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
+        py::arg("num_batches") = py::none(), "single-rank finalize from conv-epilogue partials [2, G, C] (one launch)");
   m.def("merge_sums", &merge_sums, py::arg("sums"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("momentum"), py::arg("eps"), py::arg("num_batches") = py::none());
   m.def("forward", &forward, py::arg("x"), py::arg("z"), py::arg("scale"), py::arg("shift"), py::arg("relu"),

@@ -384,6 +384,58 @@ __global__ __launch_bounds__(kBlock) void k_merge_sums(int C, const float* __res
   }
 }
 
+// single-rank finalize straight from a convolution epilogue's partials part [2][G][C] (sums of x - K
+// and (x - K)^2 per workgroup, K = running mean): the partial rows are summed in the same fixed order
+// as conv_bn's k_sum_parts (row group g takes rows g, g + 16, ...; the 16 groups are then added in
+// order), then finalized as k_merge_sums -- one launch instead of sum_parts + merge_sums.
+constexpr int kMergeRows = 16;
+template <typename Tw>
+__global__ __launch_bounds__(64 * kMergeRows) void k_merge_parts(int G, int C, const float* __restrict__ part, float n,
+                                                                 BNFinal fin, const Tw* w, const Tw* b, Tw* rmean,
+                                                                 Tw* rvar) {
+  __shared__ float sh[2][kMergeRows][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float a1 = 0.f, a2 = 0.f;
+  if (c < C) {
+    const float* p1 = part + c;
+    const float* p2 = part + (int64_t)G * C + c;
+    for (int g = rg; g < G; g += kMergeRows) {
+      a1 += p1[(int64_t)g * C];
+      a2 += p2[(int64_t)g * C];
+    }
+  }
+  sh[0][rg][cl] = a1;
+  sh[1][rg][cl] = a2;
+  __syncthreads();
+  if (rg != 0 || c >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < kMergeRows; ++q) {
+    s1 += sh[0][q][cl];
+    s2 += sh[1][q][cl];
+  }
+  const float kc = rmean ? to_f<Tw>(rmean[c]) : 0.f;
+  const float dm = n > 0.f ? s1 / n : 0.f;
+  const float mean = kc + dm;
+  const float m2 = fmaxf(s2 - s1 * dm, 0.f);
+  const float var_b = n > 0.f ? m2 / n : 0.f;
+  const float unb = n > 1.f ? m2 / (n - 1.f) : var_b;
+  const float invstd = rsqrtf(var_b + fin.eps);
+  fin.mean[c] = mean;
+  fin.invstd[c] = invstd;
+  if (fin.count && c == 0) fin.count[0] = n;
+  const float wv = w ? to_f<Tw>(w[c]) : 1.f;
+  const float bv = b ? to_f<Tw>(b[c]) : 0.f;
+  fin.scale[c] = wv * invstd;
+  fin.shift[c] = bv - mean * wv * invstd;
+  if (rmean) {
+    const float mom = bn_momentum(fin);
+    rmean[c] = from_f<Tw>((1.f - mom) * kc + mom * mean);
+    rvar[c] = from_f<Tw>((1.f - mom) * to_f<Tw>(rvar[c]) + mom * unb);
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // forward: y = x*scale[c] + shift[c] (+ z) (relu)
 // ------------------------------------------------------------------------------------------
@@ -922,6 +974,14 @@ void bn_merge_sums(int C, const float* sums, const BNFinal& fin, int dt_w, const
       hipLaunchKernelGGL((k_merge_sums<Tw>), dim3(grid), dim3(kBlock), 0, st, C, sums, fin, (const Tw*)w, (const Tw*)b,
                          (Tw*)rmean, (Tw*)rvar));
   check_launch("bn_merge_sums");
+}
+
+void bn_merge_parts(int G, int C, const float* part, float count, const BNFinal& fin, int dt_w, const void* w,
+                    const void* b, void* rmean, void* rvar, hipStream_t st) {
+  BN_DISPATCH(dt_w, Tw,
+      hipLaunchKernelGGL((k_merge_parts<Tw>), dim3((C + 63) / 64), dim3(64 * kMergeRows), 0, st, G, C, part, count,
+                         fin, (const Tw*)w, (const Tw*)b, (Tw*)rmean, (Tw*)rvar));
+  check_launch("bn_merge_parts");
 }
 
 void bn_forward(const BNShape& s, int dt_x, const void* x, int dt_z, const void* z, int dt_y, void* y,

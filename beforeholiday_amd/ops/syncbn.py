@@ -111,6 +111,19 @@ def merge_sums(sums, weight, bias, running_mean, running_var, momentum, eps, num
     return _ref_final(mean, var_b, n, weight, bias, running_mean, running_var, momentum, eps, num_batches)
 
 
+def merge_parts(part, count, weight, bias, running_mean, running_var, momentum, eps, num_batches=None):
+    """Single rank: :func:`merge_sums` straight from a convolution epilogue's partials ``part [2, G, C]``
+    (sums of ``x - running_mean`` and its square per workgroup) over ``count`` elements per channel --
+    one kernel on the GPU instead of ``conv_bn.sum_parts`` + ``merge_sums``."""
+    if part.is_cuda:
+        return _native().merge_parts(part, float(count), weight, bias, running_mean, running_var, momentum, eps,
+                                     num_batches)
+    C = part.size(2)
+    sums = torch.cat([part.sum(1).reshape(-1), torch.tensor([float(count)], dtype=part.dtype)])
+    assert sums.numel() == 2 * C + 1
+    return merge_sums(sums, weight, bias, running_mean, running_var, momentum, eps, num_batches)
+
+
 def forward(x, z, scale, shift, relu, out_dtype=None, num_batches=None):
     """y = x*scale + shift (+z) (relu); increments ``num_batches`` (num_batches_tracked) if given."""
     if x.is_cuda:

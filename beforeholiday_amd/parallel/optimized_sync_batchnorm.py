@@ -146,12 +146,15 @@ class SyncBatchnormFromStats(torch.autograd.Function):
         world = _world(process_group)
         C = input.size(1)
         count = float(input.numel() // C)
-        sums = conv_bn_ops.sum_parts(part, count)
         if world > 1:
+            sums = conv_bn_ops.sum_parts(part, count)
             with comm_stats.timed("syncbn_fwd", sums):
                 _all_reduce(sums, process_group)
-        mean, invstd, scale, shift, count_t = syncbn.merge_sums(sums, weight, bias, running_mean, running_var,
-                                                                momentum, eps, num_batches)
+            mean, invstd, scale, shift, count_t = syncbn.merge_sums(sums, weight, bias, running_mean, running_var,
+                                                                    momentum, eps, num_batches)
+        else:  # one rank: partials -> statistics in one launch
+            mean, invstd, scale, shift, count_t = syncbn.merge_parts(part, count, weight, bias, running_mean,
+                                                                     running_var, momentum, eps, num_batches)
         mask = None
         if fuse_relu and syncbn.mask_ok(input, z):
             out, mask = syncbn.forward_mask(input, z, scale, shift, num_batches)

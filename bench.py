@@ -74,10 +74,12 @@ def parse():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N>1 (nccl = RCCL over xGMI; gloo only to rehearse the "
                          "multi-rank code path, e.g. several ranks sharing one GPU)")
-    ap.add_argument("--bn-group", default="separate", choices=["separate", "world", "ipc"],
-                    help="separate: SyncBN stats use their own communicator (all ranks), so a BN all_reduce "
-                         "never queues behind a DDP gradient bucket on the same RCCL stream; ipc: SyncBN stats "
-                         "through HIP-IPC peer memory (PeerAllReduce, single node), no RCCL launch per BN layer")
+    ap.add_argument("--bn-group", default="auto", choices=["auto", "separate", "world", "ipc"],
+                    help="auto (default): ipc when every rank is on this node and the IPC setup + probe exchange "
+                         "succeed on all ranks, else separate; ipc: SyncBN stats through HIP-IPC peer memory "
+                         "(PeerAllReduce: one push + epoch-flag kernel, no RCCL launch per BN layer); separate: "
+                         "SyncBN stats on their own RCCL communicator, so a BN all_reduce never queues behind a DDP "
+                         "gradient bucket on the same RCCL stream; world: the default process group")
     ap.add_argument("--stem", default="fused", choices=["fused", "unfused"],
                     help="fused: bn1+ReLU+maxpool in one HIP pass; unfused: SyncBN+ReLU then torch max_pool2d")
     ap.add_argument("--conv1x1", default="auto", choices=["auto", "miopen", "gemm"],
@@ -91,7 +93,31 @@ def parse():
     ap.add_argument("--conv3x3", default="auto", choices=["auto", "miopen", "direct"],
                     help="stride-1 3x3 convolution forward / data gradient: the direct MFMA kernel "
                          "(kernels/conv.hip), MIOpen, or the faster per shape (auto)")
+    ap.add_argument("--gemm-table", default="auto", choices=["auto", "off", "tune"],
+                    help="library GEMMs (layer 2-4 1x1 convolutions): auto loads the shipped per-shape hipBLASLt / "
+                         "rocBLAS solution table (utils/gemm_tuning.py), tune times every solution of each new "
+                         "shape and rewrites the table (offline only), off keeps hipBLASLt's default heuristic")
     return ap.parse_args()
+
+
+def syncbn_exchange(mode, world):
+    """The SyncBN statistics reducer for ``--bn-group`` (see its help) and its name for the JSON line.
+    Every rank takes the same branch: the IPC setup and probe agree across ranks before use."""
+    if mode in ("auto", "ipc"):
+        single_node = int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world
+        if single_node or mode == "ipc":
+            from beforeholiday_amd.contrib.peer_memory import build_peer_allreduce
+
+            # [2C+1] floats for C <= 2048 channels (ResNet-50's widest BatchNorm)
+            red = build_peer_allreduce(capacity=1 << 13)
+            if red is not None:
+                return red, "ipc"
+            if mode == "ipc":
+                sys.exit("bench.py: --bn-group ipc, but HIP-IPC peer memory could not be set up on every rank")
+        mode = "separate"
+    if mode == "separate":
+        return dist.new_group(list(range(world))), "rccl-separate"
+    return None, "rccl-world"
 
 
 def main():
@@ -118,6 +144,9 @@ def main():
             dist.init_process_group("gloo")
         assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
     torch.backends.cudnn.benchmark = args.autotune
+    from beforeholiday_amd.utils import gemm_tuning
+
+    gemm_tuned = args.gemm_table != "off" and gemm_tuning.enable_tuned_gemms(tune=args.gemm_table == "tune")
 
     from beforeholiday_amd import amp
     from beforeholiday_amd._native import require_native
@@ -132,13 +161,9 @@ def main():
         os.environ["BH_AMP_DEVICE_SCALER"] = "1"  # amp/scaler.py enable_device_mode: no host sync per step
     set_stats_mode(args.syncbn_stats)
     torch.manual_seed(1234 + rank)
-    bn_group = dist.new_group(list(range(world))) if (world > 1 and args.bn_group == "separate") else None
-    if world > 1 and args.bn_group == "ipc":
-        # SyncBN statistics through HIP-IPC peer memory (one-shot push + flag kernel, no RCCL launch)
-        from beforeholiday_amd.contrib.peer_memory import PeerAllReduce, PeerMemoryPool
-
-        bn_group = PeerAllReduce(PeerMemoryPool(2 * world * (1 << 13) * 4 + 4096, 0, peer_ranks=list(range(world))),
-                                 capacity=1 << 13)
+    bn_group, bn_exchange = None, "none"
+    if world > 1:
+        bn_group, bn_exchange = syncbn_exchange(args.bn_group, world)
     model = (resnet50() if args.no_syncbn else resnet50_fused(process_group=bn_group, channel_last=True,
                                                                    conv1x1_mode=args.conv1x1, conv3x3_mode=args.conv3x3,
                                                                    stem_pool_fused=args.stem == "fused")).cuda()
@@ -266,10 +291,15 @@ def main():
             "backend": (args.backend if world > 1 else "none"),
             "ddp_bucket_mb": buckets,
             "syncbn_stats": args.syncbn_stats,
+            "syncbn_exchange": bn_exchange,
             "loss_scaler": "host" if args.host_scaler else "device",
             "hip_graph": args.graph == "on",
+            "gemm_table": dict(gemm_tuning.status(), loaded=bool(gemm_tuned)),
             "comm_ms_per_step": comm,
         }), flush=True)
+    if args.gemm_table == "tune" and rank == 0:
+        n = gemm_tuning.write_table()
+        print(f"[bench] wrote {n} tuned GEMM signatures to {gemm_tuning.table_path()}", file=sys.stderr, flush=True)
     if world > 1:
         dist.destroy_process_group()
 

@@ -40,7 +40,7 @@ setup(
     version="0.1.0",
     description="MI355X-native (gfx950) mixed-precision and distributed training library with the Apex API",
     packages=find_packages(include=["beforeholiday_amd", "beforeholiday_amd.*"]),
-    package_data={"beforeholiday_amd": ["csrc/include/bh/*.h", "csrc/kernels/*.hip", "csrc/bindings/*.cpp",
+    package_data={"beforeholiday_amd": ["utils/tuned/*.csv", "csrc/include/bh/*.h", "csrc/kernels/*.hip", "csrc/bindings/*.cpp",
                                         "csrc/bindings/*.h"]},
     ext_modules=[] if PYTHON_ONLY else [Extension("beforeholiday_amd._C", sources=[])],
     cmdclass={} if PYTHON_ONLY else {"build_ext": NinjaBuild},

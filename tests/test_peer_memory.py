@@ -190,3 +190,40 @@ def _halo_timeout(rank, world, device):
 @pytest.mark.gpu
 def test_peer_halo_timeout_poisons_and_raises():
     run_distributed(_halo_timeout, 2, "cuda")
+
+
+def _build(rank, world, device, fail_rank):
+    """build_peer_allreduce: IPC when every rank can set it up (GPU), None on EVERY rank otherwise --
+    no native pool (CPU), or one rank failing its export (the others must not hang in the exchange)."""
+    from beforeholiday_amd.contrib.peer_memory import build_peer_allreduce, peer_memory
+    if device == "cuda":
+        torch.cuda.set_device(0)
+    if rank == fail_rank:
+        def broken(*_a, **_k):
+            raise RuntimeError("injected export failure")
+        orig = peer_memory._pm
+
+        class _Proxy:
+            def __getattr__(self, name):
+                return broken if name == "get_raw_ipc_address" else getattr(orig(), name)
+        peer_memory._pm = lambda: _Proxy()
+    red = build_peer_allreduce(capacity=1024)
+    if device == "cpu" or fail_rank >= 0:
+        assert red is None
+    else:
+        assert red is not None and red.G == world
+        t = torch.full((300,), float(rank), device="cuda")
+        red.all_reduce_(t)
+        red.check()
+        assert float(t[0]) == sum(range(world))
+    dist.barrier()
+
+
+def test_build_peer_allreduce_cpu_falls_back_on_every_rank():
+    run_distributed(_build, 2, "cpu", -1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fail_rank", [-1, 1])
+def test_build_peer_allreduce_ipc_consensus_one_gpu(fail_rank):
+    run_distributed(_build, 2, "cuda", fail_rank)

@@ -411,3 +411,32 @@ def test_fused_resnet_residual_grad_folded_into_conv1(mode):
     torch.testing.assert_close(xf.grad, xr.grad, rtol=2e-3, atol=2e-3)
     for (n, p), q in zip(fold.named_parameters(), ref.parameters()):
         torch.testing.assert_close(p.grad, q.grad, rtol=2e-3, atol=2e-3, msg=n)
+
+
+@pytest.mark.parametrize("device", devices())
+@pytest.mark.parametrize("G,C", [(1, 64), (37, 256), (515, 2048)])
+def test_merge_parts_equals_sum_parts_then_merge_sums(device, G, C):
+    """Single-rank finalize from conv-epilogue partials [2, G, C] (one kernel) == sum_parts +
+    merge_sums, bit for bit (same summation order), including the running-stat update; and both match
+    the fp64 statistics of the partials."""
+    from beforeholiday_amd.ops import conv_bn, syncbn as sb
+
+    g = torch.Generator().manual_seed(G)
+    n = 4096.0 * G
+    rm0 = torch.randn(C, generator=g) * 0.1
+    rv0 = torch.rand(C, generator=g) + 0.5
+    d = torch.randn(G, C, generator=g) * 3 + 1
+    part = torch.stack([d * 64, d * d * 64 + 4096]).contiguous().to(device)
+    w = (torch.rand(C, generator=g) + 0.5).to(device)
+    b = torch.randn(C, generator=g).to(device)
+    rm_a, rv_a, rm_b, rv_b = (t.clone().to(device) for t in (rm0, rv0, rm0, rv0))
+    out_a = sb.merge_parts(part, n, w, b, rm_a, rv_a, 0.1, 1e-5)
+    out_b = sb.merge_sums(conv_bn.sum_parts(part, n), w, b, rm_b, rv_b, 0.1, 1e-5)
+    for a_, b_ in zip(list(out_a) + [rm_a, rv_a], list(out_b) + [rm_b, rv_b]):
+        torch.testing.assert_close(a_.cpu(), b_.cpu(), rtol=0 if device == "cuda" else 1e-6, atol=0 if device == "cuda" else 1e-6)
+    s1 = part[0].double().sum(0).cpu()
+    s2 = part[1].double().sum(0).cpu()
+    mean = rm0.double() + s1 / n
+    var = (s2 - s1 * s1 / n) / n
+    torch.testing.assert_close(out_a[0].cpu().double(), mean, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(out_a[1].cpu().double(), (var + 1e-5).rsqrt(), rtol=1e-4, atol=1e-5)
