@@ -79,3 +79,25 @@ def status() -> dict:
     t = _tunable()
     return {"enabled": bool(t.is_enabled()), "tuning": bool(t.tuning_is_enabled()),
             "signatures": len(list(t.get_results())) if t.is_enabled() else 0}
+
+
+def add_argument(ap) -> None:
+    """The ``--gemm-table {auto,off,tune}`` option shared by bench.py and benchmarks/*.py."""
+    ap.add_argument("--gemm-table", default="auto", choices=["auto", "off", "tune"],
+                    help="library GEMMs: auto loads the shipped per-shape hipBLASLt / rocBLAS solution table "
+                         "(utils/gemm_tuning.py), tune times every solution of each new shape and rewrites the "
+                         "table (offline only), off keeps hipBLASLt's default heuristic")
+
+
+def setup(mode: str) -> bool:
+    """Apply ``--gemm-table``; call before the first GEMM. Returns whether a table is in use."""
+    return mode != "off" and enable_tuned_gemms(tune=mode == "tune")
+
+
+def finish(mode: str, rank: int = 0) -> None:
+    """After a ``--gemm-table tune`` run, rank 0 writes the merged table (shipped + new signatures)."""
+    if mode == "tune" and rank == 0:
+        import sys
+
+        n = write_table()
+        print(f"[gemm-table] wrote {n} tuned GEMM signatures to {table_path()}", file=sys.stderr, flush=True)

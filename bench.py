@@ -93,6 +93,8 @@ def parse():
     ap.add_argument("--conv3x3", default="auto", choices=["auto", "miopen", "direct"],
                     help="stride-1 3x3 convolution forward / data gradient: the direct MFMA kernel "
                          "(kernels/conv.hip), MIOpen, or the faster per shape (auto)")
+    # (same option as utils/gemm_tuning.add_argument, spelled out: the parent of a spawned job must not
+    # import the package before its children start)
     ap.add_argument("--gemm-table", default="auto", choices=["auto", "off", "tune"],
                     help="library GEMMs (layer 2-4 1x1 convolutions): auto loads the shipped per-shape hipBLASLt / "
                          "rocBLAS solution table (utils/gemm_tuning.py), tune times every solution of each new "
@@ -146,7 +148,7 @@ def main():
     torch.backends.cudnn.benchmark = args.autotune
     from beforeholiday_amd.utils import gemm_tuning
 
-    gemm_tuned = args.gemm_table != "off" and gemm_tuning.enable_tuned_gemms(tune=args.gemm_table == "tune")
+    gemm_tuned = gemm_tuning.setup(args.gemm_table)
 
     from beforeholiday_amd import amp
     from beforeholiday_amd._native import require_native
@@ -297,9 +299,7 @@ def main():
             "gemm_table": dict(gemm_tuning.status(), loaded=bool(gemm_tuned)),
             "comm_ms_per_step": comm,
         }), flush=True)
-    if args.gemm_table == "tune" and rank == 0:
-        n = gemm_tuning.write_table()
-        print(f"[bench] wrote {n} tuned GEMM signatures to {gemm_tuning.table_path()}", file=sys.stderr, flush=True)
+    gemm_tuning.finish(args.gemm_table, rank)
     if world > 1:
         dist.destroy_process_group()
 

@@ -31,12 +31,16 @@ def main():
     ap.add_argument("--layers", type=int, default=24)
     ap.add_argument("--opt-level", default="O2", choices=["O2", "O5"])
     ap.add_argument("--dropout", type=float, default=0.1)
+    from beforeholiday_amd.utils import gemm_tuning
+
+    gemm_tuning.add_argument(ap)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
+    gemm_tuning.setup(args.gemm_table)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
     dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
@@ -105,7 +109,9 @@ def main():
             "dtype": "fp16" if fp16 else "bf16", "data": "synthetic token ids, random-init weights",
             "config": {"model": f"BERT-large ({args.layers} layers, {nparams / 1e6:.0f}M params) + FusedLayerNorm + "
                        "FusedLAMB", "global_batch": B * world, "seq_len": S, "parallelism": f"dp{world}",
-                       "final_loss": round(float(loss), 4)}}), flush=True)
+                       "final_loss": round(float(loss), 4)},
+            "gemm_table": gemm_tuning.status()}), flush=True)
+    gemm_tuning.finish(args.gemm_table, rank)
     dist.destroy_process_group()
 
 

@@ -43,6 +43,9 @@ def main():
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI; gloo only to rehearse multi-rank TP/SP on one GPU")
+    from beforeholiday_amd.utils import gemm_tuning
+
+    gemm_tuning.add_argument(ap)
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -64,6 +67,7 @@ def main():
     elif local_rank >= ndev:
         sys.exit(f"bench_gpt.py: rank {rank} wants GPU {local_rank} but only {ndev} are visible")
     torch.cuda.set_device(local_rank)
+    gemm_tuning.setup(args.gemm_table)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29534")
     if args.backend == "nccl":
@@ -141,7 +145,9 @@ def main():
             "config": {"model": f"GPT-2-medium ({args.layers} layers, {nparams_local / 1e6:.0f}M params per TP rank) "
                        "+ FusedAdam", "global_batch": B * dp, "seq_len": S,
                        "parallelism": f"tp{tp}{'-sp' if cfg.sequence_parallel else ''}-dp{dp}",
-                       "final_loss": round(float(loss.detach()), 4)}}), flush=True)
+                       "final_loss": round(float(loss.detach()), 4)},
+            "gemm_table": gemm_tuning.status()}), flush=True)
+    gemm_tuning.finish(args.gemm_table, rank)
     dist.destroy_process_group()
 
 
