@@ -88,8 +88,10 @@ def parse():
     ap.add_argument("--host-scaler", action="store_true",
                     help="dynamic loss scale read on the host every step (the reference's .item() per step); "
                          "default: device-resident scale, overflow skipped by the fused optimizer's noop flag")
-    ap.add_argument("--graph", default="off", choices=["off", "on"],
-                    help="replay the whole training step as one captured HIP graph (utils/graphs.py)")
+    ap.add_argument("--graph", default="auto", choices=["auto", "off", "on"],
+                    help="replay the whole training step as one captured HIP graph (utils/graphs.py); auto: on for "
+                         "a single rank (no collectives inside the step), off with ranks to synchronise (RCCL "
+                         "buckets and the IPC statistics exchange, whose epoch counters advance on the host)")
     ap.add_argument("--conv3x3", default="auto", choices=["auto", "miopen", "direct"],
                     help="stride-1 3x3 convolution forward / data gradient: the direct MFMA kernel "
                          "(kernels/conv.hip), MIOpen, or the faster per shape (auto)")
@@ -226,7 +228,8 @@ def main():
                   file=sys.stderr, flush=True)
     run = step
     capture_ms = None
-    if args.graph == "on":
+    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1 and not args.host_scaler)
+    if use_graph:
         from beforeholiday_amd.utils import GraphedStep
 
         run = GraphedStep(step, warmup=2).capture()
@@ -295,7 +298,7 @@ def main():
             "syncbn_stats": args.syncbn_stats,
             "syncbn_exchange": bn_exchange,
             "loss_scaler": "host" if args.host_scaler else "device",
-            "hip_graph": args.graph == "on",
+            "hip_graph": use_graph,
             "gemm_table": dict(gemm_tuning.status(), loaded=bool(gemm_tuned)),
             "comm_ms_per_step": comm,
         }), flush=True)
