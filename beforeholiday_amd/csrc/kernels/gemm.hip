@@ -443,7 +443,9 @@ BH_DEVICE __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, int64_t rows_left, 
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nrec, (int)kRsrcWord3);
 }
 
-template <typename T>
+// ACT / BWD as template parameters: one epilogue path per kernel (all of them in one function pushed
+// the register allocator past 256 VGPRs and into scratch)
+template <typename T, int ACT, bool BWD>
 __global__ __launch_bounds__(kPPThreads, 1) void k_gemm_pp(Args p) {
   __shared__ __attribute__((aligned(16))) char smem[kPPSmem];
   const int tid = threadIdx.x;
@@ -581,73 +583,137 @@ __global__ __launch_bounds__(kPPThreads, 1) void k_gemm_pp(Args p) {
   step(std::true_type{}, smem + ((nk - 1) & 1) * kPPBuf, nullptr, 0);
   if (wr == 0) raw_barrier();
 
-  // ---- epilogue straight from the accumulators. The MFMAs ran with B as the first operand, so
-  // acc[mt][nt][j] = C[row fr of 16-row tile mt][column 4 * fq + j of 16-column tile nt]: every lane
-  // holds 4 consecutive columns, and bias, activation, aux and stores work on 8-byte vectors
-  // without an LDS transpose.
+  // ---- epilogue. The MFMAs ran with B as the first operand, so acc[mt][nt][j] = C[row fr of 16-row
+  // tile mt][column 4 * fq + j of 16-column tile nt]: a lane holds 4 consecutive columns of one row,
+  // and 16 lanes of a store instruction would hit 16 rows with 8 bytes each (32-byte segments: the
+  // output then leaves at a fraction of the HBM rate). Instead every result tensor goes through a
+  // wave-private 128 x 64 LDS image (16 KiB per wave; the two 64 KiB main-loop buffers are free):
+  // lanes write their 8-byte pieces (16-byte chunk index XOR-swizzled by row & 7, 2-way at worst),
+  // then each lane reads one 16-byte chunk back and a store instruction covers 8 rows x 128 bytes.
+  // The dGELU input aux_in comes in the same way in reverse (coalesced 16-byte loads -> image ->
+  // the accumulator layout).
   const GemmEpilogue& e = p.epi;
   T* __restrict__ Cp = reinterpret_cast<T*>(p.C);
-  const int row_l = brow + wr * 128 + fr;
   const int col_l = bcol + wc * 64 + fq * 4;
-  auto body = [&](auto actc) {
-    constexpr int ACT = decltype(actc)::value;
-    if (!e.bwd_act) {
-      float bias[4][4];
+  const int row_w = brow + wr * 128;  // first row of the wave tile
+  __syncthreads();                     // every wave is past its last main-loop LDS read
+  char* img = smem + wave * 16384;
+  typedef T t4 __attribute__((ext_vector_type(4)));
+  auto img_off = [&](int r, int chunk) { return r * 128 + ((chunk ^ (r & 7)) << 4); };
+  auto put = [&](int mt, int nt, const float (&v)[4]) {
+    const int r = mt * 16 + fr;
+    t4 o;
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const int col = col_l + nt * 16;
-        if (e.bias && col < p.N) load4<T>(reinterpret_cast<const T*>(e.bias) + col, bias[nt]);
-        else bias[nt][0] = bias[nt][1] = bias[nt][2] = bias[nt][3] = 0.f;
+    for (int j = 0; j < 4; ++j) o[j] = static_cast<T>(v[j]);
+    *reinterpret_cast<t4*>(img + img_off(r, nt * 2 + (fq >> 1)) + (fq & 1) * 8) = o;
+  };
+  auto get = [&](int mt, int nt, float (&v)[4]) {
+    const int r = mt * 16 + fr;
+    const t4 o = *reinterpret_cast<const t4*>(img + img_off(r, nt * 2 + (fq >> 1)) + (fq & 1) * 8);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = static_cast<float>(o[j]);
+  };
+  const int cc = lane & 7, rq = lane >> 3;
+  const int fcol = bcol + wc * 64 + cc * 8;
+  // (four 16-byte chunks in flight per lane at a time: the accumulators stay live across a flush)
+  auto flush = [&](T* dst, int64_t ld) {  // image -> 128 rows x 64 columns of dst
+#pragma unroll 1
+    for (int i0 = 0; i0 < 16; i0 += 4) {
+#pragma unroll
+      for (int i = i0; i < i0 + 4; ++i) {
+        const int rr = i * 8 + rq, row = row_w + rr;
+        const i4v v = *reinterpret_cast<const i4v*>(img + img_off(rr, cc));
+        if (row < p.M && fcol < p.N) *reinterpret_cast<i4v*>(dst + (int64_t)row * ld + fcol) = v;
       }
+    }
+  };
+  auto fill = [&](const T* src, int64_t ld) {  // 128 rows x 64 columns of src -> image
+#pragma unroll 1
+    for (int i0 = 0; i0 < 16; i0 += 4) {
 #pragma unroll
-      for (int mt = 0; mt < 8; ++mt) {
-        const int row = row_l + mt * 16;
-        if (row >= p.M) break;
+      for (int i = i0; i < i0 + 4; ++i) {
+        const int rr = i * 8 + rq, row = row_w + rr;
+        i4v v = i4v{0, 0, 0, 0};
+        if (row < p.M && fcol < p.N) v = *reinterpret_cast<const i4v*>(src + (int64_t)row * ld + fcol);
+        *reinterpret_cast<i4v*>(img + img_off(rr, cc)) = v;
+      }
+    }
+  };
+  {
+    if constexpr (!BWD) {
+      // bias folded into the accumulators first (the pre-activation, kept in fp32 for the activation)
+      if (e.bias) {
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
           const int col = col_l + nt * 16;
-          if (col < p.N) {
-            float v[4];
+          float b[4] = {0.f, 0.f, 0.f, 0.f};
+          if (col < p.N) load4<T>(reinterpret_cast<const T*>(e.bias) + col, b);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = acc[mt][nt][j] + bias[nt][j];
-            if (e.pre_out) store4<T>(reinterpret_cast<T*>(e.pre_out) + (int64_t)row * e.ld_aux + col, v);
-            if constexpr (ACT != kActNone) {
+          for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
-              for (int j = 0; j < 4; ++j) v[j] = act_f(v[j], ACT);
-            }
-            store4<T>(Cp + (int64_t)row * p.ldc + col, v);
-          }
+            for (int j = 0; j < 4; ++j) acc[mt][nt][j] += b[j];
         }
       }
-    } else {
-      float cs[4][4] = {};
+      if (e.pre_out) {  // the pre-activation (aux) image first
 #pragma unroll
-      for (int mt = 0; mt < 8; ++mt) {
-        const int row = row_l + mt * 16;
-        if (row >= p.M) break;
+        for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          const int col = col_l + nt * 16;
-          if (col < p.N) {
+          for (int nt = 0; nt < 4; ++nt) {
             float v[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = acc[mt][nt][j];
-            if constexpr (ACT != kActNone) {
-              float a[4];
-              load4<T>(reinterpret_cast<const T*>(e.aux_in) + (int64_t)row * e.ld_aux + col, a);
-#pragma unroll
-              for (int j = 0; j < 4; ++j) v[j] *= act_d(a[j], ACT);
-            }
-            // bias grad of the value actually stored (rounded like the reference's separate pass)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              v[j] = to_f<T>(from_f<T>(v[j]));
-              cs[nt][j] += v[j];
-            }
-            store4<T>(Cp + (int64_t)row * p.ldc + col, v);
+            put(mt, nt, v);
           }
-        }
+        flush(reinterpret_cast<T*>(e.pre_out), e.ld_aux);
       }
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          float v[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = acc[mt][nt][j];
+          if constexpr (ACT != kActNone) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = act_f(v[j], ACT);
+          }
+          put(mt, nt, v);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      flush(Cp, p.ldc);
+    } else {
+      float cs[4][4] = {};
+      if constexpr (ACT != kActNone) fill(reinterpret_cast<const T*>(e.aux_in), e.ld_aux);
+      // each (mt, nt) piece of the image is read (aux), replaced by the dActivation product (same
+      // lane, same address) and the next piece follows: a piece's LDS read never waits behind more
+      // than one row of tiles, and the accumulators are consumed as they go
+#pragma unroll
+      for (int mt = 0; mt < 8; ++mt) {
+        const bool row_ok = row_w + mt * 16 + fr < p.M;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          float v[4];
+          if constexpr (ACT != kActNone) {
+            float a[4];
+            get(mt, nt, a);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = acc[mt][nt][j] * act_d(a[j], ACT);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = acc[mt][nt][j];
+          }
+          // bias grad of the value actually stored (rounded like the reference's separate pass)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[j] = to_f<T>(from_f<T>(v[j]));
+            if (row_ok && col_l + nt * 16 < p.N) cs[nt][j] += v[j];
+          }
+          put(mt, nt, v);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      flush(Cp, p.ldc);
       if (e.bgrad_part) {
         // sum over the 16 row lanes; the wave's 128 rows go to its first 64-row slab, the second
         // slab (if it exists) gets zeros so the fixed-order finalize still sees every slab written
@@ -662,7 +728,7 @@ __global__ __launch_bounds__(kPPThreads, 1) void k_gemm_pp(Args p) {
             t += __shfl_xor(t, 8);
             cs[nt][j] = t;
           }
-        const int row0 = brow + wr * 128;
+        const int row0 = row_w;
         if (fr == 0 && row0 < p.M) {
 #pragma unroll
           for (int nt = 0; nt < 4; ++nt) {
@@ -676,13 +742,6 @@ __global__ __launch_bounds__(kPPThreads, 1) void k_gemm_pp(Args p) {
         }
       }
     }
-  };
-  switch (e.act) {
-    case kActRelu: body(std::integral_constant<int, kActRelu>{}); break;
-    case kActSigmoid: body(std::integral_constant<int, kActSigmoid>{}); break;
-    case kActGelu: body(std::integral_constant<int, kActGelu>{}); break;
-    case kActGeluTanh: body(std::integral_constant<int, kActGeluTanh>{}); break;
-    default: body(std::integral_constant<int, kActNone>{}); break;
   }
 }
 
@@ -719,7 +778,18 @@ void launch_pp(const Args& a0, hipStream_t st) {
   a.tiles_n = (a.N + kPPTile - 1) / kPPTile;
   const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
   if (nwg >= (1ll << 31)) throw std::runtime_error("gemm_nt: grid too large");
-  hipLaunchKernelGGL((k_gemm_pp<T>), dim3((unsigned)nwg), dim3(kPPThreads), 0, st, a);
+  auto go = [&](auto actc) {
+    constexpr int ACT = decltype(actc)::value;
+    if (a.epi.bwd_act) hipLaunchKernelGGL((k_gemm_pp<T, ACT, true>), dim3((unsigned)nwg), dim3(kPPThreads), 0, st, a);
+    else hipLaunchKernelGGL((k_gemm_pp<T, ACT, false>), dim3((unsigned)nwg), dim3(kPPThreads), 0, st, a);
+  };
+  switch (a.epi.act) {
+    case kActRelu: go(std::integral_constant<int, kActRelu>{}); break;
+    case kActSigmoid: go(std::integral_constant<int, kActSigmoid>{}); break;
+    case kActGelu: go(std::integral_constant<int, kActGelu>{}); break;
+    case kActGeluTanh: go(std::integral_constant<int, kActGeluTanh>{}); break;
+    default: go(std::integral_constant<int, kActNone>{}); break;
+  }
 }
 
 template <typename C, typename T>
