@@ -445,7 +445,7 @@ BH_DEVICE __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, int64_t rows_left, 
 
 // ACT / BWD as template parameters: one epilogue path per kernel (all of them in one function pushed
 // the register allocator past 256 VGPRs and into scratch)
-template <typename T, int ACT, bool BWD>
+template <typename T, int ACT, bool BWD, bool STATS = false>
 __global__ __launch_bounds__(kPPThreads, 1) void k_gemm_pp(Args p) {
   __shared__ __attribute__((aligned(16))) char smem[kPPSmem];
   const int tid = threadIdx.x;
@@ -682,6 +682,56 @@ __global__ __launch_bounds__(kPPThreads, 1) void k_gemm_pp(Args p) {
         __builtin_amdgcn_sched_barrier(0);
       }
       flush(Cp, p.ldc);
+      if constexpr (STATS) {
+        // BatchNorm statistics of the stored values (bn_stats == 1): sums of c - kshift and its square
+        // per column over the wave's 128 rows (16 row lanes x 8 tiles), written to the 64-row slab of
+        // row_w (the next slab gets zeros, as the fixed-order partial reduction expects every slab)
+        float s1[4][4] = {}, s2[4][4] = {};
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const int col = col_l + nt * 16;
+          float k[4] = {0.f, 0.f, 0.f, 0.f};
+          if (e.kshift && col < p.N) {
+            const float4 kv = *reinterpret_cast<const float4*>(e.kshift + col);
+            k[0] = kv.x; k[1] = kv.y; k[2] = kv.z; k[3] = kv.w;
+          }
+#pragma unroll
+          for (int mt = 0; mt < 8; ++mt) {
+            if (row_w + mt * 16 + fr >= p.M) continue;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float d = to_f<T>(from_f<T>(acc[mt][nt][j])) - k[j];
+              s1[nt][j] += d;
+              s2[nt][j] = fmaf(d, d, s2[nt][j]);
+            }
+          }
+        }
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int m = 1; m < 16; m <<= 1) {
+              s1[nt][j] += __shfl_xor(s1[nt][j], m);
+              s2[nt][j] += __shfl_xor(s2[nt][j], m);
+            }
+        const int64_t slabs = ((int64_t)p.M + 63) / 64, slab = row_w / 64;
+        if (fr == 0 && row_w < p.M) {
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            const int col = col_l + nt * 16;
+            if (col >= p.N) continue;
+            float* d1 = e.stat_part + slab * p.N + col;
+            float* d2 = e.stat_part + (slabs + slab) * p.N + col;
+            *reinterpret_cast<float4*>(d1) = make_float4(s1[nt][0], s1[nt][1], s1[nt][2], s1[nt][3]);
+            *reinterpret_cast<float4*>(d2) = make_float4(s2[nt][0], s2[nt][1], s2[nt][2], s2[nt][3]);
+            if (row_w + 64 < p.M) {
+              *reinterpret_cast<float4*>(d1 + p.N) = make_float4(0.f, 0.f, 0.f, 0.f);
+              *reinterpret_cast<float4*>(d2 + p.N) = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+          }
+        }
+      }
     } else {
       float cs[4][4] = {};
       if constexpr (ACT != kActNone) fill(reinterpret_cast<const T*>(e.aux_in), e.ld_aux);
@@ -778,6 +828,10 @@ void launch_pp(const Args& a0, hipStream_t st) {
   a.tiles_n = (a.N + kPPTile - 1) / kPPTile;
   const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
   if (nwg >= (1ll << 31)) throw std::runtime_error("gemm_nt: grid too large");
+  if (a.epi.bn_stats == 1) {  // statistics epilogue: plain output (no bias / activation / aux)
+    hipLaunchKernelGGL((k_gemm_pp<T, kActNone, false, true>), dim3((unsigned)nwg), dim3(kPPThreads), 0, st, a);
+    return;
+  }
   auto go = [&](auto actc) {
     constexpr int ACT = decltype(actc)::value;
     if (a.epi.bwd_act) hipLaunchKernelGGL((k_gemm_pp<T, ACT, true>), dim3((unsigned)nwg), dim3(kPPThreads), 0, st, a);
@@ -837,7 +891,9 @@ void gemm_nt(int dt, const void* A, int64_t lda, const void* B, int64_t ldb, voi
   const int64_t big_wgs = ((M + CfgBig::BM - 1) / CfgBig::BM) * ((N + CfgBig::BN - 1) / CfgBig::BN);
   // the ping-pong kernel keeps row offsets of a 256-row tile in 32 bits
   const bool pp_ok = glds && lda < (1 << 22) && ldb < (1 << 22);
-  const bool pp = pp_ok && !epi.bn_stats && (tile_mode == 4 || (tile_mode == 0 && big_wgs >= 256));
+  // the ping-pong kernel has the statistics epilogue (bn_stats == 1) but not the BatchNorm-backward one
+  const bool pp_epi = epi.bn_stats == 0 || (epi.bn_stats == 1 && !epi.bias && epi.act == kActNone && !epi.pre_out);
+  const bool pp = pp_ok && pp_epi && (tile_mode == 4 || (tile_mode == 0 && big_wgs >= 256));
   const bool big = glds && !pp && (tile_mode == 2 || (tile_mode == 0 && big_wgs >= 256));
   const bool mid = glds && tile_mode == 3;
   switch (dt) {

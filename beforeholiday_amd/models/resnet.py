@@ -555,6 +555,14 @@ def _c1x1_forward_stats(x, weight, kshift, s2):
         return y2d.view(n, ho, wo, k).permute(0, 3, 1, 2), part
     if s2:
         a2d = x[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, c)
+    if _PP_STATS and k >= 2048 and a2d.size(0) >= 4 * 256 and a2d.dtype in (torch.float16, torch.bfloat16):
+        # the 2048-channel outputs of stage 4: the 256x256 ping-pong MFMA GEMM with the statistics
+        # epilogue (kernels/gemm.hip), no separate statistics pass. Narrower outputs keep the tuned
+        # library GEMM + statistics pass: with K <= 256 the ping-pong tile is prologue / epilogue bound
+        # and measured 0.15 vs 0.10 ms (K 128 -> N 512) and 0.082 vs 0.074 ms (256 -> 1024)
+        # (profiles/conv_bn_vs_unfused.jsonl, ms_tiled_gemm_bn); whole step 24.9 vs 24.6 ms with them
+        y2d, part = conv_bn.gemm_bn(a2d, w2d, "stats", kshift=kshift)
+        return y2d.view(n, ho, wo, k).permute(0, 3, 1, 2), part
     y = torch.mm(a2d, w2d.t()).view(n, ho, wo, k).permute(0, 3, 1, 2)
     return y, _part_from_tensor(y, kshift)
 
@@ -671,6 +679,7 @@ class _Conv3x3BNFn(torch.autograd.Function):
 
 
 _FOLD_BN = os.environ.get("BH_FOLD_BN", "1") != "0"
+_PP_STATS = os.environ.get("BH_PP_STATS", "1") != "0"
 _FOLD_3X3_BWD = os.environ.get("BH_FOLD_3X3_BWD", "0") == "1"
 
 

@@ -253,3 +253,20 @@ def test_c1x1_stride2_scatter_accumulate(KNHW, dt):
     out, _ = conv_bn.c1x1(a, w, b_trans=True, s2=(H, W), s2_scatter=True, resid=base)
     assert out.data_ptr() == base.data_ptr()
     torch.testing.assert_close(out.float().view(n, H, W, N), ref, **_tol(dt))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("MKN", [(33000, 256, 512), (16500, 512, 1024), (12544, 512, 2048)])
+def test_gemm_bn_stats_pingpong(MKN, dt):
+    """Grids of >= 256 256x256 tiles take the ping-pong kernel with the statistics epilogue (the
+    ResNet-50 conv3 / downsample layers of stages 2-4); partial last tile included."""
+    M, K, N = MKN
+    a, b = _data(M, K, N, dt, "cuda", seed=11)
+    kshift = torch.randn(N, device="cuda") * 0.1
+    c, part = conv_bn.gemm_bn(a, b, "stats", kshift=kshift)
+    assert part.shape == (2, (M + 63) // 64, N)
+    torch.testing.assert_close(c.float(), a.float() @ b.float().t(), **_tol(dt))
+    d = c.float() - kshift
+    ref = torch.cat([d.sum(0), (d * d).sum(0)]).cpu()
+    _stats_close(conv_bn.sum_parts(part).cpu(), ref, M)
