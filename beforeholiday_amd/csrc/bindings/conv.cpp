@@ -195,12 +195,26 @@ bool wgrad_supported(const at::Tensor& x, const at::Tensor& dy, int64_t R, int64
   return bh::conv_wgrad_plan(a, &g);
 }
 
-at::Tensor conv_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t R, int64_t stride) {
+at::Tensor conv_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t R, int64_t stride,
+                      const c10::optional<at::Tensor>& pro_scale, const c10::optional<at::Tensor>& pro_shift) {
   TORCH_CHECK(wgrad_ok(x, dy, R, stride), "conv_wgrad: needs channels_last fp16/bf16 x [N, C, sH, sW], "
                                           "dy [N, K, H, W], C and K % 64 == 0, R in {1, 3}, stride 2 only for R = 1");
   auto out = at::empty({dy.size(1), x.size(1), R, R}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto a = wgrad_args(x, dy, R, stride);
   a.out = out.data_ptr();
+  at::Tensor ps, ph;
+  if (pro_scale.has_value() && pro_scale->defined()) {
+    TORCH_CHECK(pro_shift.has_value() && pro_shift->defined() && stride == 1,
+                "conv_wgrad: the BatchNorm prologue needs pro_scale and pro_shift, stride 1");
+    ps = pro_scale->contiguous();
+    ph = pro_shift->contiguous();
+    TORCH_CHECK(ps.is_cuda() && ph.is_cuda() && ps.device() == x.device() && ph.device() == x.device() &&
+                    ps.scalar_type() == at::kFloat && ph.scalar_type() == at::kFloat && ps.numel() == x.size(1) &&
+                    ph.numel() == x.size(1),
+                "conv_wgrad: pro_scale / pro_shift must be fp32 [C] tensors on x's device");
+    a.pro_scale = ps.data_ptr<float>();
+    a.pro_shift = ph.data_ptr<float>();
+  }
   bh::ConvWgradGeo g;
   TORCH_CHECK(bh::conv_wgrad_plan(a, &g), "conv_wgrad: shape not covered (window does not fit in LDS / unaligned)");
   const int64_t nws = bh::conv_wgrad_workspace(g, a);
@@ -285,8 +299,9 @@ void register_conv(pybind11::module_& root) {
   m.def("conv3x3_bn_dgrad", &conv3x3_bn_dgrad, py::arg("grad_out"), py::arg("weight"), py::arg("by"),
         py::arg("bscale"), py::arg("bshift"), py::arg("bmean"), py::arg("brelu") = true);
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("grad_out"), py::arg("R"), py::arg("stride") = 1,
-        "weight gradient of conv2d(x, w, stride, padding=(R-1)//2), R in {1, 3} (stride 2: R = 1): [K, C, R, R] "
-        "channels_last");
+        py::arg("pro_scale") = py::none(), py::arg("pro_shift") = py::none(),
+        "weight gradient of conv2d(x', w, stride, padding=(R-1)//2), R in {1, 3} (stride 2: R = 1), x' = x or "
+        "relu(x * pro_scale + pro_shift) per channel (stride 1): [K, C, R, R] channels_last");
   m.def("wgrad_supported", &wgrad_supported, py::arg("x"), py::arg("grad_out"), py::arg("R"), py::arg("stride") = 1);
   m.def("gemm_n64", &gemm_n64, py::arg("a"), py::arg("b"), py::arg("resid") = c10::nullopt,
         "a [M, K] . b[64, K]^T (+ resid [M, 64]), K in {64, 128, 256}, M % 32 == 0 (kernels/gemm_n64.hip)");

@@ -60,6 +60,10 @@ struct ConvWgradArgs {
   int N = 0, H = 0, W = 0, C = 0, K = 0, R = 3;
   int stride = 1;            // 2: 1x1 / stride-2 convolution (R = 1; dY pixel (y, x) reads x pixel (2y, 2x))
   int wout = 0;              // set by the launcher: the real output width of a flattened 1x1 problem
+  // optional BatchNorm + ReLU prologue on x (fp32 [C] each, stride 1 only): the weight gradient of a
+  // convolution whose input relu(x * pro_scale + pro_shift) was never materialised
+  const float* pro_scale = nullptr;
+  const float* pro_shift = nullptr;
 };
 struct ConvWgradGeo {
   int G4 = 0, TH = 0, ksteps = 0, wpi = 0, nwin = 0, ctiles = 0, tiles = 0, wpw = 0, splits = 0, grid = 0, kt = 1, ct = 1, parts = 0;

@@ -107,7 +107,11 @@ BH_DEVICE i4v frag2(const char* img, int lo, int hi) {
 
 // window geometry (G4 four-pixel groups per row, TH rows) as compile-time constants: the staging
 // address math divides by them
-template <typename T, int R, int G4, int TH, int KT, int CT = 1>
+// PRO: x is the raw input of a BatchNorm + ReLU that was never applied (models/resnet.py folds it into
+// the consumers): every lane rewrites the X chunks its own LDS-DMA brought in -- relu(x * scale + shift),
+// rounded as the normalisation pass would -- after they land and before the window barrier; chunks of
+// pixels outside the image stay zero (they pad the normalised activation).
+template <typename T, int R, int G4, int TH, int KT, int CT = 1, bool PRO = false>
 __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, ConvWgradGeo g, float* __restrict__ ws,
                                                            T* __restrict__ out) {
   constexpr int P = (R - 1) / 2, RR = R * R;
@@ -122,8 +126,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
   // 32-column sub-tile of its 32 * CT input channels instead
   constexpr int NOFF = R == 1 ? CT : (RR + 1) / 2;
   static_assert(XS <= kMaxHalo && DS <= kMaxD, "window does not fit");
-  static_assert(2 * BUF <= 160 * 1024, "two window buffers must fit in LDS");
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  static_assert(2 * BUF + (PRO ? 8 * TC : 0) <= 160 * 1024, "two window buffers must fit in LDS");
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF + (PRO ? 8 * TC : 0)];
   // XCD-aware placement: hardware deals workgroup ids round-robin over the 8 XCDs; consecutive
   // logical ids (same window run, different tiles) land on one XCD so the run is read from one L2
   const int b = blockIdx.x;
@@ -153,11 +157,13 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
   constexpr int NPW = XPW + DPW;  // this wave's pieces: X pieces first, then dY pieces
   constexpr int kBad = -4096;
   int rel[NPW], hrow[NPW];
+  int xch[XPW];  // PRO: the 8-channel chunk of each X piece this lane fills (-1: pad chunk / no piece)
 #pragma unroll
   for (int i = 0; i < NPW; ++i) {
     const bool isx = i < XPW;
     const int piece = wave + 8 * (isx ? i : i - XPW);
     const int byte = piece * 1024 + lane * 16, slot = byte / XSL, ch = (byte - slot * XSL) >> 4;
+    if (isx) xch[i < XPW ? i : 0] = (piece < XP && ch < 8 * CT && slot < XS) ? ch : -1;
     if (isx) {
       const int hr = slot / HC, x = slot - hr * HC - P;
       const bool ok = piece < XP && ch < 8 * CT && slot < XS && x >= 0 && x < W;
@@ -189,6 +195,30 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
   auto win_origin = [&](int win, int& n, int& y0) {
     n = win / g.wpi;
     y0 = (win - n * g.wpi) * TH;
+  };
+  float* pss = reinterpret_cast<float*>(smem + 2 * BUF);  // PRO: scale[TC], shift[TC] of channels c0..
+  if constexpr (PRO) {
+    for (int i = tid; i < TC; i += kThreads) {
+      pss[i] = a.pro_scale[c0 + i];
+      pss[TC + i] = a.pro_shift[c0 + i];
+    }
+  }
+  // PRO: this lane's landed X chunks of window (n, y0) in buffer buf -> relu(x * scale + shift)
+  auto prologue = [&](int n, int y0, char* buf) {
+    (void)n;
+#pragma unroll
+    for (int i = 0; i < XPW; ++i) {
+      const int piece = wave + 8 * i;
+      const int y = y0 + hrow[i];
+      if (xch[i] < 0 || hrow[i] == kBad || y < 0 || y >= H) continue;
+      char* p = buf + piece * 1024 + lane * 16;
+      typedef T t8 __attribute__((ext_vector_type(8)));
+      t8 v = *reinterpret_cast<const t8*>(p);
+      const float* sc = pss + xch[i] * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = from_f<T>(fmaxf(fmaf(to_f<T>(v[e]), sc[e], sc[TC + e]), 0.f));
+      *reinterpret_cast<t8*>(p) = v;
+    }
   };
 
   // per-lane fragment addresses, fixed for the whole kernel. Transposed read: lane 4q + p of each
@@ -224,10 +254,18 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
   // fragments of k-step ks + 1 are read while the MFMAs of ks run (two register sets, one read pair
   // behind each MFMA, order pinned by sched_barrier)
   i4v fa[2][KT], fb[2][NOFF];
+  if constexpr (PRO) __syncthreads();  // scale / shift visible
   for (int win = w_begin; win < w_end; ++win) {
     const char* xs = smem + ((win - w_begin) & 1) * BUF;
     const char* ds = xs + BUFX;
     wait_vmcnt<0>();  // this wave's pieces of window `win` have landed ...
+    if constexpr (PRO) {
+      int n0, y00;
+      win_origin(win, n0, y00);
+      asm volatile("" ::: "memory");
+      prologue(n0, y00, const_cast<char*>(xs));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     raw_barrier();    // ... and everyone's; everyone is also done reading the other buffer
     // the next window's pieces are issued one behind each of the first MFMAs (their address math
     // co-issues with the matrix cores instead of stalling in front of them)
@@ -387,6 +425,7 @@ bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo) {
     return false;
   // stride 2: 1x1 only, windows of whole output rows (W divides 112)
   if (!(a.stride == 1 || (a.stride == 2 && a.R == 1 && 112 % a.W == 0))) return false;
+  if (a.pro_scale && (a.stride != 1 || !a.pro_shift)) return false;
   // 32-bit buffer offsets (the out-of-image offset sits past both tensors)
   if (2 * (int64_t)a.N * a.H * a.W * std::max(a.C * a.stride * a.stride, a.K) >= 0x7ff00000ll) return false;
   ConvWgradGeo g;
@@ -442,14 +481,19 @@ void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws
     using T = typename decltype(tt)::type;
     T* out = reinterpret_cast<T*>(a.out);
     auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(g.grid), dim3(kThreads), 0, st, b, g, ws, out); };
-    if (a.R == 1) {
-      if (g.ct == 2) g.kt == 2 ? go(k_conv_wgrad<T, 1, 28, 1, 2, 2>) : go(k_conv_wgrad<T, 1, 28, 1, 1, 2>);
-      else g.kt == 2 ? go(k_conv_wgrad<T, 1, 28, 1, 2, 1>) : go(k_conv_wgrad<T, 1, 28, 1, 1, 1>);
-    }
-    else if (g.G4 == 14) go(k_conv_wgrad<T, 3, 14, 2, 1>);
-    else if (g.G4 == 7) go(k_conv_wgrad<T, 3, 7, 4, 1>);
-    else if (g.G4 == 4) g.kt == 2 ? go(k_conv_wgrad<T, 3, 4, 7, 2>) : go(k_conv_wgrad<T, 3, 4, 7, 1>);
-    else g.kt == 2 ? go(k_conv_wgrad<T, 3, 2, 7, 2>) : go(k_conv_wgrad<T, 3, 2, 7, 1>);
+    auto pick = [&](auto proc) {
+      constexpr bool P = decltype(proc)::value;
+      if (a.R == 1) {
+        if (g.ct == 2) g.kt == 2 ? go(k_conv_wgrad<T, 1, 28, 1, 2, 2, P>) : go(k_conv_wgrad<T, 1, 28, 1, 1, 2, P>);
+        else g.kt == 2 ? go(k_conv_wgrad<T, 1, 28, 1, 2, 1, P>) : go(k_conv_wgrad<T, 1, 28, 1, 1, 1, P>);
+      }
+      else if (g.G4 == 14) go(k_conv_wgrad<T, 3, 14, 2, 1, 1, P>);
+      else if (g.G4 == 7) go(k_conv_wgrad<T, 3, 7, 4, 1, 1, P>);
+      else if (g.G4 == 4) g.kt == 2 ? go(k_conv_wgrad<T, 3, 4, 7, 2, 1, P>) : go(k_conv_wgrad<T, 3, 4, 7, 1, 1, P>);
+      else g.kt == 2 ? go(k_conv_wgrad<T, 3, 2, 7, 2, 1, P>) : go(k_conv_wgrad<T, 3, 2, 7, 1, 1, P>);
+    };
+    if (a.pro_scale) pick(std::true_type{});
+    else pick(std::false_type{});
     if (g.parts > 1)
       hipLaunchKernelGGL(k_wgrad_reduce<T>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, ws, out, n, g.parts);
   };

@@ -678,7 +678,111 @@ class _Conv3x3BNFn(torch.autograd.Function):
         return gx, gw, None, None
 
 
+class _BNConvFn(torch.autograd.Function):
+    """A training-mode (Sync)BatchNorm + ReLU whose output only feeds the next convolution, folded into
+    that convolution: the BatchNorm is never applied as a pass. Forward: the producing convolution's
+    statistics partials -> (one all-reduce across ranks) -> mean / invstd / scale / shift + running
+    stats, then the convolution reads the raw input y and applies relu(y * scale + shift) to its staged
+    tiles (the 3x3 direct kernel's halo prologue, or the 1x1 strip GEMM's A-fragment prologue) and
+    emits the NEXT BatchNorm's statistics partials. Backward: the convolution's data gradient dA (for a
+    1x1 layer with this BatchNorm's backward sums in its epilogue), its weight gradient from the same
+    prologue applied to the LDS tiles of the wgrad kernel, then the BatchNorm backward from (dA, y) with
+    the ReLU mask recomputed from y. Same parameters, running statistics and gradients as
+    ``bn(y) -> relu -> conv``; one full read + write of the activation less per direction."""
+
+    @staticmethod
+    def forward(ctx, y, part, bn_w, bn_b, running_mean, running_var, eps, momentum, process_group, num_batches,
+                conv_w, kshift_out, R):
+        from ..ops import conv_bn
+        from ..ops import syncbn
+        from ..parallel.optimized_sync_batchnorm import _all_reduce, _world
+        from ..parallel import comm_stats
+        from .._native import submodule
+
+        world = _world(process_group)
+        C = y.size(1)
+        count = float(y.numel() // C)
+        if world > 1:
+            sums = conv_bn.sum_parts(part, count)
+            with comm_stats.timed("syncbn_fwd", sums):
+                _all_reduce(sums, process_group)
+            mean, invstd, scale, shift, count_t = syncbn.merge_sums(sums, bn_w, bn_b, running_mean, running_var,
+                                                                    momentum, eps, num_batches)
+        else:
+            mean, invstd, scale, shift, count_t = syncbn.merge_parts(part, count, bn_w, bn_b, running_mean,
+                                                                     running_var, momentum, eps, num_batches)
+        if num_batches is not None:
+            num_batches.add_(1)  # (the normalisation pass would have bumped it)
+        if R == 3:
+            out, part_out = submodule("conv_cuda").conv3x3_bn_forward(y, conv_w, scale, shift, True, kshift_out)
+        else:
+            n, _, h, w = y.shape
+            k = conv_w.size(0)
+            o2d, part_out = conv_bn.c1x1(y.permute(0, 2, 3, 1).reshape(-1, C), conv_w.view(k, C), pro_scale=scale,
+                                         pro_shift=shift, epi="stats", kshift=kshift_out)
+            out = o2d.view(n, h, w, k).permute(0, 3, 1, 2)
+        ctx.save_for_backward(y, conv_w, bn_w, mean, invstd, scale, shift, count_t)
+        ctx.process_group, ctx.world, ctx.R = process_group, world, R
+        ctx.mark_non_differentiable(part_out)
+        ctx.set_materialize_grads(False)
+        return out, part_out
+
+    @staticmethod
+    def backward(ctx, gy, _gpart):
+        from ..ops import conv as bhconv
+        from ..ops import conv_bn
+        from ..ops import syncbn
+        from ..parallel.optimized_sync_batchnorm import _all_reduce
+        from ..parallel import comm_stats
+
+        y, conv_w, bn_w, mean, invstd, scale, shift, count = ctx.saved_tensors
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        n, C, h, w = y.shape
+        sums = None
+        if ctx.R == 3:
+            dA = bhconv.conv3x3_dgrad(gy, conv_w)
+        else:
+            k = conv_w.size(0)
+            gy2d = gy.permute(0, 2, 3, 1).reshape(-1, k)
+            w2d = conv_w.view(k, C)
+            y2d = y.permute(0, 2, 3, 1).reshape(-1, C)
+            if conv_bn.preferred(k, C, gy2d.size(0)) and conv_bn.supported(gy2d, w2d, epi="bwd", b_trans=True):
+                # the strip GEMM with this BatchNorm's backward sums in its epilogue (where it beats hipBLASLt)
+                dA2d, part = conv_bn.c1x1(gy2d, w2d, epi="bwd", by=y2d, bscale=scale, bshift=shift, bmean=mean,
+                                          brelu=True, b_trans=True)
+                sums = conv_bn.sum_parts(part)
+            else:
+                dA2d = torch.mm(gy2d, w2d)
+            dA = dA2d.view(n, h, w, C).permute(0, 3, 1, 2)
+        g_conv = None
+        if ctx.needs_input_grad[10]:
+            g_conv = bhconv.conv_wgrad(y, gy, ctx.R, scale, shift)
+            if g_conv.stride() != conv_w.stride():
+                g_conv = g_conv.contiguous()
+        need_w = bn_w is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
+        if sums is None:
+            sums, gw, gb = syncbn.backward_reduce(dA, y, None, mean, invstd, scale, shift, True, bn_w, need_w, None)
+        else:
+            gw = (sums[C:] * invstd).to(bn_w.dtype) if need_w else None
+            gb = sums[:C].to(bn_w.dtype) if need_w else None
+        if ctx.world > 1:
+            with comm_stats.timed("syncbn_bwd", sums):
+                _all_reduce(sums, ctx.process_group)
+        gx, _ = syncbn.backward_dgrad(dA, y, None, mean, invstd, bn_w, sums, count, scale, shift, True, False, None)
+        return gx, None, (gw if need_w else None), (gb if need_w else None), None, None, None, None, None, None, \
+            g_conv, None, None
+
+
+def _bn_conv(bn, y, part, conv_w, kshift_out, R):
+    exp_avg = bn.momentum if bn.momentum is not None else -1.0
+    return _BNConvFn.apply(y, part, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, exp_avg,
+                           bn.process_group, bn.num_batches_tracked, conv_w, kshift_out, R)
+
+
 _FOLD_BN = os.environ.get("BH_FOLD_BN", "1") != "0"
+# BatchNorm + ReLU applied inside the consuming convolution (no normalisation pass) where that
+# convolution is the 3x3 direct kernel or the 1x1 strip GEMM (BH_FOLD_APPLY=0: separate passes)
+_FOLD_APPLY = os.environ.get("BH_FOLD_APPLY", "1") != "0"
 _PP_STATS = os.environ.get("BH_PP_STATS", "1") != "0"
 _FOLD_3X3_BWD = os.environ.get("BH_FOLD_3X3_BWD", "0") == "1"
 
@@ -711,6 +815,20 @@ class Bottleneck(nn.Module):
                         and b.running_mean is not None and b.running_mean.dtype == torch.float32 for b in bns)
                 and (self.downsample is None or len(self.downsample) == 2))
 
+    def _fold_bn2(self, y2):
+        """bn2 folds into conv3 where conv3 runs on the 1x1 strip GEMM (the HBM-bound 56x56 / 28x28
+        layers): its prologue variant measured 0.083 vs 0.19 ms for BN pass + GEMM + statistics pass at
+        K 128 -> N 512 (profiles/conv_bn_vs_unfused.jsonl, mode "pro"); the wider layers keep the pass
+        and the library GEMM."""
+        from ..ops import conv_bn
+
+        n, c, h, w = y2.shape
+        k = self.conv3.weight.size(0)
+        if c > 128 or n * h * w < 100000:
+            return False
+        a2d = y2.permute(0, 2, 3, 1).reshape(-1, c)
+        return conv_bn.supported(a2d, self.conv3.weight.view(k, c), pro=True, epi="stats")
+
     def _forward_folded(self, x):
         from ..ops import conv as bhconv
         from ..parallel.optimized_sync_batchnorm import BNLink
@@ -723,16 +841,27 @@ class Bottleneck(nn.Module):
         else:
             box = {} if (torch.is_grad_enabled() and x.requires_grad) else None
             y1, p1 = _Conv1x1BNFn.apply(x, self.conv1.weight, _kshift(self.bn1), None, box, False)
-        l1 = BNLink()
-        a1 = self.bn1.forward_from_stats(y1, p1, link=l1)
         l2 = None
-        if self.stride == 1 and bhconv.supported(a1, self.conv2.weight):
-            y2, p2 = _Conv3x3BNFn.apply(a1, self.conv2.weight, _kshift(self.bn2), l1)
-            l2 = BNLink()
-            a2 = self.bn2.forward_from_stats(y2, p2, link=l2)
-        else:  # stride-2 3x3 (MIOpen): its BatchNorm computes its own statistics
-            a2 = self.bn2(self.conv2(a1))
-        y3, p3 = _Conv1x1BNFn.apply(a2, self.conv3.weight, _kshift(self.bn3), l2, None, False)
+        y3 = None
+        if _FOLD_APPLY and self.stride == 1 and bhconv.supported(y1, self.conv2.weight):
+            # bn1 + ReLU inside conv2's halo prologue; bn2 + ReLU inside conv3's strip GEMM where it runs
+            y2, p2 = _bn_conv(self.bn1, y1, p1, self.conv2.weight, _kshift(self.bn2), 3)
+            if self._fold_bn2(y2):
+                y3, p3 = _bn_conv(self.bn2, y2, p2, self.conv3.weight, _kshift(self.bn3), 1)
+            else:
+                l2 = BNLink()
+                a2 = self.bn2.forward_from_stats(y2, p2, link=l2)
+        else:
+            l1 = BNLink()
+            a1 = self.bn1.forward_from_stats(y1, p1, link=l1)
+            if self.stride == 1 and bhconv.supported(a1, self.conv2.weight):
+                y2, p2 = _Conv3x3BNFn.apply(a1, self.conv2.weight, _kshift(self.bn2), l1)
+                l2 = BNLink()
+                a2 = self.bn2.forward_from_stats(y2, p2, link=l2)
+            else:  # stride-2 3x3 (MIOpen): its BatchNorm computes its own statistics
+                a2 = self.bn2(self.conv2(a1))
+        if y3 is None:
+            y3, p3 = _Conv1x1BNFn.apply(a2, self.conv3.weight, _kshift(self.bn3), l2, None, False)
         if ds is not None:
             identity = ds[1].forward_from_stats(yd, pd)
         else:

@@ -50,13 +50,26 @@ def conv_wgrad_s2(x: torch.Tensor, dy: torch.Tensor) -> torch.Tensor:
                                                [False, True, False])[1]
 
 
-def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, r: int) -> torch.Tensor:
-    """Weight gradient of ``conv2d(x, w, stride=1, padding=(r-1)//2)`` for r in {1, 3}: the MFMA
-    kernel of kernels/conv_wgrad.hip (both operands read through LDS transposes, fp32 split partials
-    summed in a fixed order) for channels_last fp16 / bf16 with C, K multiples of 64; otherwise
+def bn_relu_apply(x: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor) -> torch.Tensor:
+    """``relu(x * scale + shift)`` per channel (NCHW-indexed), rounded to x's dtype: the activation a
+    folded BatchNorm never materialises, as the reference paths compute it."""
+    s = scale.float().view(1, -1, *([1] * (x.dim() - 2)))
+    b = shift.float().view(1, -1, *([1] * (x.dim() - 2)))
+    return torch.relu(x.float() * s + b).to(x.dtype)
+
+
+def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, r: int, pro_scale: torch.Tensor = None,
+               pro_shift: torch.Tensor = None) -> torch.Tensor:
+    """Weight gradient of ``conv2d(x', w, stride=1, padding=(r-1)//2)`` for r in {1, 3}, where x' is x or,
+    with ``pro_scale`` / ``pro_shift``, ``relu(x * pro_scale + pro_shift)`` per channel (a BatchNorm +
+    ReLU folded into the convolution, applied to the staged tiles in LDS): the MFMA kernel of
+    kernels/conv_wgrad.hip (both operands read through LDS transposes, fp32 split partials summed in a
+    fixed order) for channels_last fp16 / bf16 with C, K multiples of 64; otherwise
     ``torch.ops.aten.convolution_backward``. Returns [K, C, r, r] (channels_last on the kernel path)."""
     if wgrad_supported(x, dy, r):
-        return submodule("conv_cuda").conv_wgrad(x, dy, r)
+        return submodule("conv_cuda").conv_wgrad(x, dy, r, 1, pro_scale, pro_shift)
+    if pro_scale is not None:
+        x = bn_relu_apply(x, pro_scale, pro_shift)
     w_shape = [dy.size(1), x.size(1), r, r]
     p = (r - 1) // 2
     return torch.ops.aten.convolution_backward(dy, x, torch.empty(w_shape, device=x.device, dtype=x.dtype), None,

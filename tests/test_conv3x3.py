@@ -248,3 +248,29 @@ def test_gemm_n64_kernel(dtype, shape, resid):
     tol = 1e-2 if dtype == torch.float16 else 3e-2
     torch.testing.assert_close(c.float(), ref, rtol=tol, atol=tol)
     assert not bhconv.gemm_n64_supported(a[:M - 1] if M > 32 else a[:, :K - 8].contiguous(), b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 64, 64, 56, 56, 3), (4, 128, 128, 28, 28, 3), (3, 256, 256, 14, 14, 3),
+                                   (4, 512, 512, 7, 7, 3), (2, 64, 128, 13, 13, 3), (2, 64, 256, 56, 56, 1),
+                                   (4, 128, 512, 28, 28, 1), (4, 256, 64, 14, 14, 1)])
+def test_conv_wgrad_bn_prologue(dtype, shape):
+    """Weight gradient with the folded BatchNorm + ReLU prologue (x raw, relu(x * scale + shift) applied to
+    the LDS tiles) ~ the plain kernel on the materialised activation, and close to fp32
+    conv2d_weight; zero padding stays zero (scale / shift with relu(shift) > 0 would otherwise leak)."""
+    N, C, K, H, W, R = shape
+    g = torch.Generator(device="cuda").manual_seed(N * 7 + C + K + H + R)
+    x = torch.randn(N, C, H, W, device="cuda", dtype=dtype, generator=g).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(N, K, H, W, device="cuda", dtype=dtype, generator=g).contiguous(memory_format=torch.channels_last)
+    scale = torch.rand(C, device="cuda", generator=g) + 0.5
+    shift = torch.rand(C, device="cuda", generator=g) + 0.1  # relu(0 * s + b) = b > 0: padding must not see it
+    assert bhconv.wgrad_supported(x, dy, R)
+    a = bhconv.bn_relu_apply(x, scale, shift).contiguous(memory_format=torch.channels_last)
+    gw = bhconv.conv_wgrad(x, dy, R, scale, shift)
+    ref = torch.nn.grad.conv2d_weight(a.float(), (K, C, R, R), dy.float(), stride=1, padding=(R - 1) // 2)
+    tol = 1e-2 if dtype == torch.float16 else 2e-2
+    # the kernel's fused multiply-add may round an input differently from torch's mul + add by one ulp
+    torch.testing.assert_close(gw.float(), bhconv.conv_wgrad(a, dy, R).float(), rtol=0,
+                               atol=0.1 * tol * ref.abs().max().item())
+    torch.testing.assert_close(gw.float(), ref, rtol=tol, atol=tol * ref.abs().max().item())

@@ -89,3 +89,42 @@ def test_folded_and_unfolded_paths_agree():
     assert _rel(outs[0][1], outs[1][1]) < 2e-2
     for a, b in zip(outs[0][2], outs[1][2]):
         assert _rel(a, b) < 2e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [(256, 64, 1, 56, 32), (512, 128, 1, 28, 128)])
+def test_bn_apply_folded_into_conv2_and_conv3(cfg):
+    """bn1 + ReLU inside conv2 (3x3 halo prologue) and, at >= 100k pixels with <= 128 channels, bn2 +
+    ReLU inside conv3 (strip-GEMM prologue; weight gradients through the wgrad kernel's LDS prologue):
+    the same block with BH_FOLD_APPLY off (separate normalisation passes) agrees to rounding, including
+    running statistics and num_batches_tracked."""
+    inplanes, planes, stride, hw, batch = cfg
+    R, _, blk = _block(inplanes, planes, stride, torch.float16)
+    x = torch.randn(batch, inplanes, hw, hw, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    y2 = torch.empty(batch, planes, hw, hw, device="cuda", dtype=torch.half).contiguous(memory_format=torch.channels_last)
+    assert blk._fold_bn2(y2)
+    old = R._FOLD_APPLY
+    state0 = {k: v.clone() for k, v in blk.state_dict().items()}
+    try:
+        outs = []
+        for fold in (True, False):
+            R._FOLD_APPLY = fold
+            blk.load_state_dict(state0)
+            xx = x.clone().requires_grad_()
+            o = blk(xx)
+            o.float().square().mean().backward()
+            outs.append((o.detach(), xx.grad, [p.grad.clone() for p in blk.parameters()],
+                         {k: v.clone() for k, v in blk.state_dict().items()}))
+            for p in blk.parameters():
+                p.grad = None
+    finally:
+        R._FOLD_APPLY = old
+    assert _rel(outs[0][0], outs[1][0]) < 5e-3
+    assert _rel(outs[0][1], outs[1][1]) < 2e-2
+    for a, b in zip(outs[0][2], outs[1][2]):
+        assert _rel(a, b) < 2e-2
+    for k in outs[0][3]:
+        if "running" in k:
+            assert _rel(outs[0][3][k], outs[1][3][k]) < 1e-3, k
+        elif "num_batches" in k:
+            assert int(outs[0][3][k]) == int(outs[1][3][k]) == int(state0[k]) + 1, k
