@@ -242,6 +242,27 @@ at::Tensor stem_forward(const at::Tensor& x, const at::Tensor& w) {
   return y;
 }
 
+// stem forward + the BatchNorm statistics partials of its output ([2, G, 64] about kshift)
+std::vector<at::Tensor> stem_forward_stats(const at::Tensor& x, const at::Tensor& w,
+                                           const c10::optional<at::Tensor>& kshift) {
+  TORCH_CHECK(stem_ok(x, w), "stem_forward_stats: needs channels_last fp16/bf16 x [N, 3, 224, 224], w [64, 3, 7, 7]");
+  const float* kp = nullptr;
+  at::Tensor kc;
+  if (kshift.has_value() && kshift->defined()) {
+    kc = kshift->contiguous();
+    TORCH_CHECK(kc.is_cuda() && kc.device() == x.device() && kc.scalar_type() == at::kFloat && kc.numel() == 64,
+                "stem_forward_stats: kshift must be an fp32 [64] tensor on x's device");
+    kp = kc.data_ptr<float>();
+  }
+  const at::Tensor wc = w.contiguous(at::MemoryFormat::ChannelsLast);
+  auto y = at::empty({x.size(0), 64, 112, 112}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int G = bh::conv_stem_parts((int)x.size(0));
+  auto part = at::empty({2, G, 64}, x.options().dtype(at::kFloat));
+  bh::conv_stem_forward(dtype_code(x.scalar_type()), x.data_ptr(), wc.data_ptr(), y.data_ptr(), (int)x.size(0),
+                        stream_for(x), kp, part.data_ptr<float>());
+  return {y, part};
+}
+
 bool gemm_n64_ok(const at::Tensor& a, const at::Tensor& b) {
   auto al = [](const at::Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0; };
   return a.is_cuda() && b.is_cuda() && a.device() == b.device() && a.dim() == 2 && b.dim() == 2 && a.scalar_type() == b.scalar_type() &&
@@ -298,6 +319,8 @@ void register_conv(pybind11::module_& root) {
         py::arg("relu") = true, py::arg("r") = py::none(), py::arg("r_mul") = false);
   m.def("conv3x3_bn_dgrad", &conv3x3_bn_dgrad, py::arg("grad_out"), py::arg("weight"), py::arg("by"),
         py::arg("bscale"), py::arg("bshift"), py::arg("bmean"), py::arg("brelu") = true);
+  m.def("stem_forward_stats", &stem_forward_stats, py::arg("x"), py::arg("weight"), py::arg("kshift") = py::none(),
+        "ResNet stem conv (7x7/2, 3 -> 64) + BatchNorm statistics partials [2, G, 64] of its output about kshift");
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("grad_out"), py::arg("R"), py::arg("stride") = 1,
         py::arg("pro_scale") = py::none(), py::arg("pro_shift") = py::none(),
         "weight gradient of conv2d(x', w, stride, padding=(R-1)//2), R in {1, 3} (stride 2: R = 1), x' = x or "

@@ -216,8 +216,9 @@ std::vector<at::Tensor> merge_sums(at::Tensor sums, c10::optional<at::Tensor> w,
 std::vector<at::Tensor> merge_parts(at::Tensor part, double count, c10::optional<at::Tensor> w,
                                     c10::optional<at::Tensor> b, c10::optional<at::Tensor> rmean,
                                     c10::optional<at::Tensor> rvar, double momentum, double eps,
-                                    c10::optional<at::Tensor> num_batches) {
+                                    c10::optional<at::Tensor> num_batches, bool bump) {
   check_cuda(part, "part");
+  TORCH_CHECK(!bump || momentum >= 0, "merge_parts: bump (num_batches += 1) needs a fixed momentum");
   TORCH_CHECK(part.dim() == 3 && part.size(0) == 2 && part.scalar_type() == at::kFloat && part.is_contiguous(),
               "part must be a contiguous fp32 [2, G, C] tensor");
   check_running(rmean, rvar, w);
@@ -229,7 +230,8 @@ std::vector<at::Tensor> merge_parts(at::Tensor part, double count, c10::optional
   int dtw = wcode(w);
   if (!(w.has_value() && w->defined()) && has_run) dtw = dtype_code(rmean->scalar_type());
   bh::bn_merge_parts(G, C, part.data_ptr<float>(), (float)count, fin, dtw, wptr(w), wptr(b),
-                     has_run ? rmean->data_ptr() : nullptr, has_run ? rvar->data_ptr() : nullptr, stream_for(part));
+                     has_run ? rmean->data_ptr() : nullptr, has_run ? rvar->data_ptr() : nullptr, stream_for(part),
+                     bump);
   return r;
 }
 
@@ -408,7 +410,8 @@ void register_syncbn(pybind11::module_& root) {
         "local [sum(x-K), sum((x-K)^2), count] about K = running_mean (all_reduce SUM payload)");
   m.def("merge_parts", &merge_parts, py::arg("part"), py::arg("count"), py::arg("weight"), py::arg("bias"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
-        py::arg("num_batches") = py::none(), "single-rank finalize from conv-epilogue partials [2, G, C] (one launch)");
+        py::arg("num_batches") = py::none(), py::arg("bump") = false,
+        "single-rank finalize from conv-epilogue partials [2, G, C] (one launch); bump: num_batches += 1 too");
   m.def("merge_sums", &merge_sums, py::arg("sums"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("momentum"), py::arg("eps"), py::arg("num_batches") = py::none());
   m.def("forward", &forward, py::arg("x"), py::arg("z"), py::arg("scale"), py::arg("shift"), py::arg("relu"),

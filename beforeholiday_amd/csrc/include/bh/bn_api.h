@@ -44,8 +44,9 @@ void bn_merge_sums(int C, const float* sums, const BNFinal& fin, int dt_w, const
                    void* rvar, hipStream_t st);
 // single rank: sum a convolution epilogue's partials part [2][G][C] (fixed order) and finalize as
 // bn_merge_sums with element count `count` -- one launch
+// (bump: also num_batches += 1, for a fixed momentum only)
 void bn_merge_parts(int G, int C, const float* part, float count, const BNFinal& fin, int dt_w, const void* w,
-                    const void* b, void* rmean, void* rvar, hipStream_t st);
+                    const void* b, void* rmean, void* rvar, hipStream_t st, bool bump = false);
 // merge W gathered rows [W][2C+1] into final stats (+ running stats update, scale/shift)
 void bn_merge_ranks(int W, int C, const float* gathered, const BNFinal& fin, int dt_w, const void* w,
                     const void* b, void* rmean, void* rvar, float* var_unbiased, hipStream_t st);

@@ -77,7 +77,11 @@ void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws
 // ResNet stem forward (kernels/conv_stem.hip): 7x7 / stride 2 / pad 3, C = 3 -> K = 64, 224x224 NHWC
 // x [N, 224, 224, 3], w [64, 7, 7, 3], y [N, 112, 112, 64]
 bool conv_stem_supported(int N, int C, int H, int W, int K);
-void conv_stem_forward(int dt, const void* x, const void* w, void* y, int N, hipStream_t st);
+// part (optional, fp32 [2][conv_stem_parts(N)][64]): BatchNorm statistics partials of the output about
+// kshift (fp32 [64] or null), see kernels/conv_stem.hip
+int conv_stem_parts(int N);
+void conv_stem_forward(int dt, const void* x, const void* w, void* y, int N, hipStream_t st,
+                       const float* kshift = nullptr, float* part = nullptr);
 // its weight gradient: out [64, 7, 7, 3] from x and dy [N, 112, 112, 64]; ws holds
 // conv_stem_wgrad_parts(N) * 9408 fp32 partials
 int conv_stem_wgrad_parts(int N);

@@ -392,7 +392,10 @@ constexpr int kMergeRows = 16;
 template <typename Tw>
 __global__ __launch_bounds__(64 * kMergeRows) void k_merge_parts(int G, int C, const float* __restrict__ part, float n,
                                                                  BNFinal fin, const Tw* w, const Tw* b, Tw* rmean,
-                                                                 Tw* rvar) {
+                                                                 Tw* rvar, bool bump) {
+  // bump: this launch also advances num_batches_tracked (the host sets it only for a fixed momentum,
+  // where no thread reads the counter)
+  if (bump && fin.num_batches && blockIdx.x == 0 && threadIdx.x == 0) *fin.num_batches += 1;
   __shared__ float sh[2][kMergeRows][64];
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -977,10 +980,11 @@ void bn_merge_sums(int C, const float* sums, const BNFinal& fin, int dt_w, const
 }
 
 void bn_merge_parts(int G, int C, const float* part, float count, const BNFinal& fin, int dt_w, const void* w,
-                    const void* b, void* rmean, void* rvar, hipStream_t st) {
+                    const void* b, void* rmean, void* rvar, hipStream_t st, bool bump) {
+  if (bump && fin.momentum < 0.f) throw std::runtime_error("bn_merge_parts: bump needs a fixed momentum");
   BN_DISPATCH(dt_w, Tw,
       hipLaunchKernelGGL((k_merge_parts<Tw>), dim3((C + 63) / 64), dim3(64 * kMergeRows), 0, st, G, C, part, count,
-                         fin, (const Tw*)w, (const Tw*)b, (Tw*)rmean, (Tw*)rvar));
+                         fin, (const Tw*)w, (const Tw*)b, (Tw*)rmean, (Tw*)rvar, bump));
   check_launch("bn_merge_parts");
 }
 

@@ -46,9 +46,13 @@ constexpr int kRowHalves = 720;                // staged row: 9 pad halves, 672 
 constexpr int kLead = 9;                       // input column -3 (3 channels) = staged half 0
 constexpr int kTileStride = 72;                // epilogue LDS: halves per pixel row (64 + 8 pad)
 
-template <typename T>
+// STATS: also the BatchNorm statistics of the output (part [2][gridDim.x][64]: per-workgroup sums of
+// y - kshift and (y - kshift)^2 over the stored values), so the stem's BatchNorm needs no statistics
+// pass. Each lane accumulates its 16 (channel) values over every item the wave computes.
+template <typename T, bool STATS = false>
 __global__ __launch_bounds__(256) void k_stem_fwd(const T* __restrict__ x, const T* __restrict__ w, T* __restrict__ y,
-                                                  int N) {
+                                                  int N, const float* __restrict__ kshift = nullptr,
+                                                  float* __restrict__ part = nullptr) {
   __shared__ __attribute__((aligned(16))) uint16_t rows[kRowsIn * kRowHalves];
   __shared__ __attribute__((aligned(16))) uint16_t tile[4][16 * kTileStride];
   __shared__ __attribute__((aligned(16))) uint16_t wl[kK * kR * 32];  // [channel][r][j], j >= 21 zero
@@ -85,6 +89,14 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const T* __restrict__ x, const
     rows[row * kRowHalves + (e < kLead ? e : e + 672)] = 0;
   }
   uint16_t* tw = tile[wave];
+  // STATS: lane holds channels 16 mt + 4 (lane >> 4) + i (i < 4) of its pixel in acc[mt][i]
+  float s1[4][4] = {}, s2[4][4] = {}, ks[4][4] = {};
+  if constexpr (STATS) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ks[mt][i] = kshift ? kshift[16 * mt + 4 * (lane >> 4) + i] : 0.f;
+  }
   const int nblk = N * (kOH / kRowsOut);
   for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
     const int n = blk / (kOH / kRowsOut), yb = blk - n * (kOH / kRowsOut);
@@ -128,6 +140,14 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const T* __restrict__ x, const
         T o[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = from_f<T>(acc[mt][i]);
+        if constexpr (STATS) {  // every item is 16 whole pixels of a real output row
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float d = to_f<T>(o[i]) - ks[mt][i];
+            s1[mt][i] += d;
+            s2[mt][i] = fmaf(d, d, s2[mt][i]);
+          }
+        }
         *reinterpret_cast<uint2*>(tw + (lane & 15) * kTileStride + 16 * mt + 4 * (lane >> 4)) =
             *reinterpret_cast<const uint2*>(o);
       }
@@ -141,6 +161,38 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const T* __restrict__ x, const
                                 (((int64_t)n * kOH + oy) * kOW + pt * 16 + px) * kK + c8 * 8) = v;
       }
       __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if constexpr (STATS) {
+    // over the 16 pixel lanes of each channel group, then the 4 waves through LDS (the row stage is
+    // free); one partial row per workgroup, fixed order: deterministic
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1) {
+          s1[mt][i] += __shfl_xor(s1[mt][i], m);
+          s2[mt][i] += __shfl_xor(s2[mt][i], m);
+        }
+    float* red = reinterpret_cast<float*>(rows);  // [4 waves][2][64]
+    __syncthreads();
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = 16 * mt + 4 * (lane >> 4) + i;
+          red[(wave * 2) * 64 + c] = s1[mt][i];
+          red[(wave * 2 + 1) * 64 + c] = s2[mt][i];
+        }
+    }
+    __syncthreads();
+    if (tid < 128) {
+      const int stat = tid >> 6, c = tid & 63;
+      const float v = red[(0 * 2 + stat) * 64 + c] + red[(1 * 2 + stat) * 64 + c] + red[(2 * 2 + stat) * 64 + c] +
+                      red[(3 * 2 + stat) * 64 + c];
+      part[((int64_t)stat * gridDim.x + blockIdx.x) * 64 + c] = v;
     }
   }
 }
@@ -333,16 +385,27 @@ bool conv_stem_supported(int N, int C, int H, int W, int K) {
   return N > 0 && C == 3 && H == kH && W == kW && K == kK;
 }
 
-void conv_stem_forward(int dt, const void* x, const void* w, void* y, int N, hipStream_t st) {
-  // persistent: two workgroups per CU (57 KB of LDS each), each walks row blocks blockIdx.x + k * grid
+int conv_stem_parts(int N) {
   const int nblk = N * (kOH / kRowsOut);
-  const dim3 grid((unsigned)(nblk < 512 ? nblk : 512));
+  return nblk < 512 ? nblk : 512;
+}
+
+void conv_stem_forward(int dt, const void* x, const void* w, void* y, int N, hipStream_t st, const float* kshift,
+                       float* part) {
+  // persistent: two workgroups per CU (57 KB of LDS each), each walks row blocks blockIdx.x + k * grid
+  const dim3 grid((unsigned)conv_stem_parts(N));
   switch (dt) {
     case kF16:
-      hipLaunchKernelGGL(k_stem_fwd<f16>, grid, dim3(256), 0, st, (const f16*)x, (const f16*)w, (f16*)y, N);
+      if (part) hipLaunchKernelGGL((k_stem_fwd<f16, true>), grid, dim3(256), 0, st, (const f16*)x, (const f16*)w,
+                                   (f16*)y, N, kshift, part);
+      else hipLaunchKernelGGL((k_stem_fwd<f16, false>), grid, dim3(256), 0, st, (const f16*)x, (const f16*)w, (f16*)y,
+                              N, nullptr, nullptr);
       break;
     case kBF16:
-      hipLaunchKernelGGL(k_stem_fwd<bf16>, grid, dim3(256), 0, st, (const bf16*)x, (const bf16*)w, (bf16*)y, N);
+      if (part) hipLaunchKernelGGL((k_stem_fwd<bf16, true>), grid, dim3(256), 0, st, (const bf16*)x, (const bf16*)w,
+                                   (bf16*)y, N, kshift, part);
+      else hipLaunchKernelGGL((k_stem_fwd<bf16, false>), grid, dim3(256), 0, st, (const bf16*)x, (const bf16*)w,
+                              (bf16*)y, N, nullptr, nullptr);
       break;
     default: throw std::runtime_error("conv_stem_forward: fp16 / bf16 only");
   }

@@ -391,6 +391,27 @@ class _StemConvFn(torch.autograd.Function):
         return gx, gw, None
 
 
+class _StemStatsFn(torch.autograd.Function):
+    """The stem convolution on the MFMA stem kernel with the stem BatchNorm's statistics partials in its
+    epilogue (no statistics pass over the 112x112x64 output); backward as :class:`_StemConvFn`."""
+
+    @staticmethod
+    def forward(ctx, x, weight, kshift):
+        from .._native import submodule
+
+        y, part = submodule("conv_cuda").stem_forward_stats(x, weight, kshift)
+        ctx.save_for_backward(x, weight)
+        ctx.mode = "gemm"
+        ctx.mark_non_differentiable(part)
+        ctx.set_materialize_grads(False)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, gy, _gpart):
+        gx, gw, _ = _StemConvFn.backward(ctx, gy)
+        return gx, gw, None
+
+
 class StemConv(nn.Conv2d):
     """nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False) with the MFMA stem forward (``mode``
     "auto" times it against MIOpen once, "gemm" forces it, "miopen" is plain nn.Conv2d)."""
@@ -702,16 +723,17 @@ class _BNConvFn(torch.autograd.Function):
         world = _world(process_group)
         C = y.size(1)
         count = float(y.numel() // C)
+        bumped = world == 1 and momentum >= 0
         if world > 1:
             sums = conv_bn.sum_parts(part, count)
             with comm_stats.timed("syncbn_fwd", sums):
                 _all_reduce(sums, process_group)
             mean, invstd, scale, shift, count_t = syncbn.merge_sums(sums, bn_w, bn_b, running_mean, running_var,
                                                                     momentum, eps, num_batches)
-        else:
+        else:  # one launch; with a fixed momentum it also bumps num_batches_tracked
             mean, invstd, scale, shift, count_t = syncbn.merge_parts(part, count, bn_w, bn_b, running_mean,
-                                                                     running_var, momentum, eps, num_batches)
-        if num_batches is not None:
+                                                                     running_var, momentum, eps, num_batches, bumped)
+        if num_batches is not None and not bumped:
             num_batches.add_(1)  # (the normalisation pass would have bumped it)
         if R == 3:
             out, part_out = submodule("conv_cuda").conv3x3_bn_forward(y, conv_w, scale, shift, True, kshift_out)
@@ -783,6 +805,8 @@ _FOLD_BN = os.environ.get("BH_FOLD_BN", "1") != "0"
 # BatchNorm + ReLU applied inside the consuming convolution (no normalisation pass) where that
 # convolution is the 3x3 direct kernel or the 1x1 strip GEMM (BH_FOLD_APPLY=0: separate passes)
 _FOLD_APPLY = os.environ.get("BH_FOLD_APPLY", "1") != "0"
+# the stem convolution's epilogue reduces the stem BatchNorm's statistics (BH_STEM_STATS=0: a pass)
+_STEM_STATS = os.environ.get("BH_STEM_STATS", "1") != "0"
 _PP_STATS = os.environ.get("BH_PP_STATS", "1") != "0"
 _FOLD_3X3_BWD = os.environ.get("BH_FOLD_3X3_BWD", "0") == "1"
 
@@ -945,8 +969,22 @@ class ResNet(nn.Module):
             layers.append(block(self.inplanes, planes, norm_layer=norm_layer, fused=self.fused))
         return nn.Sequential(*layers)
 
+    def _stem_stats_ok(self, x):
+        from ..ops import conv as bhconv
+        from ..parallel import SyncBatchNorm
+
+        bn = self.bn1
+        return (_FOLD_BN and _STEM_STATS and self.training and isinstance(self.conv1, StemConv) and self.conv1.mode == "gemm"
+                and isinstance(bn, SyncBatchNorm) and bn.track_running_stats and bn.running_mean is not None
+                and bn.running_mean.dtype == torch.float32 and x.dtype == self.conv1.weight.dtype
+                and bhconv.stem_supported(x, self.conv1.weight))
+
     def forward(self, x):
-        if self.stem_pool_fused:
+        if self.stem_pool_fused and self._stem_stats_ok(x):
+            # stem conv with the BatchNorm statistics in its epilogue, then BN + ReLU + max pool in one pass
+            y, part = _StemStatsFn.apply(x, self.conv1.weight, _kshift(self.bn1))
+            x = self.bn1.forward_from_stats(y, part) if self.bn1._pool_ok(y, None) else self.bn1(y)
+        elif self.stem_pool_fused:
             x = self.bn1(self.conv1(x))
         else:
             x = self.bn1(self.conv1(x)) if self.fused else self.relu(self.bn1(self.conv1(x)))

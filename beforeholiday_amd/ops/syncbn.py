@@ -111,17 +111,21 @@ def merge_sums(sums, weight, bias, running_mean, running_var, momentum, eps, num
     return _ref_final(mean, var_b, n, weight, bias, running_mean, running_var, momentum, eps, num_batches)
 
 
-def merge_parts(part, count, weight, bias, running_mean, running_var, momentum, eps, num_batches=None):
+def merge_parts(part, count, weight, bias, running_mean, running_var, momentum, eps, num_batches=None, bump=False):
     """Single rank: :func:`merge_sums` straight from a convolution epilogue's partials ``part [2, G, C]``
     (sums of ``x - running_mean`` and its square per workgroup) over ``count`` elements per channel --
-    one kernel on the GPU instead of ``conv_bn.sum_parts`` + ``merge_sums``."""
+    one kernel on the GPU instead of ``conv_bn.sum_parts`` + ``merge_sums``. ``bump`` (fixed momentum
+    only) also advances ``num_batches`` by one in the same launch."""
     if part.is_cuda:
         return _native().merge_parts(part, float(count), weight, bias, running_mean, running_var, momentum, eps,
-                                     num_batches)
+                                     num_batches, bump)
     C = part.size(2)
     sums = torch.cat([part.sum(1).reshape(-1), torch.tensor([float(count)], dtype=part.dtype)])
     assert sums.numel() == 2 * C + 1
-    return merge_sums(sums, weight, bias, running_mean, running_var, momentum, eps, num_batches)
+    out = merge_sums(sums, weight, bias, running_mean, running_var, momentum, eps, num_batches)
+    if bump and num_batches is not None:
+        num_batches += 1
+    return out
 
 
 def forward(x, z, scale, shift, relu, out_dtype=None, num_batches=None):

@@ -142,7 +142,7 @@ class SyncBatchnormFromStats(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, input, part, z, weight, bias, running_mean, running_var, eps, momentum, process_group,
-                fuse_relu, num_batches, link):
+                fuse_relu, num_batches, link, pool=None):
         world = _world(process_group)
         C = input.size(1)
         count = float(input.numel() // C)
@@ -155,15 +155,19 @@ class SyncBatchnormFromStats(torch.autograd.Function):
         else:  # one rank: partials -> statistics in one launch
             mean, invstd, scale, shift, count_t = syncbn.merge_parts(part, count, weight, bias, running_mean,
                                                                      running_var, momentum, eps, num_batches)
-        mask = None
-        if fuse_relu and syncbn.mask_ok(input, z):
+        mask = idx = None
+        if pool is not None:  # BN (+ ReLU) + max pool in one pass (the ResNet stem): the normalised
+            out, idx = syncbn.maxpool_forward(input, scale, shift, fuse_relu, *pool, True, num_batches)
+        elif fuse_relu and syncbn.mask_ok(input, z):
             out, mask = syncbn.forward_mask(input, z, scale, shift, num_batches)
         else:
             out = syncbn.forward(input, z, scale, shift, fuse_relu, None, num_batches)
         if link is not None:
             link.y, link.scale, link.shift, link.mean, link.relu = input, scale, shift, mean, fuse_relu
             link.sums = None
-        ctx.save_for_backward(input, None if mask is not None else z, weight, mean, invstd, scale, shift, count_t, mask)
+        ctx.save_for_backward(input, None if mask is not None else z, weight, mean, invstd, scale, shift, count_t, mask,
+                              idx)
+        ctx.pool = pool
         ctx.process_group = process_group
         ctx.world = world
         ctx.fuse_relu = fuse_relu
@@ -174,7 +178,9 @@ class SyncBatchnormFromStats(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_output):
-        input, z, weight, mean, invstd, scale, shift, count, mask = ctx.saved_tensors
+        input, z, weight, mean, invstd, scale, shift, count, mask, idx = ctx.saved_tensors
+        if ctx.pool is not None:
+            grad_output = syncbn.maxpool_backward(grad_output, idx, input.size(2), input.size(3), *ctx.pool)
         link = ctx.link
         need_w = weight is not None and (ctx.needs_input_grad[3] or ctx.needs_input_grad[4])
         if link is not None and link.sums is not None:
@@ -194,7 +200,7 @@ class SyncBatchnormFromStats(torch.autograd.Function):
         grad_input, grad_z = syncbn.backward_dgrad(grad_output, input, z, mean, invstd, weight, sums, count, scale,
                                                    shift, ctx.fuse_relu, ctx.has_z and ctx.needs_input_grad[2], mask)
         return grad_input, None, grad_z, (gw if need_w else None), (gb if need_w else None), None, None, None, None, \
-            None, None, None, None
+            None, None, None, None, None
 
 
 class SyncBatchNorm(_BatchNorm):
@@ -239,11 +245,13 @@ class SyncBatchNorm(_BatchNorm):
 
     def forward_from_stats(self, input, part, z=None, link=None):
         """Training forward from the producing convolution's statistics partials (see
-        :class:`SyncBatchnormFromStats`); ``part`` must be centred on ``self.running_mean``."""
+        :class:`SyncBatchnormFromStats`); ``part`` must be centred on ``self.running_mean``. With
+        ``fuse_maxpool`` the pooled tensor is returned (BN + ReLU + max pool in one pass)."""
         exp_avg = self.momentum if self.momentum is not None else -1.0
+        pool = self.fuse_maxpool if (self.fuse_maxpool is not None and self._pool_ok(input, z)) else None
         return SyncBatchnormFromStats.apply(input, part, z, self.weight, self.bias, self.running_mean, self.running_var,
                                             self.eps, exp_avg, self.process_group, self.fuse_relu,
-                                            self.num_batches_tracked, link)
+                                            self.num_batches_tracked, link, pool)
 
     def _bn(self, input, z, pool):
         if not self.training and self.track_running_stats:

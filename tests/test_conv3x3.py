@@ -274,3 +274,56 @@ def test_conv_wgrad_bn_prologue(dtype, shape):
     torch.testing.assert_close(gw.float(), bhconv.conv_wgrad(a, dy, R).float(), rtol=0,
                                atol=0.1 * tol * ref.abs().max().item())
     torch.testing.assert_close(gw.float(), ref, rtol=tol, atol=tol * ref.abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_stem_forward_statistics_epilogue(dtype):
+    """Stem conv with the BatchNorm statistics partials in its epilogue: the same output as the plain
+    stem kernel, and partials summing to the statistics of the stored output about kshift."""
+    from beforeholiday_amd._native import submodule
+
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randn(6, 3, 224, 224, device="cuda", dtype=dtype, generator=g).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(64, 3, 7, 7, device="cuda", generator=g) * 0.1).to(dtype)
+    k = torch.randn(64, device="cuda", generator=g) * 0.1
+    y, part = submodule("conv_cuda").stem_forward_stats(x, w, k)
+    assert torch.equal(y, bhconv.stem_conv(x, w))
+    assert part.shape[0] == 2 and part.shape[2] == 64
+    d = y.float().permute(0, 2, 3, 1).reshape(-1, 64) - k
+    ref = torch.stack([d.sum(0), (d * d).sum(0)])
+    got = part.sum(1)
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.gpu
+def test_resnet_stem_statistics_path_matches_unfolded():
+    """The fused ResNet stem with the statistics epilogue (conv -> BN + ReLU + max pool from the
+    partials) vs the statistics pass: same pooled output, stem / BatchNorm gradients and running
+    statistics to rounding (stem only: a whole random fp16 network amplifies rounding differences)."""
+    from beforeholiday_amd.models import resnet as R
+
+    torch.manual_seed(0)
+    m = R.resnet50_fused(layers=(1, 1, 1, 1)).cuda().to(memory_format=torch.channels_last).half()
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.modules.batchnorm._BatchNorm):
+            mod.float()
+    x = torch.randn(8, 3, 224, 224, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    assert m._stem_stats_ok(x)
+    state0 = {k: v.clone() for k, v in m.state_dict().items()}
+    g = torch.randn(8, 64, 56, 56, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    outs = []
+    for fold in (True, False):
+        m.load_state_dict(state0)
+        if fold:
+            y, part = R._StemStatsFn.apply(x, m.conv1.weight, R._kshift(m.bn1))
+            out = m.bn1.forward_from_stats(y, part)
+        else:
+            out = m.bn1(m.conv1(x))
+        out.backward(g)
+        outs.append((out.detach(), m.conv1.weight.grad.clone(), m.bn1.weight.grad.clone(), m.bn1.bias.grad.clone(),
+                     m.bn1.running_mean.clone(), m.bn1.running_var.clone(), m.bn1.num_batches_tracked.clone()))
+        m.zero_grad(set_to_none=True)
+    assert int(outs[0][6]) == int(outs[1][6]) == int(state0["bn1.num_batches_tracked"]) + 1
+    for a, b in zip(outs[0][:6], outs[1][:6]):
+        assert float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)) < 1e-2
