@@ -403,7 +403,22 @@ __global__ __launch_bounds__(64 * kMergeRows) void k_merge_parts(int G, int C, c
   if (c < C) {
     const float* p1 = part + c;
     const float* p2 = part + (int64_t)G * C + c;
-    for (int g = rg; g < G; g += kMergeRows) {
+    int g = rg;
+    // 8 rows of loads in flight per lane (the adds stay in row order: same sums as the plain loop)
+    for (; g + 7 * kMergeRows < G; g += 8 * kMergeRows) {
+      float u[8], v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        u[j] = p1[(int64_t)(g + j * kMergeRows) * C];
+        v[j] = p2[(int64_t)(g + j * kMergeRows) * C];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        a1 += u[j];
+        a2 += v[j];
+      }
+    }
+    for (; g < G; g += kMergeRows) {
       a1 += p1[(int64_t)g * C];
       a2 += p2[(int64_t)g * C];
     }

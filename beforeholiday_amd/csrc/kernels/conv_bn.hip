@@ -387,7 +387,16 @@ __global__ __launch_bounds__(64 * kSumRows) void k_sum_parts(int G, int N, const
   float acc = 0.f;
   if (c < N) {
     const float* src = part + (int64_t)which * G * N + c;
-    for (int g = rg; g < G; g += kSumRows) acc += src[(int64_t)g * N];
+    int g = rg;
+    // 8 rows of loads in flight per lane; the adds stay in row order (bn_merge_parts sums alike)
+    for (; g + 7 * kSumRows < G; g += 8 * kSumRows) {
+      float u[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) u[j] = src[(int64_t)(g + j * kSumRows) * N];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += u[j];
+    }
+    for (; g < G; g += kSumRows) acc += src[(int64_t)g * N];
   }
   sh[rg][cl] = acc;
   __syncthreads();
