@@ -132,7 +132,22 @@ __global__ __launch_bounds__(256) void k_act_bwd(const T* __restrict__ dy, const
   const int64_t r1 = r0 + rows_per_split < M ? r0 + rows_per_split : M;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (col0 < N) {
-    for (int64_t r = r0 + threadIdx.y; r < r1; r += kRowLanes) {
+    int64_t r = r0 + threadIdx.y;
+    if (vec && col0 + 8 <= N && !keep && act == kActNone) {
+      // bias gradient only (the common transformer case): four rows of 16-byte loads in flight per lane
+      for (; r + 3 * kRowLanes < r1; r += 4 * kRowLanes) {
+        float g[4][8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) VecIO<T>::load(dy + (r + u * kRowLanes) * N + col0, g[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) acc[k] += g[u][k];
+          if (dx) VecIO<T>::store(dx + (r + u * kRowLanes) * N + col0, g[u]);
+        }
+      }
+    }
+    for (; r < r1; r += kRowLanes) {
       const int64_t off = r * N + col0;
       float g[8], a[8];
       if (vec && col0 + 8 <= N) {
