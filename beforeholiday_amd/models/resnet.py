@@ -412,6 +412,22 @@ class _StemStatsFn(torch.autograd.Function):
         return gx, gw, None
 
 
+class _GlobalAvgPoolFn(torch.autograd.Function):
+    """Global average pool of a channels_last activation to [N, C]. Backward writes the broadcast
+    gradient straight into a channels_last tensor (one pass): nn.AdaptiveAvgPool2d's backward produced
+    an NCHW gradient that the BatchNorm backward then copied to channels_last twice."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = x.shape
+        return x.mean(dim=(2, 3))
+
+    @staticmethod
+    def backward(ctx, g):
+        n, c, h, w = ctx.shape
+        return (g / (h * w)).view(n, c, 1, 1).expand(n, c, h, w).contiguous(memory_format=torch.channels_last)
+
+
 class StemConv(nn.Conv2d):
     """nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False) with the MFMA stem forward (``mode``
     "auto" times it against MIOpen once, "gemm" forces it, "miopen" is plain nn.Conv2d)."""
@@ -632,7 +648,8 @@ class _Conv1DsFn(torch.autograd.Function):
                         conv_bn.supported(gd, wd_2d, b_trans=True, s2=(h, w), s2_scatter=True):
                     conv_bn.c1x1(gd, wd_2d, b_trans=True, s2=(h, w), s2_scatter=True, resid=gx2d)
                 else:
-                    gx2d.view(n, h, w, c)[:, ::2, ::2, :] += torch.mm(gd, wd_2d).view(n, h // 2, w // 2, c)
+                    # add_ on the strided view: `view[idx] += t` would also copy the view onto itself
+                    gx2d.view(n, h, w, c)[:, ::2, ::2, :].add_(torch.mm(gd, wd_2d).view(n, h // 2, w // 2, c))
             elif conv_bn.preferred(kd, c, gd.size(0)) and conv_bn.supported(gd, wd_2d, resid=True, b_trans=True):
                 gx2d, _ = conv_bn.c1x1(gd, wd_2d, resid=gx2d, b_trans=True)
             else:
@@ -990,7 +1007,10 @@ class ResNet(nn.Module):
             x = self.bn1(self.conv1(x)) if self.fused else self.relu(self.bn1(self.conv1(x)))
             x = self.maxpool(x)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
-        x = torch.flatten(self.avgpool(x), 1)
+        if self.fused and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last) and x.size(1) > 1:
+            x = _GlobalAvgPoolFn.apply(x)
+        else:
+            x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)
 
 
