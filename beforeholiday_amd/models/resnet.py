@@ -819,9 +819,14 @@ def _bn_conv(bn, y, part, conv_w, kshift_out, R):
 
 
 _FOLD_BN = os.environ.get("BH_FOLD_BN", "1") != "0"
-# BatchNorm + ReLU applied inside the consuming convolution (no normalisation pass) where that
-# convolution is the 3x3 direct kernel or the 1x1 strip GEMM (BH_FOLD_APPLY=0: separate passes)
-_FOLD_APPLY = os.environ.get("BH_FOLD_APPLY", "1") != "0"
+# BatchNorm + ReLU applied inside the consuming convolution instead of a normalisation pass
+# (BH_FOLD_APPLY): "all" (default) folds bn1 into the 3x3 conv and bn2 into conv3's 1x1 strip GEMM; "bn2"
+# / "bn1" only one of them; "none" keeps every pass. Same box: all 10443 / 10423, bn2 10430 / 10420,
+# none 10380 / 10386 img/s (profiles/resnet50_fold_apply_ab.txt): the 3x3 weight gradient's LDS
+# prologue costs about what the removed 64-channel bn1 pass saves, bn2's fold is the net gain
+_FOLD_APPLY = {"1": "all", "0": "none"}.get(os.environ.get("BH_FOLD_APPLY", "all"),
+                                            os.environ.get("BH_FOLD_APPLY", "all"))
+assert _FOLD_APPLY in ("all", "bn1", "bn2", "none"), f"BH_FOLD_APPLY={_FOLD_APPLY!r}"
 # the stem convolution's epilogue reduces the stem BatchNorm's statistics (BH_STEM_STATS=0: a pass)
 _STEM_STATS = os.environ.get("BH_STEM_STATS", "1") != "0"
 _PP_STATS = os.environ.get("BH_PP_STATS", "1") != "0"
@@ -884,23 +889,24 @@ class Bottleneck(nn.Module):
             y1, p1 = _Conv1x1BNFn.apply(x, self.conv1.weight, _kshift(self.bn1), None, box, False)
         l2 = None
         y3 = None
-        if _FOLD_APPLY and self.stride == 1 and bhconv.supported(y1, self.conv2.weight):
-            # bn1 + ReLU inside conv2's halo prologue; bn2 + ReLU inside conv3's strip GEMM where it runs
+        y2 = None
+        if _FOLD_APPLY in ("all", "bn1") and self.stride == 1 and bhconv.supported(y1, self.conv2.weight):
+            # bn1 + ReLU inside conv2's halo prologue (and its weight gradient's LDS prologue)
             y2, p2 = _bn_conv(self.bn1, y1, p1, self.conv2.weight, _kshift(self.bn2), 3)
-            if self._fold_bn2(y2):
-                y3, p3 = _bn_conv(self.bn2, y2, p2, self.conv3.weight, _kshift(self.bn3), 1)
-            else:
-                l2 = BNLink()
-                a2 = self.bn2.forward_from_stats(y2, p2, link=l2)
         else:
             l1 = BNLink()
             a1 = self.bn1.forward_from_stats(y1, p1, link=l1)
             if self.stride == 1 and bhconv.supported(a1, self.conv2.weight):
                 y2, p2 = _Conv3x3BNFn.apply(a1, self.conv2.weight, _kshift(self.bn2), l1)
-                l2 = BNLink()
-                a2 = self.bn2.forward_from_stats(y2, p2, link=l2)
             else:  # stride-2 3x3 (MIOpen): its BatchNorm computes its own statistics
                 a2 = self.bn2(self.conv2(a1))
+        if y2 is not None:
+            if _FOLD_APPLY in ("all", "bn2") and self._fold_bn2(y2):
+                # bn2 + ReLU inside conv3's strip-GEMM prologue (statistics of bn3 in its epilogue)
+                y3, p3 = _bn_conv(self.bn2, y2, p2, self.conv3.weight, _kshift(self.bn3), 1)
+            else:
+                l2 = BNLink()
+                a2 = self.bn2.forward_from_stats(y2, p2, link=l2)
         if y3 is None:
             y3, p3 = _Conv1x1BNFn.apply(a2, self.conv3.weight, _kshift(self.bn3), l2, None, False)
         if ds is not None:

@@ -93,7 +93,7 @@ def test_folded_and_unfolded_paths_agree():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg", [(256, 64, 1, 56, 32), (512, 128, 1, 28, 128)])
-def test_bn_apply_folded_into_conv2_and_conv3(cfg):
+def test_bn_apply_folded_into_conv2_and_conv3(cfg):  # BH_FOLD_APPLY=all vs none
     """bn1 + ReLU inside conv2 (3x3 halo prologue) and, at >= 100k pixels with <= 128 channels, bn2 +
     ReLU inside conv3 (strip-GEMM prologue; weight gradients through the wgrad kernel's LDS prologue):
     the same block with BH_FOLD_APPLY off (separate normalisation passes) agrees to rounding, including
@@ -107,7 +107,7 @@ def test_bn_apply_folded_into_conv2_and_conv3(cfg):
     state0 = {k: v.clone() for k, v in blk.state_dict().items()}
     try:
         outs = []
-        for fold in (True, False):
+        for fold in ("all", "none"):
             R._FOLD_APPLY = fold
             blk.load_state_dict(state0)
             xx = x.clone().requires_grad_()
