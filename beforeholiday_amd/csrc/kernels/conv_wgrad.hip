@@ -260,11 +260,15 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
     const char* ds = xs + BUFX;
     wait_vmcnt<0>();  // this wave's pieces of window `win` have landed ...
     if constexpr (PRO) {
-      int n0, y00;
-      win_origin(win, n0, y00);
-      asm volatile("" ::: "memory");
-      prologue(n0, y00, const_cast<char*>(xs));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // the first window's tiles here; every later window's were transformed at the end of the
+      // window before it, where the VALU work overlaps that window's last MFMAs in the pipe
+      if (win == w_begin) {
+        int n0, y00;
+        win_origin(win, n0, y00);
+        asm volatile("" ::: "memory");
+        prologue(n0, y00, const_cast<char*>(xs));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
     }
     raw_barrier();    // ... and everyone's; everyone is also done reading the other buffer
     // the next window's pieces are issued one behind each of the first MFMAs (their address math
@@ -273,6 +277,18 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
     int nn = 0, ny0 = 0;
     if (pre) win_origin(win + 1, nn, ny0);
     char* nbuf = smem + ((win + 1 - w_begin) & 1) * BUF;
+    // PRO: the next window's tiles, once this wave's DMA for them has landed (nobody reads that buffer
+    // during this window; the barrier at the next window's top publishes the result)
+    auto prologue_next = [&]() __attribute__((always_inline)) {
+      if constexpr (PRO) {
+        if (pre) {
+          wait_vmcnt<0>();
+          asm volatile("" ::: "memory");
+          prologue(nn, ny0, nbuf);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+      }
+    };
     auto read_a = [&](int ks, int buf) {
 #pragma unroll
       for (int t = 0; t < KT; ++t) fa[buf][t] = frag2(ds + 16 * ks * DSL + 64 * t, a_off, a_off + 4 * DSL);
@@ -310,6 +326,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
         if (u + 1 < KL && 2 * (u + 1) + half < KSTEPS) rd(u + 1, cur ^ 1);
         __builtin_amdgcn_sched_barrier(0);
       }
+      prologue_next();
       continue;
     }
     read_a(0, 0);
@@ -335,6 +352,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
 #pragma unroll
     for (int t = KSTEPS * NOFF; t < NPW; ++t)  // pieces left over when a window has few MFMAs (R = 1)
       if (pre) issue_piece(t, nn, ny0, nbuf);
+    prologue_next();
   }
 
   if constexpr (R == 1) {
