@@ -67,6 +67,7 @@ struct ConvWgradArgs {
 };
 struct ConvWgradGeo {
   int G4 = 0, TH = 0, ksteps = 0, wpi = 0, nwin = 0, ctiles = 0, tiles = 0, wpw = 0, splits = 0, grid = 0, kt = 1, ct = 1, parts = 0;
+  bool wide = false;  // 1x1: 256 x 128 tiles, 64-pixel windows
 };
 // false when the kernel does not cover the shape (C, K % 64, 16-byte alignment, window fits in LDS)
 bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo);

@@ -24,6 +24,7 @@
 #include "bh/device.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
@@ -111,13 +112,19 @@ BH_DEVICE i4v frag2(const char* img, int lo, int hi) {
 // the consumers): every lane rewrites the X chunks its own LDS-DMA brought in -- relu(x * scale + shift),
 // rounded as the normalisation pass would -- after they land and before the window barrier; chunks of
 // pixels outside the image stay zero (they pad the normalised activation).
-template <typename T, int R, int G4, int TH, int KT, int CT = 1, bool PRO = false>
+// WIDE (1x1 only): 256 output channels per workgroup -- the four k quarters of 64 go to the four wave
+// pairs and each wave runs every k-step of the window (no split of the k-steps between the two waves of
+// a SIMD, no LDS hand-off at the end) -- which cuts the bytes staged per MFMA by a quarter; the dY slot
+// grows to 512 + 64 B (144 dwords: again four distinct bank quarters) and the window to 64 pixels.
+template <typename T, int R, int G4, int TH, int KT, int CT = 1, bool PRO = false, bool WIDE = false>
 __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, ConvWgradGeo g, float* __restrict__ ws,
                                                            T* __restrict__ out) {
   constexpr int P = (R - 1) / 2, RR = R * R;
   constexpr int HC = 4 * G4 + 2 * P, KSTEPS = (TH * G4 + 3) / 4;
   constexpr int XS = (TH + 2 * P) * HC, DS = KSTEPS * 16;  // X halo / dY pixel slots per window
-  constexpr int DSL = dslot<KT>(), TK = kTile * KT;  // dY slot bytes, output channels per workgroup
+  constexpr int KW = WIDE ? 4 : 2;  // k sub-tiles of 32 KT across the waves
+  static_assert(!WIDE || (R == 1 && KT == 2), "wide tiles: 1x1, two 32-row sub-tiles per wave");
+  constexpr int DSL = WIDE ? 576 : dslot<KT>(), TK = 32 * KT * KW;  // dY slot bytes, output channels per workgroup
   constexpr int XSL = dslot<CT>(), TC = kTile * CT;  // X slot bytes, input channels per workgroup
   constexpr int BUFX = (XS * XSL + 1023) / 1024 * 1024, BUF = BUFX + (DS * DSL + 1023) / 1024 * 1024;
   constexpr int XP = BUFX / 1024, DP = (BUF - BUFX) / 1024;  // 1-KiB LDS-DMA pieces
@@ -139,7 +146,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int kw = (wave >> 1) & 1, cw = wave & 1, half = wave >> 2;
+  const int kw = WIDE ? wave >> 1 : (wave >> 1) & 1, cw = wave & 1, half = WIDE ? 0 : wave >> 2;
   // R = 3: the two waves of a SIMD split the offsets (rs0 .. rs0 + noff - 1); R = 1 (one offset):
   // they split the k-steps instead (half h takes ks = h, h + 2, ...) and write separate partials
   const int rs0 = R == 1 ? 0 : half * NOFF, noff = R == 1 ? NOFF : min(NOFF, RR - rs0);
@@ -176,7 +183,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
     } else {
       const int dbyte = byte, dsl = dbyte / DSL, dch = (dbyte - dsl * DSL) >> 4;
       const int grp = dsl >> 2, row = grp / G4, x = 4 * (grp - row * G4) + (dsl & 3);
-      const bool ok = piece < DP && dch < 8 * KT && dsl < DS && row < TH && x < W;
+      const bool ok = piece < DP && dch < TK / 8 && dsl < DS && row < TH && x < W;
       rel[i] = ((row * W + x) * K + k0 + dch * 8) * 2;
       hrow[i] = ok ? row : kBad;
     }
@@ -301,10 +308,11 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
       fb[buf][j] = frag2(base, x_off[ks][0], x_off[ks][1]);
     };
     if constexpr (R == 1) {
-      // k-step ks = 2u + half; the X slots of a flat 1x1 window are linear in ks
-      constexpr int KL = (KSTEPS + 1) / 2;
+      // k-step ks = 2u + half (WIDE: ks = u); the X slots of a flat 1x1 window are linear in ks
+      constexpr int KL = WIDE ? KSTEPS : (KSTEPS + 1) / 2;
+      auto kstep = [&](int u) { return WIDE ? u : 2 * u + half; };
       auto rd = [&](int u, int buf) {
-        const int ks = 2 * u + half;
+        const int ks = kstep(u);
 #pragma unroll
         for (int t = 0; t < KT; ++t) fa[buf][t] = frag2(ds + 16 * ks * DSL + 64 * t, a_off, a_off + 4 * DSL);
 #pragma unroll
@@ -317,13 +325,13 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
 #pragma unroll
       for (int u = 0; u < KL; ++u) {
         const int cur = u & 1;
-        if (2 * u + half < KSTEPS) {
+        if (kstep(u) < KSTEPS) {
 #pragma unroll
           for (int j = 0; j < NOFF; ++j)
 #pragma unroll
             for (int t = 0; t < KT; ++t) acc[j][t] = MfmaW<T>::run(fa[cur][t], fb[cur][j], acc[j][t]);
         }
-        if (u + 1 < KL && 2 * (u + 1) + half < KSTEPS) rd(u + 1, cur ^ 1);
+        if (u + 1 < KL && kstep(u + 1) < KSTEPS) rd(u + 1, cur ^ 1);
         __builtin_amdgcn_sched_barrier(0);
       }
       prologue_next();
@@ -355,7 +363,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
     prologue_next();
   }
 
-  if constexpr (R == 1) {
+  if constexpr (R == 1 && !WIDE) {
     // the two waves of a SIMD hold partial sums of the same tile (even / odd k-steps): the odd
     // half hands its accumulators to the even half through LDS, so one partial slab per split
     float* red = reinterpret_cast<float*>(smem);  // NOFF * KT * 16 floats per lane, 4 waves
@@ -449,11 +457,22 @@ bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo) {
   ConvWgradGeo g;
   if (a.R == 1) {
     // no halo: the N*H*W pixels are one flat list, 112-pixel windows (one row of 28 groups)
-    if (((int64_t)a.N * a.H * a.W) % 112) return false;
-    g.G4 = 28;
+    // wide tiles (K % 256, C % 128): 64-pixel windows (two window buffers of 56 KiB)
+    static const bool wide_env = [] {
+      const char* e = getenv("BH_WGRAD_WIDE");
+      return !(e && atoi(e) == 0);
+    }();
+    const int64_t npix = (int64_t)a.N * a.H * a.W;
+    // (and at least 4 such tiles: with fewer, the extra split partials cost more than the staging saves,
+    // measured on the 128 -> 512 layer-2 shape)
+    g.wide = wide_env && a.stride == 1 && a.K % 256 == 0 && a.C % 128 == 0 && npix % 64 == 0 &&
+             (a.K / 256) * (a.C / 128) >= 4;
+    const int win = g.wide ? 64 : 112;
+    if (npix % win) return false;
+    g.G4 = win / 4;
     g.TH = 1;
     g.wpi = 1;
-    g.nwin = (int)((int64_t)a.N * a.H * a.W / 112);
+    g.nwin = (int)((int64_t)a.N * a.H * a.W / win);
   } else {
     // ~112 pixels per window: 2 rows at W = 56, 4 at 28, 7 at 14 / 7 (the instantiated geometries)
     g.G4 = (a.W + 3) / 4;
@@ -470,7 +489,7 @@ bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo) {
   g.kt = (a.K % 128 == 0 && (a.R == 1 || g.G4 == 4 || g.G4 == 2)) ? 2 : 1;
   g.ct = (a.R == 1 && a.C % 128 == 0) ? 2 : 1;  // 1x1: 128 input channels per workgroup where C allows
   g.ctiles = a.C / (kTile * g.ct);
-  g.tiles = (a.K / (kTile * g.kt)) * g.ctiles;
+  g.tiles = (a.K / (kTile * g.kt * (g.wide ? 2 : 1))) * g.ctiles;
   // one round of workgroups (one per CU), split over the windows
   int splits = std::max(1, 256 / g.tiles);
   splits = std::min(splits, g.nwin);
@@ -493,7 +512,7 @@ void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws
     b.wout = a.W;
     b.N = g.nwin;
     b.H = 1;
-    b.W = 112;
+    b.W = 4 * g.G4;
   }
   auto run = [&](auto tt) {
     using T = typename decltype(tt)::type;
@@ -501,7 +520,8 @@ void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws
     auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(g.grid), dim3(kThreads), 0, st, b, g, ws, out); };
     auto pick = [&](auto proc) {
       constexpr bool P = decltype(proc)::value;
-      if (a.R == 1) {
+      if (a.R == 1 && g.wide) go(k_conv_wgrad<T, 1, 16, 1, 2, 2, P, true>);
+      else if (a.R == 1) {
         if (g.ct == 2) g.kt == 2 ? go(k_conv_wgrad<T, 1, 28, 1, 2, 2, P>) : go(k_conv_wgrad<T, 1, 28, 1, 1, 2, P>);
         else g.kt == 2 ? go(k_conv_wgrad<T, 1, 28, 1, 2, 1, P>) : go(k_conv_wgrad<T, 1, 28, 1, 1, 1, P>);
       }

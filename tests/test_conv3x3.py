@@ -80,6 +80,9 @@ WGRAD_SHAPES = [  # N, C, K, H, W, R
     (2, 64, 64, 56, 56, 3), (3, 128, 128, 28, 28, 3), (5, 256, 64, 14, 14, 3), (7, 64, 128, 7, 7, 3),
     (9, 64, 64, 16, 16, 3), (3, 64, 192, 13, 13, 3), (4, 128, 64, 5, 5, 3), (2, 64, 256, 14, 14, 3),
     (2, 64, 256, 56, 56, 1), (4, 256, 128, 14, 14, 1), (1, 64, 64, 7, 16, 1), (2, 128, 64, 28, 28, 1),
+    # 1x1 with K % 256, C % 128 and >= 4 such tiles: 256 x 128 tiles on 64-pixel windows (pixel count
+    # % 64), else 112
+    (4, 256, 512, 28, 28, 1), (1, 256, 512, 16, 16, 1), (64, 512, 2048, 7, 7, 1), (2, 128, 256, 28, 28, 1),
 ]
 
 
@@ -254,7 +257,7 @@ def test_gemm_n64_kernel(dtype, shape, resid):
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("shape", [(2, 64, 64, 56, 56, 3), (4, 128, 128, 28, 28, 3), (3, 256, 256, 14, 14, 3),
                                    (4, 512, 512, 7, 7, 3), (2, 64, 128, 13, 13, 3), (2, 64, 256, 56, 56, 1),
-                                   (4, 128, 512, 28, 28, 1), (4, 256, 64, 14, 14, 1)])
+                                   (4, 128, 512, 28, 28, 1), (4, 256, 64, 14, 14, 1), (16, 256, 1024, 14, 14, 1)])
 def test_conv_wgrad_bn_prologue(dtype, shape):
     """Weight gradient with the folded BatchNorm + ReLU prologue (x raw, relu(x * scale + shift) applied to
     the LDS tiles) ~ the plain kernel on the materialised activation, and close to fp32
