@@ -197,6 +197,11 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
     return odd ? (got | (keep << 16)) : (keep | (got << 16));
   };
   f16v acc[NT];
+  // Narrow tiles (NC = 64): the residual / previous-output values the epilogue reads are loaded at the
+  // top of the strip's last chunk, so their HBM latency hides behind that chunk's MFMAs instead of
+  // stalling the epilogue (one 2-byte column load per row: nothing to coalesce them into). Wider tiles
+  // keep the per-tile loads (hoisting 64+ values spills).
+  constexpr bool kHoist = (RES != (EPI == kC1x1Bwd)) && S2 != 2 && NT * 16 <= 32;
   auto process = [&](int i, i4v(&a)[KS]) {
     const int q = i / nch, c = i - q * nch;
     const int strip = first + q * stride;
@@ -221,6 +226,17 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = from_f<T>(fmaxf(fmaf(to_f<T>(v[j]), sc[j], sh[j]), 0.f));
         a[s] = __builtin_bit_cast(i4v, v);
+      }
+    }
+    T xh[kHoist ? NT : 1][16];
+    if constexpr (kHoist) {
+      if (c + 1 == nch) {
+        const T* src = RES ? Rp : Yp;
+        const int64_t rh = (int64_t)strip * 32 + 4 * h;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) xh[t][v] = src[(rh + 8 * (v >> 2) + (v & 3)) * N + col0 + 32 * t + r];
       }
     }
     int boff = r * RS + 16 * h + c * KC * 2;
@@ -257,7 +273,10 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
       const int col = col0 + 32 * t + r;
       unsigned int o_prev = 0;
       float xr[16];
-      if constexpr (RES || EPI == kC1x1Bwd) {
+      if constexpr (kHoist) {
+#pragma unroll
+        for (int v = 0; v < 16; ++v) xr[v] = to_f<T>(xh[t][v]);
+      } else if constexpr (RES || EPI == kC1x1Bwd) {
         const T* src = RES ? Rp : Yp;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
