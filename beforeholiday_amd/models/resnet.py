@@ -803,7 +803,8 @@ class _BNConvFn(torch.autograd.Function):
             sums, gw, gb = syncbn.backward_reduce(dA, y, None, mean, invstd, scale, shift, True, bn_w, need_w, None)
         else:
             gw = (sums[C:] * invstd).to(bn_w.dtype) if need_w else None
-            gb = sums[:C].to(bn_w.dtype) if need_w else None
+            # a copy: `sums` is all-reduced in place below, the bias gradient stays this rank's own
+            gb = sums[:C].to(bn_w.dtype, copy=True) if need_w else None
         if ctx.world > 1:
             with comm_stats.timed("syncbn_bwd", sums):
                 _all_reduce(sums, ctx.process_group)

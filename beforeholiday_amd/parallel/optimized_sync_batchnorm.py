@@ -188,7 +188,8 @@ class SyncBatchnormFromStats(torch.autograd.Function):
             link.sums = None
             C = input.size(1)
             gw = (sums[C:] * invstd).to(weight.dtype) if need_w else None
-            gb = sums[:C].to(weight.dtype) if need_w else None
+            # a copy: `sums` is all-reduced in place below, the bias gradient stays this rank's own
+            gb = sums[:C].to(weight.dtype, copy=True) if need_w else None
         else:
             sums, gw, gb = syncbn.backward_reduce(grad_output, input, z, mean, invstd, scale, shift, ctx.fuse_relu,
                                                   weight, need_w, mask)

@@ -13,7 +13,7 @@ def _rel(a, b):
     return float((a - b).norm() / b.norm().clamp_min(1e-12))
 
 
-def _block(inplanes, planes, stride, dt):
+def _block(inplanes, planes, stride, dt, pg=None):
     from beforeholiday_amd.models import resnet as R
     from beforeholiday_amd.parallel import SyncBatchNorm
 
@@ -25,7 +25,7 @@ def _block(inplanes, planes, stride, dt):
     ref = R.Bottleneck(inplanes, planes, stride, ds_ref).cuda()
 
     def norm(c, fuse_relu=False):
-        return SyncBatchNorm(c, channel_last=True, fuse_relu=fuse_relu)
+        return SyncBatchNorm(c, process_group=pg, channel_last=True, fuse_relu=fuse_relu)
 
     if ds_ref is not None:
         ds = torch.nn.Sequential(torch.nn.Conv2d(inplanes, planes * 4, 1, stride=stride, bias=False), norm(planes * 4))
@@ -128,3 +128,48 @@ def test_bn_apply_folded_into_conv2_and_conv3(cfg):  # BH_FOLD_APPLY=all vs none
             assert _rel(outs[0][3][k], outs[1][3][k]) < 1e-3, k
         elif "num_batches" in k:
             assert int(outs[0][3][k]) == int(outs[1][3][k]) == int(state0[k]) + 1, k
+
+
+def _fold_two_ranks(rank, world):
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)  # both ranks share the one GPU of the box (gloo process group)
+    singles = [dist.new_group([r]) for r in range(world)]
+    B, C, HW = 32, 256, 56
+    torch.manual_seed(7)
+    x = torch.randn(world * B, C, HW, HW, device="cuda").half().contiguous(memory_format=torch.channels_last)
+
+    def run(pg, xs):
+        _, _, blk = _block(C, 64, 1, torch.float16, pg)
+        y2 = torch.empty(xs.shape[0], 64, HW, HW, device="cuda", dtype=torch.half)
+        assert blk._fold_ok(xs) and blk._fold_bn2(y2.contiguous(memory_format=torch.channels_last))
+        xx = xs.clone().requires_grad_()
+        o = blk(xx)
+        (o.float().square().sum() / x.shape[0]).backward()  # per-sample mean: fp16 gradients stay normal
+        return (o.detach(), xx.grad, [p.grad.clone() for p in blk.parameters()],
+                {k: v.clone() for k, v in blk.state_dict().items()})
+
+    sl = slice(rank * B, (rank + 1) * B)
+    o, gx, gp, st = run(None, x[sl])  # statistics over both ranks' halves
+    for g in gp:
+        dist.all_reduce(g)
+    o1, gx1, gp1, st1 = run(singles[rank], x)  # the whole batch on this rank alone
+    assert _rel(o, o1[sl]) < 5e-3
+    assert _rel(gx, gx1[sl]) < 2e-2
+    for a, b in zip(gp, gp1):
+        assert _rel(a, b) < 2e-2
+    for k in st:
+        if "running" in k:
+            assert _rel(st[k], st1[k]) < 1e-3, k
+        elif "num_batches" in k:
+            assert int(st[k]) == int(st1[k]) == 1, k
+
+
+@pytest.mark.gpu
+def test_folded_block_two_ranks_equals_one_rank_double_batch():
+    """The folded path at world 2 (statistics partials summed per rank, all-reduced, merged; backward
+    sums all-reduced the same way): two gloo ranks on one GPU with half the batch each equal one rank
+    with the whole batch -- outputs, input gradients, all-reduced parameter gradients, running stats."""
+    from _dist import run_distributed
+
+    run_distributed(_fold_two_ranks, 2)
