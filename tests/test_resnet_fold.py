@@ -130,19 +130,18 @@ def test_bn_apply_folded_into_conv2_and_conv3(cfg):  # BH_FOLD_APPLY=all vs none
             assert int(outs[0][3][k]) == int(outs[1][3][k]) == int(state0[k]) + 1, k
 
 
-def _fold_two_ranks(rank, world):
+def _fold_two_ranks(rank, world, cfg):
     import torch.distributed as dist
 
     torch.cuda.set_device(0)  # both ranks share the one GPU of the box (gloo process group)
     singles = [dist.new_group([r]) for r in range(world)]
-    B, C, HW = 32, 256, 56
+    C, planes, stride, HW, B = cfg
     torch.manual_seed(7)
     x = torch.randn(world * B, C, HW, HW, device="cuda").half().contiguous(memory_format=torch.channels_last)
 
     def run(pg, xs):
-        _, _, blk = _block(C, 64, 1, torch.float16, pg)
-        y2 = torch.empty(xs.shape[0], 64, HW, HW, device="cuda", dtype=torch.half)
-        assert blk._fold_ok(xs) and blk._fold_bn2(y2.contiguous(memory_format=torch.channels_last))
+        _, _, blk = _block(C, planes, stride, torch.float16, pg)
+        assert blk._fold_ok(xs)
         xx = xs.clone().requires_grad_()
         o = blk(xx)
         (o.float().square().sum() / x.shape[0]).backward()  # per-sample mean: fp16 gradients stay normal
@@ -166,10 +165,69 @@ def _fold_two_ranks(rank, world):
 
 
 @pytest.mark.gpu
-def test_folded_block_two_ranks_equals_one_rank_double_batch():
+@pytest.mark.parametrize("cfg", [(256, 64, 1, 56, 32), (256, 128, 2, 56, 16), (512, 128, 1, 28, 128)])
+def test_folded_block_two_ranks_equals_one_rank_double_batch(cfg):
     """The folded path at world 2 (statistics partials summed per rank, all-reduced, merged; backward
     sums all-reduced the same way): two gloo ranks on one GPU with half the batch each equal one rank
-    with the whole batch -- outputs, input gradients, all-reduced parameter gradients, running stats."""
+    with the whole batch -- outputs, input gradients, all-reduced parameter gradients, running stats.
+    Shapes: layer 1 with bn2 folded into conv3 (>= 100k pixels per rank), the stride-2 downsample
+    block, layer 2 with bn2 folded."""
     from _dist import run_distributed
 
-    run_distributed(_fold_two_ranks, 2)
+    run_distributed(_fold_two_ranks, 2, cfg)
+
+
+def _net_two_ranks(rank, world):
+    import torch.distributed as dist
+    from beforeholiday_amd.models import resnet as R
+    from beforeholiday_amd.parallel import SyncBatchNorm
+
+    torch.cuda.set_device(0)
+    singles = [dist.new_group([r]) for r in range(world)]
+    B = 16
+    torch.manual_seed(11)
+    x = torch.randn(world * B, 3, 224, 224, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (world * B,), device="cuda")
+
+    def run(pg, xs, ys):
+        def norm(c, fuse_relu=False, fuse_maxpool=None):
+            return SyncBatchNorm(c, process_group=pg, channel_last=True, fuse_relu=fuse_relu, fuse_maxpool=fuse_maxpool)
+
+        torch.manual_seed(0)
+        net = R.ResNet(R.Bottleneck, [1, 1, 1, 1], num_classes=10, norm_layer=norm, fused=True,
+                       stem_pool_fused=True).cuda().to(memory_format=torch.channels_last).half()
+        for m in net.modules():
+            if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+                m.float()
+        out = net(xs)
+        loss = torch.nn.functional.cross_entropy(out.float(), ys, reduction="sum") / x.shape[0]
+        loss.backward()
+        return (loss.detach(), {n: p.grad.clone() for n, p in net.named_parameters()},
+                {k: v.clone() for k, v in net.state_dict().items() if "running" in k})
+
+    sl = slice(rank * B, (rank + 1) * B)
+    loss, g, st = run(None, x[sl], y[sl])
+    dist.all_reduce(loss)
+    for t in g.values():
+        dist.all_reduce(t)
+    loss1, g1, st1 = run(singles[rank], x, y)
+    # the noise floor: the same single-rank step with the two halves of the batch swapped (another
+    # summation order). Gradients that downstream BatchNorms nearly cancel (the stem BN's bias) are
+    # rounding noise at any order; a world-size factor (the bug class this guards) sits far above it
+    perm = torch.cat([torch.arange(B, world * B), torch.arange(0, B)]).cuda()
+    _, g1p, _ = run(singles[rank], x[perm], y[perm])
+    assert abs(float(loss) - float(loss1)) < 1e-3 * abs(float(loss1))
+    for n in g:
+        floor = _rel(g1p[n], g1[n])
+        assert _rel(g[n], g1[n]) < 3 * floor + 2e-2, (n, _rel(g[n], g1[n]), floor)
+    for k in st:
+        assert _rel(st[k], st1[k]) < 2e-3, k
+
+
+@pytest.mark.gpu
+def test_fused_resnet_two_ranks_equals_one_rank_double_batch():
+    """The fused ResNet (stem statistics epilogue + folded bottlenecks + fused max pool, [1, 1, 1, 1]
+    blocks at 224x224) on two gloo ranks sharing one GPU vs one rank with the double batch."""
+    from _dist import run_distributed
+
+    run_distributed(_net_two_ranks, 2)
