@@ -177,7 +177,7 @@ def test_folded_block_two_ranks_equals_one_rank_double_batch(cfg):
     run_distributed(_fold_two_ranks, 2, cfg)
 
 
-def _net_two_ranks(rank, world):
+def _net_two_ranks(rank, world, exchange):
     import torch.distributed as dist
     from beforeholiday_amd.models import resnet as R
     from beforeholiday_amd.parallel import SyncBatchNorm
@@ -206,7 +206,13 @@ def _net_two_ranks(rank, world):
                 {k: v.clone() for k, v in net.state_dict().items() if "running" in k})
 
     sl = slice(rank * B, (rank + 1) * B)
-    loss, g, st = run(None, x[sl], y[sl])
+    pg = None
+    if exchange == "ipc":  # bench.py's default on one node: statistics through HIP-IPC peer buffers
+        from beforeholiday_amd.contrib.peer_memory import build_peer_allreduce
+
+        pg = build_peer_allreduce(capacity=1 << 13)
+        assert pg is not None, "IPC peer all-reduce setup / probe failed"
+    loss, g, st = run(pg, x[sl], y[sl])
     dist.all_reduce(loss)
     for t in g.values():
         dist.all_reduce(t)
@@ -225,9 +231,11 @@ def _net_two_ranks(rank, world):
 
 
 @pytest.mark.gpu
-def test_fused_resnet_two_ranks_equals_one_rank_double_batch():
+@pytest.mark.parametrize("exchange", ["group", "ipc"])
+def test_fused_resnet_two_ranks_equals_one_rank_double_batch(exchange):
     """The fused ResNet (stem statistics epilogue + folded bottlenecks + fused max pool, [1, 1, 1, 1]
-    blocks at 224x224) on two gloo ranks sharing one GPU vs one rank with the double batch."""
+    blocks at 224x224) on two gloo ranks sharing one GPU vs one rank with the double batch; SyncBN
+    statistics through the gloo group or through the HIP-IPC PeerAllReduce (bench.py's default)."""
     from _dist import run_distributed
 
-    run_distributed(_net_two_ranks, 2)
+    run_distributed(_net_two_ranks, 2, exchange)
