@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--layers", type=int, default=24)
     ap.add_argument("--opt-level", default="O2", choices=["O2", "O5"])
     ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU")
     from beforeholiday_amd.utils import gemm_tuning
 
     gemm_tuning.add_argument(ap)
@@ -39,11 +41,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend == "gloo":
+        local_rank %= max(1, torch.cuda.device_count())  # rehearsal: several ranks may share one GPU
     torch.cuda.set_device(local_rank)
     gemm_tuning.setup(args.gemm_table)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
-    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+    if args.backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
 
     from beforeholiday_amd import amp
     from beforeholiday_amd._native import require_native
@@ -55,7 +62,7 @@ def main():
     from beforeholiday_amd.transformer import parallel_state, tensor_parallel
 
     require_native("bench_bert")
-    parallel_state.initialize_model_parallel(1, 1)
+    parallel_state.initialize_model_parallel(1, 1, default_backend=args.backend)
     tensor_parallel.model_parallel_cuda_manual_seed(1234)
     fp16 = args.opt_level == "O2"
     cfg = TransformerConfig(hidden_size=1024, num_layers=args.layers, num_attention_heads=16, ffn_hidden_size=4096,
