@@ -86,6 +86,14 @@ def _unscale_into_models(scaler, params, stash, scale_override=None):
         scaler.unscale_with_stashed(accum, old, accum, scale_override=(grads_have, stashed_have, out_scale))
 
 
+def _keep(p):
+    """``p.grad`` to set aside across the next backward. A DDP gradient-as-bucket-view gradient lives in
+    the bucket buffer that the next backward overwrites (parallel/distributed.py), so it is cloned."""
+    from ..parallel.distributed import grad_is_bucket_view
+
+    return p.grad.clone() if grad_is_bucket_view(p) else p.grad
+
+
 class _GradPlan(object):
     def __init__(self, opt):
         self.opt = opt
@@ -139,7 +147,7 @@ class _ModelPlan(_GradPlan):
         self.ensure()
         for params, stash in self._lists():
             for i, p in enumerate(params):
-                stash[i], p.grad = p.grad, None
+                stash[i], p.grad = _keep(p), None
 
     def finish(self, scaler):
         self.ensure()
@@ -201,7 +209,7 @@ class _MasterPlan(_GradPlan):
         for p in st.all_fp16_params:  # 16-bit grads are folded into the fp32 master grads: drop them
             p.grad = None
         for i, p in enumerate(st.all_fp32_from_fp32_params):
-            st.all_fp32_from_fp32_grad_stash[i], p.grad = p.grad, None
+            st.all_fp32_from_fp32_grad_stash[i], p.grad = _keep(p), None
 
     def finish(self, scaler):
         self.ensure()
@@ -234,19 +242,11 @@ class _MasterPlan(_GradPlan):
         # set_to_none=True by default (PyTorch >= 2.0 semantics): the next prepare() drops / stashes these
         # grads anyway, so zero-filling them would only add one fill kernel per parameter plus a
         # stashed-gradient axpby pass after backward. set_to_none=False keeps the reference's zeroing.
+        from ..optimizers._common import zero_param_grads
+
         self.ensure()
         st = self.stash
-        grads = []
-        for p in st.all_fp16_params + st.all_fp32_from_fp32_params:
-            if p.grad is None:
-                continue
-            if set_to_none:
-                p.grad = None
-            else:
-                p.grad.detach_()
-                grads.append(p.grad)
-        if grads:
-            torch._foreach_zero_(grads)
+        zero_param_grads(st.all_fp16_params + st.all_fp32_from_fp32_params, set_to_none)
         for p in st.all_fp32_from_fp16_params:
             p.grad = None
 
@@ -267,9 +267,9 @@ class _FusedSGDMasterPlan(_MasterPlan):
         st.all_fp16_grad_stash = getattr(st, "all_fp16_grad_stash", [])
         st.all_fp16_grad_stash.extend([None] * (len(st.all_fp16_params) - len(st.all_fp16_grad_stash)))
         for i, p in enumerate(st.all_fp16_params):
-            st.all_fp16_grad_stash[i], p.grad = p.grad, None
+            st.all_fp16_grad_stash[i], p.grad = _keep(p), None
         for i, p in enumerate(st.all_fp32_from_fp32_params):
-            st.all_fp32_from_fp32_grad_stash[i], p.grad = p.grad, None
+            st.all_fp32_from_fp32_grad_stash[i], p.grad = _keep(p), None
 
     def finish(self, scaler):
         opt = self.opt

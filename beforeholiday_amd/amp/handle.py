@@ -59,12 +59,22 @@ class _StepGate(object):
         return out
 
 
+def _gated_step(self, closure=None):
+    return self._amp_stash.step_gate(closure)
+
+
 def _gate(optimizer):
+    """The optimizer's :class:`_StepGate`, installed on first use. ``optimizer.step`` becomes a bound
+    method (``types.MethodType``), not the gate object itself: torch's LR schedulers wrap
+    ``optimizer.step`` through its ``__func__`` (``patch_track_step_called``), so a scheduler built
+    after the first ``scale_loss`` still works."""
+    import types
+
     stash = optimizer._amp_stash
     gate = getattr(stash, "step_gate", None)
     if gate is None:
         gate = stash.step_gate = _StepGate(optimizer, optimizer.step)
-        optimizer.step = gate
+        optimizer.step = types.MethodType(_gated_step, optimizer)
     return gate
 
 

@@ -38,13 +38,9 @@ class FP16_Optimizer(object):
         self.verbose = verbose
 
     def zero_grad(self, set_grads_to_None=True):
-        for group in self.fp16_groups:
-            for p in group:
-                if set_grads_to_None:
-                    p.grad = None
-                elif p.grad is not None:
-                    p.grad.detach_()
-                    p.grad.zero_()
+        from ...optimizers._common import zero_param_grads
+
+        zero_param_grads([p for group in self.fp16_groups for p in group], set_grads_to_None)
 
     def step(self, closure=None):
         fp16_grads = [[p.grad for p in group] for group in self.fp16_groups]

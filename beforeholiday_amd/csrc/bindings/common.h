@@ -47,6 +47,7 @@ struct MTAPlan {
   bh::MTAView view;
   at::Tensor dev;   // keeps the device buffer alive
   at::Tensor host;  // pinned staging (kept alive: a captured graph may replay the H2D copy)
+  bool pinned = false;  // used inside a HIP graph capture: never evicted (the graph holds its pointers)
 };
 
 // Builds or fetches the plan for `lists` (all lists same length; list i shares dtype).

@@ -72,15 +72,19 @@ const MTAPlan& get_plan(const std::vector<std::vector<at::Tensor>>& lists, int64
   }
 
   std::lock_guard<std::mutex> lock(g_plan_mu);
-  auto it = g_plans.find(key);
-  if (it != g_plans.end()) return it->second;
-
   hipStream_t stream = stream_for(lists[0][0]);
-  // a plan recorded into a HIP graph must outlive the graph: once anything was captured the cache
-  // only grows (a captured training step creates no new plans when replayed)
-  static bool captured = false;
-  captured = captured || capturing(stream);
-  if (g_plans.size() >= kMaxPlans && !captured) g_plans.clear();
+  const bool in_capture = capturing(stream);
+  auto it = g_plans.find(key);
+  if (it != g_plans.end()) {
+    it->second.pinned = it->second.pinned || in_capture;
+    return it->second;
+  }
+
+  // a plan recorded into a HIP graph must outlive the graph: eviction (a full cache, e.g. eager work
+  // whose tensor pointers keep changing) drops only the plans no capture has used
+  if (g_plans.size() >= kMaxPlans) {
+    for (auto e = g_plans.begin(); e != g_plans.end();) e = e->second.pinned ? std::next(e) : g_plans.erase(e);
+  }
 
   // chunk schedule
   std::vector<int> chunk0(T + 1, 0);
@@ -100,7 +104,6 @@ const MTAPlan& get_plan(const std::vector<std::vector<at::Tensor>>& lists, int64
   const size_t o_cl = align_up(o_ct + sizeof(int) * C, 16);
   const size_t bytes = align_up(o_cl + sizeof(int) * C, 16) + 16;
 
-  const bool in_capture = capturing(stream);
   // pinned staging + async copy normally; while capturing (pinned allocation is not allowed then) a
   // pageable table uploaded through kernel arguments
   at::Tensor host = at::empty({(int64_t)bytes}, at::TensorOptions().dtype(at::kByte).pinned_memory(!in_capture));
@@ -146,6 +149,7 @@ const MTAPlan& get_plan(const std::vector<std::vector<at::Tensor>>& lists, int64
   plan.view.C = C;
   plan.view.depth = depth;
   plan.view.chunk = static_cast<int>(chunk);
+  plan.pinned = in_capture;
   auto res = g_plans.emplace(std::move(key), std::move(plan));
   return res.first->second;
 }

@@ -107,7 +107,10 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
       ss[c] = a.pro_scale[c];
       ss[kMaxProC + c] = a.pro_shift[c];
     }
-    // visible to the first halo_store through the __syncthreads below it
+    // the first halo_store below reads channels other threads (other waves) wrote: without this
+    // barrier a wave could normalise its first halo with stale LDS (round 3's run-to-run and
+    // rank-to-rank differences, tests/test_determinism.py)
+    __syncthreads();
   }
   // window origin of tile id t: x-tile fastest, then row window, then image group
   auto origin = [&](int t, int& n0, int& y0, int& x0) __attribute__((always_inline)) {

@@ -107,12 +107,10 @@ class FP16_Optimizer(object):
     # ---- gradients -------------------------------------------------------------------------------
 
     def zero_grad(self, set_grads_to_None=False):
-        tensors = [p for g in self.optimizer.param_groups for p in g["params"]] + self.all_fp16_params
-        for p in tensors:
-            if set_grads_to_None:
-                p.grad = None
-            elif p.grad is not None:
-                p.grad.detach_().zero_()
+        from ..optimizers._common import zero_param_grads
+
+        zero_param_grads([p for g in self.optimizer.param_groups for p in g["params"]] + self.all_fp16_params,
+                         set_grads_to_None)
 
     def backward(self, loss, update_master_grads=True, retain_graph=False):
         (loss.float() * self.loss_scaler.loss_scale()).backward(retain_graph=retain_graph)

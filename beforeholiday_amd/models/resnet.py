@@ -34,20 +34,45 @@ def _time_ms(fn, reps=3):
 _CONV1X1_CHOICE = {}
 
 
+def choice_table():
+    """The per-shape kernel choices this process has made so far (sorted, printable): identical on
+    every rank by construction (tests/test_determinism.py checks it)."""
+    return sorted((tuple(str(v) for v in k), c) for k, c in _CONV1X1_CHOICE.items())
+
+
+def _agree(choice):
+    """With ``BH_CONV_TUNE=1`` under an initialised multi-rank default group, every rank takes rank 0's
+    timed choice (one int broadcast): ranks that time for themselves pick different kernels when the
+    timings are close, and then neither compute identically nor step in lock-step. All ranks reach the
+    same ``_pick`` calls in the same order (same model, same shapes), so the broadcasts pair up."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+        return choice
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([1 if choice == "gemm" else 0], dtype=torch.int32, device=dev)
+    dist.broadcast(t, 0)
+    return "gemm" if int(t.item()) else "miopen"
+
+
 def _pick(key, gemm_fn, miopen_fn, mode):
-    """``mode`` "gemm" / "miopen" forces a path; "auto" times both once per shape (first call, e.g. a
-    warmup step) and keeps the faster. Measured on MI355X at ResNet-50 / batch 256 (benchmarks/
-    bench_conv_dirs.py): hipBLASLt wins the forward of every channel-expanding 1x1 conv (64->256:
-    0.13 vs 0.21 ms) and most data gradients; MIOpen wins the small-channel 56x56 layers."""
+    """``mode`` "gemm" / "miopen" forces a path. "auto" is the own MFMA / strip kernels ("gemm") for
+    every shape -- a static, rank-independent rule, so two processes always run the same kernels and
+    the same reduction order (round 3's timed picks diverged between two ranks sharing a GPU and broke
+    the two-rank equivalence test). ``BH_CONV_TUNE=1`` restores timing both once per shape and keeping
+    the faster, with rank 0's result broadcast to all ranks (``_agree``)."""
     if mode != "auto":
         return mode
     choice = _CONV1X1_CHOICE.get(key)
     if choice is None:
-        # interleaved A, B, A, B and the best of each: the first step runs on a cold GPU (clocks
-        # ramping, first-use kernel loads), and a pick made on one noisy sample sticks for the run
-        t_gemm, t_miopen = _time_ms(gemm_fn), _time_ms(miopen_fn)
-        t_gemm, t_miopen = min(t_gemm, _time_ms(gemm_fn)), min(t_miopen, _time_ms(miopen_fn))
-        choice = "gemm" if t_gemm < t_miopen else "miopen"
+        if os.environ.get("BH_CONV_TUNE") == "1":
+            # interleaved A, B, A, B and the best of each: the first step runs on a cold GPU (clocks
+            # ramping, first-use kernel loads), and a pick made on one noisy sample sticks for the run
+            t_gemm, t_miopen = _time_ms(gemm_fn), _time_ms(miopen_fn)
+            t_gemm, t_miopen = min(t_gemm, _time_ms(gemm_fn)), min(t_miopen, _time_ms(miopen_fn))
+            choice = _agree("gemm" if t_gemm < t_miopen else "miopen")
+        else:
+            choice = "gemm"
         _CONV1X1_CHOICE[key] = choice
     return choice
 

@@ -32,23 +32,29 @@ def grad_like_param(p: torch.Tensor) -> torch.Tensor:
     raise RuntimeError("fused optimizers support contiguous / channels_last parameters only")
 
 
-def zero_grad(opt, set_grad_none: bool, set_to_none=None):
-    none = set_grad_none if set_to_none is None else set_to_none
+def zero_param_grads(params, set_to_none: bool):
+    """``p.grad = None`` or zero-fill (one foreach launch), the torch.optim way: ``detach_()`` only a
+    gradient that has a ``grad_fn``. A gradient that is a VIEW (DDP's gradient-as-bucket-view slots)
+    cannot be detached in place, and does not need it: ``requires_grad_(False)`` is enough."""
     grads = []
-    for group in opt.param_groups:
-        for p in group["params"]:
-            if p.grad is None:
-                continue
-            if none:
-                p.grad = None
-            else:
-                if p.grad.grad_fn is not None:
-                    p.grad.detach_()
-                else:
-                    p.grad.requires_grad_(False)
-                grads.append(p.grad)
+    for p in params:
+        if p.grad is None:
+            continue
+        if set_to_none:
+            p.grad = None
+            continue
+        if p.grad.grad_fn is not None:
+            p.grad.detach_()
+        else:
+            p.grad.requires_grad_(False)
+        grads.append(p.grad)
     if grads:
         torch._foreach_zero_(grads)
+
+
+def zero_grad(opt, set_grad_none: bool, set_to_none=None):
+    none = set_grad_none if set_to_none is None else set_to_none
+    zero_param_grads([p for group in opt.param_groups for p in group["params"]], none)
 
 
 class ParamTableMixin:

@@ -18,13 +18,15 @@ MI355X / RCCL design:
   reference's element count, sized per xGMI peer (:func:`xgmi_bucket_mb`).
 * averaging uses ``ReduceOp.AVG`` inside the collective when the backend supports it (RCCL), so no
   extra scaling kernel runs per bucket.
-* gradients live IN the buckets (gradient-as-bucket-view): once the bucket structure is known each
-  parameter gets a slot view of its bucket's persistent flat buffer (``param._bh_grad_slot``,
-  same strides as the parameter). A gradient that arrives elsewhere is copied into its slot by the
-  per-parameter hook -- as it arrives, overlapped with the rest of backward -- and ``param.grad``
-  becomes the slot view; the all-reduce runs on the flat buffer in place, and nothing is copied
-  back. A backward that writes its weight gradient straight into the slot (the MFMA conv wgrad
-  kernels do, models/resnet.py) makes the hook a no-op.
+* once the bucket structure is known each parameter gets a slot view of its bucket's persistent
+  flat buffer (same strides as the parameter; the views live in the bucket, not on the Parameter).
+  The per-parameter hook copies a gradient into its slot as it arrives -- overlapped with the rest of
+  backward -- and the all-reduce runs on the flat buffer in place. By default the averaged slot is
+  copied back into ``param.grad`` afterwards; with ``gradient_as_bucket_view=True`` (torch DDP's
+  option of the same name; bench.py uses it) ``param.grad`` BECOMES the slot view and nothing is
+  copied back. A gradient-as-bucket-view ``param.grad`` is overwritten by the next backward, so
+  code that keeps a gradient across backwards (amp's accumulation stash) must copy it:
+  :func:`grad_is_bucket_view` tells it when.
 * device-agnostic: the same code runs on CPU tensors over gloo (the reference hard-codes CUDA).
 * a single-process world skips every collective.
 """
@@ -176,6 +178,30 @@ def _supports_avg(pg) -> bool:
         return False
 
 
+# parameter -> its bucket slot view, for the parameters of gradient-as-bucket-view DDP instances (weak:
+# nothing here keeps a parameter or its bucket alive)
+_VIEW_SLOTS = None
+
+
+def _view_slots():
+    global _VIEW_SLOTS
+    if _VIEW_SLOTS is None:
+        from torch.utils.weak import WeakTensorKeyDictionary
+
+        _VIEW_SLOTS = WeakTensorKeyDictionary()
+    return _VIEW_SLOTS
+
+
+def grad_is_bucket_view(p: torch.Tensor) -> bool:
+    """True when ``p.grad`` is the gradient-as-bucket-view slot of a DDP bucket: the next backward
+    writes into that memory, so a caller that keeps the gradient aside must clone it."""
+    g = p.grad
+    if g is None or _VIEW_SLOTS is None:
+        return False
+    slot = _VIEW_SLOTS.get(p)
+    return slot is not None and g.data_ptr() == slot.data_ptr()
+
+
 def _slot_view(flat: torch.Tensor, off: int, p: torch.Tensor) -> torch.Tensor:
     """View of ``flat[off:off+numel]`` with ``p``'s shape and (dense) strides."""
     n = p.numel()
@@ -210,7 +236,7 @@ class DistributedDataParallel(Module):
                  allreduce_trigger_params=None, retain_allreduce_buffers=False, allreduce_always_fp32=False,
                  num_allreduce_streams=1, allreduce_communicators=None, gradient_average=True,
                  gradient_predivide_factor=1.0, gradient_average_split_factor=None, prof=False,
-                 process_group=None, bucket_cap_mb=None, first_bucket_mb=None):
+                 process_group=None, bucket_cap_mb=None, first_bucket_mb=None, gradient_as_bucket_view=False):
         super().__init__()
         if shared_param is not None:
             raise ValueError("shared_param is no longer supported as an option.  It was misleadingly named "
@@ -238,6 +264,7 @@ class DistributedDataParallel(Module):
         self.gradient_average = gradient_average
         self.gradient_predivide_factor = gradient_predivide_factor
         self.prof = prof
+        self.gradient_as_bucket_view = bool(gradient_as_bucket_view)
         self.allreduce_buffers = []
         self.num_allreduce_streams = num_allreduce_streams
         self.custom_allreduce_triggers = False
@@ -286,9 +313,9 @@ class DistributedDataParallel(Module):
         for h in self._hooks:
             h.remove()
         self._hooks = []
-        for p in getattr(self, "active_params", []):
-            if hasattr(p, "_bh_grad_slot"):
-                del p._bh_grad_slot
+        if _VIEW_SLOTS is not None:
+            for p in getattr(self, "active_params", []):
+                _VIEW_SLOTS.pop(p, None)
         self.active_params = [p for p in self.module.parameters() if p.requires_grad]
         self._param_ids = [id(p) for p in self.active_params]
         self.needs_refresh = True
@@ -442,22 +469,28 @@ class DistributedDataParallel(Module):
         for i in b.params:
             p = self.active_params[i]
             b.slots[i] = _slot_view(b.flat, off, p)
-            p._bh_grad_slot = b.slots[i]
+            if self.gradient_as_bucket_view:
+                _view_slots()[p] = b.slots[i]
             off += p.numel()
 
     def _to_slot(self, b: _Bucket, i: int):
-        """Make ``param.grad`` the bucket slot view, copying the gradient in unless it is already there."""
+        """Copy the gradient into its bucket slot (unless it is already there); with
+        gradient_as_bucket_view ``param.grad`` then becomes the slot view."""
         if b.slots is None:
             self._alloc_slots(b)
         p, slot = self.active_params[i], b.slots[i]
         g = p.grad
         if g is None:
             slot.zero_()
+            if not self.gradient_as_bucket_view:
+                p.grad = torch.zeros_like(p)  # receives the average (other ranks may have one)
+                return
         elif g.data_ptr() != slot.data_ptr() or g.stride() != slot.stride():
             _raw(slot).copy_(_raw(g if g.stride() == slot.stride() else g.contiguous(memory_format=_fmt(slot))))
         else:
             return
-        p.grad = slot
+        if self.gradient_as_bucket_view:
+            p.grad = slot
 
     def _launch(self, b_idx):
         b = self._buckets[b_idx]
@@ -486,6 +519,9 @@ class DistributedDataParallel(Module):
             tensor.mul_(self.gradient_predivide_factor / self.world_size)
         if tensor is not b.flat:
             b.flat.copy_(tensor)
+        if not self.gradient_as_bucket_view:  # the averaged slots back into the parameters' own grads
+            ps = [self.active_params[i] for i in b.params]
+            torch._foreach_copy_([p.grad for p in ps], [b.slots[i] for i in b.params])
         if self.retain_allreduce_buffers:
             self.allreduce_buffers[b_idx] = b.flat
         b.outputs = None

@@ -189,7 +189,7 @@ def main():
     else:
         cap_mb, first_mb = args.bucket_cap_mb, args.bucket_cap_mb / 4
     model = DistributedDataParallel(model, message_size=args.message_size, bucket_cap_mb=cap_mb,
-                                    first_bucket_mb=first_mb)
+                                    first_bucket_mb=first_mb, gradient_as_bucket_view=True)
 
     dt = torch.float16 if args.opt_level in ("O1", "O2") else torch.bfloat16
     in_dt = dt if args.opt_level in ("O2", "O5") else torch.float32  # O1/O4 models stay fp32

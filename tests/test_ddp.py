@@ -169,19 +169,23 @@ def test_amp_master_params_ddp_gloo(opt_level):
 
 def _bucket_view(rank, world):
     """Gradient-as-bucket-view: after the first backward every gradient IS a view of its bucket's flat
-    buffer (no gather copy before, no scatter copy after the all-reduce), and stays correct."""
+    buffer (no gather copy before, no scatter copy after the all-reduce), and stays correct; zeroing
+    those view gradients in place (torch, amp and FP16_Optimizer zero_grad) works."""
+    from beforeholiday_amd.fp16_utils import FP16_Optimizer
+    from beforeholiday_amd.parallel.distributed import grad_is_bucket_view
+
     torch.manual_seed(100 + rank)
     model = MLP()
-    ddp = DDP(model, message_size=1000)
+    ddp = DDP(model, message_size=1000, gradient_as_bucket_view=True)
     for it in range(3):
         torch.manual_seed(it)
         x = torch.randn(8 * world, 32)
         xs = x[rank * 8:(rank + 1) * 8]
-        ddp.zero_grad(set_to_none=True)
+        ddp.zero_grad(set_to_none=it == 0)
         ddp(xs).square().sum().backward()
         flats = {id(b): b.flat for b in ddp._buckets}
         for p in model.parameters():
-            assert hasattr(p, "_bh_grad_slot") and p.grad.data_ptr() == p._bh_grad_slot.data_ptr()
+            assert grad_is_bucket_view(p) and not hasattr(p, "_bh_grad_slot")
             assert any(f.data_ptr() <= p.grad.data_ptr() < f.data_ptr() + f.numel() * f.element_size()
                        for f in flats.values())
         # all ranks hold the same (averaged) gradient
@@ -190,7 +194,102 @@ def _bucket_view(rank, world):
         dist.all_gather(gs, g)
         for other in gs:
             torch.testing.assert_close(other, g)
+    ddp.zero_grad(set_to_none=False)  # in place on the view gradients: no "can't detach views in-place"
+    assert all(p.grad is not None and not p.grad.any() for p in model.parameters())
+    ddp(torch.randn(4, 32)).sum().backward()
+    fopt = FP16_Optimizer(torch.optim.SGD(model.parameters(), lr=0.1), static_loss_scale=1.0, verbose=False)
+    fopt.zero_grad()  # the reference's default set_grads_to_None=False
+    assert all(not p.grad.any() for p in model.parameters())
 
 
 def test_ddp_gradient_as_bucket_view():
     run_distributed(_bucket_view, 2)
+
+
+def _default_copies_back(rank, world):
+    """Without gradient_as_bucket_view (the default, as in torch) param.grad stays its own tensor and
+    receives the average."""
+    from beforeholiday_amd.parallel.distributed import grad_is_bucket_view
+
+    torch.manual_seed(rank)
+    model = MLP()
+    ddp = DDP(model, message_size=1000)
+    x = torch.randn(4, 32) * (rank + 1)
+    for _ in range(2):
+        ddp.zero_grad(set_to_none=True)
+        local = []
+        out = ddp(x).sum()
+        grads = torch.autograd.grad(out, list(model.parameters()), retain_graph=True)
+        local = [g.clone() for g in grads]
+        out.backward()
+        for g, p in zip(local, model.parameters()):
+            assert not grad_is_bucket_view(p)
+            assert all(p.grad.data_ptr() != b.flat.data_ptr() for b in ddp._buckets)
+            tot = g.clone()
+            dist.all_reduce(tot)
+            torch.testing.assert_close(p.grad, tot / world, rtol=1e-5, atol=1e-6)
+
+
+def test_ddp_default_copies_back():
+    run_distributed(_default_copies_back, 2)
+
+
+def _amp_accumulate(rank, world, opt_level, view):
+    """amp with two ``scale_loss`` micro-batches per step (no delay_unscale) under DDP: the gradient
+    stashed after the first micro-batch must survive the second backward, also when it is a bucket view
+    (advisor round 3: it was overwritten by the second backward's copy into the slot)."""
+    import copy
+
+    from beforeholiday_amd import amp
+
+    torch.manual_seed(0)
+    ref = MLP()
+    model = copy.deepcopy(ref)
+    opt = torch.optim.SGD(model.parameters(), lr=0.0)
+    model, opt = amp.initialize(model, opt, opt_level=opt_level, loss_scale=128.0, verbosity=0)
+    ddp = DDP(model, message_size=300, gradient_as_bucket_view=view)
+    micro = [(torch.randn(4 * world, 32), torch.randn(4 * world, 8)) for _ in range(2)]
+    try:
+        for step in range(2):
+            for x, y in micro:
+                xs, ys = x[rank * 4:(rank + 1) * 4], y[rank * 4:(rank + 1) * 4]
+                loss = torch.nn.functional.mse_loss(ddp(xs).float(), ys)
+                with amp.scale_loss(loss, opt) as scaled:
+                    scaled.backward()
+            got = [p.grad.float().clone() for p in amp.master_params(opt)]
+            opt.zero_grad()
+        for p in ref.parameters():
+            p.grad = None
+        for x, y in micro:  # fp32, one process: the sum over micro-batches of the rank-averaged loss
+            sum(torch.nn.functional.mse_loss(ref(x[r * 4:(r + 1) * 4]), y[r * 4:(r + 1) * 4])
+                for r in range(world)).div(world).backward()
+        for g, q in zip(got, ref.parameters()):
+            torch.testing.assert_close(g, q.grad, rtol=3e-2, atol=3e-3)
+    finally:
+        amp.deactivate()
+
+
+@pytest.mark.parametrize("opt_level", ["O1", "O2"])
+@pytest.mark.parametrize("view", [False, True])
+def test_amp_accumulation_under_ddp(opt_level, view):
+    run_distributed(_amp_accumulate, 2, opt_level, view)
+
+
+def test_lr_scheduler_after_scale_loss():
+    """A torch LR scheduler built after the first scale_loss (amp has already installed its step gate)
+    wraps optimizer.step through ``__func__`` (advisor round 3)."""
+    from beforeholiday_amd import amp
+
+    model = MLP()
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    model, opt = amp.initialize(model, opt, opt_level="O2", verbosity=0)
+    try:
+        loss = model(torch.randn(2, 32)).float().sum()
+        with amp.scale_loss(loss, opt) as scaled:
+            scaled.backward()
+        sched = torch.optim.lr_scheduler.StepLR(opt, step_size=1, gamma=0.5)
+        opt.step()
+        sched.step()
+        assert abs(opt.param_groups[0]["lr"] - 0.05) < 1e-12
+    finally:
+        amp.deactivate()

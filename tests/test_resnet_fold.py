@@ -153,15 +153,15 @@ def _fold_two_ranks(rank, world, cfg):
     for g in gp:
         dist.all_reduce(g)
     o1, gx1, gp1, st1 = run(singles[rank], x)  # the whole batch on this rank alone
-    assert _rel(o, o1[sl]) < 5e-3
-    assert _rel(gx, gx1[sl]) < 2e-2
-    for a, b in zip(gp, gp1):
-        assert _rel(a, b) < 2e-2
+    assert _rel(o, o1[sl]) < 5e-3, (rank, _rel(o, o1[sl]))
+    assert _rel(gx, gx1[sl]) < 2e-2, (rank, _rel(gx, gx1[sl]))
+    for i, (a, b) in enumerate(zip(gp, gp1)):
+        assert _rel(a, b) < 2e-2, (rank, i, _rel(a, b))
     for k in st:
         if "running" in k:
-            assert _rel(st[k], st1[k]) < 1e-3, k
+            assert _rel(st[k], st1[k]) < 1e-3, (rank, k, _rel(st[k], st1[k]))
         elif "num_batches" in k:
-            assert int(st[k]) == int(st1[k]) == 1, k
+            assert int(st[k]) == int(st1[k]) == 1, (rank, k, int(st[k]), int(st1[k]))
 
 
 @pytest.mark.gpu
@@ -221,13 +221,21 @@ def _net_two_ranks(rank, world, exchange):
     # summation order). Gradients that downstream BatchNorms nearly cancel (the stem BN's bias) are
     # rounding noise at any order; a world-size factor (the bug class this guards) sits far above it
     perm = torch.cat([torch.arange(B, world * B), torch.arange(0, B)]).cuda()
-    _, g1p, _ = run(singles[rank], x[perm], y[perm])
-    assert abs(float(loss) - float(loss1)) < 1e-3 * abs(float(loss1))
+    loss1p, g1p, _ = run(singles[rank], x[perm], y[perm])
+    # the loss gets the same swapped-order noise floor as the gradients (fp16 activations through 16
+    # BatchNorms: another statistics summation order moves the loss by ~1e-3 relative)
+    lo, l1, l1p = float(loss), float(loss1), float(loss1p)
+    assert abs(lo - l1) < 3 * abs(l1p - l1) + 2e-3 * abs(l1), (rank, lo, l1, l1p)
     for n in g:
         floor = _rel(g1p[n], g1[n])
-        assert _rel(g[n], g1[n]) < 3 * floor + 2e-2, (n, _rel(g[n], g1[n]), floor)
+        assert _rel(g[n], g1[n]) < 3 * floor + 2e-2, (rank, n, _rel(g[n], g1[n]), floor)
     for k in st:
-        assert _rel(st[k], st1[k]) < 2e-3, k
+        assert _rel(st[k], st1[k]) < 2e-3, (rank, k, _rel(st[k], st1[k]))
+    # both ranks ran the single-rank double batch on identical data and weights: bitwise identical
+    # losses unless the two processes chose different kernels (tests/test_determinism.py)
+    both = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+    dist.all_gather(both, torch.tensor([l1], dtype=torch.float64))
+    assert both[0].item() == both[1].item(), (rank, [b.item() for b in both], R.choice_table())
 
 
 @pytest.mark.gpu
