@@ -105,93 +105,98 @@ def _is_optimizer(o):
     return isinstance(o, (torch.optim.Optimizer, LARC))
 
 
-def _initialize(models, optimizers, properties, num_losses=1, cast_model_outputs=None):
+def _as_list(obj, is_item, what):
+    """(list, was_list) for the ``models`` / ``optimizers`` argument: one item, a list, or None."""
+    if obj is None and what == "optimizers":
+        return [], False
+    if is_item(obj):
+        return [obj], False
+    if isinstance(obj, list):
+        return obj, True
+    raise TypeError(f"{what} must be either a single {what[:-1]} or a list of {what}.")
+
+
+class _CastingForward(object):
+    """Replacement ``model.forward``: floating-point tensors in ``args`` / ``kwargs`` are cast with
+    ``cast_in`` (None: untouched), every floating-point tensor of the output with ``cast_out``."""
+
+    def __init__(self, inner, cast_in, cast_out):
+        self.inner, self.cast_in, self.cast_out = inner, cast_in, cast_out
+
+    def __call__(self, *args, **kwargs):
+        if self.cast_in is not None:
+            args, kwargs = applier(args, self.cast_in), applier(kwargs, self.cast_in)
+        return applier(self.inner(*args, **kwargs), self.cast_out)
+
+
+def _cast_models(models, optimizers, properties, cast_model_outputs):
+    """O2 / O3 / O5: the model weights in the low dtype (BatchNorms kept fp32 when asked), inputs cast on
+    the way in, outputs on the way out (fp32 unless ``cast_model_outputs``), fp32 ``state_dict``."""
     from ..fp16_utils import convert_network
-    from .amp import init as amp_init
+
+    low = properties.cast_model_type
+    out_dtype = cast_model_outputs if cast_model_outputs is not None else torch.float32
+    for model in models:
+        if properties.keep_batchnorm_fp32:
+            convert_network(model, low)
+        else:
+            model.to(low)
+        model.forward = _CastingForward(model.forward, functools.partial(to_type, low),
+                                        functools.partial(to_type, out_dtype))
+        hook = O2StateDictHook(functools.partial(to_type, torch.float32))
+        for module in model.modules():
+            module._register_state_dict_hook(hook)
+    # state created before the cast (e.g. momentum buffers) follows the parameters' new dtype
+    for optimizer in optimizers:
+        optimizer.load_state_dict(optimizer.state_dict())
+
+
+def _casts_off_during_step(optimizer):
+    """O1 / O4: the optimizer step runs with the function-cast wrappers disabled."""
     from .handle import disable_casts
 
-    optimizers_was_list = False
-    if _is_optimizer(optimizers):
-        optimizers = [optimizers]
-    elif optimizers is None:
-        optimizers = []
-    elif isinstance(optimizers, list):
-        optimizers_was_list = True
-        check_optimizers(optimizers)
-    else:
-        check_optimizers([optimizers])
-        raise TypeError("optimizers must be either a single optimizer or a list of optimizers.")
+    inner = optimizer.step
 
-    if isinstance(models, torch.nn.Module):
-        models_was_list = False
-        models = [models]
-    elif isinstance(models, list):
-        models_was_list = True
-    else:
-        raise TypeError("models must be either a single model or a list of models.")
+    def step(self, *args, **kwargs):
+        with disable_casts():
+            return inner(*args, **kwargs)
+
+    optimizer.step = MethodType(step, optimizer)
+
+
+def _initialize(models, optimizers, properties, num_losses=1, cast_model_outputs=None):
+    from .amp import init as amp_init
+
+    if isinstance(optimizers, list):
+        check_optimizers(optimizers)
+    elif optimizers is not None and not _is_optimizer(optimizers):
+        check_optimizers([optimizers])
+    optimizers, optimizers_was_list = _as_list(optimizers, _is_optimizer, "optimizers")
+    models, models_was_list = _as_list(models, lambda m: isinstance(m, torch.nn.Module), "models")
 
     check_models(models)
     if not _amp_state.allow_incoming_model_not_fp32:
         check_params_fp32(models)
 
     if properties.cast_model_type:
-        if properties.keep_batchnorm_fp32:
-            for model in models:
-                convert_network(model, properties.cast_model_type)
-        else:
-            for model in models:
-                model.to(properties.cast_model_type)
-        input_caster = functools.partial(to_type, properties.cast_model_type)
-        output_caster = functools.partial(to_type, cast_model_outputs if cast_model_outputs is not None
-                                          else torch.float32)
-        for model in models:
-            def patch_forward(old_fwd):
-                def new_fwd(*args, **kwargs):
-                    output = old_fwd(*applier(args, input_caster), **applier(kwargs, input_caster))
-                    return applier(output, output_caster)
-                return new_fwd
-            model.forward = patch_forward(model.forward)
-        # recast per-param optimizer state (e.g. momentum buffers) to the new param types
-        for optimizer in optimizers:
-            optimizer.load_state_dict(optimizer.state_dict())
-        for model in models:
-            for module in model.modules():
-                module._register_state_dict_hook(O2StateDictHook(functools.partial(to_type, torch.float32)))
+        _cast_models(models, optimizers, properties, cast_model_outputs)
     elif cast_model_outputs is not None:
-        output_caster = functools.partial(to_type, cast_model_outputs)
         for model in models:
-            def patch_forward(old_fwd):
-                def new_fwd(*args, **kwargs):
-                    return applier(old_fwd(*args, **kwargs), output_caster)
-                return new_fwd
-            model.forward = patch_forward(model.forward)
+            model.forward = _CastingForward(model.forward, None, functools.partial(to_type, cast_model_outputs))
 
-    for i, optimizer in enumerate(optimizers):
-        optimizers[i] = _process_optimizer(optimizer, properties)
-
-    device = None
-    for model in models:
-        for p in model.parameters():
-            device = p.device
-            break
+    optimizers = [_process_optimizer(o, properties) for o in optimizers]
+    device = next((p.device for m in models for p in m.parameters()), None)
     _amp_state.loss_scalers = [LossScaler(properties.loss_scale, min_loss_scale=_amp_state.min_loss_scale,
                                           max_loss_scale=_amp_state.max_loss_scale, device=device)
                                for _ in range(num_losses)]
 
     if properties.patch_torch_functions:
-        # O1/O4: patch torch functions with cast wrappers; the optimizer step runs with casts off
         amp_init(loss_scale=properties.loss_scale, patch_type=properties.patch_torch_functions_type,
                  verbose=(_amp_state.verbosity == 2))
         for optimizer in optimizers:
-            def patch_step(old_step):
-                def new_step(self, *args, **kwargs):
-                    with disable_casts():
-                        return old_step(*args, **kwargs)
-                return new_step
-            optimizer.step = MethodType(patch_step(optimizer.step), optimizer)
+            _casts_off_during_step(optimizer)
 
+    model_ret = models if models_was_list else models[0]
     if optimizers_was_list:
-        return (models if models_was_list else models[0]), optimizers
-    if models_was_list:
-        return models if len(optimizers) == 0 else (models, optimizers[0])
-    return models[0] if len(optimizers) == 0 else (models[0], optimizers[0])
+        return model_ret, optimizers
+    return model_ret if not optimizers else (model_ret, optimizers[0])

@@ -145,75 +145,65 @@ def disable_casts():
         h._is_active = prev
 
 
-class AmpHandle(object):
-    """Legacy (pre-``amp.initialize``) handle returned by ``amp.init()``."""
+class _Handle(object):
+    """State of the O1 / O4 function patching that the cast wrappers (amp/wrap.py) consult on every
+    call: whether casting is on, the per-iteration cache of 16-bit weight copies, and the list of
+    (module, name, original) patches needed to undo it.
 
-    def __init__(self, loss_scale="dynamic", enable_caching=True, verbose=False):
-        self._enable_caching = enable_caching
-        self._verbose = verbose
-        self._cache = dict()
-        self._default_scaler = LossScaler(loss_scale)
-        self._is_active = True
-        self._all_wrappers = []
+    :class:`AmpHandle` is the live one ``amp.init()`` returns; :class:`NoOpHandle` backs the
+    ``amp.half_function``-style decorators while amp is off (never casts). The old per-optimizer
+    ``scale_loss`` API of these handles is gone (as in the reference): it raises, pointing to
+    ``amp.initialize`` / ``amp.scale_loss``."""
 
+    casting = False
+    caching = False
+
+    def __init__(self, verbose=False):
+        self._verbose = bool(verbose)
+        self._cache = {}
+        self._patches = []
+        self._is_active = self.casting
+
+    # -- queried by the cast wrappers
     def is_active(self):
         return self._is_active
 
-    @contextlib.contextmanager
-    def _disable_casts(self):
-        self._is_active = False
-        yield
-        self._is_active = True
-
-    def wrap_optimizer(self, optimizer, num_loss=1):
-        from .opt import OptimWrapper
-
-        self._default_scaler = None
-        return OptimWrapper(optimizer, self, num_loss)
-
-    @contextlib.contextmanager
-    def scale_loss(self, loss, optimizer):
-        raise RuntimeError("The old Amp API is no longer supported.  Please move to the new API, documented "
-                           "here:  https://nvidia.github.io/apex/amp.html.  Transition guide:  "
-                           "https://nvidia.github.io/apex/amp.html#transition-guide-for-old-api-users")
-
-    def _clear_cache(self):
-        self._cache.clear()
-
-    # Experimental support for saving / restoring uncasted versions of functions
-    def _save_func(self, mod, fn, func):
-        self._all_wrappers.append((mod, fn, func))
-
-    def _deactivate(self):
-        for mod, fn, func in self._all_wrappers:
-            setattr(mod, fn, func)
-        self._all_wrappers = []
+    @property
+    def verbose(self):
+        return self._verbose
 
     @property
     def has_cache(self):
-        return self._enable_caching
+        return self.caching
 
     @property
     def cache(self):
         return self._cache
 
     def remove_cache(self, param):
-        if self.has_cache and param in self.cache:
-            del self.cache[param]
+        self._cache.pop(param, None)
 
-    @property
-    def verbose(self):
-        return self._verbose
-
-
-class NoOpHandle(object):
-    def is_active(self):
-        return False
+    def _clear_cache(self):
+        self._cache.clear()
 
     @contextlib.contextmanager
     def _disable_casts(self):
-        yield
+        prev, self._is_active = self._is_active, False
+        try:
+            yield
+        finally:
+            self._is_active = prev
 
+    # -- patch bookkeeping (amp/utils.py records every replaced function here)
+    def _save_func(self, mod, fn, func):
+        self._patches.append((mod, fn, func))
+
+    def _deactivate(self):
+        while self._patches:  # newest first: nested patches of one attribute unwind correctly
+            mod, fn, func = self._patches.pop()
+            setattr(mod, fn, func)
+
+    # -- legacy optimizer API
     def wrap_optimizer(self, optimizer, num_loss=1):
         from .opt import OptimWrapper
 
@@ -221,18 +211,23 @@ class NoOpHandle(object):
 
     @contextlib.contextmanager
     def scale_loss(self, loss, optimizer):
-        yield loss
+        if not self.casting:
+            yield loss
+            return
+        raise RuntimeError("handle.scale_loss (the pre-amp.initialize API) is not supported: use "
+                           "amp.initialize(model, optimizer, opt_level=...) and amp.scale_loss(loss, optimizer)")
 
-    @property
-    def has_cache(self):
-        return False
 
-    @property
-    def verbose(self):
-        return False
+class AmpHandle(_Handle):
+    """Returned by ``amp.init()``: casting on, weight-cast cache on unless ``enable_caching=False``."""
 
-    def _clear_cache(self):
-        pass
+    casting = True
 
-    def _deactivate(self):
-        pass
+    def __init__(self, loss_scale="dynamic", enable_caching=True, verbose=False):
+        self.caching = bool(enable_caching)
+        super().__init__(verbose)
+        self.loss_scale = loss_scale
+
+
+class NoOpHandle(_Handle):
+    """Handle of the decorators while amp is not initialised: never casts, nothing to undo."""

@@ -1,6 +1,12 @@
-"""Legacy per-loss optimizer wrapper of the old amp API (reference: apex/amp/opt.py:9-103)."""
+"""Optimizer wrapper of the legacy ``handle.wrap_optimizer`` API (reference: apex/amp/opt.py:9-103):
+one dynamic loss scaler per loss of a multi-loss step, and the step skipped when any of them saw an
+overflow.
+
+Design here: the wrapper is a thin proxy (``__getattr__`` forwards everything it does not define) that
+keeps, per step, a cursor over the losses. Because the gradients of several losses accumulate into
+the same ``.grad`` tensors, loss ``i > 0`` is unscaled on its own: the gradients accumulated so far
+are moved aside before its backward and added back after it has been unscaled with ITS scale."""
 import contextlib
-import warnings
 
 from ._amp_state import maybe_print
 from .scaler import LossScaler
@@ -11,69 +17,57 @@ class OptimWrapper(object):
         self._optimizer = optimizer
         self._amp_handle = amp_handle
         self._num_loss = num_loss
-        self._loss_idx = 0
-        self._skip_next = [False] * num_loss
-        self._loss_scaler = [LossScaler("dynamic") for _ in range(num_loss)]
+        self._scalers = [LossScaler("dynamic") for _ in range(num_loss)]
+        self._overflowed = [False] * num_loss
+        self._cursor = 0  # index of the next loss of this step
+
+    def _all_params(self):
+        return [p for g in self._optimizer.param_groups for p in g["params"]]
 
     @contextlib.contextmanager
     def scale_loss(self, loss):
         if not self._amp_handle.is_active():
             yield loss
             return
-        # when there are multiple losses per-optimizer, we need to save out current grad accumulation,
-        # since we won't be able to unscale this particulare loss once the grads are all mixed together.
-        cached_grads = []
-        if self._loss_idx > 0:
-            for p in self._params():
-                cached_grads.append(None if p.grad is None else p.grad.detach().clone())
+        if not 0 <= self._cursor < self._num_loss:
+            raise RuntimeError(f"scale_loss called for more than num_loss={self._num_loss} losses in one step")
+        scaler = self._scalers[self._cursor]
+        params = self._all_params()
+        # gradients of the previous losses of this step, set aside (they carry other scales)
+        earlier = [p.grad.detach().clone() if (self._cursor > 0 and p.grad is not None) else None for p in params]
+        if self._cursor > 0:
             self._optimizer.zero_grad()
-        loss_scale = self._cur_loss_scaler().loss_scale()
-        yield loss * loss_scale
-        self._cur_loss_scaler().clear_overflow_state()
-        grads = [p.grad for p in self._params() if p.grad is not None]
-        self._cur_loss_scaler().unscale(grads, grads, loss_scale)
-        self._skip_next[self._loss_idx] = self._cur_loss_scaler().update_scale()
-        self._loss_idx += 1
-        if len(cached_grads) > 0:
-            for p, cached in zip(self._params(), cached_grads):
-                if cached is not None:
-                    p.grad.data.add_(cached)
-
-    def _params(self):
-        for group in self._optimizer.param_groups:
-            for p in group["params"]:
-                yield p
-
-    def _cur_loss_scaler(self):
-        assert 0 <= self._loss_idx < self._num_loss
-        return self._loss_scaler[self._loss_idx]
+        scale = scaler.loss_scale()
+        yield loss * scale
+        scaler.clear_overflow_state()
+        fresh = [p.grad for p in params if p.grad is not None]
+        scaler.unscale(fresh, fresh, scale)
+        self._overflowed[self._cursor] = scaler.update_scale()
+        self._cursor += 1
+        for p, g in zip(params, earlier):
+            if g is not None:
+                p.grad.data.add_(g)
 
     def step(self, closure=None):
         if not self._amp_handle.is_active():
             return self._optimizer.step(closure=closure)
-        self._loss_idx = 0
-        for group in self._optimizer.param_groups:
-            for p in group["params"]:
-                self._amp_handle.remove_cache(p)
         if closure is not None:
             raise NotImplementedError("The `closure` argument is unsupported by the amp optimizer wrapper.")
-        if any(self._skip_next):
+        self._cursor = 0
+        for p in self._all_params():
+            self._amp_handle.remove_cache(p)
+        if any(self._overflowed):
+            self._overflowed = [False] * self._num_loss
             maybe_print("Gradient overflow, skipping update")
-            self._skip_next = [False] * self._num_loss
-        else:
-            return self._optimizer.step(closure=closure)
+            return None
+        return self._optimizer.step()
 
-    def __getattr__(self, attr):
-        return getattr(self._optimizer, attr)
-
-    def __getstate__(self):
-        return self._optimizer.__getstate__()
-
-    def __setstate__(self):
-        return self._optimizer.__setstate__()
+    # everything else is the wrapped optimizer's
+    def __getattr__(self, name):
+        return getattr(self._optimizer, name)
 
     def __repr__(self):
-        return self._optimizer.__repr__()
+        return repr(self._optimizer)
 
     def state_dict(self):
         return self._optimizer.state_dict()
@@ -81,8 +75,8 @@ class OptimWrapper(object):
     def load_state_dict(self, state_dict):
         return self._optimizer.load_state_dict(state_dict)
 
-    def zero_grad(self):
-        return self._optimizer.zero_grad()
+    def zero_grad(self, *args, **kwargs):
+        return self._optimizer.zero_grad(*args, **kwargs)
 
     def add_param_group(self, param_group):
         return self._optimizer.add_param_group(param_group)

@@ -4,6 +4,7 @@
 
 #include "bh/conv_api.h"
 #include "bh/dense_api.h"
+#include "bh/igemm_api.h"
 
 namespace bhb {
 namespace {
@@ -165,7 +166,7 @@ std::vector<at::Tensor> conv3x3_bn_dgrad(const at::Tensor& dy, const at::Tensor&
 // returns [K, C, R, R] channels_last (memory [K][R][R][C])
 bool wgrad_ok(const at::Tensor& x, const at::Tensor& dy, int64_t R, int64_t stride = 1) {
   return x.is_cuda() && dy.is_cuda() && x.dim() == 4 && dy.dim() == 4 && x.size(0) == dy.size(0) &&
-         (stride == 1 || (stride == 2 && R == 1)) && x.size(2) == stride * dy.size(2) &&
+         (stride == 1 || stride == 2) && x.size(2) == stride * dy.size(2) &&
          x.size(3) == stride * dy.size(3) && x.scalar_type() == dy.scalar_type() &&
          (x.scalar_type() == at::kHalf || x.scalar_type() == at::kBFloat16) &&
          x.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
@@ -198,14 +199,14 @@ bool wgrad_supported(const at::Tensor& x, const at::Tensor& dy, int64_t R, int64
 at::Tensor conv_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t R, int64_t stride,
                       const c10::optional<at::Tensor>& pro_scale, const c10::optional<at::Tensor>& pro_shift) {
   TORCH_CHECK(wgrad_ok(x, dy, R, stride), "conv_wgrad: needs channels_last fp16/bf16 x [N, C, sH, sW], "
-                                          "dy [N, K, H, W], C and K % 64 == 0, R in {1, 3}, stride 2 only for R = 1");
+                                          "dy [N, K, H, W], C and K % 64 == 0, R in {1, 3}, stride in {1, 2}");
   auto out = at::empty({dy.size(1), x.size(1), R, R}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto a = wgrad_args(x, dy, R, stride);
   a.out = out.data_ptr();
   at::Tensor ps, ph;
   if (pro_scale.has_value() && pro_scale->defined()) {
-    TORCH_CHECK(pro_shift.has_value() && pro_shift->defined() && stride == 1,
-                "conv_wgrad: the BatchNorm prologue needs pro_scale and pro_shift, stride 1");
+    TORCH_CHECK(pro_shift.has_value() && pro_shift->defined() && (stride == 1 || R == 3),
+                "conv_wgrad: the BatchNorm prologue needs pro_scale and pro_shift (1x1: stride 1)");
     ps = pro_scale->contiguous();
     ph = pro_shift->contiguous();
     TORCH_CHECK(ps.is_cuda() && ph.is_cuda() && ps.device() == x.device() && ph.device() == x.device() &&
@@ -304,6 +305,79 @@ at::Tensor stem_wgrad(const at::Tensor& x, const at::Tensor& dy) {
   return out;
 }
 
+// ---- stride-2 3x3 / pad 1 (kernels/conv_igemm.hip) ----
+bool s2_ok(const at::Tensor& x, const at::Tensor& w) {
+  return shapes_ok(x, w) && w.size(0) % 64 == 0 && x.size(2) % 2 == 0 && x.size(3) % 2 == 0 && w.device() == x.device();
+}
+
+bool s2_supported(const at::Tensor& x, const at::Tensor& w) {
+  if (!s2_ok(x, w)) return false;
+  const at::Tensor wc = w.contiguous(at::MemoryFormat::ChannelsLast);
+  auto a = bh::igemm_conv3x3_s2_fwd(x.data_ptr(), wc.data_ptr(), x.data_ptr(), (int)x.size(0), (int)x.size(2),
+                                    (int)x.size(3), (int)x.size(1), (int)w.size(0));
+  return bh::igemm_supported(a);
+}
+
+// conv2d(x, w, stride 2, padding 1) of channels_last x [N, C, H, W] (H, W even), w [K, C, 3, 3]; with
+// pro_scale / pro_shift x is the raw input of a BatchNorm + ReLU applied on the fly (padding stays zero);
+// stats: also the statistics partials [2, G, K] of the output about kshift
+std::vector<at::Tensor> conv3x3_s2_forward(const at::Tensor& x, const at::Tensor& w,
+                                           const c10::optional<at::Tensor>& pro_scale,
+                                           const c10::optional<at::Tensor>& pro_shift, bool stats,
+                                           const c10::optional<at::Tensor>& kshift) {
+  TORCH_CHECK(s2_ok(x, w), "conv3x3_s2_forward: needs channels_last fp16/bf16 x [N, C, H, W] (H, W even), "
+                           "w [K, C, 3, 3], C and K % 64 == 0");
+  const at::Tensor wc = w.contiguous(at::MemoryFormat::ChannelsLast);
+  auto y = at::empty({x.size(0), w.size(0), x.size(2) / 2, x.size(3) / 2},
+                     x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto a = bh::igemm_conv3x3_s2_fwd(x.data_ptr(), wc.data_ptr(), y.data_ptr(), (int)x.size(0), (int)x.size(2),
+                                    (int)x.size(3), (int)x.size(1), (int)w.size(0));
+  at::Tensor ps, ph, kc, part;
+  if (pro_scale.has_value() && pro_scale->defined()) {
+    TORCH_CHECK(pro_shift.has_value() && pro_shift->defined(), "conv3x3_s2_forward: pro_scale needs pro_shift");
+    ps = pro_scale->contiguous();
+    ph = pro_shift->contiguous();
+    TORCH_CHECK(ps.scalar_type() == at::kFloat && ph.scalar_type() == at::kFloat && ps.numel() == x.size(1) &&
+                    ph.numel() == x.size(1) && ps.device() == x.device() && ph.device() == x.device(),
+                "conv3x3_s2_forward: pro_scale / pro_shift must be fp32 [C] on x's device");
+    a.pro_scale = ps.data_ptr<float>();
+    a.pro_shift = ph.data_ptr<float>();
+  }
+  if (stats) {
+    if (kshift.has_value() && kshift->defined()) {
+      kc = kshift->contiguous();
+      TORCH_CHECK(kc.scalar_type() == at::kFloat && kc.numel() == w.size(0) && kc.device() == x.device(),
+                  "conv3x3_s2_forward: kshift must be fp32 [K] on x's device");
+      a.kshift = kc.data_ptr<float>();
+    }
+    part = at::empty({2, (int64_t)bh::igemm_parts(a), w.size(0)}, x.options().dtype(at::kFloat));
+    a.part = part.data_ptr<float>();
+  } else {
+    part = at::empty({0}, x.options().dtype(at::kFloat));
+  }
+  TORCH_CHECK(bh::igemm_supported(a), "conv3x3_s2_forward: unsupported arguments (alignment / size)");
+  bh::igemm_run(dtype_code(x.scalar_type()), a, stream_for(x));
+  return {y, part};
+}
+
+// grad of conv2d(x, w, stride 2, padding 1) w.r.t. x (x [N, C, H, W], H and W even) from dy [N, K, H/2, W/2]
+at::Tensor conv3x3_s2_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H, int64_t W) {
+  TORCH_CHECK(dy.is_cuda() && w.is_cuda() && dy.dim() == 4 && w.dim() == 4 && w.size(0) == dy.size(1) &&
+                  w.size(2) == 3 && w.size(3) == 3 && dy.scalar_type() == w.scalar_type() &&
+                  (dy.scalar_type() == at::kHalf || dy.scalar_type() == at::kBFloat16) &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast) && dy.size(1) % 64 == 0 && w.size(1) % 64 == 0 &&
+                  H % 2 == 0 && W % 2 == 0 && dy.size(2) == H / 2 && dy.size(3) == W / 2,
+              "conv3x3_s2_dgrad: needs channels_last fp16/bf16 dy [N, K, H/2, W/2], w [K, C, 3, 3], C and K % 64 == 0");
+  // [C][3][3][K]: the weights with input and output channels swapped (a 9 C K-element copy)
+  const at::Tensor wt = w.transpose(0, 1).contiguous(at::MemoryFormat::ChannelsLast);
+  auto dx = at::empty({dy.size(0), w.size(1), H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto a = bh::igemm_conv3x3_s2_dgrad(dy.data_ptr(), wt.data_ptr(), dx.data_ptr(), (int)dy.size(0), (int)H, (int)W,
+                                      (int)w.size(1), (int)w.size(0));
+  TORCH_CHECK(bh::igemm_supported(a), "conv3x3_s2_dgrad: unsupported arguments (alignment / size)");
+  bh::igemm_run(dtype_code(dy.scalar_type()), a, stream_for(dy));
+  return dx;
+}
+
 }  // namespace
 
 void register_conv(pybind11::module_& root) {
@@ -323,14 +397,21 @@ void register_conv(pybind11::module_& root) {
         "ResNet stem conv (7x7/2, 3 -> 64) + BatchNorm statistics partials [2, G, 64] of its output about kshift");
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("grad_out"), py::arg("R"), py::arg("stride") = 1,
         py::arg("pro_scale") = py::none(), py::arg("pro_shift") = py::none(),
-        "weight gradient of conv2d(x', w, stride, padding=(R-1)//2), R in {1, 3} (stride 2: R = 1), x' = x or "
-        "relu(x * pro_scale + pro_shift) per channel (stride 1): [K, C, R, R] channels_last");
+        "weight gradient of conv2d(x', w, stride, padding=(R-1)//2), R in {1, 3}, stride in {1, 2}, x' = x or "
+        "relu(x * pro_scale + pro_shift) per channel: [K, C, R, R] channels_last");
   m.def("wgrad_supported", &wgrad_supported, py::arg("x"), py::arg("grad_out"), py::arg("R"), py::arg("stride") = 1);
   m.def("gemm_n64", &gemm_n64, py::arg("a"), py::arg("b"), py::arg("resid") = c10::nullopt,
         "a [M, K] . b[64, K]^T (+ resid [M, 64]), K in {64, 128, 256}, M % 32 == 0 (kernels/gemm_n64.hip)");
   m.def("gemm_n64_supported", &gemm_n64_ok, py::arg("a"), py::arg("b"));
   m.def("stem_forward", &stem_forward, py::arg("x"), py::arg("weight"),
         "ResNet stem conv2d(x, w, stride=2, padding=3), 3 -> 64 channels at 224x224, channels_last fp16 / bf16");
+  m.def("conv3x3_s2_forward", &conv3x3_s2_forward, py::arg("x"), py::arg("weight"), py::arg("pro_scale") = py::none(),
+        py::arg("pro_shift") = py::none(), py::arg("stats") = false, py::arg("kshift") = py::none(),
+        "conv2d(x', w, stride=2, padding=1) on the implicit-GEMM MFMA kernel (x' = x or relu(x * pro_scale + "
+        "pro_shift)); returns [y, statistics partials [2, G, K] about kshift (empty unless stats)]");
+  m.def("conv3x3_s2_dgrad", &conv3x3_s2_dgrad, py::arg("grad_out"), py::arg("weight"), py::arg("H"), py::arg("W"),
+        "grad of conv2d(x, w, stride=2, padding=1) w.r.t. x [N, C, H, W]: four stride-1 phase convolutions in one launch");
+  m.def("s2_supported", &s2_supported, py::arg("x"), py::arg("weight"));
   m.def("stem_supported", &stem_ok, py::arg("x"), py::arg("weight"));
   m.def("stem_wgrad", &stem_wgrad, py::arg("x"), py::arg("grad_out"),
         "weight gradient of the ResNet stem conv (7x7 / 2, 3 -> 64 at 224x224): [64, 3, 7, 7] channels_last");

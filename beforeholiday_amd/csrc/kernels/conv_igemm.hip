@@ -1,0 +1,388 @@
+// Implicit-GEMM NHWC convolution on MFMA 32x32x16 (gfx950): see bh/igemm_api.h.
+//
+// GEMM view: rows = output pixels of the grid, columns = output channels, reduction = (tap, input
+// channel). A workgroup (4 waves) owns a tile of 4 * MW pixels x NC output channels; each k-step is one
+// tap x 64 input channels. The A operand (pixels x channels) never touches LDS: lane (r, h) of a wave
+// loads channels 16 ks + 8 h .. + 7 of its pixel r straight into its MFMA fragment (16-byte buffer
+// loads through a whole-tensor resource: a tap that falls outside the image gets an out-of-range
+// offset and reads zeros -- the convolution's padding -- with no select in front of the MFMAs). The
+// stride-2 gather is only address math: the re-reads of an input pixel by its <= 4 taps hit L2. The
+// B operand (the [NC x 64] weight slice of the k-step) is staged in LDS, double buffered, rows padded
+// by 16 bytes (the 16-lane phases of a ds_read_b128 hit distinct banks); its next slice and the next
+// A fragments are in flight during the current k-step's MFMAs. Each lane keeps MW / 32 x NC / 32
+// accumulator tiles (the B fragment read from LDS is reused MW / 32 times).
+//
+// Epilogue: acc[m][t][v] is output pixel 32 m + 8 (v >> 2) + 4 h + (v & 3) of the wave's rows,
+// channel 32 t + r: 2-byte stores, 32 lanes = 64 contiguous bytes of one pixel. The statistics of
+// the stored values (the next BatchNorm) are reduced per workgroup in a fixed order (lane halves,
+// then waves through LDS) into one partial row per pixel tile: deterministic, no atomics.
+#include "bh/api.h"
+#include "bh/device.h"
+#include "bh/igemm_api.h"
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
+
+namespace bh {
+namespace {
+
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef __bf16 b8v __attribute__((ext_vector_type(8)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+typedef int i4v __attribute__((ext_vector_type(4)));
+
+template <typename T> struct Mfi;
+template <> struct Mfi<f16> {
+  typedef h8v v8;
+  static BH_DEVICE f16v run(i4v a, i4v b, f16v c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8v, a), __builtin_bit_cast(h8v, b), c, 0, 0, 0);
+  }
+};
+template <> struct Mfi<bf16> {
+  typedef b8v v8;
+  static BH_DEVICE f16v run(i4v a, i4v b, f16v c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(b8v, a), __builtin_bit_cast(b8v, b), c, 0, 0, 0);
+  }
+};
+
+constexpr int kThreads = 256;
+constexpr int kWaves = 4;
+constexpr int kCK = 64;            // input channels per k-step
+constexpr int kRS = kCK * 2 + 16;  // LDS bytes per staged weight row
+constexpr int kMaxProC = 512;
+constexpr int kOutOfRange = 0x7ff00000;  // a byte offset past every tensor the kernel reads
+
+template <typename T, int NC, int MW, bool PRO, bool STATS>
+__global__ __launch_bounds__(kThreads, 2) void k_igemm(IgemmArgs a, int tiles_m) {
+  constexpr int NT = NC / 32, MT = MW / 32, NB = NC / 32;  // NB: 16-byte weight pieces per thread per k-step
+  using V8 = typename Mfi<T>::v8;
+  __shared__ __attribute__((aligned(16))) char smem[2 * NC * kRS + (PRO ? 8 * kMaxProC : 0)];
+  const int mt = blockIdx.x;
+  if (mt >= tiles_m) return;  // (whole workgroup, before any barrier)
+  const IgemmPhase& ph = a.ph[blockIdx.z];
+  const int o0 = blockIdx.y * NC;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int Ha = a.Ha, Wa = a.Wa, Ca = a.Ca;
+  const int HWg = a.Hg * a.Wg;
+  const int64_t P = (int64_t)a.N * HWg;
+  float* ss = reinterpret_cast<float*>(smem + 2 * NC * kRS);
+  if constexpr (PRO) {
+    for (int c = tid; c < Ca; c += kThreads) {
+      ss[c] = a.pro_scale[c];
+      ss[kMaxProC + c] = a.pro_shift[c];
+    }
+  }
+  // this lane's A pixel of each 32-row sub-strip
+  int pn[MT], pi[MT], pj[MT];
+  bool pv[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const int64_t p = (int64_t)mt * (kWaves * MW) + wave * MW + 32 * m + r;
+    pv[m] = p < P;
+    const int pp = pv[m] ? (int)p : 0;
+    pn[m] = pp / HWg;
+    const int rem = pp - pn[m] * HWg;
+    pi[m] = rem / a.Wg;
+    pj[m] = rem - pi[m] * a.Wg;
+  }
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(a.a), 0, (int)((int64_t)a.N * Ha * Wa * Ca * 2), 0x00020000);
+  const T* __restrict__ Bw = reinterpret_cast<const T*>(a.b);
+  const int nch = Ca / kCK, steps = ph.ntaps * nch;
+
+  // A fragments of k-step s: ar[m][ks] = channels 16 ks + 8 h .. + 7 of the tap's input pixel
+  auto a_load = [&](int s, i4v(&ar)[MT][4], uint32_t& msk) __attribute__((always_inline)) {
+    const int t = s / nch, c = s - t * nch;
+    const int oy = ph.oy[t], ox = ph.ox[t];
+    msk = 0;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      const int yi = pi[m] * a.sa + oy, xi = pj[m] * a.sa + ox;
+      const bool ok = pv[m] && yi >= 0 && yi < Ha && xi >= 0 && xi < Wa;
+      const int off = ok ? (((pn[m] * Ha + yi) * Wa + xi) * Ca + c * kCK + 8 * h) * 2 : kOutOfRange;
+      msk |= (ok ? 1u : 0u) << m;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) ar[m][ks] = __builtin_amdgcn_raw_buffer_load_b128(rsA, off + 32 * ks, 0, 0);
+    }
+  };
+  // weight slice of k-step s: rows o0 .. o0 + NC - 1, channels c * 64 .. + 63 of tap tap[t]
+  auto b_load = [&](int s, i4v(&br)[NB]) __attribute__((always_inline)) {
+    const int t = s / nch, c = s - t * nch;
+    const int tap = ph.tap[t];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int q = tid + i * kThreads, row = q >> 3, ch = q & 7;
+      br[i] = *reinterpret_cast<const i4v*>(Bw + ((int64_t)(o0 + row) * a.taps_total + tap) * Ca + c * kCK + ch * 8);
+    }
+  };
+  auto b_store = [&](char* buf, const i4v(&br)[NB]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int q = tid + i * kThreads;
+      *reinterpret_cast<i4v*>(buf + (q >> 3) * kRS + (q & 7) * 16) = br[i];
+    }
+  };
+
+  f16v acc[MT][NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[m][t][i] = 0.f;
+
+  auto compute = [&](const char* buf, i4v(&ar)[MT][4], uint32_t msk, int s) __attribute__((always_inline)) {
+    if constexpr (PRO) {
+      const int c = s - (s / nch) * nch;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int cb = c * kCK + 16 * ks + 8 * h;
+        const float4 c0 = *reinterpret_cast<const float4*>(ss + cb);
+        const float4 c1 = *reinterpret_cast<const float4*>(ss + cb + 4);
+        const float4 d0 = *reinterpret_cast<const float4*>(ss + kMaxProC + cb);
+        const float4 d1 = *reinterpret_cast<const float4*>(ss + kMaxProC + cb + 4);
+        const float sc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        const float sh[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          if (!((msk >> m) & 1u)) continue;  // padding pads the normalised activation: stays zero
+          V8 v = __builtin_bit_cast(V8, ar[m][ks]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = from_f<T>(fmaxf(fmaf(to_f<T>(v[j]), sc[j], sh[j]), 0.f));
+          ar[m][ks] = __builtin_bit_cast(i4v, v);
+        }
+      }
+    }
+    (void)msk;
+    (void)s;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const i4v bf = *reinterpret_cast<const i4v*>(buf + (32 * t + r) * kRS + 32 * ks + 16 * h);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m][t] = Mfi<T>::run(ar[m][ks], bf, acc[m][t]);
+      }
+  };
+
+  char* buf0 = smem;
+  char* buf1 = smem + NC * kRS;
+  i4v a0[MT][4], a1[MT][4], br[NB];
+  uint32_t m0 = 0, m1 = 0;
+  a_load(0, a0, m0);
+  b_load(0, br);
+  b_store(buf0, br);
+  __syncthreads();  // weight slice 0 (and the prologue constants) visible
+  for (int s = 0; s < steps; s += 2) {
+    if (s + 1 < steps) {
+      a_load(s + 1, a1, m1);
+      b_load(s + 1, br);
+    }
+    compute(buf0, a0, m0, s);
+    if (s + 1 < steps) b_store(buf1, br);
+    __syncthreads();
+    if (s + 1 >= steps) break;
+    if (s + 2 < steps) {
+      a_load(s + 2, a0, m0);
+      b_load(s + 2, br);
+    }
+    compute(buf1, a1, m1, s + 1);
+    if (s + 2 < steps) b_store(buf0, br);
+    __syncthreads();
+  }
+
+  // ---- epilogue ----
+  T* __restrict__ Y = reinterpret_cast<T*>(a.y);
+  float s1[NT], s2[NT], e0[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    s1[t] = s2[t] = 0.f;
+    e0[t] = (STATS && a.kshift) ? a.kshift[o0 + 32 * t + r] : 0.f;
+  }
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int64_t p = (int64_t)mt * (kWaves * MW) + wave * MW + 32 * m + 8 * (v >> 2) + 4 * h + (v & 3);
+      if (p >= P) continue;
+      const int n = (int)(p / HWg), rem = (int)(p - (int64_t)n * HWg), i = rem / a.Wg, j = rem - i * a.Wg;
+      const int64_t off = (((int64_t)n * a.Hy + i * a.so + ph.py) * a.Wy + j * a.so + ph.px) * a.Nout + o0 + r;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const T o = from_f<T>(acc[m][t][v]);
+        Y[off + 32 * t] = o;
+        if constexpr (STATS) {
+          const float d = to_f<T>(o) - e0[t];
+          s1[t] += d;
+          s2[t] = fmaf(d, d, s2[t]);
+        }
+      }
+    }
+  if constexpr (STATS) {
+    float* red = reinterpret_cast<float*>(smem);  // [waves][2][NC] (the weight buffers are free)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      s1[t] += __shfl_xor(s1[t], 32);
+      s2[t] += __shfl_xor(s2[t], 32);
+      if (h == 0) {
+        red[(wave * 2) * NC + 32 * t + r] = s1[t];
+        red[(wave * 2 + 1) * NC + 32 * t + r] = s2[t];
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < 2 * NC; c += kThreads) {
+      const int stat = c / NC, col = c - stat * NC;
+      float u = 0.f;
+#pragma unroll
+      for (int q = 0; q < kWaves; ++q) u += red[(q * 2 + stat) * NC + col];
+      a.part[((int64_t)stat * tiles_m + mt) * a.Nout + o0 + col] = u;
+    }
+  }
+}
+
+struct Plan {
+  int NC, MW, tiles_m;
+};
+
+Plan make_plan(const IgemmArgs& a) {
+  Plan p;
+  p.NC = a.Nout % 128 == 0 ? 128 : 64;
+  const int64_t P = (int64_t)a.N * a.Hg * a.Wg;
+  const int64_t slices = a.Nout / p.NC;
+  // 128-channel tiles: 32 pixel rows per wave (64 x 128 spills at two waves per SIMD). 64-channel
+  // tiles without the prologue: 64 pixel rows per wave (each weight fragment read from LDS feeds two
+  // MFMAs) while that still leaves >= 2 workgroups per CU
+  p.MW = (p.NC == 64 && !a.pro_scale && ((P + 255) / 256) * slices * a.nphase >= 512) ? 64 : 32;
+  p.tiles_m = (int)((P + 4 * p.MW - 1) / (4 * p.MW));
+  return p;
+}
+
+template <typename T> struct Tag { using type = T; };
+
+}  // namespace
+
+bool igemm_supported(const IgemmArgs& a) {
+  auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (a.N <= 0 || a.Ha <= 0 || a.Wa <= 0 || a.Hg <= 0 || a.Wg <= 0 || a.Ca <= 0 || a.Nout <= 0) return false;
+  if (a.Ca % kCK || a.Nout % 64 || !al(a.a) || !al(a.b) || !al(a.y)) return false;
+  if (a.nphase < 1 || a.nphase > 4 || a.taps_total < 1 || a.taps_total > 255) return false;
+  for (int z = 0; z < a.nphase; ++z) {
+    if (a.ph[z].ntaps < 1 || a.ph[z].ntaps > 9) return false;
+    for (int t = 0; t < a.ph[z].ntaps; ++t)
+      if (a.ph[z].tap[t] >= a.taps_total) return false;
+  }
+  // 32-bit buffer offsets for a (the out-of-range sentinel sits past it), 32-bit pixel indices
+  if ((int64_t)a.N * a.Ha * a.Wa * a.Ca * 2 + 128 >= kOutOfRange) return false;
+  if ((int64_t)a.N * a.Hg * a.Wg >= (1ll << 31)) return false;
+  if (a.pro_scale && (!a.pro_shift || a.Ca > kMaxProC)) return false;
+  if (a.part && a.nphase != 1) return false;
+  return true;
+}
+
+int igemm_parts(const IgemmArgs& a) { return make_plan(a).tiles_m; }
+
+void igemm_run(int dt, const IgemmArgs& a, hipStream_t st) {
+  if (!igemm_supported(a)) throw std::runtime_error("igemm: unsupported shape / arguments");
+  const Plan pl = make_plan(a);
+  const dim3 grid((unsigned)pl.tiles_m, (unsigned)(a.Nout / pl.NC), (unsigned)a.nphase);
+  const bool pro = a.pro_scale != nullptr, stats = a.part != nullptr;
+  auto go = [&](auto tt, auto nc, auto mw) {
+    using T = typename decltype(tt)::type;
+    constexpr int NC = decltype(nc)::value, MW = decltype(mw)::value;
+    auto L = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(kThreads), 0, st, a, pl.tiles_m); };
+    if constexpr (MW == 32) {  // the prologue variants at 64 rows per wave spill
+      if (pro && stats) return L(k_igemm<T, NC, MW, true, true>);
+      if (pro) return L(k_igemm<T, NC, MW, true, false>);
+    }
+    if (stats) L(k_igemm<T, NC, MW, false, true>);
+    else L(k_igemm<T, NC, MW, false, false>);
+  };
+  auto by_mw = [&](auto tt, auto nc) {
+    if constexpr (decltype(nc)::value == 64) {
+      if (pl.MW == 64) return go(tt, nc, std::integral_constant<int, 64>{});
+    }
+    go(tt, nc, std::integral_constant<int, 32>{});
+  };
+  auto by_nc = [&](auto tt) {
+    if (pl.NC == 128) by_mw(tt, std::integral_constant<int, 128>{});
+    else by_mw(tt, std::integral_constant<int, 64>{});
+  };
+  switch (dt) {
+    case kF16: by_nc(Tag<f16>{}); break;
+    case kBF16: by_nc(Tag<bf16>{}); break;
+    default: throw std::runtime_error("igemm: fp16 / bf16 only");
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("igemm: ") + hipGetErrorString(e));
+}
+
+IgemmArgs igemm_conv3x3_s2_fwd(const void* x, const void* w, void* y, int N, int H, int W, int C, int K) {
+  IgemmArgs a;
+  a.a = x;
+  a.b = w;
+  a.y = y;
+  a.N = N;
+  a.Ha = H;
+  a.Wa = W;
+  a.Ca = C;
+  a.Nout = K;
+  a.taps_total = 9;
+  a.Hg = a.Hy = (H + 1) / 2;
+  a.Wg = a.Wy = (W + 1) / 2;
+  a.sa = 2;
+  a.so = 1;
+  a.nphase = 1;
+  IgemmPhase& p = a.ph[0];
+  p.ntaps = 9;
+  for (int t = 0; t < 9; ++t) {
+    p.oy[t] = (signed char)(t / 3 - 1);
+    p.ox[t] = (signed char)(t % 3 - 1);
+    p.tap[t] = (unsigned char)t;
+  }
+  return a;
+}
+
+IgemmArgs igemm_conv3x3_s2_dgrad(const void* dy, const void* wt, void* dx, int N, int H, int W, int C, int K) {
+  // dx[2i + py, 2j + px] = sum over taps (r, s) with 2 yo + r - 1 = 2i + py (and likewise columns) of
+  // dy[yo, xo] . w[r, s]: an even output row takes r = 1 (yo = i), an odd one r = 0 (yo = i + 1) and
+  // r = 2 (yo = i); four phases of 1, 2, 2 and 4 taps over the (H/2) x (W/2) grid
+  IgemmArgs a;
+  a.a = dy;
+  a.b = wt;
+  a.y = dx;
+  a.N = N;
+  a.Ha = H / 2;
+  a.Wa = W / 2;
+  a.Ca = K;
+  a.Nout = C;
+  a.taps_total = 9;
+  a.Hg = H / 2;
+  a.Wg = W / 2;
+  a.sa = 1;
+  a.Hy = H;
+  a.Wy = W;
+  a.so = 2;
+  a.nphase = 4;
+  for (int z = 0; z < 4; ++z) {
+    const int py = z >> 1, px = z & 1;
+    IgemmPhase& p = a.ph[z];
+    p.py = py;
+    p.px = px;
+    p.ntaps = 0;
+    for (int rr = 0; rr < 3; ++rr) {
+      if ((rr & 1) == py) continue;  // parity: 2 yo + rr - 1 == 2 i + py needs rr odd for py = 0, even for 1
+      for (int sc = 0; sc < 3; ++sc) {
+        if ((sc & 1) == px) continue;
+        p.oy[p.ntaps] = (signed char)((py + 1 - rr) / 2);
+        p.ox[p.ntaps] = (signed char)((px + 1 - sc) / 2);
+        p.tap[p.ntaps] = (unsigned char)(rr * 3 + sc);
+        ++p.ntaps;
+      }
+    }
+  }
+  return a;
+}
+
+}  // namespace bh

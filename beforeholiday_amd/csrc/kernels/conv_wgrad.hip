@@ -59,7 +59,7 @@ constexpr int kTile = 64;        // k and c per workgroup
 // 32-lane half) are conflict free, and a slot's address is LINEAR in the slot index: the R*R
 // shifted X fragments are one base register plus immediate offsets (no per-read swizzle math).
 constexpr int kSlot = 192;
-constexpr int kMaxHalo = 240;    // X slots per window
+constexpr int kMaxHalo = 288;    // X slots per window
 constexpr int kMaxD = 128;       // dY slots per window (k-steps x 16)
 // dY slots hold 64 * KT channels: 128 + 64 B (KT = 1) or 256 + 64 B (KT = 2, again four distinct
 // bank quarters for four consecutive slots)
@@ -116,12 +116,17 @@ BH_DEVICE i4v frag2(const char* img, int lo, int hi) {
 // pairs and each wave runs every k-step of the window (no split of the k-steps between the two waves of
 // a SIMD, no LDS hand-off at the end) -- which cuts the bytes staged per MFMA by a quarter; the dY slot
 // grows to 512 + 64 B (144 dwords: again four distinct bank quarters) and the window to 64 pixels.
-template <typename T, int R, int G4, int TH, int KT, int CT = 1, bool PRO = false, bool WIDE = false>
+// S (R = 3 only): the convolution's stride. At S = 2 (the ResNet downsampling 3x3) dY pixel (y, x) of the
+// window reads X pixel (2 y + r - 1, 2 x + s - 1): the X halo is (2 TH + 1) x (8 G4 + 1) slots and the
+// fragment of shift (r, s) sits at slot 2 (row * HC + x) + r * HC + s -- still one base address plus
+// an immediate per shift; only the slot map and the staging addresses change.
+template <typename T, int R, int G4, int TH, int KT, int CT = 1, bool PRO = false, bool WIDE = false, int S = 1>
 __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, ConvWgradGeo g, float* __restrict__ ws,
                                                            T* __restrict__ out) {
+  static_assert(S == 1 || R == 3, "the strided halo is a 3x3 geometry (1x1 stride 2 uses flat windows)");
   constexpr int P = (R - 1) / 2, RR = R * R;
-  constexpr int HC = 4 * G4 + 2 * P, KSTEPS = (TH * G4 + 3) / 4;
-  constexpr int XS = (TH + 2 * P) * HC, DS = KSTEPS * 16;  // X halo / dY pixel slots per window
+  constexpr int HC = S * (4 * G4 - 1) + R, KSTEPS = (TH * G4 + 3) / 4;
+  constexpr int XS = (S * (TH - 1) + R) * HC, DS = KSTEPS * 16;  // X halo / dY pixel slots per window
   constexpr int KW = WIDE ? 4 : 2;  // k sub-tiles of 32 KT across the waves
   static_assert(!WIDE || (R == 1 && KT == 2), "wide tiles: 1x1, two 32-row sub-tiles per wave");
   constexpr int DSL = WIDE ? 576 : dslot<KT>(), TK = 32 * KT * KW;  // dY slot bytes, output channels per workgroup
@@ -173,12 +178,12 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
     if (isx) xch[i < XPW ? i : 0] = (piece < XP && ch < 8 * CT && slot < XS) ? ch : -1;
     if (isx) {
       const int hr = slot / HC, x = slot - hr * HC - P;
-      const bool ok = piece < XP && ch < 8 * CT && slot < XS && x >= 0 && x < W;
+      const bool ok = piece < XP && ch < 8 * CT && slot < XS && x >= 0 && x < S * W;
       // 1x1 / stride 2 (flat windows of whole output rows): dY pixel x of the window reads x pixel
       // 2 x + 2 wout (x / wout) from the window's x origin (input rows are twice as long, and every
       // other one is skipped)
-      const int xin = a.stride == 2 ? 2 * x + 2 * a.wout * (x / a.wout) : x;
-      rel[i] = (((hr - P) * W + xin) * C + c0 + ch * 8) * 2;
+      const int xin = (R == 1 && a.stride == 2) ? 2 * x + 2 * a.wout * (x / a.wout) : x;
+      rel[i] = (((hr - P) * S * W + xin) * C + c0 + ch * 8) * 2;
       hrow[i] = ok ? hr - P : kBad;
     } else {
       const int dbyte = byte, dsl = dbyte / DSL, dch = (dbyte - dsl * DSL) >> 4;
@@ -193,8 +198,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
     const bool isx = i < XPW;
     const int piece = wave + 8 * (isx ? i : i - XPW);
     if (piece >= (isx ? XP : DP)) return;
-    const int y = y0 + hrow[i];
-    const bool ok = hrow[i] != kBad && y >= 0 && y < H;
+    const int sy = isx ? S : 1;  // X rows of a strided 3x3 window start at input row S y0
+    const int y = sy * y0 + hrow[i];
+    const bool ok = hrow[i] != kBad && y >= 0 && y < sy * H;
     const int off = ok ? (n * H + y0) * W * (isx ? C * sx : K) * 2 + rel[i] : kOut;
     if (isx) dma16(rsX, off, __builtin_amdgcn_readfirstlane(lds_addr(buf + piece * 1024)));
     else dma16(rsD, off, __builtin_amdgcn_readfirstlane(lds_addr(buf + BUFX + piece * 1024)));
@@ -216,8 +222,8 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
 #pragma unroll
     for (int i = 0; i < XPW; ++i) {
       const int piece = wave + 8 * i;
-      const int y = y0 + hrow[i];
-      if (xch[i] < 0 || hrow[i] == kBad || y < 0 || y >= H) continue;
+      const int y = S * y0 + hrow[i];
+      if (xch[i] < 0 || hrow[i] == kBad || y < 0 || y >= S * H) continue;
       char* p = buf + piece * 1024 + lane * 16;
       typedef T t8 __attribute__((ext_vector_type(8)));
       t8 v = *reinterpret_cast<const t8*>(p);
@@ -241,7 +247,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int grp = min(4 * ks + 2 * h + j, ng - 1), row = grp / G4;
-      x_off[ks][j] = (row * HC + 4 * (grp - row * G4) + q) * XSL + 2 * 32 * CT * cw + colb;
+      x_off[ks][j] = S * (row * HC + 4 * (grp - row * G4) + q) * XSL + 2 * 32 * CT * cw + colb;
     }
 
   f16v acc[NOFF][KT];
@@ -449,9 +455,12 @@ bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo) {
   if (!(a.R == 1 || a.R == 3) || a.N <= 0 || a.H <= 0 || a.W <= 0 || a.C % kTile || a.K % kTile || !al(a.x) ||
       !al(a.dy) || !al(a.out))
     return false;
-  // stride 2: 1x1 only, windows of whole output rows (W divides 112)
-  if (!(a.stride == 1 || (a.stride == 2 && a.R == 1 && 112 % a.W == 0))) return false;
-  if (a.pro_scale && (a.stride != 1 || !a.pro_shift)) return false;
+  // stride 2: 1x1 (windows of whole output rows, W divides 112) or 3x3 (strided halo, the three
+  // ResNet-50 output widths 28 / 14 / 7)
+  const bool s2r3 = a.stride == 2 && a.R == 3;
+  if (!(a.stride == 1 || (a.stride == 2 && a.R == 1 && 112 % a.W == 0) || (s2r3 && (a.W == 28 || a.W == 14 || a.W == 7))))
+    return false;
+  if (a.pro_scale && ((a.stride != 1 && !s2r3) || !a.pro_shift)) return false;
   // 32-bit buffer offsets (the out-of-image offset sits past both tensors)
   if (2 * (int64_t)a.N * a.H * a.W * std::max(a.C * a.stride * a.stride, a.K) >= 0x7ff00000ll) return false;
   ConvWgradGeo g;
@@ -473,6 +482,13 @@ bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo) {
     g.TH = 1;
     g.wpi = 1;
     g.nwin = (int)((int64_t)a.N * a.H * a.W / win);
+  } else if (s2r3) {
+    // stride 2: the X halo of a window is ~4x its dY pixels, so the windows are shorter (2 rows at
+    // W = 28, 3 at 14, 7 at 7: <= 285 X slots, two buffers <= 139 KiB)
+    g.G4 = (a.W + 3) / 4;
+    g.TH = a.W == 28 ? 2 : (a.W == 14 ? 3 : 7);
+    g.wpi = (a.H + g.TH - 1) / g.TH;
+    g.nwin = a.N * g.wpi;
   } else {
     // ~112 pixels per window: 2 rows at W = 56, 4 at 28, 7 at 14 / 7 (the instantiated geometries)
     g.G4 = (a.W + 3) / 4;
@@ -524,6 +540,11 @@ void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws
       else if (a.R == 1) {
         if (g.ct == 2) g.kt == 2 ? go(k_conv_wgrad<T, 1, 28, 1, 2, 2, P>) : go(k_conv_wgrad<T, 1, 28, 1, 1, 2, P>);
         else g.kt == 2 ? go(k_conv_wgrad<T, 1, 28, 1, 2, 1, P>) : go(k_conv_wgrad<T, 1, 28, 1, 1, 1, P>);
+      }
+      else if (a.stride == 2) {
+        if (g.G4 == 7) go(k_conv_wgrad<T, 3, 7, 2, 1, 1, P, false, 2>);
+        else if (g.G4 == 4) g.kt == 2 ? go(k_conv_wgrad<T, 3, 4, 3, 2, 1, P, false, 2>) : go(k_conv_wgrad<T, 3, 4, 3, 1, 1, P, false, 2>);
+        else g.kt == 2 ? go(k_conv_wgrad<T, 3, 2, 7, 2, 1, P, false, 2>) : go(k_conv_wgrad<T, 3, 2, 7, 1, 1, P, false, 2>);
       }
       else if (g.G4 == 14) go(k_conv_wgrad<T, 3, 14, 2, 1, 1, P>);
       else if (g.G4 == 7) go(k_conv_wgrad<T, 3, 7, 4, 1, 1, P>);

@@ -14,8 +14,8 @@ import torch.nn as nn
 
 
 def conv3x3(cin, cout, stride=1):
-    if _CONV3X3_MODE != "miopen" and stride == 1:
-        return Conv3x3(cin, cout, 3, stride=1, padding=1, bias=False, mode=_CONV3X3_MODE)
+    if _CONV3X3_MODE != "miopen" and stride in (1, 2):
+        return Conv3x3(cin, cout, 3, stride=stride, padding=1, bias=False, mode=_CONV3X3_MODE)
     return nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
 
 
@@ -266,9 +266,41 @@ class _Conv3x3Fn(torch.autograd.Function):
         return gx, gw, None
 
 
+class _Conv3x3S2Fn(torch.autograd.Function):
+    """3x3 / stride-2 / pad-1 convolution of a channels_last activation (the ResNet downsampling
+    blocks' middle conv) on the own MFMA kernels in all three directions: forward and data gradient on
+    the implicit-GEMM kernel (kernels/conv_igemm.hip; the data gradient as four stride-1 phase
+    convolutions), weight gradient on the strided-halo wgrad kernel. No MIOpen: its stride-2 weight
+    gradient is split-K with atomics (not run-to-run repeatable, profiles/miopen_s2_determinism.jsonl)."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        from ..ops import conv as bhconv
+
+        y, _ = bhconv.conv3x3_s2(x, weight)
+        ctx.save_for_backward(x, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from ..ops import conv as bhconv
+
+        x, weight = ctx.saved_tensors
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            gx = bhconv.conv3x3_s2_dgrad(gy, weight, (x.size(2), x.size(3)))
+        if ctx.needs_input_grad[1]:
+            gw = bhconv.conv_wgrad(x, gy, 3, stride=2)
+            if gw.stride() != weight.stride():
+                gw = gw.contiguous()
+        return gx, gw
+
+
 class Conv3x3(nn.Conv2d):
-    """nn.Conv2d(k=3, stride=1, padding=1, bias=False) whose channels_last fp16 / bf16 GPU path picks
-    the direct MFMA kernel or MIOpen per shape (``mode`` "auto" / "direct" / "miopen")."""
+    """nn.Conv2d(k=3, stride=1 or 2, padding=1, bias=False) whose channels_last fp16 / bf16 GPU path
+    runs the own MFMA kernels: stride 1 the direct kernel (or MIOpen per shape, ``mode`` "auto" /
+    "direct" / "miopen"), stride 2 the implicit-GEMM kernels (:class:`_Conv3x3S2Fn`)."""
 
     def __init__(self, *args, mode="auto", **kw):
         super().__init__(*args, **kw)
@@ -276,14 +308,19 @@ class Conv3x3(nn.Conv2d):
 
     def fast_path(self, x):
         if not (self.mode != "miopen" and x.is_cuda and x.dim() == 4 and x.dtype == self.weight.dtype
-                and self.stride == (1, 1) and self.padding == (1, 1) and self.dilation == (1, 1) and self.groups == 1):
+                and self.stride in ((1, 1), (2, 2)) and self.padding == (1, 1) and self.dilation == (1, 1)
+                and self.groups == 1):
             return False
         from ..ops import conv as bhconv
 
+        if self.stride == (2, 2):
+            return bhconv.s2_supported(x, self.weight)
         return bhconv.supported(x, self.weight)
 
     def forward(self, x):
         if self.fast_path(x):
+            if self.stride == (2, 2):
+                return _Conv3x3S2Fn.apply(x, self.weight)
             return _Conv3x3Fn.apply(x, self.weight, self.mode)
         return super().forward(x)
 
@@ -755,7 +792,7 @@ class _BNConvFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, y, part, bn_w, bn_b, running_mean, running_var, eps, momentum, process_group, num_batches,
-                conv_w, kshift_out, R):
+                conv_w, kshift_out, R, stride=1):
         from ..ops import conv_bn
         from ..ops import syncbn
         from ..parallel.optimized_sync_batchnorm import _all_reduce, _world
@@ -777,7 +814,9 @@ class _BNConvFn(torch.autograd.Function):
                                                                      running_var, momentum, eps, num_batches, bumped)
         if num_batches is not None and not bumped:
             num_batches.add_(1)  # (the normalisation pass would have bumped it)
-        if R == 3:
+        if R == 3 and stride == 2:  # the downsampling 3x3 on the implicit-GEMM kernel
+            out, part_out = submodule("conv_cuda").conv3x3_s2_forward(y, conv_w, scale, shift, True, kshift_out)
+        elif R == 3:
             out, part_out = submodule("conv_cuda").conv3x3_bn_forward(y, conv_w, scale, shift, True, kshift_out)
         else:
             n, _, h, w = y.shape
@@ -786,7 +825,7 @@ class _BNConvFn(torch.autograd.Function):
                                          pro_shift=shift, epi="stats", kshift=kshift_out)
             out = o2d.view(n, h, w, k).permute(0, 3, 1, 2)
         ctx.save_for_backward(y, conv_w, bn_w, mean, invstd, scale, shift, count_t)
-        ctx.process_group, ctx.world, ctx.R = process_group, world, R
+        ctx.process_group, ctx.world, ctx.R, ctx.stride = process_group, world, R, stride
         ctx.mark_non_differentiable(part_out)
         ctx.set_materialize_grads(False)
         return out, part_out
@@ -803,7 +842,9 @@ class _BNConvFn(torch.autograd.Function):
         gy = gy.contiguous(memory_format=torch.channels_last)
         n, C, h, w = y.shape
         sums = None
-        if ctx.R == 3:
+        if ctx.R == 3 and ctx.stride == 2:
+            dA = bhconv.conv3x3_s2_dgrad(gy, conv_w, (h, w))
+        elif ctx.R == 3:
             dA = bhconv.conv3x3_dgrad(gy, conv_w)
         else:
             k = conv_w.size(0)
@@ -820,7 +861,7 @@ class _BNConvFn(torch.autograd.Function):
             dA = dA2d.view(n, h, w, C).permute(0, 3, 1, 2)
         g_conv = None
         if ctx.needs_input_grad[10]:
-            g_conv = bhconv.conv_wgrad(y, gy, ctx.R, scale, shift)
+            g_conv = bhconv.conv_wgrad(y, gy, ctx.R, scale, shift, stride=ctx.stride)
             if g_conv.stride() != conv_w.stride():
                 g_conv = g_conv.contiguous()
         need_w = bn_w is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
@@ -835,13 +876,13 @@ class _BNConvFn(torch.autograd.Function):
                 _all_reduce(sums, ctx.process_group)
         gx, _ = syncbn.backward_dgrad(dA, y, None, mean, invstd, bn_w, sums, count, scale, shift, True, False, None)
         return gx, None, (gw if need_w else None), (gb if need_w else None), None, None, None, None, None, None, \
-            g_conv, None, None
+            g_conv, None, None, None
 
 
-def _bn_conv(bn, y, part, conv_w, kshift_out, R):
+def _bn_conv(bn, y, part, conv_w, kshift_out, R, stride=1):
     exp_avg = bn.momentum if bn.momentum is not None else -1.0
     return _BNConvFn.apply(y, part, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, exp_avg,
-                           bn.process_group, bn.num_batches_tracked, conv_w, kshift_out, R)
+                           bn.process_group, bn.num_batches_tracked, conv_w, kshift_out, R, stride)
 
 
 _FOLD_BN = os.environ.get("BH_FOLD_BN", "1") != "0"
@@ -919,6 +960,10 @@ class Bottleneck(nn.Module):
         if _FOLD_APPLY in ("all", "bn1") and self.stride == 1 and bhconv.supported(y1, self.conv2.weight):
             # bn1 + ReLU inside conv2's halo prologue (and its weight gradient's LDS prologue)
             y2, p2 = _bn_conv(self.bn1, y1, p1, self.conv2.weight, _kshift(self.bn2), 3)
+        elif self.stride == 2 and bhconv.s2_supported(y1, self.conv2.weight):
+            # the downsampling 3x3: bn1 + ReLU in the implicit-GEMM kernel's A-fragment prologue (and the
+            # strided wgrad kernel's LDS prologue), bn2's statistics in its epilogue
+            y2, p2 = _bn_conv(self.bn1, y1, p1, self.conv2.weight, _kshift(self.bn2), 3, stride=2)
         else:
             l1 = BNLink()
             a1 = self.bn1.forward_from_stats(y1, p1, link=l1)

@@ -58,22 +58,63 @@ def bn_relu_apply(x: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor) -> 
     return torch.relu(x.float() * s + b).to(x.dtype)
 
 
+def s2_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """The stride-2 3x3 / pad-1 kernels (kernels/conv_igemm.hip forward and data gradient,
+    kernels/conv_wgrad.hip weight gradient) cover (x, w): channels_last fp16 / bf16, C and K
+    multiples of 64, even H and W."""
+    return x.is_cuda and available() and submodule("conv_cuda").s2_supported(x, w)
+
+
+def conv3x3_s2(x: torch.Tensor, w: torch.Tensor, pro_scale: torch.Tensor = None, pro_shift: torch.Tensor = None,
+               stats: bool = False, kshift: torch.Tensor = None):
+    """``conv2d(x', w, stride=2, padding=1)`` on the implicit-GEMM MFMA kernel, x' = x or
+    ``relu(x * pro_scale + pro_shift)`` (a BatchNorm + ReLU folded into the convolution; the padding
+    stays zero). Returns ``(y, part)``: part is the [2, G, K] statistics partials of y about kshift
+    when ``stats`` (empty otherwise). Fallback: ``F.conv2d`` (+ a statistics pass)."""
+    if s2_supported(x, w):
+        y, part = submodule("conv_cuda").conv3x3_s2_forward(x, w, pro_scale, pro_shift, stats, kshift)
+        return y, part
+    xin = bn_relu_apply(x, pro_scale, pro_shift) if pro_scale is not None else x
+    y = F.conv2d(xin, w, stride=2, padding=1)
+    part = torch.empty(0, device=x.device)
+    if stats:
+        yf = y.float().transpose(0, 1).reshape(y.size(1), -1)
+        if kshift is not None:
+            yf = yf - kshift.view(-1, 1)
+        part = torch.stack([yf.sum(1), yf.square().sum(1)]).view(2, 1, -1)
+    return y, part
+
+
+def conv3x3_s2_dgrad(dy: torch.Tensor, w: torch.Tensor, hw) -> torch.Tensor:
+    """dX [N, C, H, W] of ``conv2d(x, w, stride=2, padding=1)`` from dY: four stride-1 phase
+    convolutions of dY (1, 2, 2 and 4 taps) in one launch of the implicit-GEMM kernel."""
+    H, W = hw
+    if dy.is_cuda and available() and H % 2 == 0 and W % 2 == 0 and dy.is_contiguous(memory_format=torch.channels_last) \
+            and dy.dtype in (torch.float16, torch.bfloat16) and dy.size(1) % 64 == 0 and w.size(1) % 64 == 0:
+        return submodule("conv_cuda").conv3x3_s2_dgrad(dy, w, H, W)
+    x = torch.empty(dy.size(0), w.size(1), H, W, device=dy.device, dtype=dy.dtype)
+    return torch.ops.aten.convolution_backward(dy, x, w, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1,
+                                               [True, False, False])[0]
+
+
 def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, r: int, pro_scale: torch.Tensor = None,
-               pro_shift: torch.Tensor = None) -> torch.Tensor:
-    """Weight gradient of ``conv2d(x', w, stride=1, padding=(r-1)//2)`` for r in {1, 3}, where x' is x or,
+               pro_shift: torch.Tensor = None, stride: int = 1) -> torch.Tensor:
+    """Weight gradient of ``conv2d(x', w, stride, padding=(r-1)//2)`` for r in {1, 3}, where x' is x or,
     with ``pro_scale`` / ``pro_shift``, ``relu(x * pro_scale + pro_shift)`` per channel (a BatchNorm +
     ReLU folded into the convolution, applied to the staged tiles in LDS): the MFMA kernel of
     kernels/conv_wgrad.hip (both operands read through LDS transposes, fp32 split partials summed in a
-    fixed order) for channels_last fp16 / bf16 with C, K multiples of 64; otherwise
+    fixed order; stride 2: 1x1, or 3x3 at output widths 28 / 14 / 7) for channels_last fp16 / bf16
+    with C, K multiples of 64; otherwise
     ``torch.ops.aten.convolution_backward``. Returns [K, C, r, r] (channels_last on the kernel path)."""
-    if wgrad_supported(x, dy, r):
-        return submodule("conv_cuda").conv_wgrad(x, dy, r, 1, pro_scale, pro_shift)
+    if wgrad_supported(x, dy, r, stride):
+        return submodule("conv_cuda").conv_wgrad(x, dy, r, stride, pro_scale, pro_shift)
     if pro_scale is not None:
         x = bn_relu_apply(x, pro_scale, pro_shift)
     w_shape = [dy.size(1), x.size(1), r, r]
     p = (r - 1) // 2
     return torch.ops.aten.convolution_backward(dy, x, torch.empty(w_shape, device=x.device, dtype=x.dtype), None,
-                                               [1, 1], [p, p], [1, 1], False, [0, 0], 1, [False, True, False])[1]
+                                               [stride, stride], [p, p], [1, 1], False, [0, 0], 1,
+                                               [False, True, False])[1]
 
 
 def stem_supported(x: torch.Tensor, w: torch.Tensor) -> bool:
