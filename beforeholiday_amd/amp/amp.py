@@ -148,6 +148,7 @@ def init(enabled=True, loss_scale="dynamic", patch_type=torch.float16, enable_ca
                            "torch.float16 and torch.bfloat16.")
     low_list, low_cast = _LOW[patch_type]
     handle = AmpHandle(loss_scale, enable_caching, verbose)
+    handle.cast_dtype = patch_type
     for rule in list(_rules(low_list, low_cast, allow_banned)):
         rule.apply(rule.module, rule.name, handle, verbose)
     _USER_RULES.clear()
@@ -157,3 +158,26 @@ def init(enabled=True, loss_scale="dynamic", patch_type=torch.float16, enable_ca
     _DECORATOR_HANDLE = handle
     _amp_state.handle = handle
     return handle
+
+
+def kernel_cast_dtype():
+    """The 16-bit dtype amp's O1 / O4 function patching casts matmul-class ops to (None when that
+    patching is off or disabled, e.g. inside the optimizer step). Modules that call the own MFMA
+    kernels directly -- which the patched torch functions never see -- use it to run those kernels in
+    the same precision the cast lists give ``conv2d`` / ``linear`` (reference:
+    apex/amp/lists/functional_overrides.py:18-32)."""
+    h = _amp_state.handle
+    if h is None or not h.is_active():
+        return None
+    return getattr(h, "cast_dtype", None)
+
+
+def kernel_cast(t):
+    """``t`` in :func:`kernel_cast_dtype` through amp's per-iteration weight-cast cache (a leaf fp32
+    parameter is cast once per iteration; the cast is differentiable, so the parameter still gets an
+    fp32 gradient). Returns ``t`` unchanged when no cast applies."""
+    dt = kernel_cast_dtype()
+    if dt is None or not t.is_floating_point() or t.dtype == dt:
+        return t
+    fn = utils.maybe_half if dt == torch.float16 else utils.maybe_bfloat16
+    return utils.cached_cast(fn, t, _amp_state.handle.cache)

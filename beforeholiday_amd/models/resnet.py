@@ -30,6 +30,31 @@ def _time_ms(fn, reps=3):
     return a.elapsed_time(b) / reps
 
 
+def _kx(x):
+    """x as the own kernels consume it: under amp O1 / O4 (fp32 model, torch functions patched to
+    cast to 16 bits) an fp32 activation is cast to amp's dtype here, since the kernel paths below are
+    not torch functions the cast lists could see. Otherwise x unchanged."""
+    from ..amp.amp import kernel_cast_dtype
+
+    dt = kernel_cast_dtype()
+    if dt is not None and x.is_cuda and x.dtype == torch.float32:
+        return x.to(dt)
+    return x
+
+
+def _kw(weight, x):
+    """``weight`` in x's dtype for the kernel paths: the weight itself for a 16-bit model (O2 / O5 / a
+    .half() model), amp's per-iteration 16-bit copy of an fp32 weight under O1 / O4 (differentiable:
+    the fp32 parameter gets an fp32 gradient), None when the kernel paths do not apply."""
+    if weight.dtype == x.dtype:
+        return weight
+    from ..amp.amp import kernel_cast, kernel_cast_dtype
+
+    if weight.dtype == torch.float32 and x.dtype == kernel_cast_dtype():
+        return kernel_cast(weight)
+    return None
+
+
 # per-shape choice of the 1x1 / stride-1 convolution paths: {(N, Cin, H, W, Cout, dtype, dir): "gemm" | "miopen"}
 _CONV1X1_CHOICE = {}
 
@@ -208,13 +233,16 @@ class Conv1x1(nn.Conv2d):
         super().__init__(*args, **kw)
         self.mode = mode
 
-    def fast_path(self, x):
+    def fast_path(self, x, w=None):
+        w = self.weight if w is None else w
         return (x.is_cuda and self.stride == (1, 1) and self.groups == 1 and x.dim() == 4 and self.mode != "miopen"
-                and x.is_contiguous(memory_format=torch.channels_last) and x.dtype == self.weight.dtype)
+                and x.is_contiguous(memory_format=torch.channels_last) and x.dtype == w.dtype)
 
     def forward(self, x, box=None):
-        if self.fast_path(x):
-            return _Conv1x1Fn.apply(x, self.weight, self.mode, box)
+        xk = _kx(x)
+        w = _kw(self.weight, xk)
+        if w is not None and self.fast_path(xk, w):
+            return _Conv1x1Fn.apply(xk, w, self.mode, box)
         return super().forward(x)
 
 
@@ -306,22 +334,25 @@ class Conv3x3(nn.Conv2d):
         super().__init__(*args, **kw)
         self.mode = mode
 
-    def fast_path(self, x):
-        if not (self.mode != "miopen" and x.is_cuda and x.dim() == 4 and x.dtype == self.weight.dtype
+    def fast_path(self, x, w=None):
+        w = self.weight if w is None else w
+        if not (self.mode != "miopen" and x.is_cuda and x.dim() == 4 and x.dtype == w.dtype
                 and self.stride in ((1, 1), (2, 2)) and self.padding == (1, 1) and self.dilation == (1, 1)
                 and self.groups == 1):
             return False
         from ..ops import conv as bhconv
 
         if self.stride == (2, 2):
-            return bhconv.s2_supported(x, self.weight)
-        return bhconv.supported(x, self.weight)
+            return bhconv.s2_supported(x, w)
+        return bhconv.supported(x, w)
 
     def forward(self, x):
-        if self.fast_path(x):
+        xk = _kx(x)
+        w = _kw(self.weight, xk)
+        if w is not None and self.fast_path(xk, w):
             if self.stride == (2, 2):
-                return _Conv3x3S2Fn.apply(x, self.weight)
-            return _Conv3x3Fn.apply(x, self.weight, self.mode)
+                return _Conv3x3S2Fn.apply(xk, w)
+            return _Conv3x3Fn.apply(xk, w, self.mode)
         return super().forward(x)
 
 
@@ -499,11 +530,13 @@ class StemConv(nn.Conv2d):
         self.mode = mode
 
     def forward(self, x):
-        if self.mode != "miopen" and x.is_cuda and x.dtype == self.weight.dtype:
+        xk = _kx(x)
+        w = _kw(self.weight, xk)
+        if self.mode != "miopen" and x.is_cuda and w is not None:
             from ..ops import conv as bhconv
 
-            if bhconv.stem_supported(x, self.weight):
-                return _StemConvFn.apply(x, self.weight, self.mode)
+            if bhconv.stem_supported(xk, w):
+                return _StemConvFn.apply(xk, w, self.mode)
         return super().forward(x)
 
 
@@ -518,10 +551,12 @@ class Conv1x1S2(nn.Conv2d):
         self.gather = gather
 
     def forward(self, x):
-        if (x.is_cuda and self.mode != "miopen" and x.dim() == 4 and x.dtype == self.weight.dtype
-                and x.is_contiguous(memory_format=torch.channels_last) and x.size(2) % 2 == 0 and x.size(3) % 2 == 0):
+        xk = _kx(x)
+        w = _kw(self.weight, xk)
+        if (x.is_cuda and self.mode != "miopen" and x.dim() == 4 and w is not None
+                and xk.is_contiguous(memory_format=torch.channels_last) and x.size(2) % 2 == 0 and x.size(3) % 2 == 0):
             fn = _Conv1x1S2Fn if self.gather else _Conv1x1S2WFn
-            return fn.apply(x, self.weight, self.mode)
+            return fn.apply(xk, w, self.mode)
         return super().forward(x)
 
 
@@ -923,7 +958,7 @@ class Bottleneck(nn.Module):
 
         bns = [self.bn1, self.bn2, self.bn3] + ([self.downsample[1]] if self.downsample is not None else [])
         return (_FOLD_BN and self.training and x.is_cuda and x.dim() == 4 and x.dtype in (torch.float16, torch.bfloat16)
-                and x.is_contiguous(memory_format=torch.channels_last) and self.conv1.weight.dtype == x.dtype
+                and x.is_contiguous(memory_format=torch.channels_last) and _kw(self.conv1.weight, x) is not None
                 and all(isinstance(b, SyncBatchNorm) and b.track_running_stats and b.channel_last
                         and b.running_mean is not None and b.running_mean.dtype == torch.float32 for b in bns)
                 and (self.downsample is None or len(self.downsample) == 2))
@@ -940,46 +975,50 @@ class Bottleneck(nn.Module):
         if c > 128 or n * h * w < 100000:
             return False
         a2d = y2.permute(0, 2, 3, 1).reshape(-1, c)
-        return conv_bn.supported(a2d, self.conv3.weight.view(k, c), pro=True, epi="stats")
+        w3 = self.conv3.weight if self.conv3.weight.dtype == y2.dtype else self.conv3.weight.detach().to(y2.dtype)
+        return conv_bn.supported(a2d, w3.view(k, c), pro=True, epi="stats")
 
     def _forward_folded(self, x):
         from ..ops import conv as bhconv
         from ..parallel.optimized_sync_batchnorm import BNLink
 
         ds = self.downsample
+        # the convolutions' weights in x's dtype (amp O1 / O4: the per-iteration 16-bit copies)
+        w1, w2, w3 = (_kw(c.weight, x) for c in (self.conv1, self.conv2, self.conv3))
+        wd = _kw(ds[0].weight, x) if ds is not None else None
         if ds is not None:  # conv1 and the downsample conv as one node (no residual stash needed)
-            y1, p1, yd, pd = _Conv1DsFn.apply(x, self.conv1.weight, ds[0].weight, _kshift(self.bn1), _kshift(ds[1]),
+            y1, p1, yd, pd = _Conv1DsFn.apply(x, w1, wd, _kshift(self.bn1), _kshift(ds[1]),
                                               self.stride == 2)
             box = None
         else:
             box = {} if (torch.is_grad_enabled() and x.requires_grad) else None
-            y1, p1 = _Conv1x1BNFn.apply(x, self.conv1.weight, _kshift(self.bn1), None, box, False)
+            y1, p1 = _Conv1x1BNFn.apply(x, w1, _kshift(self.bn1), None, box, False)
         l2 = None
         y3 = None
         y2 = None
-        if _FOLD_APPLY in ("all", "bn1") and self.stride == 1 and bhconv.supported(y1, self.conv2.weight):
+        if _FOLD_APPLY in ("all", "bn1") and self.stride == 1 and bhconv.supported(y1, w2):
             # bn1 + ReLU inside conv2's halo prologue (and its weight gradient's LDS prologue)
-            y2, p2 = _bn_conv(self.bn1, y1, p1, self.conv2.weight, _kshift(self.bn2), 3)
-        elif self.stride == 2 and bhconv.s2_supported(y1, self.conv2.weight):
+            y2, p2 = _bn_conv(self.bn1, y1, p1, w2, _kshift(self.bn2), 3)
+        elif self.stride == 2 and bhconv.s2_supported(y1, w2):
             # the downsampling 3x3: bn1 + ReLU in the implicit-GEMM kernel's A-fragment prologue (and the
             # strided wgrad kernel's LDS prologue), bn2's statistics in its epilogue
-            y2, p2 = _bn_conv(self.bn1, y1, p1, self.conv2.weight, _kshift(self.bn2), 3, stride=2)
+            y2, p2 = _bn_conv(self.bn1, y1, p1, w2, _kshift(self.bn2), 3, stride=2)
         else:
             l1 = BNLink()
             a1 = self.bn1.forward_from_stats(y1, p1, link=l1)
-            if self.stride == 1 and bhconv.supported(a1, self.conv2.weight):
-                y2, p2 = _Conv3x3BNFn.apply(a1, self.conv2.weight, _kshift(self.bn2), l1)
+            if self.stride == 1 and bhconv.supported(a1, w2):
+                y2, p2 = _Conv3x3BNFn.apply(a1, w2, _kshift(self.bn2), l1)
             else:  # stride-2 3x3 (MIOpen): its BatchNorm computes its own statistics
                 a2 = self.bn2(self.conv2(a1))
         if y2 is not None:
             if _FOLD_APPLY in ("all", "bn2") and self._fold_bn2(y2):
                 # bn2 + ReLU inside conv3's strip-GEMM prologue (statistics of bn3 in its epilogue)
-                y3, p3 = _bn_conv(self.bn2, y2, p2, self.conv3.weight, _kshift(self.bn3), 1)
+                y3, p3 = _bn_conv(self.bn2, y2, p2, w3, _kshift(self.bn3), 1)
             else:
                 l2 = BNLink()
                 a2 = self.bn2.forward_from_stats(y2, p2, link=l2)
         if y3 is None:
-            y3, p3 = _Conv1x1BNFn.apply(a2, self.conv3.weight, _kshift(self.bn3), l2, None, False)
+            y3, p3 = _Conv1x1BNFn.apply(a2, w3, _kshift(self.bn3), l2, None, False)
         if ds is not None:
             identity = ds[1].forward_from_stats(yd, pd)
         else:
@@ -1070,13 +1109,15 @@ class ResNet(nn.Module):
         bn = self.bn1
         return (_FOLD_BN and _STEM_STATS and self.training and isinstance(self.conv1, StemConv) and self.conv1.mode == "gemm"
                 and isinstance(bn, SyncBatchNorm) and bn.track_running_stats and bn.running_mean is not None
-                and bn.running_mean.dtype == torch.float32 and x.dtype == self.conv1.weight.dtype
-                and bhconv.stem_supported(x, self.conv1.weight))
+                and bn.running_mean.dtype == torch.float32 and _kw(self.conv1.weight, x) is not None
+                and bhconv.stem_supported(x, _kw(self.conv1.weight, x)))
 
     def forward(self, x):
+        if self.fused:
+            x = _kx(x)  # amp O1 / O4: the whole network runs the 16-bit kernels (fp32 parameters)
         if self.stem_pool_fused and self._stem_stats_ok(x):
             # stem conv with the BatchNorm statistics in its epilogue, then BN + ReLU + max pool in one pass
-            y, part = _StemStatsFn.apply(x, self.conv1.weight, _kshift(self.bn1))
+            y, part = _StemStatsFn.apply(x, _kw(self.conv1.weight, x), _kshift(self.bn1))
             x = self.bn1.forward_from_stats(y, part) if self.bn1._pool_ok(y, None) else self.bn1(y)
         elif self.stem_pool_fused:
             x = self.bn1(self.conv1(x))

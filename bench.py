@@ -173,10 +173,15 @@ def main():
                                                                    stem_pool_fused=args.stem == "fused")).cuda()
     model = model.to(memory_format=torch.channels_last)
     global_batch = args.batch * world
+    # the whole step as one HIP graph (single rank; the loss scale must live on the device: FusedLAMB /
+    # FusedSGD with the device scaler, or a static scale -- O4 / O5 -- for FusedAdam, whose lr / step
+    # then stay on the device too: capturable=True)
+    graph_ok = world == 1 and not args.host_scaler and (args.optimizer != "adam" or args.opt_level in ("O4", "O5"))
+    use_graph = args.graph == "on" or (args.graph == "auto" and graph_ok)
     if args.optimizer == "lamb":
         opt = FusedLAMB(model.parameters(), lr=4e-3 * global_batch / 4096, weight_decay=0.01)
     elif args.optimizer == "adam":
-        opt = FusedAdam(model.parameters(), lr=1e-3, weight_decay=0.01)
+        opt = FusedAdam(model.parameters(), lr=1e-3, weight_decay=0.01, capturable=use_graph)
     else:
         opt = FusedSGD(model.parameters(), lr=0.1 * global_batch / 256, momentum=0.9, weight_decay=1e-4)
     model, opt = amp.initialize(model, opt, opt_level=args.opt_level, verbosity=0,
@@ -228,7 +233,6 @@ def main():
                   file=sys.stderr, flush=True)
     run = step
     capture_ms = None
-    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1 and not args.host_scaler)
     if use_graph:
         from beforeholiday_amd.utils import GraphedStep
 
