@@ -62,7 +62,8 @@ class PeerMemoryPool(object):
             pm = _pm()
             handle, failure = b"", ""
             try:
-                self.raw = pm.allocate_raw(self.static_size + self.dynamic_size)
+                # (an empty pool still exports one block: its peers' mapping handshake is collective)
+                self.raw = pm.allocate_raw(max(_ALIGN, self.static_size + self.dynamic_size))
                 handle = pm.get_raw_ipc_address(self.raw).numpy().tobytes()
             except Exception as e:  # noqa: BLE001 - reported to every rank below
                 if not consensus:

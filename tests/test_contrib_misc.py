@@ -88,8 +88,8 @@ def _spatial(rank, world):
                                                             HaloExchangerSendRecv(list(range(world)), rank)))
     sp.load_state_dict(ref.state_dict())
     torch.manual_seed(3)
-    x = torch.randn(2, 16, 8, 6)
-    H = 8 // world
+    H = 4 if world == 2 else 3
+    x = torch.randn(2, 16, H * world, 6)
     xs = x[:, :, rank * H:(rank + 1) * H].clone().requires_grad_()
     y = sp(xs)
     xr = x.clone().requires_grad_()
@@ -105,8 +105,11 @@ def _spatial(rank, world):
     torch.testing.assert_close(wg, ref.conv2.weight.grad, rtol=1e-4, atol=1e-3)
 
 
-def test_spatial_bottleneck_halo():
-    run_distributed(_spatial, 2)
+@pytest.mark.parametrize("world", [2, 3])
+def test_spatial_bottleneck_halo(world):
+    """H split over 2 or 3 ranks (the middle rank has both neighbours): output, input gradient and the
+    all-reduced conv2 weight gradient equal the unsplit block's."""
+    run_distributed(_spatial, world)
 
 
 def _halo_exchangers(rank, world):
@@ -192,3 +195,53 @@ def test_fmha_varlen_fused_attention_path(dtype):
     g1 = torch.autograd.grad(out, qkv, g)[0]
     g2 = torch.autograd.grad(ref, qf, g.float())[0]
     torch.testing.assert_close(g1.float(), g2, rtol=tol, atol=tol * 2)
+
+
+def _spatial_gpu(rank, world, c_in, planes, hw):
+    """fp16 H-split block on the MFMA kernels (two gloo ranks sharing one GPU) vs the unsplit block."""
+    from beforeholiday_amd.contrib.bottleneck import Bottleneck, SpatialBottleneck
+    from beforeholiday_amd.contrib.bottleneck.halo_exchangers import HaloExchangerAllGather
+    torch.cuda.set_device(0)
+    torch.manual_seed(2)
+    ref = Bottleneck(c_in, planes, c_in)
+    _randomize_bn(ref)
+    ex = HaloExchangerAllGather(list(range(world)), rank, torch.distributed.group.WORLD)
+    sp = SpatialBottleneck(c_in, planes, c_in, spatial_parallel_args=(world, rank, None, ex))
+    sp.load_state_dict(ref.state_dict())
+    ref = ref.cuda().half().to(memory_format=torch.channels_last)
+    sp = sp.cuda().half().to(memory_format=torch.channels_last)
+    torch.manual_seed(3)
+    # batch 4: the 1x1 strip kernel tiles 32-row pixel strips (4 x 14 x 28 rows per rank)
+    x = torch.randn(4, c_in, hw, hw, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    H = hw // world
+    sl = slice(rank * H, (rank + 1) * H)
+    xs = x[:, :, sl].contiguous(memory_format=torch.channels_last).requires_grad_()
+    calls = []
+    conv2d = torch.nn.functional.conv2d
+    torch.nn.functional.conv2d = lambda *a, **k: (calls.append(a[0].shape), conv2d(*a, **k))[1]
+    try:
+        y = sp(xs)
+    finally:
+        torch.nn.functional.conv2d = conv2d
+    assert not calls, f"library convolutions on the spatial path: {calls}"
+    xr = x.clone().requires_grad_()
+    yr = ref(xr)
+
+    def rel(a, b):
+        return float((a.float() - b.float()).norm() / b.float().norm())
+
+    assert rel(y, yr[:, :, sl]) < 2e-3, rel(y, yr[:, :, sl])
+    g = torch.randn_like(yr)
+    y.backward(g[:, :, sl].contiguous(memory_format=torch.channels_last))
+    yr.backward(g)
+    assert rel(xs.grad, xr.grad[:, :, sl]) < 1e-2, rel(xs.grad, xr.grad[:, :, sl])
+    for a, b in zip(sp.w_conv, ref.w_conv):
+        wg = a.grad.float().clone()
+        torch.distributed.all_reduce(wg)
+        assert rel(wg, b.grad) < 1e-2, rel(wg, b.grad)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(256, 64, 56), (512, 128, 28)])
+def test_spatial_bottleneck_gpu_matches_unsplit(shape):
+    run_distributed(_spatial_gpu, 2, *shape)
