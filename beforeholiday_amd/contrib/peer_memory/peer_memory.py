@@ -288,11 +288,45 @@ class PeerAllReduce:
         self._watch.after_launch()
         return t
 
+    def all_reduce_async(self, t):
+        """:meth:`all_reduce_` issued on this reducer's own HIP stream (after the work already queued on
+        the current stream): the current stream continues with independent kernels -- e.g. a weight
+        gradient -- while the exchange's flag wait runs. Returns a handle whose ``wait()`` makes the
+        current stream wait for the result. Every exchange goes through the one side stream, so the
+        calls stay in the same order on every rank."""
+        if not (self.native and t.is_cuda):
+            return _DoneHandle(self.all_reduce_(t))
+        side = getattr(self, "_side", None)
+        if side is None:
+            side = self._side = torch.cuda.Stream(device=t.device)
+        side.wait_stream(torch.cuda.current_stream(t.device))
+        with torch.cuda.stream(side):
+            self.all_reduce_(t)
+        t.record_stream(side)
+        return _StreamHandle(side, t)
+
     def check(self):
         """Raise :class:`PeerTimeoutError` if any exchange so far timed out (synchronises; call it at
         a step boundary, e.g. next to the loss read)."""
         if self.native:
             self._watch.check(sync=True)
+
+
+class _DoneHandle:
+    def __init__(self, t):
+        self.t = t
+
+    def wait(self):
+        return self.t
+
+
+class _StreamHandle:
+    def __init__(self, side, t):
+        self.side, self.t = side, t
+
+    def wait(self):
+        torch.cuda.current_stream(self.t.device).wait_stream(self.side)
+        return self.t
 
 
 def build_peer_allreduce(capacity=1 << 13, max_spins=1 << 26, group=None):

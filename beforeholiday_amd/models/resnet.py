@@ -870,7 +870,7 @@ class _BNConvFn(torch.autograd.Function):
         from ..ops import conv as bhconv
         from ..ops import conv_bn
         from ..ops import syncbn
-        from ..parallel.optimized_sync_batchnorm import _all_reduce
+        from ..parallel.optimized_sync_batchnorm import _all_reduce_async
         from ..parallel import comm_stats
 
         y, conv_w, bn_w, mean, invstd, scale, shift, count = ctx.saved_tensors
@@ -894,11 +894,6 @@ class _BNConvFn(torch.autograd.Function):
             else:
                 dA2d = torch.mm(gy2d, w2d)
             dA = dA2d.view(n, h, w, C).permute(0, 3, 1, 2)
-        g_conv = None
-        if ctx.needs_input_grad[10]:
-            g_conv = bhconv.conv_wgrad(y, gy, ctx.R, scale, shift, stride=ctx.stride)
-            if g_conv.stride() != conv_w.stride():
-                g_conv = g_conv.contiguous()
         need_w = bn_w is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
         if sums is None:
             sums, gw, gb = syncbn.backward_reduce(dA, y, None, mean, invstd, scale, shift, True, bn_w, need_w, None)
@@ -906,9 +901,17 @@ class _BNConvFn(torch.autograd.Function):
             gw = (sums[C:] * invstd).to(bn_w.dtype) if need_w else None
             # a copy: `sums` is all-reduced in place below, the bias gradient stays this rank's own
             gb = sums[:C].to(bn_w.dtype, copy=True) if need_w else None
-        if ctx.world > 1:
+        # the cross-rank exchange of the BatchNorm's backward sums runs (IPC side stream / async RCCL)
+        # while the convolution's weight gradient -- which does not depend on it -- computes
+        pending = _all_reduce_async(sums, ctx.process_group) if ctx.world > 1 else None
+        g_conv = None
+        if ctx.needs_input_grad[10]:
+            g_conv = bhconv.conv_wgrad(y, gy, ctx.R, scale, shift, stride=ctx.stride)
+            if g_conv.stride() != conv_w.stride():
+                g_conv = g_conv.contiguous()
+        if pending is not None:
             with comm_stats.timed("syncbn_bwd", sums):
-                _all_reduce(sums, ctx.process_group)
+                pending.wait()
         gx, _ = syncbn.backward_dgrad(dA, y, None, mean, invstd, bn_w, sums, count, scale, shift, True, False, None)
         return gx, None, (gw if need_w else None), (gb if need_w else None), None, None, None, None, None, None, \
             g_conv, None, None, None

@@ -54,6 +54,31 @@ def _all_reduce(t, pg):
         dist.all_reduce(t, group=pg)
 
 
+class _WorkHandle:
+    def __init__(self, work, t):
+        self.work, self.t = work, t
+
+    def wait(self):
+        self.work.wait()
+        return self.t
+
+
+def _all_reduce_async(t, pg):
+    """Start the SUM all-reduce of ``t`` without blocking the current stream: the IPC reducer's side
+    stream, or an async RCCL / gloo collective. ``.wait()`` on the result before using ``t``."""
+    if hasattr(pg, "all_reduce_async"):
+        return pg.all_reduce_async(t)
+    if hasattr(pg, "all_reduce_"):
+        pg.all_reduce_(t)
+        return _WorkHandle(_NoWork(), t)
+    return _WorkHandle(dist.all_reduce(t, group=pg, async_op=True), t)
+
+
+class _NoWork:
+    def wait(self):
+        return True
+
+
 class SyncBatchnormFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, input, z, weight, bias, running_mean, running_var, eps, momentum, process_group,
