@@ -21,7 +21,6 @@
 #include "bh/igemm_api.h"
 
 #include <algorithm>
-#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
@@ -55,10 +54,8 @@ constexpr int kRS = kCK * 2 + 16;  // LDS bytes per staged weight row
 constexpr int kMaxProC = 512;
 constexpr int kOutOfRange = 0x7ff00000;  // a byte offset past every tensor the kernel reads
 
-// OCC: resident workgroups per CU the register budget is sized for (2: 256 VGPRs; 1: 512 -- the
-// 64 x 128 wave tile, whose weight fragments each feed two MFMAs)
-template <typename T, int NC, int MW, bool PRO, bool STATS, int OCC = 2>
-__global__ __launch_bounds__(kThreads, OCC) void k_igemm(IgemmArgs a, int tiles_m) {
+template <typename T, int NC, int MW, bool PRO, bool STATS>
+__global__ __launch_bounds__(kThreads, 2) void k_igemm(IgemmArgs a, int tiles_m) {
   constexpr int NT = NC / 32, MT = MW / 32, NB = NC / 32;  // NB: 16-byte weight pieces per thread per k-step
   using V8 = typename Mfi<T>::v8;
   __shared__ __attribute__((aligned(16))) char smem[2 * NC * kRS + (PRO ? 8 * kMaxProC : 0)];
@@ -258,12 +255,8 @@ Plan make_plan(const IgemmArgs& a) {
   // tiles without the prologue: 64 pixel rows per wave (each weight fragment read from LDS feeds two
   // MFMAs) while that still leaves >= 2 workgroups per CU
   p.MW = (p.NC == 64 && !a.pro_scale && ((P + 255) / 256) * slices * a.nphase >= 512) ? 64 : 32;
-  // BH_IGEMM_WIDE=1 (A/B): 64 x 128 wave tiles at one workgroup per CU on the large grids
-  static const bool wide = [] {
-    const char* e = getenv("BH_IGEMM_WIDE");
-    return e && atoi(e) == 1;
-  }();
-  if (wide && p.NC == 128 && !a.pro_scale && ((P + 255) / 256) * slices * a.nphase >= 256) p.MW = 64;
+  // (64 x 128 wave tiles at one workgroup per CU -- 512 registers, each weight fragment feeding two
+  // MFMAs -- measured 0.69-0.99x of this at the three ResNet-50 shapes: profiles/conv3x3_s2_vs_miopen.jsonl)
   p.tiles_m = (int)((P + 4 * p.MW - 1) / (4 * p.MW));
   return p;
 }
@@ -301,10 +294,7 @@ void igemm_run(int dt, const IgemmArgs& a, hipStream_t st) {
     using T = typename decltype(tt)::type;
     constexpr int NC = decltype(nc)::value, MW = decltype(mw)::value;
     auto L = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(kThreads), 0, st, a, pl.tiles_m); };
-    if constexpr (NC == 128 && MW == 64) {  // one workgroup per CU: 512 registers (no prologue: spills)
-      if (stats) L(k_igemm<T, NC, MW, false, true, 1>);
-      else L(k_igemm<T, NC, MW, false, false, 1>);
-    } else if constexpr (MW == 32) {
+    if constexpr (MW == 32) {
       if (pro && stats) L(k_igemm<T, NC, MW, true, true>);
       else if (pro) L(k_igemm<T, NC, MW, true, false>);
       else if (stats) L(k_igemm<T, NC, MW, false, true>);
@@ -315,7 +305,9 @@ void igemm_run(int dt, const IgemmArgs& a, hipStream_t st) {
     }
   };
   auto by_mw = [&](auto tt, auto nc) {
-    if (pl.MW == 64) return go(tt, nc, std::integral_constant<int, 64>{});
+    if constexpr (decltype(nc)::value == 64) {
+      if (pl.MW == 64) return go(tt, nc, std::integral_constant<int, 64>{});
+    }
     go(tt, nc, std::integral_constant<int, 32>{});
   };
   auto by_nc = [&](auto tt) {
