@@ -56,9 +56,12 @@ def _gpt_tp(rank, world, sequence_parallel):
     ps.destroy_model_parallel()
 
 
+@pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("sequence_parallel", [False, True])
-def test_gpt_tensor_parallel_matches_single_rank(sequence_parallel):
-    run_distributed(_gpt_tp, 2, sequence_parallel)
+def test_gpt_tensor_parallel_matches_single_rank(sequence_parallel, world):
+    """TP = 2 and TP = 4 (BASELINE configs[4]'s degree: one head and a quarter of the vocabulary per
+    rank), with and without sequence parallelism."""
+    run_distributed(_gpt_tp, world, sequence_parallel)
 
 
 def _gpt_pp(rank, world):
