@@ -55,6 +55,70 @@ def _kw(weight, x):
     return None
 
 
+# ------------------------------------------------------------------------------------------------
+# Weight gradients on a second HIP stream. In backward, a convolution's weight gradient depends only on
+# its saved input and dY, and nothing downstream reads it before the optimizer -- while the data gradient
+# feeds the next BatchNorm-backward passes. The MFMA wgrad kernels are compute / LDS bound (one
+# 141 KiB workgroup per CU) and the BatchNorm passes HBM bound (a few KiB of LDS), so running the wgrads
+# on a side stream lets the two kinds co-reside on the CUs; in the captured HIP graph of the training
+# step the side stream becomes a parallel branch. The side stream joins the compute stream once, at the
+# end of the backward pass (an autograd-engine callback), before any gradient consumer runs.
+# Opt-in (BH_WGRAD_STREAM=1): same-box A/B at batch 256 measured no reliable gain -- eager 10204 vs
+# 10082, graphed 9936 vs 10171 img/s (profiles/resnet50_wgrad_side_stream_ab.txt)
+_WGRAD_STREAM = os.environ.get("BH_WGRAD_STREAM", "0") == "1"
+_SIDE = {}
+_JOIN_QUEUED = set()
+
+
+def _side_ok(weight, x):
+    """The weight gradient may run on the side stream: a CUDA leaf parameter whose .grad is empty
+    (AccumulateGrad then just takes the tensor: no kernel reads it before the join), and no gradient
+    hooks of a multi-rank DDP (which copy it into a bucket on the compute stream right away)."""
+    if not (_WGRAD_STREAM and x.is_cuda and weight is not None and weight.is_leaf and weight.grad is None):
+        return False
+    import torch.distributed as dist
+
+    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+
+
+def _join(dev):
+    key = dev.index
+    _JOIN_QUEUED.discard(key)
+    torch.cuda.current_stream(dev).wait_stream(_SIDE[key])
+
+
+def _on_side(fn, *inputs):
+    """``fn()`` (a weight gradient of ``inputs``) issued on the side stream after the work queued so
+    far on the compute stream; the compute stream waits for it at the end of this backward pass."""
+    dev = inputs[0].device
+    main = torch.cuda.current_stream(dev)
+    side = _SIDE.get(dev.index)
+    if side is None:
+        side = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        g = fn()
+    for t in inputs:
+        if torch.is_tensor(t):
+            t.record_stream(side)  # (their blocks are not reused by the compute stream meanwhile)
+    g.record_stream(main)
+    if dev.index not in _JOIN_QUEUED:
+        _JOIN_QUEUED.add(dev.index)
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: _join(dev))
+    return g
+
+
+def _wgrad_maybe_side(wparam, fn, *inputs):
+    """(gradient, ran_on_side) -- see :func:`_side_ok`."""
+    if _side_ok(wparam, inputs[0]):
+        return _on_side(fn, *inputs), True
+    return fn(), False
+
+
+def _like(g, weight):
+    return g if g.stride() == weight.stride() else g.contiguous()
+
+
 # per-shape choice of the 1x1 / stride-1 convolution paths: {(N, Cin, H, W, Cout, dtype, dir): "gemm" | "miopen"}
 _CONV1X1_CHOICE = {}
 
@@ -495,6 +559,7 @@ class _StemStatsFn(torch.autograd.Function):
         y, part = submodule("conv_cuda").stem_forward_stats(x, weight, kshift)
         ctx.save_for_backward(x, weight)
         ctx.mode = "gemm"
+        ctx.wparam = weight
         ctx.mark_non_differentiable(part)
         ctx.set_materialize_grads(False)
         return y, part
@@ -608,7 +673,7 @@ class _Conv1x1BNFn(torch.autograd.Function):
     def forward(ctx, x, weight, kshift, link_in, box, s2):
         y, part = _c1x1_forward_stats(x, weight, kshift, s2)
         ctx.save_for_backward(x, weight)
-        ctx.link_in, ctx.box, ctx.s2 = link_in, box, s2
+        ctx.link_in, ctx.box, ctx.s2, ctx.wparam = link_in, box, s2, weight
         ctx.mark_non_differentiable(part)
         ctx.set_materialize_grads(False)
         return y, part
@@ -631,6 +696,19 @@ class _Conv1x1BNFn(torch.autograd.Function):
                                     and acc.shape == x.shape):
             acc = acc.contiguous(memory_format=torch.channels_last).to(gy.dtype)
         gx = gw = None
+
+        def wfn():
+            if ctx.s2:
+                return _like(bhconv.conv_wgrad_s2(x, gy) if bhconv.wgrad_supported(x, gy, 1, 2) else
+                             conv_bwd(gy, x, weight, None, *args, [False, True, False])[1], weight)
+            # the MFMA wgrad kernel wins every ResNet-50 1x1 shape (profiles/conv_wgrad_vs_miopen.jsonl):
+            # no per-shape timing (it would JIT-compile MIOpen's solver on the first step)
+            return _wgrad(x, gy, weight, 1, "gemm", lambda: conv_bwd(gy, x, weight, None, *args,
+                                                                     [False, True, False])[1])
+
+        side = ctx.needs_input_grad[1] and _side_ok(ctx.wparam, x)
+        if side:
+            gw = _on_side(wfn, x, gy)
         if ctx.needs_input_grad[0]:
             if ctx.s2:
                 gx = conv_bwd(gy, x, weight, None, *args, [True, False, False])[0]
@@ -658,17 +736,8 @@ class _Conv1x1BNFn(torch.autograd.Function):
             acc = None
         if box is not None:
             box["conv_done"] = True
-        if ctx.needs_input_grad[1]:
-            if ctx.s2:
-                gw = bhconv.conv_wgrad_s2(x, gy) if bhconv.wgrad_supported(x, gy, 1, 2) else \
-                    conv_bwd(gy, x, weight, None, *args, [False, True, False])[1]
-                if gw.stride() != weight.stride():
-                    gw = gw.contiguous()
-            else:
-                # the MFMA wgrad kernel wins every ResNet-50 1x1 shape (profiles/conv_wgrad_vs_miopen.jsonl):
-                # no per-shape timing (it would JIT-compile MIOpen's solver on the first step)
-                gw = _wgrad(x, gy, weight, 1, "gemm", lambda: conv_bwd(gy, x, weight, None, *args,
-                                                                       [False, True, False])[1])
+        if ctx.needs_input_grad[1] and not side:
+            gw = wfn()
         return gx, gw, None, None, None, None
 
 
@@ -714,7 +783,7 @@ class _Conv1DsFn(torch.autograd.Function):
         y1, p1 = _c1x1_forward_stats(x, w1, k1, False)
         yd, pd = _c1x1_forward_stats(x, wd, kd, s2)
         ctx.save_for_backward(x, w1, wd)
-        ctx.s2 = s2
+        ctx.s2, ctx.wparams = s2, (w1, wd)
         ctx.mark_non_differentiable(p1, pd)
         ctx.set_materialize_grads(False)
         return y1, p1, yd, pd
@@ -733,6 +802,25 @@ class _Conv1DsFn(torch.autograd.Function):
         gd = gyd.permute(0, 2, 3, 1).reshape(-1, kd)
         w1_2d, wd_2d = w1.view(k1, c), wd.view(kd, c)
         gx = gw1 = gwd = None
+        conv_bwd = torch.ops.aten.convolution_backward
+        a1 = ([1, 1], [0, 0], [1, 1], False, [0, 0], 1)
+
+        def w1fn():
+            return _wgrad(x, gy1, w1, 1, "gemm", lambda: conv_bwd(gy1, x, w1, None, *a1, [False, True, False])[1])
+
+        def wdfn():
+            if ctx.s2:
+                a2 = ([2, 2], [0, 0], [1, 1], False, [0, 0], 1)
+                return _like(bhconv.conv_wgrad_s2(x, gyd) if bhconv.wgrad_supported(x, gyd, 1, 2) else
+                             conv_bwd(gyd, x, wd, None, *a2, [False, True, False])[1], wd)
+            return _wgrad(x, gyd, wd, 1, "gemm", lambda: conv_bwd(gyd, x, wd, None, *a1, [False, True, False])[1])
+
+        side1 = ctx.needs_input_grad[1] and _side_ok(ctx.wparams[0], x)
+        sided = ctx.needs_input_grad[2] and _side_ok(ctx.wparams[1], x)
+        if side1:
+            gw1 = _on_side(w1fn, x, gy1)
+        if sided:
+            gwd = _on_side(wdfn, x, gyd)
         if ctx.needs_input_grad[0]:
             if conv_bn.preferred(k1, c, g1.size(0)) and conv_bn.supported(g1, w1_2d, b_trans=True):
                 gx2d, _ = conv_bn.c1x1(g1, w1_2d, b_trans=True)
@@ -752,20 +840,10 @@ class _Conv1DsFn(torch.autograd.Function):
             else:
                 torch.addmm(gx2d, gd, wd_2d, out=gx2d)
             gx = gx2d.view(n, h, w, c).permute(0, 3, 1, 2)
-        conv_bwd = torch.ops.aten.convolution_backward
-        if ctx.needs_input_grad[1]:
-            args = ([1, 1], [0, 0], [1, 1], False, [0, 0], 1)
-            gw1 = _wgrad(x, gy1, w1, 1, "gemm", lambda: conv_bwd(gy1, x, w1, None, *args, [False, True, False])[1])
-        if ctx.needs_input_grad[2]:
-            if ctx.s2:
-                args = ([2, 2], [0, 0], [1, 1], False, [0, 0], 1)
-                gwd = bhconv.conv_wgrad_s2(x, gyd) if bhconv.wgrad_supported(x, gyd, 1, 2) else \
-                    conv_bwd(gyd, x, wd, None, *args, [False, True, False])[1]
-                if gwd.stride() != wd.stride():
-                    gwd = gwd.contiguous()
-            else:
-                args = ([1, 1], [0, 0], [1, 1], False, [0, 0], 1)
-                gwd = _wgrad(x, gyd, wd, 1, "gemm", lambda: conv_bwd(gyd, x, wd, None, *args, [False, True, False])[1])
+        if ctx.needs_input_grad[1] and not side1:
+            gw1 = w1fn()
+        if ctx.needs_input_grad[2] and not sided:
+            gwd = wdfn()
         return gx, gw1, gwd, None, None, None
 
 
@@ -780,7 +858,7 @@ class _Conv3x3BNFn(torch.autograd.Function):
 
         y, part = submodule("conv_cuda").conv3x3_bn_forward(x, weight, None, None, True, kshift)
         ctx.save_for_backward(x, weight)
-        ctx.link_in = link_in
+        ctx.link_in, ctx.wparam = link_in, weight
         ctx.mark_non_differentiable(part)
         ctx.set_materialize_grads(False)
         return y, part
@@ -797,6 +875,11 @@ class _Conv3x3BNFn(torch.autograd.Function):
         conv_bwd = torch.ops.aten.convolution_backward
         args = ([1, 1], [1, 1], [1, 1], False, [0, 0], 1)
         gx = gw = None
+        wfn = lambda: _wgrad(x, gy, weight, 3, "gemm",  # noqa: E731
+                             lambda: conv_bwd(gy, x, weight, None, *args, [False, True, False])[1])
+        side = ctx.needs_input_grad[1] and _side_ok(ctx.wparam, x)
+        if side:
+            gw = _on_side(wfn, x, gy)
         if ctx.needs_input_grad[0]:
             link = ctx.link_in
             # the 3x3 data gradient's BatchNorm-sums epilogue reads the previous BatchNorm's input 2 bytes
@@ -808,8 +891,8 @@ class _Conv3x3BNFn(torch.autograd.Function):
                 link.sums = conv_bn.sum_parts(part)
             else:
                 gx = bhconv.conv3x3_dgrad(gy, weight)
-        if ctx.needs_input_grad[1]:
-            gw = _wgrad(x, gy, weight, 3, "gemm", lambda: conv_bwd(gy, x, weight, None, *args, [False, True, False])[1])
+        if ctx.needs_input_grad[1] and not side:
+            gw = wfn()
         return gx, gw, None, None
 
 
@@ -861,6 +944,7 @@ class _BNConvFn(torch.autograd.Function):
             out = o2d.view(n, h, w, k).permute(0, 3, 1, 2)
         ctx.save_for_backward(y, conv_w, bn_w, mean, invstd, scale, shift, count_t)
         ctx.process_group, ctx.world, ctx.R, ctx.stride = process_group, world, R, stride
+        ctx.wparam = conv_w
         ctx.mark_non_differentiable(part_out)
         ctx.set_materialize_grads(False)
         return out, part_out
@@ -877,6 +961,9 @@ class _BNConvFn(torch.autograd.Function):
         gy = gy.contiguous(memory_format=torch.channels_last)
         n, C, h, w = y.shape
         sums = None
+        wfn = lambda: _like(bhconv.conv_wgrad(y, gy, ctx.R, scale, shift, stride=ctx.stride), conv_w)  # noqa: E731
+        side = ctx.needs_input_grad[10] and _side_ok(ctx.wparam, y)
+        g_conv = _on_side(wfn, y, gy, scale, shift) if side else None
         if ctx.R == 3 and ctx.stride == 2:
             dA = bhconv.conv3x3_s2_dgrad(gy, conv_w, (h, w))
         elif ctx.R == 3:
@@ -904,11 +991,8 @@ class _BNConvFn(torch.autograd.Function):
         # the cross-rank exchange of the BatchNorm's backward sums runs (IPC side stream / async RCCL)
         # while the convolution's weight gradient -- which does not depend on it -- computes
         pending = _all_reduce_async(sums, ctx.process_group) if ctx.world > 1 else None
-        g_conv = None
-        if ctx.needs_input_grad[10]:
-            g_conv = bhconv.conv_wgrad(y, gy, ctx.R, scale, shift, stride=ctx.stride)
-            if g_conv.stride() != conv_w.stride():
-                g_conv = g_conv.contiguous()
+        if ctx.needs_input_grad[10] and not side:
+            g_conv = wfn()
         if pending is not None:
             with comm_stats.timed("syncbn_bwd", sums):
                 pending.wait()
