@@ -297,7 +297,8 @@ std::vector<at::Tensor> backward_reduce(at::Tensor dy_in, at::Tensor x_in, c10::
   if (relu && z.has_value() && z->defined()) zt = like(*z, L.x);
   if (relu) TORCH_CHECK(scale.has_value() && shift.has_value(), "relu recompute needs scale/shift");
   const int C = L.s.C;
-  const int splits = bh::bn_num_splits_reduce(L.s);
+  const bool masked = relu && mask.has_value() && mask->defined();
+  const int splits = bh::bn_num_splits_reduce(L.s, masked);
   auto part = at::empty({2 * (int64_t)splits * C}, fopt(L.x));
   auto sums = at::empty({2 * (int64_t)C}, fopt(L.x));
   at::Tensor gw, gb;

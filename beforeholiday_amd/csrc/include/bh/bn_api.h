@@ -29,7 +29,7 @@ struct BNFinal {
 };
 
 int bn_num_splits(const BNShape& s);         // statistics partials
-int bn_num_splits_reduce(const BNShape& s);  // backward-reduction partials
+int bn_num_splits_reduce(const BNShape& s, bool masked = false);  // backward-reduction partials
 // partial Welford stats: pmean/pm2 [splits][C]; pn [splits] (channels_last) or [splits][C] (NCHW)
 void bn_stats(const BNShape& s, int dt_x, const void* x, int splits, float* pmean, float* pm2, float* pn,
               hipStream_t st);

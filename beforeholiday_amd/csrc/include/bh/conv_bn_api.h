@@ -52,6 +52,9 @@ struct C1x1Args {
   const float* a_shift = nullptr;
   bool relu = false;
   bool r_mul = false;
+  // A-operand loads: 0 nontemporal (streaming hint), 1 ordinary cached loads (set by c1x1_run from
+  // BH_C1X1_ALOAD when left at -1)
+  int a_load = -1;
 };
 
 // whether the kernel covers the shape (K % 64, N % 64, M % 32, LDS budget, 16-byte alignment)

@@ -900,6 +900,10 @@ int64_t knob_ew_rows() { static const int64_t v = env_knob("BH_BN_EW_ROWS", 8); 
 // stats best at ~1024 workgroups x 32 rows/lane, the two-input backward reduction at ~256)
 int64_t knob_stat_blocks() { static const int64_t v = env_knob("BH_BN_STAT_BLOCKS", 1024); return v; }
 int64_t knob_red_blocks() { static const int64_t v = env_knob("BH_BN_RED_BLOCKS", 256); return v; }
+// with the stored ReLU bit mask (three streams: dy, x, mask) the reduction wants twice the workgroups
+// (benchmarks/sweep_bn_reduce.py on MI355X, batch-256 ResNet-50 shapes: 56x56x256 201 -> 150 us,
+// 28x28x512 105 -> 80 us at 512; the two-stream recomputed-ReLU shapes lose 1-2 us there)
+int64_t knob_red_blocks_mask() { static const int64_t v = env_knob("BH_BN_RED_BLOCKS_MASK", 512); return v; }
 int64_t knob_red_rows() { static const int64_t v = env_knob("BH_BN_RED_ROWS", 32); return v; }
 // channel vectors (x8 channels) per workgroup of the two reductions (stats, backward reduce): fewer
 // channels per workgroup -> more row lanes merged in LDS, so a layer reaches the workgroup target
@@ -937,7 +941,9 @@ static int splits_for(const BNShape& s, int64_t target_blocks, int geom) {
 }
 
 int bn_num_splits(const BNShape& s) { return splits_for(s, knob_stat_blocks(), 2); }
-int bn_num_splits_reduce(const BNShape& s) { return splits_for(s, knob_red_blocks(), 1); }
+int bn_num_splits_reduce(const BNShape& s, bool masked) {
+  return splits_for(s, masked ? knob_red_blocks_mask() : knob_red_blocks(), 1);
+}
 
 void bn_stats(const BNShape& s, int dt_x, const void* x, int splits, float* pmean, float* pm2, float* pn,
               hipStream_t st) {

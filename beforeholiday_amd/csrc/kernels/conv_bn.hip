@@ -24,6 +24,7 @@
 #include "bh/device.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <type_traits>
@@ -161,8 +162,13 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
   auto load = [&](int i, i4v(&a)[KS]) {
     const int q = i / nch, c = i - q * nch;
     const T* src = A + arow(first + q * stride) * K + c * KC + 8 * h;
+    if (p.a_load == 1) {
 #pragma unroll
-    for (int s = 0; s < KS; ++s) a[s] = __builtin_nontemporal_load(reinterpret_cast<const i4v*>(src + 16 * s));
+      for (int s = 0; s < KS; ++s) a[s] = *reinterpret_cast<const i4v*>(src + 16 * s);
+    } else {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) a[s] = __builtin_nontemporal_load(reinterpret_cast<const i4v*>(src + 16 * s));
+    }
   };
   // Output staging (all but the scatter variant): the lane-per-column MFMA result leaves as 128-byte
   // row segments (whole cache lines: 64-byte half lines measured ~20% slower on the HBM-bound shapes)
@@ -510,8 +516,14 @@ int c1x1_parts(const C1x1Args& a) {
   return make_plan(a, &pl) ? pl.g.G : 0;
 }
 
-void c1x1_run(int dt, const C1x1Args& a, hipStream_t st) {
-  if (!c1x1_supported(a)) throw std::runtime_error("c1x1: unsupported shape / arguments");
+void c1x1_run(int dt, const C1x1Args& a_in, hipStream_t st) {
+  if (!c1x1_supported(a_in)) throw std::runtime_error("c1x1: unsupported shape / arguments");
+  static const int a_load_env = [] {
+    const char* e = getenv("BH_C1X1_ALOAD");
+    return e ? atoi(e) : 0;
+  }();
+  C1x1Args a = a_in;
+  if (a.a_load < 0) a.a_load = a_load_env;
   Plan pl;
   make_plan(a, &pl);
   const dim3 grid(pl.g.nslices * pl.g.G), block(kThreads);
