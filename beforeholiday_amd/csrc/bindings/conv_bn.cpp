@@ -158,28 +158,32 @@ at::Tensor sum_parts(const at::Tensor& part, double count) {
   return out;
 }
 
-// C = A . B^T on the tiled MFMA GEMM (kernels/gemm.hip) with a BatchNorm statistics epilogue (epi 1:
-// forward statistics centred on kshift; epi 2: the previous BatchNorm's backward sums with by / bscale
-// / bshift / bmean) -- the compute-bound 1x1 layers. Returns (C [M, N], partials [2, slabs, N]).
+// C = A . B^T (+ resid) on the tiled MFMA GEMM (kernels/gemm.hip) with a BatchNorm epilogue (epi 0: none;
+// 1: forward statistics centred on kshift; 2: the previous BatchNorm's backward sums with by / bscale /
+// bshift / bmean) -- the compute-bound 1x1 layers. Returns (C [M, N], partials [2, slabs, N] or empty).
 std::vector<at::Tensor> gemm_bn(const at::Tensor& a, const at::Tensor& b, int64_t epi,
                                 const c10::optional<at::Tensor>& kshift, const c10::optional<at::Tensor>& by,
                                 const c10::optional<at::Tensor>& bscale, const c10::optional<at::Tensor>& bshift,
-                                const c10::optional<at::Tensor>& bmean, bool brelu) {
+                                const c10::optional<at::Tensor>& bmean, bool brelu,
+                                const c10::optional<at::Tensor>& resid) {
   TORCH_CHECK(a.is_cuda() && b.is_cuda() && a.device() == b.device() && a.dim() == 2 && b.dim() == 2 &&
                   a.is_contiguous() && b.is_contiguous() && a.scalar_type() == b.scalar_type() &&
                   (a.scalar_type() == at::kHalf || a.scalar_type() == at::kBFloat16) && a.size(1) == b.size(1),
               "conv_bn.gemm_bn: a [M, K] and b [N, K] contiguous fp16/bf16 GPU tensors");
-  TORCH_CHECK(epi == 1 || epi == 2, "conv_bn.gemm_bn: epi must be 1 (statistics) or 2 (backward sums)");
+  TORCH_CHECK(epi >= 0 && epi <= 2, "conv_bn.gemm_bn: epi must be 0 (none), 1 (statistics) or 2 (backward sums)");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
   auto c = at::empty({M, N}, a.options());
   TORCH_CHECK(bh::gemm_supported(M, N, K, K, K, N, a.data_ptr(), b.data_ptr(), c.data_ptr()) && N % 64 == 0,
               "conv_bn.gemm_bn: unsupported shape");
-  const int64_t slabs = bh::gemm_bgrad_slabs(M);
-  auto part = at::empty({2, slabs, N}, a.options().dtype(at::kFloat));
   bh::GemmEpilogue e;
-  e.bn_stats = (int)epi;
-  e.stat_part = part.data_ptr<float>();
-  e.kshift = fptr(kshift, N, "kshift");
+  at::Tensor part;
+  if (epi) {
+    const int64_t slabs = bh::gemm_bgrad_slabs(M);
+    part = at::empty({2, slabs, N}, a.options().dtype(at::kFloat));
+    e.bn_stats = (int)epi;
+    e.stat_part = part.data_ptr<float>();
+    e.kshift = fptr(kshift, N, "kshift");
+  }
   if (epi == 2) {
     TORCH_CHECK(by.has_value() && by->defined() && by->is_cuda() && by->scalar_type() == a.scalar_type() &&
                     by->is_contiguous() && by->numel() == M * N,
@@ -190,6 +194,12 @@ std::vector<at::Tensor> gemm_bn(const at::Tensor& a, const at::Tensor& b, int64_
     e.bn_mean = fptr(bmean, N, "bmean");
     TORCH_CHECK(e.bn_scale && e.bn_shift && e.bn_mean, "conv_bn.gemm_bn: bscale / bshift / bmean required");
     e.bn_relu = brelu;
+  }
+  if (resid.has_value() && resid->defined()) {
+    TORCH_CHECK(resid->is_cuda() && resid->scalar_type() == a.scalar_type() && resid->is_contiguous() &&
+                    resid->numel() == M * N && K % 64 == 0,
+                "conv_bn.gemm_bn: resid must be a contiguous [M, N] tensor of a's dtype (and K % 64 == 0)");
+    e.resid = resid->data_ptr();
   }
   bh::gemm_nt(dtype_code(a.scalar_type()), a.data_ptr(), K, b.data_ptr(), K, c.data_ptr(), N, M, N, K, e,
               stream_for(a));
@@ -216,7 +226,7 @@ void register_conv_bn(pybind11::module_& root) {
   m.def("sum_parts", &sum_parts, py::arg("part"), py::arg("count") = -1.0);
   m.def("gemm_bn", &gemm_bn, py::arg("a"), py::arg("b"), py::arg("epi"), py::arg("kshift") = py::none(),
         py::arg("by") = py::none(), py::arg("bscale") = py::none(), py::arg("bshift") = py::none(),
-        py::arg("bmean") = py::none(), py::arg("brelu") = true);
+        py::arg("bmean") = py::none(), py::arg("brelu") = true, py::arg("resid") = py::none());
 }
 
 }  // namespace bhb

@@ -120,12 +120,13 @@ bool mfma_ok(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c) {
 // a warmup step) and the faster is kept. The MFMA kernel wins where the fused epilogue saves a pass
 // that matters (K <= 1024: the GPT-2-medium fc1 forward, small MLPs); hipBLASLt's main loop wins the
 // large-K shapes (fc2 forward / fc1 backward at K = 4096: 0.12 vs 0.08 ms,
-// profiles/gemm_mfma_big_tile_vs_hipblaslt.jsonl). BH_DENSE_TUNE=0 uses the static K <= 1024 rule;
-// during HIP-graph capture the cached choice (or the static rule) is used, never a timing run.
+// profiles/gemm_mfma_big_tile_vs_hipblaslt.jsonl). The timing is opt-in (BH_DENSE_TUNE=1): a per-process
+// timing pick can differ between ranks (another kernel, other rounding), so by default the static
+// K <= 1024 rule decides; during HIP-graph capture the cached choice (or the rule) is used.
 bool tune_enabled() {
   static const bool on = [] {
     const char* v = std::getenv("BH_DENSE_TUNE");
-    return !(v && v[0] == '0');
+    return v && v[0] == '1';
   }();
   return on;
 }
@@ -418,6 +419,36 @@ void register_dense(pybind11::module_& root) {
     check_cuda(dy, "dy");
     return linear_dact(dy, wt, aux.has_value() ? *aux : at::Tensor(), act, want_bgrad);
   }, py::arg("dy"), py::arg("wt"), py::arg("aux"), py::arg("act"), py::arg("want_bgrad"));
+  gm.def("mm_nt", [](at::Tensor a, at::Tensor b, c10::optional<at::Tensor> bias) {
+    // C = a . b^T (+ bias) on the MFMA GEMM, unconditionally (no measured dispatch, no library
+    // fallback: a fixed kernel per shape, so every rank computes bitwise the same); unsupported
+    // shapes / layouts raise
+    check_cuda(a, "a");
+    check_cuda(b, "b");
+    TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(1) && a.scalar_type() == b.scalar_type() &&
+                    (a.scalar_type() == at::kHalf || a.scalar_type() == at::kBFloat16),
+                "gemm.mm_nt: a [M, K] and b [N, K] fp16 / bf16");
+    auto c = at::empty({a.size(0), b.size(0)}, a.options());
+    const bool bias_ok = !bias.has_value() || !bias->defined() ||
+                         (bias->is_contiguous() && al16(*bias) && bias->scalar_type() == a.scalar_type() &&
+                          bias->numel() == b.size(0));
+    TORCH_CHECK(bias_ok && a.stride(1) == 1 && b.stride(1) == 1 &&
+                    bh::gemm_supported(a.size(0), b.size(0), a.size(1), a.stride(0), b.stride(0), c.stride(0),
+                                       a.data_ptr(), b.data_ptr(), c.data_ptr()),
+                "gemm.mm_nt: unsupported shape / layout (K % 8, N % 8, 16-byte aligned rows)");
+    bh::GemmEpilogue e;
+    e.bias = (bias.has_value() && bias->defined()) ? bias->data_ptr() : nullptr;
+    bh::gemm_nt(dtype_code(a.scalar_type()), a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(),
+                c.stride(0), a.size(0), b.size(0), a.size(1), e, stream_for(a));
+    return c;
+  }, py::arg("a"), py::arg("b"), py::arg("bias") = py::none());
+  gm.def("transpose", [](at::Tensor x) {
+    check_cuda(x, "x");
+    TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.element_size() == 2, "gemm.transpose: contiguous 2-D 16-bit");
+    auto y = at::empty({x.size(1), x.size(0)}, x.options());
+    bh::transpose16(x.data_ptr(), x.size(0), x.size(1), y.data_ptr(), stream_for(x));
+    return y;
+  }, py::arg("x"), "x.t().contiguous() for a 2-D 16-bit tensor (64 x 64 LDS tiles, 16-byte accesses)");
   gm.def("mfma_enabled", &mfma_enabled);
   gm.def("set_tile_mode", &bh::gemm_set_tile_mode, "0 auto, 1 128x128, 2 256x256, 3 256x128, 4 ping-pong 256x256");
   gm.def("tile_mode", &bh::gemm_tile_mode);

@@ -24,8 +24,11 @@ struct GemmEpilogue {
   const void* aux_in = nullptr;   // [M, ld_aux] backward
   int64_t ld_aux = 0;
   float* bgrad_part = nullptr;    // [gemm_bgrad_slabs(M), N]
+  // [M, ldc] added to the accumulator before the epilogue (C = A.B^T + resid; forward epilogues of the
+  // ping-pong kernel only: a call with resid needs K % 64 == 0)
+  const void* resid = nullptr;
   // BatchNorm statistics of the output, per 64-row slab into stat_part [2][slabs][N] (no activation /
-  // bias with these; the 128x128 / 256x128 / 256x256 kernels, never the ping-pong one):
+  // bias with these):
   //   1: sums of (c - kshift[n]) and its square, c the stored value (the next BatchNorm's statistics);
   //   2: with y = bn_y[m, n] (ld = ldc): dz = c * (y * bn_scale + bn_shift > 0 | !bn_relu), sums of dz
   //      and dz * (y - bn_mean[n]) (the previous BatchNorm's backward reduction)
@@ -50,6 +53,8 @@ void gemm_nt(int dt, const void* A, int64_t lda, const void* B, int64_t ldb, voi
 // 3 256x128 three-stage, 4 ping-pong forced (K % 64 == 0 only); default from BH_GEMM_TILE
 int gemm_tile_mode();
 void gemm_set_tile_mode(int mode);
+// out [C, R] = in [R, C]^T, 16-bit elements (R, C multiples of 8, 16-byte aligned)
+void transpose16(const void* in, int64_t R, int64_t C, void* out, hipStream_t st);
 // out[N] (dtype dt) = sum_r part[r][N]
 void gemm_colsum_finalize(int dt, const float* part, int64_t slabs, int64_t N, void* out, hipStream_t st);
 

@@ -515,6 +515,148 @@ __global__ __launch_bounds__(kBlock) void k_fwd_nhwc(const T* __restrict__ x, co
   }
 }
 
+// flat variant of k_fwd_nhwc: the NHWC tensor as one run of 16-byte chunks (8 channels each), chunk i
+// -> channels (i mod C/8) * 8; lanes take consecutive chunks (every wave instruction one contiguous
+// 1-KiB run), kFlatU chunks per lane in flight, grid-stride over tiles of 256 * kFlatU chunks; the
+// per-channel scale / shift sit in LDS (loaded once per workgroup). The mask byte of chunk i is
+// mbits[i] ([row][C/8] is the chunk order).
+constexpr int kFlatU = 4;
+template <typename T> using Vec8 = T __attribute__((ext_vector_type(8)));
+BH_DEVICE int64_t chunk_chan(int64_t i, int C8, bool pow2) { return pow2 ? (i & (C8 - 1)) : (i % C8); }
+
+template <typename T, typename Tz, typename Ty>
+__global__ __launch_bounds__(kBlock) void k_fwd_flat(const T* __restrict__ x, const Tz* __restrict__ z,
+                                                     Ty* __restrict__ y, const float* __restrict__ scale,
+                                                     const float* __restrict__ shift, int64_t chunks, int C, bool relu,
+                                                     int64_t* counter, uint8_t* __restrict__ mbits) {
+  extern __shared__ float prm[];  // [2][C]: scale, shift
+  for (int c = threadIdx.x; c < C; c += kBlock) {
+    prm[c] = scale[c];
+    prm[C + c] = shift[c];
+  }
+  __syncthreads();
+  if (counter && blockIdx.x == 0 && threadIdx.x == 0) *counter += 1;
+  const int C8 = C >> 3;
+  const bool pow2 = (C8 & (C8 - 1)) == 0;
+  const int64_t step = (int64_t)gridDim.x * kBlock * kFlatU;
+  for (int64_t t0 = (int64_t)blockIdx.x * kBlock * kFlatU + threadIdx.x; t0 < chunks; t0 += step) {
+    // raw 8-element vectors in flight (4 registers per 16-bit chunk), converted at use
+    Vec8<T> xr[kFlatU];
+    Vec8<Tz> zr[kFlatU];
+#pragma unroll
+    for (int u = 0; u < kFlatU; ++u) {
+      const int64_t i = t0 + (int64_t)u * kBlock;
+      if (i < chunks) {
+        xr[u] = *reinterpret_cast<const Vec8<T>*>(x + i * 8);
+        if (z) zr[u] = *reinterpret_cast<const Vec8<Tz>*>(z + i * 8);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kFlatU; ++u) {
+      const int64_t i = t0 + (int64_t)u * kBlock;
+      if (i >= chunks) continue;
+      const int c0 = (int)chunk_chan(i, C8, pow2) * 8;
+      float sc[8], sh[8], o8[8];
+      VecIO<float>::load(prm + c0, sc);
+      VecIO<float>::load(prm + C + c0, sh);
+      uint32_t bits = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float o = fmaf(to_f<T>(xr[u][k]), sc[k], sh[k]);
+        if (z) o += to_f<Tz>(zr[u][k]);
+        bits |= (o > 0.f ? 1u : 0u) << k;
+        if (relu) o = fmaxf(o, 0.f);
+        o8[k] = o;
+      }
+      VecIO<Ty>::store(y + i * 8, o8);
+      if (mbits) mbits[i] = (uint8_t)bits;
+    }
+  }
+}
+
+// flat variant of k_dgrad_nhwc (same chunk walk as k_fwd_flat): dx = dy' * A + x * B + D with the
+// per-channel A / B / D (and the ReLU recompute's scale / shift) built into LDS once per workgroup
+template <typename T, typename Tz, typename Tw>
+__global__ __launch_bounds__(kBlock) void k_dgrad_flat(const T* __restrict__ dy, const T* __restrict__ x,
+                                                       const Tz* __restrict__ z, const float* __restrict__ mean,
+                                                       const float* __restrict__ invstd, const Tw* __restrict__ w,
+                                                       const float* __restrict__ sums, const float* __restrict__ count,
+                                                       const float* __restrict__ scale, const float* __restrict__ shift,
+                                                       bool relu, T* __restrict__ dx, Tz* __restrict__ dz,
+                                                       int64_t chunks, int C, const uint8_t* __restrict__ mbits) {
+  extern __shared__ float prm[];  // [5][C]: A, B, D, scale, shift
+  const float inv_n = 1.f / count[0];
+  const bool recompute = relu && !mbits;
+  for (int c = threadIdx.x; c < C; c += kBlock) {
+    const float is = invstd[c], wv = w ? to_f<Tw>(w[c]) : 1.f;
+    const float mdy = sums[c] * inv_n, mdyx = sums[C + c] * inv_n;
+    prm[c] = is * wv;
+    prm[C + c] = -is * is * is * wv * mdyx;
+    prm[2 * C + c] = is * wv * (mean[c] * is * is * mdyx - mdy);
+    if (recompute) {
+      prm[3 * C + c] = scale[c];
+      prm[4 * C + c] = shift[c];
+    }
+  }
+  __syncthreads();
+  const bool use_z = recompute && z;
+  const int C8 = C >> 3;
+  const bool pow2 = (C8 & (C8 - 1)) == 0;
+  const int64_t step = (int64_t)gridDim.x * kBlock * kFlatU;
+  for (int64_t t0 = (int64_t)blockIdx.x * kBlock * kFlatU + threadIdx.x; t0 < chunks; t0 += step) {
+    Vec8<T> gr[kFlatU], xr[kFlatU];
+    Vec8<Tz> zr[kFlatU];
+    uint32_t bits[kFlatU];
+#pragma unroll
+    for (int u = 0; u < kFlatU; ++u) {
+      const int64_t i = t0 + (int64_t)u * kBlock;
+      bits[u] = 0xffu;
+      if (i < chunks) {
+        gr[u] = *reinterpret_cast<const Vec8<T>*>(dy + i * 8);
+        xr[u] = *reinterpret_cast<const Vec8<T>*>(x + i * 8);
+        if (use_z) zr[u] = *reinterpret_cast<const Vec8<Tz>*>(z + i * 8);
+        if (mbits) bits[u] = mbits[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kFlatU; ++u) {
+      const int64_t i = t0 + (int64_t)u * kBlock;
+      if (i >= chunks) continue;
+      const int c0 = (int)chunk_chan(i, C8, pow2) * 8;
+      float g[1][8], xv[1][8], zv[1][8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        g[0][k] = to_f<T>(gr[u][k]);
+        xv[0][k] = to_f<T>(xr[u][k]);
+        zv[0][k] = use_z ? to_f<Tz>(zr[u][k]) : 0.f;
+      }
+      if (mbits) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (!((bits[u] >> k) & 1u)) g[0][k] = 0.f;
+      } else if (relu) {
+        float sc[8], sh[8];
+        VecIO<float>::load(prm + 3 * C + c0, sc);
+        VecIO<float>::load(prm + 4 * C + c0, sh);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float o = fmaf(xv[0][k], sc[k], sh[k]);
+          if (use_z) o += zv[0][k];
+          if (o <= 0.f) g[0][k] = 0.f;
+        }
+      }
+      if (dz) VecIO<Tz>::store(dz + i * 8, g[0]);
+      float A[8], B[8], D[8];
+      VecIO<float>::load(prm + c0, A);
+      VecIO<float>::load(prm + C + c0, B);
+      VecIO<float>::load(prm + 2 * C + c0, D);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) xv[0][k] = fmaf(g[0][k], A[k], fmaf(xv[0][k], B[k], D[k]));
+      VecIO<T>::store(dx + i * 8, xv[0]);
+    }
+  }
+}
+
 // generic (NCHW or unaligned NHWC): element i -> channel (i / inner) % C
 template <typename T, typename Tz, typename Ty>
 __global__ __launch_bounds__(kBlock) void k_fwd_generic(const T* __restrict__ x, const Tz* __restrict__ z,
@@ -1009,13 +1151,28 @@ void bn_merge_parts(int G, int C, const float* part, float count, const BNFinal&
   check_launch("bn_merge_parts");
 }
 
+// the flat chunk-walk apply / data-gradient kernels (k_fwd_flat, k_dgrad_flat) instead of the 2-D
+// channel-owned ones; BH_BN_FLAT=0 restores those. BH_BN_FLAT_BLOCKS caps the grid.
+bool knob_flat() { static const bool v = env_knob("BH_BN_FLAT", 1) != 0; return v; }
+unsigned flat_grid(int64_t chunks) {
+  static const int64_t cap = env_knob("BH_BN_FLAT_BLOCKS", 2048);
+  const int64_t need = (chunks + kBlock * kFlatU - 1) / (kBlock * kFlatU);
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, cap));
+}
+
 void bn_forward(const BNShape& s, int dt_x, const void* x, int dt_z, const void* z, int dt_y, void* y,
                 const float* scale, const float* shift, bool relu, int64_t* counter, hipStream_t st,
                 uint8_t* mbits) {
   const int64_t total = s.outer * s.C * s.inner;
   if (total == 0) return;
   if (dt_z < 0) dt_z = dt_x;
-  if (s.channels_last && s.C % 8 == 0) {
+  if (s.channels_last && s.C % 8 == 0 && knob_flat()) {
+    const int64_t chunks = total / 8;
+    const size_t shm = sizeof(float) * 2 * s.C;
+    BN_DISPATCH(dt_x, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_y, Ty,
+        hipLaunchKernelGGL((k_fwd_flat<T, Tz, Ty>), dim3(flat_grid(chunks)), dim3(kBlock), shm, st, (const T*)x,
+                           (const Tz*)z, (Ty*)y, scale, shift, chunks, s.C, relu, counter, mbits))));
+  } else if (s.channels_last && s.C % 8 == 0) {
     const NhwcGeom g = nhwc_geom(s.C);
     const int64_t splits = nhwc_splits(s, knob_ew_blocks(), knob_ew_rows());
     const int64_t rps = (s.outer + splits - 1) / splits;
@@ -1081,7 +1238,14 @@ void bn_backward_dgrad(const BNShape& s, int dt, const void* dy, const void* x, 
   const int64_t total = s.outer * s.C * s.inner;
   if (total == 0) return;
   if (dt_z < 0) dt_z = dt;
-  if (s.channels_last && s.C % 8 == 0) {
+  if (s.channels_last && s.C % 8 == 0 && knob_flat()) {
+    const int64_t chunks = total / 8;
+    const size_t shm = sizeof(float) * 5 * s.C;
+    BN_DISPATCH(dt, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_w, Tw,
+        hipLaunchKernelGGL((k_dgrad_flat<T, Tz, Tw>), dim3(flat_grid(chunks)), dim3(kBlock), shm, st, (const T*)dy,
+                           (const T*)x, (const Tz*)z, mean, invstd, (const Tw*)w, sums, count, scale, shift, relu,
+                           (T*)dx, (Tz*)dz, chunks, s.C, mbits))));
+  } else if (s.channels_last && s.C % 8 == 0) {
     const NhwcGeom g = nhwc_geom(s.C);
     const int64_t splits = nhwc_splits(s, knob_ew_blocks(), knob_ew_rows());
     const int64_t rps = (s.outer + splits - 1) / splits;

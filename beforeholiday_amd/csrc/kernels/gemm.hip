@@ -445,7 +445,8 @@ BH_DEVICE __amdgpu_buffer_rsrc_t tile_rsrc(const void* base, int64_t rows_left, 
 
 // ACT / BWD as template parameters: one epilogue path per kernel (all of them in one function pushed
 // the register allocator past 256 VGPRs and into scratch)
-template <typename T, int ACT, bool BWD, bool STATS = false>
+// STATS: 0 none, 1 forward statistics (bn_stats 1), 2 the previous BatchNorm's backward sums (bn_stats 2)
+template <typename T, int ACT, bool BWD, int STATS = 0>
 __global__ __launch_bounds__(kPPThreads, 1) void k_gemm_pp(Args p) {
   __shared__ __attribute__((aligned(16))) char smem[kPPSmem];
   const int tid = threadIdx.x;
@@ -641,6 +642,19 @@ __global__ __launch_bounds__(kPPThreads, 1) void k_gemm_pp(Args p) {
   };
   {
     if constexpr (!BWD) {
+      if (e.resid) {  // C = A.B^T + resid: the residual comes in through the image, then onto the accumulators
+        fill(reinterpret_cast<const T*>(e.resid), p.ldc);
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            float r[4];
+            get(mt, nt, r);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[mt][nt][j] += r[j];
+          }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // image reads done before it is rewritten
+      }
       // bias folded into the accumulators first (the pre-activation, kept in fp32 for the activation)
       if (e.bias) {
 #pragma unroll
@@ -666,46 +680,109 @@ __global__ __launch_bounds__(kPPThreads, 1) void k_gemm_pp(Args p) {
           }
         flush(reinterpret_cast<T*>(e.pre_out), e.ld_aux);
       }
+      // BatchNorm statistics of the stored values (bn_stats == 1): sums of c - kshift and its square
+      // per column, accumulated while the tile goes into the image (the accumulators die there; the
+      // stats never hold them live across the flush), over the wave's 128 rows (16 row lanes x 8
+      // tiles), written to the 64-row slab of row_w (the next slab gets zeros, as the fixed-order
+      // partial reduction expects every slab)
+      float s1[4][4] = {}, s2[4][4] = {}, kc[4][4] = {};
+      if constexpr (STATS == 1) {
+        if (e.kshift) {
 #pragma unroll
-      for (int mt = 0; mt < 8; ++mt) {
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          float v[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = acc[mt][nt][j];
-          if constexpr (ACT != kActNone) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[j] = act_f(v[j], ACT);
-          }
-          put(mt, nt, v);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      flush(Cp, p.ldc);
-      if constexpr (STATS) {
-        // BatchNorm statistics of the stored values (bn_stats == 1): sums of c - kshift and its square
-        // per column over the wave's 128 rows (16 row lanes x 8 tiles), written to the 64-row slab of
-        // row_w (the next slab gets zeros, as the fixed-order partial reduction expects every slab)
-        float s1[4][4] = {}, s2[4][4] = {};
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          const int col = col_l + nt * 16;
-          float k[4] = {0.f, 0.f, 0.f, 0.f};
-          if (e.kshift && col < p.N) {
-            const float4 kv = *reinterpret_cast<const float4*>(e.kshift + col);
-            k[0] = kv.x; k[1] = kv.y; k[2] = kv.z; k[3] = kv.w;
-          }
-#pragma unroll
-          for (int mt = 0; mt < 8; ++mt) {
-            if (row_w + mt * 16 + fr >= p.M) continue;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const float d = to_f<T>(from_f<T>(acc[mt][nt][j])) - k[j];
-              s1[nt][j] += d;
-              s2[nt][j] = fmaf(d, d, s2[nt][j]);
+          for (int nt = 0; nt < 4; ++nt) {
+            const int col = col_l + nt * 16;
+            if (col < p.N) {
+              const float4 kv = *reinterpret_cast<const float4*>(e.kshift + col);
+              kc[nt][0] = kv.x; kc[nt][1] = kv.y; kc[nt][2] = kv.z; kc[nt][3] = kv.w;
             }
           }
         }
+      }
+      if constexpr (STATS == 2) {
+        // backward sums of the BatchNorm whose input y = bn_y feeds this layer's output gradient:
+        // y comes into the image with coalesced loads; each (mt, nt) piece is read back in the
+        // accumulator layout and replaced by the output (the dGELU pattern below). Column-tile
+        // outer loop: one column tile's scale / shift / mean live at a time.
+        fill(reinterpret_cast<const T*>(e.bn_y), p.ldc);
+        const int64_t slabs = ((int64_t)p.M + 63) / 64, slab = row_w / 64;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const int col = col_l + nt * 16;
+          float sc[4] = {0.f, 0.f, 0.f, 0.f}, sh[4] = {0.f, 0.f, 0.f, 0.f}, mu[4] = {0.f, 0.f, 0.f, 0.f};
+          if (col < p.N) {
+            const float4 a = *reinterpret_cast<const float4*>(e.bn_scale + col);
+            const float4 b = *reinterpret_cast<const float4*>(e.bn_shift + col);
+            const float4 c = *reinterpret_cast<const float4*>(e.bn_mean + col);
+            sc[0] = a.x; sc[1] = a.y; sc[2] = a.z; sc[3] = a.w;
+            sh[0] = b.x; sh[1] = b.y; sh[2] = b.z; sh[3] = b.w;
+            mu[0] = c.x; mu[1] = c.y; mu[2] = c.z; mu[3] = c.w;
+          }
+          float t1[4] = {0.f, 0.f, 0.f, 0.f}, t2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int mt = 0; mt < 8; ++mt) {
+            const bool row_ok = row_w + mt * 16 + fr < p.M;
+            float y[4], v[4];
+            get(mt, nt, y);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = acc[mt][nt][j];
+            put(mt, nt, v);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float g = to_f<T>(from_f<T>(v[j]));
+              const bool pass = row_ok && (!e.bn_relu || fmaf(y[j], sc[j], sh[j]) > 0.f);
+              const float dz = pass ? g : 0.f;
+              t1[j] += dz;
+              t2[j] = fmaf(dz, row_ok ? y[j] - mu[j] : 0.f, t2[j]);
+            }
+          }
+          // this column tile's sums over the 16 row lanes, written right away (few live registers)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int m = 1; m < 16; m <<= 1) {
+              t1[j] += __shfl_xor(t1[j], m);
+              t2[j] += __shfl_xor(t2[j], m);
+            }
+          if (fr == 0 && row_w < p.M && col < p.N) {
+            float* d1 = e.stat_part + slab * p.N + col;
+            float* d2 = e.stat_part + (slabs + slab) * p.N + col;
+            *reinterpret_cast<float4*>(d1) = make_float4(t1[0], t1[1], t1[2], t1[3]);
+            *reinterpret_cast<float4*>(d2) = make_float4(t2[0], t2[1], t2[2], t2[3]);
+            if (row_w + 64 < p.M) {
+              *reinterpret_cast<float4*>(d1 + p.N) = make_float4(0.f, 0.f, 0.f, 0.f);
+              *reinterpret_cast<float4*>(d2 + p.N) = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+#pragma unroll
+        for (int mt = 0; mt < 8; ++mt) {
+          const bool row_ok = row_w + mt * 16 + fr < p.M;
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) {
+            float v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = acc[mt][nt][j];
+            if constexpr (ACT != kActNone) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[j] = act_f(v[j], ACT);
+            }
+            put(mt, nt, v);
+            if constexpr (STATS == 1) {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const float d = row_ok ? to_f<T>(from_f<T>(v[j])) - kc[nt][j] : 0.f;
+                s1[nt][j] += d;
+                s2[nt][j] = fmaf(d, d, s2[nt][j]);
+              }
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      flush(Cp, p.ldc);
+      if constexpr (STATS == 1) {
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
@@ -802,6 +879,47 @@ __global__ __launch_bounds__(64 * kColsumLanes) void k_colsum(const float* __res
   colsum_partials_block<T>(part, slabs, N, out, sh);
 }
 
+// out [C, R] = in [R, C]^T for 16-bit elements: 64 x 64 tiles through LDS (ushort rows padded to 66 so the
+// column reads spread over banks), 16-byte loads along input rows and 16-byte stores along output rows.
+// Used for the weight transposes of the GEMM data gradients (dX = dY . W needs W^T as the [N, K] operand).
+__global__ __launch_bounds__(256) void k_transpose16(const uint16_t* __restrict__ in, int64_t R, int64_t C,
+                                                      uint16_t* __restrict__ out) {
+  __shared__ uint16_t t[64][66];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = tid + i * 256, rr = q >> 3, cc = (q & 7) * 8;
+    const int64_t r = r0 + rr, c = c0 + cc;
+    uint16_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (r < R && c + 8 <= C) {
+      const uint4 u = *reinterpret_cast<const uint4*>(in + r * C + c);
+      __builtin_memcpy(v, &u, 16);
+    } else if (r < R) {
+      for (int j = 0; j < 8; ++j) if (c + j < C) v[j] = in[r * C + c + j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[rr][cc + j] = v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int q = tid + i * 256, cc = q >> 3, rr = (q & 7) * 8;  // output row c0 + cc, columns r0 + rr ..
+    const int64_t c = c0 + cc, r = r0 + rr;
+    if (c >= C) continue;
+    uint16_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = t[rr + j][cc];
+    if (r + 8 <= R) {
+      uint4 u;
+      __builtin_memcpy(&u, v, 16);
+      *reinterpret_cast<uint4*>(out + c * R + r) = u;
+    } else {
+      for (int j = 0; j < 8; ++j) if (r + j < R) out[c * R + r + j] = v[j];
+    }
+  }
+}
+
 inline void check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
@@ -829,7 +947,11 @@ void launch_pp(const Args& a0, hipStream_t st) {
   const int64_t nwg = (int64_t)a.tiles_m * a.tiles_n;
   if (nwg >= (1ll << 31)) throw std::runtime_error("gemm_nt: grid too large");
   if (a.epi.bn_stats == 1) {  // statistics epilogue: plain output (no bias / activation / aux)
-    hipLaunchKernelGGL((k_gemm_pp<T, kActNone, false, true>), dim3((unsigned)nwg), dim3(kPPThreads), 0, st, a);
+    hipLaunchKernelGGL((k_gemm_pp<T, kActNone, false, 1>), dim3((unsigned)nwg), dim3(kPPThreads), 0, st, a);
+    return;
+  }
+  if (a.epi.bn_stats == 2) {  // backward-sums epilogue: plain output
+    hipLaunchKernelGGL((k_gemm_pp<T, kActNone, false, 2>), dim3((unsigned)nwg), dim3(kPPThreads), 0, st, a);
     return;
   }
   auto go = [&](auto actc) {
@@ -891,9 +1013,15 @@ void gemm_nt(int dt, const void* A, int64_t lda, const void* B, int64_t ldb, voi
   const int64_t big_wgs = ((M + CfgBig::BM - 1) / CfgBig::BM) * ((N + CfgBig::BN - 1) / CfgBig::BN);
   // the ping-pong kernel keeps row offsets of a 256-row tile in 32 bits
   const bool pp_ok = glds && lda < (1 << 22) && ldb < (1 << 22);
-  // the ping-pong kernel has the statistics epilogue (bn_stats == 1) but not the BatchNorm-backward one
-  const bool pp_epi = epi.bn_stats == 0 || (epi.bn_stats == 1 && !epi.bias && epi.act == kActNone && !epi.pre_out);
-  const bool pp = pp_ok && pp_epi && (tile_mode == 4 || (tile_mode == 0 && big_wgs >= 256));
+  // the ping-pong kernel's BatchNorm epilogues (statistics, backward sums) come with a plain output
+  const bool pp_epi = epi.bn_stats == 0 || (!epi.bias && epi.act == kActNone && !epi.pre_out && !epi.bwd_act);
+  // auto: the ping-pong kernel from 160 of its 256x256 tiles on (it beats the 128x128 kernel there,
+  // benchmarks/bench_resnet_gemms.py), never for outputs of at most 128 columns (half its tile idle:
+  // 132 vs ~60 us for the 200704 x 128 x 512 BatchNorm-backward GEMM in the ResNet-50 step)
+  const bool pp_auto = N > 128 && big_wgs >= 160;
+  const bool pp = pp_ok && pp_epi && (tile_mode == 4 || epi.resid || (tile_mode == 0 && pp_auto));
+  if (epi.resid && epi.bwd_act) throw std::runtime_error("gemm_nt: a residual input needs a forward epilogue");
+  if (epi.resid && !pp) throw std::runtime_error("gemm_nt: a residual input needs the ping-pong kernel (K % 64 == 0)");
   const bool big = glds && !pp && (tile_mode == 2 || (tile_mode == 0 && big_wgs >= 256));
   const bool mid = glds && tile_mode == 3;
   switch (dt) {
@@ -912,6 +1040,16 @@ void gemm_nt(int dt, const void* A, int64_t lda, const void* B, int64_t ldb, voi
     default: throw std::runtime_error("gemm_nt: fp16 / bf16 only");
   }
   check_launch("gemm_nt");
+}
+
+void transpose16(const void* in, int64_t R, int64_t C, void* out, hipStream_t st) {
+  if (R <= 0 || C <= 0) return;
+  const bool vec = R % 8 == 0 && C % 8 == 0 && al16(in) && al16(out);
+  if (!vec) throw std::runtime_error("transpose16: rows / columns must be multiples of 8 and 16-byte aligned");
+  const dim3 grid((unsigned)((C + 63) / 64), (unsigned)((R + 63) / 64));
+  hipLaunchKernelGGL(k_transpose16, grid, dim3(256), 0, st, reinterpret_cast<const uint16_t*>(in), R, C,
+                     reinterpret_cast<uint16_t*>(out));
+  check_launch("transpose16");
 }
 
 void gemm_colsum_finalize(int dt, const float* part, int64_t slabs, int64_t N, void* out, hipStream_t st) {

@@ -586,6 +586,68 @@ class _GlobalAvgPoolFn(torch.autograd.Function):
         return (g / (h * w)).view(n, c, 1, 1).expand(n, c, h, w).contiguous(memory_format=torch.channels_last)
 
 
+def _tr(t):
+    """``t.t().contiguous()`` of a 2-D tensor; 16-bit GPU tensors through the LDS-tiled transpose kernel
+    (gemm.transpose: torch's strided copy took ~9 us per ResNet-50 weight)."""
+    if t.is_cuda and t.dtype in (torch.float16, torch.bfloat16) and t.is_contiguous() and t.size(0) % 8 == 0 \
+            and t.size(1) % 8 == 0:
+        from .._native import submodule
+
+        return submodule("gemm").transpose(t)
+    return t.t().contiguous()
+
+
+class _FcFn(torch.autograd.Function):
+    """The classifier ``x W^T + b`` on the MFMA GEMM (kernels/gemm.hip, ``gemm.mm_nt``) in all three
+    directions: one fixed kernel per shape, so every rank (and every run) computes it bitwise the
+    same -- a library GEMM may pick a split-K / stream-K solution for these skinny shapes, whose
+    accumulation order is not fixed. The class dimension is padded to a multiple of 8 with zero
+    weight rows (10- or 1000-way heads); the transposed operands are small copies."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        from .._native import submodule
+
+        gm = submodule("gemm")
+        n = w.size(0)
+        n8 = (n + 7) // 8 * 8
+        wp = w if n8 == n else torch.cat([w, w.new_zeros(n8 - n, w.size(1))])
+        bp = None if b is None else (b if n8 == n else torch.cat([b, b.new_zeros(n8 - n)]))
+        y = gm.mm_nt(x, wp, bp)
+        ctx.save_for_backward(x, wp)
+        ctx.n, ctx.has_b = n, b is not None
+        return y[:, :n] if n8 != n else y
+
+    @staticmethod
+    def backward(ctx, gy):
+        from .._native import submodule
+
+        gm = submodule("gemm")
+        x, wp = ctx.saved_tensors
+        n, n8 = ctx.n, wp.size(0)
+        gyp = gy.contiguous() if n8 == n else torch.cat([gy, gy.new_zeros(gy.size(0), n8 - n)], 1)
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = gm.mm_nt(gyp, _tr(wp))  # dX = dY . W
+        if ctx.needs_input_grad[1]:
+            gw = gm.mm_nt(_tr(gyp), _tr(x))[:n]  # dW = dY^T . X
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            gb = gy.float().sum(0).to(gy.dtype)
+        return gx, gw, gb
+
+
+def _fc_args(fc, x):
+    """(weight, bias) in x's dtype for :class:`_FcFn` (amp O1 / O4: the 16-bit copies), or None."""
+    if not (x.is_cuda and x.dim() == 2 and x.dtype in (torch.float16, torch.bfloat16) and x.size(0) % 8 == 0
+            and x.size(1) % 8 == 0 and x.is_contiguous()):
+        return None
+    w = _kw(fc.weight, x)
+    b = _kw(fc.bias, x) if fc.bias is not None else None
+    if w is None or (fc.bias is not None and b is None):
+        return None
+    return w, b
+
+
 class StemConv(nn.Conv2d):
     """nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False) with the MFMA stem forward (``mode``
     "auto" times it against MIOpen once, "gemm" forces it, "miopen" is plain nn.Conv2d)."""
@@ -728,6 +790,18 @@ class _Conv1x1BNFn(torch.autograd.Function):
                     link.sums = conv_bn.sum_parts(part)
                 elif fast and conv_bn.supported(gy2d, w2d, resid=r2d is not None, b_trans=True):
                     gx2d, _ = conv_bn.c1x1(gy2d, w2d, resid=r2d, b_trans=True)
+                elif _own("resid" if r2d is not None else ("bwd" if _link_ok(link, c) else "plain")) and \
+                        conv_bn.gemm_bn_supported(gy2d, w2d.t(), resid=r2d is not None):
+                    # the tiled MFMA GEMM: dX = dY . W (+ the parked residual gradient), with the previous
+                    # BatchNorm's backward sums in its epilogue when that BatchNorm is linked
+                    wt = _tr(w2d)
+                    if _link_ok(link, c):
+                        y2d = link.y.permute(0, 2, 3, 1).reshape(-1, c)
+                        gx2d, part = conv_bn.gemm_bn(gy2d, wt, "bwd", by=y2d, bscale=link.scale, bshift=link.shift,
+                                                     bmean=link.mean, brelu=link.relu, resid=r2d)
+                        link.sums = conv_bn.sum_parts(part)
+                    else:
+                        gx2d, _ = conv_bn.gemm_bn(gy2d, wt, "plain", resid=r2d)
                 elif r2d is not None:  # beta = 1 into the parked residual gradient (no output copy)
                     gx2d = torch.addmm(r2d, gy2d, w2d, out=r2d)
                 else:
@@ -758,12 +832,10 @@ def _c1x1_forward_stats(x, weight, kshift, s2):
         return y2d.view(n, ho, wo, k).permute(0, 3, 1, 2), part
     if s2:
         a2d = x[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, c)
-    if _PP_STATS and k >= 2048 and a2d.size(0) >= 4 * 256 and a2d.dtype in (torch.float16, torch.bfloat16):
-        # the 2048-channel outputs of stage 4: the 256x256 ping-pong MFMA GEMM with the statistics
-        # epilogue (kernels/gemm.hip), no separate statistics pass. Narrower outputs keep the tuned
-        # library GEMM + statistics pass: with K <= 256 the ping-pong tile is prologue / epilogue bound
-        # and measured 0.15 vs 0.10 ms (K 128 -> N 512) and 0.082 vs 0.074 ms (256 -> 1024)
-        # (profiles/conv_bn_vs_unfused.jsonl, ms_tiled_gemm_bn); whole step 24.9 vs 24.6 ms with them
+    if _own("fwd") and conv_bn.gemm_bn_supported(a2d, w2d):
+        # the MFMA-bound layers (K or N >= 512, or the small 14x14 / 7x7 grids): the tiled MFMA GEMM
+        # with the statistics epilogue (kernels/gemm.hip; the ping-pong 256x256 kernel from 160 tiles),
+        # no library GEMM and no separate statistics pass (benchmarks/bench_resnet_gemms.py)
         y2d, part = conv_bn.gemm_bn(a2d, w2d, "stats", kshift=kshift)
         return y2d.view(n, ho, wo, k).permute(0, 3, 1, 2), part
     y = torch.mm(a2d, w2d.t()).view(n, ho, wo, k).permute(0, 3, 1, 2)
@@ -824,6 +896,8 @@ class _Conv1DsFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if conv_bn.preferred(k1, c, g1.size(0)) and conv_bn.supported(g1, w1_2d, b_trans=True):
                 gx2d, _ = conv_bn.c1x1(g1, w1_2d, b_trans=True)
+            elif _own("plain") and conv_bn.gemm_bn_supported(g1, w1_2d.t()):
+                gx2d, _ = conv_bn.gemm_bn(g1, _tr(w1_2d), "plain")
             else:
                 gx2d = torch.mm(g1, w1_2d)
             if ctx.s2:
@@ -833,10 +907,16 @@ class _Conv1DsFn(torch.autograd.Function):
                         conv_bn.supported(gd, wd_2d, b_trans=True, s2=(h, w), s2_scatter=True):
                     conv_bn.c1x1(gd, wd_2d, b_trans=True, s2=(h, w), s2_scatter=True, resid=gx2d)
                 else:
+                    if _own("plain") and conv_bn.gemm_bn_supported(gd, wd_2d.t()):
+                        gdx = conv_bn.gemm_bn(gd, _tr(wd_2d), "plain")[0]
+                    else:
+                        gdx = torch.mm(gd, wd_2d)
                     # add_ on the strided view: `view[idx] += t` would also copy the view onto itself
-                    gx2d.view(n, h, w, c)[:, ::2, ::2, :].add_(torch.mm(gd, wd_2d).view(n, h // 2, w // 2, c))
+                    gx2d.view(n, h, w, c)[:, ::2, ::2, :].add_(gdx.view(n, h // 2, w // 2, c))
             elif conv_bn.preferred(kd, c, gd.size(0)) and conv_bn.supported(gd, wd_2d, resid=True, b_trans=True):
                 gx2d, _ = conv_bn.c1x1(gd, wd_2d, resid=gx2d, b_trans=True)
+            elif _own("resid") and conv_bn.gemm_bn_supported(gd, wd_2d.t(), resid=True):
+                gx2d, _ = conv_bn.gemm_bn(gd, _tr(wd_2d), "plain", resid=gx2d)
             else:
                 torch.addmm(gx2d, gd, wd_2d, out=gx2d)
             gx = gx2d.view(n, h, w, c).permute(0, 3, 1, 2)
@@ -978,6 +1058,10 @@ class _BNConvFn(torch.autograd.Function):
                 dA2d, part = conv_bn.c1x1(gy2d, w2d, epi="bwd", by=y2d, bscale=scale, bshift=shift, bmean=mean,
                                           brelu=True, b_trans=True)
                 sums = conv_bn.sum_parts(part)
+            elif _own("bwd") and conv_bn.gemm_bn_supported(gy2d, w2d.t()):
+                dA2d, part = conv_bn.gemm_bn(gy2d, _tr(w2d), "bwd", by=y2d, bscale=scale, bshift=shift,
+                                             bmean=mean, brelu=True)
+                sums = conv_bn.sum_parts(part)
             else:
                 dA2d = torch.mm(gy2d, w2d)
             dA = dA2d.view(n, h, w, C).permute(0, 3, 1, 2)
@@ -1018,7 +1102,28 @@ _FOLD_APPLY = {"1": "all", "0": "none"}.get(os.environ.get("BH_FOLD_APPLY", "all
 assert _FOLD_APPLY in ("all", "bn1", "bn2", "none"), f"BH_FOLD_APPLY={_FOLD_APPLY!r}"
 # the stem convolution's epilogue reduces the stem BatchNorm's statistics (BH_STEM_STATS=0: a pass)
 _STEM_STATS = os.environ.get("BH_STEM_STATS", "1") != "0"
-_PP_STATS = os.environ.get("BH_PP_STATS", "1") != "0"
+# the 1x1 layers the strip kernel does not take run on the own tiled MFMA GEMM (kernels/gemm.hip) with
+# the BatchNorm epilogues; BH_OWN_GEMM=0 puts them back on hipBLASLt + separate passes (A/B)
+def _own_gemm_kinds(v):
+    v = v.strip().lower()
+    if v in ("1", "all"):
+        return {"fwd", "bwd", "plain", "resid"}
+    if v in ("0", "none", ""):
+        return set()
+    kinds = {k.strip() for k in v.split(",")}
+    assert kinds <= {"fwd", "bwd", "plain", "resid"}, f"BH_OWN_GEMM={v!r}"
+    return kinds
+
+
+# which of those GEMM kinds take the own kernel: "fwd" (forward + statistics epilogue), "bwd" (data
+# gradient + the previous BatchNorm's backward sums), "plain" (data gradient), "resid" (data gradient
+# + the parked residual gradient); a comma list, "all" or "none"
+_OWN_GEMM_KINDS = _own_gemm_kinds(os.environ.get("BH_OWN_GEMM", "fwd,plain"))
+_OWN_GEMM = bool(_OWN_GEMM_KINDS)
+
+
+def _own(kind):
+    return kind in _OWN_GEMM_KINDS
 _FOLD_3X3_BWD = os.environ.get("BH_FOLD_3X3_BWD", "0") == "1"
 
 
@@ -1216,6 +1321,9 @@ class ResNet(nn.Module):
             x = _GlobalAvgPoolFn.apply(x)
         else:
             x = torch.flatten(self.avgpool(x), 1)
+        fc = _fc_args(self.fc, x) if self.fused else None
+        if fc is not None:  # the classifier on the MFMA GEMM too (fixed kernels, rank-identical)
+            return _FcFn.apply(x, *fc)
         return self.fc(x)
 
 

@@ -134,10 +134,21 @@ def sum_parts(part: torch.Tensor, count: float = -1.0) -> torch.Tensor:
 
 
 def gemm_bn(a: torch.Tensor, b: torch.Tensor, epi: str = "stats", kshift=None, by=None, bscale=None, bshift=None,
-            bmean=None, brelu: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
-    """``C = a @ b.T`` on the tiled MFMA GEMM (kernels/gemm.hip, 128x128 / 256x128 / 256x256 tiles) with the
-    same BatchNorm epilogues as :func:`c1x1` (``epi`` "stats" or "bwd"; partials per 64-row slab):
-    the compute-bound 1x1 layers (K or N >= 512) that the strip kernel runs at low MFMA rates."""
+            bmean=None, brelu: bool = True, resid: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``C = a @ b.T (+ resid)`` on the tiled MFMA GEMM (kernels/gemm.hip: ping-pong 256x256, 128x128 /
+    256x128 / 256x256 tiles) with the same BatchNorm epilogues as :func:`c1x1` (``epi`` "plain", "stats"
+    or "bwd"; partials per 64-row slab): the compute-bound 1x1 layers (K or N >= 512) that the strip
+    kernel runs at low MFMA rates. ``resid`` needs ``K % 64 == 0``. Returns ``(C, part)`` (``part`` None
+    for "plain")."""
     if not a.is_cuda:
-        return _reference(a, b, None, None, None, None, epi, kshift, by, bscale, bshift, bmean, brelu)
-    return submodule("conv_bn").gemm_bn(a, b, _EPI[epi], kshift, by, bscale, bshift, bmean, brelu)
+        c, part = _reference(a, b, None, None, resid, None, epi, kshift, by, bscale, bshift, bmean, brelu)
+        return c, (part if epi != "plain" else None)
+    return tuple(submodule("conv_bn").gemm_bn(a, b, _EPI[epi], kshift, by, bscale, bshift, bmean, brelu, resid))
+
+
+def gemm_bn_supported(a: torch.Tensor, b: torch.Tensor, resid: bool = False) -> bool:
+    """Shapes :func:`gemm_bn` takes on the GPU: 16-bit ``a [M, K]`` / ``b [N, K]``, K % 8 == 0 (K % 64
+    with a residual), N % 64 == 0."""
+    K, N = a.size(1), b.size(0)
+    return (a.is_cuda and available() and a.dtype in (torch.float16, torch.bfloat16) and b.dtype == a.dtype
+            and K % (64 if resid else 8) == 0 and N % 64 == 0)

@@ -56,15 +56,56 @@ for m in net.modules():
         m.float()
 state = {k: v.clone() for k, v in net.state_dict().items()}
 torch.manual_seed(11)
-x = torch.randn(16, 3, 224, 224, device="cuda").half().contiguous(memory_format=torch.channels_last)
+import os
+B = int(os.environ.get("DIAG_BATCH", "16"))
+x = torch.randn(B, 3, 224, 224, device="cuda").half().contiguous(memory_format=torch.channels_last)
+def poison(fill):
+    """Fill the caching allocator's free blocks with ``fill`` (grab them with tensors of decreasing
+    size, write, release): an op that reads memory it never wrote then sees other values."""
+    held = []
+    free = torch.cuda.memory_reserved() - torch.cuda.memory_allocated()
+    size = 1 << 30
+    while size >= 512 and free > 0:
+        try:
+            t = torch.empty(size // 4, dtype=torch.float32, device="cuda")
+        except RuntimeError:
+            size //= 2
+            continue
+        if torch.cuda.memory_reserved() - torch.cuda.memory_allocated() < 0:
+            break
+        t.fill_(fill)
+        held.append(t)
+        free -= size
+        if torch.cuda.memory_reserved() - torch.cuda.memory_allocated() < size:
+            size //= 2
+    del held
+    torch.cuda.synchronize()
+
+
+REPS = int(os.environ.get("DIAG_REPS", "3"))
+pre = os.environ.get("DIAG_PRE")  # "0" / "1": first a step on that half of the batch (like a 2-rank run)
+if pre is not None:
+    half = x[: B // 2] if pre == "0" else x[B // 2:]
+    net.load_state_dict(state)
+    (net(half).float().square().sum() / B).backward()
+    net.zero_grad(set_to_none=True)
+    torch.cuda.synchronize()
+BWD = os.environ.get("DIAG_BWD") == "1"
 runs = []
-for rep in range(3):
+for rep in range(REPS):
+    if os.environ.get("DIAG_POISON") and rep > 0:
+        poison(float("nan") if rep % 2 else 12345.0)
     net.load_state_dict(state)
     LOG.clear()
+    net.zero_grad(set_to_none=True)
     out = net(x)
+    if BWD:  # then every parameter gradient too, in parameter order
+        (out.float().square().sum() / x.shape[0]).backward()
+        for n, p in net.named_parameters():
+            LOG.append((f"grad {n}", [p.grad.detach().clone()]))
     torch.cuda.synchronize()
     runs.append(list(LOG))
-for rep in (1, 2):
+for rep in range(1, REPS):
     bad = None
     for i, ((n0, t0), (n1, t1)) in enumerate(zip(runs[0], runs[rep])):
         for j, (a, b) in enumerate(zip(t0, t1)):
@@ -79,3 +120,11 @@ for rep in (1, 2):
     if bad is None:
         print(f"run {rep}: all {len(runs[0])} ops bitwise identical")
 print("ops:", [n for n, _ in runs[0]])
+dump = os.environ.get("DIAG_DUMP")
+if dump:  # per-op output checksums, to compare two processes (python diag_determinism.py a; ... b; diff)
+    import hashlib
+
+    with open(dump, "w") as f:
+        for i, (n, ts) in enumerate(runs[0]):
+            hs = [hashlib.sha1(t.detach().contiguous().reshape(-1).view(torch.uint8).cpu().numpy().tobytes()).hexdigest()[:12] for t in ts]
+            f.write(f"{i} {n} {' '.join(hs)}\n")

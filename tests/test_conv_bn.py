@@ -270,3 +270,76 @@ def test_gemm_bn_stats_pingpong(MKN, dt):
     d = c.float() - kshift
     ref = torch.cat([d.sum(0), (d * d).sum(0)]).cpu()
     _stats_close(conv_bn.sum_parts(part).cpu(), ref, M)
+
+
+def _bwd_sums_ref(c, y, sc, sh, mean):
+    # the ReLU mask in float64: y * sc is exact there, so the sign matches the kernels' fused fmaf
+    # (a float32 mul + add can round a tiny positive pre-activation to zero or flip it)
+    cf, yf = c.float(), y.float()
+    dz = cf * ((y.double() * sc.double() + sh.double()) > 0).float()
+    return torch.cat([dz.sum(0), (dz * (yf - mean)).sum(0)])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("MKN", [(200704, 128, 512), (50176, 256, 1024), (12544, 512, 2048), (50000, 1024, 256),
+                                 (200704, 512, 128)])
+@pytest.mark.parametrize("mode", ["bwd", "plain_resid", "bwd_resid"])
+def test_gemm_bn_large_bwd_and_resid(MKN, dt, mode):
+    """The ResNet-50 (batch 256) data-gradient GEMMs at their real row counts (12.5k - 200k rows, so
+    the large-grid slab partials and the ping-pong kernel's backward-sums / residual epilogues are
+    exercised): C = A.B^T (+ resid) against the fp32 product, and the previous BatchNorm's backward
+    sums against an fp32 reduction of OUR stored output."""
+    M, K, N = MKN
+    torch.manual_seed(13)
+    a, b = _data(M, K, N, dt, "cuda", seed=13)
+    resid = (torch.randn(M, N, device="cuda") * 0.5).to(dt) if "resid" in mode else None
+    y = (torch.randn(M, N, device="cuda") * 2 + 0.3).to(dt)
+    sc, sh = torch.rand(N, device="cuda") + 0.5, torch.randn(N, device="cuda") * 0.3
+    mean = torch.randn(N, device="cuda") * 0.1
+    if mode.startswith("bwd"):
+        c, part = conv_bn.gemm_bn(a, b, "bwd", by=y, bscale=sc, bshift=sh, bmean=mean, resid=resid)
+        assert part.shape == (2, (M + 63) // 64, N)
+    else:
+        c, part = conv_bn.gemm_bn(a, b, "plain", resid=resid)
+        assert part is None
+    ref = a.float() @ b.float().t()
+    if resid is not None:
+        ref = ref + resid.float()
+    torch.testing.assert_close(c.float(), ref, **_tol(dt))
+    if part is not None:
+        _stats_close(conv_bn.sum_parts(part).cpu(), _bwd_sums_ref(c, y, sc, sh, mean).cpu(), M)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("KN,epi", [((64, 256), "stats"), ((256, 64), "stats"), ((64, 64), "pro"),
+                                    ((256, 64), "bwd"), ((64, 256), "bwd")])
+def test_c1x1_large_m(KN, epi, dt):
+    """The strip kernel at the ResNet-50 stage-1 row count (256 x 56 x 56 = 802,816 rows): the
+    grid-wide partial layout and sum_parts at the model's real scale."""
+    K, N = KN
+    M = 256 * 56 * 56
+    torch.manual_seed(17)
+    a, b = _data(M, K, N, dt, "cuda", seed=17)
+    kshift = torch.randn(N, device="cuda") * 0.1
+    if epi == "bwd":
+        y = (torch.randn(M, N, device="cuda") * 2 + 0.3).to(dt)
+        sc, sh = torch.rand(N, device="cuda") + 0.5, torch.randn(N, device="cuda") * 0.3
+        mean = torch.randn(N, device="cuda") * 0.1
+        w = b.t().contiguous()  # the data gradient reads the forward weight [K, N] transposed
+        assert conv_bn.supported(a, w, epi="bwd", b_trans=True)
+        c, part = conv_bn.c1x1(a, w, epi="bwd", by=y, bscale=sc, bshift=sh, bmean=mean, b_trans=True)
+        torch.testing.assert_close(c.float(), a.float() @ b.float().t(), **_tol(dt))
+        _stats_close(conv_bn.sum_parts(part).cpu(), _bwd_sums_ref(c, y, sc, sh, mean).cpu(), M)
+        return
+    if epi == "pro":
+        ps, pb = torch.rand(K, device="cuda") + 0.5, torch.randn(K, device="cuda") * 0.3
+        c, part = conv_bn.c1x1(a, b, pro_scale=ps, pro_shift=pb, epi="stats", kshift=kshift)
+        af = torch.relu(a.float() * ps + pb).to(dt).float()
+    else:
+        c, part = conv_bn.c1x1(a, b, epi="stats", kshift=kshift)
+        af = a.float()
+    torch.testing.assert_close(c.float(), af @ b.float().t(), **_tol(dt))
+    d = c.float() - kshift
+    _stats_close(conv_bn.sum_parts(part, M)[:2 * N].cpu(), torch.cat([d.sum(0), (d * d).sum(0)]).cpu(), M)

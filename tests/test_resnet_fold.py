@@ -4,6 +4,8 @@ epilogues) against a plain fp32 PyTorch Bottleneck (nn.Conv2d + nn.BatchNorm2d) 
 weights: output, input gradient, every parameter gradient, running statistics. A single block is
 well conditioned, so fp16 / bf16 rounding stays at the 1e-2 level (a whole fp16 network at batch 8 on
 64x64 images amplifies rounding through 16 BatchNorm backwards to ~30% in either implementation)."""
+import os
+
 import pytest
 import torch
 
@@ -216,7 +218,16 @@ def _net_two_ranks(rank, world, exchange):
     dist.all_reduce(loss)
     for t in g.values():
         dist.all_reduce(t)
+    dump = os.environ.get("BH_TEST_OPDUMP")  # debugging: per-op checksums of this run, one file per rank
+    if dump:
+        import _oplog
+
+        _oplog.install()
+        _oplog.start()
     loss1, g1, st1 = run(singles[rank], x, y)
+    if dump:
+        os.makedirs(dump, exist_ok=True)
+        _oplog.stop(os.path.join(dump, f"{exchange}_rank{rank}.txt"))
     # the noise floor: the same single-rank step with the two halves of the batch swapped (another
     # summation order). Gradients that downstream BatchNorms nearly cancel (the stem BN's bias) are
     # rounding noise at any order; a world-size factor (the bug class this guards) sits far above it
