@@ -1152,10 +1152,12 @@ void bn_merge_parts(int G, int C, const float* part, float count, const BNFinal&
 }
 
 // the flat chunk-walk apply / data-gradient kernels (k_fwd_flat, k_dgrad_flat) instead of the 2-D
-// channel-owned ones; BH_BN_FLAT=0 restores those. BH_BN_FLAT_BLOCKS caps the grid.
+// channel-owned ones; BH_BN_FLAT=0 restores those. BH_BN_FLAT_BLOCKS caps the grid (bench_hbm_roofline.py
+// at 256x256x56x56: 1024 / 2048 / 4096 / 16384 workgroups -> 5.2 / 5.3-5.4 / 5.4 / 5.6-5.7 TB/s; the
+// 2-D kernels 5.0)
 bool knob_flat() { static const bool v = env_knob("BH_BN_FLAT", 1) != 0; return v; }
 unsigned flat_grid(int64_t chunks) {
-  static const int64_t cap = env_knob("BH_BN_FLAT_BLOCKS", 2048);
+  static const int64_t cap = env_knob("BH_BN_FLAT_BLOCKS", 16384);
   const int64_t need = (chunks + kBlock * kFlatU - 1) / (kBlock * kFlatU);
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, cap));
 }

@@ -84,6 +84,18 @@ template <> struct Mfma<bf16> {
   }
 };
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// sum over the 16 lanes of a DPP row (every lane gets it): quad_perm [1,0,3,2] and [2,3,0,1] sum each
+// quad, row_half_mirror pairs the two quads of each half, row_mirror the two halves (fixed order)
+BH_DEVICE float row16_sum(float x) {
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, false));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x141, 0xF, 0xF, false));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x140, 0xF, 0xF, false));
+  return x;
+}
+
 BH_DEVICE int swz(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4); }
 
 template <int N> BH_DEVICE void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
@@ -601,12 +613,15 @@ __global__ __launch_bounds__(kPPThreads, 1) void k_gemm_pp(Args p) {
   char* img = smem + wave * 16384;
   typedef T t4 __attribute__((ext_vector_type(4)));
   auto img_off = [&](int r, int chunk) { return r * 128 + ((chunk ^ (r & 7)) << 4); };
-  auto put = [&](int mt, int nt, const float (&v)[4]) {
+  auto put_h = [&](int mt, int nt, const t4& o) {
     const int r = mt * 16 + fr;
+    *reinterpret_cast<t4*>(img + img_off(r, nt * 2 + (fq >> 1)) + (fq & 1) * 8) = o;
+  };
+  auto put = [&](int mt, int nt, const float (&v)[4]) {
     t4 o;
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = static_cast<T>(v[j]);
-    *reinterpret_cast<t4*>(img + img_off(r, nt * 2 + (fq >> 1)) + (fq & 1) * 8) = o;
+    put_h(mt, nt, o);
   };
   auto get = [&](int mt, int nt, float (&v)[4]) {
     const int r = mt * 16 + fr;
@@ -685,7 +700,9 @@ __global__ __launch_bounds__(kPPThreads, 1) void k_gemm_pp(Args p) {
       // stats never hold them live across the flush), over the wave's 128 rows (16 row lanes x 8
       // tiles), written to the 64-row slab of row_w (the next slab gets zeros, as the fixed-order
       // partial reduction expects every slab)
-      float s1[4][4] = {}, s2[4][4] = {}, kc[4][4] = {};
+      // (packed fp32: v_pk_add_f32 / v_pk_fma_f32 on column pairs; the epilogue runs while the CU's
+      // matrix cores idle, so its VALU count is step time)
+      f2v s1[4][2] = {}, s2[4][2] = {}, kc[4][2] = {};
       if constexpr (STATS == 1) {
         if (e.kshift) {
 #pragma unroll
@@ -693,7 +710,8 @@ __global__ __launch_bounds__(kPPThreads, 1) void k_gemm_pp(Args p) {
             const int col = col_l + nt * 16;
             if (col < p.N) {
               const float4 kv = *reinterpret_cast<const float4*>(e.kshift + col);
-              kc[nt][0] = kv.x; kc[nt][1] = kv.y; kc[nt][2] = kv.z; kc[nt][3] = kv.w;
+              kc[nt][0] = f2v{kv.x, kv.y};
+              kc[nt][1] = f2v{kv.z, kv.w};
             }
           }
         }
@@ -756,6 +774,7 @@ __global__ __launch_bounds__(kPPThreads, 1) void k_gemm_pp(Args p) {
           __builtin_amdgcn_sched_barrier(0);
         }
       } else {
+        const bool partial = row_w + 128 > p.M;  // wave-uniform: only the last row tile masks rows
 #pragma unroll
         for (int mt = 0; mt < 8; ++mt) {
           const bool row_ok = row_w + mt * 16 + fr < p.M;
@@ -768,13 +787,17 @@ __global__ __launch_bounds__(kPPThreads, 1) void k_gemm_pp(Args p) {
 #pragma unroll
               for (int j = 0; j < 4; ++j) v[j] = act_f(v[j], ACT);
             }
-            put(mt, nt, v);
-            if constexpr (STATS == 1) {
+            t4 o;
 #pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                const float d = row_ok ? to_f<T>(from_f<T>(v[j])) - kc[nt][j] : 0.f;
-                s1[nt][j] += d;
-                s2[nt][j] = fmaf(d, d, s2[nt][j]);
+            for (int j = 0; j < 4; ++j) o[j] = static_cast<T>(v[j]);
+            put_h(mt, nt, o);
+            if constexpr (STATS == 1) {  // statistics of the stored (rounded) values
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                f2v d = f2v{static_cast<float>(o[2 * h]), static_cast<float>(o[2 * h + 1])} - kc[nt][h];
+                if (partial && !row_ok) d = f2v{0.f, 0.f};
+                s1[nt][h] += d;
+                s2[nt][h] = __builtin_elementwise_fma(d, d, s2[nt][h]);
               }
             }
           }
@@ -783,15 +806,14 @@ __global__ __launch_bounds__(kPPThreads, 1) void k_gemm_pp(Args p) {
       }
       flush(Cp, p.ldc);
       if constexpr (STATS == 1) {
+        float r1[4][4], r2[4][4];
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int m = 1; m < 16; m <<= 1) {
-              s1[nt][j] += __shfl_xor(s1[nt][j], m);
-              s2[nt][j] += __shfl_xor(s2[nt][j], m);
-            }
+          for (int j = 0; j < 4; ++j) {
+            r1[nt][j] = row16_sum(s1[nt][j >> 1][j & 1]);
+            r2[nt][j] = row16_sum(s2[nt][j >> 1][j & 1]);
+          }
         const int64_t slabs = ((int64_t)p.M + 63) / 64, slab = row_w / 64;
         if (fr == 0 && row_w < p.M) {
 #pragma unroll
@@ -800,8 +822,8 @@ __global__ __launch_bounds__(kPPThreads, 1) void k_gemm_pp(Args p) {
             if (col >= p.N) continue;
             float* d1 = e.stat_part + slab * p.N + col;
             float* d2 = e.stat_part + (slabs + slab) * p.N + col;
-            *reinterpret_cast<float4*>(d1) = make_float4(s1[nt][0], s1[nt][1], s1[nt][2], s1[nt][3]);
-            *reinterpret_cast<float4*>(d2) = make_float4(s2[nt][0], s2[nt][1], s2[nt][2], s2[nt][3]);
+            *reinterpret_cast<float4*>(d1) = make_float4(r1[nt][0], r1[nt][1], r1[nt][2], r1[nt][3]);
+            *reinterpret_cast<float4*>(d2) = make_float4(r2[nt][0], r2[nt][1], r2[nt][2], r2[nt][3]);
             if (row_w + 64 < p.M) {
               *reinterpret_cast<float4*>(d1 + p.N) = make_float4(0.f, 0.f, 0.f, 0.f);
               *reinterpret_cast<float4*>(d2 + p.N) = make_float4(0.f, 0.f, 0.f, 0.f);
