@@ -457,7 +457,12 @@ bool make_plan(const C1x1Args& a, Plan* pl) {
   const int max_nc = bwd ? (a.R ? 64 : 128) : 256;
   int NC = 0, occ = 0;
   // the widest column slice (A read once per slice) that still leaves two workgroups per CU; else one
-  for (int want_occ = 2; want_occ >= 1 && !NC; --want_occ)
+  // (BH_C1X1_OCC: the resident-workgroup target, an experiment knob; the kernels' registers must allow it)
+  static const int occ_max = [] {
+    const char* e = getenv("BH_C1X1_OCC");
+    return e ? std::max(1, std::min(4, atoi(e))) : 2;
+  }();
+  for (int want_occ = occ_max; want_occ >= 1 && !NC; --want_occ)
     for (int nc : {256, 128, 64})
       if (nc <= max_nc && a.N % nc == 0 &&
           lds_bytes(nc, a.K, pro, bwd, aff, stats, scatter) <= 160 * 1024 / want_occ) {
