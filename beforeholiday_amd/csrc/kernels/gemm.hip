@@ -25,6 +25,7 @@
 #include "bh/device.h"
 #include "bh/gemm_api.h"
 
+#include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
@@ -1044,8 +1045,15 @@ void gemm_nt(int dt, const void* A, int64_t lda, const void* B, int64_t ldb, voi
   const bool pp = pp_ok && pp_epi && (tile_mode == 4 || epi.resid || (tile_mode == 0 && pp_auto));
   if (epi.resid && epi.bwd_act) throw std::runtime_error("gemm_nt: a residual input needs a forward epilogue");
   if (epi.resid && !pp) throw std::runtime_error("gemm_nt: a residual input needs the ping-pong kernel (K % 64 == 0)");
-  const bool big = glds && !pp && (tile_mode == 2 || (tile_mode == 0 && big_wgs >= 256));
+  // (the one-barrier 256x256 kernel only where the ping-pong one is not allowed, never for N <= 128:
+  // 108 vs 62 us for the 200704 x 128 x 512 statistics GEMM of the ResNet-50 step)
+  const bool big = glds && !pp && (tile_mode == 2 || (tile_mode == 0 && big_wgs >= 256 && N > 128));
   const bool mid = glds && tile_mode == 3;
+  static const bool log_shapes = env_mode("BH_GEMM_LOG", 0) != 0;  // debugging: which kernel per shape
+  if (log_shapes)
+    fprintf(stderr, "[gemm_nt] M %lld N %lld K %lld epi %d resid %d -> %s\n", (long long)M, (long long)N,
+            (long long)K, epi.bn_stats, epi.resid != nullptr,
+            pp ? "pingpong" : mid ? "256x128" : big ? "256x256" : glds ? "128x128" : "128x128-regs");
   switch (dt) {
     case kF16:
       if (pp) launch_pp<f16>(a, st);

@@ -832,10 +832,12 @@ def _c1x1_forward_stats(x, weight, kshift, s2):
         return y2d.view(n, ho, wo, k).permute(0, 3, 1, 2), part
     if s2:
         a2d = x[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, c)
-    if _own("fwd") and conv_bn.gemm_bn_supported(a2d, w2d):
+    if _own("fwd") and conv_bn.gemm_bn_supported(a2d, w2d) and not (c <= 256 and k >= 1024):
         # the MFMA-bound layers (K or N >= 512, or the small 14x14 / 7x7 grids): the tiled MFMA GEMM
         # with the statistics epilogue (kernels/gemm.hip; the ping-pong 256x256 kernel from 160 tiles),
-        # no library GEMM and no separate statistics pass (benchmarks/bench_resnet_gemms.py)
+        # no library GEMM and no separate statistics pass (benchmarks/bench_resnet_gemms.py). Not the
+        # K <= 256 -> N >= 1024 expansions (stage-3 conv3): four K-steps, the epilogue dominates the
+        # one-workgroup-per-CU tile (67 vs 57 us for hipBLASLt + the statistics pass in the step)
         y2d, part = conv_bn.gemm_bn(a2d, w2d, "stats", kshift=kshift)
         return y2d.view(n, ho, wo, k).permute(0, 3, 1, 2), part
     y = torch.mm(a2d, w2d.t()).view(n, ho, wo, k).permute(0, 3, 1, 2)
