@@ -196,8 +196,11 @@ bool wgrad_supported(const at::Tensor& x, const at::Tensor& dy, int64_t R, int64
   return bh::conv_wgrad_plan(a, &g);
 }
 
-at::Tensor conv_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t R, int64_t stride,
-                      const c10::optional<at::Tensor>& pro_scale, const c10::optional<at::Tensor>& pro_shift) {
+// defer = true: the split partials are returned instead of summed ([out, ws or None]); the caller sums
+// them with conv_wgrad_reduce (on a side stream: nothing on the critical path waits for them)
+std::vector<at::Tensor> conv_wgrad_impl(const at::Tensor& x, const at::Tensor& dy, int64_t R, int64_t stride,
+                                        const c10::optional<at::Tensor>& pro_scale,
+                                        const c10::optional<at::Tensor>& pro_shift, bool defer) {
   TORCH_CHECK(wgrad_ok(x, dy, R, stride), "conv_wgrad: needs channels_last fp16/bf16 x [N, C, sH, sW], "
                                           "dy [N, K, H, W], C and K % 64 == 0, R in {1, 3}, stride in {1, 2}");
   auto out = at::empty({dy.size(1), x.size(1), R, R}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
@@ -221,8 +224,24 @@ at::Tensor conv_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t R, int6
   const int64_t nws = bh::conv_wgrad_workspace(g, a);
   at::Tensor ws;
   if (nws > 0) ws = at::empty({nws}, x.options().dtype(at::kFloat));
-  bh::conv_wgrad(dtype_code(x.scalar_type()), a, g, nws > 0 ? ws.data_ptr<float>() : nullptr, stream_for(x));
-  return out;
+  bh::conv_wgrad(dtype_code(x.scalar_type()), a, g, nws > 0 ? ws.data_ptr<float>() : nullptr, stream_for(x), !defer);
+  if (!defer || nws == 0) return {out, at::Tensor()};
+  return {out, ws.view({(int64_t)g.parts, -1})};
+}
+
+at::Tensor conv_wgrad(const at::Tensor& x, const at::Tensor& dy, int64_t R, int64_t stride,
+                      const c10::optional<at::Tensor>& pro_scale, const c10::optional<at::Tensor>& pro_shift) {
+  return conv_wgrad_impl(x, dy, R, stride, pro_scale, pro_shift, false)[0];
+}
+
+// out (the [K, C, R, R] gradient conv_wgrad_deferred returned) = sum over the rows of ws [parts, n],
+// on the current stream
+void conv_wgrad_reduce(const at::Tensor& ws, const at::Tensor& out) {
+  TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat && ws.dim() == 2 && ws.is_contiguous() &&
+                  out.is_cuda() && ws.size(1) == out.numel() && ws.size(1) % 4 == 0,
+              "conv_wgrad_reduce: ws [parts, n] fp32 and out with n elements");
+  bh::conv_wgrad_reduce(dtype_code(out.scalar_type()), ws.data_ptr<float>(), out.data_ptr(), ws.size(1),
+                        (int)ws.size(0), stream_for(out));
 }
 
 bool stem_ok(const at::Tensor& x, const at::Tensor& w) {
@@ -399,6 +418,13 @@ void register_conv(pybind11::module_& root) {
         py::arg("pro_scale") = py::none(), py::arg("pro_shift") = py::none(),
         "weight gradient of conv2d(x', w, stride, padding=(R-1)//2), R in {1, 3}, stride in {1, 2}, x' = x or "
         "relu(x * pro_scale + pro_shift) per channel: [K, C, R, R] channels_last");
+  m.def("conv_wgrad_deferred", [](const at::Tensor& x, const at::Tensor& dy, int64_t R, int64_t stride,
+                                  const c10::optional<at::Tensor>& ps, const c10::optional<at::Tensor>& ph) {
+    return conv_wgrad_impl(x, dy, R, stride, ps, ph, true);
+  }, py::arg("x"), py::arg("grad_out"), py::arg("R"), py::arg("stride") = 1, py::arg("pro_scale") = py::none(),
+        py::arg("pro_shift") = py::none(),
+        "conv_wgrad without the split-partials sum: [out (not yet written when ws is returned), ws [parts, n] or None]");
+  m.def("conv_wgrad_reduce", &conv_wgrad_reduce, py::arg("ws"), py::arg("out"));
   m.def("wgrad_supported", &wgrad_supported, py::arg("x"), py::arg("grad_out"), py::arg("R"), py::arg("stride") = 1);
   m.def("gemm_n64", &gemm_n64, py::arg("a"), py::arg("b"), py::arg("resid") = c10::nullopt,
         "a [M, K] . b[64, K]^T (+ resid [M, 64]), K in {64, 128, 256}, M % 32 == 0 (kernels/gemm_n64.hip)");

@@ -73,7 +73,10 @@ struct ConvWgradGeo {
 bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo);
 // fp32 elements of split partials the launch needs (0: the kernel writes `out` directly)
 int64_t conv_wgrad_workspace(const ConvWgradGeo& g, const ConvWgradArgs& a);
-void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws, hipStream_t st);
+// reduce = false: only the partials kernel; conv_wgrad_reduce then sums the g.parts split partials
+// of ws into a.out (possibly on another stream: the weight gradient is off the critical path)
+void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws, hipStream_t st, bool reduce = true);
+void conv_wgrad_reduce(int dt, const float* ws, void* out, int64_t n, int parts, hipStream_t st);
 
 // ResNet stem forward (kernels/conv_stem.hip): 7x7 / stride 2 / pad 3, C = 3 -> K = 64, 224x224 NHWC
 // x [N, 224, 224, 3], w [64, 7, 7, 3], y [N, 112, 112, 64]

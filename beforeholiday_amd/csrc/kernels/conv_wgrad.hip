@@ -521,7 +521,7 @@ int64_t conv_wgrad_workspace(const ConvWgradGeo& g, const ConvWgradArgs& a) {
   return g.parts > 1 ? (int64_t)g.parts * a.K * a.C * a.R * a.R : 0;
 }
 
-void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws, hipStream_t st) {
+void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws, hipStream_t st, bool reduce) {
   const int64_t n = (int64_t)a.K * a.C * a.R * a.R;
   ConvWgradArgs b = a;
   if (a.R == 1) {  // flat pixel list: windows are the rows of an [nwin, 1, 112] image
@@ -553,7 +553,7 @@ void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws
     };
     if (a.pro_scale) pick(std::true_type{});
     else pick(std::false_type{});
-    if (g.parts > 1)
+    if (g.parts > 1 && reduce)
       hipLaunchKernelGGL(k_wgrad_reduce<T>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, ws, out, n, g.parts);
   };
   switch (dt) {
@@ -563,6 +563,18 @@ void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("conv_wgrad: ") + hipGetErrorString(e));
+}
+
+void conv_wgrad_reduce(int dt, const float* ws, void* out, int64_t n, int parts, hipStream_t st) {
+  if (parts <= 1) return;
+  const dim3 grid((unsigned)((n + 63) / 64));
+  switch (dt) {
+    case kF16: hipLaunchKernelGGL(k_wgrad_reduce<f16>, grid, dim3(256), 0, st, ws, (f16*)out, n, parts); break;
+    case kBF16: hipLaunchKernelGGL(k_wgrad_reduce<bf16>, grid, dim3(256), 0, st, ws, (bf16*)out, n, parts); break;
+    default: throw std::runtime_error("conv_wgrad_reduce: fp16 / bf16 only");
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("conv_wgrad_reduce: ") + hipGetErrorString(e));
 }
 
 }  // namespace bh

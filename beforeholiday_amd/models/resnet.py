@@ -119,6 +119,54 @@ def _like(g, weight):
     return g if g.stride() == weight.stride() else g.contiguous()
 
 
+# Opt-in (BH_WGRAD_REDUCE_SIDE=1): the split partials of the MFMA weight-gradient kernels summed on the
+# side stream (one rank, a leaf parameter without a .grad or hooks, a layout the parameter already has),
+# so the ~50 small reduce launches per ResNet-50 step could overlap the next data-gradient kernels; the
+# compute stream joins at the end of the backward pass. Same-box A/B: 10595 / 10418 img/s with it vs
+# 10813 / 10836 without (profiles/resnet50_wgrad_reduce_side_ab.txt): the concurrent reduces slow the
+# critical-path kernels more than their own launches cost
+_WGRAD_REDUCE_SIDE = os.environ.get("BH_WGRAD_REDUCE_SIDE", "0") == "1"
+
+
+def _reduce_side_ok(weight, x):
+    if not (_WGRAD_REDUCE_SIDE and x.is_cuda and weight is not None and weight.is_leaf and weight.grad is None):
+        return False
+    # a gradient hook (DDP's bucket copy, user hooks) would read it on the compute stream right away
+    if getattr(weight, "_post_accumulate_grad_hooks", None) or getattr(weight, "_backward_hooks", None):
+        return False
+    import torch.distributed as dist
+
+    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+
+
+def _conv_wgrad(x, gy, r, weight, scale=None, shift=None, stride=1):
+    """``ops.conv.conv_wgrad`` in ``weight``'s layout, with the split-partials sum on the side stream
+    where :func:`_reduce_side_ok` allows it."""
+    from ..ops import conv as bhconv
+
+    if not (_reduce_side_ok(weight, x) and bhconv.wgrad_supported(x, gy, r, stride)):
+        return _like(bhconv.conv_wgrad(x, gy, r, scale, shift, stride=stride), weight)
+    out, ws = bhconv.conv_wgrad_deferred(x, gy, r, scale, shift, stride=stride)
+    if ws is None:
+        return _like(out, weight)
+    if out.stride() != weight.stride():  # a layout copy would read it on the compute stream
+        bhconv.conv_wgrad_reduce(ws, out)
+        return out.contiguous()
+    dev = x.device
+    main = torch.cuda.current_stream(dev)
+    side = _SIDE.get(dev.index)
+    if side is None:
+        side = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        bhconv.conv_wgrad_reduce(ws, out)
+    ws.record_stream(side)
+    if dev.index not in _JOIN_QUEUED:
+        _JOIN_QUEUED.add(dev.index)
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: _join(dev))
+    return out
+
+
 # per-shape choice of the 1x1 / stride-1 convolution paths: {(N, Cin, H, W, Cout, dtype, dir): "gemm" | "miopen"}
 _CONV1X1_CHOICE = {}
 
@@ -180,10 +228,7 @@ def _wgrad(x, gy, weight, r, mode, miopen_fn):
     how = _pick((n, c, h, w, gy.size(1), x.dtype, f"wgrad{r}"), lambda: bhconv.conv_wgrad(x, gy, r), miopen_fn, mode)
     if how != "gemm":
         return miopen_fn()
-    gw = bhconv.conv_wgrad(x, gy, r)  # channels_last [K, C, r, r]
-    if gw.stride() != weight.stride():  # match the parameter's layout (a contiguous-format weight)
-        gw = gw.contiguous()
-    return gw
+    return _conv_wgrad(x, gy, r, weight)  # in the parameter's layout
 
 
 class _GradStash(torch.autograd.Function):
@@ -761,8 +806,8 @@ class _Conv1x1BNFn(torch.autograd.Function):
 
         def wfn():
             if ctx.s2:
-                return _like(bhconv.conv_wgrad_s2(x, gy) if bhconv.wgrad_supported(x, gy, 1, 2) else
-                             conv_bwd(gy, x, weight, None, *args, [False, True, False])[1], weight)
+                return (_conv_wgrad(x, gy, 1, weight, stride=2) if bhconv.wgrad_supported(x, gy, 1, 2) else
+                        _like(conv_bwd(gy, x, weight, None, *args, [False, True, False])[1], weight))
             # the MFMA wgrad kernel wins every ResNet-50 1x1 shape (profiles/conv_wgrad_vs_miopen.jsonl):
             # no per-shape timing (it would JIT-compile MIOpen's solver on the first step)
             return _wgrad(x, gy, weight, 1, "gemm", lambda: conv_bwd(gy, x, weight, None, *args,
@@ -885,8 +930,8 @@ class _Conv1DsFn(torch.autograd.Function):
         def wdfn():
             if ctx.s2:
                 a2 = ([2, 2], [0, 0], [1, 1], False, [0, 0], 1)
-                return _like(bhconv.conv_wgrad_s2(x, gyd) if bhconv.wgrad_supported(x, gyd, 1, 2) else
-                             conv_bwd(gyd, x, wd, None, *a2, [False, True, False])[1], wd)
+                return (_conv_wgrad(x, gyd, 1, wd, stride=2) if bhconv.wgrad_supported(x, gyd, 1, 2) else
+                        _like(conv_bwd(gyd, x, wd, None, *a2, [False, True, False])[1], wd))
             return _wgrad(x, gyd, wd, 1, "gemm", lambda: conv_bwd(gyd, x, wd, None, *a1, [False, True, False])[1])
 
         side1 = ctx.needs_input_grad[1] and _side_ok(ctx.wparams[0], x)
@@ -1043,7 +1088,7 @@ class _BNConvFn(torch.autograd.Function):
         gy = gy.contiguous(memory_format=torch.channels_last)
         n, C, h, w = y.shape
         sums = None
-        wfn = lambda: _like(bhconv.conv_wgrad(y, gy, ctx.R, scale, shift, stride=ctx.stride), conv_w)  # noqa: E731
+        wfn = lambda: _conv_wgrad(y, gy, ctx.R, conv_w, scale, shift, stride=ctx.stride)  # noqa: E731
         side = ctx.needs_input_grad[10] and _side_ok(ctx.wparam, y)
         g_conv = _on_side(wfn, y, gy, scale, shift) if side else None
         if ctx.R == 3 and ctx.stride == 2:

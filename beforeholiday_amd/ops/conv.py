@@ -97,6 +97,20 @@ def conv3x3_s2_dgrad(dy: torch.Tensor, w: torch.Tensor, hw) -> torch.Tensor:
                                                [True, False, False])[0]
 
 
+def conv_wgrad_deferred(x: torch.Tensor, dy: torch.Tensor, r: int, pro_scale: torch.Tensor = None,
+                        pro_shift: torch.Tensor = None, stride: int = 1):
+    """:func:`conv_wgrad` on the MFMA kernel without its split-partials sum: ``(out, ws)``. With ``ws``
+    not None, ``out`` is written only by :func:`conv_wgrad_reduce` ``(ws, out)`` -- which may run on
+    another stream (models/resnet.py sums them on a side stream: nothing on the critical path waits
+    for a weight gradient). Only for shapes :func:`wgrad_supported` covers."""
+    out, ws = submodule("conv_cuda").conv_wgrad_deferred(x, dy, r, stride, pro_scale, pro_shift)
+    return out, ws
+
+
+def conv_wgrad_reduce(ws: torch.Tensor, out: torch.Tensor) -> None:
+    submodule("conv_cuda").conv_wgrad_reduce(ws, out)
+
+
 def conv_wgrad(x: torch.Tensor, dy: torch.Tensor, r: int, pro_scale: torch.Tensor = None,
                pro_shift: torch.Tensor = None, stride: int = 1) -> torch.Tensor:
     """Weight gradient of ``conv2d(x', w, stride, padding=(r-1)//2)`` for r in {1, 3}, where x' is x or,
