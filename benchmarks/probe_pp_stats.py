@@ -1,3 +1,5 @@
+"""Kernel-time probe for rocprofv3 (scripts/prof_one.sh): the ping-pong GEMM (tile mode 4) with and
+without its BatchNorm-statistics epilogue at two ResNet-50 1x1 shapes, 10 launches each."""
 import os, sys, torch
 sys.path.insert(0, os.getcwd())
 from beforeholiday_amd._native import submodule
