@@ -138,6 +138,33 @@ def mlp_backward(use_bias: int, activation: int, grad_o, outputs, inputs) -> Lis
     return grads
 
 
+# the MFMA weight-gradient kernel (kernels/conv_wgrad.hip, tokens as a 1 x 1 x M image) beats the library
+# GEMM on the transposed-operand product dW = dY^T . X when the weight has at most ~2.2M elements and
+# there are >= 4096 tokens: 1.05-2.4x at 512^2 - 2048 x 1024, 0.8x from 3072 x 1024 up
+# (profiles/wgrad_transformer_shapes.jsonl). A static shape rule: every rank runs the same kernel.
+_WGRAD_MAX_ELEMS = 2048 * 1088
+_WGRAD_MIN_TOKENS = 4096
+_WGRAD_MFMA = __import__("os").environ.get("BH_DENSE_WGRAD", "1") != "0"  # A/B switch
+
+
+def weight_grad(d_output: torch.Tensor, input: torch.Tensor) -> torch.Tensor:
+    """``d_output^T @ input`` for 2-D ``[tokens, out]`` / ``[tokens, in]`` tensors: the dense layers'
+    weight gradient ``[out, in]`` in ``d_output``'s dtype."""
+    M, K = d_output.shape
+    C = input.size(1)
+    if (_WGRAD_MFMA and d_output.is_cuda and d_output.dtype in (torch.float16, torch.bfloat16)
+            and input.dtype == d_output.dtype
+            and M >= _WGRAD_MIN_TOKENS and K * C <= _WGRAD_MAX_ELEMS and d_output.is_contiguous()
+            and input.is_contiguous()):
+        from . import conv as _conv
+
+        x4 = input.view(1, 1, M, C).permute(0, 3, 1, 2)
+        dy4 = d_output.view(1, 1, M, K).permute(0, 3, 1, 2)
+        if _conv.wgrad_supported(x4, dy4, 1):
+            return submodule("conv_cuda").conv_wgrad(x4, dy4, 1, 1).view(K, C)
+    return d_output.t().matmul(input)
+
+
 def wgrad_gemm_accum_fp32(input, d_output, main_grad):
     """main_grad (fp32) += d_output^T @ input, accumulated in fp32 in place."""
     if input.is_cuda:

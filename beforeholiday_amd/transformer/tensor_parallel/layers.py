@@ -18,6 +18,7 @@ from torch.nn.parameter import Parameter
 
 from ..._autocast_utils import _cast_if_autocast_enabled
 from ...ops.fused_dense import bias_grad as _bias_grad
+from ...ops.fused_dense import weight_grad as _weight_grad
 from ..parallel_state import (get_tensor_model_parallel_group, get_tensor_model_parallel_rank,
                               get_tensor_model_parallel_world_size)
 from ..utils import divide
@@ -172,7 +173,7 @@ class LinearWithGradAccumulationAndAsyncCommunication(torch.autograd.Function):
             _wgrad_accumulate(total_input_2d, grad_output_2d, weight.main_grad, ctx.use_16bit_in_wgrad_accum_fusion)
             grad_weight = None
         else:
-            grad_weight = grad_output_2d.t().matmul(total_input_2d)
+            grad_weight = _weight_grad(grad_output_2d, total_input_2d)
         grad_bias = _bias_grad(grad_output_2d) if ctx.use_bias else None
         if comm is not None:
             comm.wait()

@@ -227,3 +227,23 @@ def test_bias_dropout_add_seeds_give_unrelated_masks():
     agree = (b1 == b2).float().mean().item()
     assert abs(agree - 0.5) < 0.01, agree
     assert abs(b1.float().mean().item() - 0.5) < 0.01
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("MKC", [(8192, 1024, 1024), (4096, 768, 3072), (8192, 512, 512), (8192, 3072, 1024),
+                                 (1000, 256, 256)])
+def test_weight_grad_matches_fp32(MKC, dt):
+    """ops.fused_dense.weight_grad: dY^T . X on the MFMA weight-gradient kernel where the static shape
+    rule takes it (<= ~2.2M weight elements, >= 4096 tokens), the library GEMM otherwise."""
+    from beforeholiday_amd.ops import fused_dense as fd
+
+    M, K, C = MKC
+    torch.manual_seed(0)
+    dy = torch.randn(M, K, device="cuda").to(dt)
+    x = torch.randn(M, C, device="cuda").to(dt)
+    got = fd.weight_grad(dy, x)
+    ref = dy.float().t() @ x.float()
+    assert got.shape == (K, C) and got.dtype == dt
+    torch.testing.assert_close(got.float(), ref, rtol=2e-2, atol=2e-2 * M ** 0.5 / 8)
+    assert torch.equal(fd.weight_grad(dy, x), got)  # fixed reduction order
