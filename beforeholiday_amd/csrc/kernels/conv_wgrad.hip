@@ -130,7 +130,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
   constexpr int KW = WIDE ? 4 : 2;  // k sub-tiles of 32 KT across the waves
   static_assert(!WIDE || (R == 1 && KT == 2), "wide tiles: 1x1, two 32-row sub-tiles per wave");
   constexpr int DSL = WIDE ? 576 : dslot<KT>(), TK = 32 * KT * KW;  // dY slot bytes, output channels per workgroup
-  constexpr int XSL = dslot<CT>(), TC = kTile * CT;  // X slot bytes, input channels per workgroup
+  // X slot bytes (CT = 4, the 256 x 256 wide tile: 512 + 64 B, 144 dwords like the wide dY slot), input
+  // channels per workgroup
+  constexpr int XSL = CT == 4 ? 576 : dslot<CT>(), TC = kTile * CT;
   constexpr int BUFX = (XS * XSL + 1023) / 1024 * 1024, BUF = BUFX + (DS * DSL + 1023) / 1024 * 1024;
   constexpr int XP = BUFX / 1024, DP = (BUF - BUFX) / 1024;  // 1-KiB LDS-DMA pieces
   constexpr int XPW = (XP + 7) / 8, DPW = (DP + 7) / 8;  // pieces per wave
@@ -504,6 +506,15 @@ bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo) {
   // 14- / 7-wide windows (measured 1.1x there; the 28-wide instantiation spills and is slower)
   g.kt = (a.K % 128 == 0 && (a.R == 1 || g.G4 == 4 || g.G4 == 2)) ? 2 : 1;
   g.ct = (a.R == 1 && a.C % 128 == 0) ? 2 : 1;  // 1x1: 128 input channels per workgroup where C allows
+  // 256 x 256 wide tiles (each wave 64 x 128: eight MFMA tiles per k-step on six fragments instead of
+  // four on four -- a quarter fewer LDS bytes per MFMA, and twice the MFMA work per window against its
+  // fixed staging cost) where K, C % 256 and at least 32 such tiles remain (the large transformer
+  // weight gradients); BH_WGRAD_WIDE2=0 keeps 256 x 128
+  static const bool wide2_env = [] {
+    const char* e = getenv("BH_WGRAD_WIDE2");
+    return !(e && atoi(e) == 0);
+  }();
+  if (g.wide && wide2_env && a.C % 256 == 0 && (a.K / 256) * (a.C / 256) >= 32) g.ct = 4;
   g.ctiles = a.C / (kTile * g.ct);
   g.tiles = (a.K / (kTile * g.kt * (g.wide ? 2 : 1))) * g.ctiles;
   // one round of workgroups (one per CU), split over the windows
@@ -536,7 +547,8 @@ void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws
     auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3(g.grid), dim3(kThreads), 0, st, b, g, ws, out); };
     auto pick = [&](auto proc) {
       constexpr bool P = decltype(proc)::value;
-      if (a.R == 1 && g.wide) go(k_conv_wgrad<T, 1, 16, 1, 2, 2, P, true>);
+      if (a.R == 1 && g.wide && g.ct == 4) go(k_conv_wgrad<T, 1, 16, 1, 2, 4, P, true>);
+      else if (a.R == 1 && g.wide) go(k_conv_wgrad<T, 1, 16, 1, 2, 2, P, true>);
       else if (a.R == 1) {
         if (g.ct == 2) g.kt == 2 ? go(k_conv_wgrad<T, 1, 28, 1, 2, 2, P>) : go(k_conv_wgrad<T, 1, 28, 1, 1, 2, P>);
         else g.kt == 2 ? go(k_conv_wgrad<T, 1, 28, 1, 2, 1, P>) : go(k_conv_wgrad<T, 1, 28, 1, 1, 1, P>);

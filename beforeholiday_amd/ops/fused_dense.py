@@ -139,10 +139,11 @@ def mlp_backward(use_bias: int, activation: int, grad_o, outputs, inputs) -> Lis
 
 
 # the MFMA weight-gradient kernel (kernels/conv_wgrad.hip, tokens as a 1 x 1 x M image) beats the library
-# GEMM on the transposed-operand product dW = dY^T . X when the weight has at most ~2.2M elements and
-# there are >= 4096 tokens: 1.05-2.4x at 512^2 - 2048 x 1024, 0.8x from 3072 x 1024 up
-# (profiles/wgrad_transformer_shapes.jsonl). A static shape rule: every rank runs the same kernel.
-_WGRAD_MAX_ELEMS = 2048 * 1088
+# GEMM on the transposed-operand product dW = dY^T . X when the weight has at most ~2.4M elements and
+# there are >= 4096 tokens: 1.05-2.4x at 512^2 - 3072 x 768, parity at 3072 x 1024, 0.88x at 4096 x 1024
+# (profiles/wgrad_transformer_shapes.jsonl, with the 256 x 256 wide tiles). A static shape rule: every
+# rank runs the same kernel.
+_WGRAD_MAX_ELEMS = 3072 * 800
 _WGRAD_MIN_TOKENS = 4096
 _WGRAD_MFMA = __import__("os").environ.get("BH_DENSE_WGRAD", "1") != "0"  # A/B switch
 

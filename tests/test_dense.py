@@ -247,3 +247,21 @@ def test_weight_grad_matches_fp32(MKC, dt):
     assert got.shape == (K, C) and got.dtype == dt
     torch.testing.assert_close(got.float(), ref, rtol=2e-2, atol=2e-2 * M ** 0.5 / 8)
     assert torch.equal(fd.weight_grad(dy, x), got)  # fixed reduction order
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("MKC", [(4096, 2048, 1024), (8192, 3072, 1024), (2048, 1024, 4096)])
+def test_wgrad_kernel_wide_256x256_tiles(MKC):
+    """The 1x1 weight-gradient kernel's 256 x 256 tiles (K, C % 256 and >= 32 tiles: the large
+    transformer weights) on the [tokens, channels] views, against the fp32 product."""
+    from beforeholiday_amd.ops import conv as bhconv
+
+    M, K, C = MKC
+    torch.manual_seed(1)
+    dy = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    x = torch.randn(M, C, device="cuda").to(torch.bfloat16)
+    x4, dy4 = x.view(1, 1, M, C).permute(0, 3, 1, 2), dy.view(1, 1, M, K).permute(0, 3, 1, 2)
+    assert bhconv.wgrad_supported(x4, dy4, 1)
+    got = bhconv.conv_wgrad(x4, dy4, 1).view(K, C).float()
+    ref = dy.float().t() @ x.float()
+    assert float((got - ref).norm() / ref.norm()) < 4e-3
