@@ -77,10 +77,11 @@ def main():
     per = collections.defaultdict(list)
     for s_, e_, name in last:
         per[re.sub(r"\(.*", "", name.replace("(anonymous namespace)::", ""))[:110]].append(round((e_ - s_) / 1e3, 1))
-    lines.append("\n## per-launch us (last step, launch order) for kernels > 0.5 ms/step\n")
+    lines.append("\n## per-launch us (last step, launch order) for kernels > 0.5 ms/step (and PROF_LIST matches)\n")
+    extra = re.compile(os.environ["PROF_LIST"]) if os.environ.get("PROF_LIST") else None
     for k, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0]):
-        if t / n / 1e6 < 0.5:
-            break
+        if t / n / 1e6 < 0.5 and not (extra and extra.search(k)):
+            continue
         lines.append(f"* `{k[:60]}`: {per[k]}")
     # neighbours of library helper kernels (fills, copies) in the last step: which op launched them
     helpers = re.compile(os.environ.get("PROF_NEIGHBOURS", r"SubTensorOp|copyBuffer|fillBuffer"))
