@@ -116,10 +116,11 @@ class FusedSelfAttnFn(torch.autograd.Function):
     """qkv [s, B*heads, 3, 64] (the QKV projection output, viewed) -> context [s, B*heads, 64].
     Backward writes d(qkv) in the same layout, so the projection's dgrad / wgrad GEMMs consume it
     without any gather of separate dq / dk / dv tensors. ``fill`` is the value of a masked score
-    (-inf: MHA semantics, a fully masked row gives zeros; -10000: Megatron semantics)."""
+    (-inf: MHA semantics, a fully masked row gives zeros; -10000: Megatron semantics). ``bits``:
+    the mode-4 mask packed once by ``flash_mask_bits`` (shared by every layer of a forward)."""
 
     @staticmethod
-    def forward(ctx, qkv, heads, scale, mask, mask_mode, p, training, fill=float("-inf")):
+    def forward(ctx, qkv, heads, scale, mask, mask_mode, p, training, fill=float("-inf"), bits=None):
         seed = _seed()
         fa = submodule("fused_attention")
         q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
@@ -128,16 +129,16 @@ class FusedSelfAttnFn(torch.autograd.Function):
             out = fa.forward(q, k, v, mask_mode, mask, heads, scale, p, training, seed)
             lse = torch.empty(0)
         else:
-            out, lse = fa.flash_forward(q, k, v, mask_mode, mask, heads, scale, p, training, seed, fill)
+            out, lse = fa.flash_forward(q, k, v, mask_mode, mask, heads, scale, p, training, seed, fill, bits)
         ctx.save_for_backward(qkv, mask if mask is not None else torch.empty(0), out if not short else torch.empty(0),
-                              lse)
-        ctx.args = (heads, scale, mask_mode, p, training, seed, mask is not None, fill, short)
+                              lse, bits if bits is not None else torch.empty(0))
+        ctx.args = (heads, scale, mask_mode, p, training, seed, mask is not None, fill, short, bits is not None)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        qkv, mask, out, lse = ctx.saved_tensors
-        heads, scale, mask_mode, p, training, seed, has_mask, fill, short = ctx.args
+        qkv, mask, out, lse, bits = ctx.saved_tensors
+        heads, scale, mask_mode, p, training, seed, has_mask, fill, short, has_bits = ctx.args
         dqkv = torch.empty_like(qkv)
         fa = submodule("fused_attention")
         q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
@@ -147,8 +148,8 @@ class FusedSelfAttnFn(torch.autograd.Function):
                         dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2])
         else:
             fa.flash_backward(dout.contiguous(), q, k, v, out, lse, mask_mode, m, heads, scale, p, training, seed,
-                              fill, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2])
-        return dqkv, None, None, None, None, None, None, None
+                              fill, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2], bits if has_bits else None)
+        return dqkv, None, None, None, None, None, None, None, None
 
 
 class FusedEncdecAttnFn(torch.autograd.Function):

@@ -373,12 +373,63 @@ void attn_bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, int mas
 
 void register_contrib_impl(pybind11::module_& root);
 
+// mode 4 on the 32x32 flash kernels: the uint8 mask packed to bits, [bits | bits_t] in one int32
+// tensor (AttnArgs::mbits / mbits_t). ``pre`` = the packing done once by flash_mask_bits (a BERT
+// forward shares one mask over all layers); otherwise packed here. BH_FLASH_M4_WIDE=0: the 16-wide
+// kernels read the bytes instead.
+bool m4_wide() {
+  static const bool wide = [] {
+    const char* e = getenv("BH_FLASH_M4_WIDE");
+    return !(e && e[0] == '0');
+  }();
+  return wide;
+}
+
+void attach_mask_bits(bh::AttnArgs& a, const at::Tensor& q, const c10::optional<at::Tensor>& pre, at::Tensor& mb) {
+  if (a.mask_mode != 4 || !m4_wide()) return;
+  const int64_t B = a.BH / a.heads;
+  const int64_t nb = B * a.sq * ((a.sk + 31) / 32), nbt = B * a.sk * ((a.sq + 31) / 32);
+  if (pre.has_value() && pre->defined()) {
+    check_cuda(*pre, "mask bits");
+    TORCH_CHECK(pre->scalar_type() == at::kInt && pre->is_contiguous() && pre->numel() == nb + nbt,
+                "flash: mask bits must be the int32 [", nb + nbt, "] tensor of flash_mask_bits for this shape");
+    mb = *pre;
+  } else {
+    mb = at::empty({nb + nbt}, q.options().dtype(at::kInt));
+    auto* w = reinterpret_cast<uint32_t*>(mb.data_ptr());
+    bh::flash_mask_bits(a, w, w + nb, stream_for(q));
+  }
+  a.mbits = reinterpret_cast<const uint32_t*>(mb.data_ptr());
+  a.mbits_t = a.mbits + nb;
+}
+
+// mask [B, sq, sk] (bool / uint8) -> the packed bits for flash_forward / flash_backward (mode 4)
+at::Tensor flash_mask_bits_op(at::Tensor mask) {
+  check_cuda(mask, "mask");
+  TORCH_CHECK(mask.dim() == 3, "flash_mask_bits: mask must be [B, sq, sk]");
+  auto m = mask.to(at::kByte).contiguous();
+  bh::AttnArgs a;
+  a.mask_mode = 4;
+  a.mask = m.data_ptr();
+  a.heads = 1;
+  a.BH = (int)m.size(0);
+  a.sq = (int)m.size(1);
+  a.sk = (int)m.size(2);
+  const int64_t nb = (int64_t)a.BH * a.sq * ((a.sk + 31) / 32), nbt = (int64_t)a.BH * a.sk * ((a.sq + 31) / 32);
+  auto mb = at::empty({nb + nbt}, m.options().dtype(at::kInt));
+  auto* w = reinterpret_cast<uint32_t*>(mb.data_ptr());
+  bh::flash_mask_bits(a, w, w + nb, stream_for(m));
+  return mb;
+}
+
 std::vector<at::Tensor> flash_fwd(at::Tensor q, at::Tensor k, at::Tensor v, int mask_mode,
                                   c10::optional<at::Tensor> mask, int64_t heads, double scale, double p, bool training,
-                                  int64_t seed, double mask_fill) {
+                                  int64_t seed, double mask_fill, c10::optional<at::Tensor> bits) {
   at::Tensor mk;
   auto a = attn_args(q, k, v, mask_mode, mask, heads, scale, p, training, seed, mk, /*flash=*/true);
   a.mask_fill = (float)mask_fill;
+  at::Tensor mb;
+  attach_mask_bits(a, q, bits, mb);
   auto o = at::empty({q.size(0), q.size(1), 64}, q.options());
   auto lse = at::empty({q.size(1), q.size(0)}, q.options().dtype(at::kFloat));
   a.o = o.data_ptr(); a.o_st = o.stride(0); a.o_sbh = o.stride(1);
@@ -389,10 +440,12 @@ std::vector<at::Tensor> flash_fwd(at::Tensor q, at::Tensor k, at::Tensor v, int 
 
 void flash_bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse, int mask_mode,
                c10::optional<at::Tensor> mask, int64_t heads, double scale, double p, bool training, int64_t seed,
-               double mask_fill, at::Tensor dq, at::Tensor dk, at::Tensor dv) {
+               double mask_fill, at::Tensor dq, at::Tensor dk, at::Tensor dv, c10::optional<at::Tensor> bits) {
   at::Tensor mk;
   auto a = attn_args(q, k, v, mask_mode, mask, heads, scale, p, training, seed, mk, /*flash=*/true);
   a.mask_fill = (float)mask_fill;
+  at::Tensor mb;
+  attach_mask_bits(a, q, bits, mb);
   attn_check(dout, "dout");
   attn_check(o, "o");
   attn_check(dq, "dq");
@@ -420,8 +473,15 @@ void register_contrib(pybind11::module_& root) {
   fa.def("forward", &attn_fwd);
   fa.def("backward", &attn_bwd);
   fa.def("max_sk", &bh::attn_max_sk);
-  fa.def("flash_forward", &flash_fwd, "any-length attention forward -> (o, lse)");
-  fa.def("flash_backward", &flash_bwd, "any-length attention backward into dq / dk / dv");
+  namespace py = pybind11;
+  fa.def("flash_forward", &flash_fwd, "any-length attention forward -> (o, lse)", py::arg("q"), py::arg("k"),
+         py::arg("v"), py::arg("mask_mode"), py::arg("mask"), py::arg("heads"), py::arg("scale"), py::arg("p"),
+         py::arg("training"), py::arg("seed"), py::arg("mask_fill"), py::arg("bits") = py::none());
+  fa.def("flash_backward", &flash_bwd, "any-length attention backward into dq / dk / dv", py::arg("dout"),
+         py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("lse"), py::arg("mask_mode"),
+         py::arg("mask"), py::arg("heads"), py::arg("scale"), py::arg("p"), py::arg("training"), py::arg("seed"),
+         py::arg("mask_fill"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("bits") = py::none());
+  fa.def("flash_mask_bits", &flash_mask_bits_op, "mode-4 mask [B, sq, sk] -> packed bits for the flash kernels");
 }
 
 namespace {

@@ -40,6 +40,10 @@ struct AttnArgs {
   // flash
   float* lse = nullptr;          // [BH, sq]
   const float* delta = nullptr;  // [BH, sq]
+  // mode 4 as bits for the 32x32 flash kernels (flash_mask_bits): mbits [B, sq, ceil(sk/32)] words
+  // over keys (bit j of word w = key 32w+j), mbits_t [B, sk, ceil(sq/32)] words over queries
+  const uint32_t* mbits = nullptr;
+  const uint32_t* mbits_t = nullptr;
 };
 
 int attn_max_sk();
@@ -49,5 +53,7 @@ void flash_forward(int dt, const AttnArgs& a, hipStream_t st);          // needs
 // delta[bh, q] = sum_d dout * o  (o given in a.o / a.o_st / a.o_sbh, dout in a.dout)
 void flash_delta(int dt, const AttnArgs& a, float* delta, hipStream_t st);
 void flash_backward(int dt, const AttnArgs& a, hipStream_t st);         // needs a.lse, a.delta
+// packs the mode-4 uint8 mask a.mask into bits (see AttnArgs::mbits); bits_t may be null
+void flash_mask_bits(const AttnArgs& a, uint32_t* bits, uint32_t* bits_t, hipStream_t st);
 
 }  // namespace bh

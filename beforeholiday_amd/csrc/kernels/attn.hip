@@ -825,6 +825,14 @@ BH_DEVICE float half_pair(float x, bool sum) {
   return sum ? a + b : fmaxf(a, b);
 }
 
+// mode-4 mask words of a 32x32 tile (AttnArgs::mbits / mbits_t): word t covers rows 32t.. of the
+// 64-row block at r0; shifted right by 4h so that register i tests bit (i&3) + 8(i>>2)
+BH_DEVICE void mask_words(uint32_t (&w)[2], const uint32_t* row, int r0, int n, int h) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t) w[t] = r0 + 32 * t < n ? row[(r0 >> 5) + t] >> (4 * h) : 0u;
+}
+BH_DEVICE bool reg_bit(uint32_t w, int i) { return (w >> ((i & 3) + 8 * (i >> 2))) & 1u; }
+
 // attn.hip is built with -fno-honor-nans (no canonicalising v_max in front of every fmaxf of an
 // MFMA result: the max trees below become pure v_max3_f32) and -fno-slp-vectorize (adjacent f32
 // adds are not packed into v_pk_add_f32, which co-issues badly beside MFMAs); see _build.py.
@@ -869,6 +877,10 @@ __global__ __launch_bounds__(kThreads, 3) void k_flash_fwd32(AttnArgs a) {
   const float kscale = a.p_drop < 1.f ? 1.f / (1.f - a.p_drop) : 0.f;
   const uint32_t thresh = keep_thresh(a.p_drop);
   const uint32_t rowh = DROP ? row_hash(a, bh, myq) : 0u;
+  // mode 4: this query's key bits; a masked raw score becomes mask_fill / scale (= mask_fill scaled)
+  const uint32_t* mrow = MODE == 4 ? a.mbits + ((int64_t)(bh / a.heads) * a.sq + min(myq, a.sq - 1)) * ((a.sk + 31) >> 5)
+                                   : nullptr;
+  const float fillraw = a.mask_fill / a.scale;
   float m = -INFINITY, l = 0.f;  // running base-2 max (shared by both halves), this half's sum
   f16v O[2];                      // O^T: dims 32dn + (i&3) + 8(i>>2) + 4h, query myq
 #pragma unroll
@@ -895,6 +907,8 @@ __global__ __launch_bounds__(kThreads, 3) void k_flash_fwd32(AttnArgs a) {
       vs.load(rv, kb + kKB, a.sk, tid);
     }
     if (MODE != 5 || kb <= q_last) {  // wave-uniform: a causal block past every query of the wave is skipped
+      uint32_t mw[2] = {0u, 0u};
+      if (MODE == 4) mask_words(mw, mrow, kb, a.sk, h);
       // all LDS reads of the block up front (K row fragments, then V^T fragments): the MFMAs then
       // wait on the first reads only and the V reads land under QK^T and the softmax
       i4v kf[2][4], vf[2][2][2];
@@ -932,6 +946,13 @@ __global__ __launch_bounds__(kThreads, 3) void k_flash_fwd32(AttnArgs a) {
 #pragma unroll
           for (int i = 0; i < 16; ++i)
             if (32 * t + (i & 3) + 8 * (i >> 2) > lim) S[t][i] = -INFINITY;
+      }
+      if (MODE == 4 && __any((mw[0] | mw[1]) != 0u)) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (reg_bit(mw[t], i)) S[t][i] = fillraw;
       }
       const float mx = half_pair(tree_max(S), false) * c;
       if (__any(mx > m + 8.f)) {
@@ -1000,7 +1021,7 @@ __global__ __launch_bounds__(kThreads, 3) void k_flash_fwd32(AttnArgs a) {
   }
 }
 
-// dQ, 32x32x16 form (mask modes 0 / 5). Same layout as k_flash_fwd32 (query on the lane): S^T =
+// dQ, 32x32x16 form (mask modes 0 / 4 / 5). Same layout as k_flash_fwd32 (query on the lane): S^T =
 // K.Q^T and dP^T = V.dO^T from K / V row fragments, P^T rebuilt from the saved LSE in base 2,
 // dS^T = P^T (dP^T - delta) stays in registers and feeds dQ^T = K^T.dS^T (K^T by transposed reads
 // of the same K image); the softmax scale is applied once to dQ in the epilogue.
@@ -1033,6 +1054,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_flash_dq32(AttnArgs a) {
   const float kscale = a.p_drop < 1.f ? 1.f / (1.f - a.p_drop) : 0.f;
   const uint32_t thresh = keep_thresh(a.p_drop);
   const uint32_t rowh = DROP ? row_hash(a, bh, myq) : 0u;
+  // mode 4: a masked score's gradient is zero (masked_fill), so its P is dropped to 0 here
+  const uint32_t* mrow = MODE == 4 ? a.mbits + ((int64_t)(bh / a.heads) * a.sq + qr) * ((a.sk + 31) >> 5) : nullptr;
   f16v acc[2];
 #pragma unroll
   for (int dn = 0; dn < 2; ++dn)
@@ -1057,6 +1080,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_flash_dq32(AttnArgs a) {
       vs.load(rv, kb + kKB, a.sk, tid);
     }
     if (MODE != 5 || kb <= q_last) {
+      uint32_t mw[2] = {0u, 0u};
+      if (MODE == 4) mask_words(mw, mrow, kb, a.sk, h);
       f16v S[2], P[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -1089,6 +1114,13 @@ __global__ __launch_bounds__(kThreads, 2) void k_flash_dq32(AttnArgs a) {
 #pragma unroll
           for (int i = 0; i < 16; ++i)
             if (32 * t + (i & 3) + 8 * (i >> 2) > lim) S[t][i] = -INFINITY;
+      }
+      if (MODE == 4 && __any((mw[0] | mw[1]) != 0u)) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (reg_bit(mw[t], i)) S[t][i] = -INFINITY;
       }
       // dS'^T = P^T (dP^T_dropped - delta), into P (scale applied in the epilogue)
 #pragma unroll
@@ -1136,7 +1168,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_flash_dq32(AttnArgs a) {
   }
 }
 
-// dK / dV, 32x32x16 form (mask modes 0 / 5). Workgroup = 4 waves x 32 keys, key on the lane: S =
+// dK / dV, 32x32x16 form (mask modes 0 / 4 / 5). Workgroup = 4 waves x 32 keys, key on the lane: S =
 // Q.K^T and dP = dO.V^T per 32-query tile (A = Q / dO row fragments from LDS, B = K / V fragments
 // held in registers), P from the per-query base-2 LSE row constants, and P_dropped / dS feed dV^T
 // = dO^T.P and dK^T = Q^T.dS straight from the accumulators (dO^T, Q^T by transposed reads of the
@@ -1170,6 +1202,11 @@ __global__ __launch_bounds__(kThreads, 2) void k_flash_dkdv32(AttnArgs a) {
   const float c = a.scale * 1.4426950408889634f;
   const float kscale = a.p_drop < 1.f ? 1.f / (1.f - a.p_drop) : 0.f;
   const uint32_t thresh = keep_thresh(a.p_drop);
+  // mode 4: this key's query bits; a masked score is mask_fill (P keeps it: dV) with dS = 0
+  const uint32_t* mcol = MODE == 4 ? a.mbits_t + ((int64_t)(bh / a.heads) * a.sk + min(mykey, a.sk - 1)) *
+                                                     ((a.sq + 31) >> 5)
+                                   : nullptr;
+  const float fillraw = a.mask_fill / a.scale;
   f16v dK[2], dV[2];  // dims 32dn + (i&3) + 8(i>>2) + 4h, key mykey
 #pragma unroll
   for (int dn = 0; dn < 2; ++dn)
@@ -1218,6 +1255,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_flash_dkdv32(AttnArgs a) {
     const uint32_t* rhp = reinterpret_cast<const uint32_t*>(dlp + kQB);
     if (iq + 1 < nqb) load_blk(q0 + kQB);
     if (MODE != 5 || q0 + kQB - 1 >= k0w) {  // wave-uniform: some query of the block sees a key of the wave
+      uint32_t mw[2] = {0u, 0u};
+      if (MODE == 4) mask_words(mw, mcol, q0, a.sq, h);
       f16v S[2], P[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -1255,15 +1294,16 @@ __global__ __launch_bounds__(kThreads, 2) void k_flash_dkdv32(AttnArgs a) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int i = 4 * g + j;
-            const float p = __builtin_amdgcn_exp2f(fmaf(S[t][i], c, n4[j]));
+            const bool mk = MODE == 4 && reg_bit(mw[t], i);  // mode 4: score mask_fill, dS 0
+            const float p = __builtin_amdgcn_exp2f(fmaf(mk ? fillraw : S[t][i], c, n4[j]));
             if (DROP) {
               const bool kp = keep_elem((uint32_t)r4[j], mykey, thresh);
               const float kk = kp ? kscale : 0.f;
-              S[t][i] = p * kk;                     // P dropped
-              P[t][i] = p * (P[t][i] * kk - d4[j]);  // dS'
+              S[t][i] = p * kk;                                // P dropped
+              P[t][i] = mk ? 0.f : p * (P[t][i] * kk - d4[j]);  // dS'
             } else {
               S[t][i] = p;
-              P[t][i] = p * (P[t][i] - d4[j]);
+              P[t][i] = mk ? 0.f : p * (P[t][i] - d4[j]);
             }
           }
         }
@@ -1559,7 +1599,48 @@ inline void check_launch(const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// mode-4 mask bits. bits: one thread per word (row r = b*sq + q, word w), 32 bytes of the row.
+__global__ __launch_bounds__(256) void k_mask_bits(const uint8_t* __restrict__ m, uint32_t* __restrict__ bits,
+                                                   int64_t rows, int sk) {
+  const int mw = (sk + 31) >> 5;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * mw) return;
+  const int64_t r = i / mw;
+  const int w = (int)(i - r * mw), n = min(32, sk - 32 * w);
+  const uint8_t* p = m + r * sk + 32 * w;
+  uint32_t v = 0u;
+  for (int j = 0; j < n; ++j) v |= (p[j] != 0 ? 1u : 0u) << j;
+  bits[i] = v;
+}
+// bits_t: word (b, k, w) over queries 32w..; thread order (b, w, k) so a wave reads consecutive keys
+__global__ __launch_bounds__(256) void k_mask_bits_t(const uint8_t* __restrict__ m, uint32_t* __restrict__ bits_t,
+                                                     int B, int sq, int sk) {
+  const int mw = (sq + 31) >> 5;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)B * mw * sk) return;
+  const int k = (int)(i % sk);
+  const int64_t bw = i / sk;
+  const int w = (int)(bw % mw), b = (int)(bw / mw), n = min(32, sq - 32 * w);
+  const uint8_t* p = m + ((int64_t)b * sq + 32 * w) * sk + k;
+  uint32_t v = 0u;
+  for (int j = 0; j < n; ++j) v |= (p[(int64_t)j * sk] != 0 ? 1u : 0u) << j;
+  bits_t[((int64_t)b * sk + k) * mw + w] = v;
+}
+
 }  // namespace
+
+void flash_mask_bits(const AttnArgs& a, uint32_t* bits, uint32_t* bits_t, hipStream_t st) {
+  if (a.mask_mode != 4 || !a.mask) throw std::runtime_error("flash_mask_bits: needs a mode-4 mask");
+  const int B = a.BH / a.heads;
+  const auto* m = reinterpret_cast<const uint8_t*>(a.mask);
+  const int64_t nw = (int64_t)B * a.sq * ((a.sk + 31) >> 5);
+  if (bits) hipLaunchKernelGGL(k_mask_bits, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, m, bits,
+                               (int64_t)B * a.sq, a.sk);
+  const int64_t nt = (int64_t)B * a.sk * ((a.sq + 31) >> 5);
+  if (bits_t) hipLaunchKernelGGL(k_mask_bits_t, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, m, bits_t, B,
+                                 a.sq, a.sk);
+  check_launch("flash_mask_bits");
+}
 
 int attn_max_sk() { return 128; }
 
@@ -1601,12 +1682,12 @@ void flash_forward(int dt, const AttnArgs& a, hipStream_t st) {
     const char* e = getenv("BH_FLASH_FWD16");
     return e && e[0] == '1';
   }();
-  if (!legacy && (a.mask_mode == 0 || a.mask_mode == 5)) {
+  if (!legacy && (a.mask_mode == 0 || a.mask_mode == 5 || (a.mask_mode == 4 && a.mbits))) {
     const dim3 grid((unsigned)((a.sq + kFQ - 1) / kFQ), (unsigned)a.BH);
     flash_dispatch(dt, a.mask_mode, "flash_forward", [&](auto tt, auto mm) {
       using T = typename decltype(tt)::type;
       constexpr int M = decltype(mm)::value;
-      if constexpr (M == 0 || M == 5) {
+      if constexpr (M == 0 || M == 4 || M == 5) {
         if (a.training && a.p_drop > 0.f) hipLaunchKernelGGL((k_flash_fwd32<T, M, true>), grid, dim3(kThreads), 0, st, a);
         else hipLaunchKernelGGL((k_flash_fwd32<T, M, false>), grid, dim3(kThreads), 0, st, a);
       }
@@ -1639,14 +1720,14 @@ void flash_backward(int dt, const AttnArgs& a, hipStream_t st) {
     const char* e = getenv("BH_FLASH_BWD16");
     return e && e[0] == '1';
   }();
-  if (!legacy && (a.mask_mode == 0 || a.mask_mode == 5)) {
+  if (!legacy && (a.mask_mode == 0 || a.mask_mode == 5 || (a.mask_mode == 4 && a.mbits && a.mbits_t))) {
     const dim3 gq((unsigned)((a.sq + kFQ - 1) / kFQ), (unsigned)a.BH);
     const dim3 gk((unsigned)((a.sk + kFQ - 1) / kFQ), (unsigned)a.BH);
     const bool dr = a.training && a.p_drop > 0.f;
     flash_dispatch(dt, a.mask_mode, "flash_backward", [&](auto tt, auto mm) {
       using T = typename decltype(tt)::type;
       constexpr int M = decltype(mm)::value;
-      if constexpr (M == 0 || M == 5) {
+      if constexpr (M == 0 || M == 4 || M == 5) {
         if (dr) {
           hipLaunchKernelGGL((k_flash_dkdv32<T, M, true>), gk, dim3(kThreads), 0, st, a);
           hipLaunchKernelGGL((k_flash_dq32<T, M, true>), gq, dim3(kThreads), 0, st, a);

@@ -86,6 +86,21 @@ def attention_mask_func(attention_scores: torch.Tensor, attention_mask: torch.Te
     return attention_scores.masked_fill_(attention_mask, -10000.0)
 
 
+def _flash_mask(attention_mask, b, sq):
+    """The padding mask of the flash path once per forward, not once per layer: the [b, sq, sq]
+    uint8 copy and its packed bits (fused_attention.flash_mask_bits) are cached on the mask tensor
+    that every layer receives (invalidated by an in-place change of it)."""
+    hit = getattr(attention_mask, "_bh_flash_mask", None)
+    if hit is not None and hit[0] == attention_mask._version and hit[1].shape == (b, sq, sq):
+        return hit[1], hit[2]
+    from .._native import submodule
+
+    mask = attention_mask.expand(b, 1, sq, sq).reshape(b, sq, sq).to(torch.uint8).contiguous()
+    bits = submodule("fused_attention").flash_mask_bits(mask)
+    attention_mask._bh_flash_mask = (attention_mask._version, mask, bits)
+    return mask, bits
+
+
 def _device(config=None):
     if (config is not None and config.use_cpu_initialization) or not torch.cuda.is_available():
         return torch.device("cpu")
@@ -293,13 +308,13 @@ class CoreAttention(MegatronModule):
             mode, mask, fill = MASK_CAUSAL, None, float("-inf")
         elif attention_mask is not None:
             mode, fill = MASK_FULL, -10000.0
-            mask = attention_mask.expand(b, 1, sq, sq).reshape(b, sq, sq)
+            mask, bits = _flash_mask(attention_mask, b, sq)
         else:
             mode, mask, fill = MASK_NONE, None, float("-inf")
         p = self.attention_dropout.p if self.training else 0.0
         ctx = FusedSelfAttnFn.apply(qkv, self.num_attention_heads_per_partition,
                                     1.0 / math.sqrt(self.hidden_size_per_attention_head), mask, mode, p,
-                                    self.training, fill)
+                                    self.training, fill, bits if mode == MASK_FULL else None)
         return ctx.view(sq, b, self.hidden_size_per_partition)
 
     def forward(self, query, key, value, attention_mask):

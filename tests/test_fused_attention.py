@@ -227,3 +227,31 @@ def test_flash_dropout_regenerated(dtype):
     _fa().flash_backward(dout, q, k, eye, o, lse, 0, None, heads, 0.125, p, True, 99, float("-inf"), dq, dk, dv)
     for got, want in ((dq, qf.grad), (dk, kf.grad), (dv, vf.grad)):
         torch.testing.assert_close(got.float(), want, rtol=tol, atol=tol * 2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("sq", [200, 64])
+def test_flash_dropout_full_mask(dtype, sq):
+    """Mask mode 4 (BERT's [B, sq, sk] padding mask, fill -10000) with dropout: the keep mask is
+    recovered through V = I as above; masked scores have P = 0 except the fully masked row (uniform),
+    whose gradient must still be blocked by the mask."""
+    sk, B, heads, p = 64, 2, 2, 0.2
+    BH = B * heads
+    g = torch.Generator(device="cuda").manual_seed(13)
+    q = torch.randn(sq, BH, 64, device="cuda", dtype=dtype, generator=g)
+    k = torch.randn(sk, BH, 64, device="cuda", dtype=dtype, generator=g)
+    mask = torch.rand(B, sq, sk, device="cuda", generator=g) < 0.25
+    mask[1, 3, :] = True
+    eye = torch.eye(64, device="cuda", dtype=dtype).unsqueeze(1).expand(64, BH, 64).contiguous()
+    o, lse = _fa().flash_forward(q, k, eye, 4, mask, heads, 0.125, p, True, 7, -10000.0)
+    keep = (o.float() != 0).permute(1, 0, 2).float()
+    qf, kf, vf = (t.float().requires_grad_(True) for t in (q, k, eye))
+    ref = _reference_full(qf, kf, vf, 0.125, 4, mask, heads, -10000.0, keep=keep, p=p)
+    tol = 2e-2 if dtype == torch.float16 else 5e-2
+    torch.testing.assert_close(o.float(), ref, rtol=tol, atol=tol)
+    dout = torch.randn_like(o)
+    ref.backward(dout.float())
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(eye)
+    _fa().flash_backward(dout, q, k, eye, o, lse, 4, mask, heads, 0.125, p, True, 7, -10000.0, dq, dk, dv)
+    for got, want in ((dq, qf.grad), (dk, kf.grad), (dv, vf.grad)):
+        torch.testing.assert_close(got.float(), want, rtol=tol, atol=tol * 2)

@@ -141,6 +141,8 @@ def _gpt_pp(rank, world):
 
 
 def test_gpt_pipeline_parallel_matches_single_rank():
+    if torch.cuda.is_available():
+        pytest.skip("CPU (gloo) rehearsal: build_model places stages on the GPU when one is visible")
     run_distributed(_gpt_pp, 2)
 
 
