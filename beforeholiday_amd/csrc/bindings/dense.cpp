@@ -390,6 +390,30 @@ std::vector<at::Tensor> act_backward_py(at::Tensor dy, at::Tensor aux, int act, 
 
 }  // namespace
 
+namespace {
+// embedding weight gradient without torch's host read-back of the segment count (kernels/dense.hip)
+at::Tensor embedding_bwd(at::Tensor dy, at::Tensor ids, int64_t num_weights, int64_t padding_idx) {
+  check_cuda(dy, "dy");
+  check_cuda(ids, "ids");
+  const int64_t H = dy.size(-1);
+  auto d2 = dy.reshape({-1, H}).contiguous();
+  auto flat = ids.reshape({-1}).to(at::kLong);
+  TORCH_CHECK(flat.numel() == d2.size(0), "embedding_backward: ", flat.numel(), " ids for ", d2.size(0), " rows");
+  TORCH_CHECK(H > 0 && H <= INT32_MAX, "embedding_backward: bad hidden size");
+  auto sp = at::sort(flat, /*stable=*/true, 0, false);
+  const at::Tensor& sorted = std::get<0>(sp);
+  const at::Tensor& perm = std::get<1>(sp);
+  auto dw = at::zeros({num_weights, H}, dy.options());
+  const int64_t n = d2.size(0);
+  if (n == 0) return dw;
+  auto piece = at::empty({n, H}, dy.options().dtype(at::kFloat));
+  bh::embedding_backward(dtype_code(dy.scalar_type()), sorted.data_ptr<int64_t>(), perm.data_ptr<int64_t>(),
+                         d2.data_ptr(), piece.data_ptr<float>(), dw.data_ptr(), n, (int)H, padding_idx,
+                         stream_for(dy));
+  return dw;
+}
+}  // namespace
+
 void register_dense(pybind11::module_& root) {
   namespace py = pybind11;
   auto fd = root.def_submodule("fused_dense_cuda", "GEMM + bias / GELU dense layers");
@@ -399,6 +423,8 @@ void register_dense(pybind11::module_& root) {
   fd.def("linear_gelu_linear_backward", &linear_gelu_linear_backward);
   fd.def("act_forward", &act_forward_py, py::arg("x"), py::arg("bias"), py::arg("act"));
   fd.def("act_backward", &act_backward_py, py::arg("dy"), py::arg("aux"), py::arg("act"), py::arg("want_bgrad"));
+  fd.def("embedding_backward", &embedding_bwd, py::arg("dy"), py::arg("ids"), py::arg("num_weights"),
+         py::arg("padding_idx") = -1, "deterministic embedding weight gradient [num_weights, H], no host sync");
   fd.def("bias_grad", [](at::Tensor dy) {
     check_cuda(dy, "dy");
     return bias_grad(dy.contiguous());

@@ -31,4 +31,9 @@ void dense_dropout_backward(int dt, const void* dy, const uint8_t* keep, float k
 bool gemm_n64_supported(int64_t M, int K, int N);
 void gemm_n64(int dt, const void* a, const void* b, const void* resid, void* c, int64_t M, int K, hipStream_t st);
 
+// embedding weight gradient dw[V, H] (zero-filled by the caller) from dy[n, H] and the stably sorted
+// token ids + permutation; piece = fp32 [n, H] scratch. Deterministic, no host synchronisation.
+void embedding_backward(int dt, const int64_t* sorted, const int64_t* perm, const void* dy, float* piece, void* dw,
+                        int64_t n, int H, int64_t padding_idx, hipStream_t st);
+
 }  // namespace bh

@@ -194,6 +194,58 @@ __global__ __launch_bounds__(64 * kColsumLanes) void k_colsum_finalize(const flo
   colsum_partials_block<T>(part, splits, N, out, sh);
 }
 
+
+// ---- embedding weight gradient: deterministic, no host synchronisation (torch's embedding backward
+// reads its segment count back to the host every call). Token ids come sorted (stable) with their
+// permutation; sorted positions are cut into chunks of kEmbChunk. Pass 1: one workgroup per (chunk,
+// column slab) sums each run-piece of equal ids inside its chunk in order and stores the fp32 sum at
+// the piece's first position. Pass 2: the first position of every run adds its pieces (the run start,
+// then each chunk boundary the run crosses) in order and writes the weight-gradient row. Rows of ids
+// that never occur keep the zero fill; padding_idx rows stay zero.
+constexpr int kEmbChunk = 32;
+constexpr int kEmbCols = 512;  // columns per workgroup: 256 threads x 2
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_embed_pieces(const int64_t* __restrict__ sorted, const int64_t* __restrict__ perm,
+                                                      const T* __restrict__ dy, float* __restrict__ piece, int64_t n,
+                                                      int H) {
+  const int64_t p0 = (int64_t)blockIdx.x * kEmbChunk;
+  const int c = blockIdx.y * kEmbCols + threadIdx.x * 2;
+  if (c >= H) return;
+  const int64_t pe = min(n, p0 + kEmbChunk);
+  float a0 = 0.f, a1 = 0.f;
+  int64_t start = p0;
+  for (int64_t p = p0; p < pe; ++p) {
+    const T* r = dy + perm[p] * (int64_t)H + c;
+    a0 += to_f<T>(r[0]);
+    if (c + 1 < H) a1 += to_f<T>(r[1]);
+    if (p + 1 == pe || sorted[p + 1] != sorted[p]) {
+      float* o = piece + start * (int64_t)H + c;
+      o[0] = a0;
+      if (c + 1 < H) o[1] = a1;
+      a0 = a1 = 0.f;
+      start = p + 1;
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_embed_runs(const int64_t* __restrict__ sorted, const float* __restrict__ piece,
+                                                    T* __restrict__ dw, int64_t n, int H, int64_t pad) {
+  const int64_t i = blockIdx.x;
+  const int64_t id = sorted[i];
+  if ((i > 0 && sorted[i - 1] == id) || id == pad) return;
+  const int c = blockIdx.y * kEmbCols + threadIdx.x * 2;
+  if (c >= H) return;
+  float a0 = piece[i * H + c], a1 = c + 1 < H ? piece[i * H + c + 1] : 0.f;
+  for (int64_t j = (i / kEmbChunk + 1) * kEmbChunk; j < n && sorted[j] == id; j += kEmbChunk) {
+    a0 += piece[j * H + c];
+    if (c + 1 < H) a1 += piece[j * H + c + 1];
+  }
+  dw[id * H + c] = from_f<T>(a0);
+  if (c + 1 < H) dw[id * H + c + 1] = from_f<T>(a1);
+}
+
 }  // namespace
 
 void dense_act_forward(int dt, const void* x, const void* bias, void* y, int64_t M, int N, int act, bool vec,
@@ -264,6 +316,19 @@ void dense_dropout_backward(int dt, const void* dy, const uint8_t* keep, float k
                            part, splits, N, (T*)bgrad);
         check_launch("dense_dropout_bgrad_finalize");
       });
+}
+
+void embedding_backward(int dt, const int64_t* sorted, const int64_t* perm, const void* dy, float* piece, void* dw,
+                        int64_t n, int H, int64_t padding_idx, hipStream_t st) {
+  if (n <= 0) return;
+  const unsigned slabs = (unsigned)((H + kEmbCols - 1) / kEmbCols);
+  DN_DISPATCH(dt, T, {
+    hipLaunchKernelGGL((k_embed_pieces<T>), dim3((unsigned)((n + kEmbChunk - 1) / kEmbChunk), slabs), dim3(256), 0,
+                       st, sorted, perm, (const T*)dy, piece, n, H);
+    hipLaunchKernelGGL((k_embed_runs<T>), dim3((unsigned)n, slabs), dim3(256), 0, st, sorted, piece, (T*)dw, n, H,
+                       padding_idx);
+  });
+  check_launch("embedding_backward");
 }
 
 }  // namespace bh

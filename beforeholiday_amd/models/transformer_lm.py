@@ -535,10 +535,10 @@ class Embedding(MegatronModule):
         self.embedding_dropout = torch.nn.Dropout(config.hidden_dropout)
 
     def forward(self, input_ids, position_ids, tokentype_ids=None):
-        emb = self.word_embeddings(input_ids) + self.position_embeddings(position_ids)
+        emb = self.word_embeddings(input_ids) + _fd.embedding(position_ids, self.position_embeddings.weight)
         if tokentype_ids is not None:
             assert self.tokentype_embeddings is not None
-            emb = emb + self.tokentype_embeddings(tokentype_ids)
+            emb = emb + _fd.embedding(tokentype_ids, self.tokentype_embeddings.weight)
         emb = emb.transpose(0, 1).contiguous()
         if self.fp32_residual_connection:
             emb = emb.float()

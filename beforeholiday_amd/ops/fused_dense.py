@@ -234,3 +234,32 @@ def bias_dropout_add(x: torch.Tensor, bias: Optional[torch.Tensor], residual: to
     else:
         out = F.dropout(x + bias if bias is not None else x, p=prob, training=training)
     return residual + out
+
+
+class _EmbeddingFn(torch.autograd.Function):
+    """F.embedding with the weight gradient from kernels/dense.hip (embedding_backward): stable sort of
+    the ids, ordered per-id sums in fp32, no host synchronisation (torch's CUDA embedding backward
+    reads its segment count back every call, which stalls the launch queue once per step)."""
+
+    @staticmethod
+    def forward(ctx, ids, weight, padding_idx):
+        ctx.save_for_backward(ids)
+        ctx.meta = (weight.size(0), -1 if padding_idx is None else int(padding_idx))
+        return F.embedding(ids, weight, padding_idx)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (ids,) = ctx.saved_tensors
+        v, pad = ctx.meta
+        return None, _fd().embedding_backward(dy, ids, v, pad), None
+
+
+def embedding(ids: torch.Tensor, weight: torch.Tensor, padding_idx: Optional[int] = None) -> torch.Tensor:
+    """``F.embedding(ids, weight, padding_idx)``; on the GPU (fp32 / fp16 / bf16 weights that need a
+    gradient) the backward runs the deterministic sync-free kernel above."""
+    if (weight.is_cuda and weight.requires_grad and torch.is_grad_enabled()
+            and weight.dtype in (torch.float32, torch.float16, torch.bfloat16)):
+        if padding_idx is not None and padding_idx < 0:
+            padding_idx += weight.size(0)
+        return _EmbeddingFn.apply(ids, weight, padding_idx)
+    return F.embedding(ids, weight, padding_idx)

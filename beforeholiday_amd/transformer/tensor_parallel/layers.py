@@ -119,8 +119,13 @@ class VocabParallelEmbedding(torch.nn.Module):
             masked_input = (input_ - self.vocab_start_index).masked_fill_(input_mask, 0)
         else:
             masked_input = input_
-        output_parallel = F.embedding(masked_input, self.weight, self.padding_idx, self.max_norm, self.norm_type,
-                                      self.scale_grad_by_freq, self.sparse)
+        if self.max_norm is None and not self.scale_grad_by_freq and not self.sparse:
+            from ...ops import fused_dense as _fd
+
+            output_parallel = _fd.embedding(masked_input, self.weight, self.padding_idx)
+        else:
+            output_parallel = F.embedding(masked_input, self.weight, self.padding_idx, self.max_norm, self.norm_type,
+                                          self.scale_grad_by_freq, self.sparse)
         if self.tensor_model_parallel_size > 1:
             output_parallel = output_parallel.masked_fill(input_mask.unsqueeze(-1), 0.0)
         return reduce_from_tensor_model_parallel_region(output_parallel)

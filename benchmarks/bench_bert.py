@@ -97,6 +97,18 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if os.environ.get("BH_SYNC_DEBUG") == "1":  # report every host-synchronising op of the timed steps
+        import traceback
+        import warnings
+
+        def _show(msg, *a, **k):
+            print("SYNC:", msg, "".join(traceback.format_stack(limit=10)[:-2]), flush=True)
+        warnings.showwarning = _show
+        if os.environ.get("BH_SYNC_DEBUG_ERROR") == "1":  # raise at the first one, with the forward stack
+            torch.autograd.set_detect_anomaly(True, check_nan=False)
+            torch.cuda.set_sync_debug_mode("error")
+            step()
+        torch.cuda.set_sync_debug_mode("warn")
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()

@@ -265,3 +265,31 @@ def test_wgrad_kernel_wide_256x256_tiles(MKC):
     got = bhconv.conv_wgrad(x4, dy4, 1).view(K, C).float()
     ref = dy.float().t() @ x.float()
     assert float((got - ref).norm() / ref.norm()) < 4e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("V,H,n,pad", [(30592, 1024, 8192, None), (2, 1024, 8192, None), (512, 1000, 4100, 3),
+                                       (64, 7, 333, None)])
+def test_embedding_backward_matches_fp32(dtype, V, H, n, pad):
+    """ops.fused_dense.embedding: forward = F.embedding, weight gradient = fp32 index_add reference
+    (runs far longer than one sort chunk when V is small), padding row zero, bitwise repeatable."""
+    from beforeholiday_amd.ops import fused_dense as fd
+
+    g = torch.Generator(device="cuda").manual_seed(V + H + n)
+    ids = torch.randint(0, V, (n,), device="cuda", generator=g).view(-1, 1) if n % 2 else \
+        torch.randint(0, V, (n // 2, 2), device="cuda", generator=g)
+    w = (torch.randn(V, H, device="cuda", generator=g) * 0.1).to(dtype).requires_grad_(True)
+    out = fd.embedding(ids, w, pad)
+    torch.testing.assert_close(out, F.embedding(ids, w.detach(), pad), rtol=0, atol=0)
+    dy = torch.randn(out.shape, device="cuda", generator=g).to(dtype)
+    out.backward(dy)
+    ref = torch.zeros(V, H, device="cuda").index_add_(0, ids.reshape(-1), dy.reshape(-1, H).float())
+    if pad is not None:
+        ref[pad] = 0
+    tol = 1e-5 if dtype == torch.float32 else (1e-2 if dtype == torch.float16 else 4e-2)
+    torch.testing.assert_close(w.grad.float(), ref, rtol=tol, atol=tol * max(1.0, (n / V) ** 0.5))
+    g1 = w.grad.clone()
+    w.grad = None
+    fd.embedding(ids, w, pad).backward(dy)
+    assert torch.equal(w.grad, g1)
