@@ -165,7 +165,9 @@ class _FusedGeluMLP(torch.autograd.Function):
         x2d, pre, inter, w1, w2 = ctx.saved_tensors
         dy2d = dy.reshape(-1, dy.size(-1)).contiguous()
         dw2 = _fd.weight_grad(dy2d, inter)
-        dpre, db1 = submodule("gemm").linear_dact(dy2d, w2.t().contiguous(), pre, _fd.ACT_GELU, True)
+        gm = submodule("gemm")
+        w2t = gm.transpose(w2) if w2.size(0) % 8 == 0 and w2.size(1) % 8 == 0 else w2.t().contiguous()
+        dpre, db1 = gm.linear_dact(dy2d, w2t, pre, _fd.ACT_GELU, True)
         dw1 = _fd.weight_grad(dpre, x2d)
         dx = torch.mm(dpre, w1).view(ctx.in_shape)
         return dx, dw1, db1, dw2
