@@ -97,6 +97,38 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if os.environ.get("BH_HOST_PROFILE") == "1":  # CPU-side op profile: a blocking op has a long self time
+        from torch.profiler import ProfilerActivity, profile
+        torch.cuda.synchronize()
+        with profile(activities=[ProfilerActivity.CPU]) as prof:
+            for _ in range(3):
+                step()
+        if rank == 0:
+            print(prof.key_averages().table(sort_by="self_cpu_time_total", row_limit=25), flush=True)
+    if os.environ.get("BH_HOST_TIMING") == "1":  # host-side time per phase (a sync shows as a long phase)
+        import collections
+        acc = collections.defaultdict(float)
+        torch.cuda.synchronize()
+        for _ in range(5):
+            t = [time.perf_counter()]
+            lm_loss, nsp_logits = model(tokens, mask, tokentype_ids=types, lm_labels=labels)
+            t.append(time.perf_counter())
+            loss = (lm_loss.float() * loss_mask).sum() / loss_mask.sum() + F.cross_entropy(nsp_logits.float(), nsp)
+            t.append(time.perf_counter())
+            with amp.scale_loss(loss, opt) as scaled:
+                scaled.backward()
+                t.append(time.perf_counter())
+            t.append(time.perf_counter())
+            opt.step()
+            t.append(time.perf_counter())
+            opt.zero_grad()
+            t.append(time.perf_counter())
+            torch.cuda.synchronize()
+            t.append(time.perf_counter())
+            for k, name in enumerate(["forward", "loss", "backward", "amp_exit", "opt_step", "zero_grad", "gpu_drain"]):
+                acc[name] += (t[k + 1] - t[k]) * 1e3 / 5
+        if rank == 0:
+            print(json.dumps({"host_ms": {k: round(v, 3) for k, v in acc.items()}}), flush=True)
     if os.environ.get("BH_SYNC_DEBUG") == "1":  # report every host-synchronising op of the timed steps
         import traceback
         import warnings
