@@ -4,6 +4,7 @@ GPU tensors run ``beforeholiday_amd._C`` (GEMMs on hipBLASLt via ATen, activatio
 bias-grad passes in kernels/dense.hip); CPU tensors run the PyTorch reference below with the same
 semantics (exact-erf GELU; ReLU / sigmoid derivatives taken from the activation output).
 """
+import os
 from typing import List, Optional
 
 import torch
@@ -236,6 +237,9 @@ def bias_dropout_add(x: torch.Tensor, bias: Optional[torch.Tensor], residual: to
     return residual + out
 
 
+_EMBED_NATIVE = os.environ.get("BH_EMBED_NATIVE", "1") != "0"  # 0: torch's embedding backward (A/B)
+
+
 class _EmbeddingFn(torch.autograd.Function):
     """F.embedding with the weight gradient from kernels/dense.hip (embedding_backward): stable sort of
     the ids, ordered per-id sums in fp32, no host synchronisation (torch's CUDA embedding backward
@@ -258,7 +262,7 @@ def embedding(ids: torch.Tensor, weight: torch.Tensor, padding_idx: Optional[int
     """``F.embedding(ids, weight, padding_idx)``; on the GPU (fp32 / fp16 / bf16 weights that need a
     gradient) the backward runs the deterministic sync-free kernel above."""
     if (weight.is_cuda and weight.requires_grad and torch.is_grad_enabled()
-            and weight.dtype in (torch.float32, torch.float16, torch.bfloat16)):
+            and weight.dtype in (torch.float32, torch.float16, torch.bfloat16) and _EMBED_NATIVE):
         if padding_idx is not None and padding_idx < 0:
             padding_idx += weight.size(0)
         return _EmbeddingFn.apply(ids, weight, padding_idx)
