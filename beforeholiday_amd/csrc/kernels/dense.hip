@@ -146,6 +146,28 @@ __global__ __launch_bounds__(256) void k_act_bwd(const T* __restrict__ dy, const
           if (dx) VecIO<T>::store(dx + (r + u * kRowLanes) * N + col0, g[u]);
         }
       }
+    } else if (vec && col0 + 8 <= N && keep && act == kActNone) {
+      // dropout backward + bias gradient (Megatron's bias-dropout-add): the same four rows in flight,
+      // with their keep bytes (same per-row order of the sums as the one-row loop below)
+      for (; r + 3 * kRowLanes < r1; r += 4 * kRowLanes) {
+        float g[4][8];
+        uint32_t bits[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t off = (r + u * kRowLanes) * N + col0;
+          VecIO<T>::load(dy + off, g[u]);
+          bits[u] = keep[off >> 3];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            g[u][k] = ((bits[u] >> k) & 1u) ? g[u][k] * keep_scale : 0.f;
+            acc[k] += g[u][k];
+          }
+          if (dx) VecIO<T>::store(dx + (r + u * kRowLanes) * N + col0, g[u]);
+        }
+      }
     }
     for (; r < r1; r += kRowLanes) {
       const int64_t off = r * N + col0;
@@ -262,7 +284,8 @@ void dense_act_forward(int dt, const void* x, const void* bias, void* y, int64_t
 int dense_bgrad_splits(int64_t M, int N) {
   const int64_t col_blocks = (N + kCols - 1) / kCols;
   int64_t splits = (2048 + col_blocks - 1) / col_blocks;       // aim for ~2048 workgroups
-  const int64_t max_splits = (M + 63) / 64;                    // >= 64 rows per split
+  // >= 64 rows per split (the 4-row unrolled loops need 32 rows per pass of the 8 row lanes)
+  const int64_t max_splits = (M + 63) / 64;
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   if (splits > 1024) splits = 1024;
