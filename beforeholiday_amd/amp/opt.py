@@ -45,7 +45,11 @@ class OptimWrapper(object):
         self._overflowed[self._cursor] = scaler.update_scale()
         self._cursor += 1
         for p, g in zip(params, earlier):
-            if g is not None:
+            if g is None:
+                continue
+            if p.grad is None:  # this loss did not reach p (zero_grad set its grad to None)
+                p.grad = g
+            else:
                 p.grad.data.add_(g)
 
     def step(self, closure=None):

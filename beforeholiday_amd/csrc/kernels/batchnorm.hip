@@ -1156,6 +1156,14 @@ void bn_merge_parts(int G, int C, const float* part, float count, const BNFinal&
 // at 256x256x56x56: 1024 / 2048 / 4096 / 16384 workgroups -> 5.2 / 5.3-5.4 / 5.4 / 5.6-5.7 TB/s; the
 // 2-D kernels 5.0)
 bool knob_flat() { static const bool v = env_knob("BH_BN_FLAT", 1) != 0; return v; }
+// the flat kernels keep `floats_per_channel` per-channel constants for ALL C channels in dynamic LDS
+// (k_fwd_flat 2, k_dgrad_flat 5); past the default 64 KiB dynamic-LDS launch limit the channel-owned
+// 2-D kernels (which cap channels per workgroup) take the shape
+constexpr size_t kFlatLdsCap = 64 * 1024;
+bool flat_ok(const BNShape& s, int floats_per_channel) {
+  return s.channels_last && s.C % 8 == 0 && knob_flat() &&
+         sizeof(float) * (size_t)floats_per_channel * (size_t)s.C <= kFlatLdsCap;
+}
 unsigned flat_grid(int64_t chunks) {
   static const int64_t cap = env_knob("BH_BN_FLAT_BLOCKS", 16384);
   const int64_t need = (chunks + kBlock * kFlatU - 1) / (kBlock * kFlatU);
@@ -1168,7 +1176,7 @@ void bn_forward(const BNShape& s, int dt_x, const void* x, int dt_z, const void*
   const int64_t total = s.outer * s.C * s.inner;
   if (total == 0) return;
   if (dt_z < 0) dt_z = dt_x;
-  if (s.channels_last && s.C % 8 == 0 && knob_flat()) {
+  if (flat_ok(s, 2)) {
     const int64_t chunks = total / 8;
     const size_t shm = sizeof(float) * 2 * s.C;
     BN_DISPATCH(dt_x, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_y, Ty,
@@ -1240,7 +1248,7 @@ void bn_backward_dgrad(const BNShape& s, int dt, const void* dy, const void* x, 
   const int64_t total = s.outer * s.C * s.inner;
   if (total == 0) return;
   if (dt_z < 0) dt_z = dt;
-  if (s.channels_last && s.C % 8 == 0 && knob_flat()) {
+  if (flat_ok(s, 5)) {
     const int64_t chunks = total / 8;
     const size_t shm = sizeof(float) * 5 * s.C;
     BN_DISPATCH(dt, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_w, Tw,

@@ -1238,9 +1238,12 @@ class Bottleneck(nn.Module):
         if _FOLD_APPLY in ("all", "bn1") and self.stride == 1 and bhconv.supported(y1, w2):
             # bn1 + ReLU inside conv2's halo prologue (and its weight gradient's LDS prologue)
             y2, p2 = _bn_conv(self.bn1, y1, p1, w2, _kshift(self.bn2), 3)
-        elif self.stride == 2 and bhconv.s2_supported(y1, w2):
+        elif _FOLD_APPLY in ("all", "bn1") and self.stride == 2 and y1.size(1) <= 512 and \
+                bhconv.s2_supported(y1, w2):
             # the downsampling 3x3: bn1 + ReLU in the implicit-GEMM kernel's A-fragment prologue (and the
-            # strided wgrad kernel's LDS prologue), bn2's statistics in its epilogue
+            # strided wgrad kernel's LDS prologue), bn2's statistics in its epilogue. The prologue variant
+            # of the implicit GEMM takes at most 512 input channels (kMaxProC, kernels/conv_igemm.hip);
+            # s2_supported() checks the shape without a prologue
             y2, p2 = _bn_conv(self.bn1, y1, p1, w2, _kshift(self.bn2), 3, stride=2)
         else:
             l1 = BNLink()

@@ -178,8 +178,9 @@ def _supports_avg(pg) -> bool:
         return False
 
 
-# parameter -> its bucket slot view, for the parameters of gradient-as-bucket-view DDP instances (weak:
-# nothing here keeps a parameter or its bucket alive)
+# parameter -> the data pointer of its bucket slot, for the parameters of gradient-as-bucket-view DDP
+# instances. The keys are weak and the values are plain ints, so nothing here keeps a parameter or its
+# bucket buffer alive (a stored slot VIEW would pin the whole flat bucket as long as the parameter lives)
 _VIEW_SLOTS = None
 
 
@@ -198,8 +199,8 @@ def grad_is_bucket_view(p: torch.Tensor) -> bool:
     g = p.grad
     if g is None or _VIEW_SLOTS is None:
         return False
-    slot = _VIEW_SLOTS.get(p)
-    return slot is not None and g.data_ptr() == slot.data_ptr()
+    ptr = _VIEW_SLOTS.get(p)
+    return ptr is not None and g.data_ptr() == ptr
 
 
 def _slot_view(flat: torch.Tensor, off: int, p: torch.Tensor) -> torch.Tensor:
@@ -211,7 +212,7 @@ def _slot_view(flat: torch.Tensor, off: int, p: torch.Tensor) -> torch.Tensor:
 
 
 class _Bucket:
-    __slots__ = ("params", "numel", "dtype", "flat", "work", "launched", "ready", "outputs", "slots")
+    __slots__ = ("params", "numel", "dtype", "flat", "work", "launched", "ready", "outputs", "slots", "placed")
 
     def __init__(self, params, dtype):
         self.params = params  # list of param indices
@@ -223,6 +224,7 @@ class _Bucket:
         self.ready = 0
         self.outputs = None
         self.slots = None  # per-parameter views of flat
+        self.placed = set()  # params whose gradient the hooks already put into their slot this backward
 
 
 class DistributedDataParallel(Module):
@@ -384,6 +386,7 @@ class DistributedDataParallel(Module):
                 if b_idx is not None:
                     b = self._buckets[b_idx]
                     self._to_slot(b, idx)
+                    b.placed.add(idx)
                     b.ready += 1
                     if b.ready == len(b.params):
                         self._launch_ready_in_order()
@@ -470,7 +473,7 @@ class DistributedDataParallel(Module):
             p = self.active_params[i]
             b.slots[i] = _slot_view(b.flat, off, p)
             if self.gradient_as_bucket_view:
-                _view_slots()[p] = b.slots[i]
+                _view_slots()[p] = b.slots[i].data_ptr()
             off += p.numel()
 
     def _to_slot(self, b: _Bucket, i: int):
@@ -499,7 +502,8 @@ class DistributedDataParallel(Module):
         if b.slots is None:
             self._alloc_slots(b)
         for i in b.params:  # parameters the hooks have not placed yet (first / delayed / unused)
-            self._to_slot(b, i)
+            if i not in b.placed:
+                self._to_slot(b, i)
         tensor = b.flat.float() if self.allreduce_always_fp32 and b.flat.dtype != torch.float32 else b.flat
         if self.gradient_predivide_factor != 1.0:
             tensor.mul_(1.0 / self.gradient_predivide_factor)
@@ -544,5 +548,6 @@ class DistributedDataParallel(Module):
         self._next_bucket = 0
         for b in self._buckets:
             b.launched, b.ready = False, 0
+            b.placed.clear()
         if self.prof:
             torch.cuda.nvtx.range_pop()

@@ -424,3 +424,33 @@ def test_checkpoint_across_opt_levels(device, save_level, load_level):
         s.backward()
     opt2.step()
     assert all(torch.isfinite(p).all() for p in model2.parameters())
+
+
+def test_optim_wrapper_second_loss_touches_subset_of_params():
+    """Legacy multi-loss OptimWrapper: loss 1 reaches only one of two parameters. zero_grad() before
+    its backward leaves the other parameter's .grad None; the wrapper must restore loss 0's gradient
+    there instead of failing on None.add_()."""
+    from beforeholiday_amd.amp.opt import OptimWrapper
+
+    class _Handle:
+        def is_active(self):
+            return True
+
+        def remove_cache(self, p):
+            pass
+
+    torch.manual_seed(0)
+    a = torch.nn.Parameter(torch.randn(4))
+    b = torch.nn.Parameter(torch.randn(4))
+    opt = OptimWrapper(torch.optim.SGD([a, b], lr=0.1), _Handle(), num_loss=2)
+    with opt.scale_loss((a * b).sum()) as s:
+        s.backward()
+    ga, gb = a.grad.clone(), b.grad.clone()
+    with opt.scale_loss((a * 3).sum()) as s:
+        s.backward()
+    torch.testing.assert_close(a.grad, ga + 3)
+    torch.testing.assert_close(b.grad, gb)
+    a0, b0 = a.detach().clone(), b.detach().clone()
+    opt.step()
+    torch.testing.assert_close(a.detach(), a0 - 0.1 * (ga + 3))
+    torch.testing.assert_close(b.detach(), b0 - 0.1 * gb)

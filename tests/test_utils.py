@@ -54,3 +54,49 @@ def test_install_apex_aliases():
     import apex  # noqa: F401
     from apex.optimizers import FusedLAMB  # noqa: F401
     assert "amp_C" in sys.modules and "apex_C" in sys.modules
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_pipeline_timers(device, capsys):
+    """_Timers: accumulate over start/stop pairs, cut a running interval in elapsed(), reset, log."""
+    import time
+
+    from beforeholiday_amd.transformer.pipeline_parallel._timers import _Timers
+
+    if device == "cuda":
+        torch.cuda.init()
+        x = torch.randn(2048, 2048, device="cuda")
+    timers = _Timers()
+    t = timers("fwd")
+    for _ in range(2):
+        t.start()
+        if device == "cuda":
+            for _ in range(20):
+                x = x @ x / 2048
+        else:
+            time.sleep(0.01)
+        t.stop()
+    with pytest.raises(RuntimeError):
+        t.stop()
+    v = t.elapsed(reset=False)
+    assert v > (0.015 if device == "cpu" else 0.0)
+    assert t.elapsed(reset=True) == pytest.approx(v)
+    assert t.elapsed() == 0.0
+    t.start()
+    assert t.elapsed() >= 0.0 and t.running  # cut and restarted
+    t.stop()
+    timers("bwd").start()
+    timers("bwd").stop()
+    timers.log(["fwd", "bwd"])
+    assert capsys.readouterr().out.startswith("time (ms) | fwd:")
+
+    class _W:
+        def __init__(self):
+            self.rows = []
+
+        def add_scalar(self, k, v, it):
+            self.rows.append((k, it))
+
+    w = _W()
+    timers.write(["fwd"], w, 7)
+    assert w.rows == [("fwd-time", 7)]
