@@ -67,5 +67,6 @@ void register_contrib(pybind11::module_& m);
 void register_misc(pybind11::module_& m);
 void register_conv(pybind11::module_& m);
 void register_conv_bn(pybind11::module_& m);
+void register_bn_fold(pybind11::module_& m);
 
 }  // namespace bhb

@@ -200,7 +200,7 @@ bool wgrad_supported(const at::Tensor& x, const at::Tensor& dy, int64_t R, int64
 // them with conv_wgrad_reduce (on a side stream: nothing on the critical path waits for them)
 std::vector<at::Tensor> conv_wgrad_impl(const at::Tensor& x, const at::Tensor& dy, int64_t R, int64_t stride,
                                         const c10::optional<at::Tensor>& pro_scale,
-                                        const c10::optional<at::Tensor>& pro_shift, bool defer) {
+                                        const c10::optional<at::Tensor>& pro_shift, bool defer, bool f32 = false) {
   TORCH_CHECK(wgrad_ok(x, dy, R, stride), "conv_wgrad: needs channels_last fp16/bf16 x [N, C, sH, sW], "
                                           "dy [N, K, H, W], C and K % 64 == 0, R in {1, 3}, stride in {1, 2}");
   auto out = at::empty({dy.size(1), x.size(1), R, R}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
@@ -221,6 +221,7 @@ std::vector<at::Tensor> conv_wgrad_impl(const at::Tensor& x, const at::Tensor& d
   }
   bh::ConvWgradGeo g;
   TORCH_CHECK(bh::conv_wgrad_plan(a, &g), "conv_wgrad: shape not covered (window does not fit in LDS / unaligned)");
+  g.f32 = f32;
   const int64_t nws = bh::conv_wgrad_workspace(g, a);
   at::Tensor ws;
   if (nws > 0) ws = at::empty({nws}, x.options().dtype(at::kFloat));
@@ -425,6 +426,13 @@ void register_conv(pybind11::module_& root) {
         py::arg("pro_shift") = py::none(),
         "conv_wgrad without the split-partials sum: [out (not yet written when ws is returned), ws [parts, n] or None]");
   m.def("conv_wgrad_reduce", &conv_wgrad_reduce, py::arg("ws"), py::arg("out"));
+  m.def("conv_wgrad_f32", [](const at::Tensor& x, const at::Tensor& dy, int64_t R, int64_t stride,
+                             const c10::optional<at::Tensor>& ps, const c10::optional<at::Tensor>& ph) {
+    return conv_wgrad_impl(x, dy, R, stride, ps, ph, true, true)[1];
+  }, py::arg("x"), py::arg("grad_out"), py::arg("R"), py::arg("stride") = 1, py::arg("pro_scale") = py::none(),
+        py::arg("pro_shift") = py::none(),
+        "the weight-gradient product as fp32 split partials [parts, K * C * R * R] (never rounded to 16 bits; "
+        "sum over dim 0 in any fixed order)");
   m.def("wgrad_supported", &wgrad_supported, py::arg("x"), py::arg("grad_out"), py::arg("R"), py::arg("stride") = 1);
   m.def("gemm_n64", &gemm_n64, py::arg("a"), py::arg("b"), py::arg("resid") = c10::nullopt,
         "a [M, K] . b[64, K]^T (+ resid [M, 64]), K in {64, 128, 256}, M % 32 == 0 (kernels/gemm_n64.hip)");

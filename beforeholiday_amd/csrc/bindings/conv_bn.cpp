@@ -71,7 +71,8 @@ std::vector<at::Tensor> c1x1(const at::Tensor& a, const at::Tensor& b, bool b_tr
                              const c10::optional<at::Tensor>& bscale, const c10::optional<at::Tensor>& bshift,
                              const c10::optional<at::Tensor>& bmean, bool brelu, bool s2_scatter,
                              const c10::optional<at::Tensor>& a_scale, const c10::optional<at::Tensor>& a_shift,
-                             bool relu, bool r_mul) {
+                             bool relu, bool r_mul, const c10::optional<at::Tensor>& bnb,
+                             const c10::optional<at::Tensor>& bnb_y, const c10::optional<at::Tensor>& mbits) {
   at::Tensor c;
   if (s2_scatter) {
     // accumulate into the full-resolution tensor `resid` in place: a is [M, K], resid [4M, N]
@@ -100,8 +101,21 @@ std::vector<at::Tensor> c1x1(const at::Tensor& a, const at::Tensor& b, bool b_tr
     p.relu = relu;
     p.r_mul = r_mul;
   }
+  if (bnb.has_value() && bnb->defined()) {
+    p.bnb = fptr(bnb, 3 * (int64_t)p.K, "bnb");
+    TORCH_CHECK(bnb_y.has_value() && bnb_y->defined() && bnb_y->is_cuda() && bnb_y->device() == a.device() &&
+                    bnb_y->scalar_type() == a.scalar_type() && bnb_y->is_contiguous() && bnb_y->sizes() == a.sizes(),
+                "conv_bn.c1x1: bnb_y must be a contiguous tensor shaped like a, of a's dtype");
+    p.bnb_y = bnb_y->data_ptr();
+  }
+  if (epi == bh::kC1x1Mask) {
+    TORCH_CHECK(mbits.has_value() && mbits->defined() && mbits->is_cuda() && mbits->device() == a.device() &&
+                    mbits->scalar_type() == at::kByte && mbits->is_contiguous() && mbits->numel() == M * p.N / 8,
+                "conv_bn.c1x1: the mask epilogue needs mbits, a contiguous uint8 [M, N/8] tensor");
+    p.mbits = mbits->data_ptr<uint8_t>();
+  }
   at::Tensor part;
-  if (epi == bh::kC1x1Stats || epi == bh::kC1x1Bwd) {
+  if (epi == bh::kC1x1Stats || epi == bh::kC1x1Bwd || epi == bh::kC1x1Mask) {
     const int G = bh::c1x1_parts(p);
     TORCH_CHECK(G > 0, "conv_bn.c1x1: unsupported shape");
     part = at::empty({2, (int64_t)G, (int64_t)p.N}, a.options().dtype(at::kFloat));
@@ -116,7 +130,7 @@ std::vector<at::Tensor> c1x1(const at::Tensor& a, const at::Tensor& b, bool b_tr
 }
 
 bool c1x1_supported(const at::Tensor& a, const at::Tensor& b, bool b_trans, int64_t M, bool pro, bool resid,
-                    int64_t s2_h, int64_t s2_w, int64_t epi, bool s2_scatter) {
+                    int64_t s2_h, int64_t s2_w, int64_t epi, bool s2_scatter, bool bnb) {
   if (!(a.is_cuda() && b.is_cuda() && a.dim() == 2 && b.dim() == 2 && a.is_contiguous() && b.is_contiguous() &&
         a.scalar_type() == b.scalar_type() && a.size(1) == b.size(b_trans ? 0 : 1) &&
         (a.scalar_type() == at::kHalf || a.scalar_type() == at::kBFloat16)))
@@ -132,6 +146,8 @@ bool c1x1_supported(const at::Tensor& a, const at::Tensor& b, bool b_trans, int6
   p.N = (int)b.size(b_trans ? 1 : 0);
   p.pro_scale = pro ? dummy : nullptr;
   p.pro_shift = pro ? dummy : nullptr;
+  p.bnb = bnb ? dummy : nullptr;
+  p.bnb_y = bnb ? a.data_ptr() : nullptr;
   p.R = resid ? a.data_ptr() : nullptr;
   if (s2_scatter) p.R = p.C;
   p.s2_scatter = s2_scatter;
@@ -144,6 +160,7 @@ bool c1x1_supported(const at::Tensor& a, const at::Tensor& b, bool b_trans, int6
     p.by = a.data_ptr();
     p.bscale = p.bshift = p.bmean = dummy;
   }
+  if (epi == bh::kC1x1Mask) p.mbits = reinterpret_cast<const uint8_t*>(dummy);
   return bh::c1x1_supported(p);
 }
 
@@ -218,11 +235,13 @@ void register_conv_bn(pybind11::module_& root) {
         py::arg("epi") = 0, py::arg("kshift") = py::none(), py::arg("by") = py::none(), py::arg("bscale") = py::none(),
         py::arg("bshift") = py::none(), py::arg("bmean") = py::none(), py::arg("brelu") = true,
         py::arg("s2_scatter") = false, py::arg("a_scale") = py::none(), py::arg("a_shift") = py::none(),
-        py::arg("relu") = false, py::arg("r_mul") = false);
+        py::arg("relu") = false, py::arg("r_mul") = false, py::arg("bnb") = py::none(), py::arg("bnb_y") = py::none(),
+        py::arg("mbits") = py::none());
+  m.attr("EPI_MASK") = (int)bh::kC1x1Mask;
   m.attr("EPI_AFFINE") = (int)bh::kC1x1Affine;
   m.def("c1x1_supported", &c1x1_supported, py::arg("a"), py::arg("b"), py::arg("b_trans"), py::arg("M"), py::arg("pro") = false,
         py::arg("resid") = false, py::arg("s2_h") = 0, py::arg("s2_w") = 0, py::arg("epi") = 0,
-        py::arg("s2_scatter") = false);
+        py::arg("s2_scatter") = false, py::arg("bnb") = false);
   m.def("sum_parts", &sum_parts, py::arg("part"), py::arg("count") = -1.0);
   m.def("gemm_bn", &gemm_bn, py::arg("a"), py::arg("b"), py::arg("epi"), py::arg("kshift") = py::none(),
         py::arg("by") = py::none(), py::arg("bscale") = py::none(), py::arg("bshift") = py::none(),

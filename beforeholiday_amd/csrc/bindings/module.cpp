@@ -17,4 +17,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   bhb::register_peer_memory(m);
   bhb::register_conv(m);
   bhb::register_conv_bn(m);
+  bhb::register_bn_fold(m);
 }

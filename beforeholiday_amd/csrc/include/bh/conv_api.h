@@ -68,6 +68,9 @@ struct ConvWgradArgs {
 struct ConvWgradGeo {
   int G4 = 0, TH = 0, ksteps = 0, wpi = 0, nwin = 0, ctiles = 0, tiles = 0, wpw = 0, splits = 0, grid = 0, kt = 1, ct = 1, parts = 0;
   bool wide = false;  // 1x1: 256 x 128 tiles, 64-pixel windows
+  // set by the caller after conv_wgrad_plan: every split (even a single one) writes fp32 partials to ws,
+  // never the 16-bit `out` (the BatchNorm fold combines the raw fp32 product, bh/bn_fold_api.h)
+  bool f32 = false;
 };
 // false when the kernel does not cover the shape (C, K % 64, 16-byte alignment, window fits in LDS)
 bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo);

@@ -3,7 +3,7 @@
 // C[M, N] = f(A)[M, K] . B[N, K]^T on NHWC activations viewed as [pixels, channels], fp32 accumulation:
 //   * prologue (pro_scale != null): f(a) = relu(a * pro_scale[k] + pro_shift[k]) -- the BatchNorm(+ReLU)
 //     of the producing layer applied while the operand is loaded, so the normalised activation is never
-//     written to HBM;
+//     written to HBM; or (bnb != null) the BatchNorm-backward prologue f(a) = A[k] a + B[k] y + D[k];
 //   * stride-2 gather (s2_H > 0): output row (n, y, x) reads input row (n, 2y, 2x) of an [N, s2_H, s2_W, K]
 //     tensor (the ResNet downsample branch), no gathered copy;
 //   * epilogue, optional residual R[M, N] added before rounding;
@@ -14,6 +14,9 @@
 //       kBwd:   with y = by[m, n] (the raw input of the previous BatchNorm), mask = (y * bscale[n] +
 //               bshift[n] > 0) when brelu: sums of dz = c * mask and dz * (y - bmean[n]) -- that
 //               BatchNorm's backward reduction, computed on the data gradient as it is produced.
+//       kMask:  c = c * bit(m, n) of the saved ReLU bit mask mbits [M, N/8] (bit n % 8 of byte n / 8) and
+//               sums of the masked c (second statistic zero) -- the gradient through a residual block's
+//               BatchNorm + add + ReLU output, masked where it is produced (models/resnet.py _ConvBNResFn).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -21,7 +24,7 @@
 
 namespace bh {
 
-enum C1x1Epi { kC1x1Plain = 0, kC1x1Stats = 1, kC1x1Bwd = 2, kC1x1Affine = 3 };
+enum C1x1Epi { kC1x1Plain = 0, kC1x1Stats = 1, kC1x1Bwd = 2, kC1x1Affine = 3, kC1x1Mask = 4 };
 
 struct C1x1Args {
   const void* A = nullptr;  // [rows, K] (rows = M, or N * s2_H * s2_W with the stride-2 gather)
@@ -33,6 +36,13 @@ struct C1x1Args {
   int K = 0, N = 0;
   const float* pro_scale = nullptr;  // [K] prologue BatchNorm (with ReLU)
   const float* pro_shift = nullptr;
+  // BatchNorm-backward prologue (instead of pro_scale / pro_shift): f(a) = A[k] a + B[k] bnb_y + D[k], with
+  // bnb = [A (K), B (K), D (K)] fp32 and bnb_y [M, K] -- the data gradient of a convolution whose output y
+  // went through a training BatchNorm, formed per fragment from the BatchNorm's output gradient a and its
+  // input y (kernels/bn_fold.hip: the BatchNorm input gradient is never written)
+  const float* bnb = nullptr;
+  const void* bnb_y = nullptr;
+  const uint8_t* mbits = nullptr;  // kMask: [M, N/8] ReLU bit mask (N % 32 == 0, 4-byte aligned)
   int s2_H = 0, s2_W = 0;  // > 0: stride-2 gather from an [.., s2_H, s2_W, K] input; output is [.., s2_H/2, s2_W/2, N]
   // with s2_H > 0: scatter instead -- row (n, y, x) of the [M, N] result is ADDED into row (n, 2y, 2x) of
   // the full-resolution C [.., s2_H, s2_W, N] (R must equal C): the data gradient of a 1x1 / stride-2

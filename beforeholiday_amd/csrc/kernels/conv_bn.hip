@@ -66,7 +66,8 @@ struct Geo {
 
 // S2: 0 none, 1 stride-2 gather of the A rows, 2 stride-2 scatter of the C rows (output row (n, y, x)
 // of the quarter-resolution problem lands in row (n, 2y, 2x) of the full-resolution C)
-template <typename T, int KC, int NC, int EPI, bool PRO, int S2, bool RES>
+// PRO: 0 none, 1 BatchNorm + ReLU of the A operand, 2 BatchNorm backward (A a + B y + D from a second stream)
+template <typename T, int KC, int NC, int EPI, int PRO, int S2, bool RES>
 __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NT = NC / 32;  // 32-column tiles per wave
@@ -85,6 +86,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
   const int RS = 2 * K + 16;
   char* bl = smem;
   float* ss = reinterpret_cast<float*>(smem + g.ss_off);
+  float* se = ss + (PRO == 1 ? 2 * K : (PRO == 2 ? 3 * K : 0));  // the epilogue's per-column constants
   {
     if (!p.b_trans) {
       const T* Bp = reinterpret_cast<const T*>(p.B) + (int64_t)col0 * K;
@@ -107,23 +109,26 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
         for (int j = 0; j < 8; ++j) *reinterpret_cast<T*>(bl + (n8 * 8 + j) * RS + 2 * k) = v[j];
       }
     }
-    if constexpr (PRO) {
+    if constexpr (PRO == 1) {
       for (int c = threadIdx.x; c < K; c += kThreads) {
         ss[c] = p.pro_scale[c];
         ss[K + c] = p.pro_shift[c];
       }
     }
+    if constexpr (PRO == 2) {
+      for (int c = threadIdx.x; c < 3 * K; c += kThreads) ss[c] = p.bnb[c];
+    }
     if constexpr (EPI == kC1x1Affine) {  // frozen per-column scale / shift of the epilogue
       for (int c = threadIdx.x; c < NC; c += kThreads) {
-        ss[c] = p.a_scale[col0 + c];
-        ss[NC + c] = p.a_shift[col0 + c];
+        se[c] = p.a_scale[col0 + c];
+        se[NC + c] = p.a_shift[col0 + c];
       }
     }
     if constexpr (EPI == kC1x1Bwd) {  // the previous BatchNorm's per-column constants, read per tile
       for (int c = threadIdx.x; c < NC; c += kThreads) {
-        ss[c] = p.bscale[col0 + c];
-        ss[NC + c] = p.bshift[col0 + c];
-        ss[2 * NC + c] = p.bmean[col0 + c];
+        se[c] = p.bscale[col0 + c];
+        se[NC + c] = p.bshift[col0 + c];
+        se[2 * NC + c] = p.bmean[col0 + c];
       }
     }
   }
@@ -159,15 +164,22 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
   const int first = grp * kWaves + wave;
   const int total = (first < g.strips ? (g.strips - first + stride - 1) / stride : 0) * nch;
   i4v a0[KS], a1[KS];
-  auto load = [&](int i, i4v(&a)[KS]) {
+  i4v y0[PRO == 2 ? KS : 1], y1[PRO == 2 ? KS : 1];  // PRO 2: the BatchNorm input's fragments
+  const T* __restrict__ BY = reinterpret_cast<const T*>(p.bnb_y);
+  auto load = [&](int i, i4v(&a)[KS], i4v(&yv)[PRO == 2 ? KS : 1]) {
     const int q = i / nch, c = i - q * nch;
-    const T* src = A + arow(first + q * stride) * K + c * KC + 8 * h;
+    const int64_t off = arow(first + q * stride) * K + c * KC + 8 * h;
+    const T* src = A + off;
     if (p.a_load == 1) {
 #pragma unroll
       for (int s = 0; s < KS; ++s) a[s] = *reinterpret_cast<const i4v*>(src + 16 * s);
     } else {
 #pragma unroll
       for (int s = 0; s < KS; ++s) a[s] = __builtin_nontemporal_load(reinterpret_cast<const i4v*>(src + 16 * s));
+    }
+    if constexpr (PRO == 2) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) yv[s] = __builtin_nontemporal_load(reinterpret_cast<const i4v*>(BY + off + 16 * s));
     }
   };
   // Output staging (all but the scatter variant): the lane-per-column MFMA result leaves as 128-byte
@@ -207,8 +219,9 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
   // top of the strip's last chunk, so their HBM latency hides behind that chunk's MFMAs instead of
   // stalling the epilogue (one 2-byte column load per row: nothing to coalesce them into). Wider tiles
   // keep the per-tile loads (hoisting 64+ values spills).
-  constexpr bool kHoist = (RES != (EPI == kC1x1Bwd)) && S2 != 2 && NT * 16 <= 32;
-  auto process = [&](int i, i4v(&a)[KS]) {
+  // (not next to the BatchNorm-backward prologue's second fragment stream: registers)
+  constexpr bool kHoist = (RES != (EPI == kC1x1Bwd)) && S2 != 2 && NT * 16 <= 32 && PRO != 2;
+  auto process = [&](int i, i4v(&a)[KS], i4v(&yv)[PRO == 2 ? KS : 1]) {
     const int q = i / nch, c = i - q * nch;
     const int strip = first + q * stride;
     if (c == 0) {
@@ -217,7 +230,21 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
 #pragma unroll
         for (int v = 0; v < 16; ++v) acc[t][v] = 0.f;
     }
-    if constexpr (PRO) {
+    if constexpr (PRO == 2) {
+      // BatchNorm backward on the fragment: A a + B y + D in fp32, rounded once (the input gradient as the
+      // separate data-gradient pass would have stored it)
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int kb = c * KC + 16 * s + 8 * h;
+        V8 v = __builtin_bit_cast(V8, a[s]);
+        const V8 yy = __builtin_bit_cast(V8, yv[s]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[j] = from_f<T>(fmaf(to_f<T>(v[j]), ss[kb + j], fmaf(to_f<T>(yy[j]), ss[K + kb + j], ss[2 * K + kb + j])));
+        a[s] = __builtin_bit_cast(i4v, v);
+      }
+    }
+    if constexpr (PRO == 1) {
       // BatchNorm + ReLU of the producing layer, on the fragment (channels 16 s + 8 h .. + 7)
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
@@ -291,10 +318,17 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
       }
       float bsc = 0.f, bsh = 0.f, bmn = 0.f;
       if constexpr (EPI == kC1x1Bwd || EPI == kC1x1Affine) {
-        bsc = ss[32 * t + r];
-        bsh = ss[NC + 32 * t + r];
+        bsc = se[32 * t + r];
+        bsh = se[NC + 32 * t + r];
       }
-      if constexpr (EPI == kC1x1Bwd) bmn = ss[2 * NC + 32 * t + r];
+      if constexpr (EPI == kC1x1Bwd) bmn = se[2 * NC + 32 * t + r];
+      uint32_t mw[EPI == kC1x1Mask ? 16 : 1];  // kMask: the 32 mask bits of this tile's columns, per row
+      if constexpr (EPI == kC1x1Mask) {
+        const uint32_t* mp = reinterpret_cast<const uint32_t*>(p.mbits);
+        const int wcol = (col0 + 32 * t) >> 5;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) mw[v] = mp[out_row(v) * (N >> 5) + wcol];
+      }
       float yv[16];
       if constexpr (RES && EPI == kC1x1Bwd) {
 #pragma unroll
@@ -321,6 +355,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
           } else if constexpr (RES) {
             x += xr[v];
           }
+          if constexpr (EPI == kC1x1Mask) x = ((mw[v] >> r) & 1u) ? x : 0.f;
           const T o = from_f<T>(x);
           if constexpr (S2 == 2) {
             Cp[out_row(v) * N + col] = o;
@@ -357,24 +392,26 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
             const float dz = (!p.brelu || fmaf(y, bsc, bsh) > 0.f) ? f : 0.f;
             s1[t] += dz;
             s2[t] = fmaf(dz, y - bmn, s2[t]);
+          } else if constexpr (EPI == kC1x1Mask) {
+            s1[t] += f;
           }
         }
       // one tile's residual / input loads at a time: hoisting every tile's 16-32 loads to the top
       // of the epilogue spills at NC >= 128
-      if constexpr (RES || EPI == kC1x1Bwd) __builtin_amdgcn_sched_barrier(0);
+      if constexpr (RES || EPI == kC1x1Bwd || EPI == kC1x1Mask) __builtin_amdgcn_sched_barrier(0);
     }
   };
-  if (total > 0) load(0, a0);
+  if (total > 0) load(0, a0, y0);
   for (int i = 0; i < total; i += 2) {
-    if (i + 1 < total) load(i + 1, a1);
-    process(i, a0);
+    if (i + 1 < total) load(i + 1, a1, y1);
+    process(i, a0, y0);
     if (i + 1 < total) {
-      if (i + 2 < total) load(i + 2, a0);
-      process(i + 1, a1);
+      if (i + 2 < total) load(i + 2, a0, y0);
+      process(i + 1, a1, y1);
     }
   }
 
-  if constexpr (EPI == kC1x1Stats || EPI == kC1x1Bwd) {
+  if constexpr (EPI == kC1x1Stats || EPI == kC1x1Bwd || EPI == kC1x1Mask) {
     float* red = reinterpret_cast<float*>(smem + g.red_off);  // [waves][2][NC], aliases the staging tiles
     __syncthreads();
 #pragma unroll
@@ -440,9 +477,12 @@ struct Plan {
   Geo g;
 };
 
-int ss_bytes(int NC, int K, bool pro, bool bwd, bool aff) { return pro ? 8 * K : (bwd ? 12 * NC : (aff ? 8 * NC : 0)); }
+int ss_bytes(int NC, int K, int pro, bool bwd, bool aff) {
+  // prologue constants per k (1: scale, shift; 2: A, B, D), then the epilogue's per column
+  return (pro == 1 ? 8 * K : (pro == 2 ? 12 * K : 0)) + (bwd ? 12 * NC : (aff ? 8 * NC : 0));
+}
 
-int lds_bytes(int NC, int K, bool pro, bool bwd, bool aff, bool stats, bool scatter) {
+int lds_bytes(int NC, int K, int pro, bool bwd, bool aff, bool stats, bool scatter) {
   // the statistics reduction buffer (used after the strip loop) aliases the output staging tiles
   return NC * (2 * K + 16) + ss_bytes(NC, K, pro, bwd, aff) +
          std::max(stats ? kWaves * 2 * NC * 4 : 0, scatter ? 0 : kWaves * kStageBytes);
@@ -451,10 +491,12 @@ int lds_bytes(int NC, int K, bool pro, bool bwd, bool aff, bool stats, bool scat
 bool make_plan(const C1x1Args& a, Plan* pl) {
   if (a.K <= 0 || a.N <= 0 || a.M <= 0 || a.K % 64 != 0 || a.N % 64 != 0 || a.M % 32 != 0) return false;
   if (a.M / 32 >= (1ll << 31)) return false;
-  const bool pro = a.pro_scale != nullptr, stats = a.epi == kC1x1Stats || a.epi == kC1x1Bwd,
+  const int pro = a.bnb ? 2 : (a.pro_scale != nullptr ? 1 : 0);
+  const bool stats = a.epi == kC1x1Stats || a.epi == kC1x1Bwd || a.epi == kC1x1Mask,
              bwd = a.epi == kC1x1Bwd, aff = a.epi == kC1x1Affine, scatter = a.s2_H > 0 && a.s2_scatter;
   // register budget: the backward epilogue (input loads + statistics) fits 4 column tiles per wave
-  const int max_nc = bwd ? (a.R ? 64 : 128) : 256;
+  // (the mask epilogue's per-row mask words spill at wider slices)
+  const int max_nc = a.epi == kC1x1Mask ? 64 : (bwd ? (a.R ? 64 : 128) : 256);
   int NC = 0, occ = 0;
   // the widest column slice (A read once per slice) that still leaves two workgroups per CU; else one
   // (BH_C1X1_OCC: the resident-workgroup target, an experiment knob; the kernels' registers must allow it)
@@ -472,7 +514,8 @@ bool make_plan(const C1x1Args& a, Plan* pl) {
       }
   if (!NC) return false;
   // registers: two A chunks of KC / 4 VGPRs each next to NC / 2 accumulators
-  const int KC = (NC <= 128 && a.K % 128 == 0 && !(bwd && NC == 128)) ? 128 : 64;
+  // (the BatchNorm-backward prologue's second fragment stream leaves room for 64-deep chunks only)
+  const int KC = (NC <= 128 && a.K % 128 == 0 && !(bwd && NC == 128) && pro != 2) ? 128 : 64;
   Geo g{};
   g.nslices = a.N / NC;
   g.strips = (int)(a.M / 32);
@@ -502,7 +545,10 @@ bool c1x1_supported(const C1x1Args& a) {
   if (!al16(a.A) || !al16(a.B) || !al16(a.C) || (a.R && !al16(a.R))) return false;
   if (a.epi == kC1x1Bwd && (!a.by || !a.bscale || !a.bshift || !a.bmean)) return false;
   if (a.epi == kC1x1Affine && (!a.a_scale || !a.a_shift || a.pro_scale || a.s2_scatter)) return false;
-  if ((a.epi == kC1x1Stats || a.epi == kC1x1Bwd) && !a.part) return false;
+  if ((a.epi == kC1x1Stats || a.epi == kC1x1Bwd || a.epi == kC1x1Mask) && !a.part) return false;
+  if (a.epi == kC1x1Mask &&
+      (!a.mbits || (reinterpret_cast<uintptr_t>(a.mbits) & 3) || a.N % 32 || a.pro_scale || a.bnb || a.s2_H > 0))
+    return false;
   if (a.s2_H > 0) {
     if (a.s2_H % 2 || a.s2_W % 2 || a.M % ((int64_t)(a.s2_H / 2) * (a.s2_W / 2))) return false;
     if (a.pro_scale || a.epi == kC1x1Bwd) return false;  // combinations not instantiated
@@ -513,6 +559,10 @@ bool c1x1_supported(const C1x1Args& a) {
     return false;
   }
   if (a.pro_scale && (a.R || a.epi != kC1x1Stats)) return false;
+  // BatchNorm-backward prologue: a second [M, K] stream; plain or backward-sums epilogue, no residual / stride 2
+  if (a.bnb && (!a.bnb_y || !al16(a.bnb_y) || a.pro_scale || a.R || a.s2_H > 0 ||
+                (a.epi != kC1x1Plain && a.epi != kC1x1Bwd)))
+    return false;
   return true;
 }
 
@@ -532,7 +582,7 @@ void c1x1_run(int dt, const C1x1Args& a_in, hipStream_t st) {
   Plan pl;
   make_plan(a, &pl);
   const dim3 grid(pl.g.nslices * pl.g.G), block(kThreads);
-  const bool pro = a.pro_scale != nullptr, s2 = a.s2_H > 0, res = a.R != nullptr;
+  const bool pro = a.pro_scale != nullptr, s2 = a.s2_H > 0, res = a.R != nullptr, bnb = a.bnb != nullptr;
   // instantiated flag combinations: (epi, pro, s2, res)
   auto go = [&](auto tt, auto kc, auto nc) {
     using T = typename decltype(tt)::type;
@@ -541,30 +591,40 @@ void c1x1_run(int dt, const C1x1Args& a_in, hipStream_t st) {
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, pl.lds);
       hipLaunchKernelGGL(kern, grid, block, pl.lds, st, a, pl.g);
     };
-    if (a.epi == kC1x1Stats) {
-      if (pro) L(k_c1x1<T, KC, NC, kC1x1Stats, true, 0, false>);
-      else if (s2) L(k_c1x1<T, KC, NC, kC1x1Stats, false, 1, false>);
-      else L(k_c1x1<T, KC, NC, kC1x1Stats, false, 0, false>);
+    if (bnb) {  // BatchNorm-backward prologue (KC 64 only, see make_plan)
+      if constexpr (KC == 64 && NC <= 128) {
+        if (a.epi == kC1x1Bwd) L(k_c1x1<T, KC, NC, kC1x1Bwd, 2, 0, false>);
+        else L(k_c1x1<T, KC, NC, kC1x1Plain, 2, 0, false>);
+      }
+    } else if (a.epi == kC1x1Mask) {
+      if constexpr (NC == 64) {
+        if (res) L(k_c1x1<T, KC, NC, kC1x1Mask, 0, 0, true>);
+        else L(k_c1x1<T, KC, NC, kC1x1Mask, 0, 0, false>);
+      }
+    } else if (a.epi == kC1x1Stats) {
+      if (pro) L(k_c1x1<T, KC, NC, kC1x1Stats, 1, 0, false>);
+      else if (s2) L(k_c1x1<T, KC, NC, kC1x1Stats, 0, 1, false>);
+      else L(k_c1x1<T, KC, NC, kC1x1Stats, 0, 0, false>);
     } else if (a.epi == kC1x1Bwd) {
       if constexpr (NC <= 64) {
-        if (res) L(k_c1x1<T, KC, NC, kC1x1Bwd, false, 0, true>);
+        if (res) L(k_c1x1<T, KC, NC, kC1x1Bwd, 0, 0, true>);
       }
       if constexpr (NC <= 128) {
-        if (!res) L(k_c1x1<T, KC, NC, kC1x1Bwd, false, 0, false>);
+        if (!res) L(k_c1x1<T, KC, NC, kC1x1Bwd, 0, 0, false>);
       }
     } else if (a.epi == kC1x1Affine) {
       if (s2) {
-        if (res) L(k_c1x1<T, KC, NC, kC1x1Affine, false, 1, true>);
-        else L(k_c1x1<T, KC, NC, kC1x1Affine, false, 1, false>);
+        if (res) L(k_c1x1<T, KC, NC, kC1x1Affine, 0, 1, true>);
+        else L(k_c1x1<T, KC, NC, kC1x1Affine, 0, 1, false>);
       } else {
-        if (res) L(k_c1x1<T, KC, NC, kC1x1Affine, false, 0, true>);
-        else L(k_c1x1<T, KC, NC, kC1x1Affine, false, 0, false>);
+        if (res) L(k_c1x1<T, KC, NC, kC1x1Affine, 0, 0, true>);
+        else L(k_c1x1<T, KC, NC, kC1x1Affine, 0, 0, false>);
       }
     } else {
-      if (s2 && a.s2_scatter) L(k_c1x1<T, KC, NC, kC1x1Plain, false, 2, true>);
-      else if (s2) L(k_c1x1<T, KC, NC, kC1x1Plain, false, 1, false>);
-      else if (res) L(k_c1x1<T, KC, NC, kC1x1Plain, false, 0, true>);
-      else L(k_c1x1<T, KC, NC, kC1x1Plain, false, 0, false>);
+      if (s2 && a.s2_scatter) L(k_c1x1<T, KC, NC, kC1x1Plain, 0, 2, true>);
+      else if (s2) L(k_c1x1<T, KC, NC, kC1x1Plain, 0, 1, false>);
+      else if (res) L(k_c1x1<T, KC, NC, kC1x1Plain, 0, 0, true>);
+      else L(k_c1x1<T, KC, NC, kC1x1Plain, 0, 0, false>);
     }
   };
   auto by_nc = [&](auto tt, auto kc) {

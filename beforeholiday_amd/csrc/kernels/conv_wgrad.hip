@@ -410,7 +410,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_conv_wgrad(ConvWgradArgs a, Con
         for (int i = 0; i < 4; ++i) {
           const int k = k0 + 32 * KT * kw + 32 * t + 8 * j + 4 * h + i;
           const int64_t o = ((int64_t)k * RR + rs) * C + c;
-          if (g.parts == 1) out[o] = from_f<T>(acc[jo][t][4 * j + i]);
+          if (g.parts == 1 && !g.f32) out[o] = from_f<T>(acc[jo][t][4 * j + i]);
           else ws[(int64_t)split * K * RR * C + o] = acc[jo][t][4 * j + i];
         }
   }
@@ -529,7 +529,7 @@ bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo) {
 }
 
 int64_t conv_wgrad_workspace(const ConvWgradGeo& g, const ConvWgradArgs& a) {
-  return g.parts > 1 ? (int64_t)g.parts * a.K * a.C * a.R * a.R : 0;
+  return (g.parts > 1 || g.f32) ? (int64_t)g.parts * a.K * a.C * a.R * a.R : 0;
 }
 
 void conv_wgrad(int dt, const ConvWgradArgs& a, const ConvWgradGeo& g, float* ws, hipStream_t st, bool reduce) {

@@ -777,10 +777,11 @@ class _Conv1x1BNFn(torch.autograd.Function):
     epilogue, weight gradient on the MFMA wgrad kernel (or MIOpen, per shape)."""
 
     @staticmethod
-    def forward(ctx, x, weight, kshift, link_in, box, s2):
+    def forward(ctx, x, weight, kshift, link_in, box, s2, mlink=None):
         y, part = _c1x1_forward_stats(x, weight, kshift, s2)
         ctx.save_for_backward(x, weight)
         ctx.link_in, ctx.box, ctx.s2, ctx.wparam = link_in, box, s2, weight
+        ctx.mlink = mlink  # the producing block's ReLU mask (_MaskLink): applied in the data gradient's epilogue
         ctx.mark_non_differentiable(part)
         ctx.set_materialize_grads(False)
         return y, part
@@ -827,8 +828,15 @@ class _Conv1x1BNFn(torch.autograd.Function):
                 r2d = acc.permute(0, 2, 3, 1).reshape(-1, c) if acc is not None else None
                 link = ctx.link_in
                 fast = conv_bn.preferred(k, c, gy2d.size(0))
-                if fast and _link_ok(link, c) and conv_bn.supported(gy2d, w2d, resid=r2d is not None, epi="bwd",
-                                                                    b_trans=True):
+                ml = ctx.mlink
+                if ml is not None and conv_bn.supported(gy2d, w2d, resid=r2d is not None, epi="mask", b_trans=True) \
+                        and (fast or _MASK_PRODUCER_ANY):
+                    # dX = dY . W (+ the parked residual gradient), masked by the previous block's output ReLU,
+                    # with its column sums: that block's tail (_ConvBNResFn) skips its mask pass
+                    gx2d, part = conv_bn.c1x1(gy2d, w2d, resid=r2d, epi="mask", mbits=ml.bits, b_trans=True)
+                    ml.sg, ml.ptr = part[0], gx2d.data_ptr()
+                elif fast and _link_ok(link, c) and conv_bn.supported(gy2d, w2d, resid=r2d is not None, epi="bwd",
+                                                                      b_trans=True):
                     y2d = link.y.permute(0, 2, 3, 1).reshape(-1, c)
                     gx2d, part = conv_bn.c1x1(gy2d, w2d, resid=r2d, epi="bwd", by=y2d, bscale=link.scale,
                                               bshift=link.shift, bmean=link.mean, brelu=link.relu, b_trans=True)
@@ -857,7 +865,7 @@ class _Conv1x1BNFn(torch.autograd.Function):
             box["conv_done"] = True
         if ctx.needs_input_grad[1] and not side:
             gw = wfn()
-        return gx, gw, None, None, None, None
+        return gx, gw, None, None, None, None, None
 
 
 def _c1x1_forward_stats(x, weight, kshift, s2):
@@ -1132,6 +1140,230 @@ class _BNConvFn(torch.autograd.Function):
             g_conv, None, None, None
 
 
+class _MaskLink(object):
+    """Hands a residual block's saved ReLU bit mask to the node that produces the gradient of that block's
+    output (the next block's conv1 data gradient): it applies the mask in its epilogue and leaves the column
+    sums there (``sg``), and records the tensor it wrote (``ptr``) so the block's backward can tell that the
+    gradient it receives is exactly that one (autograd added nothing to it) and skip its own mask pass."""
+
+    __slots__ = ("bits", "ptr", "sg", "__weakref__")
+
+    def __init__(self, bits):
+        self.bits, self.ptr, self.sg = bits, None, None
+
+
+class _FoldCfg(object):
+    """Non-tensor arguments of :class:`_ConvBNResFn`: the BatchNorm modules (running statistics,
+    momentum, eps, process group) and the link of an unfolded bn2."""
+
+    __slots__ = ("bn_in", "bn_out", "link_in")
+
+    def __init__(self, bn_in, bn_out, link_in):
+        self.bn_in, self.bn_out, self.link_in = bn_in, bn_out, link_in
+
+
+def _bn_finalize(bn, part, count, world, bump_in_merge):
+    """Partials of a conv epilogue -> (mean, invstd, scale, shift, count) of the training BatchNorm ``bn``
+    (running statistics updated; one all-reduce across ranks). ``bump_in_merge``: the merge kernel also
+    advances num_batches_tracked (fixed momentum, one rank); else the caller's normalisation pass does."""
+    from ..ops import conv_bn
+    from ..ops import syncbn
+    from ..parallel.optimized_sync_batchnorm import _all_reduce
+    from ..parallel import comm_stats
+
+    mom = bn.momentum if bn.momentum is not None else -1.0
+    if world > 1:
+        sums = conv_bn.sum_parts(part, count)
+        with comm_stats.timed("syncbn_fwd", sums):
+            _all_reduce(sums, bn.process_group)
+        return syncbn.merge_sums(sums, bn.weight, bn.bias, bn.running_mean, bn.running_var, mom, bn.eps,
+                                 bn.num_batches_tracked)
+    return syncbn.merge_parts(part, count, bn.weight, bn.bias, bn.running_mean, bn.running_var, mom, bn.eps,
+                              bn.num_batches_tracked, bump_in_merge)
+
+
+class _ConvBNResFn(torch.autograd.Function):
+    """The tail of a bottleneck as ONE node: [bn2 + ReLU folded into the prologue] -> conv3 (1x1) -> bn3 ->
+    + z -> ReLU, whose backward never touches conv3's output y or bn3's input gradient (ops/bn_fold.py):
+
+    forward: conv3 (strip / tiled GEMM with bn3's statistics in the epilogue) -> merge -> one pass
+      out = relu(bn3(y) + z) that also stores the 1-bit ReLU mask. y is NOT saved.
+    backward, from g_out: g = mask * g_out with its column sums (one pass; g is also z's gradient) ->
+      P = g^T a (the weight-gradient kernel, fp32) and Gm = a^T a (Gram kernel over the 4x narrower a) ->
+      bn3's sums, dW3, dgamma3, dbeta3 from small matrices -> da = g @ Wa (GEMM) + a @ H + c (strip kernel,
+      with bn2's backward sums in its epilogue) -> bn2's data gradient (folded case).
+    Replaces bn3's backward-reduce and data-gradient passes over the [M, N] tensors (two reads of g_out and y,
+    writes of gx and dz) and the reads of gx by conv3's data and weight gradients.
+
+    ``src``: bn2's raw input y2 (``cfg.bn_in`` given: bn2 + ReLU in conv3's prologue) or the materialised a2
+    (``cfg.link_in``: the unfolded bn2's link, its backward sums come from the data-gradient epilogue)."""
+
+    @staticmethod
+    def forward(ctx, src, p_src, w3, bn_in_w, bn_in_b, bn_w, bn_b, z, cfg):
+        from ..ops import conv_bn
+        from ..ops import syncbn
+        from ..parallel.optimized_sync_batchnorm import _world
+
+        bn_in, bn = cfg.bn_in, cfg.bn_out
+        world = _world(bn.process_group)
+        n, K, h, w = src.shape
+        N = w3.size(0)
+        M = n * h * w
+        src2d = src.permute(0, 2, 3, 1).reshape(-1, K)
+        pro = None
+        if bn_in is not None:
+            nb_in = bn_in.num_batches_tracked
+            bumped = world == 1 and bn_in.momentum is not None
+            mean_i, invstd_i, scale_i, shift_i, count_i = _bn_finalize(bn_in, p_src, float(M), world, bumped)
+            if nb_in is not None and not bumped:
+                nb_in.add_(1)
+            pro = (scale_i, shift_i)
+            y2d, part = conv_bn.c1x1(src2d, w3.view(N, K), pro_scale=scale_i, pro_shift=shift_i, epi="stats",
+                                     kshift=_kshift(bn))
+            y = y2d.view(n, h, w, N).permute(0, 3, 1, 2)
+        else:
+            mean_i = invstd_i = scale_i = shift_i = count_i = None
+            y, part = _c1x1_forward_stats(src, w3, _kshift(bn), False)
+        mean, invstd, scale, shift, count = _bn_finalize(bn, part, float(M), world, False)
+        out, bits = syncbn.forward_mask(y, z, scale, shift, bn.num_batches_tracked)
+        ctx.save_for_backward(src, w3, y, bn_w, mean, invstd, count, bits, bn_in_w, mean_i, invstd_i, scale_i,
+                              shift_i, count_i)
+        ctx.cfg, ctx.world, ctx.pro = cfg, world, pro is not None
+        ctx.mlink = _MaskLink(bits) if _MASK_PRODUCER else None
+        if ctx.mlink is not None:
+            out._bh_mask = ctx.mlink  # read by the next block's conv1 (its data gradient masks for us)
+        ctx.mark_non_differentiable(bits)
+        return out
+
+    @staticmethod
+    def backward(ctx, g_out):
+        from ..ops import bn_fold
+        from ..ops import conv_bn
+        from ..ops import syncbn
+        from ..parallel.optimized_sync_batchnorm import _all_reduce_async
+        from ..parallel import comm_stats
+
+        src, w3, y, bn_w, mean, invstd, count, bits, bn_in_w, mean_i, invstd_i, scale_i, shift_i, count_i = \
+            ctx.saved_tensors
+        cfg = ctx.cfg
+        n, K, h, w = src.shape
+        N = w3.size(0)
+        g_out = g_out.contiguous(memory_format=torch.channels_last)
+        ml = ctx.mlink
+        if ml is not None and ml.ptr is not None and ml.ptr == g_out.data_ptr() and ml.sg is not None:
+            # the producer already applied the mask and summed the columns (and nothing was added since)
+            g2d, sg_ws = g_out.permute(0, 2, 3, 1).reshape(-1, N), ml.sg
+        else:  # (masking is idempotent: a gradient summed from a masked and an unmasked part is handled too)
+            g2d, sg_ws = bn_fold.mask_colsum_partials(g_out.permute(0, 2, 3, 1).reshape(-1, N), bits)
+        if ml is not None:
+            ml.ptr = ml.sg = None
+        g = g2d.view(n, h, w, N).permute(0, 3, 1, 2)  # bn3's masked output gradient = z's gradient
+        W = w3.view(N, K)
+        ps, ph = (scale_i, shift_i) if ctx.pro else (None, None)
+        src2d = src.permute(0, 2, 3, 1).reshape(-1, K)
+        # conv3's weight gradient and bn3's sums from P = g^T a and the Gram matrix of a (ops/bn_fold.py)
+        p_ws = bn_fold.wgrad_partials(src, g, ps, ph)
+        g_ws, sa_ws = bn_fold.gram_partials(src2d, ps, ph)
+        P, Gm, Sa, sums, bn_grads = bn_fold.fold_reduce(W, p_ws, g_ws, sa_ws, sg_ws, mean, invstd)
+        need_bn = bn_w is not None and (ctx.needs_input_grad[5] or ctx.needs_input_grad[6])
+        gw = bn_grads[:N].to(bn_w.dtype) if need_bn else None  # this rank's own (bn_grads is not all-reduced)
+        gb = bn_grads[N:].to(bn_w.dtype) if need_bn else None
+        if ctx.world > 1:
+            with comm_stats.timed("syncbn_bwd", sums):
+                _all_reduce_async(sums, cfg.bn_out.process_group).wait()
+        dW, abd = bn_fold.fold_finish(W, sums, count, mean, invstd, bn_w, P, Gm, Sa)
+        gw3 = dW.view(N, K, 1, 1)
+        if gw3.stride() != w3.stride():
+            gw3 = gw3.contiguous(memory_format=torch.channels_last)
+        # conv3's data gradient gx3 @ W3, gx3 = A g + B y + D: formed per fragment inside the strip GEMM where
+        # it runs, else one elementwise pass; the previous BatchNorm's backward sums in the epilogue
+        y2d = y.permute(0, 2, 3, 1).reshape(-1, N)
+        M = g2d.size(0)
+        if ctx.pro:
+            lk = (src2d, scale_i, shift_i, mean_i, True)
+        elif _link_ok(cfg.link_in, K):
+            l = cfg.link_in
+            lk = (l.y.permute(0, 2, 3, 1).reshape(-1, K), l.scale, l.shift, l.mean, l.relu)
+        else:
+            lk = None
+        s_i = None
+        epi = "bwd" if lk is not None else "plain"
+        if conv_bn.preferred(N, K, M) and conv_bn.supported(g2d, W, epi=epi, b_trans=True, bnb=True):
+            kw = dict(epi=epi, by=lk[0], bscale=lk[1], bshift=lk[2], bmean=lk[3], brelu=lk[4]) if lk else {}
+            da2d, part = conv_bn.c1x1(g2d, W, b_trans=True, bnb=abd, bnb_y=y2d, **kw)
+            if lk is not None:
+                s_i = conv_bn.sum_parts(part)
+        else:
+            gx3, _ = syncbn.backward_dgrad(g, y, None, mean, invstd, bn_w, sums, count, None, None, False, False, None)
+            gx3 = gx3.permute(0, 2, 3, 1).reshape(-1, N)
+            da2d, s_i = _dgrad_bn_sums(gx3, W, lk)
+        da = da2d.view(n, h, w, K).permute(0, 3, 1, 2)
+        gw_i = gb_i = None
+        if ctx.pro:
+            need_i = bn_in_w is not None and (ctx.needs_input_grad[3] or ctx.needs_input_grad[4])
+            if s_i is None:
+                s_i, gw_i, gb_i = syncbn.backward_reduce(da, src, None, mean_i, invstd_i, scale_i, shift_i, True,
+                                                         bn_in_w, need_i, None)
+            elif need_i:
+                gw_i = (s_i[K:] * invstd_i).to(bn_in_w.dtype)
+                gb_i = s_i[:K].to(bn_in_w.dtype, copy=True)  # (s_i is all-reduced in place below)
+            if ctx.world > 1:
+                with comm_stats.timed("syncbn_bwd", s_i):
+                    _all_reduce_async(s_i, cfg.bn_in.process_group).wait()
+            gx, _ = syncbn.backward_dgrad(da, src, None, mean_i, invstd_i, bn_in_w, s_i, count_i, scale_i, shift_i,
+                                          True, False, None)
+            if not need_i:
+                gw_i = gb_i = None
+        else:
+            if s_i is not None:
+                cfg.link_in.sums = s_i
+            gx = da
+        return gx, None, gw3, gw_i, gb_i, gw, gb, g, None
+
+
+def _dgrad_bn_sums(gy2d, w2d, lk):
+    """``gy2d @ w2d`` (``w2d [N, K]``: the data gradient of a 1x1 convolution) with the backward sums of the
+    BatchNorm ``lk = (y2d, scale, shift, mean, relu)`` that produced its input in the epilogue where an own
+    kernel runs (strip GEMM or tiled MFMA GEMM), else hipBLASLt: ``(dA2d, sums or None)``."""
+    from ..ops import conv_bn
+
+    N, K = w2d.shape
+    M = gy2d.size(0)
+    if conv_bn.preferred(N, K, M) and conv_bn.supported(gy2d, w2d, epi="bwd" if lk else "plain", b_trans=True):
+        if lk is not None:
+            da, part = conv_bn.c1x1(gy2d, w2d, epi="bwd", by=lk[0], bscale=lk[1], bshift=lk[2], bmean=lk[3],
+                                    brelu=lk[4], b_trans=True)
+            return da, conv_bn.sum_parts(part)
+        return conv_bn.c1x1(gy2d, w2d, b_trans=True)[0], None
+    if _own("bwd" if lk else "plain") and conv_bn.gemm_bn_supported(gy2d, w2d.t()):
+        wt = _tr(w2d)
+        if lk is not None:
+            da, part = conv_bn.gemm_bn(gy2d, wt, "bwd", by=lk[0], bscale=lk[1], bshift=lk[2], bmean=lk[3], brelu=lk[4])
+            return da, conv_bn.sum_parts(part)
+        return conv_bn.gemm_bn(gy2d, wt, "plain")[0], None
+    return torch.mm(gy2d, w2d), None
+
+
+def _conv_bn_res_ok(src, w3, z, pro):
+    """Whether :class:`_ConvBNResFn` covers the shapes (else the per-layer path runs). ``BH_BN_RES_FOLD``:
+    "pro" (default) only where bn2 is folded into conv3's prologue (the HBM-bound 56x56 / 28x28 stages),
+    "all" also the wider stages, "0" never."""
+    from ..ops import conv as bhconv
+    from ..ops import syncbn
+
+    if _BN_RES_FOLD == "0" or (_BN_RES_FOLD == "pro" and not pro):
+        return False
+    if not (src.is_cuda and z is not None and z.dtype == src.dtype and
+            z.is_contiguous(memory_format=torch.channels_last) and src.is_contiguous(memory_format=torch.channels_last)):
+        return False
+    n, K, h, w = src.shape
+    N = w3.size(0)
+    if tuple(z.shape) != (n, N, h, w) or K % 64 or N % 64 or w3.dtype != src.dtype:
+        return False
+    # z stands in for conv3's output (same shape, dtype and layout) in the shape checks
+    return syncbn.mask_ok(z, z) and bhconv.wgrad_supported(src, z, 1)
+
+
 def _bn_conv(bn, y, part, conv_w, kshift_out, R, stride=1):
     exp_avg = bn.momentum if bn.momentum is not None else -1.0
     return _BNConvFn.apply(y, part, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps, exp_avg,
@@ -1172,6 +1404,15 @@ _OWN_GEMM = bool(_OWN_GEMM_KINDS)
 def _own(kind):
     return kind in _OWN_GEMM_KINDS
 _FOLD_3X3_BWD = os.environ.get("BH_FOLD_3X3_BWD", "0") == "1"
+# bottleneck tail (conv3 -> bn3 -> + z -> ReLU) as one node whose backward folds bn3 into conv3 by linear
+# algebra (_ConvBNResFn); BH_BN_RES_FOLD=0 keeps the per-layer nodes (A/B)
+_BN_RES_FOLD = {"1": "pro"}.get(os.environ.get("BH_BN_RES_FOLD", "pro"), os.environ.get("BH_BN_RES_FOLD", "pro"))
+assert _BN_RES_FOLD in ("pro", "all", "0"), f"BH_BN_RES_FOLD={_BN_RES_FOLD!r}"
+# the next block's conv1 data gradient applies the tail's ReLU mask in its epilogue, on the strip kernel
+# also where hipBLASLt's residual GEMM ran before ("any", default); "1": only where the strip kernel is
+# preferred anyway; "0": the tail's own mask pass. Same box: 0 11102, 1 11195, any 11286 img/s
+_MASK_PRODUCER = os.environ.get("BH_MASK_PRODUCER", "any") != "0"
+_MASK_PRODUCER_ANY = os.environ.get("BH_MASK_PRODUCER", "any") == "any"
 
 
 class Bottleneck(nn.Module):
@@ -1231,7 +1472,7 @@ class Bottleneck(nn.Module):
             box = None
         else:
             box = {} if (torch.is_grad_enabled() and x.requires_grad) else None
-            y1, p1 = _Conv1x1BNFn.apply(x, w1, _kshift(self.bn1), None, box, False)
+            y1, p1 = _Conv1x1BNFn.apply(x, w1, _kshift(self.bn1), None, box, False, getattr(x, "_bh_mask", None))
         l2 = None
         y3 = None
         y2 = None
@@ -1252,13 +1493,31 @@ class Bottleneck(nn.Module):
                 y2, p2 = _Conv3x3BNFn.apply(a1, w2, _kshift(self.bn2), l1)
             else:  # stride-2 3x3 (MIOpen): its BatchNorm computes its own statistics
                 a2 = self.bn2(self.conv2(a1))
-        if y2 is not None:
-            if _FOLD_APPLY in ("all", "bn2") and self._fold_bn2(y2):
-                # bn2 + ReLU inside conv3's strip-GEMM prologue (statistics of bn3 in its epilogue)
+        fold2 = y2 is not None and _FOLD_APPLY in ("all", "bn2") and self._fold_bn2(y2)
+        if y2 is not None and not fold2:
+            l2 = BNLink()
+            a2 = self.bn2.forward_from_stats(y2, p2, link=l2)
+        src = y2 if fold2 else a2
+        # the tail as one node (conv3 -> bn3 -> + z -> ReLU, bn3's backward folded into conv3's): z is the
+        # block input or the downsample BatchNorm's output, both shaped like conv3's output
+        if _conv_bn_res_ok(src, w3, yd if ds is not None else x, fold2):
+            if ds is not None:
+                identity = ds[1].forward_from_stats(yd, pd)
+            else:
+                identity = _GradStash.apply(x, box) if box is not None else x
+            if _conv_bn_res_ok(src, w3, identity, fold2):
+                cfg = _FoldCfg(self.bn2 if fold2 else None, self.bn3, None if fold2 else l2)
+                return _ConvBNResFn.apply(src, p2 if fold2 else None, w3, self.bn2.weight if fold2 else None,
+                                          self.bn2.bias if fold2 else None, self.bn3.weight, self.bn3.bias, identity,
+                                          cfg)
+            if fold2:
                 y3, p3 = _bn_conv(self.bn2, y2, p2, w3, _kshift(self.bn3), 1)
             else:
-                l2 = BNLink()
-                a2 = self.bn2.forward_from_stats(y2, p2, link=l2)
+                y3, p3 = _Conv1x1BNFn.apply(a2, w3, _kshift(self.bn3), l2, None, False)
+            return self.bn3.forward_from_stats(y3, p3, z=identity)
+        if fold2:
+            # bn2 + ReLU inside conv3's strip-GEMM prologue (statistics of bn3 in its epilogue)
+            y3, p3 = _bn_conv(self.bn2, y2, p2, w3, _kshift(self.bn3), 1)
         if y3 is None:
             y3, p3 = _Conv1x1BNFn.apply(a2, w3, _kshift(self.bn3), l2, None, False)
         if ds is not None:

@@ -24,7 +24,7 @@ import torch
 
 from .._native import available, submodule
 
-_EPI = {"plain": 0, "stats": 1, "bwd": 2, "affine": 3}
+_EPI = {"plain": 0, "stats": 1, "bwd": 2, "affine": 3, "mask": 4}
 
 
 def _gather_s2(a: torch.Tensor, s2) -> torch.Tensor:
@@ -33,21 +33,33 @@ def _gather_s2(a: torch.Tensor, s2) -> torch.Tensor:
     return a.view(-1, H, W, K)[:, ::2, ::2, :].reshape(-1, K)
 
 
-def _reference(a, b, pro_scale, pro_shift, resid, s2, epi, kshift, by, bscale, bshift, bmean, brelu):
+def _bit_mask(bits, M, N):
+    return ((bits.view(M, N // 8, 1).to(torch.int32) >> torch.arange(8, dtype=torch.int32)) & 1).view(M, N).bool()
+
+
+def _reference(a, b, pro_scale, pro_shift, resid, s2, epi, kshift, by, bscale, bshift, bmean, brelu, bnb=None,
+               bnb_y=None, mbits=None):
     if s2 is not None:
         a = _gather_s2(a, s2)
     af = a.float()
     if pro_scale is not None:
         af = torch.relu(af * pro_scale + pro_shift).to(a.dtype).float()
+    if bnb is not None:
+        K = a.size(1)
+        af = (af * bnb[:K] + bnb_y.float() * bnb[K:2 * K] + bnb[2 * K:]).to(a.dtype).float()
     c = af @ b.float().t()
     if resid is not None:
         c = c + resid.float()
+    N = b.size(0)
+    if epi == "mask":
+        c = torch.where(_bit_mask(mbits, c.size(0), N), c, torch.zeros_like(c))
     c = c.to(a.dtype)
     cf = c.float()
-    N = b.size(0)
     if epi == "stats":
         d = cf - (kshift if kshift is not None else 0.0)
         part = torch.stack([d.sum(0), (d * d).sum(0)]).view(2, 1, N)
+    elif epi == "mask":
+        part = torch.stack([cf.sum(0), torch.zeros_like(cf[0])]).view(2, 1, N)
     elif epi == "bwd":
         y = by.float()
         dz = cf * ((y * bscale + bshift) > 0).float() if brelu else cf
@@ -62,8 +74,13 @@ def c1x1(a: torch.Tensor, b: torch.Tensor, pro_scale: Optional[torch.Tensor] = N
          epi: str = "plain", kshift: Optional[torch.Tensor] = None, by: Optional[torch.Tensor] = None,
          bscale: Optional[torch.Tensor] = None, bshift: Optional[torch.Tensor] = None,
          bmean: Optional[torch.Tensor] = None, brelu: bool = True,
-         b_trans: bool = False, s2_scatter: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+         b_trans: bool = False, s2_scatter: bool = False, bnb: Optional[torch.Tensor] = None,
+         bnb_y: Optional[torch.Tensor] = None, mbits: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """``b_trans``: ``b`` is given as ``[K, N]`` (e.g. a forward weight for the data gradient).
+    ``bnb`` (fp32 ``[3K]`` = A, B, D) with ``bnb_y`` (shaped like ``a``): the BatchNorm-backward prologue
+    ``f(a) = A * a + B * bnb_y + D`` per input channel, rounded to a's dtype (ops/bn_fold.py).
+    ``epi="mask"`` with ``mbits`` (uint8 ``[M, N/8]``, syncbn.forward_mask's ReLU bits): C is masked and
+    ``part[0]`` holds its column-sum partials.
     ``s2_scatter`` (with ``s2=(H, W)`` and ``resid`` the full-resolution ``[N*H*W, N]`` tensor): row
     (n, y, x) of ``a @ b.T`` is ADDED in place into row (n, 2y, 2x) of ``resid``, which is returned --
     the 1x1 / stride-2 data gradient accumulated onto the other branch's gradient."""
@@ -77,10 +94,11 @@ def c1x1(a: torch.Tensor, b: torch.Tensor, pro_scale: Optional[torch.Tensor] = N
             view = resid.view(-1, H, W, resid.size(1))[:, ::2, ::2, :]
             view.copy_((view.float() + add.view(view.shape)).to(resid.dtype))
             return resid, torch.empty(0)
-        return _reference(a, bb, pro_scale, pro_shift, resid, s2, epi, kshift, by, bscale, bshift, bmean, brelu)
+        return _reference(a, bb, pro_scale, pro_shift, resid, s2, epi, kshift, by, bscale, bshift, bmean, brelu, bnb,
+                          bnb_y, mbits)
     H, W = s2 if s2 is not None else (0, 0)
     return submodule("conv_bn").c1x1(a, b, b_trans, M, pro_scale, pro_shift, resid, H, W, _EPI[epi], kshift, by,
-                                     bscale, bshift, bmean, brelu, s2_scatter)
+                                     bscale, bshift, bmean, brelu, s2_scatter, bnb=bnb, bnb_y=bnb_y, mbits=mbits)
 
 
 def c1x1_affine(a: torch.Tensor, b: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, relu: bool = True,
@@ -104,12 +122,12 @@ def c1x1_affine(a: torch.Tensor, b: torch.Tensor, scale: torch.Tensor, shift: to
 
 
 def supported(a: torch.Tensor, b: torch.Tensor, pro: bool = False, resid: bool = False, s2=None,
-              epi: str = "plain", b_trans: bool = False, s2_scatter: bool = False) -> bool:
+              epi: str = "plain", b_trans: bool = False, s2_scatter: bool = False, bnb: bool = False) -> bool:
     if not (a.is_cuda and available()):
         return False
     H, W = s2 if s2 is not None else (0, 0)
     M = a.size(0) // 4 if (s2 is not None and not s2_scatter) else a.size(0)
-    return submodule("conv_bn").c1x1_supported(a, b, b_trans, M, pro, resid, H, W, _EPI[epi], s2_scatter)
+    return submodule("conv_bn").c1x1_supported(a, b, b_trans, M, pro, resid, H, W, _EPI[epi], s2_scatter, bnb)
 
 
 def preferred(K: int, N: int, M: int, s2: bool = False) -> bool:

@@ -1,0 +1,274 @@
+"""BatchNorm backward folded into the 1x1 convolution by linear algebra (ops/bn_fold.py, kernels/bn_fold.hip,
+models/resnet.py ``_ConvBNResFn``).
+
+CPU: the algebra itself (P, Gm, sums -> dW, da, dgamma, dbeta, dz) against autograd through
+conv -> batch_norm -> + z -> ReLU in fp64. GPU: each kernel (Gram with / without the BatchNorm prologue, mask +
+column sums, fp32 weight-gradient partials, the strip GEMM's prologue + residual + bias + backward-sums
+epilogue) against an fp32 PyTorch reference, and the fused bottleneck tail against the per-layer path."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from beforeholiday_amd.ops import bn_fold
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def test_fold_algebra_matches_autograd_fp64():
+    torch.manual_seed(0)
+    M, K, N, eps = 2048, 16, 64, 1e-5
+    dt = torch.float64
+    a = torch.relu(torch.randn(M, K, dtype=dt)).requires_grad_()
+    W = (torch.randn(N, K, dtype=dt) * 0.3).requires_grad_()
+    gam = (torch.rand(N, dtype=dt) + 0.5).requires_grad_()
+    bet = (torch.randn(N, dtype=dt) * 0.1).requires_grad_()
+    z = torch.randn(M, N, dtype=dt).requires_grad_()
+    y = a @ W.t()
+    out = torch.relu(F.batch_norm(y, None, None, gam, bet, training=True, eps=eps) + z)
+    gout = torch.randn(M, N, dtype=dt)
+    out.backward(gout)
+    with torch.no_grad():
+        yv = a @ W.t()
+        mean = yv.mean(0)
+        invstd = (yv.var(0, unbiased=False) + eps).rsqrt()
+        g = gout * (out > 0)
+        P = g.t() @ a
+        Gm, Sa = a.t() @ a, a.sum(0)
+        sums = bn_fold.local_sums(W, P.float(), g.sum(0).float(), mean.float()).double()
+        dW, abd = bn_fold.combine(W, P, Gm, Sa, sums, mean, invstd, gam, torch.tensor([float(M)]))
+        gx = abd[:N] * g + abd[N:2 * N] * yv + abd[2 * N:]
+        da = gx @ W
+    assert _rel(da, a.grad) < 1e-5
+    assert _rel(dW, W.grad) < 1e-5
+    assert _rel(sums[N:] * invstd, gam.grad) < 1e-5
+    assert _rel(sums[:N], bet.grad) < 1e-5
+    assert _rel(g, z.grad) == 0.0
+
+
+def test_cpu_references_of_the_kernels():
+    torch.manual_seed(1)
+    a = torch.randn(300, 64)
+    s, t = torch.rand(64) + 0.5, torch.randn(64) * 0.1
+    Gm, Sa = bn_fold.gram(a, s, t)
+    ap = torch.relu(a * s + t)
+    torch.testing.assert_close(Gm, ap.t() @ ap)
+    torch.testing.assert_close(Sa, ap.sum(0))
+    g = torch.randn(300, 16)
+    bits = torch.randint(0, 256, (300, 2), dtype=torch.uint8)
+    gp, sg = bn_fold.mask_colsum(g, bits)
+    m = torch.stack([(bits[:, c // 8].int() >> (c % 8)) & 1 for c in range(16)], 1).bool()
+    torch.testing.assert_close(gp, torch.where(m, g, torch.zeros_like(g)))
+    torch.testing.assert_close(sg, gp.sum(0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("M,K", [(4096, 64), (1000, 128), (3136, 256), (777, 512)])
+@pytest.mark.parametrize("pro", [False, True])
+def test_gram_kernel(M, K, pro, dt):
+    torch.manual_seed(0)
+    a = torch.randn(M, K, device="cuda").to(dt)
+    s = (torch.rand(K, device="cuda") + 0.5) if pro else None
+    t = (torch.randn(K, device="cuda") * 0.2) if pro else None
+    Gm, Sa = bn_fold.gram(a, s, t)
+    Gr, Sr = bn_fold.gram(a.cpu(), s.cpu() if pro else None, t.cpu() if pro else None)
+    assert _rel(Gm, Gr) < 1e-5
+    assert _rel(Sa, Sr) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("M,N", [(8192, 256), (999, 64), (3136, 2048)])
+def test_mask_colsum_kernel(M, N, dt):
+    torch.manual_seed(0)
+    g = torch.randn(M, N, device="cuda").to(dt)
+    bits = torch.randint(0, 256, (M, N // 8), dtype=torch.uint8, device="cuda")
+    gp, sg = bn_fold.mask_colsum(g, bits)
+    gr, sr = bn_fold.mask_colsum(g.cpu(), bits.cpu())
+    assert torch.equal(gp.cpu(), gr)
+    assert _rel(sg, sr) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(8, 64, 56, 56, 256), (4, 128, 28, 28, 512), (64, 512, 7, 7, 2048)])
+@pytest.mark.parametrize("pro", [False, True])
+def test_wgrad_f32_partials(shape, pro):
+    n, C, h, w, K = shape
+    torch.manual_seed(0)
+    x = torch.randn(n, C, h, w, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(n, K, h, w, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    s = (torch.rand(C, device="cuda") + 0.5) if pro else None
+    t = (torch.randn(C, device="cuda") * 0.2) if pro else None
+    P = bn_fold.wgrad_f32(x, dy, s, t)
+    assert P.dtype == torch.float32 and P.shape == (K, C)
+    Pr = bn_fold.wgrad_f32(x.cpu(), dy.cpu(), s.cpu() if pro else None, t.cpu() if pro else None)
+    assert _rel(P, Pr) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("K,N", [(256, 64), (128, 64), (256, 128)])
+@pytest.mark.parametrize("epi", ["bwd", "plain"])
+def test_c1x1_batchnorm_backward_prologue(K, N, epi, dt):
+    """The strip kernel's BatchNorm-backward prologue: (A g + B y + D) @ W with the previous BatchNorm's
+    backward sums in the epilogue -- conv3's data gradient in _ConvBNResFn."""
+    from beforeholiday_amd.ops import conv_bn
+
+    torch.manual_seed(0)
+    M = 8192
+    g = torch.randn(M, K, device="cuda").to(dt)
+    y = torch.randn(M, K, device="cuda").to(dt)
+    W = (torch.randn(K, N, device="cuda") / K ** 0.5).to(dt)  # [K, N]: b_trans
+    abd = torch.cat([torch.rand(K, device="cuda") + 0.5, torch.randn(K, device="cuda") * 0.3,
+                     torch.randn(K, device="cuda") * 0.1])
+    by = torch.randn(M, N, device="cuda").to(dt)
+    s, t, mu = torch.rand(N, device="cuda") + 0.5, torch.randn(N, device="cuda") * 0.2, torch.randn(N, device="cuda")
+    kw = dict(epi=epi, b_trans=True, bnb=abd, bnb_y=y)
+    if epi == "bwd":
+        kw.update(by=by, bscale=s, bshift=t, bmean=mu, brelu=True)
+    assert conv_bn.supported(g, W, epi=epi, b_trans=True, bnb=True)
+    out, part = conv_bn.c1x1(g, W, **kw)
+    cpu = {k: (v.cpu() if torch.is_tensor(v) else v) for k, v in kw.items()}
+    ref, pref = conv_bn.c1x1(g.cpu(), W.cpu(), **cpu)
+    tol = 2e-3 if dt == torch.float16 else 1.5e-2
+    assert _rel(out, ref) < tol
+    if epi == "bwd":
+        assert _rel(conv_bn.sum_parts(part), conv_bn.sum_parts(pref)) < tol
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [(256, 64, 1, 56), (64, 64, 1, 56), (256, 128, 2, 56), (512, 128, 1, 28),
+                                 (1024, 256, 1, 14), (2048, 512, 1, 7)])
+def test_fused_tail_matches_per_layer_path(cfg):
+    """The same fp16 block with the tail as one node (_ConvBNResFn) and as per-layer nodes: outputs equal
+    (same forward kernels), every gradient within fp16 rounding, running statistics and
+    num_batches_tracked identical."""
+    from test_resnet_fold import _block
+
+    inplanes, planes, stride, hw = cfg
+    R, _, blk = _block(inplanes, planes, stride, torch.float16)
+    x = torch.randn(4, inplanes, hw, hw, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    g = torch.randn(4, planes * 4, (hw + stride - 1) // stride, (hw + stride - 1) // stride, device="cuda").half()
+    g = g.contiguous(memory_format=torch.channels_last)
+    old = R._BN_RES_FOLD
+    res = []
+    state0 = {k: v.clone() for k, v in blk.state_dict().items()}
+    try:
+        for on in (True, False):
+            R._BN_RES_FOLD = "all" if on else "0"
+            blk.load_state_dict(state0)
+            blk.zero_grad(set_to_none=True)
+            xi = x.clone().requires_grad_()
+            out = blk(xi)
+            out.backward(g)
+            res.append((out.detach().clone(), xi.grad.clone(), {n: p.grad.clone() for n, p in blk.named_parameters()},
+                        {n: b.clone() for n, b in blk.named_buffers()}))
+    finally:
+        R._BN_RES_FOLD = old
+    (o1, gx1, pg1, b1), (o2, gx2, pg2, b2) = res
+    assert torch.equal(o1, o2)
+    assert _rel(gx1, gx2) < 2e-2
+    for n in pg2:
+        assert _rel(pg1[n], pg2[n]) < 2e-2, n
+    for n in b2:
+        if "num_batches" in n:
+            assert int(b1[n]) == int(b2[n]), n
+        else:
+            assert _rel(b1[n], b2[n]) < 1e-5, n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [(256, 64, 1, 56), (256, 128, 2, 56), (512, 128, 1, 28), (1024, 256, 1, 14)])
+@pytest.mark.parametrize("loss", ["randn", "square"])
+def test_fused_tail_accuracy_vs_fp32(cfg, loss):
+    """Against the fp32 nn.Conv2d / nn.BatchNorm2d block, the folded tail is at least as accurate as the
+    per-layer 16-bit path (it skips the fp16 rounding of conv3's output gradient), for a random output
+    gradient and for the ill-conditioned square loss."""
+    from test_resnet_fold import _block
+
+    inplanes, planes, stride, hw = cfg
+    R, ref, blk = _block(inplanes, planes, stride, torch.float16)
+    x = torch.randn(8, inplanes, hw, hw, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    xr = x.float().clone().requires_grad_()
+    out_r = ref(xr)
+    g = torch.randn_like(out_r) if loss == "randn" else 2 * out_r.detach()
+    out_r.backward(g)
+    errs = {}
+    old = R._BN_RES_FOLD
+    state0 = {k: v.clone() for k, v in blk.state_dict().items()}
+    try:
+        for on in (True, False):
+            R._BN_RES_FOLD = "all" if on else "0"
+            blk.load_state_dict(state0)
+            blk.zero_grad(set_to_none=True)
+            xi = x.clone().requires_grad_()
+            out = blk(xi)
+            out.backward(g.half() if loss == "randn" else 2 * out.detach())
+            e = {"x": _rel(xi.grad, xr.grad)}
+            for (n, p), q in zip(blk.named_parameters(), ref.parameters()):
+                e[n] = _rel(p.grad, q.grad)
+            errs[on] = e
+    finally:
+        R._BN_RES_FOLD = old
+    for n in errs[False]:
+        assert errs[True][n] <= 1.25 * errs[False][n] + 3e-3, (n, errs[True][n], errs[False][n])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("K,N", [(64, 256), (128, 512)])
+@pytest.mark.parametrize("resid", [True, False])
+def test_c1x1_mask_epilogue(K, N, resid, dt):
+    """The strip kernel's residual-ReLU mask epilogue: C = (A @ W (+ R)) * bit, column sums of C."""
+    from beforeholiday_amd.ops import conv_bn
+
+    torch.manual_seed(0)
+    M = 8192
+    a = torch.randn(M, K, device="cuda").to(dt)
+    W = (torch.randn(K, N, device="cuda") / K ** 0.5).to(dt)
+    R = torch.randn(M, N, device="cuda").to(dt) if resid else None
+    bits = torch.randint(0, 256, (M, N // 8), dtype=torch.uint8, device="cuda")
+    assert conv_bn.supported(a, W, resid=resid, epi="mask", b_trans=True)
+    out, part = conv_bn.c1x1(a, W, resid=R, epi="mask", mbits=bits, b_trans=True)
+    ref, pref = conv_bn.c1x1(a.cpu(), W.cpu(), resid=R.cpu() if resid else None, epi="mask", mbits=bits.cpu(),
+                             b_trans=True)
+    tol = 2e-3 if dt == torch.float16 else 1.5e-2
+    assert _rel(out, ref) < tol
+    assert torch.equal(out.cpu() == 0, ref == 0) or _rel(out, ref) < tol
+    assert _rel(part[0].sum(0), pref[0].sum(0)) < tol
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["1", "any"])
+def test_mask_in_producer_matches_own_pass(mode):
+    """Two consecutive identity blocks (the second one's conv1 data gradient masks the first one's tail
+    gradient in its epilogue): same gradients as with the first block's own mask pass."""
+    from test_resnet_fold import _block
+
+    R, _, b1 = _block(256, 64, 1, torch.float16)
+    _, _, b2 = _block(256, 64, 1, torch.float16)
+    x = torch.randn(8, 256, 56, 56, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    g = torch.randn(8, 256, 56, 56, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    oldp, olda = R._MASK_PRODUCER, R._MASK_PRODUCER_ANY
+    s1 = {k: v.clone() for k, v in b1.state_dict().items()}
+    s2 = {k: v.clone() for k, v in b2.state_dict().items()}
+    res = []
+    try:
+        for on in (True, False):
+            R._MASK_PRODUCER, R._MASK_PRODUCER_ANY = on, on and mode == "any"
+            b1.load_state_dict(s1)
+            b2.load_state_dict(s2)
+            for b in (b1, b2):
+                b.zero_grad(set_to_none=True)
+            xi = x.clone().requires_grad_()
+            out = b2(b1(xi))
+            out.backward(g)
+            res.append((xi.grad.clone(), [p.grad.clone() for p in list(b1.parameters()) + list(b2.parameters())]))
+    finally:
+        R._MASK_PRODUCER, R._MASK_PRODUCER_ANY = oldp, olda
+    assert _rel(res[0][0], res[1][0]) < 1e-2
+    for a, b in zip(res[0][1], res[1][1]):
+        assert _rel(a, b) < 1e-2

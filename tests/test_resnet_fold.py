@@ -88,9 +88,12 @@ def test_folded_and_unfolded_paths_agree():
     finally:
         R._FOLD_BN = old
     assert _rel(outs[0][0], outs[1][0]) < 5e-3
-    assert _rel(outs[0][1], outs[1][1]) < 2e-2
+    # the folded path's bottleneck tail computes bn3's backward algebraically (no fp16 rounding of conv3's
+    # output gradient), so the two 16-bit paths round differently; tests/test_bn_fold.py checks that the
+    # folded one is at least as close to fp32
+    assert _rel(outs[0][1], outs[1][1]) < 3e-2
     for a, b in zip(outs[0][2], outs[1][2]):
-        assert _rel(a, b) < 2e-2
+        assert _rel(a, b) < 3e-2
 
 
 @pytest.mark.gpu
@@ -114,7 +117,8 @@ def test_bn_apply_folded_into_conv2_and_conv3(cfg):  # BH_FOLD_APPLY=all vs none
             blk.load_state_dict(state0)
             xx = x.clone().requires_grad_()
             o = blk(xx)
-            o.float().square().mean().backward()
+            # per-sample mean: .mean() puts the fp16 gradients in the subnormal range, .sum() overflows them
+            (o.float().square().sum() / x.shape[0]).backward()
             outs.append((o.detach(), xx.grad, [p.grad.clone() for p in blk.parameters()],
                          {k: v.clone() for k, v in blk.state_dict().items()}))
             for p in blk.parameters():
@@ -122,9 +126,12 @@ def test_bn_apply_folded_into_conv2_and_conv3(cfg):  # BH_FOLD_APPLY=all vs none
     finally:
         R._FOLD_APPLY = old
     assert _rel(outs[0][0], outs[1][0]) < 5e-3
-    assert _rel(outs[0][1], outs[1][1]) < 2e-2
+    # the folded path's bottleneck tail computes bn3's backward algebraically (no fp16 rounding of conv3's
+    # output gradient), so the two 16-bit paths round differently; tests/test_bn_fold.py checks that the
+    # folded one is at least as close to fp32
+    assert _rel(outs[0][1], outs[1][1]) < 3e-2
     for a, b in zip(outs[0][2], outs[1][2]):
-        assert _rel(a, b) < 2e-2
+        assert _rel(a, b) < 3e-2
     for k in outs[0][3]:
         if "running" in k:
             assert _rel(outs[0][3][k], outs[1][3][k]) < 1e-3, k
