@@ -72,7 +72,8 @@ std::vector<at::Tensor> c1x1(const at::Tensor& a, const at::Tensor& b, bool b_tr
                              const c10::optional<at::Tensor>& bmean, bool brelu, bool s2_scatter,
                              const c10::optional<at::Tensor>& a_scale, const c10::optional<at::Tensor>& a_shift,
                              bool relu, bool r_mul, const c10::optional<at::Tensor>& bnb,
-                             const c10::optional<at::Tensor>& bnb_y, const c10::optional<at::Tensor>& mbits) {
+                             const c10::optional<at::Tensor>& bnb_y, const c10::optional<at::Tensor>& mbits,
+                             int64_t lda) {
   at::Tensor c;
   if (s2_scatter) {
     // accumulate into the full-resolution tensor `resid` in place: a is [M, K], resid [4M, N]
@@ -83,7 +84,13 @@ std::vector<at::Tensor> c1x1(const at::Tensor& a, const at::Tensor& b, bool b_tr
                 "conv_bn.c1x1: the stride-2 scatter accumulates into a contiguous [4M, N] resid");
     c = *resid;
   }
-  bh::C1x1Args p = make_args(a, b, b_trans, M, pro_scale, pro_shift, s2_scatter ? c10::optional<at::Tensor>() : resid,
+  // lda > 0: a (and bnb_y) are [M, K] column slices of row-major [M, lda] tensors
+  TORCH_CHECK(lda == 0 || (a.dim() == 2 && a.stride(1) == 1 && a.stride(0) == lda &&
+                           (!bnb_y.has_value() || !bnb_y->defined() ||
+                            (bnb_y->dim() == 2 && bnb_y->stride(1) == 1 && bnb_y->stride(0) == lda))),
+              "conv_bn.c1x1: lda must equal the row stride of a (and bnb_y)");
+  bh::C1x1Args p = make_args(lda ? a.as_strided({a.size(0), a.size(1)}, {a.size(1), 1}) : a, b, b_trans, M, pro_scale,
+                             pro_shift, s2_scatter ? c10::optional<at::Tensor>() : resid,
                              s2_scatter ? 0 : s2_h, s2_scatter ? 0 : s2_w, epi, kshift, by, bscale, bshift, bmean,
                              brelu);
   if (s2_scatter) {
@@ -104,10 +111,12 @@ std::vector<at::Tensor> c1x1(const at::Tensor& a, const at::Tensor& b, bool b_tr
   if (bnb.has_value() && bnb->defined()) {
     p.bnb = fptr(bnb, 3 * (int64_t)p.K, "bnb");
     TORCH_CHECK(bnb_y.has_value() && bnb_y->defined() && bnb_y->is_cuda() && bnb_y->device() == a.device() &&
-                    bnb_y->scalar_type() == a.scalar_type() && bnb_y->is_contiguous() && bnb_y->sizes() == a.sizes(),
-                "conv_bn.c1x1: bnb_y must be a contiguous tensor shaped like a, of a's dtype");
+                    bnb_y->scalar_type() == a.scalar_type() && (lda ? true : bnb_y->is_contiguous()) &&
+                    bnb_y->sizes() == a.sizes(),
+                "conv_bn.c1x1: bnb_y must be a tensor shaped (and strided) like a, of a's dtype");
     p.bnb_y = bnb_y->data_ptr();
   }
+  p.lda = (int)lda;
   if (epi == bh::kC1x1Mask) {
     TORCH_CHECK(mbits.has_value() && mbits->defined() && mbits->is_cuda() && mbits->device() == a.device() &&
                     mbits->scalar_type() == at::kByte && mbits->is_contiguous() && mbits->numel() == M * p.N / 8,
@@ -236,7 +245,7 @@ void register_conv_bn(pybind11::module_& root) {
         py::arg("bshift") = py::none(), py::arg("bmean") = py::none(), py::arg("brelu") = true,
         py::arg("s2_scatter") = false, py::arg("a_scale") = py::none(), py::arg("a_shift") = py::none(),
         py::arg("relu") = false, py::arg("r_mul") = false, py::arg("bnb") = py::none(), py::arg("bnb_y") = py::none(),
-        py::arg("mbits") = py::none());
+        py::arg("mbits") = py::none(), py::arg("lda") = 0);
   m.attr("EPI_MASK") = (int)bh::kC1x1Mask;
   m.attr("EPI_AFFINE") = (int)bh::kC1x1Affine;
   m.def("c1x1_supported", &c1x1_supported, py::arg("a"), py::arg("b"), py::arg("b_trans"), py::arg("M"), py::arg("pro") = false,

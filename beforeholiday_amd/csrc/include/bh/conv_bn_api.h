@@ -43,6 +43,9 @@ struct C1x1Args {
   const float* bnb = nullptr;
   const void* bnb_y = nullptr;
   const uint8_t* mbits = nullptr;  // kMask: [M, N/8] ReLU bit mask (N % 32 == 0, 4-byte aligned)
+  // row stride (elements) of A and bnb_y when they are a K-column slice of wider rows (0: K). The split-K
+  // data gradient runs the BatchNorm-backward prologue over column ranges of a wider gradient.
+  int lda = 0;
   int s2_H = 0, s2_W = 0;  // > 0: stride-2 gather from an [.., s2_H, s2_W, K] input; output is [.., s2_H/2, s2_W/2, N]
   // with s2_H > 0: scatter instead -- row (n, y, x) of the [M, N] result is ADDED into row (n, 2y, 2x) of
   // the full-resolution C [.., s2_H, s2_W, N] (R must equal C): the data gradient of a 1x1 / stride-2

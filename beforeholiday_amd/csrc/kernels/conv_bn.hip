@@ -168,7 +168,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
   const T* __restrict__ BY = reinterpret_cast<const T*>(p.bnb_y);
   auto load = [&](int i, i4v(&a)[KS], i4v(&yv)[PRO == 2 ? KS : 1]) {
     const int q = i / nch, c = i - q * nch;
-    const int64_t off = arow(first + q * stride) * K + c * KC + 8 * h;
+    const int64_t off = arow(first + q * stride) * (p.lda ? p.lda : K) + c * KC + 8 * h;
     const T* src = A + off;
     if (p.a_load == 1) {
 #pragma unroll
@@ -560,9 +560,10 @@ bool c1x1_supported(const C1x1Args& a) {
   }
   if (a.pro_scale && (a.R || a.epi != kC1x1Stats)) return false;
   // BatchNorm-backward prologue: a second [M, K] stream; plain or backward-sums epilogue, no residual / stride 2
-  if (a.bnb && (!a.bnb_y || !al16(a.bnb_y) || a.pro_scale || a.R || a.s2_H > 0 ||
+  if (a.bnb && (!a.bnb_y || !al16(a.bnb_y) || a.pro_scale || a.s2_H > 0 ||
                 (a.epi != kC1x1Plain && a.epi != kC1x1Bwd)))
     return false;
+  if (a.lda && (a.lda < a.K || a.lda % 8 || a.s2_H > 0)) return false;
   return true;
 }
 
@@ -592,9 +593,13 @@ void c1x1_run(int dt, const C1x1Args& a_in, hipStream_t st) {
       hipLaunchKernelGGL(kern, grid, block, pl.lds, st, a, pl.g);
     };
     if (bnb) {  // BatchNorm-backward prologue (KC 64 only, see make_plan)
+      if constexpr (KC == 64 && NC <= 64) {
+        if (a.epi == kC1x1Bwd && res) L(k_c1x1<T, KC, NC, kC1x1Bwd, 2, 0, true>);
+      }
       if constexpr (KC == 64 && NC <= 128) {
-        if (a.epi == kC1x1Bwd) L(k_c1x1<T, KC, NC, kC1x1Bwd, 2, 0, false>);
-        else L(k_c1x1<T, KC, NC, kC1x1Plain, 2, 0, false>);
+        if (a.epi == kC1x1Bwd && !res) L(k_c1x1<T, KC, NC, kC1x1Bwd, 2, 0, false>);
+        else if (a.epi != kC1x1Bwd && !res) L(k_c1x1<T, KC, NC, kC1x1Plain, 2, 0, false>);
+        else if (a.epi != kC1x1Bwd) L(k_c1x1<T, KC, NC, kC1x1Plain, 2, 0, true>);
       }
     } else if (a.epi == kC1x1Mask) {
       if constexpr (NC == 64) {

@@ -1288,9 +1288,24 @@ class _ConvBNResFn(torch.autograd.Function):
             lk = None
         s_i = None
         epi = "bwd" if lk is not None else "plain"
-        if conv_bn.preferred(N, K, M) and conv_bn.supported(g2d, W, epi=epi, b_trans=True, bnb=True):
-            kw = dict(epi=epi, by=lk[0], bscale=lk[1], bshift=lk[2], bmean=lk[3], brelu=lk[4]) if lk else {}
+        kw = dict(epi=epi, by=lk[0], bscale=lk[1], bshift=lk[2], bmean=lk[3], brelu=lk[4]) if lk else {}
+        nseg = _bnb_segments(g2d, W, epi)
+        if nseg == 1:
             da2d, part = conv_bn.c1x1(g2d, W, b_trans=True, bnb=abd, bnb_y=y2d, **kw)
+            if lk is not None:
+                s_i = conv_bn.sum_parts(part)
+        elif nseg > 1:
+            # split-K: the strip kernel keeps its B slice in LDS, so a wide gradient runs as column segments
+            # accumulated through the residual input; the BatchNorm-backward sums come with the last one
+            Ks = N // nseg
+            abd3 = abd.view(3, N)
+            da2d = None
+            for sgi in range(nseg):
+                cols = slice(sgi * Ks, (sgi + 1) * Ks)
+                bnb_s = abd3[:, cols].reshape(-1).contiguous()
+                last = sgi == nseg - 1
+                da2d, part = conv_bn.c1x1(g2d[:, cols], W[cols], b_trans=True, bnb=bnb_s, bnb_y=y2d[:, cols], lda=N,
+                                          resid=da2d, **(kw if last else {}))
             if lk is not None:
                 s_i = conv_bn.sum_parts(part)
         else:
@@ -1319,6 +1334,24 @@ class _ConvBNResFn(torch.autograd.Function):
                 cfg.link_in.sums = s_i
             gx = da
         return gx, None, gw3, gw_i, gb_i, gw, gb, g, None
+
+
+def _bnb_segments(g2d, W, epi):
+    """Column segments for conv3's data gradient with the BatchNorm-backward prologue on the strip kernel:
+    1 where the whole [N, K] weight fits one strip-kernel call, 2 / 4 for the wider 28x28 layers (each segment
+    <= 256 channels), 0 where the strip kernel does not take the shape (then gx is formed in its own pass)."""
+    from ..ops import conv_bn
+
+    N, K = W.shape
+    M = g2d.size(0)
+    if conv_bn.preferred(N, K, M) and conv_bn.supported(g2d, W, epi=epi, b_trans=True, bnb=True):
+        return 1
+    if M < 100000 or N % 256 or N // 256 > 4:
+        return 0
+    probe = g2d.new_empty((M, 256))
+    ok = (conv_bn.supported(probe, W[:256], epi="plain", b_trans=True, bnb=True) and
+          conv_bn.supported(probe, W[:256], epi=epi, resid=True, b_trans=True, bnb=True))
+    return N // 256 if ok else 0
 
 
 def _dgrad_bn_sums(gy2d, w2d, lk):

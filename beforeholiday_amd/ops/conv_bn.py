@@ -75,12 +75,14 @@ def c1x1(a: torch.Tensor, b: torch.Tensor, pro_scale: Optional[torch.Tensor] = N
          bscale: Optional[torch.Tensor] = None, bshift: Optional[torch.Tensor] = None,
          bmean: Optional[torch.Tensor] = None, brelu: bool = True,
          b_trans: bool = False, s2_scatter: bool = False, bnb: Optional[torch.Tensor] = None,
-         bnb_y: Optional[torch.Tensor] = None, mbits: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+         bnb_y: Optional[torch.Tensor] = None, mbits: Optional[torch.Tensor] = None,
+         lda: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
     """``b_trans``: ``b`` is given as ``[K, N]`` (e.g. a forward weight for the data gradient).
     ``bnb`` (fp32 ``[3K]`` = A, B, D) with ``bnb_y`` (shaped like ``a``): the BatchNorm-backward prologue
     ``f(a) = A * a + B * bnb_y + D`` per input channel, rounded to a's dtype (ops/bn_fold.py).
     ``epi="mask"`` with ``mbits`` (uint8 ``[M, N/8]``, syncbn.forward_mask's ReLU bits): C is masked and
-    ``part[0]`` holds its column-sum partials.
+    ``part[0]`` holds its column-sum partials. ``lda``: ``a`` (and ``bnb_y``) are column slices of row-major
+    tensors with that row stride (a split-K data gradient).
     ``s2_scatter`` (with ``s2=(H, W)`` and ``resid`` the full-resolution ``[N*H*W, N]`` tensor): row
     (n, y, x) of ``a @ b.T`` is ADDED in place into row (n, 2y, 2x) of ``resid``, which is returned --
     the 1x1 / stride-2 data gradient accumulated onto the other branch's gradient."""
@@ -98,7 +100,8 @@ def c1x1(a: torch.Tensor, b: torch.Tensor, pro_scale: Optional[torch.Tensor] = N
                           bnb_y, mbits)
     H, W = s2 if s2 is not None else (0, 0)
     return submodule("conv_bn").c1x1(a, b, b_trans, M, pro_scale, pro_shift, resid, H, W, _EPI[epi], kshift, by,
-                                     bscale, bshift, bmean, brelu, s2_scatter, bnb=bnb, bnb_y=bnb_y, mbits=mbits)
+                                     bscale, bshift, bmean, brelu, s2_scatter, bnb=bnb, bnb_y=bnb_y, mbits=mbits,
+                                     lda=lda)
 
 
 def c1x1_affine(a: torch.Tensor, b: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, relu: bool = True,

@@ -140,18 +140,19 @@ def test_c1x1_batchnorm_backward_prologue(K, N, epi, dt):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", [(256, 64, 1, 56), (64, 64, 1, 56), (256, 128, 2, 56), (512, 128, 1, 28),
-                                 (1024, 256, 1, 14), (2048, 512, 1, 7)])
+@pytest.mark.parametrize("cfg", [(256, 64, 1, 56, 4), (64, 64, 1, 56, 4), (256, 128, 2, 56, 4), (512, 128, 1, 28, 4),
+                                 (1024, 256, 1, 14, 4), (2048, 512, 1, 7, 4),
+                                 (256, 64, 1, 56, 32), (512, 128, 1, 28, 128)])  # strip-kernel sizes (split-K)
 def test_fused_tail_matches_per_layer_path(cfg):
     """The same fp16 block with the tail as one node (_ConvBNResFn) and as per-layer nodes: outputs equal
     (same forward kernels), every gradient within fp16 rounding, running statistics and
     num_batches_tracked identical."""
     from test_resnet_fold import _block
 
-    inplanes, planes, stride, hw = cfg
+    inplanes, planes, stride, hw, bs = cfg
     R, _, blk = _block(inplanes, planes, stride, torch.float16)
-    x = torch.randn(4, inplanes, hw, hw, device="cuda").half().contiguous(memory_format=torch.channels_last)
-    g = torch.randn(4, planes * 4, (hw + stride - 1) // stride, (hw + stride - 1) // stride, device="cuda").half()
+    x = torch.randn(bs, inplanes, hw, hw, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    g = torch.randn(bs, planes * 4, (hw + stride - 1) // stride, (hw + stride - 1) // stride, device="cuda").half()
     g = g.contiguous(memory_format=torch.channels_last)
     old = R._BN_RES_FOLD
     res = []
@@ -272,3 +273,26 @@ def test_mask_in_producer_matches_own_pass(mode):
     assert _rel(res[0][0], res[1][0]) < 1e-2
     for a, b in zip(res[0][1], res[1][1]):
         assert _rel(a, b) < 1e-2
+
+
+@pytest.mark.gpu
+def test_c1x1_column_slice_lda():
+    """The BatchNorm-backward prologue on column slices of wider rows (lda), accumulated through the residual:
+    the split-K data gradient equals the one-call product."""
+    from beforeholiday_amd.ops import conv_bn
+
+    torch.manual_seed(0)
+    M, N, K = 4096, 512, 128
+    g = torch.randn(M, N, device="cuda").half()
+    y = torch.randn(M, N, device="cuda").half()
+    W = (torch.randn(N, K, device="cuda") / N ** 0.5).half()
+    abd = torch.cat([torch.rand(N, device="cuda") + 0.5, torch.randn(N, device="cuda") * 0.3,
+                     torch.randn(N, device="cuda") * 0.1])
+    ref, _ = conv_bn.c1x1(g.cpu(), W.cpu(), b_trans=True, bnb=abd.cpu(), bnb_y=y.cpu())
+    out = None
+    a3 = abd.view(3, N)
+    for s in range(2):
+        cols = slice(s * 256, (s + 1) * 256)
+        out, _ = conv_bn.c1x1(g[:, cols], W[cols], b_trans=True, bnb=a3[:, cols].reshape(-1).contiguous(),
+                              bnb_y=y[:, cols], lda=N, resid=out)
+    assert _rel(out, ref) < 3e-3
