@@ -14,10 +14,13 @@ bool half_2d(const at::Tensor& t) {
 
 // (gram partials [S, K, K], column-sum partials [S, K]) of a' = a or relu(a * pro_scale + pro_shift)
 std::vector<at::Tensor> gram(const at::Tensor& a, const c10::optional<at::Tensor>& pro_scale,
-                             const c10::optional<at::Tensor>& pro_shift) {
+                             const c10::optional<at::Tensor>& pro_shift, int64_t s2_h, int64_t s2_w) {
   TORCH_CHECK(half_2d(a) && a.size(1) % 64 == 0 && a.size(0) > 0,
               "bn_fold.gram: a must be a contiguous 16-byte aligned fp16/bf16 [M, K] GPU tensor, K % 64 == 0");
-  const int64_t M = a.size(0), K = a.size(1);
+  const int64_t M = s2_h > 0 ? a.size(0) / 4 : a.size(0), K = a.size(1);
+  TORCH_CHECK(s2_h == 0 || (s2_h % 2 == 0 && s2_w % 2 == 0 && a.size(0) % (s2_h * s2_w) == 0),
+              "bn_fold.gram: stride-2 rows need a [N * s2_h * s2_w, K] input with even s2_h, s2_w");
+  TORCH_CHECK(!(s2_h > 0 && pro_scale.has_value() && pro_scale->defined()), "bn_fold.gram: no prologue at stride 2");
   const float *ps = nullptr, *ph = nullptr;
   at::Tensor psc, phc;
   if (pro_scale.has_value() && pro_scale->defined()) {
@@ -34,7 +37,7 @@ std::vector<at::Tensor> gram(const at::Tensor& a, const c10::optional<at::Tensor
   auto gp = at::empty({S, K, K}, a.options().dtype(at::kFloat));
   auto cp = at::empty({S, K}, a.options().dtype(at::kFloat));
   bh::gram_partials(dtype_code(a.scalar_type()), a.data_ptr(), M, (int)K, ps, ph, gp.data_ptr<float>(),
-                    cp.data_ptr<float>(), stream_for(a));
+                    cp.data_ptr<float>(), stream_for(a), (int)s2_h, (int)s2_w);
   return {gp, cp};
 }
 
@@ -128,7 +131,8 @@ std::vector<at::Tensor> fold_finish(const at::Tensor& W, const at::Tensor& sums,
 
 void register_bn_fold(pybind11::module_& root) {
   auto m = root.def_submodule("bn_fold", "BatchNorm-backward fold: Gram partials, residual-ReLU mask + column sums");
-  m.def("gram", &gram, py::arg("a"), py::arg("pro_scale") = py::none(), py::arg("pro_shift") = py::none());
+  m.def("gram", &gram, py::arg("a"), py::arg("pro_scale") = py::none(), py::arg("pro_shift") = py::none(),
+        py::arg("s2_h") = 0, py::arg("s2_w") = 0);
   m.def("mask_colsum", &mask_colsum, py::arg("g"), py::arg("bits"));
   m.def("fold_reduce", &fold_reduce, py::arg("W"), py::arg("p_ws"), py::arg("g_ws"), py::arg("sa_ws"), py::arg("sg_ws"),
         py::arg("mean"), py::arg("invstd"));

@@ -261,7 +261,8 @@ bool mask_ok(const at::Tensor& x) {
 // forward that also returns the ReLU mask as uint8 [rows, C/8] (bit k: channel 8j+k > 0), so the
 // backward of BN + add + ReLU does not keep reading the residual input z
 std::vector<at::Tensor> forward_mask(at::Tensor x_in, c10::optional<at::Tensor> z, at::Tensor scale, at::Tensor shift,
-                                     c10::optional<at::Tensor> num_batches) {
+                                     c10::optional<at::Tensor> num_batches, c10::optional<at::Tensor> zscale,
+                                     c10::optional<at::Tensor> zshift) {
   check_cuda(x_in, "input");
   Layout L = layout_of(x_in);
   TORCH_CHECK(L.s.channels_last && L.s.C % 8 == 0, "forward_mask: needs channels_last with C % 8 == 0");
@@ -271,10 +272,20 @@ std::vector<at::Tensor> forward_mask(at::Tensor x_in, c10::optional<at::Tensor> 
   TORCH_CHECK(scale.scalar_type() == at::kFloat && shift.scalar_type() == at::kFloat && scale.numel() == L.s.C,
               "scale/shift must be fp32 [C]");
   auto mask = at::empty({L.s.outer, (int64_t)(L.s.C / 8)}, L.x.options().dtype(at::kByte).memory_format(at::MemoryFormat::Contiguous));
+  at::Tensor zs, zh;
+  if (zscale.has_value() && zscale->defined()) {
+    TORCH_CHECK(zt.defined() && zshift.has_value() && zshift->defined(), "forward_mask: zscale needs z and zshift");
+    zs = zscale->contiguous();
+    zh = zshift->contiguous();
+    TORCH_CHECK(zs.scalar_type() == at::kFloat && zh.scalar_type() == at::kFloat && zs.numel() == L.s.C &&
+                    zh.numel() == L.s.C,
+                "forward_mask: zscale / zshift must be fp32 [C]");
+  }
   bh::bn_forward(L.s, dtype_code(L.x.scalar_type()), L.x.data_ptr(), zt.defined() ? dtype_code(zt.scalar_type()) : -1,
                  zt.defined() ? zt.data_ptr() : nullptr, dtype_code(y.scalar_type()), y.data_ptr(),
                  scale.contiguous().data_ptr<float>(), shift.contiguous().data_ptr<float>(), true,
-                 counter_ptr(num_batches), stream_for(L.x), mask.data_ptr<uint8_t>());
+                 counter_ptr(num_batches), stream_for(L.x), mask.data_ptr<uint8_t>(),
+                 zs.defined() ? zs.data_ptr<float>() : nullptr, zs.defined() ? zh.data_ptr<float>() : nullptr);
   return {y, mask};
 }
 
@@ -424,7 +435,8 @@ void register_syncbn(pybind11::module_& root) {
         py::arg("invstd"), py::arg("weight"), py::arg("sums"), py::arg("count"), py::arg("scale"), py::arg("shift"),
         py::arg("relu"), py::arg("need_dz"), py::arg("mask") = py::none());
   m.def("forward_mask", &forward_mask, py::arg("x"), py::arg("z"), py::arg("scale"), py::arg("shift"),
-        py::arg("num_batches") = py::none(), "fused BN + (z) + ReLU that also returns the uint8 [rows, C/8] ReLU bit mask");
+        py::arg("num_batches") = py::none(), py::arg("zscale") = py::none(), py::arg("zshift") = py::none(),
+        "fused BN + (z, or BN(z) with zscale / zshift) + ReLU that also returns the uint8 [rows, C/8] ReLU bit mask");
   m.def("mask_ok", &mask_ok);
   m.def("maxpool_forward", &maxpool_forward, py::arg("x"), py::arg("scale"), py::arg("shift"), py::arg("relu"),
         py::arg("kernel_size"), py::arg("stride"), py::arg("padding"), py::arg("want_idx"),

@@ -53,7 +53,8 @@ void bn_merge_ranks(int W, int C, const float* gathered, const BNFinal& fin, int
 // y = x*scale + shift (+z) (relu); dt_z = -1 when z is null
 void bn_forward(const BNShape& s, int dt_x, const void* x, int dt_z, const void* z, int dt_y, void* y,
                 const float* scale, const float* shift, bool relu, int64_t* counter, hipStream_t st,
-                uint8_t* mbits = nullptr);  // mbits: optional [rows][C/8] ReLU bit mask (NHWC, C % 8 == 0)
+                uint8_t* mbits = nullptr,  // mbits: optional [rows][C/8] ReLU bit mask (NHWC, C % 8 == 0)
+                const float* zscale = nullptr, const float* zshift = nullptr);  // z -> z * zscale + zshift
 // partial sums of dy' and dy'*(x-mean); dy' = dy masked by (x*scale+shift(+z) > 0) when relu
 void bn_backward_reduce(const BNShape& s, int dt, const void* dy, const void* x, int dt_z, const void* z,
                         const float* mean, const float* scale, const float* shift, bool relu, int splits,

@@ -22,8 +22,9 @@ namespace bh {
 // a' = relu(a * pro_scale[k] + pro_shift[k]) rounded to the input type: fp32 partials
 // gram_part[s][K][K] (s < gram_splits) and column sums colsum_part[s][K]. K % 64 == 0.
 int gram_splits(int64_t M, int K);
+// s2_H > 0: row m is pixel (n, 2y, 2x) of an [.., s2_H, s2_W, K] input (M = its quarter-resolution rows)
 void gram_partials(int dt, const void* a, int64_t M, int K, const float* pro_scale, const float* pro_shift,
-                   float* gram_part, float* colsum_part, hipStream_t st);
+                   float* gram_part, float* colsum_part, hipStream_t st, int s2_H = 0, int s2_W = 0);
 
 // g_pre[m, n] = bits(m, n) ? g[m, n] : 0 with bits [M, N/8] (bit n % 8 of byte n / 8), and the column sums
 // of g_pre as fp32 partials colsum_part[s][N] (s < mask_colsum_splits). N % 8 == 0.

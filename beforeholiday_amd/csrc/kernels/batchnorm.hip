@@ -524,15 +524,23 @@ constexpr int kFlatU = 4;
 template <typename T> using Vec8 = T __attribute__((ext_vector_type(8)));
 BH_DEVICE int64_t chunk_chan(int64_t i, int C8, bool pow2) { return pow2 ? (i & (C8 - 1)) : (i % C8); }
 
+// zscale / zshift (optional): z is itself a BatchNorm input, normalised here too -- the downsampling
+// block's bn3(y) + bn_ds(y_ds) + ReLU in one pass (no normalised identity tensor is written)
 template <typename T, typename Tz, typename Ty>
 __global__ __launch_bounds__(kBlock) void k_fwd_flat(const T* __restrict__ x, const Tz* __restrict__ z,
                                                      Ty* __restrict__ y, const float* __restrict__ scale,
                                                      const float* __restrict__ shift, int64_t chunks, int C, bool relu,
-                                                     int64_t* counter, uint8_t* __restrict__ mbits) {
-  extern __shared__ float prm[];  // [2][C]: scale, shift
+                                                     int64_t* counter, uint8_t* __restrict__ mbits,
+                                                     const float* __restrict__ zscale,
+                                                     const float* __restrict__ zshift) {
+  extern __shared__ float prm[];  // [2 or 4][C]: scale, shift (, zscale, zshift)
   for (int c = threadIdx.x; c < C; c += kBlock) {
     prm[c] = scale[c];
     prm[C + c] = shift[c];
+    if (zscale) {
+      prm[2 * C + c] = zscale[c];
+      prm[3 * C + c] = zshift[c];
+    }
   }
   __syncthreads();
   if (counter && blockIdx.x == 0 && threadIdx.x == 0) *counter += 1;
@@ -556,14 +564,18 @@ __global__ __launch_bounds__(kBlock) void k_fwd_flat(const T* __restrict__ x, co
       const int64_t i = t0 + (int64_t)u * kBlock;
       if (i >= chunks) continue;
       const int c0 = (int)chunk_chan(i, C8, pow2) * 8;
-      float sc[8], sh[8], o8[8];
+      float sc[8], sh[8], o8[8], zs[8], zh[8];
       VecIO<float>::load(prm + c0, sc);
       VecIO<float>::load(prm + C + c0, sh);
+      if (zscale) {
+        VecIO<float>::load(prm + 2 * C + c0, zs);
+        VecIO<float>::load(prm + 3 * C + c0, zh);
+      }
       uint32_t bits = 0;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float o = fmaf(to_f<T>(xr[u][k]), sc[k], sh[k]);
-        if (z) o += to_f<Tz>(zr[u][k]);
+        if (z) o += zscale ? fmaf(to_f<Tz>(zr[u][k]), zs[k], zh[k]) : to_f<Tz>(zr[u][k]);
         bits |= (o > 0.f ? 1u : 0u) << k;
         if (relu) o = fmaxf(o, 0.f);
         o8[k] = o;
@@ -1172,16 +1184,18 @@ unsigned flat_grid(int64_t chunks) {
 
 void bn_forward(const BNShape& s, int dt_x, const void* x, int dt_z, const void* z, int dt_y, void* y,
                 const float* scale, const float* shift, bool relu, int64_t* counter, hipStream_t st,
-                uint8_t* mbits) {
+                uint8_t* mbits, const float* zscale, const float* zshift) {
   const int64_t total = s.outer * s.C * s.inner;
   if (total == 0) return;
   if (dt_z < 0) dt_z = dt_x;
-  if (flat_ok(s, 2)) {
+  if (zscale && !(z && flat_ok(s, 4)))
+    throw std::runtime_error("bn_forward: a normalised z needs channels_last, C % 8 == 0 and 16 C floats of LDS");
+  if (flat_ok(s, zscale ? 4 : 2)) {
     const int64_t chunks = total / 8;
-    const size_t shm = sizeof(float) * 2 * s.C;
+    const size_t shm = sizeof(float) * (zscale ? 4 : 2) * s.C;
     BN_DISPATCH(dt_x, T, BN_DISPATCH(dt_z, Tz, BN_DISPATCH(dt_y, Ty,
         hipLaunchKernelGGL((k_fwd_flat<T, Tz, Ty>), dim3(flat_grid(chunks)), dim3(kBlock), shm, st, (const T*)x,
-                           (const Tz*)z, (Ty*)y, scale, shift, chunks, s.C, relu, counter, mbits))));
+                           (const Tz*)z, (Ty*)y, scale, shift, chunks, s.C, relu, counter, mbits, zscale, zshift))));
   } else if (s.channels_last && s.C % 8 == 0) {
     const NhwcGeom g = nhwc_geom(s.C);
     const int64_t splits = nhwc_splits(s, knob_ew_blocks(), knob_ew_rows());

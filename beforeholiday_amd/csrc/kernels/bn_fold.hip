@@ -30,7 +30,7 @@ template <> struct Mf<bf16> {
 };
 
 constexpr int kThreads = 256;
-constexpr int kGramTargetWG = 256;  // one workgroup per CU: fewer partial slabs for the reduce
+constexpr int kGramTargetWG = 512;  // two workgroups per CU
 
 // ------------------------------------------------------------------------------------------------
 // Gram partials. Workgroup = (channel block pair (jb, kb) of BJ x BJ outputs, row split). Per RM-row chunk
@@ -41,22 +41,28 @@ constexpr int kGramTargetWG = 256;  // one workgroup per CU: fewer partial slabs
 // multiplied. Row ranges per split are contiguous and summed in order, the splits reduced by the caller in
 // a fixed order: deterministic. Diagonal workgroups (jb == kb) also sum their channels (the column sums
 // of a'). Rows past M are loaded clamped and zeroed by a select (no divergent branches).
-template <int BJ> struct GramGeo {
-  static constexpr int RM = BJ == 64 ? 128 : 64;   // rows per chunk: <= 256 staging items per slice pair
+// ONE: K == BJ (a single, diagonal block pair: one slice to stage), else two slices. Rows per chunk such
+// that every one of the 256 threads stages exactly one 8x8 block per chunk.
+template <int BJ, bool ONE> struct GramGeo {
+  static constexpr int RM = (ONE ? 16384 : 8192) / BJ;
   static constexpr int PITCH = (RM + 8) * 2;       // bytes per channel row (16-byte aligned, staggered banks)
   static constexpr int ITEMS = (BJ / 8) * (RM / 8);  // 8x8 blocks per slice
 };
 
-template <typename T, bool PRO, int BJ>
+// s2_H > 0: row m of the [M, K] problem is pixel (n, 2y, 2x) of an [.., s2_H, s2_W, K] input (the 1x1 / stride-2
+// downsample convolution's input, read in place)
+template <typename T, bool PRO, int BJ, bool ONE>
 __global__ __launch_bounds__(kThreads, 2) void k_gram(const T* __restrict__ a, int64_t M, int K,
                                                       const float* __restrict__ pro_scale,
                                                       const float* __restrict__ pro_shift, int splits,
-                                                      float* __restrict__ gram_part, float* __restrict__ colsum_part) {
-  using G = GramGeo<BJ>;
+                                                      float* __restrict__ gram_part, float* __restrict__ colsum_part,
+                                                      int s2_H, int s2_W) {
+  using G = GramGeo<BJ, ONE>;
   constexpr int RM = G::RM, PITCH = G::PITCH, ITEMS = G::ITEMS;
-  constexpr int IPT = (2 * ITEMS + kThreads - 1) / kThreads;  // staging items per thread (both slices)
+  constexpr int IPT = ((ONE ? 1 : 2) * ITEMS + kThreads - 1) / kThreads;  // staging items per thread
+  static_assert(IPT == 1, "one 8x8 block per thread and chunk");
   constexpr int TPW = BJ / 64;                                 // 32-wide tiles per wave per dimension
-  __shared__ __attribute__((aligned(16))) char img[2][BJ * PITCH];
+  __shared__ __attribute__((aligned(16))) char img[ONE ? 1 : 2][BJ * PITCH];
 
   const int nb = K / BJ;
   const int pair = blockIdx.x % (nb * nb), split = blockIdx.x / (nb * nb);
@@ -109,7 +115,13 @@ __global__ __launch_bounds__(kThreads, 2) void k_gram(const T* __restrict__ a, i
       const int cb = (it_sl[q] == 0 ? jb : kb) * BJ + it_c8[q] * 8;
 #pragma unroll
       for (int rr = 0; rr < 8; ++rr) {
-        const int64_t m = std::min<int64_t>(ch * RM + it_rg[q] * 8 + rr, M - 1);
+        int64_t m = std::min<int64_t>(ch * RM + it_rg[q] * 8 + rr, M - 1);
+        if (s2_H > 0) {
+          const int Wo = s2_W >> 1, HWo = (s2_H >> 1) * Wo;
+          const int64_t n = m / HWo;
+          const int rem = (int)(m - n * HWo), yo = rem / Wo, xo = rem - yo * Wo;
+          m = (n * s2_H + 2 * yo) * s2_W + 2 * xo;
+        }
         if (it_on[q]) v[q][rr] = *reinterpret_cast<const t8*>(a + m * K + cb);
       }
     }
@@ -132,13 +144,13 @@ __global__ __launch_bounds__(kThreads, 2) void k_gram(const T* __restrict__ a, i
           col[e][rr] = from_f<T>(f);
         }
       }
-      char* base = img[it_sl[q]] + (it_c8[q] * 8) * PITCH + it_rg[q] * 16;
+      char* base = img[ONE ? 0 : it_sl[q]] + (it_c8[q] * 8) * PITCH + it_rg[q] * 16;
 #pragma unroll
       for (int e = 0; e < 8; ++e) *reinterpret_cast<t8*>(base + e * PITCH) = col[e];
     }
     __syncthreads();
     const char* iJ = img[0];
-    const char* iK = diag ? img[0] : img[1];
+    const char* iK = (diag || ONE) ? img[0] : img[ONE ? 0 : 1];
 #pragma unroll
     for (int ks = 0; ks < RM / 16; ++ks) {
       i4v fa[TPW], fb[TPW];
@@ -352,27 +364,34 @@ int mask_cvb(int N) { return std::min(N / 8, 64); }
 int gram_splits(int64_t M, int K) {
   const int BJ = K % 128 == 0 ? 128 : 64;
   const int pairs = (K / BJ) * (K / BJ);
-  const int RM = BJ == 64 ? GramGeo<64>::RM : GramGeo<128>::RM;
+  const bool one = K == BJ;
+  const int RM = BJ == 64 ? (one ? GramGeo<64, true>::RM : GramGeo<64, false>::RM)
+                          : (one ? GramGeo<128, true>::RM : GramGeo<128, false>::RM);
   const int64_t nchunks = (M + RM - 1) / RM;
   return (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, kGramTargetWG / pairs));
 }
 
 void gram_partials(int dt, const void* a, int64_t M, int K, const float* pro_scale, const float* pro_shift,
-                   float* gram_part, float* colsum_part, hipStream_t st) {
+                   float* gram_part, float* colsum_part, hipStream_t st, int s2_H, int s2_W) {
   if (K % 64 != 0 || K <= 0 || M <= 0) throw std::runtime_error("gram_partials: K % 64 == 0, M > 0");
   const int BJ = K % 128 == 0 ? 128 : 64;
   const int nb = K / BJ, splits = gram_splits(M, K);
   const dim3 grid(nb * nb * splits), block(kThreads);
   const bool pro = pro_scale != nullptr;
+  const bool one = K == BJ;
   auto go = [&](auto tag) {
     using T = decltype(tag);
     const T* ap = reinterpret_cast<const T*>(a);
+    auto L = [&](auto kern) {
+      hipLaunchKernelGGL(kern, grid, block, 0, st, ap, M, K, pro_scale, pro_shift, splits, gram_part, colsum_part,
+                         s2_H, s2_W);
+    };
     if (BJ == 128) {
-      if (pro) hipLaunchKernelGGL((k_gram<T, true, 128>), grid, block, 0, st, ap, M, K, pro_scale, pro_shift, splits, gram_part, colsum_part);
-      else hipLaunchKernelGGL((k_gram<T, false, 128>), grid, block, 0, st, ap, M, K, pro_scale, pro_shift, splits, gram_part, colsum_part);
+      if (one) { if (pro) L(k_gram<T, true, 128, true>); else L(k_gram<T, false, 128, true>); }
+      else { if (pro) L(k_gram<T, true, 128, false>); else L(k_gram<T, false, 128, false>); }
     } else {
-      if (pro) hipLaunchKernelGGL((k_gram<T, true, 64>), grid, block, 0, st, ap, M, K, pro_scale, pro_shift, splits, gram_part, colsum_part);
-      else hipLaunchKernelGGL((k_gram<T, false, 64>), grid, block, 0, st, ap, M, K, pro_scale, pro_shift, splits, gram_part, colsum_part);
+      if (one) { if (pro) L(k_gram<T, true, 64, true>); else L(k_gram<T, false, 64, true>); }
+      else { if (pro) L(k_gram<T, true, 64, false>); else L(k_gram<T, false, 64, false>); }
     }
   };
   switch (dt) {

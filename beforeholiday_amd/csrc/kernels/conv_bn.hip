@@ -496,7 +496,8 @@ bool make_plan(const C1x1Args& a, Plan* pl) {
              bwd = a.epi == kC1x1Bwd, aff = a.epi == kC1x1Affine, scatter = a.s2_H > 0 && a.s2_scatter;
   // register budget: the backward epilogue (input loads + statistics) fits 4 column tiles per wave
   // (the mask epilogue's per-row mask words spill at wider slices)
-  const int max_nc = a.epi == kC1x1Mask ? 64 : (bwd ? (a.R ? 64 : 128) : 256);
+  int max_nc = a.epi == kC1x1Mask ? 64 : (bwd ? (a.R ? 64 : 128) : 256);
+  if (a.bnb) max_nc = std::min(max_nc, scatter ? 64 : 128);  // (the second fragment stream's registers)
   int NC = 0, occ = 0;
   // the widest column slice (A read once per slice) that still leaves two workgroups per CU; else one
   // (BH_C1X1_OCC: the resident-workgroup target, an experiment knob; the kernels' registers must allow it)
@@ -552,6 +553,9 @@ bool c1x1_supported(const C1x1Args& a) {
   if (a.s2_H > 0) {
     if (a.s2_H % 2 || a.s2_W % 2 || a.M % ((int64_t)(a.s2_H / 2) * (a.s2_W / 2))) return false;
     if (a.pro_scale || a.epi == kC1x1Bwd) return false;  // combinations not instantiated
+    if (a.bnb && a.lda) return false;
+    // (bnb scatter: 64-column slices re-read A and its y stream per slice; past 256 channels that leaves L2)
+    if (a.bnb && a.K > 256) return false;
     // gather: no residual (the affine epilogue excepted); scatter: plain epilogue accumulating into the
     // full-resolution C (R == C)
     if (a.s2_scatter ? (a.epi != kC1x1Plain || a.R != a.C) : (a.R != nullptr && a.epi != kC1x1Affine)) return false;
@@ -560,7 +564,7 @@ bool c1x1_supported(const C1x1Args& a) {
   }
   if (a.pro_scale && (a.R || a.epi != kC1x1Stats)) return false;
   // BatchNorm-backward prologue: a second [M, K] stream; plain or backward-sums epilogue, no residual / stride 2
-  if (a.bnb && (!a.bnb_y || !al16(a.bnb_y) || a.pro_scale || a.s2_H > 0 ||
+  if (a.bnb && (!a.bnb_y || !al16(a.bnb_y) || a.pro_scale || (a.s2_H > 0 && !a.s2_scatter) ||
                 (a.epi != kC1x1Plain && a.epi != kC1x1Bwd)))
     return false;
   if (a.lda && (a.lda < a.K || a.lda % 8 || a.s2_H > 0)) return false;
@@ -596,10 +600,13 @@ void c1x1_run(int dt, const C1x1Args& a_in, hipStream_t st) {
       if constexpr (KC == 64 && NC <= 64) {
         if (a.epi == kC1x1Bwd && res) L(k_c1x1<T, KC, NC, kC1x1Bwd, 2, 0, true>);
       }
+      if constexpr (KC == 64 && NC <= 64) {  // the downsample's data gradient scattered onto conv1's
+        if (s2 && a.s2_scatter) L(k_c1x1<T, KC, NC, kC1x1Plain, 2, 2, true>);
+      }
       if constexpr (KC == 64 && NC <= 128) {
         if (a.epi == kC1x1Bwd && !res) L(k_c1x1<T, KC, NC, kC1x1Bwd, 2, 0, false>);
         else if (a.epi != kC1x1Bwd && !res) L(k_c1x1<T, KC, NC, kC1x1Plain, 2, 0, false>);
-        else if (a.epi != kC1x1Bwd) L(k_c1x1<T, KC, NC, kC1x1Plain, 2, 0, true>);
+        else if (a.epi != kC1x1Bwd && !s2) L(k_c1x1<T, KC, NC, kC1x1Plain, 2, 0, true>);
       }
     } else if (a.epi == kC1x1Mask) {
       if constexpr (NC == 64) {

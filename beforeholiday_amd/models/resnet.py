@@ -906,11 +906,15 @@ class _Conv1DsFn(torch.autograd.Function):
     plus an add). Weight gradients on the MFMA wgrad kernels."""
 
     @staticmethod
-    def forward(ctx, x, w1, wd, k1, kd, s2):
+    def forward(ctx, x, w1, wd, k1, kd, s2, ds_box=None):
         y1, p1 = _c1x1_forward_stats(x, w1, k1, False)
         yd, pd = _c1x1_forward_stats(x, wd, kd, s2)
         ctx.save_for_backward(x, w1, wd)
         ctx.s2, ctx.wparams = s2, (w1, wd)
+        # ds_box: filled by the block's tail (_ConvBNResFn) when it folds the downsample BatchNorm: the
+        # downsample conv's weight gradient is then the tail's, and its data gradient is formed here from
+        # (g, y_ds, A, B, D) with the BatchNorm-backward prologue
+        ctx.ds_box = ds_box
         ctx.mark_non_differentiable(p1, pd)
         ctx.set_materialize_grads(False)
         return y1, p1, yd, pd
@@ -924,9 +928,10 @@ class _Conv1DsFn(torch.autograd.Function):
         n, c, h, w = x.shape
         k1, kd = w1.size(0), wd.size(0)
         gy1 = gy1.contiguous(memory_format=torch.channels_last)
-        gyd = gyd.contiguous(memory_format=torch.channels_last)
+        if gyd is not None:  # (None: the tail folded the downsample BatchNorm, see ds_box)
+            gyd = gyd.contiguous(memory_format=torch.channels_last)
+            gd = gyd.permute(0, 2, 3, 1).reshape(-1, kd)
         g1 = gy1.permute(0, 2, 3, 1).reshape(-1, k1)
-        gd = gyd.permute(0, 2, 3, 1).reshape(-1, kd)
         w1_2d, wd_2d = w1.view(k1, c), wd.view(kd, c)
         gx = gw1 = gwd = None
         conv_bwd = torch.ops.aten.convolution_backward
@@ -942,8 +947,9 @@ class _Conv1DsFn(torch.autograd.Function):
                         _like(conv_bwd(gyd, x, wd, None, *a2, [False, True, False])[1], wd))
             return _wgrad(x, gyd, wd, 1, "gemm", lambda: conv_bwd(gyd, x, wd, None, *a1, [False, True, False])[1])
 
+        dsb = ctx.ds_box.pop("ds", None) if ctx.ds_box is not None else None
         side1 = ctx.needs_input_grad[1] and _side_ok(ctx.wparams[0], x)
-        sided = ctx.needs_input_grad[2] and _side_ok(ctx.wparams[1], x)
+        sided = dsb is None and ctx.needs_input_grad[2] and _side_ok(ctx.wparams[1], x)
         if side1:
             gw1 = _on_side(w1fn, x, gy1)
         if sided:
@@ -955,7 +961,9 @@ class _Conv1DsFn(torch.autograd.Function):
                 gx2d, _ = conv_bn.gemm_bn(g1, _tr(w1_2d), "plain")
             else:
                 gx2d = torch.mm(g1, w1_2d)
-            if ctx.s2:
+            if dsb is not None:
+                gx2d = _ds_dgrad_folded(gx2d, dsb, ctx.s2, (n, c, h, w))
+            elif ctx.s2:
                 # the scatter epilogue wins only where the strip kernel does (K = downsample channels
                 # <= 256); else hipBLASLt + a strided add over the quarter of the pixels
                 if conv_bn.preferred(kd, c, gd.size(0)) and \
@@ -977,9 +985,35 @@ class _Conv1DsFn(torch.autograd.Function):
             gx = gx2d.view(n, h, w, c).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1] and not side1:
             gw1 = w1fn()
-        if ctx.needs_input_grad[2] and not sided:
+        if ctx.needs_input_grad[2] and not sided and dsb is None:
             gwd = wdfn()
-        return gx, gw1, gwd, None, None, None
+        return gx, gw1, gwd, None, None, None, None
+
+
+def _ds_dgrad_folded(gx2d, dsb, s2, shape):
+    """conv1's data gradient gx2d plus the downsample convolution's (gx_ds @ W_ds, gx_ds = A g + B y_ds + D:
+    the folded downsample BatchNorm's input gradient, never written): the strip kernel's BatchNorm-backward
+    prologue with gx2d as the residual (scatter-accumulated in place at the even pixels for stride 2), else
+    gx_ds formed in a pass and a library GEMM. Returns the sum (gx2d itself where accumulated in place)."""
+    from ..ops import conv_bn
+
+    from ..ops import syncbn
+
+    n, c, h, w = shape
+    g2d, abd, y2d, Wd, bn_args = dsb  # g2d / y2d: [M_ds, kd]; Wd: [kd, c]; bn_args: the BatchNorm's own terms
+    kd = Wd.size(0)
+    if s2:
+        if conv_bn.supported(g2d, Wd, b_trans=True, s2=(h, w), s2_scatter=True, bnb=True):
+            return conv_bn.c1x1(g2d, Wd, b_trans=True, bnb=abd, bnb_y=y2d, s2=(h, w), s2_scatter=True, resid=gx2d)[0]
+    elif conv_bn.supported(g2d, Wd, resid=True, b_trans=True, bnb=True):
+        return conv_bn.c1x1(g2d, Wd, b_trans=True, bnb=abd, bnb_y=y2d, resid=gx2d)[0]
+    g4, y4, mean, invstd, weight, sums, count = bn_args
+    gxd = syncbn.backward_dgrad(g4, y4, None, mean, invstd, weight, sums, count, None, None, False, False, None)[0]
+    gxd = gxd.permute(0, 2, 3, 1).reshape(-1, kd)
+    if s2:
+        gx2d.view(n, h, w, c)[:, ::2, ::2, :].add_(torch.mm(gxd, Wd).view(n, h // 2, w // 2, c))
+        return gx2d
+    return torch.addmm(gx2d, gxd, Wd, out=gx2d)
 
 
 class _Conv3x3BNFn(torch.autograd.Function):
@@ -1156,10 +1190,13 @@ class _FoldCfg(object):
     """Non-tensor arguments of :class:`_ConvBNResFn`: the BatchNorm modules (running statistics,
     momentum, eps, process group) and the link of an unfolded bn2."""
 
-    __slots__ = ("bn_in", "bn_out", "link_in")
+    __slots__ = ("bn_in", "bn_out", "link_in", "bn_ds", "ds_box", "ds_s2")
 
-    def __init__(self, bn_in, bn_out, link_in):
+    def __init__(self, bn_in, bn_out, link_in, bn_ds=None, ds_box=None, ds_s2=False):
         self.bn_in, self.bn_out, self.link_in = bn_in, bn_out, link_in
+        # downsampling block: the downsample BatchNorm (its input y_ds comes in as `yd`), the box through which
+        # the downsample conv's data-gradient inputs go to _Conv1DsFn, and its stride
+        self.bn_ds, self.ds_box, self.ds_s2 = bn_ds, ds_box, ds_s2
 
 
 def _bn_finalize(bn, part, count, world, bump_in_merge):
@@ -1199,7 +1236,8 @@ class _ConvBNResFn(torch.autograd.Function):
     (``cfg.link_in``: the unfolded bn2's link, its backward sums come from the data-gradient epilogue)."""
 
     @staticmethod
-    def forward(ctx, src, p_src, w3, bn_in_w, bn_in_b, bn_w, bn_b, z, cfg):
+    def forward(ctx, src, p_src, w3, bn_in_w, bn_in_b, bn_w, bn_b, z, cfg, yd=None, pd=None, xd=None, wd=None,
+                bnd_w=None, bnd_b=None):
         from ..ops import conv_bn
         from ..ops import syncbn
         from ..parallel.optimized_sync_batchnorm import _world
@@ -1225,9 +1263,21 @@ class _ConvBNResFn(torch.autograd.Function):
             mean_i = invstd_i = scale_i = shift_i = count_i = None
             y, part = _c1x1_forward_stats(src, w3, _kshift(bn), False)
         mean, invstd, scale, shift, count = _bn_finalize(bn, part, float(M), world, False)
-        out, bits = syncbn.forward_mask(y, z, scale, shift, bn.num_batches_tracked)
+        ds = cfg.bn_ds
+        if ds is not None:
+            # downsampling block: the downsample BatchNorm is normalised inside the residual pass
+            # (relu(bn3(y) + bn_ds(y_ds)): no normalised identity tensor) and its backward folded too
+            nb_d = ds.num_batches_tracked
+            bumped_d = world == 1 and ds.momentum is not None
+            mean_d, invstd_d, scale_d, shift_d, count_d = _bn_finalize(ds, pd, float(M), world, bumped_d)
+            if nb_d is not None and not bumped_d:
+                nb_d.add_(1)
+            out, bits = syncbn.forward_mask(y, yd, scale, shift, bn.num_batches_tracked, scale_d, shift_d)
+        else:
+            mean_d = invstd_d = count_d = None
+            out, bits = syncbn.forward_mask(y, z, scale, shift, bn.num_batches_tracked)
         ctx.save_for_backward(src, w3, y, bn_w, mean, invstd, count, bits, bn_in_w, mean_i, invstd_i, scale_i,
-                              shift_i, count_i)
+                              shift_i, count_i, yd, xd, wd, bnd_w, mean_d, invstd_d, count_d)
         ctx.cfg, ctx.world, ctx.pro = cfg, world, pro is not None
         ctx.mlink = _MaskLink(bits) if _MASK_PRODUCER else None
         if ctx.mlink is not None:
@@ -1243,8 +1293,8 @@ class _ConvBNResFn(torch.autograd.Function):
         from ..parallel.optimized_sync_batchnorm import _all_reduce_async
         from ..parallel import comm_stats
 
-        src, w3, y, bn_w, mean, invstd, count, bits, bn_in_w, mean_i, invstd_i, scale_i, shift_i, count_i = \
-            ctx.saved_tensors
+        src, w3, y, bn_w, mean, invstd, count, bits, bn_in_w, mean_i, invstd_i, scale_i, shift_i, count_i, \
+            yd, xd, wd, bnd_w, mean_d, invstd_d, count_d = ctx.saved_tensors
         cfg = ctx.cfg
         n, K, h, w = src.shape
         N = w3.size(0)
@@ -1275,6 +1325,31 @@ class _ConvBNResFn(torch.autograd.Function):
         gw3 = dW.view(N, K, 1, 1)
         if gw3.stride() != w3.stride():
             gw3 = gw3.contiguous(memory_format=torch.channels_last)
+        gwd = gw_d = gb_d = None
+        if cfg.bn_ds is not None:
+            # the downsample BatchNorm after the 1x1 (stride 1 or 2) downsample conv of the block input x: the
+            # same algebra on (g, x) -- dW_ds and its sums from P_ds = g^T x_s and the Gram matrix of x_s
+            # (the even pixels at stride 2); its data gradient is formed in _Conv1DsFn from (g, y_ds, A, B, D)
+            Cin = xd.size(1)
+            Wd = wd.view(N, Cin)
+            st = 2 if cfg.ds_s2 else 1
+            p_ws_d = bn_fold.wgrad_partials(xd, g, None, None, st)
+            g_ws_d, sa_ws_d = bn_fold.gram_partials(xd.permute(0, 2, 3, 1).reshape(-1, Cin), None, None,
+                                                    (xd.size(2), xd.size(3)) if cfg.ds_s2 else None)
+            P_d, Gm_d, Sa_d, sums_d, bn_grads_d = bn_fold.fold_reduce(Wd, p_ws_d, g_ws_d, sa_ws_d, sg_ws, mean_d,
+                                                                     invstd_d)
+            need_d = bnd_w is not None and (ctx.needs_input_grad[13] or ctx.needs_input_grad[14])
+            gw_d = bn_grads_d[:N].to(bnd_w.dtype) if need_d else None
+            gb_d = bn_grads_d[N:].to(bnd_w.dtype) if need_d else None
+            if ctx.world > 1:
+                with comm_stats.timed("syncbn_bwd", sums_d):
+                    _all_reduce_async(sums_d, cfg.bn_ds.process_group).wait()
+            dWd, abd_d = bn_fold.fold_finish(Wd, sums_d, count_d, mean_d, invstd_d, bnd_w, P_d, Gm_d, Sa_d)
+            gwd = dWd.view(N, Cin, 1, 1)
+            if gwd.stride() != wd.stride():
+                gwd = gwd.contiguous(memory_format=torch.channels_last)
+            cfg.ds_box["ds"] = (g2d, abd_d, yd.permute(0, 2, 3, 1).reshape(-1, N), Wd,
+                                (g, yd, mean_d, invstd_d, bnd_w, sums_d, count_d))
         # conv3's data gradient gx3 @ W3, gx3 = A g + B y + D: formed per fragment inside the strip GEMM where
         # it runs, else one elementwise pass; the previous BatchNorm's backward sums in the epilogue
         y2d = y.permute(0, 2, 3, 1).reshape(-1, N)
@@ -1333,7 +1408,8 @@ class _ConvBNResFn(torch.autograd.Function):
             if s_i is not None:
                 cfg.link_in.sums = s_i
             gx = da
-        return gx, None, gw3, gw_i, gb_i, gw, gb, g, None
+        gz = g if cfg.bn_ds is None else None
+        return gx, None, gw3, gw_i, gb_i, gw, gb, gz, None, None, None, None, gwd, gw_d, gb_d
 
 
 def _bnb_segments(g2d, W, epi):
@@ -1445,6 +1521,8 @@ assert _BN_RES_FOLD in ("pro", "all", "0"), f"BH_BN_RES_FOLD={_BN_RES_FOLD!r}"
 # also where hipBLASLt's residual GEMM ran before ("any", default); "1": only where the strip kernel is
 # preferred anyway; "0": the tail's own mask pass. Same box: 0 11102, 1 11195, any 11286 img/s
 _MASK_PRODUCER = os.environ.get("BH_MASK_PRODUCER", "any") != "0"
+# the downsample BatchNorm folded into the tail node too (BH_DS_FOLD=0: its own passes, A/B)
+_DS_FOLD = {"0": False, "1": True}.get(os.environ.get("BH_DS_FOLD", "1"), os.environ.get("BH_DS_FOLD", "1"))
 _MASK_PRODUCER_ANY = os.environ.get("BH_MASK_PRODUCER", "any") == "any"
 
 
@@ -1476,6 +1554,20 @@ class Bottleneck(nn.Module):
                         and b.running_mean is not None and b.running_mean.dtype == torch.float32 for b in bns)
                 and (self.downsample is None or len(self.downsample) == 2))
 
+    def _ds_fold_ok(self, x, yd, wd):
+        """The downsample BatchNorm folds into the tail node (_ConvBNResFn): the two-BatchNorm residual pass
+        keeps 4 C floats in LDS, the downsample conv's fp32 weight-gradient partials and Gram cover x."""
+        from ..ops import conv as bhconv
+
+        C, Cin = yd.size(1), x.size(1)
+        st = self.stride
+        # stride 1 only (by default): at stride 2 the Gram of the gathered input costs about what the removed
+        # passes save (BH_DS_FOLD=all also folds those)
+        if st == 2 and _DS_FOLD != "all":
+            return False
+        return (C <= 4096 and Cin % 64 == 0 and wd.dtype == x.dtype and bhconv.wgrad_supported(x, yd, 1, st) and
+                (st == 1 or (x.size(2) % 2 == 0 and x.size(3) % 2 == 0)))
+
     def _fold_bn2(self, y2):
         """bn2 folds into conv3 where conv3 runs on the 1x1 strip GEMM (the HBM-bound 56x56 / 28x28
         layers): its prologue variant measured 0.083 vs 0.19 ms for BN pass + GEMM + statistics pass at
@@ -1499,9 +1591,11 @@ class Bottleneck(nn.Module):
         # the convolutions' weights in x's dtype (amp O1 / O4: the per-iteration 16-bit copies)
         w1, w2, w3 = (_kw(c.weight, x) for c in (self.conv1, self.conv2, self.conv3))
         wd = _kw(ds[0].weight, x) if ds is not None else None
+        ds_box = None
         if ds is not None:  # conv1 and the downsample conv as one node (no residual stash needed)
+            ds_box = {}
             y1, p1, yd, pd = _Conv1DsFn.apply(x, w1, wd, _kshift(self.bn1), _kshift(ds[1]),
-                                              self.stride == 2)
+                                              self.stride == 2, ds_box)
             box = None
         else:
             box = {} if (torch.is_grad_enabled() and x.requires_grad) else None
@@ -1534,6 +1628,12 @@ class Bottleneck(nn.Module):
         # the tail as one node (conv3 -> bn3 -> + z -> ReLU, bn3's backward folded into conv3's): z is the
         # block input or the downsample BatchNorm's output, both shaped like conv3's output
         if _conv_bn_res_ok(src, w3, yd if ds is not None else x, fold2):
+            if ds is not None and _DS_FOLD and self._ds_fold_ok(x, yd, wd):
+                cfg = _FoldCfg(self.bn2 if fold2 else None, self.bn3, None if fold2 else l2, ds[1], ds_box,
+                               self.stride == 2)
+                return _ConvBNResFn.apply(src, p2 if fold2 else None, w3, self.bn2.weight if fold2 else None,
+                                          self.bn2.bias if fold2 else None, self.bn3.weight, self.bn3.bias, None,
+                                          cfg, yd, pd, x, wd, ds[1].weight, ds[1].bias)
             if ds is not None:
                 identity = ds[1].forward_from_stats(yd, pd)
             else:

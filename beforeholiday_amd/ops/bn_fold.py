@@ -39,12 +39,16 @@ def _bn():
 
 
 def gram(a: torch.Tensor, pro_scale: Optional[torch.Tensor] = None,
-         pro_shift: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+         pro_shift: Optional[torch.Tensor] = None, s2=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """``(a'.T @ a', colsum(a'))`` in fp32 for ``a [M, K]``, ``a' = relu(a * pro_scale + pro_shift)`` rounded to
-    a's dtype when a prologue is given (the activation a folded BatchNorm + ReLU never wrote)."""
+    a's dtype when a prologue is given (the activation a folded BatchNorm + ReLU never wrote). ``s2=(H, W)``:
+    the rows are the even pixels (2y, 2x) of ``a`` viewed as ``[.., H, W, K]``."""
     if a.is_cuda:
-        gp, cp = _bn().gram(a, pro_scale, pro_shift)
+        gp, cp = _bn().gram(a, pro_scale, pro_shift, *(s2 or (0, 0)))
         return gp.sum(0), cp.sum(0)
+    if s2 is not None:
+        H, W = s2
+        a = a.view(-1, H, W, a.size(1))[:, ::2, ::2, :].reshape(-1, a.size(1))
     af = a.float()
     if pro_scale is not None:
         af = torch.relu(af * pro_scale + pro_shift).to(a.dtype).float()
@@ -64,14 +68,16 @@ def mask_colsum(g: torch.Tensor, bits: torch.Tensor) -> Tuple[torch.Tensor, torc
 
 
 def wgrad_f32(x: torch.Tensor, dy: torch.Tensor, pro_scale: Optional[torch.Tensor] = None,
-              pro_shift: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``dy.T @ x'`` over the pixels of two channels_last NCHW tensors (1x1 convolution, stride 1) as fp32
+              pro_shift: Optional[torch.Tensor] = None, stride: int = 1) -> torch.Tensor:
+    """``dy.T @ x'`` over the pixels of two channels_last NCHW tensors (1x1 convolution, stride 1 or 2) as fp32
     ``[K_out, C_in]``, never rounded to 16 bits (kernels/conv_wgrad.hip partials, summed here)."""
-    n, c, h, w = x.shape
     k = dy.size(1)
+    c = x.size(1)
     if x.is_cuda:
-        ws = submodule("conv_cuda").conv_wgrad_f32(x, dy, 1, 1, pro_scale, pro_shift)
+        ws = submodule("conv_cuda").conv_wgrad_f32(x, dy, 1, stride, pro_scale, pro_shift)
         return ws.sum(0).view(k, c)
+    if stride == 2:
+        x = x[:, :, ::2, ::2]
     xf = x.permute(0, 2, 3, 1).reshape(-1, c).float()
     if pro_scale is not None:
         xf = torch.relu(xf * pro_scale + pro_shift).to(x.dtype).float()
@@ -111,14 +117,14 @@ def mask_colsum_partials(g: torch.Tensor, bits: torch.Tensor):
     return _bn().mask_colsum(g, bits)
 
 
-def gram_partials(a: torch.Tensor, pro_scale=None, pro_shift=None):
-    """GPU: ``(Gram partials [S, K, K], column-sum partials [S, K])`` of ``a'``."""
-    return _bn().gram(a, pro_scale, pro_shift)
+def gram_partials(a: torch.Tensor, pro_scale=None, pro_shift=None, s2=None):
+    """GPU: ``(Gram partials [S, K, K], column-sum partials [S, K])`` of ``a'`` (``s2``: see :func:`gram`)."""
+    return _bn().gram(a, pro_scale, pro_shift, *(s2 or (0, 0)))
 
 
-def wgrad_partials(x: torch.Tensor, dy: torch.Tensor, pro_scale=None, pro_shift=None) -> torch.Tensor:
+def wgrad_partials(x: torch.Tensor, dy: torch.Tensor, pro_scale=None, pro_shift=None, stride: int = 1) -> torch.Tensor:
     """GPU: ``dy.T @ x'`` as fp32 split partials ``[parts, K_out * C_in]``."""
-    return submodule("conv_cuda").conv_wgrad_f32(x, dy, 1, 1, pro_scale, pro_shift)
+    return submodule("conv_cuda").conv_wgrad_f32(x, dy, 1, stride, pro_scale, pro_shift)
 
 
 def fold_reduce(W, p_ws, g_ws, sa_ws, sg_ws, mean, invstd):

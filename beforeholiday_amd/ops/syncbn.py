@@ -147,10 +147,20 @@ def mask_ok(x, z):
     return x.is_cuda and z is not None and z.dtype == x.dtype and z.shape == x.shape and _native().mask_ok(x)
 
 
-def forward_mask(x, z, scale, shift, num_batches=None):
+def forward_mask(x, z, scale, shift, num_batches=None, zscale=None, zshift=None):
     """Fused ``relu(x*scale + shift + z)`` that also returns the ReLU mask packed 8 channels per byte
-    (uint8 ``[rows, C/8]``); backward then reads 1 bit per element instead of the residual ``z``."""
-    return _native().forward_mask(x, z, scale, shift, num_batches)
+    (uint8 ``[rows, C/8]``); backward then reads 1 bit per element instead of the residual ``z``. With
+    ``zscale / zshift`` the residual is ``z*zscale + zshift`` (a second BatchNorm normalised in the same pass)."""
+    if not x.is_cuda:
+        zz = z.float() if zscale is None else z.float() * _bcast(zscale, z) + _bcast(zshift, z)
+        if num_batches is not None:
+            num_batches += 1
+        pre = x.float() * _bcast(scale, x) + _bcast(shift, x) + zz
+        out = torch.relu(pre).to(x.dtype).contiguous(memory_format=torch.channels_last)
+        pos = (pre > 0).permute(0, 2, 3, 1).reshape(-1, x.size(1) // 8, 8).to(torch.int32)
+        bits = (pos << torch.arange(8, dtype=torch.int32)).sum(-1).to(torch.uint8)
+        return out, bits
+    return _native().forward_mask(x, z, scale, shift, num_batches, zscale, zshift)
 
 
 def _pool_out(n, k, s, p):

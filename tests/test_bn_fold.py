@@ -170,7 +170,9 @@ def test_fused_tail_matches_per_layer_path(cfg):
     finally:
         R._BN_RES_FOLD = old
     (o1, gx1, pg1, b1), (o2, gx2, pg2, b2) = res
-    assert torch.equal(o1, o2)
+    # (identity blocks: the same forward kernels; downsampling blocks: the downsample BatchNorm is applied in
+    # the residual pass without rounding the normalised identity to 16 bits first)
+    assert torch.equal(o1, o2) if stride == 1 and inplanes == 4 * planes else _rel(o1, o2) < 2e-3
     assert _rel(gx1, gx2) < 2e-2
     for n in pg2:
         assert _rel(pg1[n], pg2[n]) < 2e-2, n
@@ -296,3 +298,61 @@ def test_c1x1_column_slice_lda():
         out, _ = conv_bn.c1x1(g[:, cols], W[cols], b_trans=True, bnb=a3[:, cols].reshape(-1).contiguous(),
                               bnb_y=y[:, cols], lda=N, resid=out)
     assert _rel(out, ref) < 3e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C", [256, 2048])
+def test_forward_mask_two_batchnorms(C):
+    """relu(x * s + t + z * sz + tz) with the ReLU bit mask in one pass (the downsampling block's residual)."""
+    from beforeholiday_amd.ops import syncbn
+
+    torch.manual_seed(0)
+    x = torch.randn(4, C, 7, 9, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    z = torch.randn(4, C, 7, 9, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    s, t = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.2
+    sz, tz = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.2
+    nb = torch.zeros((), dtype=torch.long, device="cuda")
+    out, bits = syncbn.forward_mask(x, z, s, t, nb, sz, tz)
+    ro, rb = syncbn.forward_mask(x.cpu(), z.cpu(), s.cpu(), t.cpu(), None, sz.cpu(), tz.cpu())
+    assert _rel(out, ro) < 2e-3
+    assert int(nb) == 1
+    assert (bits.cpu() != rb).float().mean() < 1e-3  # ties at 0 may round either way
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [(64, 64, 1, 56, 16), (256, 128, 2, 56, 16)])
+def test_downsample_fold_matches_own_passes(cfg):
+    """Downsampling block with the downsample BatchNorm folded into the tail (BH_DS_FOLD) vs its own passes."""
+    from test_resnet_fold import _block
+
+    inplanes, planes, stride, hw, bs = cfg
+    R, _, blk = _block(inplanes, planes, stride, torch.float16)
+    x = torch.randn(bs, inplanes, hw, hw, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    ho = (hw + stride - 1) // stride
+    g = torch.randn(bs, planes * 4, ho, ho, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    old, oldr = R._DS_FOLD, R._BN_RES_FOLD
+    state0 = {k: v.clone() for k, v in blk.state_dict().items()}
+    res = []
+    try:
+        R._BN_RES_FOLD = "all"
+        for on in (True, False):
+            R._DS_FOLD = "all" if on else False
+            blk.load_state_dict(state0)
+            blk.zero_grad(set_to_none=True)
+            xi = x.clone().requires_grad_()
+            out = blk(xi)
+            out.backward(g)
+            res.append((out.detach().clone(), xi.grad.clone(), {n: p.grad.clone() for n, p in blk.named_parameters()},
+                        {n: b.clone() for n, b in blk.named_buffers()}))
+    finally:
+        R._DS_FOLD, R._BN_RES_FOLD = old, oldr
+    (o1, gx1, pg1, b1), (o2, gx2, pg2, b2) = res
+    assert _rel(o1, o2) < 2e-3
+    assert _rel(gx1, gx2) < 2e-2
+    for n in pg2:
+        assert _rel(pg1[n], pg2[n]) < 2e-2, n
+    for n in b2:
+        if "num_batches" in n:
+            assert int(b1[n]) == int(b2[n]), n
+        else:
+            assert _rel(b1[n], b2[n]) < 1e-5, n
