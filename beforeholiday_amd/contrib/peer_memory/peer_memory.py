@@ -251,7 +251,11 @@ class PeerAllReduce:
     statistics exchange of group batch norm (reference: apex/contrib/csrc/groupbn/ipc.cu:22-129 and
     the peer-buffer exchange of nhwc_batch_norm_kernel.h). Every rank must issue the same sequence of
     calls with the same payload sizes, like any collective. Without a native pool (CPU / gloo) it
-    falls back to ``dist.all_reduce``."""
+    falls back to ``dist.all_reduce``.
+
+    The exchange epoch lives in device memory (``epoch_dev``): each kernel takes the previous value + 1
+    and stores it back, so the exchange can be captured in a HIP graph and every replay publishes and
+    waits for a fresh epoch on every rank (a host counter would be frozen into the captured kernel)."""
 
     def __init__(self, peer_pool, capacity=1 << 14, group=None, max_spins=1 << 22):
         self.pool = peer_pool
@@ -269,6 +273,7 @@ class PeerAllReduce:
             self._slot_ptrs = [t.data_ptr() for t in self.slots]
             self._flag_ptrs = [t.data_ptr() for t in self.flags]
             self.err = torch.zeros(1, dtype=torch.int32, device="cuda")
+            self.epoch_dev = torch.zeros(1, dtype=torch.int32, device="cuda")
             self._watch = _ErrorWatch(self.err, "PeerAllReduce")
 
     @property
@@ -281,10 +286,10 @@ class PeerAllReduce:
             dist.all_reduce(t, group=self.group)
             return t
         assert t.dtype == torch.float32 and t.is_contiguous(), "PeerAllReduce: contiguous fp32 tensors only"
-        self.epoch += 1
+        self.epoch += 1  # (host count of calls; the kernel's epoch is the device counter)
         self._watch.check()  # an earlier exchange timed out: raise before adding to the damage
-        _pm().peer_allreduce(t, t, self._slot_ptrs, self._flag_ptrs, self.capacity, self.me, self.epoch, self.err,
-                             self.max_spins)
+        _pm().peer_allreduce(t, t, self._slot_ptrs, self._flag_ptrs, self.capacity, self.me, 1, self.err,
+                             self.max_spins, self.epoch_dev)
         self._watch.after_launch()
         return t
 

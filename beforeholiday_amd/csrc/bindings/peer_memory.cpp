@@ -176,7 +176,8 @@ void push_pull_halos_1d(at::Tensor out_lo, at::Tensor out_hi, at::Tensor in_lo, 
 // SUM all-reduce of the fp32 vector `in` (into `out`, may alias) over the pool's ranks: slots[q] /
 // flags[q] are the device addresses of rank q's [2, G, capacity] slot array and int32 [G] flags.
 void peer_allreduce(at::Tensor in, at::Tensor out, std::vector<int64_t> slots, std::vector<int64_t> flags,
-                    int64_t capacity, int64_t me, int64_t epoch, at::Tensor err, int64_t max_spins) {
+                    int64_t capacity, int64_t me, int64_t epoch, at::Tensor err, int64_t max_spins,
+                    c10::optional<at::Tensor> epoch_dev) {
   TORCH_CHECK(in.is_cuda() && in.scalar_type() == at::kFloat && in.is_contiguous(), "in must be contiguous fp32 GPU");
   TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() == in.numel(),
               "out must match in");
@@ -199,6 +200,11 @@ void peer_allreduce(at::Tensor in, at::Tensor out, std::vector<int64_t> slots, s
   a.epoch = (int)epoch;
   a.max_spins = (int)max_spins;
   a.err = err.data_ptr<int>();
+  if (epoch_dev.has_value() && epoch_dev->defined()) {
+    TORCH_CHECK(epoch_dev->is_cuda() && epoch_dev->scalar_type() == at::kInt && epoch_dev->numel() == 1,
+                "epoch_dev must be a GPU int32 [1] tensor");
+    a.epoch_dev = epoch_dev->data_ptr<int>();
+  }
   bh::peer_allreduce(a, stream_for(in));
 }
 
@@ -217,7 +223,10 @@ void register_peer_memory(pybind11::module_& root) {
   m.def("blob_view_float", [](int64_t raw, std::vector<int64_t> shape, bool cl) { return blob_view(raw, shape, cl, at::kFloat); });
   m.def("blob_view_int", [](int64_t raw, std::vector<int64_t> shape, bool cl) { return blob_view(raw, shape, cl, at::kInt); });
   m.def("push_pull_halos_1d", &push_pull_halos_1d);
-  m.def("peer_allreduce", &peer_allreduce, "one-shot IPC SUM all-reduce of a small fp32 vector (group BN statistics)");
+  m.def("peer_allreduce", &peer_allreduce, py::arg("in"), py::arg("out"), py::arg("slots"), py::arg("flags"),
+        py::arg("capacity"), py::arg("me"), py::arg("epoch"), py::arg("err"), py::arg("max_spins"),
+        py::arg("epoch_dev") = py::none(),
+        "one-shot IPC SUM all-reduce of a small fp32 vector (group BN statistics); epoch_dev: device epoch counter");
 }
 
 }  // namespace bhb

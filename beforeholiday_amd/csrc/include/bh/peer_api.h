@@ -57,6 +57,9 @@ struct PeerReduceArgs {
   int* flags[kPeerMaxRanks];    // int32 [G] flag array of each rank
   int G, me, L, epoch, max_spins;
   int* err;
+  // device-resident epoch counter (int32 [1]); when set, the kernel takes epoch = *epoch_dev + 1 and stores it
+  // back, so a captured HIP graph replays with a fresh epoch each time (the host epoch is ignored)
+  int* epoch_dev = nullptr;
 };
 void peer_allreduce(const PeerReduceArgs& a, hipStream_t st);
 

@@ -129,7 +129,11 @@ __global__ __launch_bounds__(kBlock) void k_halo_1d(HaloArgs a) {
 constexpr int kReduceBlock = 512;
 
 __global__ __launch_bounds__(kReduceBlock) void k_peer_allreduce(PeerReduceArgs a) {
-  const int parity = a.epoch & 1;
+  __shared__ int ep;
+  if (threadIdx.x == 0) ep = a.epoch_dev ? a.epoch_dev[0] + 1 : a.epoch;
+  __syncthreads();
+  const int epoch = ep;
+  const int parity = epoch & 1;
   // 1. push: my payload into row `me` of every rank's slot array (vector stores over xGMI)
   for (int q = 0; q < a.G; ++q) {
     float* dst = a.slots[q] + ((int64_t)parity * a.G + a.me) * a.L;
@@ -140,14 +144,14 @@ __global__ __launch_bounds__(kReduceBlock) void k_peer_allreduce(PeerReduceArgs 
   if (threadIdx.x == 0) {
     __atomic_thread_fence(__ATOMIC_RELEASE);
     for (int q = 0; q < a.G; ++q)
-      if (q != a.me) __hip_atomic_store(a.flags[q] + a.me, a.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (q != a.me) __hip_atomic_store(a.flags[q] + a.me, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   // 3. one lane per peer waits (bounded) for that peer's rows of this epoch
   __shared__ int ok;
   if (threadIdx.x == 0) ok = 1;
   __syncthreads();
   const int q = threadIdx.x;
-  if (q < a.G && q != a.me && !wait_epoch(a.flags[a.me] + q, a.epoch, a.max_spins)) {
+  if (q < a.G && q != a.me && !wait_epoch(a.flags[a.me] + q, epoch, a.max_spins)) {
     ok = 0;
     __hip_atomic_store(a.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -164,6 +168,7 @@ __global__ __launch_bounds__(kReduceBlock) void k_peer_allreduce(PeerReduceArgs 
     }
     a.out[i] = s;
   }
+  if (a.epoch_dev && threadIdx.x == 0) a.epoch_dev[0] = epoch;  // (read above, before the barrier)
 }
 
 }  // namespace

@@ -238,7 +238,8 @@ class DistributedDataParallel(Module):
                  allreduce_trigger_params=None, retain_allreduce_buffers=False, allreduce_always_fp32=False,
                  num_allreduce_streams=1, allreduce_communicators=None, gradient_average=True,
                  gradient_predivide_factor=1.0, gradient_average_split_factor=None, prof=False,
-                 process_group=None, bucket_cap_mb=None, first_bucket_mb=None, gradient_as_bucket_view=False):
+                 process_group=None, bucket_cap_mb=None, first_bucket_mb=None, gradient_as_bucket_view=False,
+                 force_collectives=False):
         super().__init__()
         if shared_param is not None:
             raise ValueError("shared_param is no longer supported as an option.  It was misleadingly named "
@@ -254,6 +255,10 @@ class DistributedDataParallel(Module):
         self.process_group = process_group
         self.world_size = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
+        # a single-process world skips every collective unless force_collectives (an initialised process
+        # group is required then): the bucket / hook / async all-reduce path runs as with several ranks --
+        # how a one-GPU box exercises the RCCL code paths (tests/test_rccl_world1.py)
+        self._collectives = self.world_size > 1 or (bool(force_collectives) and dist.is_initialized())
         self.message_size = int(message_size)
         # byte-based bucket policy (MI355X): ``bucket_cap_mb`` replaces the element-count
         # ``message_size`` cut; ``first_bucket_mb`` makes the first bucket of each dtype small so its
@@ -289,7 +294,7 @@ class DistributedDataParallel(Module):
         self._hooks = []
 
         # sync parameters and buffers from rank 0
-        if self.world_size > 1:
+        if self._collectives:
             root = _group_rank0(process_group)
             tensors = [p.data for p in module.parameters()] + [b.data for b in module.buffers()]
             for bucket in split_by_type(tensors):
@@ -325,7 +330,7 @@ class DistributedDataParallel(Module):
         self._param_to_bucket = {}
         self._arrival = []
         self._next_bucket = 0
-        if self.world_size > 1:
+        if self._collectives:
             for idx, p in enumerate(self.active_params):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(idx)))
 
@@ -353,7 +358,7 @@ class DistributedDataParallel(Module):
     def forward(self, *inputs, **kwargs):
         if self.prof:
             torch.cuda.nvtx.range_push("forward pass DDP logic")
-        if self.world_size > 1:
+        if self._collectives:
             if [id(p) for p in self.module.parameters() if p.requires_grad] != self._param_ids:
                 self._refresh_params()
             self._callback_queued = False

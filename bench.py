@@ -173,9 +173,11 @@ def main():
                                                                    stem_pool_fused=args.stem == "fused")).cuda()
     model = model.to(memory_format=torch.channels_last)
     global_batch = args.batch * world
-    # the whole step as one HIP graph (single rank; the loss scale must live on the device: FusedLAMB /
-    # FusedSGD with the device scaler, or a static scale -- O4 / O5 -- for FusedAdam, whose lr / step
-    # then stay on the device too: capturable=True)
+    # the whole step as one HIP graph (the loss scale must live on the device: FusedLAMB / FusedSGD with the
+    # device scaler, or a static scale -- O4 / O5 -- for FusedAdam, whose lr / step then stay on the device
+    # too: capturable=True). By default with one rank only: several ranks can capture too (--graph on: the
+    # IPC statistics exchange keeps its epoch on the device, RCCL all-reduces capture -- tests/test_rccl_world1.py),
+    # but that path has not been measured on an 8-GPU node, and the step is GPU-bound (graph vs eager +1 %)
     graph_ok = world == 1 and not args.host_scaler and (args.optimizer != "adam" or args.opt_level in ("O4", "O5"))
     use_graph = args.graph == "on" or (args.graph == "auto" and graph_ok)
     if args.optimizer == "lamb":
