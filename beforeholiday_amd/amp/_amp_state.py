@@ -39,7 +39,12 @@ def maybe_print(msg, rank0=False):
 
 
 def master_params(optimizer):
-    """Iterates over the params owned by ``optimizer`` (the fp32 masters under O2)."""
+    """Iterates over the params owned by ``optimizer`` (the fp32 masters under O2). A pending fused
+    mixed-precision step first materialises the master gradients, so e.g. gradient clipping on them
+    sees what the unfused path would have produced."""
+    plan = getattr(getattr(optimizer, "_amp_stash", None), "plan", None)
+    if plan is not None and hasattr(plan, "materialize"):
+        plan.materialize()
     for group in optimizer.param_groups:
         for p in group["params"]:
             yield p

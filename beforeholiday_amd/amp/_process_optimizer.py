@@ -12,6 +12,16 @@ and a :class:`_GradPlan` that implements the three moments of a mixed-precision 
 * after ``optimizer.step()`` the fp32 masters are copied back into the 16-bit model parameters (one
   launch per dtype; FusedSGD writes them inside its own kernel).
 
+Fused mixed-precision step (O2 / O5 with FusedLAMB or FusedAdam on the GPU): ``finish`` leaves the
+scaled 16-bit gradients where they are -- under a dynamic scale it only runs the norm of them, which
+sets the overflow flag and is the scaled global norm LAMB needs -- and ``optimizer.step()`` runs ONE
+native call whose kernels read those gradients times the device inverse scale, update the fp32
+masters and write the 16-bit model parameters (the reference's mixed-precision LAMB,
+csrc/multi_tensor_lamb_mp.cu:41,248,367; FusedSGD's 4-list copy, apex/optimizers/fused_sgd.py:245-252).
+Neither the fp32 master gradients nor the separate master-to-model pass exist on that path. Anything
+that needs the master gradients before the step (``amp.master_params``, a second ``scale_loss``
+accumulating into the same step) materialises them first, so the unfused semantics are kept.
+
 Three plans: :class:`_MasterPlan` (O2 / O5: fp32 master copies replace the 16-bit parameters inside
 the optimizer), :class:`_FusedSGDMasterPlan` (FusedSGD folds the unscale into its kernel unless
 ``materialize_master_grads``) and :class:`_ModelPlan` (O1 / O4 / O0: the model parameters are the
@@ -23,10 +33,13 @@ import types
 
 import torch
 
-from ..multi_tensor_apply import multi_tensor_applier
+from ..multi_tensor_apply import multi_tensor_applier, multi_tensor_applier_l2norm
 from ..ops import amp_C
 
 _LOW = (torch.float16, torch.bfloat16)
+
+# the fused mixed-precision step (module docstring); False keeps the unscale + step + copy sequence
+fused_master_step = True
 
 
 class AmpOptimizerState(object):
@@ -203,17 +216,104 @@ class _MasterPlan(_GradPlan):
         for p in masters + fp32:
             p.grad = None
 
+    _fused = None  # (inverse scale tensor or None, scaled norm or None) while a fused step is pending
+    _inv = None
+    _inv_of = None
+    _models = None
+
     def prepare(self):
         self.ensure()
         st = self.stash
+        if self._fused is not None:  # a second backward before the step: accumulate the unfused way
+            self.materialize()
         for p in st.all_fp16_params:  # 16-bit grads are folded into the fp32 master grads: drop them
             p.grad = None
         for i, p in enumerate(st.all_fp32_from_fp32_params):
             st.all_fp32_from_fp32_grad_stash[i], p.grad = _keep(p), None
 
+    # ---- fused mixed-precision step
+    def _fused_wanted(self, scaler):
+        from .scaler import LossScaler
+
+        ok = getattr(self.opt, "_amp_fused_ok", None)
+        return (fused_master_step and ok is not None and LossScaler.has_fused_kernel and ok()
+                and all(m.grad is None for m in self.stash.all_fp32_from_fp16_params))
+
+    def _inverse_scale(self, scaler, dev):
+        """A one-element device tensor holding 1/scale of this backward (None for a static scale of 1).
+        Plan-owned, so the scale update between ``finish`` and the step cannot change it."""
+        if scaler.device_mode:
+            if self._inv is None or self._inv.device != dev:
+                self._inv = torch.empty(1, dtype=torch.float32, device=dev)
+            torch.reciprocal(scaler._scale_dev, out=self._inv)
+            self._inv_of = None
+            return self._inv
+        scale = float(scaler.loss_scale())
+        if scale == 1.0:
+            return None
+        if self._inv is None or self._inv.device != dev or self._inv_of != scale:
+            self._inv = torch.full((1,), 1.0 / scale, dtype=torch.float32, device=dev)
+            self._inv_of = scale
+        return self._inv
+
+    def _start_fused(self, scaler, grads):
+        inv = self._inverse_scale(scaler, grads[0].device)
+        norm = None
+        if scaler.dynamic:
+            # the overflow check: a non-finite partial sum sets the flag update_scale reads; the value
+            # is the norm of the scaled gradients, which LAMB's global norm reuses
+            flag = scaler._overflow_buf if scaler.device_mode else scaler._flag_for(grads)
+            by_dt = {}
+            for g in grads:
+                by_dt.setdefault(g.dtype, []).append(g)
+            norms = [multi_tensor_applier_l2norm(amp_C.multi_tensor_l2norm, flag, [gl], False)[0]
+                     for gl in by_dt.values()]
+            norm = norms[0] if len(norms) == 1 else multi_tensor_applier_l2norm(
+                amp_C.multi_tensor_l2norm, flag, [norms], False)[0]
+        self._fused = (inv, norm)
+
+    def fused_pending(self):
+        return self._fused is not None
+
+    def discard(self):
+        """The pending fused step is dropped (skipped overflow step, zero_grad)."""
+        self._fused = None
+
+    def materialize(self):
+        """Turn a pending fused step back into fp32 master gradients (the unfused state)."""
+        if self._fused is None:
+            return
+        inv, _ = self._fused
+        self._fused = None
+        st = self.stash
+        pairs = []
+        for low, master in zip(st.all_fp16_params, st.all_fp32_from_fp16_params):
+            if low.grad is not None:
+                master.grad = torch.empty_like(master)
+                pairs.append((low.grad, master.grad))
+        for ins, outs in _by_dtype(pairs).values():
+            multi_tensor_applier(amp_C.multi_tensor_scale, st.dummy_overflow_buf, [ins, outs],
+                                 inv if inv is not None else 1.0)
+
+    def fused_step(self):
+        inv, norm = self._fused
+        self._fused = None
+        st = self.stash
+        if self._models is None or len(self._models) != len(st.all_fp16_params):
+            self._models = {id(m): p for m, p in zip(st.all_fp32_from_fp16_params, st.all_fp16_params)}
+        with torch.no_grad():
+            self.opt._amp_fused_step(self._models, inv, norm)
+
     def finish(self, scaler):
         self.ensure()
         st = self.stash
+        if self._fused is None and self._fused_wanted(scaler):
+            grads = [p.grad for p in st.all_fp16_params if p.grad is not None]
+            if grads:
+                self._start_fused(scaler, grads)
+                _unscale_into_models(scaler, st.all_fp32_from_fp32_params, st.all_fp32_from_fp32_grad_stash)
+                return
+        self.materialize()
         new_pairs, acc_pairs = [], []
         for low, master in zip(st.all_fp16_params, st.all_fp32_from_fp16_params):
             if low.grad is None:
@@ -246,6 +346,7 @@ class _MasterPlan(_GradPlan):
 
         self.ensure()
         st = self.stash
+        self.discard()
         zero_param_grads(st.all_fp16_params + st.all_fp32_from_fp32_params, set_to_none)
         for p in st.all_fp32_from_fp16_params:
             p.grad = None
@@ -311,9 +412,12 @@ def _process_optimizer(optimizer, properties):
         def step(self, closure=None):
             if closure is not None:
                 raise RuntimeError("Currently, Amp does not support closure use with optimizers.")
-            out = inner_step()
-            if not fused_sgd:  # FusedSGD writes the 16-bit params inside its kernel
-                plan.masters_to_model()
+            if plan.fused_pending():  # one native call: unscale + update + 16-bit write
+                out = plan.fused_step()
+            else:
+                out = inner_step()
+                if not fused_sgd:  # FusedSGD writes the 16-bit params inside its kernel
+                    plan.masters_to_model()
             for p in self._amp_stash.all_fp32_from_fp16_params:
                 p.grad = None
             return out

@@ -12,15 +12,19 @@ from .scaler import LossScaler
 def _device_scaler_wanted(loss_scaler, optimizers):
     """BH_AMP_DEVICE_SCALER=1, dynamic scaling, the fused unscale kernel, a CUDA loss, and only fused
     optimizers whose kernels return early on a set noop flag (``_dummy_overflow_buf``): FusedLAMB
-    (both stages) and FusedSGD."""
+    (both stages), FusedSGD and FusedAdam (table path)."""
     import os
 
-    from ..optimizers import FusedLAMB, FusedSGD
+    from ..optimizers import FusedAdam, FusedLAMB, FusedSGD
+
+    def flag_aware(o):
+        if isinstance(o, FusedAdam):  # the native table path reads the flag; capturable has its own scaler API
+            return not o.capturable and not o.master_weights
+        return isinstance(o, (FusedLAMB, FusedSGD))
 
     return (os.environ.get("BH_AMP_DEVICE_SCALER", "0") == "1" and loss_scaler.dynamic
             and LossScaler.has_fused_kernel and torch.cuda.is_available()
-            and all(isinstance(o, (FusedLAMB, FusedSGD)) and hasattr(o, "_dummy_overflow_buf")
-                    for o in optimizers))
+            and all(flag_aware(o) and hasattr(o, "_dummy_overflow_buf") for o in optimizers))
 
 
 class _StepGate(object):
@@ -49,6 +53,9 @@ class _StepGate(object):
             opt = self.optimizer
             for p in getattr(opt._amp_stash, "all_fp32_from_fp16_params", ()):
                 p.grad = None
+            plan = getattr(opt._amp_stash, "plan", None)
+            if plan is not None and hasattr(plan, "discard"):
+                plan.discard()
             if hasattr(opt, "most_recent_scale"):
                 opt.most_recent_scale = 1.0
                 opt.scale_set_by_backward = False

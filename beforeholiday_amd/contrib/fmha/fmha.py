@@ -1,36 +1,65 @@
 """Fused multi-head attention over variable-length packed sequences
-(reference: apex/contrib/fmha/fmha.py:34-76, ``fmhalib``: sm80-only kernels for seq <= 512, head 64).
+(reference: apex/contrib/fmha/fmha.py:34-76, ``fmhalib`` fwd / bwd taking ``cu_seqlens``,
+apex/contrib/csrc/fmha/fmha_api.cpp:358-360; sm80-only kernels for seq <= 512, head 64).
 
-Input ``qkv`` [total_tokens, 3, heads, head_dim] with ``cu_seqlens`` [batch + 1]. Sequences are
-scattered into a padded batch once. Head size 64 (the reference's only head size; its sequence
-cap is 512) runs the MFMA fused attention kernels (kernels/attn.hip: whole-row kernels up to 128
-tokens, flash kernels beyond; key padding mask, Philox dropout regenerated in backward) on a
-[S, B*heads, 3, 64] padded layout; other head sizes use batched GEMMs (hipBLASLt) around the fused mask + softmax + dropout kernel of
-``contrib.multihead_attn``. Any sequence length up to 4096 and any head size.
+Input ``qkv`` [total_tokens, 3, heads, head_dim] with ``cu_seqlens`` int32 [batch + 1] and the
+caller's bound ``max_s`` on the lengths. Head size 64 on the GPU runs the MFMA flash kernels
+(kernels/attn.hip, 32x32x16 tiles, online softmax, Philox dropout regenerated in backward) straight
+on the packed tokens: every (sequence, head) problem rebases its q / k / v / o pointers by
+``cu_seqlens[b]`` on the device and bounds its rows by the sequence length (``varlen_rebase``), so
+there is no padding copy, no host read of the lengths, and the call is capturable in a HIP graph.
+The backward writes d(qkv) in the packed layout. Other head sizes / CPU: padded batched GEMMs around
+the fused mask + softmax + dropout kernel of ``contrib.multihead_attn`` (that path reads the lengths on
+the host).
 """
 import torch
 
-from ..multihead_attn._core import MASK_PAD, FusedSelfAttnFn, MaskSoftmaxDropoutFn, _fused_ok
+from ..._native import submodule
+from ..multihead_attn._core import MASK_PAD, MaskSoftmaxDropoutFn, _fused_ok, _seed
 
 
-def fmha_varlen(qkv, cu_seqlens, p_dropout, max_s, is_training):
+class FlashVarlenFn(torch.autograd.Function):
+    """qkv [total, 3, heads, 64] (packed) -> context [total, heads, 64]."""
+
+    @staticmethod
+    def forward(ctx, qkv, cu_seqlens, max_s, p_dropout, is_training, causal=False):
+        fa = submodule("fused_attention")
+        seed = _seed()
+        scale = qkv.size(-1) ** -0.5
+        cu = cu_seqlens.to(device=qkv.device, dtype=torch.int32).contiguous()
+        out, lse = fa.flash_varlen_forward(qkv[:, 0], qkv[:, 1], qkv[:, 2], cu, int(max_s), causal, scale,
+                                           float(p_dropout), bool(is_training), seed)
+        ctx.save_for_backward(qkv, cu, out, lse)
+        ctx.args = (int(max_s), causal, scale, float(p_dropout), bool(is_training), seed)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, cu, out, lse = ctx.saved_tensors
+        max_s, causal, scale, p, training, seed = ctx.args
+        dqkv = torch.empty_like(qkv)
+        submodule("fused_attention").flash_varlen_backward(
+            dout.contiguous(), qkv[:, 0], qkv[:, 1], qkv[:, 2], out, lse, cu, max_s, causal, scale, p, training, seed,
+            dqkv[:, 0], dqkv[:, 1], dqkv[:, 2])
+        return dqkv, None, None, None, None, None
+
+
+def _aligned(qkv):
+    return qkv.stride(-1) == 1 and qkv.stride(0) % 8 == 0 and qkv.stride(1) % 8 == 0 and qkv.stride(2) % 8 == 0 \
+        and qkv.data_ptr() % 16 == 0
+
+
+def fmha_varlen(qkv, cu_seqlens, p_dropout, max_s, is_training, causal=False):
     total, three, h, d = qkv.shape
     assert three == 3
+    if _fused_ok(qkv, d, max_s) and _aligned(qkv):
+        return FlashVarlenFn.apply(qkv, cu_seqlens, max_s, p_dropout, is_training, causal)
+    assert not causal, "fmha_varlen: causal masking needs the fused (head_dim 64, GPU) path"
     lens = (cu_seqlens[1:] - cu_seqlens[:-1]).tolist()
     B = len(lens)
     S = max(max(lens), 1) if lens else 1
     pos = torch.arange(S, device=qkv.device).unsqueeze(0)
     valid = pos < torch.tensor(lens, device=qkv.device).unsqueeze(1)  # [B, S]
-    if _fused_ok(qkv, d, S):
-        # [S, B, heads, 3, d] -> q/k/v are [S, B*heads, d] views with a uniform batch*head stride
-        padded = qkv.new_zeros(S, B, h, 3, d)
-        tok = valid.t().nonzero(as_tuple=True)  # (t, b) of every valid token
-        src = qkv[(cu_seqlens[:-1][tok[1]] + tok[0]).long()]  # [n, 3, h, d]
-        padded[tok[0], tok[1]] = src.permute(0, 2, 1, 3)
-        ctx = FusedSelfAttnFn.apply(padded.view(S, B * h, 3, d), h, d ** -0.5, ~valid, MASK_PAD, p_dropout,
-                                    is_training)
-        ctx = ctx.view(S, B, h, d).transpose(0, 1)  # [B, S, h, d]
-        return ctx[valid]
     padded = qkv.new_zeros(B, S, 3, h, d)
     padded = padded.index_put((valid.nonzero(as_tuple=True)), qkv)
     q, k, v = (padded[:, :, i].permute(0, 2, 1, 3) for i in range(3))  # [B, h, S, d]

@@ -465,6 +465,74 @@ void flash_bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Te
   bh::flash_backward(dt, a, stream_for(q));
 }
 
+// varlen: q / k / v / o / dout / dq / dk / dv are packed [total_tokens, heads, 64] views (e.g. the
+// slices of one [total, 3, heads, 64] qkv tensor), cu_seqlens int32 [B + 1] on the device. max_s
+// (the caller's bound on the lengths, as in fmhalib) sizes the grid; nothing is read back.
+bh::AttnArgs varlen_args(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, const at::Tensor& cu,
+                         int64_t max_s, bool causal, double scale, double p, bool training, int64_t seed) {
+  attn_check(q, "q");
+  attn_check(k, "k");
+  attn_check(v, "v");
+  check_cuda(cu, "cu_seqlens");
+  TORCH_CHECK(cu.scalar_type() == at::kInt && cu.dim() == 1 && cu.numel() >= 2 && cu.is_contiguous(),
+              "flash varlen: cu_seqlens must be a contiguous int32 [B + 1] tensor");
+  TORCH_CHECK(q.scalar_type() == k.scalar_type() && q.scalar_type() == v.scalar_type(), "flash varlen: dtype mismatch");
+  TORCH_CHECK(q.sizes() == k.sizes() && q.sizes() == v.sizes(), "flash varlen: q / k / v shape mismatch");
+  TORCH_CHECK(max_s >= 1, "flash varlen: max_s must be >= 1");
+  bh::AttnArgs a;
+  a.q = q.data_ptr(); a.k = k.data_ptr(); a.v = v.data_ptr();
+  a.q_st = q.stride(0); a.q_sbh = q.stride(1);
+  a.k_st = k.stride(0); a.k_sbh = k.stride(1);
+  a.v_st = v.stride(0); a.v_sbh = v.stride(1);
+  a.heads = (int)q.size(1);
+  a.BH = (int)((cu.numel() - 1) * q.size(1));
+  a.sq = a.sk = (int)max_s;
+  a.cu_seqlens = cu.data_ptr<int>();
+  a.mask_mode = causal ? 5 : 0;
+  a.scale = (float)scale;
+  a.p_drop = (float)p;
+  a.training = training;
+  a.seed = (uint64_t)seed;
+  return a;
+}
+
+std::vector<at::Tensor> flash_varlen_fwd(at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor cu, int64_t max_s,
+                                         bool causal, double scale, double p, bool training, int64_t seed) {
+  auto a = varlen_args(q, k, v, cu, max_s, causal, scale, p, training, seed);
+  auto o = at::empty({q.size(0), q.size(1), 64}, q.options());
+  auto lse = at::empty({(int64_t)a.BH, max_s}, q.options().dtype(at::kFloat));
+  a.o = o.data_ptr(); a.o_st = o.stride(0); a.o_sbh = o.stride(1);
+  a.lse = lse.data_ptr<float>();
+  if (q.size(0) > 0) bh::flash_forward(dtype_code(q.scalar_type()), a, stream_for(q));
+  return {o, lse};
+}
+
+void flash_varlen_bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse,
+                      at::Tensor cu, int64_t max_s, bool causal, double scale, double p, bool training, int64_t seed,
+                      at::Tensor dq, at::Tensor dk, at::Tensor dv) {
+  auto a = varlen_args(q, k, v, cu, max_s, causal, scale, p, training, seed);
+  attn_check(dout, "dout");
+  attn_check(o, "o");
+  attn_check(dq, "dq");
+  attn_check(dk, "dk");
+  attn_check(dv, "dv");
+  for (const auto* t : {&dout, &o, &dq, &dk, &dv})
+    TORCH_CHECK(t->sizes() == q.sizes(), "flash varlen backward: gradient / output shape mismatch");
+  TORCH_CHECK(lse.is_contiguous() && lse.numel() == (int64_t)a.BH * max_s, "flash varlen backward: lse must be [BH, max_s]");
+  if (q.size(0) == 0) return;
+  a.o = o.data_ptr(); a.o_st = o.stride(0); a.o_sbh = o.stride(1);
+  a.dout = dout.data_ptr(); a.do_st = dout.stride(0); a.do_sbh = dout.stride(1);
+  a.dq = dq.data_ptr(); a.dq_st = dq.stride(0); a.dq_sbh = dq.stride(1);
+  a.dk = dk.data_ptr(); a.dk_st = dk.stride(0); a.dk_sbh = dk.stride(1);
+  a.dv = dv.data_ptr(); a.dv_st = dv.stride(0); a.dv_sbh = dv.stride(1);
+  auto delta = at::empty_like(lse);
+  a.lse = lse.data_ptr<float>();
+  const int dt = dtype_code(q.scalar_type());
+  bh::flash_delta(dt, a, delta.data_ptr<float>(), stream_for(q));
+  a.delta = delta.data_ptr<float>();
+  bh::flash_backward(dt, a, stream_for(q));
+}
+
 }  // namespace
 
 void register_contrib(pybind11::module_& root) {
@@ -481,6 +549,13 @@ void register_contrib(pybind11::module_& root) {
          py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("lse"), py::arg("mask_mode"),
          py::arg("mask"), py::arg("heads"), py::arg("scale"), py::arg("p"), py::arg("training"), py::arg("seed"),
          py::arg("mask_fill"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("bits") = py::none());
+  fa.def("flash_varlen_forward", &flash_varlen_fwd, "packed variable-length attention forward -> (o, lse)",
+         py::arg("q"), py::arg("k"), py::arg("v"), py::arg("cu_seqlens"), py::arg("max_s"), py::arg("causal"),
+         py::arg("scale"), py::arg("p"), py::arg("training"), py::arg("seed"));
+  fa.def("flash_varlen_backward", &flash_varlen_bwd, "packed variable-length attention backward into dq / dk / dv",
+         py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("lse"),
+         py::arg("cu_seqlens"), py::arg("max_s"), py::arg("causal"), py::arg("scale"), py::arg("p"),
+         py::arg("training"), py::arg("seed"), py::arg("dq"), py::arg("dk"), py::arg("dv"));
   fa.def("flash_mask_bits", &flash_mask_bits_op, "mode-4 mask [B, sq, sk] -> packed bits for the flash kernels");
 }
 

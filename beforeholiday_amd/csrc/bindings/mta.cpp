@@ -525,36 +525,66 @@ class ParamTable {
 
   // hyper[g] = {lr, beta1, beta2, eps, step, bias_correction, weight_decay, grad_averaging}
   // steps (optional): int32 [groups] device step counters (amp's device-resident loss scale): the
-  // bias corrections use them, so a step skipped on the device does not advance them
+  // bias corrections use them, so a step skipped on the device does not advance them.
+  // An entry with a master tensor updates the fp32 master from the gradient of its (16-bit) parameter
+  // and writes the parameter back in stage 2 (the 5-list mixed-precision launch of
+  // csrc/multi_tensor_lamb_mp.cu:41,248,367 in the reference). With ``inv_scale`` those gradients
+  // are still loss-scaled: the kernels unscale them on the fly, and the global norm blends
+  // ``scaled_norm`` (their norm, computed by amp's overflow check) times inv_scale with the norm of
+  // the plain gradients -- no fp32 master gradient is ever materialised.
   bool lamb_step(at::Tensor noop, std::vector<std::vector<double>> hyper, int64_t mode, double max_grad_norm,
-                 bool nvlamb, c10::optional<at::Tensor> steps) {
+                 bool nvlamb, c10::optional<at::Tensor> steps, c10::optional<at::Tensor> inv_scale,
+                 c10::optional<at::Tensor> scaled_norm) {
     TORCH_CHECK(hyper.size() == groups_.size(), "ParamTable.lamb_step: one hyper-parameter row per group");
-    std::vector<std::map<std::pair<int, int>, Lists>> buckets(groups_.size());
-    std::map<int, std::vector<at::Tensor>> by_gdt;
+    const bool scaled = inv_scale.has_value();
+    // key: (target dtype, grad dtype, copy dtype or -1)
+    std::vector<std::map<std::tuple<int, int, int>, Lists>> buckets(groups_.size());
+    std::map<int, std::vector<at::Tensor>> plain_gdt, scaled_gdt;
     for (size_t gi = 0; gi < groups_.size(); ++gi) {
       const Group& g = groups_[gi];
       for (size_t i = 0; i < g.p.size(); ++i) {
         at::Tensor grad = grad_of(g.p[i], "FusedLAMB");
         if (!grad.defined()) continue;
         if (!g.s0[i].defined() || !g.s1[i].defined()) return false;
-        auto& l = buckets[gi][{(int)g.p[i].scalar_type(), (int)grad.scalar_type()}];
-        if (l.empty()) l.resize(4);
+        const bool use_master = g.master[i].defined();
+        const at::Tensor& target = use_master ? g.master[i] : g.p[i];
+        auto& l = buckets[gi][{(int)target.scalar_type(), (int)grad.scalar_type(),
+                               use_master ? (int)g.p[i].scalar_type() : -1}];
+        if (l.empty()) l.resize(use_master ? 5 : 4);
         l[0].push_back(grad);
-        l[1].push_back(g.p[i]);
+        l[1].push_back(target);
         l[2].push_back(g.s0[i]);
         l[3].push_back(g.s1[i]);
-        by_gdt[(int)grad.scalar_type()].push_back(grad);
+        if (use_master) l[4].push_back(g.p[i]);
+        ((use_master && scaled) ? scaled_gdt : plain_gdt)[(int)grad.scalar_type()].push_back(grad);
       }
     }
-    if (by_gdt.empty()) return true;
+    if (plain_gdt.empty() && scaled_gdt.empty()) return true;
     check_noop(noop);
     if (steps.has_value())
       TORCH_CHECK(steps->is_cuda() && steps->scalar_type() == at::kInt && steps->numel() >= (int64_t)groups_.size(),
                   "ParamTable.lamb_step: steps must be a CUDA int32 tensor with one counter per group");
+    if (scaled)
+      TORCH_CHECK(inv_scale->is_cuda() && inv_scale->scalar_type() == at::kFloat && inv_scale->numel() == 1,
+                  "ParamTable.lamb_step: inv_scale must be a one-element CUDA fp32 tensor");
     // global gradient norm: one deterministic norm per gradient dtype, blended on the device
+    auto norm_of = [&](std::vector<at::Tensor> l) {
+      return std::get<0>(norm_impl(kNormChunk, noop, {std::move(l)}, false, 2, false, 1.0, false));
+    };
     std::vector<at::Tensor> norms;
-    for (auto& kv : by_gdt) norms.push_back(std::get<0>(norm_impl(kNormChunk, noop, {kv.second}, false, 2, false, 1.0, false)));
-    at::Tensor gnorm = norms.size() == 1 ? norms[0] : std::get<0>(norm_impl(kNormChunk, noop, {norms}, false, 2, false, 1.0, false));
+    for (auto& kv : plain_gdt) norms.push_back(norm_of(kv.second));
+    if (!scaled_gdt.empty()) {
+      at::Tensor sn;
+      if (scaled_norm.has_value()) {
+        sn = *scaled_norm;
+      } else {
+        std::vector<at::Tensor> sl;
+        for (auto& kv : scaled_gdt) sl.push_back(norm_of(kv.second));
+        sn = sl.size() == 1 ? sl[0] : norm_of(sl);
+      }
+      norms.push_back(at::mul(sn.reshape({1}), *inv_scale));
+    }
+    at::Tensor gnorm = norms.size() == 1 ? norms[0] : norm_of(norms);
     for (size_t gi = 0; gi < groups_.size(); ++gi) {
       const auto& h = hyper[gi];
       TORCH_CHECK(h.size() == 8, "ParamTable.lamb_step: 8 hyper-parameters per group");
@@ -564,6 +594,7 @@ class ParamTable {
         a.grad_norm = gnorm.data_ptr<float>();
         a.noop = noop.data_ptr<int>();  // a set flag (amp's device-resident overflow) skips the step
         if (steps.has_value()) a.step_ptr = steps->data_ptr<int>() + gi;
+        if (scaled && kv.second.size() == 5) a.inv_scale = inv_scale->data_ptr<float>();
         lamb_run(kv.second, kElemChunk, noop, a);
       }
     }
@@ -571,12 +602,16 @@ class ParamTable {
   }
 
   // hyper[g] = {lr, beta1, beta2, eps, step, bias_correction, weight_decay}; a group entry with a
-  // master tensor updates the fp32 master and writes the 16-bit parameter in the same launch
-  bool adam_step(at::Tensor noop, std::vector<std::vector<double>> hyper, int64_t mode) {
+  // master tensor updates the fp32 master and writes the 16-bit parameter in the same launch, reading
+  // the parameter's gradient times ``inv_scale`` when given (amp O2 / O5 without master gradients).
+  // A set noop flag skips every launch; ``steps`` are device step counters as in lamb_step.
+  bool adam_step(at::Tensor noop, std::vector<std::vector<double>> hyper, int64_t mode,
+                 c10::optional<at::Tensor> steps, c10::optional<at::Tensor> inv_scale) {
     TORCH_CHECK(hyper.size() == groups_.size(), "ParamTable.adam_step: one hyper-parameter row per group");
     // every group is checked before anything launches: a retry after state creation must not
     // update the groups that were already complete a second time
-    std::vector<std::map<std::tuple<int, int, int, bool>, Lists>> all(groups_.size());
+    std::vector<std::map<std::tuple<int, int, int, int>, Lists>> all(groups_.size());
+    bool any = false;
     for (size_t gi = 0; gi < groups_.size(); ++gi) {
       const Group& g = groups_[gi];
       auto& buckets = all[gi];
@@ -586,23 +621,49 @@ class ParamTable {
         if (!g.s0[i].defined() || !g.s1[i].defined()) return false;
         const bool use_master = g.master[i].defined();
         const at::Tensor& target = use_master ? g.master[i] : g.p[i];
-        auto& l = buckets[{(int)target.scalar_type(), (int)g.s0[i].scalar_type(), (int)grad.scalar_type(), use_master}];
+        auto& l = buckets[{(int)target.scalar_type(), (int)g.s0[i].scalar_type(), (int)grad.scalar_type(),
+                           use_master ? (int)g.p[i].scalar_type() : -1}];
         if (l.empty()) l.resize(use_master ? 5 : 4);
         l[0].push_back(grad);
         l[1].push_back(target);
         l[2].push_back(g.s0[i]);
         l[3].push_back(g.s1[i]);
         if (use_master) l[4].push_back(g.p[i]);
+        any = true;
       }
     }
+    if (!any) return true;
+    check_noop(noop);
+    if (steps.has_value())
+      TORCH_CHECK(steps->is_cuda() && steps->scalar_type() == at::kInt && steps->numel() >= (int64_t)groups_.size(),
+                  "ParamTable.adam_step: steps must be a CUDA int32 tensor with one counter per group");
+    if (inv_scale.has_value())
+      TORCH_CHECK(inv_scale->is_cuda() && inv_scale->scalar_type() == at::kFloat && inv_scale->numel() == 1,
+                  "ParamTable.adam_step: inv_scale must be a one-element CUDA fp32 tensor");
     for (size_t gi = 0; gi < groups_.size(); ++gi) {
       auto& buckets = all[gi];
       if (buckets.empty()) continue;
       const auto& h = hyper[gi];
       TORCH_CHECK(h.size() == 7, "ParamTable.adam_step: 7 hyper-parameters per group");
-      for (auto& kv : buckets)
-        multi_tensor_adam(kElemChunk, noop, kv.second, h[0], h[1], h[2], h[3], (int64_t)h[4], mode, (int64_t)h[5],
-                          h[6]);
+      for (auto& kv : buckets) {
+        const Lists& lists = kv.second;
+        bh::AdamArgs a{};
+        a.lr = (float)h[0];
+        a.beta1 = (float)h[1];
+        a.beta2 = (float)h[2];
+        a.eps = (float)h[3];
+        a.bias_correction = (int)h[5];
+        a.bc1 = a.bias_correction ? 1.f - (float)std::pow(h[1], h[4]) : 1.f;
+        a.bc2 = a.bias_correction ? 1.f - (float)std::pow(h[2], h[4]) : 1.f;
+        a.decay = (float)h[6];
+        a.mode = (int)mode;
+        a.noop = noop.data_ptr<int>();
+        if (steps.has_value()) a.step_ptr = steps->data_ptr<int>() + gi;
+        if (inv_scale.has_value() && lists.size() == 5) a.inv_scale = inv_scale->data_ptr<float>();
+        const auto& p = get_plan(lists, kElemChunk);
+        bh::mta_adam(p.view, list_dtype(lists[0], "adam"), list_dtype(lists[1], "adam"),
+                     list_dtype(lists[2], "adam"), copy_dtype(lists, 4), a, stream_for(noop));
+      }
     }
     return true;
   }
@@ -622,10 +683,18 @@ class ParamTable {
     const auto st = p.scalar_type();
     TORCH_CHECK(st == at::kFloat || st == at::kHalf || st == at::kBFloat16 || st == at::kDouble, who,
                 " only supports fp16, bf16, fp32 and fp64 parameters");
-    if (p.numel() <= 1 || g.strides() == p.strides()) return g;
+    if (p.numel() <= 1 || same_order(g, p)) return g;
     at::Tensor c = g.contiguous(p.suggest_memory_format());
-    TORCH_CHECK(c.strides() == p.strides(), who, ": gradient layout differs from the parameter's");
+    TORCH_CHECK(same_order(c, p), who, ": gradient layout differs from the parameter's");
     return c;
+  }
+  // the same element order in memory: equal strides on every dimension longer than 1 (a [K, C, 1, 1]
+  // weight is both contiguous and channels_last, with different strides on the unit dims)
+  static bool same_order(const at::Tensor& a, const at::Tensor& b) {
+    if (a.sizes() != b.sizes()) return false;
+    for (int64_t d = 0; d < a.dim(); ++d)
+      if (a.size(d) > 1 && a.stride(d) != b.stride(d)) return false;
+    return true;
   }
 
   std::vector<Group> groups_;
@@ -672,8 +741,10 @@ void register_amp_C(pybind11::module_& root) {
            py::arg("master") = std::vector<c10::optional<at::Tensor>>())
       .def("num_groups", &ParamTable::num_groups)
       .def("lamb_step", &ParamTable::lamb_step, py::arg("noop_flag"), py::arg("hyper"), py::arg("mode"),
-           py::arg("max_grad_norm"), py::arg("use_nvlamb"), py::arg("steps") = py::none())
-      .def("adam_step", &ParamTable::adam_step, py::arg("noop_flag"), py::arg("hyper"), py::arg("mode"));
+           py::arg("max_grad_norm"), py::arg("use_nvlamb"), py::arg("steps") = py::none(),
+           py::arg("inv_scale") = py::none(), py::arg("scaled_norm") = py::none())
+      .def("adam_step", &ParamTable::adam_step, py::arg("noop_flag"), py::arg("hyper"), py::arg("mode"),
+           py::arg("steps") = py::none(), py::arg("inv_scale") = py::none());
   m.def("plan_cache_clear", &plan_cache_clear);
 }
 

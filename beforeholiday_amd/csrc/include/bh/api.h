@@ -68,6 +68,7 @@ struct AdamArgs {
   const float* found_inf;    // optional: skip when != 0
   const int* step_ptr;       // optional device step: bias corrections computed on device
   int bias_correction;
+  const int* noop;           // optional skip flag (int; amp's device-resident overflow)
 };
 // lists: g, p, m, v [, p_copy]  (depth 4 or 5)
 void mta_adam(const MTAView& v, int dt_g, int dt_p, int dt_s, int dt_copy, const AdamArgs& a,

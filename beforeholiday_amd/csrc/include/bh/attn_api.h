@@ -44,6 +44,10 @@ struct AttnArgs {
   // over keys (bit j of word w = key 32w+j), mbits_t [B, sk, ceil(sq/32)] words over queries
   const uint32_t* mbits = nullptr;
   const uint32_t* mbits_t = nullptr;
+  // varlen: int32 [B + 1] prefix sums of the sequence lengths (device). The q/k/v/o/grad tensors are
+  // then packed [total_tokens, heads, 64] (st = token stride, sbh = head stride), BH = B * heads,
+  // sq = sk = max_s, lse / delta [BH, max_s]. Flash 32x32 kernels, mask modes 0 / 5.
+  const int* cu_seqlens = nullptr;
 };
 
 int attn_max_sk();

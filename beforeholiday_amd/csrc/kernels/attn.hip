@@ -420,6 +420,41 @@ BH_DEVICE void flash_tile(int& tile, int& bh) {
   bh = (slot / nx) * 8 + (id & 7);
 }
 
+// Variable-length packed sequences (AttnArgs::cu_seqlens; the reference's fmhalib takes cu_seqlens,
+// apex/contrib/csrc/fmha/fmha_api.cpp:358-360): problem bh = (sequence b, head hd) owns tokens
+// cu[b] .. cu[b+1]-1 of the packed q / k / v / o / dO / dQ / dK / dV (token stride *_st, head stride
+// *_sbh), and lse / delta stay [BH, max_s] with a.sq = a.sk = max_s on entry. The kernels address a
+// problem as base + bh * sbh + row * st with a.sq / a.sk rows, so rebasing every pointer by
+// (cu[b] * st + hd * sbh - bh * sbh) and setting sq = sk = the sequence length lets the same code run
+// on the packed tokens: no padding copy, no host read of the lengths. Returns false when the tile
+// starting at row ``first`` lies past the sequence (the whole workgroup exits).
+template <typename T>
+BH_DEVICE bool varlen_rebase(AttnArgs& a, int bh, int first) {
+  const int b = bh / a.heads, hd = bh - b * a.heads;
+  const int s0 = a.cu_seqlens[b];
+  const int n = min(a.cu_seqlens[b + 1] - s0, a.sq);  // max_s bounds the lse / delta rows of a problem
+  if (first >= n) return false;
+  auto cshift = [&](const void*& p, int64_t st, int64_t sbh) {
+    if (p) p = reinterpret_cast<const T*>(p) + (int64_t)s0 * st + (int64_t)hd * sbh - (int64_t)bh * sbh;
+  };
+  auto shift = [&](void*& p, int64_t st, int64_t sbh) {
+    if (p) p = reinterpret_cast<T*>(p) + (int64_t)s0 * st + (int64_t)hd * sbh - (int64_t)bh * sbh;
+  };
+  cshift(a.q, a.q_st, a.q_sbh);
+  cshift(a.k, a.k_st, a.k_sbh);
+  cshift(a.v, a.v_st, a.v_sbh);
+  cshift(a.dout, a.do_st, a.do_sbh);
+  shift(a.o, a.o_st, a.o_sbh);
+  shift(a.dq, a.dq_st, a.dq_sbh);
+  shift(a.dk, a.dk_st, a.dk_sbh);
+  shift(a.dv, a.dv_st, a.dv_sbh);
+  const int64_t d = (int64_t)bh * (a.sq - n);  // lse[bh * max_s + q] == lse'[bh * n + q]
+  if (a.lse) a.lse += d;
+  if (a.delta) a.delta += d;
+  a.sq = a.sk = n;
+  return true;
+}
+
 // 64 rows x 128 B of a head operand: 2 x 16-byte chunks per thread. The loads are unconditional
 // (rows past `valid` re-read the last valid row) and the zero fill of those rows happens when the
 // registers are written to LDS: a select right after a load would make the compiler wait for the
@@ -861,6 +896,7 @@ __global__ __launch_bounds__(kThreads, 3) void k_flash_fwd32(AttnArgs a) {
   int qtile, bh;
   flash_tile(qtile, bh);
   if (MODE == 5) qtile = gridDim.x - 1 - qtile;  // longest causal prefix first
+  if (a.cu_seqlens && !varlen_rebase<T>(a, bh, qtile * kFQ)) return;
   const int q0w = qtile * kFQ + wave * 32;
   const int myq = q0w + r32;
 
@@ -1034,6 +1070,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_flash_dq32(AttnArgs a) {
   int qtile, bh;
   flash_tile(qtile, bh);
   if (MODE == 5) qtile = gridDim.x - 1 - qtile;
+  if (a.cu_seqlens && !varlen_rebase<T>(a, bh, qtile * kFQ)) return;
   const int q0w = qtile * kFQ + wave * 32;
   const int myq = q0w + r32;
   const T* K = reinterpret_cast<const T*>(a.k) + (int64_t)bh * a.k_sbh;
@@ -1184,6 +1221,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_flash_dkdv32(AttnArgs a) {
   const int r32 = lane & 31, h = lane >> 5;
   int ktile, bh;
   flash_tile(ktile, bh);
+  if (a.cu_seqlens && !varlen_rebase<T>(a, bh, ktile * kFQ)) return;
   const int k0w = ktile * kFQ + wave * 32;
   const int mykey = k0w + r32;
   const T* K = reinterpret_cast<const T*>(a.k) + (int64_t)bh * a.k_sbh;
@@ -1346,6 +1384,10 @@ __global__ __launch_bounds__(256) void k_flash_delta(AttnArgs a, float* __restri
   const int sub = threadIdx.x & 15;
   if (row >= (int64_t)a.BH * a.sq) return;
   const int bh = (int)(row / a.sq), q = (int)(row % a.sq);
+  if (a.cu_seqlens && !varlen_rebase<T>(a, bh, q)) {  // a padding row of a shorter sequence
+    if (sub == 0) delta[row] = 0.f;
+    return;
+  }
   const T* o = reinterpret_cast<const T*>(a.o) + (int64_t)q * a.o_st + (int64_t)bh * a.o_sbh + sub * 4;
   const T* d = reinterpret_cast<const T*>(a.dout) + (int64_t)q * a.do_st + (int64_t)bh * a.do_sbh + sub * 4;
   float acc = 0.f;
@@ -1682,6 +1724,8 @@ void flash_forward(int dt, const AttnArgs& a, hipStream_t st) {
     const char* e = getenv("BH_FLASH_FWD16");
     return e && e[0] == '1';
   }();
+  if (a.cu_seqlens && (legacy || (a.mask_mode != 0 && a.mask_mode != 5)))
+    throw std::runtime_error("flash_forward: varlen runs the 32x32 kernels with mask mode 0 or 5 only");
   if (!legacy && (a.mask_mode == 0 || a.mask_mode == 5 || (a.mask_mode == 4 && a.mbits))) {
     const dim3 grid((unsigned)((a.sq + kFQ - 1) / kFQ), (unsigned)a.BH);
     flash_dispatch(dt, a.mask_mode, "flash_forward", [&](auto tt, auto mm) {
@@ -1720,6 +1764,8 @@ void flash_backward(int dt, const AttnArgs& a, hipStream_t st) {
     const char* e = getenv("BH_FLASH_BWD16");
     return e && e[0] == '1';
   }();
+  if (a.cu_seqlens && (legacy || (a.mask_mode != 0 && a.mask_mode != 5)))
+    throw std::runtime_error("flash_backward: varlen runs the 32x32 kernels with mask mode 0 or 5 only");
   if (!legacy && (a.mask_mode == 0 || a.mask_mode == 5 || (a.mask_mode == 4 && a.mbits && a.mbits_t))) {
     const dim3 gq((unsigned)((a.sq + kFQ - 1) / kFQ), (unsigned)a.BH);
     const dim3 gk((unsigned)((a.sk + kFQ - 1) / kFQ), (unsigned)a.BH);

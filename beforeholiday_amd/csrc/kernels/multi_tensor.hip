@@ -191,7 +191,7 @@ __global__ __launch_bounds__(kBlock) void k_norm_finalize(MTAView v, const float
 // ------------------------------------------------------------------------------------
 template <typename Tg, typename Tp, typename Ts, typename Tc>
 __global__ __launch_bounds__(kBlock) void k_adam(MTAView v, AdamArgs a) {
-  if (a.found_inf && *a.found_inf != 0.f) return;
+  if ((a.found_inf && *a.found_inf != 0.f) || (a.noop && *a.noop)) return;
   MTA_PROLOGUE(v);
   const Tg* g = mta_ptr<const Tg>(v, 0, t, base);
   Tp* p = mta_ptr<Tp>(v, 1, t, base);

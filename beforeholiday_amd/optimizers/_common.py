@@ -62,10 +62,17 @@ class ParamTableMixin:
     once in a native ``amp_C.ParamTable`` and a step is ONE call that reads the gradients in C++
     (see csrc/bindings/mta.cpp). The table is rebuilt when the param groups change, after
     ``load_state_dict`` / ``add_param_group``, and when a parameter gets its first gradient (the step
-    returns False before launching anything, the optimizer creates that state and retries)."""
+    returns False before launching anything, the optimizer creates that state and retries).
+
+    Under amp O2 / O5 a second table (``_amp_native_table``) pairs every fp32 master (the optimizer's
+    parameter, owner of the state) with its 16-bit model parameter: the step reads the model
+    parameter's (still loss-scaled) gradient and writes the model parameter back in the same launch
+    (amp/_process_optimizer.py, ``_MasterPlan`` fused path)."""
 
     _table = None
     _table_sig = None
+    _amp_table = None
+    _amp_table_sig = None
     native_table = True  # False: always the per-step tensor-list path (kept for A/B tests)
 
     def _table_signature(self):
@@ -87,6 +94,40 @@ class ParamTableMixin:
         self._table, self._table_sig = table, sig
         return table
 
+    def _amp_native_table(self, state_keys, models):
+        """``models``: {id(fp32 master): 16-bit model parameter}. Entries whose parameter is not a
+        master (amp's fp32-from-fp32 parameters) are plain entries."""
+        sig = (self._table_signature(), len(models))
+        if self._amp_table is not None and self._amp_table_sig == sig:
+            return self._amp_table
+        from .._native import submodule
+
+        table = submodule("amp_C").ParamTable()
+        for g in self.param_groups:
+            sts = [self.state.get(p) or {} for p in g["params"]]
+            table.add_group([models.get(id(p), p) for p in g["params"]],
+                            [st.get(state_keys[0]) for st in sts], [st.get(state_keys[1]) for st in sts],
+                            [p if id(p) in models else None for p in g["params"]])
+        self._amp_table, self._amp_table_sig = table, sig
+        return table
+
+    def _reset_tables(self):
+        self._table = None
+        self._amp_table = None
+
+    def _device_step_counters(self):
+        """amp's device-resident loss scale: the noop flag may skip a step on the device, so the step
+        counters the bias corrections use advance on the device only when it does not (None when the
+        host counters are exact)."""
+        if not getattr(self, "_device_step", False):
+            return None
+        steps = getattr(self, "_device_steps", None)
+        if steps is None or steps.numel() != len(self.param_groups):
+            steps = self._device_steps = torch.tensor([g["step"] - 1 for g in self.param_groups], dtype=torch.int32,
+                                                      device=self._dummy_overflow_buf.device)
+        steps.add_((self._dummy_overflow_buf == 0).to(torch.int32))
+        return steps
+
     def _fast_path_ok(self):
         if not self.native_table:
             return False
@@ -97,10 +138,18 @@ class ParamTableMixin:
 
         return available()
 
+    def state_dict(self):
+        steps = getattr(self, "_device_steps", None)
+        if steps is not None:  # the device counters are the real step counts (skipped steps excluded)
+            for g, st in zip(self.param_groups, steps.tolist()):
+                g["step"] = int(st)
+        return super().state_dict()
+
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
-        self._table = None
+        self._reset_tables()
+        self._device_steps = None  # re-seeded from the loaded host counters
 
     def add_param_group(self, param_group):
         super().add_param_group(param_group)
-        self._table = None
+        self._reset_tables()

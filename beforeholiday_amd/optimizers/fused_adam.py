@@ -60,8 +60,12 @@ class FusedAdam(ParamTableMixin, torch.optim.Optimizer):
             state["exp_avg_sq"] = torch.zeros_like(target, dtype=sdt)
         return state, use_master, target
 
-    def _native_step(self):
-        """GPU step through the native parameter table (one host call for every group's launches)."""
+    def _native_step(self, amp_models=None, inv_scale=None):
+        """GPU step through the native parameter table (one host call for every group's launches).
+        ``amp_models`` ({id(master): 16-bit model param}): amp O2 / O5's fused step -- the fp32
+        masters (this optimizer's parameters) are updated from the model parameters' 16-bit
+        gradients times the device ``inv_scale`` and the model parameters are written in the same
+        launch (no fp32 master gradient, no separate master-to-model copy)."""
         hyper = []
         for group in self.param_groups:
             group["step"] = group.get("step", 0) + 1
@@ -69,15 +73,29 @@ class FusedAdam(ParamTableMixin, torch.optim.Optimizer):
             hyper.append([float(group["lr"]), beta1, beta2, group["eps"], group["step"],
                           1 if group["bias_correction"] else 0, group["weight_decay"]])
         master = "master_param" if self.master_weights else None
-        args = (self._dummy_overflow_buf, hyper, self.adam_w_mode)
-        if not self._native_table(("exp_avg", "exp_avg_sq"), master).adam_step(*args):
+        keys = ("exp_avg", "exp_avg_sq")
+        args = (self._dummy_overflow_buf, hyper, self.adam_w_mode, self._device_step_counters(), inv_scale)
+
+        def table():
+            if amp_models is None:
+                return self._native_table(keys, master)
+            return self._amp_native_table(keys, amp_models)
+
+        if not table().adam_step(*args):
             for group in self.param_groups:
                 for p in group["params"]:
-                    if p.grad is not None:
+                    src = p if amp_models is None else amp_models.get(id(p), p)
+                    if src.grad is not None:
                         self._init_state(p)
-            self._table = None
-            if not self._native_table(("exp_avg", "exp_avg_sq"), master).adam_step(*args):
+            self._reset_tables()
+            if not table().adam_step(*args):
                 raise RuntimeError("FusedAdam: optimizer state missing after initialisation")
+
+    def _amp_fused_ok(self):
+        return not self.capturable and not self.master_weights and self._fast_path_ok()
+
+    def _amp_fused_step(self, models, inv_scale, scaled_norm):
+        self._native_step(models, inv_scale)
 
     @torch.no_grad()
     def step(self, closure=None, grads=None, output_params=None, scale=None, grad_norms=None,
@@ -91,6 +109,10 @@ class FusedAdam(ParamTableMixin, torch.optim.Optimizer):
                 loss = closure()
         if not self.capturable and grad_scaler is None and self._fast_path_ok():
             self._native_step()
+            return loss
+        if getattr(self, "_device_step", False) and bool(self._dummy_overflow_buf.item()):
+            # device-scaled amp on the list path: the list kernels do not read the flag, and the host
+            # step counters must not advance for a skipped step either
             return loss
         inv_scale = found_inf = None
         if grad_scaler is not None:

@@ -51,9 +51,14 @@ class FusedLAMB(ParamTableMixin, torch.optim.Optimizer):
             return norms[0]
         return multi_tensor_applier_l2norm(self.multi_tensor_l2norm, self._dummy_overflow_buf, [norms], False)[0]
 
-    def _native_step(self):
+    def _native_step(self, amp_models=None, inv_scale=None, scaled_norm=None):
         """GPU step through the native parameter table: one host call for the global norm and every
-        group's LAMB launches (same kernels and semantics as the list path below)."""
+        group's LAMB launches (same kernels and semantics as the list path below).
+
+        ``amp_models`` ({id(master): 16-bit model param}) is amp O2's fused mixed-precision step: the
+        gradients are read from the model parameters, unscaled by the device ``inv_scale`` inside the
+        kernels, and stage 2 writes the model parameters (reference: csrc/multi_tensor_lamb_mp.cu:41,
+        248,367). ``scaled_norm`` is the norm of those scaled gradients if amp already computed it."""
         hyper = []
         for group in self.param_groups:
             group["step"] = group.get("step", 0) + 1
@@ -61,37 +66,30 @@ class FusedLAMB(ParamTableMixin, torch.optim.Optimizer):
             hyper.append([float(group["lr"]), beta1, beta2, group["eps"], group["step"],
                           1 if group["bias_correction"] else 0, group["weight_decay"],
                           1 if group["grad_averaging"] else 0])
-        steps = None
-        if getattr(self, "_device_step", False):
-            # amp's device-resident loss scale: the noop flag may skip this step on the device, so the
-            # step counters the bias corrections use advance on the device only when it does not
-            if getattr(self, "_device_steps", None) is None or self._device_steps.numel() != len(self.param_groups):
-                self._device_steps = torch.tensor([g["step"] - 1 for g in self.param_groups], dtype=torch.int32,
-                                                  device=self._dummy_overflow_buf.device)
-            self._device_steps.add_((self._dummy_overflow_buf == 0).to(torch.int32))
-            steps = self._device_steps
+        steps = self._device_step_counters()
+        keys = ("exp_avg", "exp_avg_sq")
         args = (self._dummy_overflow_buf, hyper, self.adam_w_mode, self.defaults["max_grad_norm"], self.use_nvlamb,
-                steps)
-        if not self._native_table(("exp_avg", "exp_avg_sq")).lamb_step(*args):
+                steps, inv_scale, scaled_norm)
+
+        def table():
+            return self._native_table(keys) if amp_models is None else self._amp_native_table(keys, amp_models)
+
+        if not table().lamb_step(*args):
             for group in self.param_groups:
                 for p in group["params"]:
-                    if p.grad is not None and "exp_avg" not in self.state[p]:
+                    src = p if amp_models is None else amp_models.get(id(p), p)
+                    if src.grad is not None and "exp_avg" not in self.state[p]:
                         self.state[p]["exp_avg"] = torch.zeros_like(p)
                         self.state[p]["exp_avg_sq"] = torch.zeros_like(p)
-            self._table = None
-            if not self._native_table(("exp_avg", "exp_avg_sq")).lamb_step(*args):
+            self._reset_tables()
+            if not table().lamb_step(*args):
                 raise RuntimeError("FusedLAMB: optimizer state missing after initialisation")
 
-    def state_dict(self):
-        steps = getattr(self, "_device_steps", None)
-        if steps is not None:  # the device counters are the real step counts (skipped steps excluded)
-            for g, st in zip(self.param_groups, steps.tolist()):
-                g["step"] = int(st)
-        return super().state_dict()
+    def _amp_fused_ok(self):
+        return self._fast_path_ok()
 
-    def load_state_dict(self, state_dict):
-        super().load_state_dict(state_dict)
-        self._device_steps = None  # re-seeded from the loaded host counters
+    def _amp_fused_step(self, models, inv_scale, scaled_norm):
+        self._native_step(models, inv_scale, scaled_norm)
 
     @torch.no_grad()
     def step(self, closure=None):
