@@ -35,7 +35,20 @@ def native():
                 _build.build()
                 _C = importlib.import_module("beforeholiday_amd._C")
                 _err = None
+        if _C is not None:  # the native run-time switches come from the typed config (config.py)
+            from . import config
+
+            config.push_native(_C)
     return _C
+
+
+def loaded() -> bool:
+    """Whether the extension has been imported already (without importing it)."""
+    return _C is not None
+
+
+def module():
+    return native()
 
 
 def _register_exit_cleanup(mod):

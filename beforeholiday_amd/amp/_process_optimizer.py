@@ -33,13 +33,23 @@ import types
 
 import torch
 
+from .. import config as _config
 from ..multi_tensor_apply import multi_tensor_applier, multi_tensor_applier_l2norm
 from ..ops import amp_C
 
 _LOW = (torch.float16, torch.bfloat16)
 
-# the fused mixed-precision step (module docstring); False keeps the unscale + step + copy sequence
+# the fused mixed-precision step (module docstring; Config.amp_fused_master_step); False keeps the
+# unscale + step + copy sequence
 fused_master_step = True
+
+
+def _apply_config(c):
+    global fused_master_step
+    fused_master_step = c.amp_fused_master_step
+
+
+_config.on_change(_apply_config)
 
 
 class AmpOptimizerState(object):

@@ -10,11 +10,10 @@ from .scaler import LossScaler
 
 
 def _device_scaler_wanted(loss_scaler, optimizers):
-    """BH_AMP_DEVICE_SCALER=1, dynamic scaling, the fused unscale kernel, a CUDA loss, and only fused
+    """Config.amp_device_scaler (BH_AMP_DEVICE_SCALER=1), dynamic scaling, the fused unscale kernel, a CUDA loss, and only fused
     optimizers whose kernels return early on a set noop flag (``_dummy_overflow_buf``): FusedLAMB
     (both stages), FusedSGD and FusedAdam (table path)."""
-    import os
-
+    from .. import config
     from ..optimizers import FusedAdam, FusedLAMB, FusedSGD
 
     def flag_aware(o):
@@ -22,7 +21,7 @@ def _device_scaler_wanted(loss_scaler, optimizers):
             return not o.capturable and not o.master_weights
         return isinstance(o, (FusedLAMB, FusedSGD))
 
-    return (os.environ.get("BH_AMP_DEVICE_SCALER", "0") == "1" and loss_scaler.dynamic
+    return (config.get().amp_device_scaler and loss_scaler.dynamic
             and LossScaler.has_fused_kernel and torch.cuda.is_available()
             and all(flag_aware(o) and hasattr(o, "_dummy_overflow_buf") for o in optimizers))
 

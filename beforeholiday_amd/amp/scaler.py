@@ -6,9 +6,9 @@ overflow flag), the flag is read once per step in ``update_scale``.
 """
 from __future__ import annotations
 
-import os
-
 import torch
+
+from .. import config as _config
 
 from ..multi_tensor_apply import multi_tensor_applier
 from ..ops import amp_C
@@ -25,8 +25,8 @@ class LossScaler(object):
     warned_no_fused_kernel = False
     warned_unscaling_non_fp32_grad = False
     # False = the reference's "python-only install" path (per-tensor checks and copies, no
-    # multi-tensor kernel); the L1 cross-product test compares both bitwise. BH_AMP_PYTHON_SCALER=1.
-    has_fused_kernel = os.environ.get("BH_AMP_PYTHON_SCALER", "0") != "1"
+    # multi-tensor kernel); the L1 cross-product test compares both bitwise. Config.amp_python_scaler.
+    has_fused_kernel = not _config.get().amp_python_scaler
 
     def __init__(self, loss_scale, init_scale=2.0 ** 16, scale_factor=2.0, scale_window=2000,
                  min_loss_scale=None, max_loss_scale=2.0 ** 24, device=None):
@@ -55,7 +55,7 @@ class LossScaler(object):
     # never waits for the backward to finish. FusedLAMB keeps device step counters that advance only
     # on steps the flag did not skip, so trajectories match the host path (to the rounding of fp32
     # bias corrections); the skip is not
-    # printed. Enabled by BH_AMP_DEVICE_SCALER=1 (bench.py) for dynamic scaling with fused optimizers.
+    # printed. Enabled by Config.amp_device_scaler (bench.py) for dynamic scaling with fused optimizers.
     device_mode = False
 
     def enable_device_mode(self, device):

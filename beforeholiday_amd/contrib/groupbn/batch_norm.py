@@ -9,13 +9,13 @@ layer. ``BH_GROUPBN_IPC=0`` (or CPU tensors / no native extension) uses an RCCL 
 the same ranks instead. Inputs are physical NHWC [N, H, W, C] tensors (or channels_last NCHW with
 ``torch_channels_last=True``); kernels are the channel-owned BN kernels of kernels/batchnorm.hip.
 """
-import os
 
 import torch
 import torch.distributed as dist
 from torch.nn.modules.batchnorm import _BatchNorm
 
 from ... import _native
+from ... import config as _config
 from ...parallel.optimized_sync_batchnorm import SyncBatchnormFunction
 from ...ops import syncbn as _bn
 
@@ -27,7 +27,7 @@ _IPC_CAPACITY = 1 << 14  # floats per slot row: 2C+1 for C <= 8191 channels
 def _ipc_reducer(size):
     """The IPC reducer of this rank's group of ``size`` consecutive ranks, or None."""
     if (size <= 1 or not dist.is_initialized() or not torch.cuda.is_available() or not _native.available()
-            or os.environ.get("BH_GROUPBN_IPC", "1") == "0"):
+            or not _config.get().groupbn_ipc):
         return None
     if size not in _IPC:
         from ..peer_memory import PeerAllReduce, PeerMemoryPool

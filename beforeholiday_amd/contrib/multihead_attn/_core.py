@@ -6,11 +6,11 @@ torch ops; the memory-bound middle — mask, softmax, dropout — is ONE HIP pas
 backward (``fast_multihead_attn`` in kernels/mha.hip, dropout regenerated from a Philox seed so no
 mask tensor is stored). On CPU the same math runs as torch ops.
 """
-import os
 
 import torch
 import torch.nn.functional as F
 
+from ... import config
 from ..._native import submodule
 
 MASK_NONE, MASK_PAD, MASK_ADDITIVE, MASK_TIME = 0, 1, 2, 3
@@ -104,12 +104,12 @@ def _fused_ok(x, hd, sk):
     whole-row kernels, longer sequences the flash (64-key block, online softmax) kernels."""
     if not x.is_cuda or x.dtype not in (torch.float16, torch.bfloat16) or hd != 64:
         return False
-    return os.environ.get("BH_MHA_FUSED", "1") != "0"
+    return config.get().mha_fused
 
 
 def _short_ok(sk, mask_mode, fill):
     return (sk <= submodule("fused_attention").max_sk() and mask_mode <= MASK_TIME and fill == float("-inf")
-            and os.environ.get("BH_ATTN_FLASH_ONLY", "0") != "1")
+            and not config.get().attn_flash_only)
 
 
 class FusedSelfAttnFn(torch.autograd.Function):

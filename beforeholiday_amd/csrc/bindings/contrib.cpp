@@ -375,18 +375,10 @@ void register_contrib_impl(pybind11::module_& root);
 
 // mode 4 on the 32x32 flash kernels: the uint8 mask packed to bits, [bits | bits_t] in one int32
 // tensor (AttnArgs::mbits / mbits_t). ``pre`` = the packing done once by flash_mask_bits (a BERT
-// forward shares one mask over all layers); otherwise packed here. BH_FLASH_M4_WIDE=0: the 16-wide
-// kernels read the bytes instead.
-bool m4_wide() {
-  static const bool wide = [] {
-    const char* e = getenv("BH_FLASH_M4_WIDE");
-    return !(e && e[0] == '0');
-  }();
-  return wide;
-}
-
+// forward shares one mask over all layers); otherwise packed here. (The 16-wide kernels reading the
+// mask bytes lost: profiles/bert_flash_mode4_wide_ab.txt.)
 void attach_mask_bits(bh::AttnArgs& a, const at::Tensor& q, const c10::optional<at::Tensor>& pre, at::Tensor& mb) {
-  if (a.mask_mode != 4 || !m4_wide()) return;
+  if (a.mask_mode != 4) return;
   const int64_t B = a.BH / a.heads;
   const int64_t nb = B * a.sq * ((a.sk + 31) / 32), nbt = B * a.sk * ((a.sq + 31) / 32);
   if (pre.has_value() && pre->defined()) {

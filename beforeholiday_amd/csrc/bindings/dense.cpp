@@ -7,6 +7,7 @@
 // place into the fp32 main_grad, C == D). Activation, dActivation and bias-gradient reductions are
 // the HIP kernels in kernels/dense.hip.
 #include "common.h"
+#include "bh/knobs.h"
 
 #include <map>
 #include <mutex>
@@ -95,16 +96,10 @@ std::vector<at::Tensor> dropout_backward(const at::Tensor& dy, const at::Tensor&
 }
 
 // ------------------------------------------------------------------------------------------------
-// MFMA GEMM with fused epilogue (kernels/gemm.hip). BH_DENSE_MFMA=0 routes everything back to
-// hipBLASLt + the separate epilogue passes (A/B switch for benchmarks).
+// MFMA GEMM with fused epilogue (kernels/gemm.hip). Config.dense_mfma = False routes everything back
+// to hipBLASLt + the separate epilogue passes (A/B switch for benchmarks).
 // ------------------------------------------------------------------------------------------------
-bool mfma_enabled() {
-  static const bool on = [] {
-    const char* v = std::getenv("BH_DENSE_MFMA");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
+bool mfma_enabled() { return bh::knob("dense_mfma", 1) != 0; }
 
 bool mfma_ok(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c) {
   const auto t = a.scalar_type();
@@ -120,16 +115,10 @@ bool mfma_ok(const at::Tensor& a, const at::Tensor& b, const at::Tensor& c) {
 // a warmup step) and the faster is kept. The MFMA kernel wins where the fused epilogue saves a pass
 // that matters (K <= 1024: the GPT-2-medium fc1 forward, small MLPs); hipBLASLt's main loop wins the
 // large-K shapes (fc2 forward / fc1 backward at K = 4096: 0.12 vs 0.08 ms,
-// profiles/gemm_mfma_big_tile_vs_hipblaslt.jsonl). The timing is opt-in (BH_DENSE_TUNE=1): a per-process
+// profiles/gemm_mfma_big_tile_vs_hipblaslt.jsonl). The timing is opt-in (Config.dense_tune): a per-process
 // timing pick can differ between ranks (another kernel, other rounding), so by default the static
 // K <= 1024 rule decides; during HIP-graph capture the cached choice (or the rule) is used.
-bool tune_enabled() {
-  static const bool on = [] {
-    const char* v = std::getenv("BH_DENSE_TUNE");
-    return v && v[0] == '1';
-  }();
-  return on;
-}
+bool tune_enabled() { return bh::knob("dense_tune", 0) != 0; }
 
 template <typename F>
 float time_ms(hipStream_t st, F&& fn) {

@@ -1720,13 +1720,9 @@ void attn_backward(int dt, const AttnArgs& a, hipStream_t st) {
 
 void flash_forward(int dt, const AttnArgs& a, hipStream_t st) {
   if (a.sk < 1 || a.sq < 1 || !a.lse) throw std::runtime_error("flash_forward: bad shape or missing lse");
-  static const bool legacy = [] {
-    const char* e = getenv("BH_FLASH_FWD16");
-    return e && e[0] == '1';
-  }();
-  if (a.cu_seqlens && (legacy || (a.mask_mode != 0 && a.mask_mode != 5)))
+  if (a.cu_seqlens && a.mask_mode != 0 && a.mask_mode != 5)
     throw std::runtime_error("flash_forward: varlen runs the 32x32 kernels with mask mode 0 or 5 only");
-  if (!legacy && (a.mask_mode == 0 || a.mask_mode == 5 || (a.mask_mode == 4 && a.mbits))) {
+  if ((a.mask_mode == 0 || a.mask_mode == 5 || (a.mask_mode == 4 && a.mbits))) {
     const dim3 grid((unsigned)((a.sq + kFQ - 1) / kFQ), (unsigned)a.BH);
     flash_dispatch(dt, a.mask_mode, "flash_forward", [&](auto tt, auto mm) {
       using T = typename decltype(tt)::type;
@@ -1760,13 +1756,9 @@ void flash_delta(int dt, const AttnArgs& a, float* delta, hipStream_t st) {
 
 void flash_backward(int dt, const AttnArgs& a, hipStream_t st) {
   if (a.sk < 1 || a.sq < 1 || !a.lse || !a.delta) throw std::runtime_error("flash_backward: bad args");
-  static const bool legacy = [] {
-    const char* e = getenv("BH_FLASH_BWD16");
-    return e && e[0] == '1';
-  }();
-  if (a.cu_seqlens && (legacy || (a.mask_mode != 0 && a.mask_mode != 5)))
+  if (a.cu_seqlens && a.mask_mode != 0 && a.mask_mode != 5)
     throw std::runtime_error("flash_backward: varlen runs the 32x32 kernels with mask mode 0 or 5 only");
-  if (!legacy && (a.mask_mode == 0 || a.mask_mode == 5 || (a.mask_mode == 4 && a.mbits && a.mbits_t))) {
+  if ((a.mask_mode == 0 || a.mask_mode == 5 || (a.mask_mode == 4 && a.mbits && a.mbits_t))) {
     const dim3 gq((unsigned)((a.sq + kFQ - 1) / kFQ), (unsigned)a.BH);
     const dim3 gk((unsigned)((a.sk + kFQ - 1) / kFQ), (unsigned)a.BH);
     const bool dr = a.training && a.p_drop > 0.f;

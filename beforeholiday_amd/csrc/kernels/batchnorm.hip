@@ -1043,51 +1043,42 @@ int grid_for(int64_t work_items) {
 // host API (bh/bn_api.h)
 // ==========================================================================================
 // row splits for a streaming NHWC pass: ~target workgroups, >= min_iter rows per lane
-// launch-geometry knobs (env overrides for tuning sweeps: benchmarks/bench_bn.py)
-int64_t env_knob(const char* name, int64_t dflt) {
-  const char* v = getenv(name);
-  return v ? atoll(v) : dflt;
-}
-int64_t knob_ew_blocks() { static const int64_t v = env_knob("BH_BN_EW_BLOCKS", 2048); return v; }
-int64_t knob_ew_rows() { static const int64_t v = env_knob("BH_BN_EW_ROWS", 8); return v; }
+// launch geometry, tuned on MI355X with benchmarks/bench_bn.py sweeps (fixed: the round-4 environment
+// overrides of these values are gone)
+int64_t knob_ew_blocks() { return 2048; }
+int64_t knob_ew_rows() { return 8; }
 // statistics and backward-reduction launches are tuned separately (bench_bn.py sweep on MI355X:
 // stats best at ~1024 workgroups x 32 rows/lane, the two-input backward reduction at ~256)
-int64_t knob_stat_blocks() { static const int64_t v = env_knob("BH_BN_STAT_BLOCKS", 1024); return v; }
-int64_t knob_red_blocks() { static const int64_t v = env_knob("BH_BN_RED_BLOCKS", 256); return v; }
+int64_t knob_stat_blocks() { return 1024; }
+int64_t knob_red_blocks() { return 256; }
 // with the stored ReLU bit mask (three streams: dy, x, mask) the reduction wants twice the workgroups
 // (benchmarks/sweep_bn_reduce.py on MI355X, batch-256 ResNet-50 shapes: 56x56x256 201 -> 150 us,
 // 28x28x512 105 -> 80 us at 512; the two-stream recomputed-ReLU shapes lose 1-2 us there)
-int64_t knob_red_blocks_mask() { static const int64_t v = env_knob("BH_BN_RED_BLOCKS_MASK", 512); return v; }
-int64_t knob_red_rows() { static const int64_t v = env_knob("BH_BN_RED_ROWS", 32); return v; }
+int64_t knob_red_blocks_mask() { return 512; }
+int64_t knob_red_rows() { return 32; }
 // channel vectors (x8 channels) per workgroup of the two reductions (stats, backward reduce): fewer
 // channels per workgroup -> more row lanes merged in LDS, so a layer reaches the workgroup target
 // with fewer split partials (small 7x7 / 14x14 layers were latency-bound with one row lane)
 // (bench_bn.py sweep on MI355X: statistics 1.83 -> 1.66 ms per ResNet-50 step with 16 vectors / 1024
 // workgroups; the two-input backward reduction is best left at 256 vectors / 256 workgroups)
-int64_t knob_red_cvb() { static const int64_t v = env_knob("BH_BN_RED_CVB", 256); return v; }
-int64_t knob_stat_cvb() { static const int64_t v = env_knob("BH_BN_STAT_CVB", 16); return v; }
+int64_t knob_red_cvb() { return 256; }
+int64_t knob_stat_cvb() { return 16; }
 NhwcGeom red_geom(int C) { return nhwc_geom(C, (int)knob_red_cvb()); }
 NhwcGeom stat_geom(int C) { return nhwc_geom(C, (int)knob_stat_cvb()); }
 
-// small-layer split boost: measured slower on MI355X (bench_bn.py: 28x28x128 stats 27 -> 35 us, the
-// finalize merges more partials), so off by default; BH_BN_SMALL_ELEMS=<elements> enables it.
-int64_t knob_small_elems() { static const int64_t v = env_knob("BH_BN_SMALL_ELEMS", 0); return v; }
 
 int64_t nhwc_splits(const BNShape& s, int64_t target, int64_t min_iter, int geom = 0) {
   const NhwcGeom g = geom == 2 ? stat_geom(s.C) : geom == 1 ? red_geom(s.C) : nhwc_geom(s.C);
   int64_t splits = std::max<int64_t>(1, target / g.gx);
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, s.outer / (g.R * min_iter)));
-  // Small layers (ResNet stages 2-4 at batch 256: 6-32 M elements) are latency-bound with the
-  // big-layer geometry: each lane walks 32+ rows in dependent rounds of 4 loads (15 us for a 13 MB
-  // tensor). Spread them over up to 1024 workgroups at >= 8 rows per lane instead.
-  if (s.outer * (int64_t)s.C <= knob_small_elems() && g.gx * splits < 1024)
-    splits = std::max<int64_t>(splits, std::min<int64_t>(1024 / g.gx, std::max<int64_t>(1, s.outer / (g.R * 8))));
+  // (a small-layer split boost -- more workgroups for the 6-32 M element layers -- measured slower:
+  // 28x28x128 statistics 27 -> 35 us, the finalize merges more partials; removed)
   return std::max<int64_t>(1, splits);
 }
 
 static int splits_for(const BNShape& s, int64_t target_blocks, int geom) {
   if (s.channels_last)
-    return (int)nhwc_splits(s, target_blocks, geom == 2 ? env_knob("BH_BN_STAT_ROWS", 16) : knob_red_rows(), geom);
+    return (int)nhwc_splits(s, target_blocks, geom == 2 ? 16 : knob_red_rows(), geom);
   const int64_t per_c = s.outer * s.inner;
   int64_t splits = std::max<int64_t>(1, 2048 / std::max(1, s.C));
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, per_c / (kBlock * 16)));
@@ -1164,20 +1155,19 @@ void bn_merge_parts(int G, int C, const float* part, float count, const BNFinal&
 }
 
 // the flat chunk-walk apply / data-gradient kernels (k_fwd_flat, k_dgrad_flat) instead of the 2-D
-// channel-owned ones; BH_BN_FLAT=0 restores those. BH_BN_FLAT_BLOCKS caps the grid (bench_hbm_roofline.py
+// channel-owned ones where their LDS fits; the grid is capped at 16384 workgroups (bench_hbm_roofline.py
 // at 256x256x56x56: 1024 / 2048 / 4096 / 16384 workgroups -> 5.2 / 5.3-5.4 / 5.4 / 5.6-5.7 TB/s; the
 // 2-D kernels 5.0)
-bool knob_flat() { static const bool v = env_knob("BH_BN_FLAT", 1) != 0; return v; }
 // the flat kernels keep `floats_per_channel` per-channel constants for ALL C channels in dynamic LDS
 // (k_fwd_flat 2, k_dgrad_flat 5); past the default 64 KiB dynamic-LDS launch limit the channel-owned
 // 2-D kernels (which cap channels per workgroup) take the shape
 constexpr size_t kFlatLdsCap = 64 * 1024;
 bool flat_ok(const BNShape& s, int floats_per_channel) {
-  return s.channels_last && s.C % 8 == 0 && knob_flat() &&
+  return s.channels_last && s.C % 8 == 0 &&
          sizeof(float) * (size_t)floats_per_channel * (size_t)s.C <= kFlatLdsCap;
 }
 unsigned flat_grid(int64_t chunks) {
-  static const int64_t cap = env_knob("BH_BN_FLAT_BLOCKS", 16384);
+  constexpr int64_t cap = 16384;
   const int64_t need = (chunks + kBlock * kFlatU - 1) / (kBlock * kFlatU);
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, cap));
 }

@@ -500,11 +500,8 @@ bool make_plan(const C1x1Args& a, Plan* pl) {
   if (a.bnb) max_nc = std::min(max_nc, scatter ? 64 : 128);  // (the second fragment stream's registers)
   int NC = 0, occ = 0;
   // the widest column slice (A read once per slice) that still leaves two workgroups per CU; else one
-  // (BH_C1X1_OCC: the resident-workgroup target, an experiment knob; the kernels' registers must allow it)
-  static const int occ_max = [] {
-    const char* e = getenv("BH_C1X1_OCC");
-    return e ? std::max(1, std::min(4, atoi(e))) : 2;
-  }();
+  // (a higher resident-workgroup target measured no better: profiles/c1x1_occupancy_ab.txt)
+  constexpr int occ_max = 2;
   for (int want_occ = occ_max; want_occ >= 1 && !NC; --want_occ)
     for (int nc : {256, 128, 64})
       if (nc <= max_nc && a.N % nc == 0 &&
@@ -578,12 +575,8 @@ int c1x1_parts(const C1x1Args& a) {
 
 void c1x1_run(int dt, const C1x1Args& a_in, hipStream_t st) {
   if (!c1x1_supported(a_in)) throw std::runtime_error("c1x1: unsupported shape / arguments");
-  static const int a_load_env = [] {
-    const char* e = getenv("BH_C1X1_ALOAD");
-    return e ? atoi(e) : 0;
-  }();
   C1x1Args a = a_in;
-  if (a.a_load < 0) a.a_load = a_load_env;
+  if (a.a_load < 0) a.a_load = 0;
   Plan pl;
   make_plan(a, &pl);
   const dim3 grid(pl.g.nslices * pl.g.G), block(kThreads);

@@ -249,12 +249,8 @@ struct Plan {
 
 Plan make_plan(const IgemmArgs& a) {
   Plan p;
-  // BH_IGEMM_NC64=1 (A/B knob): 64-channel tiles everywhere (then 64 x 64 wave tiles without the prologue)
-  static const bool nc64 = [] {
-    const char* e = getenv("BH_IGEMM_NC64");
-    return e && atoi(e) == 1;
-  }();
-  p.NC = (a.Nout % 128 == 0 && !nc64) ? 128 : 64;
+  // (64-channel tiles everywhere measured slower: profiles/igemm_nc64_ab.txt)
+  p.NC = a.Nout % 128 == 0 ? 128 : 64;
   const int64_t P = (int64_t)a.N * a.Hg * a.Wg;
   const int64_t slices = a.Nout / p.NC;
   // 128-channel tiles: 32 pixel rows per wave (64 x 128 spills at two waves per SIMD). 64-channel

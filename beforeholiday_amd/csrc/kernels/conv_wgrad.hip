@@ -469,14 +469,10 @@ bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo) {
   if (a.R == 1) {
     // no halo: the N*H*W pixels are one flat list, 112-pixel windows (one row of 28 groups)
     // wide tiles (K % 256, C % 128): 64-pixel windows (two window buffers of 56 KiB)
-    static const bool wide_env = [] {
-      const char* e = getenv("BH_WGRAD_WIDE");
-      return !(e && atoi(e) == 0);
-    }();
     const int64_t npix = (int64_t)a.N * a.H * a.W;
     // (and at least 4 such tiles: with fewer, the extra split partials cost more than the staging saves,
     // measured on the 128 -> 512 layer-2 shape)
-    g.wide = wide_env && a.stride == 1 && a.K % 256 == 0 && a.C % 128 == 0 && npix % 64 == 0 &&
+    g.wide = a.stride == 1 && a.K % 256 == 0 && a.C % 128 == 0 && npix % 64 == 0 &&
              (a.K / 256) * (a.C / 128) >= 4;
     const int win = g.wide ? 64 : 112;
     if (npix % win) return false;
@@ -509,12 +505,8 @@ bool conv_wgrad_plan(const ConvWgradArgs& a, ConvWgradGeo* geo) {
   // 256 x 256 wide tiles (each wave 64 x 128: eight MFMA tiles per k-step on six fragments instead of
   // four on four -- a quarter fewer LDS bytes per MFMA, and twice the MFMA work per window against its
   // fixed staging cost) where K, C % 256 and at least 32 such tiles remain (the large transformer
-  // weight gradients); BH_WGRAD_WIDE2=0 keeps 256 x 128
-  static const bool wide2_env = [] {
-    const char* e = getenv("BH_WGRAD_WIDE2");
-    return !(e && atoi(e) == 0);
-  }();
-  if (g.wide && wide2_env && a.C % 256 == 0 && (a.K / 256) * (a.C / 256) >= 32) g.ct = 4;
+  // weight gradients)
+  if (g.wide && a.C % 256 == 0 && (a.K / 256) * (a.C / 256) >= 32) g.ct = 4;
   g.ctiles = a.C / (kTile * g.ct);
   g.tiles = (a.K / (kTile * g.kt * (g.wide ? 2 : 1))) * g.ctiles;
   // one round of workgroups (one per CU), split over the windows

@@ -21,6 +21,7 @@
 //    16-byte vectors, C is written with 16-byte stores, and bias-gradient column sums are reduced
 //    over the wave's 64 rows with xor-shuffles into a deterministic per-slab partial.
 #include "bh/act.h"
+#include "bh/knobs.h"
 #include "bh/api.h"
 #include "bh/device.h"
 #include "bh/gemm_api.h"
@@ -1002,17 +1003,13 @@ void launch(const Args& a0, bool glds, hipStream_t st) {
   else hipLaunchKernelGGL((k_gemm_nt<CfgSmall, T, false>), dim3((unsigned)nwg), dim3(CfgSmall::kThreads), 0, st, a);
 }
 
-int env_mode(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return v && v[0] ? std::atoi(v) : dflt;
-}
 }  // namespace
 
 namespace {
 int g_tile_mode = -1;
 }
 int gemm_tile_mode() {
-  if (g_tile_mode < 0) g_tile_mode = env_mode("BH_GEMM_TILE", 0);
+  if (g_tile_mode < 0) g_tile_mode = knob("gemm_tile", 0);
   return g_tile_mode;
 }
 void gemm_set_tile_mode(int mode) { g_tile_mode = mode; }
@@ -1028,11 +1025,9 @@ void gemm_nt(int dt, const void* A, int64_t lda, const void* B, int64_t ldb, voi
   a.lda = lda; a.ldb = ldb; a.ldc = ldc;
   a.M = (int)M; a.N = (int)N; a.K = (int)K;
   a.epi = epi;
-  // BH_GEMM_GLDS=0 forces register staging; tile mode (BH_GEMM_TILE / gemm_set_tile_mode):
-  // 1 small / 2 big / 3 mid / 4 ping-pong / 0 auto
-  static const bool glds_on = env_mode("BH_GEMM_GLDS", 1) != 0;
+  // tile mode (Config.gemm_tile / gemm_set_tile_mode): 1 small / 2 big / 3 mid / 4 ping-pong / 0 auto
   const int tile_mode = gemm_tile_mode();
-  const bool glds = glds_on && (K % BK) == 0;
+  const bool glds = (K % BK) == 0;
   const int64_t big_wgs = ((M + CfgBig::BM - 1) / CfgBig::BM) * ((N + CfgBig::BN - 1) / CfgBig::BN);
   // the ping-pong kernel keeps row offsets of a 256-row tile in 32 bits
   const bool pp_ok = glds && lda < (1 << 22) && ldb < (1 << 22);
@@ -1049,7 +1044,7 @@ void gemm_nt(int dt, const void* A, int64_t lda, const void* B, int64_t ldb, voi
   // 108 vs 62 us for the 200704 x 128 x 512 statistics GEMM of the ResNet-50 step)
   const bool big = glds && !pp && (tile_mode == 2 || (tile_mode == 0 && big_wgs >= 256 && N > 128));
   const bool mid = glds && tile_mode == 3;
-  static const bool log_shapes = env_mode("BH_GEMM_LOG", 0) != 0;  // debugging: which kernel per shape
+  const bool log_shapes = knob("gemm_log", 0) != 0;  // debugging: which kernel per shape
   if (log_shapes)
     fprintf(stderr, "[gemm_nt] M %lld N %lld K %lld epi %d resid %d -> %s\n", (long long)M, (long long)N,
             (long long)K, epi.bn_stats, epi.resid != nullptr,

@@ -423,17 +423,9 @@ int ln_wgrad_splits(int64_t n1, int n2) {
   int R = kBlock / cvb, p = 1;
   while (p * 2 <= R) p *= 2;
   const int gx = (cv + cvb - 1) / cvb;
-  // >= rows_min rows per row lane (BH_LN_WGRAD_ROWS, default 8: 16 -> 8 took the 8192 x 1024 fp16
-  // backward from 85 to 66 us, benchmarks/bench_ln_bwd.py) and ~target workgroups (BH_LN_WGRAD_WGS,
-  // default 512)
-  static const int rows_min = [] {
-    const char* e = std::getenv("BH_LN_WGRAD_ROWS");
-    return e && std::atoi(e) > 0 ? std::atoi(e) : 8;
-  }();
-  static const int target = [] {
-    const char* e = std::getenv("BH_LN_WGRAD_WGS");
-    return e && std::atoi(e) > 0 ? std::atoi(e) : 512;
-  }();
+  // >= 8 rows per row lane (16 -> 8 took the 8192 x 1024 fp16 backward from 85 to 66 us,
+  // benchmarks/bench_ln_bwd.py; profiles/ln_bwd_wgrad_split_sweep.txt) and ~512 workgroups
+  constexpr int rows_min = 8, target = 512;
   int64_t splits = std::max<int64_t>(1, target / gx);
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, n1 / (p * rows_min)));
   return (int)splits;

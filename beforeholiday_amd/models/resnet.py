@@ -7,10 +7,10 @@ from __future__ import annotations
 
 from typing import List, Optional, Type
 
-import os
-
 import torch
 import torch.nn as nn
+
+from .. import config as _config
 
 
 def conv3x3(cin, cout, stride=1):
@@ -55,116 +55,18 @@ def _kw(weight, x):
     return None
 
 
-# ------------------------------------------------------------------------------------------------
-# Weight gradients on a second HIP stream. In backward, a convolution's weight gradient depends only on
-# its saved input and dY, and nothing downstream reads it before the optimizer -- while the data gradient
-# feeds the next BatchNorm-backward passes. The MFMA wgrad kernels are compute / LDS bound (one
-# 141 KiB workgroup per CU) and the BatchNorm passes HBM bound (a few KiB of LDS), so running the wgrads
-# on a side stream lets the two kinds co-reside on the CUs; in the captured HIP graph of the training
-# step the side stream becomes a parallel branch. The side stream joins the compute stream once, at the
-# end of the backward pass (an autograd-engine callback), before any gradient consumer runs.
-# Opt-in (BH_WGRAD_STREAM=1): same-box A/B at batch 256 measured no reliable gain -- eager 10204 vs
-# 10082, graphed 9936 vs 10171 img/s (profiles/resnet50_wgrad_side_stream_ab.txt)
-_WGRAD_STREAM = os.environ.get("BH_WGRAD_STREAM", "0") == "1"
-_SIDE = {}
-_JOIN_QUEUED = set()
-
-
-def _side_ok(weight, x):
-    """The weight gradient may run on the side stream: a CUDA leaf parameter whose .grad is empty
-    (AccumulateGrad then just takes the tensor: no kernel reads it before the join), and no gradient
-    hooks of a multi-rank DDP (which copy it into a bucket on the compute stream right away)."""
-    if not (_WGRAD_STREAM and x.is_cuda and weight is not None and weight.is_leaf and weight.grad is None):
-        return False
-    import torch.distributed as dist
-
-    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
-
-
-def _join(dev):
-    key = dev.index
-    _JOIN_QUEUED.discard(key)
-    torch.cuda.current_stream(dev).wait_stream(_SIDE[key])
-
-
-def _on_side(fn, *inputs):
-    """``fn()`` (a weight gradient of ``inputs``) issued on the side stream after the work queued so
-    far on the compute stream; the compute stream waits for it at the end of this backward pass."""
-    dev = inputs[0].device
-    main = torch.cuda.current_stream(dev)
-    side = _SIDE.get(dev.index)
-    if side is None:
-        side = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
-    side.wait_stream(main)
-    with torch.cuda.stream(side):
-        g = fn()
-    for t in inputs:
-        if torch.is_tensor(t):
-            t.record_stream(side)  # (their blocks are not reused by the compute stream meanwhile)
-    g.record_stream(main)
-    if dev.index not in _JOIN_QUEUED:
-        _JOIN_QUEUED.add(dev.index)
-        torch.autograd.Variable._execution_engine.queue_callback(lambda: _join(dev))
-    return g
-
-
-def _wgrad_maybe_side(wparam, fn, *inputs):
-    """(gradient, ran_on_side) -- see :func:`_side_ok`."""
-    if _side_ok(wparam, inputs[0]):
-        return _on_side(fn, *inputs), True
-    return fn(), False
-
-
 def _like(g, weight):
     return g if g.stride() == weight.stride() else g.contiguous()
 
 
-# Opt-in (BH_WGRAD_REDUCE_SIDE=1): the split partials of the MFMA weight-gradient kernels summed on the
-# side stream (one rank, a leaf parameter without a .grad or hooks, a layout the parameter already has),
-# so the ~50 small reduce launches per ResNet-50 step could overlap the next data-gradient kernels; the
-# compute stream joins at the end of the backward pass. Same-box A/B: 10595 / 10418 img/s with it vs
-# 10813 / 10836 without (profiles/resnet50_wgrad_reduce_side_ab.txt): the concurrent reduces slow the
-# critical-path kernels more than their own launches cost
-_WGRAD_REDUCE_SIDE = os.environ.get("BH_WGRAD_REDUCE_SIDE", "0") == "1"
-
-
-def _reduce_side_ok(weight, x):
-    if not (_WGRAD_REDUCE_SIDE and x.is_cuda and weight is not None and weight.is_leaf and weight.grad is None):
-        return False
-    # a gradient hook (DDP's bucket copy, user hooks) would read it on the compute stream right away
-    if getattr(weight, "_post_accumulate_grad_hooks", None) or getattr(weight, "_backward_hooks", None):
-        return False
-    import torch.distributed as dist
-
-    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
-
-
 def _conv_wgrad(x, gy, r, weight, scale=None, shift=None, stride=1):
-    """``ops.conv.conv_wgrad`` in ``weight``'s layout, with the split-partials sum on the side stream
-    where :func:`_reduce_side_ok` allows it."""
+    """``ops.conv.conv_wgrad`` in ``weight``'s layout. (Rounds 3-4 also tried the weight gradients and
+    their split-partial sums on a second HIP stream; both lost on the same box --
+    profiles/resnet50_wgrad_side_stream_ab.txt, profiles/resnet50_wgrad_reduce_side_ab.txt -- and were
+    removed.)"""
     from ..ops import conv as bhconv
 
-    if not (_reduce_side_ok(weight, x) and bhconv.wgrad_supported(x, gy, r, stride)):
-        return _like(bhconv.conv_wgrad(x, gy, r, scale, shift, stride=stride), weight)
-    out, ws = bhconv.conv_wgrad_deferred(x, gy, r, scale, shift, stride=stride)
-    if ws is None:
-        return _like(out, weight)
-    if out.stride() != weight.stride():  # a layout copy would read it on the compute stream
-        bhconv.conv_wgrad_reduce(ws, out)
-        return out.contiguous()
-    dev = x.device
-    main = torch.cuda.current_stream(dev)
-    side = _SIDE.get(dev.index)
-    if side is None:
-        side = _SIDE[dev.index] = torch.cuda.Stream(device=dev)
-    side.wait_stream(main)
-    with torch.cuda.stream(side):
-        bhconv.conv_wgrad_reduce(ws, out)
-    ws.record_stream(side)
-    if dev.index not in _JOIN_QUEUED:
-        _JOIN_QUEUED.add(dev.index)
-        torch.autograd.Variable._execution_engine.queue_callback(lambda: _join(dev))
-    return out
+    return _like(bhconv.conv_wgrad(x, gy, r, scale, shift, stride=stride), weight)
 
 
 # per-shape choice of the 1x1 / stride-1 convolution paths: {(N, Cin, H, W, Cout, dtype, dir): "gemm" | "miopen"}
@@ -202,7 +104,7 @@ def _pick(key, gemm_fn, miopen_fn, mode):
         return mode
     choice = _CONV1X1_CHOICE.get(key)
     if choice is None:
-        if os.environ.get("BH_CONV_TUNE") == "1":
+        if _config.get().conv_tune:
             # interleaved A, B, A, B and the best of each: the first step runs on a cold GPU (clocks
             # ramping, first-use kernel loads), and a pick made on one noisy sample sticks for the run
             t_gemm, t_miopen = _time_ms(gemm_fn), _time_ms(miopen_fn)
@@ -220,7 +122,7 @@ def _wgrad(x, gy, weight, r, mode, miopen_fn):
     profiles/conv_wgrad_vs_miopen.jsonl."""
     from ..ops import conv as bhconv
 
-    if os.environ.get("BH_CONV_WGRAD") == "miopen":  # A/B switch (benchmarks)
+    if _config.get().conv_wgrad == "miopen":  # A/B switch (benchmarks)
         mode = "miopen"
     if mode == "miopen" or not bhconv.wgrad_supported(x, gy, r):
         return miopen_fn()
@@ -259,7 +161,7 @@ def _mm64(a2d, b):
     ``BH_GEMM_N64=0`` keeps hipBLASLt (A/B switch)."""
     from ..ops import conv as bhconv
 
-    if b.size(0) == 64 and os.environ.get("BH_GEMM_N64", "1") != "0" and bhconv.gemm_n64_supported(a2d, b):
+    if b.size(0) == 64 and _config.get().gemm_n64 and bhconv.gemm_n64_supported(a2d, b):
         return bhconv.gemm_n64(a2d, b)
     return torch.mm(a2d, b.t())
 
@@ -304,7 +206,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             wt = weight.view(weight.size(0), c).t().contiguous() if c == 64 else None
             from ..ops import conv as bhconv
 
-            if wt is not None and os.environ.get("BH_GEMM_N64", "1") != "0" and bhconv.gemm_n64_supported(gy2d, wt):
+            if wt is not None and _config.get().gemm_n64 and bhconv.gemm_n64_supported(gy2d, wt):
                 # 64-channel input (layer1's first block): the streaming kernel adds the stash in its epilogue
                 gx = bhconv.gemm_n64(gy2d, wt, acc2d).view(n, h, w, c).permute(0, 3, 1, 2)
             else:
@@ -541,7 +443,7 @@ class _Conv1x1S2WFn(torch.autograd.Function):
             gx = conv_bwd(gy, x, weight, None, *args, [True, False, False])[0]
         if ctx.needs_input_grad[1]:
             miopen = lambda: conv_bwd(gy, x, weight, None, *args, [False, True, False])[1]  # noqa: E731
-            mode = "miopen" if os.environ.get("BH_CONV_WGRAD") == "miopen" else ctx.mode
+            mode = "miopen" if _config.get().conv_wgrad == "miopen" else ctx.mode
             if mode == "miopen" or not bhconv.wgrad_supported(x, gy, 1, 2):
                 return gx, miopen(), None
             n, c, h, w = x.shape
@@ -604,7 +506,6 @@ class _StemStatsFn(torch.autograd.Function):
         y, part = submodule("conv_cuda").stem_forward_stats(x, weight, kshift)
         ctx.save_for_backward(x, weight)
         ctx.mode = "gemm"
-        ctx.wparam = weight
         ctx.mark_non_differentiable(part)
         ctx.set_materialize_grads(False)
         return y, part
@@ -738,7 +639,7 @@ def conv1x1(cin, cout, stride=1):
     # the gathered-input path is opt-in (BH_CONV1X1_S2=gather): measured 27.7 vs 26.4 ms per
     # ResNet-50 step on the same box, the strided gather / zero-fill + scatter cost more than
     # MIOpen's stride-2 kernels (profiles/resnet50_conv1x1_s2_ab.txt); BH_CONV1X1_S2=0 is plain MIOpen
-    s2 = os.environ.get("BH_CONV1X1_S2", "wgrad")
+    s2 = {"miopen": "0"}.get(_config.get().conv1x1_s2, _config.get().conv1x1_s2)
     if _CONV1X1_MODE != "miopen" and stride == 2 and s2 in ("wgrad", "gather"):
         return Conv1x1S2(cin, cout, 1, stride=2, bias=False, mode=_CONV1X1_MODE, gather=s2 == "gather")
     return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
@@ -780,7 +681,7 @@ class _Conv1x1BNFn(torch.autograd.Function):
     def forward(ctx, x, weight, kshift, link_in, box, s2, mlink=None):
         y, part = _c1x1_forward_stats(x, weight, kshift, s2)
         ctx.save_for_backward(x, weight)
-        ctx.link_in, ctx.box, ctx.s2, ctx.wparam = link_in, box, s2, weight
+        ctx.link_in, ctx.box, ctx.s2 = link_in, box, s2
         ctx.mlink = mlink  # the producing block's ReLU mask (_MaskLink): applied in the data gradient's epilogue
         ctx.mark_non_differentiable(part)
         ctx.set_materialize_grads(False)
@@ -814,9 +715,6 @@ class _Conv1x1BNFn(torch.autograd.Function):
             return _wgrad(x, gy, weight, 1, "gemm", lambda: conv_bwd(gy, x, weight, None, *args,
                                                                      [False, True, False])[1])
 
-        side = ctx.needs_input_grad[1] and _side_ok(ctx.wparam, x)
-        if side:
-            gw = _on_side(wfn, x, gy)
         if ctx.needs_input_grad[0]:
             if ctx.s2:
                 gx = conv_bwd(gy, x, weight, None, *args, [True, False, False])[0]
@@ -863,7 +761,7 @@ class _Conv1x1BNFn(torch.autograd.Function):
             acc = None
         if box is not None:
             box["conv_done"] = True
-        if ctx.needs_input_grad[1] and not side:
+        if ctx.needs_input_grad[1]:
             gw = wfn()
         return gx, gw, None, None, None, None, None
 
@@ -910,7 +808,7 @@ class _Conv1DsFn(torch.autograd.Function):
         y1, p1 = _c1x1_forward_stats(x, w1, k1, False)
         yd, pd = _c1x1_forward_stats(x, wd, kd, s2)
         ctx.save_for_backward(x, w1, wd)
-        ctx.s2, ctx.wparams = s2, (w1, wd)
+        ctx.s2 = s2
         # ds_box: filled by the block's tail (_ConvBNResFn) when it folds the downsample BatchNorm: the
         # downsample conv's weight gradient is then the tail's, and its data gradient is formed here from
         # (g, y_ds, A, B, D) with the BatchNorm-backward prologue
@@ -948,12 +846,6 @@ class _Conv1DsFn(torch.autograd.Function):
             return _wgrad(x, gyd, wd, 1, "gemm", lambda: conv_bwd(gyd, x, wd, None, *a1, [False, True, False])[1])
 
         dsb = ctx.ds_box.pop("ds", None) if ctx.ds_box is not None else None
-        side1 = ctx.needs_input_grad[1] and _side_ok(ctx.wparams[0], x)
-        sided = dsb is None and ctx.needs_input_grad[2] and _side_ok(ctx.wparams[1], x)
-        if side1:
-            gw1 = _on_side(w1fn, x, gy1)
-        if sided:
-            gwd = _on_side(wdfn, x, gyd)
         if ctx.needs_input_grad[0]:
             if conv_bn.preferred(k1, c, g1.size(0)) and conv_bn.supported(g1, w1_2d, b_trans=True):
                 gx2d, _ = conv_bn.c1x1(g1, w1_2d, b_trans=True)
@@ -983,9 +875,9 @@ class _Conv1DsFn(torch.autograd.Function):
             else:
                 torch.addmm(gx2d, gd, wd_2d, out=gx2d)
             gx = gx2d.view(n, h, w, c).permute(0, 3, 1, 2)
-        if ctx.needs_input_grad[1] and not side1:
+        if ctx.needs_input_grad[1]:
             gw1 = w1fn()
-        if ctx.needs_input_grad[2] and not sided and dsb is None:
+        if ctx.needs_input_grad[2] and dsb is None:
             gwd = wdfn()
         return gx, gw1, gwd, None, None, None, None
 
@@ -1027,7 +919,7 @@ class _Conv3x3BNFn(torch.autograd.Function):
 
         y, part = submodule("conv_cuda").conv3x3_bn_forward(x, weight, None, None, True, kshift)
         ctx.save_for_backward(x, weight)
-        ctx.link_in, ctx.wparam = link_in, weight
+        ctx.link_in = link_in
         ctx.mark_non_differentiable(part)
         ctx.set_materialize_grads(False)
         return y, part
@@ -1046,21 +938,11 @@ class _Conv3x3BNFn(torch.autograd.Function):
         gx = gw = None
         wfn = lambda: _wgrad(x, gy, weight, 3, "gemm",  # noqa: E731
                              lambda: conv_bwd(gy, x, weight, None, *args, [False, True, False])[1])
-        side = ctx.needs_input_grad[1] and _side_ok(ctx.wparam, x)
-        if side:
-            gw = _on_side(wfn, x, gy)
         if ctx.needs_input_grad[0]:
-            link = ctx.link_in
-            # the 3x3 data gradient's BatchNorm-sums epilogue reads the previous BatchNorm's input 2 bytes
-            # per lane; measured slower than the separate reduce pass at 56x56 (170 vs 104 + 50 us), so
-            # it is opt-in (BH_FOLD_3X3_BWD=1)
-            if _FOLD_3X3_BWD and _link_ok(link, c) and link.y.is_contiguous(memory_format=torch.channels_last):
-                gx, part = submodule("conv_cuda").conv3x3_bn_dgrad(gy, weight, link.y, link.scale, link.shift,
-                                                                   link.mean, link.relu)
-                link.sums = conv_bn.sum_parts(part)
-            else:
-                gx = bhconv.conv3x3_dgrad(gy, weight)
-        if ctx.needs_input_grad[1] and not side:
+            # (a BatchNorm-sums epilogue on the 3x3 data gradient measured slower than the separate
+            # reduce pass at 56x56 -- 170 vs 104 + 50 us -- and was removed)
+            gx = bhconv.conv3x3_dgrad(gy, weight)
+        if ctx.needs_input_grad[1]:
             gw = wfn()
         return gx, gw, None, None
 
@@ -1113,7 +995,6 @@ class _BNConvFn(torch.autograd.Function):
             out = o2d.view(n, h, w, k).permute(0, 3, 1, 2)
         ctx.save_for_backward(y, conv_w, bn_w, mean, invstd, scale, shift, count_t)
         ctx.process_group, ctx.world, ctx.R, ctx.stride = process_group, world, R, stride
-        ctx.wparam = conv_w
         ctx.mark_non_differentiable(part_out)
         ctx.set_materialize_grads(False)
         return out, part_out
@@ -1131,8 +1012,7 @@ class _BNConvFn(torch.autograd.Function):
         n, C, h, w = y.shape
         sums = None
         wfn = lambda: _conv_wgrad(y, gy, ctx.R, conv_w, scale, shift, stride=ctx.stride)  # noqa: E731
-        side = ctx.needs_input_grad[10] and _side_ok(ctx.wparam, y)
-        g_conv = _on_side(wfn, y, gy, scale, shift) if side else None
+        g_conv = None
         if ctx.R == 3 and ctx.stride == 2:
             dA = bhconv.conv3x3_s2_dgrad(gy, conv_w, (h, w))
         elif ctx.R == 3:
@@ -1164,7 +1044,7 @@ class _BNConvFn(torch.autograd.Function):
         # the cross-rank exchange of the BatchNorm's backward sums runs (IPC side stream / async RCCL)
         # while the convolution's weight gradient -- which does not depend on it -- computes
         pending = _all_reduce_async(sums, ctx.process_group) if ctx.world > 1 else None
-        if ctx.needs_input_grad[10] and not side:
+        if ctx.needs_input_grad[10]:
             g_conv = wfn()
         if pending is not None:
             with comm_stats.timed("syncbn_bwd", sums):
@@ -1479,51 +1359,54 @@ def _bn_conv(bn, y, part, conv_w, kshift_out, R, stride=1):
                            bn.process_group, bn.num_batches_tracked, conv_w, kshift_out, R, stride)
 
 
-_FOLD_BN = os.environ.get("BH_FOLD_BN", "1") != "0"
-# BatchNorm + ReLU applied inside the consuming convolution instead of a normalisation pass
-# (BH_FOLD_APPLY): "all" (default) folds bn1 into the 3x3 conv and bn2 into conv3's 1x1 strip GEMM; "bn2"
-# / "bn1" only one of them; "none" keeps every pass. Same box: all 10443 / 10423, bn2 10430 / 10420,
-# none 10380 / 10386 img/s (profiles/resnet50_fold_apply_ab.txt): the 3x3 weight gradient's LDS
-# prologue costs about what the removed 64-channel bn1 pass saves, bn2's fold is the net gain
-_FOLD_APPLY = {"1": "all", "0": "none"}.get(os.environ.get("BH_FOLD_APPLY", "all"),
-                                            os.environ.get("BH_FOLD_APPLY", "all"))
-assert _FOLD_APPLY in ("all", "bn1", "bn2", "none"), f"BH_FOLD_APPLY={_FOLD_APPLY!r}"
-# the stem convolution's epilogue reduces the stem BatchNorm's statistics (BH_STEM_STATS=0: a pass)
-_STEM_STATS = os.environ.get("BH_STEM_STATS", "1") != "0"
-# the 1x1 layers the strip kernel does not take run on the own tiled MFMA GEMM (kernels/gemm.hip) with
-# the BatchNorm epilogues; BH_OWN_GEMM=0 puts them back on hipBLASLt + separate passes (A/B)
-def _own_gemm_kinds(v):
-    v = v.strip().lower()
-    if v in ("1", "all"):
-        return {"fwd", "bwd", "plain", "resid"}
-    if v in ("0", "none", ""):
-        return set()
-    kinds = {k.strip() for k in v.split(",")}
-    assert kinds <= {"fwd", "bwd", "plain", "resid"}, f"BH_OWN_GEMM={v!r}"
-    return kinds
+# Switches of the fused model, from the typed configuration (beforeholiday_amd/config.py; the env names in
+# brackets). Kept as module globals (refreshed by config.set) so the hot path reads a plain global.
+#  _FOLD_BN [BH_FOLD_BN]: BatchNorm statistics / apply folded into the convolutions.
+#  _FOLD_APPLY [BH_FOLD_APPLY]: BatchNorm + ReLU applied inside the consuming convolution instead of a
+#    normalisation pass: "all" folds bn1 into the 3x3 conv and bn2 into conv3's 1x1 strip GEMM; "bn2" /
+#    "bn1" only one of them; "none" keeps every pass. Same box: all 10443 / 10423, bn2 10430 / 10420, none
+#    10380 / 10386 img/s (profiles/resnet50_fold_apply_ab.txt).
+#  _STEM_STATS [BH_STEM_STATS]: the stem convolution's epilogue reduces the stem BatchNorm's statistics.
+#  _OWN_GEMM_KINDS [BH_OWN_GEMM]: the 1x1 layers the strip kernel does not take run on the own tiled MFMA
+#    GEMM (kernels/gemm.hip) with the BatchNorm epilogues: "fwd" (forward + statistics epilogue), "bwd"
+#    (data gradient + the previous BatchNorm's backward sums), "plain" (data gradient), "resid" (data
+#    gradient + the parked residual gradient).
+#  _BN_RES_FOLD [BH_BN_RES_FOLD]: bottleneck tail (conv3 -> bn3 -> + z -> ReLU) as one node whose backward
+#    folds bn3 into conv3 by linear algebra (_ConvBNResFn): "pro" where bn2 is folded into conv3's
+#    prologue, "all" everywhere, "0" never.
+#  _MASK_PRODUCER / _MASK_PRODUCER_ANY [BH_MASK_PRODUCER]: the next block's conv1 data gradient applies the
+#    tail's ReLU mask in its epilogue, also where hipBLASLt's residual GEMM ran before ("any"); "fast":
+#    only where the strip kernel is preferred anyway; "off": the tail's own mask pass. Same box: off 11102,
+#    fast 11195, any 11286 img/s.
+#  _DS_FOLD [BH_DS_FOLD]: the downsample BatchNorm folded into the tail node too (True: stride-1 blocks,
+#    "all": also stride 2, False: its own passes).
+_FOLD_BN = True
+_FOLD_APPLY = "all"
+_STEM_STATS = True
+_OWN_GEMM_KINDS = {"fwd", "plain"}
+_OWN_GEMM = True
+_BN_RES_FOLD = "pro"
+_MASK_PRODUCER = True
+_MASK_PRODUCER_ANY = True
+_DS_FOLD = True
 
 
-# which of those GEMM kinds take the own kernel: "fwd" (forward + statistics epilogue), "bwd" (data
-# gradient + the previous BatchNorm's backward sums), "plain" (data gradient), "resid" (data gradient
-# + the parked residual gradient); a comma list, "all" or "none"
-_OWN_GEMM_KINDS = _own_gemm_kinds(os.environ.get("BH_OWN_GEMM", "fwd,plain"))
-_OWN_GEMM = bool(_OWN_GEMM_KINDS)
+def _apply_config(c):
+    global _FOLD_BN, _FOLD_APPLY, _STEM_STATS, _OWN_GEMM_KINDS, _OWN_GEMM, _BN_RES_FOLD, _MASK_PRODUCER
+    global _MASK_PRODUCER_ANY, _DS_FOLD
+    _FOLD_BN, _FOLD_APPLY, _STEM_STATS = c.fold_bn, c.fold_apply, c.stem_stats
+    _OWN_GEMM_KINDS = {k for k in c.own_gemm.split(",") if k}
+    _OWN_GEMM = bool(_OWN_GEMM_KINDS)
+    _BN_RES_FOLD = {"off": "0"}.get(c.bn_res_fold, c.bn_res_fold)
+    _MASK_PRODUCER, _MASK_PRODUCER_ANY = c.mask_producer != "off", c.mask_producer == "any"
+    _DS_FOLD = {"off": False, "stride1": True, "all": "all"}[c.ds_fold]
 
 
 def _own(kind):
     return kind in _OWN_GEMM_KINDS
-_FOLD_3X3_BWD = os.environ.get("BH_FOLD_3X3_BWD", "0") == "1"
-# bottleneck tail (conv3 -> bn3 -> + z -> ReLU) as one node whose backward folds bn3 into conv3 by linear
-# algebra (_ConvBNResFn); BH_BN_RES_FOLD=0 keeps the per-layer nodes (A/B)
-_BN_RES_FOLD = {"1": "pro"}.get(os.environ.get("BH_BN_RES_FOLD", "pro"), os.environ.get("BH_BN_RES_FOLD", "pro"))
-assert _BN_RES_FOLD in ("pro", "all", "0"), f"BH_BN_RES_FOLD={_BN_RES_FOLD!r}"
-# the next block's conv1 data gradient applies the tail's ReLU mask in its epilogue, on the strip kernel
-# also where hipBLASLt's residual GEMM ran before ("any", default); "1": only where the strip kernel is
-# preferred anyway; "0": the tail's own mask pass. Same box: 0 11102, 1 11195, any 11286 img/s
-_MASK_PRODUCER = os.environ.get("BH_MASK_PRODUCER", "any") != "0"
-# the downsample BatchNorm folded into the tail node too (BH_DS_FOLD=0: its own passes, A/B)
-_DS_FOLD = {"0": False, "1": True}.get(os.environ.get("BH_DS_FOLD", "1"), os.environ.get("BH_DS_FOLD", "1"))
-_MASK_PRODUCER_ANY = os.environ.get("BH_MASK_PRODUCER", "any") == "any"
+
+
+_config.on_change(_apply_config)
 
 
 class Bottleneck(nn.Module):

@@ -18,6 +18,8 @@ from dataclasses import dataclass, field
 from typing import Optional
 
 import torch
+
+from .. import config as _config
 import torch.nn.functional as F
 
 from ..ops import fused_dense as _fd
@@ -180,7 +182,7 @@ def _fused_mlp_ok(x, mlp) -> bool:
     return (x.is_cuda and x.dtype in (torch.float16, torch.bfloat16) and mlp.bias_gelu_fusion
             and c.weight.dtype == x.dtype and r.weight.dtype == x.dtype and c.bias is not None
             and not c.gradient_accumulation_fusion and not r.gradient_accumulation_fusion
-            and os.environ.get("BH_FUSED_MLP", "1") != "0")
+            and _config.get().fused_mlp)
 
 
 def openai_gelu(x):
@@ -295,7 +297,7 @@ class CoreAttention(MegatronModule):
         import os
 
         return (x.is_cuda and x.dtype in (torch.float16, torch.bfloat16) and hn == 64
-                and os.environ.get("BH_FLASH_ATTN", "1") != "0")
+                and _config.get().flash_attn)
 
     def flash(self, qkv, attention_mask):
         """qkv [sq, b*np, 3, 64] (the fused QKV projection output, viewed) -> context [sq, b, np*64].

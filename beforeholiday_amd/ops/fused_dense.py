@@ -4,10 +4,11 @@ GPU tensors run ``beforeholiday_amd._C`` (GEMMs on hipBLASLt via ATen, activatio
 bias-grad passes in kernels/dense.hip); CPU tensors run the PyTorch reference below with the same
 semantics (exact-erf GELU; ReLU / sigmoid derivatives taken from the activation output).
 """
-import os
 from typing import List, Optional
 
 import torch
+
+from .. import config as _config
 import torch.nn.functional as F
 
 from .._native import submodule
@@ -146,7 +147,6 @@ def mlp_backward(use_bias: int, activation: int, grad_o, outputs, inputs) -> Lis
 # rank runs the same kernel.
 _WGRAD_MAX_ELEMS = 3072 * 800
 _WGRAD_MIN_TOKENS = 4096
-_WGRAD_MFMA = __import__("os").environ.get("BH_DENSE_WGRAD", "1") != "0"  # A/B switch
 
 
 def weight_grad(d_output: torch.Tensor, input: torch.Tensor) -> torch.Tensor:
@@ -154,7 +154,7 @@ def weight_grad(d_output: torch.Tensor, input: torch.Tensor) -> torch.Tensor:
     weight gradient ``[out, in]`` in ``d_output``'s dtype."""
     M, K = d_output.shape
     C = input.size(1)
-    if (_WGRAD_MFMA and d_output.is_cuda and d_output.dtype in (torch.float16, torch.bfloat16)
+    if (_config.get().dense_wgrad_mfma and d_output.is_cuda and d_output.dtype in (torch.float16, torch.bfloat16)
             and input.dtype == d_output.dtype
             and M >= _WGRAD_MIN_TOKENS and K * C <= _WGRAD_MAX_ELEMS and d_output.is_contiguous()
             and input.is_contiguous()):
@@ -237,7 +237,6 @@ def bias_dropout_add(x: torch.Tensor, bias: Optional[torch.Tensor], residual: to
     return residual + out
 
 
-_EMBED_NATIVE = os.environ.get("BH_EMBED_NATIVE", "1") != "0"  # 0: torch's embedding backward (A/B)
 
 
 class _EmbeddingFn(torch.autograd.Function):
@@ -262,7 +261,7 @@ def embedding(ids: torch.Tensor, weight: torch.Tensor, padding_idx: Optional[int
     """``F.embedding(ids, weight, padding_idx)``; on the GPU (fp32 / fp16 / bf16 weights that need a
     gradient) the backward runs the deterministic sync-free kernel above."""
     if (weight.is_cuda and weight.requires_grad and torch.is_grad_enabled()
-            and weight.dtype in (torch.float32, torch.float16, torch.bfloat16) and _EMBED_NATIVE):
+            and weight.dtype in (torch.float32, torch.float16, torch.bfloat16) and _config.get().embed_native):
         if padding_idx is not None and padding_idx < 0:
             padding_idx += weight.size(0)
         return _EmbeddingFn.apply(ids, weight, padding_idx)

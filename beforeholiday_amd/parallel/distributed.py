@@ -295,6 +295,10 @@ class DistributedDataParallel(Module):
 
         # sync parameters and buffers from rank 0
         if self._collectives:
+            if self.world_size > 1:  # every rank runs the same kernels / fold modes (beforeholiday_amd.config)
+                from .. import config
+
+                config.check_ranks(process_group)
             root = _group_rank0(process_group)
             tensors = [p.data for p in module.parameters()] + [b.data for b in module.buffers()]
             for bucket in split_by_type(tensors):

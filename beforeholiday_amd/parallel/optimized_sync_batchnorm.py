@@ -12,7 +12,6 @@ collectives are skipped and the merge is fused into the statistics finalize.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.distributed as dist
@@ -23,20 +22,21 @@ from ..ops import conv_bn as conv_bn_ops
 from ..ops import syncbn
 from . import comm_stats
 
-_STATS_MODE = os.environ.get("BH_SYNCBN_STATS", "allreduce")
-
-
 def stats_mode() -> str:
-    """How ranks combine forward statistics: ``"allreduce"`` (default; one [2C+1] SUM all-reduce of
-    shifted sums) or ``"allgather"`` (the reference's [W, 2C+1] all_gather + Welford merge)."""
-    return _STATS_MODE
+    """How ranks combine forward statistics (``Config.syncbn_stats``): ``"allreduce"`` (default; one
+    [2C+1] SUM all-reduce of shifted sums) or ``"allgather"`` (the reference's [W, 2C+1] all_gather +
+    Welford merge)."""
+    from .. import config
+
+    return config.get().syncbn_stats
 
 
 def set_stats_mode(mode: str) -> None:
-    global _STATS_MODE
+    from .. import config
+
     if mode not in ("allreduce", "allgather"):
         raise ValueError(f"SyncBatchNorm stats mode must be 'allreduce' or 'allgather', got {mode!r}")
-    _STATS_MODE = mode
+    config.set(syncbn_stats=mode)
 
 
 def _world(pg):

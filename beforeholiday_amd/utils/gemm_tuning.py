@@ -30,7 +30,9 @@ def _tunable():
 
 
 def table_path(path: Optional[str] = None) -> str:
-    return path or os.environ.get("BH_GEMM_TABLE", DEFAULT_TABLE)
+    from .. import config
+
+    return path or config.get().gemm_table or DEFAULT_TABLE
 
 
 def enable_tuned_gemms(path: Optional[str] = None, tune: bool = False, max_tuning_ms: int = 20,

@@ -152,7 +152,7 @@ def main():
 
     gemm_tuned = gemm_tuning.setup(args.gemm_table)
 
-    from beforeholiday_amd import amp
+    from beforeholiday_amd import amp, config
     from beforeholiday_amd._native import require_native
     from beforeholiday_amd.models import resnet50, resnet50_fused
     from beforeholiday_amd.optimizers import FusedAdam, FusedLAMB, FusedSGD
@@ -162,8 +162,9 @@ def main():
 
     require_native("bench")
     if not args.host_scaler:
-        os.environ["BH_AMP_DEVICE_SCALER"] = "1"  # amp/scaler.py enable_device_mode: no host sync per step
+        config.set(amp_device_scaler=True)  # amp/scaler.py enable_device_mode: no host sync per step
     set_stats_mode(args.syncbn_stats)
+    config.check_ranks()  # every rank runs the same typed configuration (raises otherwise)
     torch.manual_seed(1234 + rank)
     bn_group, bn_exchange = None, "none"
     if world > 1:

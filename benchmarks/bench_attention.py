@@ -31,6 +31,7 @@ def timeit(fn, iters=10, warm=3):
 
 
 def main():
+    from beforeholiday_amd import config
     from beforeholiday_amd._native import require_native, submodule
     from beforeholiday_amd.contrib.multihead_attn._core import MASK_CAUSAL, MASK_NONE, FusedSelfAttnFn
 
@@ -42,7 +43,7 @@ def main():
         g = torch.randn(S, B * H, 64, device="cuda", dtype=dt)
         mode = MASK_CAUSAL if causal else MASK_NONE
         flops = 4 * B * H * S * S * 64 * (0.5 if causal else 1.0)
-        os.environ["BH_ATTN_FLASH_ONLY"] = "1"
+        config.set(attn_flash_only=True)
 
         def ours():
             return FusedSelfAttnFn.apply(qkv, H, 0.125, None, mode, p, True, float("-inf"))
@@ -71,7 +72,7 @@ def main():
             except Exception as e:  # noqa: BLE001 - e.g. SDPA backend unavailable
                 r = {"B": B, "H": H, "S": S, "impl": name, "error": repr(e)[:200]}
             print(json.dumps(r), flush=True)
-        os.environ.pop("BH_ATTN_FLASH_ONLY")
+        config.set(attn_flash_only=False)
         del qkv, g
         torch.cuda.empty_cache()
 

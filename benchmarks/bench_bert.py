@@ -57,7 +57,10 @@ def main():
     from beforeholiday_amd.models import BertModel, TransformerConfig
     from beforeholiday_amd.optimizers import FusedLAMB
 
-    os.environ.setdefault("BH_AMP_DEVICE_SCALER", "1")  # device-resident loss scale (amp/scaler.py), as bench.py
+    if "BH_AMP_DEVICE_SCALER" not in os.environ:  # device-resident loss scale (amp/scaler.py), as bench.py
+        from beforeholiday_amd import config
+
+        config.set(amp_device_scaler=True)
     from beforeholiday_amd.parallel import DistributedDataParallel
     from beforeholiday_amd.transformer import parallel_state, tensor_parallel
 

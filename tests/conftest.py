@@ -32,3 +32,17 @@ def pytest_collection_modifyitems(config, items):
 def devices():
     """Parametrisation helper: cpu always, cuda as a gpu-marked case."""
     return [pytest.param("cpu"), pytest.param("cuda", marks=pytest.mark.gpu)]
+
+
+@pytest.fixture(autouse=True)
+def _restore_bh_config():
+    """Tests switch paths with ``beforeholiday_amd.config.set(...)``; every test starts from and leaves
+    behind the process's configuration as it was."""
+    import dataclasses
+
+    from beforeholiday_amd import config
+
+    old = config.get()
+    yield
+    if config.get() != old:
+        config.set(**dataclasses.asdict(old))

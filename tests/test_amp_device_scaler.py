@@ -7,6 +7,8 @@ growth after ``scale_window`` clean steps), and on an injected overflow: paramet
 the skipped step and the scale halved."""
 import pytest
 import torch
+
+from beforeholiday_amd import config
 import torch.nn.functional as F
 
 
@@ -15,7 +17,7 @@ def _run(device_mode, steps, inf_at=None, monkeypatch=None, window=3, init_scale
     from beforeholiday_amd.amp._amp_state import _amp_state
     from beforeholiday_amd.optimizers import FusedLAMB
 
-    monkeypatch.setenv("BH_AMP_DEVICE_SCALER", "1" if device_mode else "0")
+    config.set(amp_device_scaler=device_mode)
     torch.manual_seed(0)
     model = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.BatchNorm1d(64), torch.nn.ReLU(),
                                 torch.nn.Linear(64, 8)).cuda()

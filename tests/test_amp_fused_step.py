@@ -9,6 +9,8 @@ device-resident loss scale, gradient accumulation (a second backward materialise
 ``amp.master_params`` (materialises the master gradients before it yields), and O5 (bf16, no scale)."""
 import pytest
 import torch
+
+from beforeholiday_amd import config
 import torch.nn.functional as F
 
 
@@ -19,8 +21,8 @@ def _run(monkeypatch, fused, opt_name="lamb", device_mode=True, steps=5, inf_at=
     from beforeholiday_amd.amp._amp_state import _amp_state
     from beforeholiday_amd.optimizers import FusedAdam, FusedLAMB
 
-    monkeypatch.setenv("BH_AMP_DEVICE_SCALER", "1" if device_mode else "0")
-    monkeypatch.setattr(_process_optimizer, "fused_master_step", fused)
+    config.set(amp_device_scaler=device_mode)
+    config.set(amp_fused_master_step=fused)
     torch.manual_seed(0)
     model = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.BatchNorm1d(64), torch.nn.ReLU(),
                                 torch.nn.Linear(64, 24), torch.nn.ReLU(), torch.nn.Linear(24, 8)).cuda()
@@ -142,17 +144,17 @@ def test_fused_plan_flow_cpu(monkeypatch):
     ``amp.master_params`` materialises exactly the unfused master gradients."""
     from beforeholiday_amd.amp import _process_optimizer
 
-    monkeypatch.setenv("BH_AMP_DEVICE_SCALER", "0")
+    config.set(amp_device_scaler=False)
     x = torch.randn(16, 32).half()
     y = torch.randint(0, 8, (16,))
 
-    monkeypatch.setattr(_process_optimizer, "fused_master_step", False)
+    config.set(amp_fused_master_step=False)
     amp, model, opt = _cpu_setup()
     with amp.scale_loss(F.cross_entropy(model(x).float(), y), opt) as s:
         s.backward()
     want = [p.grad.clone() for p in amp.master_params(opt)]
 
-    monkeypatch.setattr(_process_optimizer, "fused_master_step", True)
+    config.set(amp_fused_master_step=True)
     amp, model, opt = _cpu_setup()
     calls = []
     opt._amp_fused_ok = lambda: True

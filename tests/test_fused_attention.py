@@ -8,6 +8,8 @@ running the reference backward with that same mask.
 import pytest
 import torch
 
+from beforeholiday_amd import config
+
 pytestmark = pytest.mark.gpu
 
 
@@ -122,7 +124,7 @@ def test_self_mha_module_fused_matches_unfused(impl, mask, monkeypatch):
     kpm = (torch.rand(8, 64, device="cuda") < 0.2) if mask == "pad" else None
 
     def run(fused):
-        monkeypatch.setenv("BH_MHA_FUSED", "1" if fused else "0")
+        config.set(mha_fused=fused)
         xi = x.clone().requires_grad_(True)
         m.zero_grad()
         out, _ = m(xi, xi, xi, key_padding_mask=kpm, need_weights=False, attn_mask=None, is_training=True)

@@ -20,12 +20,18 @@ def test_weight_grad_cpu_fallback():
                                            ("none", set()), ("0", set()), ("fwd,plain", {"fwd", "plain"}),
                                            (" bwd ", {"bwd"})])
 def test_own_gemm_kinds(setting, kinds):
-    assert R._own_gemm_kinds(setting) == kinds
+    from beforeholiday_amd import config
+
+    c = config.Config.from_env({"BH_OWN_GEMM": setting})
+    with config.override(own_gemm=c.own_gemm):
+        assert R._OWN_GEMM_KINDS == kinds and R._OWN_GEMM == bool(kinds)
 
 
 def test_own_gemm_kinds_rejects_unknown():
-    with pytest.raises(AssertionError):
-        R._own_gemm_kinds("fwd,bogus")
+    from beforeholiday_amd import config
+
+    with pytest.raises(ValueError):
+        config.Config.from_env({"BH_OWN_GEMM": "fwd,bogus"})
 
 
 def test_tr_cpu():

@@ -2,6 +2,8 @@
 training step, replayed, must produce the same parameters and losses as the same steps run eagerly."""
 import pytest
 import torch
+
+from beforeholiday_amd import config
 import torch.nn.functional as F
 
 
@@ -46,7 +48,7 @@ def _train(graph: bool, steps: int = 4):
 
 @pytest.mark.gpu
 def test_graphed_step_matches_eager(monkeypatch):
-    monkeypatch.setenv("BH_AMP_DEVICE_SCALER", "1")  # no host synchronisation inside the step
+    config.set(amp_device_scaler=True)  # no host synchronisation inside the step
     l_eager, p_eager = _train(False)
     l_graph, p_graph = _train(True)
     torch.testing.assert_close(l_graph, l_eager, rtol=2e-3, atol=2e-3)

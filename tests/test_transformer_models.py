@@ -3,6 +3,8 @@ single-rank model exactly (fp64, dropout off, CPU ranks over gloo)."""
 import pytest
 import torch
 
+from beforeholiday_amd import config
+
 from tests._dist import run_distributed
 
 
@@ -234,14 +236,13 @@ def _gpt_fused_mlp(rank, world):
     mask, _, pos = get_ltor_masks_and_position_ids(tokens, -1, False, False, False)
     res = {}
     for fused in ("1", "0"):
-        os.environ["BH_FUSED_MLP"] = fused
+        config.set(fused_mlp=fused == "1")
         model.zero_grad(set_to_none=True)
         loss = model(tokens, pos, mask, labels=labels)
         loss.float().mean().backward()
         mlp = model.language_model.encoder.layers[0].mlp
         res[fused] = (loss.detach().float(), mlp.dense_h_to_4h.weight.grad.float(), mlp.dense_h_to_4h.bias.grad.float(),
                       mlp.dense_4h_to_h.weight.grad.float(), model.language_model.embedding.word_embeddings.weight.grad.float())
-    os.environ.pop("BH_FUSED_MLP")
     for a, b in zip(res["1"], res["0"]):
         torch.testing.assert_close(a, b, rtol=5e-2, atol=5e-2)
     ps.destroy_model_parallel()
@@ -281,7 +282,7 @@ def _flash_vs_unfused(rank, world, kind):
             return loss.float().mean() + binary.float().sum() * 0.01
     res = {}
     for flash in ("1", "0"):
-        os.environ["BH_FLASH_ATTN"] = flash
+        config.set(flash_attn=flash == "1")
         model.zero_grad(set_to_none=True)
         loss = run()
         loss.backward()
@@ -289,7 +290,6 @@ def _flash_vs_unfused(rank, world, kind):
         res[flash] = (loss.detach(), layer.self_attention.query_key_value.weight.grad.float(),
                       layer.self_attention.dense.weight.grad.float(),
                       model.language_model.embedding.word_embeddings.weight.grad.float())
-    os.environ.pop("BH_FLASH_ATTN")
     for a, b in zip(res["1"], res["0"]):
         torch.testing.assert_close(a, b, rtol=5e-2, atol=5e-2)
     ps.destroy_model_parallel()
