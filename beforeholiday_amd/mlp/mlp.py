@@ -1,7 +1,12 @@
 """N-layer MLP in one autograd node (reference: apex/mlp/mlp.py:7-79).
 
-Forward: per layer one hipBLASLt GEMM (bias in the epilogue) + one in-place activation pass.
-Backward: per layer one fused dActivation + bias-grad pass, then the wgrad / dgrad GEMMs.
+Forward: per layer ONE GEMM with bias + activation in its epilogue -- the MFMA kernel of
+kernels/gemm.hip where its static rule picks it (K <= 1024), else hipBLASLt's addmm + one in-place
+activation pass (``gemm.linear_act``).
+Backward: the last layer's dActivation + bias gradient in one pass; every earlier layer's dActivation
+and bias gradient inside the data-gradient GEMM's epilogue (``gemm.linear_dact``); the weight
+gradients on the MFMA weight-gradient kernel where it applies (``ops.fused_dense.weight_grad``: <= ~2.4M
+elements, >= 4096 rows), hipBLASLt otherwise.
 The activation follows EVERY layer (including the last), like the reference.
 """
 import math

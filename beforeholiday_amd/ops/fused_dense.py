@@ -7,10 +7,9 @@ semantics (exact-erf GELU; ReLU / sigmoid derivatives taken from the activation 
 from typing import List, Optional
 
 import torch
-
-from .. import config as _config
 import torch.nn.functional as F
 
+from .. import config as _config
 from .._native import submodule
 
 ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_GELU, ACT_GELU_TANH = 0, 1, 2, 3, 4
@@ -73,14 +72,42 @@ def bias_grad(dy: torch.Tensor) -> torch.Tensor:
     return dy.reshape(-1, dy.size(-1)).float().sum(0).to(dy.dtype)
 
 
+def _gemm_ok(*ts):
+    return all(t.is_cuda and t.dtype in (torch.float16, torch.bfloat16) for t in ts) and len({t.dtype for t in ts}) == 1
+
+
+def _transposed(w):
+    """w.t().contiguous() through the LDS-tiled transpose kernel (16-byte accesses) where it applies."""
+    if w.dim() == 2 and w.is_contiguous() and w.size(0) % 8 == 0 and w.size(1) % 8 == 0 and w.element_size() == 2:
+        return submodule("gemm").transpose(w)
+    return w.t().contiguous()
+
+
 def linear_bias_forward(input, weight, bias):
+    """y = x . W^T + b. 16-bit GPU tensors: the MFMA GEMM with the bias in its epilogue where the static
+    dispatch rule of kernels/gemm.hip picks it (K <= 1024, ``gemm.linear_act``), hipBLASLt's addmm
+    otherwise -- the same rule for every rank."""
     if input.is_cuda:
+        if _gemm_ok(input, weight) and (bias is None or bias.dtype == input.dtype):
+            x = input.reshape(-1, input.size(-1)).contiguous()
+            y = submodule("gemm").linear_act(x, weight.contiguous(), bias, ACT_NONE, False)[0]
+            return y.view(*input.shape[:-1], weight.size(0))
         return _fd().linear_bias_forward(input, weight, bias)
     return F.linear(input, weight, bias)
 
 
 def linear_bias_backward(input, weight, d_output):
+    """(d_input, d_weight, d_bias). 16-bit GPU tensors: the weight gradient on the MFMA weight-gradient
+    kernel (``weight_grad``: <= ~2.4M-element weights, >= 4096 tokens), the input gradient through
+    ``gemm.linear_dact`` (its rule keeps hipBLASLt for a plain data gradient, where the library
+    measured 1.0-1.18x faster: profiles/dgrad_transformer_nt_vs_hipblaslt.jsonl), the bias gradient as
+    one column-sum pass."""
     if input.is_cuda:
+        if _gemm_ok(input, weight, d_output):
+            dy = d_output.reshape(-1, d_output.size(-1)).contiguous()
+            x = input.reshape(-1, input.size(-1)).contiguous()
+            dx = submodule("gemm").linear_dact(dy, _transposed(weight), None, ACT_NONE, False)[0]
+            return dx.view(input.shape), weight_grad(dy, x), bias_grad(dy)
         return _fd().linear_bias_backward(input, weight, d_output)
     dy = d_output.reshape(-1, d_output.size(-1))
     x = input.reshape(-1, input.size(-1))
@@ -88,8 +115,15 @@ def linear_bias_backward(input, weight, d_output):
 
 
 def linear_gelu_linear_forward(input, weight1, bias1, weight2, bias2):
-    """Returns (gelu_in, gelu_out, output)."""
+    """Returns (gelu_in, gelu_out, output): both GEMMs through ``gemm.linear_act`` (bias + GELU + the
+    pre-activation in the first one's epilogue, bias in the second's) on 16-bit GPU tensors."""
     if input.is_cuda:
+        if _gemm_ok(input, weight1, weight2) and bias1 is not None and bias2 is not None:
+            gm = submodule("gemm")
+            x = input.reshape(-1, input.size(-1)).contiguous()
+            gelu_out, gelu_in = gm.linear_act(x, weight1.contiguous(), bias1.contiguous(), ACT_GELU, True)
+            out = gm.linear_act(gelu_out, weight2.contiguous(), bias2.contiguous(), ACT_NONE, False)[0]
+            return gelu_in, gelu_out, out
         return _fd().linear_gelu_linear_forward(input, weight1, bias1, weight2, bias2)
     x = input.reshape(-1, input.size(-1))
     gelu_in = F.linear(x, weight1, bias1)
@@ -98,8 +132,19 @@ def linear_gelu_linear_forward(input, weight1, bias1, weight2, bias2):
 
 
 def linear_gelu_linear_backward(input, gelu_in, output1, weight1, weight2, d_output2):
-    """Returns (d_input, d_weight1, d_bias1, d_weight2, d_bias2) — with the dGELU applied."""
+    """Returns (d_input, d_weight1, d_bias1, d_weight2, d_bias2) — with the dGELU applied. On 16-bit GPU
+    tensors: d(gelu_in) and d_bias1 from one ``gemm.linear_dact`` (dGELU + bias-gradient epilogue), the
+    weight gradients on the MFMA weight-gradient kernel (``weight_grad``)."""
     if input.is_cuda:
+        if _gemm_ok(input, weight1, weight2, d_output2):
+            gm = submodule("gemm")
+            x = input.reshape(-1, input.size(-1)).contiguous()
+            dy = d_output2.reshape(-1, d_output2.size(-1)).contiguous()
+            h = output1.reshape(-1, output1.size(-1)).contiguous()
+            d_h, d_b1 = gm.linear_dact(dy, _transposed(weight2), gelu_in.reshape(-1, gelu_in.size(-1)).contiguous(),
+                                       ACT_GELU, True)
+            d_in = gm.linear_dact(d_h, _transposed(weight1), None, ACT_NONE, False)[0]
+            return d_in.view(input.shape), weight_grad(d_h, x), d_b1, weight_grad(dy, h), bias_grad(dy)
         return _fd().linear_gelu_linear_backward(input, gelu_in, output1, weight1, weight2, d_output2)
     x = input.reshape(-1, input.size(-1))
     dy = d_output2.reshape(-1, d_output2.size(-1))
@@ -123,8 +168,34 @@ def mlp_forward(use_bias: int, activation: int, inputs: List[torch.Tensor]) -> L
 
 
 def mlp_backward(use_bias: int, activation: int, grad_o, outputs, inputs) -> List[torch.Tensor]:
+    """Gradients for ``inputs``. On the GPU one native call (dActivation + bias gradient inside the
+    data-gradient GEMM's epilogue); the weight gradients of 16-bit layers then go to the MFMA
+    weight-gradient kernel where it applies (``weight_grad``) instead of hipBLASLt."""
     if inputs[0].is_cuda:
-        return submodule("mlp_cuda").backward(use_bias, activation, grad_o, list(outputs), list(inputs))
+        if not (_gemm_ok(*inputs) and _gemm_ok(grad_o, *outputs)):
+            return submodule("mlp_cuda").backward(use_bias, activation, grad_o, list(outputs), list(inputs))
+        gm = submodule("gemm")
+        n = (len(inputs) - 1) // 2 if use_bias else len(inputs) - 1
+        act = {0: ACT_NONE, 1: ACT_RELU, 2: ACT_SIGMOID}[activation]
+        grads = [None] * len(inputs)
+        g = grad_o.contiguous()
+        if act == ACT_NONE:
+            dpre, db = g, (bias_grad(g) if use_bias else None)
+        else:
+            dpre, db = act_backward(g, outputs[n - 1].contiguous(), act, bool(use_bias))
+        for i in range(n - 1, -1, -1):
+            x = (inputs[0] if i == 0 else outputs[i - 1]).contiguous()
+            grads[1 + i] = weight_grad(dpre, x)
+            if use_bias:
+                grads[1 + n + i] = db
+            if i > 0:
+                dpre, db = gm.linear_dact(dpre, _transposed(inputs[1 + i]), outputs[i - 1].contiguous(), act,
+                                          bool(use_bias))
+            else:
+                g = (gm.linear_dact(dpre, _transposed(inputs[1]), None, ACT_NONE, False)[0]
+                     if inputs[0].requires_grad else None)
+        grads[0] = g if g is not None else torch.zeros_like(inputs[0])
+        return grads
     n = (len(inputs) - 1) // 2 if use_bias else len(inputs) - 1
     act = {0: ACT_NONE, 1: ACT_RELU, 2: ACT_SIGMOID}[activation]
     grads = [None] * len(inputs)

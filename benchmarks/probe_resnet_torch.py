@@ -51,13 +51,14 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--variants", type=int, default=5, help="run only the first N variants (1: fp16 channels_last)")
     args = ap.parse_args()
     variants = [
         (torch.float16, True, 256, False), (torch.bfloat16, True, 256, False),
         (torch.float16, False, 256, False), (torch.bfloat16, False, 256, False),
         (torch.bfloat16, True, 128, False),
     ]
-    for dt, cl, bs, bench in variants:
+    for dt, cl, bs, bench in variants[:args.variants]:
         t0 = time.time()
         try:
             ips, ms = run(dt, cl, bs, args.steps, args.warmup, bench)

@@ -293,3 +293,64 @@ def test_embedding_backward_matches_fp32(dtype, V, H, n, pad):
     w.grad = None
     fd.embedding(ids, w, pad).backward(dy)
     assert torch.equal(w.grad, g1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_fused_dense_mfma_paths_large(dtype):
+    """16-bit FusedDense / FusedDenseGeluDense / MLP at >= 4096 rows: forward on the MFMA GEMM with the
+    bias (GELU) epilogue, weight gradients on the MFMA weight-gradient kernel, dGELU + bias gradient in
+    the data-gradient epilogue -- vs fp32 PyTorch."""
+    from beforeholiday_amd.fused_dense import FusedDense, FusedDenseGeluDense
+    from beforeholiday_amd.mlp import MLP
+
+    torch.manual_seed(5)
+    tol = dict(rtol=3e-2, atol=3e-2) if dtype == torch.float16 else dict(rtol=6e-2, atol=6e-2)
+    x = (torch.randn(4096, 256, device="cuda") * 0.5).to(dtype).requires_grad_()
+    xr = x.detach().float().requires_grad_()
+
+    m = FusedDense(256, 128).cuda().to(dtype)
+    w, b = m.weight.detach().float().requires_grad_(), m.bias.detach().float().requires_grad_()
+    y, yr = m(x), F.linear(xr, w, b)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    g = torch.randn_like(yr) * 0.1
+    y.backward(g.to(dtype))
+    yr.backward(g)
+    torch.testing.assert_close(x.grad.float(), xr.grad, **tol)
+    torch.testing.assert_close(m.weight.grad.float(), w.grad, rtol=tol["rtol"], atol=tol["atol"] * 20)
+    torch.testing.assert_close(m.bias.grad.float(), b.grad, rtol=tol["rtol"], atol=tol["atol"] * 20)
+
+    x.grad = None
+    xr.grad = None
+    m2 = FusedDenseGeluDense(256, 512, 128).cuda().to(dtype)
+    with torch.no_grad():  # (as test_fused_dense_gelu_dense: the 16-bit hidden activation rounds relative to
+        for p in m2.parameters():  # its magnitude, so keep the two-layer outputs O(1))
+            p.mul_(0.2)
+    ps = [p.detach().float().requires_grad_() for p in (m2.weight, m2.bias, m2.weight2, m2.bias2)]
+    y2 = m2(x)
+    yr2 = F.linear(F.gelu(F.linear(xr, ps[0], ps[1])), ps[2], ps[3])
+    torch.testing.assert_close(y2.float(), yr2, **tol)
+    y2.backward(g.to(dtype))
+    yr2.backward(g)
+    torch.testing.assert_close(x.grad.float(), xr.grad, **tol)
+    for p, r in zip((m2.weight, m2.bias, m2.weight2, m2.bias2), ps):
+        torch.testing.assert_close(p.grad.float(), r.grad, rtol=tol["rtol"], atol=tol["atol"] * 20)
+
+    for act in ("relu", "none"):
+        x.grad = None
+        mlp = MLP([256, 512, 128], bias=True, activation=act).cuda().to(dtype)
+        ws = [t.detach().float().requires_grad_() for t in list(mlp.weights) + list(mlp.biases)]
+        xr3 = x.detach().float().requires_grad_()
+        h = xr3
+        for i in range(2):
+            h = F.linear(h, ws[i], ws[2 + i])
+            h = torch.relu(h) if act == "relu" else h
+        y3 = mlp(x)
+        torch.testing.assert_close(y3.float(), h, **tol)
+        y3.backward(g.to(dtype))
+        h.backward(g)
+        # (16-bit hidden activations and pre-activation gradients: a rare element lands ~1 rounding step
+        # of the hidden layer past the single-layer tolerance)
+        torch.testing.assert_close(x.grad.float(), xr3.grad, rtol=tol["rtol"], atol=2 * tol["atol"])
+        for p, r in zip(list(mlp.weights) + list(mlp.biases), ws):
+            torch.testing.assert_close(p.grad.float(), r.grad, rtol=tol["rtol"], atol=tol["atol"] * 20)
