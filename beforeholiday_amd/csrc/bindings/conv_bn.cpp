@@ -184,6 +184,22 @@ at::Tensor sum_parts(const at::Tensor& part, double count) {
   return out;
 }
 
+// sum_parts plus the BatchNorm's fp32 parameter gradients from the same launch: (sums, gw = sums[N:] * invstd,
+// gb = sums[:N] as a separate tensor -- this rank's own, the sums may be all-reduced in place afterwards)
+std::vector<at::Tensor> sum_parts_grads(const at::Tensor& part, double count, const at::Tensor& invstd) {
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.dim() == 3 && part.size(0) == 2 &&
+                  part.is_contiguous(),
+              "conv_bn.sum_parts: part must be a contiguous fp32 [2, G, N] GPU tensor");
+  const int64_t G = part.size(1), N = part.size(2);
+  TORCH_CHECK(invstd.is_cuda() && invstd.scalar_type() == at::kFloat && invstd.is_contiguous() && invstd.numel() == N,
+              "conv_bn.sum_parts: invstd must be a contiguous fp32 [N] GPU tensor");
+  auto out = at::empty({2 * N + (count >= 0 ? 1 : 0)}, part.options());
+  auto gw = at::empty({N}, part.options()), gb = at::empty({N}, part.options());
+  bh::c1x1_sum_parts((int)G, (int)N, part.data_ptr<float>(), out.data_ptr<float>(), (float)count, stream_for(part),
+                     invstd.data_ptr<float>(), gw.data_ptr<float>(), gb.data_ptr<float>());
+  return {out, gw, gb};
+}
+
 // C = A . B^T (+ resid) on the tiled MFMA GEMM (kernels/gemm.hip) with a BatchNorm epilogue (epi 0: none;
 // 1: forward statistics centred on kshift; 2: the previous BatchNorm's backward sums with by / bscale /
 // bshift / bmean) -- the compute-bound 1x1 layers. Returns (C [M, N], partials [2, slabs, N] or empty).
@@ -252,6 +268,7 @@ void register_conv_bn(pybind11::module_& root) {
         py::arg("resid") = false, py::arg("s2_h") = 0, py::arg("s2_w") = 0, py::arg("epi") = 0,
         py::arg("s2_scatter") = false, py::arg("bnb") = false);
   m.def("sum_parts", &sum_parts, py::arg("part"), py::arg("count") = -1.0);
+  m.def("sum_parts_grads", &sum_parts_grads, py::arg("part"), py::arg("count"), py::arg("invstd"));
   m.def("gemm_bn", &gemm_bn, py::arg("a"), py::arg("b"), py::arg("epi"), py::arg("kshift") = py::none(),
         py::arg("by") = py::none(), py::arg("bscale") = py::none(), py::arg("bshift") = py::none(),
         py::arg("bmean") = py::none(), py::arg("brelu") = true, py::arg("resid") = py::none());

@@ -78,6 +78,7 @@ void c1x1_run(int dt, const C1x1Args& a, hipStream_t st);
 
 // sums[n] = sum_g part[g][n], sums[N + n] = sum_g part[G + g][n], sums[2N] = count (if count >= 0):
 // the [2N+1] layout of syncbn.stats_local_sums (forward) or [2N] (sum_dy, sum_dy_xmu) (backward)
-void c1x1_sum_parts(int G, int N, const float* part, float* sums, float count, hipStream_t st);
+void c1x1_sum_parts(int G, int N, const float* part, float* sums, float count, hipStream_t st,
+                    const float* invstd = nullptr, float* gw = nullptr, float* gb = nullptr);
 
 }  // namespace bh

@@ -439,8 +439,12 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
 
 constexpr int kSumRows = 16;  // partial rows summed in parallel per column
 
+// (optional) the BatchNorm's parameter gradients from the same sums: gb = sum dy (statistic 0), gw = sum
+// dy x_hat = (statistic 1) * invstd -- the two tiny elementwise launches per BatchNorm they replace
 __global__ __launch_bounds__(64 * kSumRows) void k_sum_parts(int G, int N, const float* __restrict__ part,
-                                                             float* __restrict__ sums, float count) {
+                                                             float* __restrict__ sums, float count,
+                                                             const float* __restrict__ invstd, float* __restrict__ gw,
+                                                             float* __restrict__ gb) {
   // block = 64 columns x kSumRows row groups of one statistic (blockIdx.y); coalesced 256-byte rows,
   // a fixed order (strided per group, then the groups in order): deterministic
   __shared__ float sh[kSumRows][64];
@@ -467,6 +471,8 @@ __global__ __launch_bounds__(64 * kSumRows) void k_sum_parts(int G, int N, const
 #pragma unroll
     for (int q = 0; q < kSumRows; ++q) t += sh[q][cl];
     sums[(int64_t)which * N + c] = t;
+    if (which == 0 && gb) gb[c] = t;
+    if (which == 1 && gw) gw[c] = t * invstd[c];
   }
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && count >= 0.f) sums[2 * N] = count;
 }
@@ -654,8 +660,10 @@ void c1x1_run(int dt, const C1x1Args& a_in, hipStream_t st) {
   if (e != hipSuccess) throw std::runtime_error(std::string("c1x1: ") + hipGetErrorString(e));
 }
 
-void c1x1_sum_parts(int G, int N, const float* part, float* sums, float count, hipStream_t st) {
-  hipLaunchKernelGGL(k_sum_parts, dim3((N + 63) / 64, 2), dim3(64 * kSumRows), 0, st, G, N, part, sums, count);
+void c1x1_sum_parts(int G, int N, const float* part, float* sums, float count, hipStream_t st, const float* invstd,
+                    float* gw, float* gb) {
+  hipLaunchKernelGGL(k_sum_parts, dim3((N + 63) / 64, 2), dim3(64 * kSumRows), 0, st, G, N, part, sums, count, invstd,
+                     gw, gb);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("c1x1_sum_parts: ") + hipGetErrorString(e));
 }

@@ -738,7 +738,7 @@ class _Conv1x1BNFn(torch.autograd.Function):
                     y2d = link.y.permute(0, 2, 3, 1).reshape(-1, c)
                     gx2d, part = conv_bn.c1x1(gy2d, w2d, resid=r2d, epi="bwd", by=y2d, bscale=link.scale,
                                               bshift=link.shift, bmean=link.mean, brelu=link.relu, b_trans=True)
-                    link.sums = conv_bn.sum_parts(part)
+                    link.take_part(part)
                 elif fast and conv_bn.supported(gy2d, w2d, resid=r2d is not None, b_trans=True):
                     gx2d, _ = conv_bn.c1x1(gy2d, w2d, resid=r2d, b_trans=True)
                 elif _own("resid" if r2d is not None else ("bwd" if _link_ok(link, c) else "plain")) and \
@@ -750,7 +750,7 @@ class _Conv1x1BNFn(torch.autograd.Function):
                         y2d = link.y.permute(0, 2, 3, 1).reshape(-1, c)
                         gx2d, part = conv_bn.gemm_bn(gy2d, wt, "bwd", by=y2d, bscale=link.scale, bshift=link.shift,
                                                      bmean=link.mean, brelu=link.relu, resid=r2d)
-                        link.sums = conv_bn.sum_parts(part)
+                        link.take_part(part)
                     else:
                         gx2d, _ = conv_bn.gemm_bn(gy2d, wt, "plain", resid=r2d)
                 elif r2d is not None:  # beta = 1 into the parked residual gradient (no output copy)
@@ -1010,7 +1010,7 @@ class _BNConvFn(torch.autograd.Function):
         y, conv_w, bn_w, mean, invstd, scale, shift, count = ctx.saved_tensors
         gy = gy.contiguous(memory_format=torch.channels_last)
         n, C, h, w = y.shape
-        sums = None
+        part = None
         wfn = lambda: _conv_wgrad(y, gy, ctx.R, conv_w, scale, shift, stride=ctx.stride)  # noqa: E731
         g_conv = None
         if ctx.R == 3 and ctx.stride == 2:
@@ -1026,21 +1026,18 @@ class _BNConvFn(torch.autograd.Function):
                 # the strip GEMM with this BatchNorm's backward sums in its epilogue (where it beats hipBLASLt)
                 dA2d, part = conv_bn.c1x1(gy2d, w2d, epi="bwd", by=y2d, bscale=scale, bshift=shift, bmean=mean,
                                           brelu=True, b_trans=True)
-                sums = conv_bn.sum_parts(part)
             elif _own("bwd") and conv_bn.gemm_bn_supported(gy2d, w2d.t()):
                 dA2d, part = conv_bn.gemm_bn(gy2d, _tr(w2d), "bwd", by=y2d, bscale=scale, bshift=shift,
                                              bmean=mean, brelu=True)
-                sums = conv_bn.sum_parts(part)
             else:
                 dA2d = torch.mm(gy2d, w2d)
             dA = dA2d.view(n, h, w, C).permute(0, 3, 1, 2)
         need_w = bn_w is not None and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3])
-        if sums is None:
+        if part is None:
             sums, gw, gb = syncbn.backward_reduce(dA, y, None, mean, invstd, scale, shift, True, bn_w, need_w, None)
         else:
-            gw = (sums[C:] * invstd).to(bn_w.dtype) if need_w else None
-            # a copy: `sums` is all-reduced in place below, the bias gradient stays this rank's own
-            gb = sums[:C].to(bn_w.dtype, copy=True) if need_w else None
+            # gb a separate tensor: `sums` is all-reduced in place below, the bias gradient stays this rank's own
+            sums, gw, gb = conv_bn.sum_parts_grads(part, invstd, bn_w, need_w)
         # the cross-rank exchange of the BatchNorm's backward sums runs (IPC side stream / async RCCL)
         # while the convolution's weight gradient -- which does not depend on it -- computes
         pending = _all_reduce_async(sums, ctx.process_group) if ctx.world > 1 else None
@@ -1241,28 +1238,28 @@ class _ConvBNResFn(torch.autograd.Function):
             lk = (l.y.permute(0, 2, 3, 1).reshape(-1, K), l.scale, l.shift, l.mean, l.relu)
         else:
             lk = None
-        s_i = None
+        s_i = part_i = None
         epi = "bwd" if lk is not None else "plain"
         kw = dict(epi=epi, by=lk[0], bscale=lk[1], bshift=lk[2], bmean=lk[3], brelu=lk[4]) if lk else {}
         nseg = _bnb_segments(g2d, W, epi)
         if nseg == 1:
             da2d, part = conv_bn.c1x1(g2d, W, b_trans=True, bnb=abd, bnb_y=y2d, **kw)
             if lk is not None:
-                s_i = conv_bn.sum_parts(part)
+                part_i = part
         elif nseg > 1:
             # split-K: the strip kernel keeps its B slice in LDS, so a wide gradient runs as column segments
-            # accumulated through the residual input; the BatchNorm-backward sums come with the last one
+            # accumulated through the residual input; the BatchNorm-backward sums come with the last one.
+            # The segments' (A, B, D) constants regrouped by one copy: [nseg][3][Ks]
             Ks = N // nseg
-            abd3 = abd.view(3, N)
+            abd_seg = abd.view(3, nseg, Ks).permute(1, 0, 2).contiguous()
             da2d = None
             for sgi in range(nseg):
                 cols = slice(sgi * Ks, (sgi + 1) * Ks)
-                bnb_s = abd3[:, cols].reshape(-1).contiguous()
                 last = sgi == nseg - 1
-                da2d, part = conv_bn.c1x1(g2d[:, cols], W[cols], b_trans=True, bnb=bnb_s, bnb_y=y2d[:, cols], lda=N,
-                                          resid=da2d, **(kw if last else {}))
+                da2d, part = conv_bn.c1x1(g2d[:, cols], W[cols], b_trans=True, bnb=abd_seg[sgi].reshape(-1),
+                                          bnb_y=y2d[:, cols], lda=N, resid=da2d, **(kw if last else {}))
             if lk is not None:
-                s_i = conv_bn.sum_parts(part)
+                part_i = part
         else:
             gx3, _ = syncbn.backward_dgrad(g, y, None, mean, invstd, bn_w, sums, count, None, None, False, False, None)
             gx3 = gx3.permute(0, 2, 3, 1).reshape(-1, N)
@@ -1271,7 +1268,9 @@ class _ConvBNResFn(torch.autograd.Function):
         gw_i = gb_i = None
         if ctx.pro:
             need_i = bn_in_w is not None and (ctx.needs_input_grad[3] or ctx.needs_input_grad[4])
-            if s_i is None:
+            if part_i is not None:  # sums and fp32 parameter gradients from one launch
+                s_i, gw_i, gb_i = conv_bn.sum_parts_grads(part_i, invstd_i, bn_in_w, need_i)
+            elif s_i is None:
                 s_i, gw_i, gb_i = syncbn.backward_reduce(da, src, None, mean_i, invstd_i, scale_i, shift_i, True,
                                                          bn_in_w, need_i, None)
             elif need_i:
@@ -1285,7 +1284,9 @@ class _ConvBNResFn(torch.autograd.Function):
             if not need_i:
                 gw_i = gb_i = None
         else:
-            if s_i is not None:
+            if part_i is not None:
+                cfg.link_in.take_part(part_i)
+            elif s_i is not None:
                 cfg.link_in.sums = s_i
             gx = da
         gz = g if cfg.bn_ds is None else None

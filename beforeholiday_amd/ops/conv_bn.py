@@ -154,6 +154,22 @@ def sum_parts(part: torch.Tensor, count: float = -1.0) -> torch.Tensor:
     return out
 
 
+def sum_parts_grads(part: torch.Tensor, invstd: torch.Tensor, weight: Optional[torch.Tensor], need: bool,
+                    count: float = -1.0):
+    """(sums, gw, gb) of a BatchNorm's backward: :func:`sum_parts` plus the parameter gradients gw = sum(dy
+    x_hat) = sums[N:] * invstd and gb = sum(dy) (a separate tensor: the sums may be all-reduced in place
+    later). fp32 parameters on the GPU get both from the summing launch itself; gw / gb are None when
+    ``need`` is False."""
+    n = part.size(2)
+    if need and part.is_cuda and weight is not None and weight.dtype == torch.float32:
+        sums, gw, gb = submodule("conv_bn").sum_parts_grads(part, float(count), invstd.contiguous())
+        return sums, gw, gb
+    sums = sum_parts(part, count)
+    if not need or weight is None:
+        return sums, None, None
+    return sums, (sums[n:2 * n] * invstd).to(weight.dtype), sums[:n].to(weight.dtype, copy=True)
+
+
 def gemm_bn(a: torch.Tensor, b: torch.Tensor, epi: str = "stats", kshift=None, by=None, bscale=None, bshift=None,
             bmean=None, brelu: bool = True, resid: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """``C = a @ b.T (+ resid)`` on the tiled MFMA GEMM (kernels/gemm.hip: ping-pong 256x256, 128x128 /

@@ -149,13 +149,23 @@ class BNLink(object):
     The BatchNorm's forward records its raw input ``y`` and per-channel ``scale / shift / mean``; the
     consuming convolution's backward reads them to reduce the BatchNorm's backward sums inside its
     data-gradient epilogue and leaves them in ``sums`` (``[sum_dz, sum_dz*(y-mean)]``, local to this
-    rank); the BatchNorm's backward then skips its own reduction pass over ``dA`` and ``y``."""
+    rank); the BatchNorm's backward then skips its own reduction pass over ``dA`` and ``y``. The forward also
+    records ``invstd`` and the BatchNorm ``weight``, so the launch that sums the epilogue partials can emit
+    the fp32 parameter gradients too (``grads`` = (gw, gb), ops.conv_bn.sum_parts_grads)."""
 
-    __slots__ = ("y", "scale", "shift", "mean", "relu", "sums")
+    __slots__ = ("y", "scale", "shift", "mean", "relu", "sums", "invstd", "weight", "grads")
 
     def __init__(self):
-        self.y = self.scale = self.shift = self.mean = self.sums = None
+        self.y = self.scale = self.shift = self.mean = self.sums = self.invstd = self.weight = self.grads = None
         self.relu = True
+
+    def take_part(self, part):
+        """Sum a consumer's epilogue partials into ``sums`` (+ ``grads`` for fp32 parameters that need them)."""
+        from ..ops import conv_bn as _cb
+
+        need = self.weight is not None and self.weight.requires_grad and self.invstd is not None
+        self.sums, gw, gb = _cb.sum_parts_grads(part, self.invstd, self.weight, need)
+        self.grads = (gw, gb) if gw is not None else None
 
 
 class SyncBatchnormFromStats(torch.autograd.Function):
@@ -189,7 +199,8 @@ class SyncBatchnormFromStats(torch.autograd.Function):
             out = syncbn.forward(input, z, scale, shift, fuse_relu, None, num_batches)
         if link is not None:
             link.y, link.scale, link.shift, link.mean, link.relu = input, scale, shift, mean, fuse_relu
-            link.sums = None
+            link.invstd, link.weight = invstd, weight
+            link.sums = link.grads = None
         ctx.save_for_backward(input, None if mask is not None else z, weight, mean, invstd, scale, shift, count_t, mask,
                               idx)
         ctx.pool = pool
@@ -210,16 +221,19 @@ class SyncBatchnormFromStats(torch.autograd.Function):
         need_w = weight is not None and (ctx.needs_input_grad[3] or ctx.needs_input_grad[4])
         if link is not None and link.sums is not None:
             sums = link.sums  # reduced by the consuming convolution's data-gradient epilogue
-            link.sums = None
+            grads, link.sums, link.grads = link.grads, None, None
             C = input.size(1)
-            gw = (sums[C:] * invstd).to(weight.dtype) if need_w else None
-            # a copy: `sums` is all-reduced in place below, the bias gradient stays this rank's own
-            gb = sums[:C].to(weight.dtype, copy=True) if need_w else None
+            if need_w and grads is not None:
+                gw, gb = grads  # from the summing launch (fp32 parameters)
+            else:
+                gw = (sums[C:] * invstd).to(weight.dtype) if need_w else None
+                # a copy: `sums` is all-reduced in place below, the bias gradient stays this rank's own
+                gb = sums[:C].to(weight.dtype, copy=True) if need_w else None
         else:
             sums, gw, gb = syncbn.backward_reduce(grad_output, input, z, mean, invstd, scale, shift, ctx.fuse_relu,
                                                   weight, need_w, mask)
         if link is not None:
-            link.y = None  # release the saved activation reference
+            link.y = link.invstd = link.weight = None  # release the saved references
         if ctx.world > 1:
             with comm_stats.timed("syncbn_bwd", sums):
                 _all_reduce(sums, ctx.process_group)
