@@ -125,9 +125,13 @@ def scale_loss(loss, optimizers, loss_id=0, model=None, delay_unscale=False, del
             for opt in optimizers:
                 opt._post_amp_backward(scaler)
                 opt._amp_stash.params_have_scaled_gradients = False
-            if scaler.device_mode:
-                scaler.fold_pass_into_step()
-            if not delay_overflow_check and scaler.update_scale():
+            if scaler.device_mode and not delay_overflow_check:
+                should_skip = scaler.fold_and_update_device()
+            else:
+                if scaler.device_mode:
+                    scaler.fold_pass_into_step()
+                should_skip = not delay_overflow_check and scaler.update_scale()
+            if should_skip:
                 msg = "Gradient overflow.  Skipping step, loss scaler {} reducing loss scale to {}".format(
                     loss_id, scaler.loss_scale())
                 for opt in optimizers:

@@ -194,6 +194,19 @@ class LossScaler(object):
         self._has_overflow = False
         self._overflow_buf.zero_()
 
+    def fold_and_update_device(self):
+        """Device mode: ``fold_pass_into_step`` + ``update_scale`` as ONE native launch (the ~10 tiny
+        torch ops they are otherwise). Returns False (never skips on the host)."""
+        from .._native import available, submodule
+
+        fn = getattr(submodule("amp_C"), "update_scale_device", None) if available() else None
+        if fn is None or not self._scale_dev.is_cuda:
+            self.fold_pass_into_step()
+            return self.update_scale()
+        fn(self._scale_dev, self._unskipped_dev, self._overflow_buf, self._step_flag, float(self._scale_factor),
+           int(self._scale_seq_len), float(self._min_loss_scale or 0.0), float(self._max_loss_scale))
+        return False
+
     def update_scale(self):
         if self.device_mode:
             # on the device: overflow -> scale / factor (>= min), counter 0; else counter + 1 and

@@ -269,6 +269,37 @@ void register_conv_bn(pybind11::module_& root) {
         py::arg("s2_scatter") = false, py::arg("bnb") = false);
   m.def("sum_parts", &sum_parts, py::arg("part"), py::arg("count") = -1.0);
   m.def("sum_parts_grads", &sum_parts_grads, py::arg("part"), py::arg("count"), py::arg("invstd"));
+  // x: NCHW-shaped channels_last 16-bit; returns the channels_last [n, c, h / 2, w / 2] stride-2 gather
+  m.def("s2_gather", [](at::Tensor x) {
+    TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.size(1) % 8 == 0 &&
+                    x.size(2) % 2 == 0 && x.size(3) % 2 == 0 && x.element_size() == 2,
+                "conv_bn.s2_gather: channels_last 16-bit [n, c, h, w] with c % 8 == 0 and even h, w");
+    auto q = at::empty({x.size(0), x.size(1), x.size(2) / 2, x.size(3) / 2},
+                       x.options().memory_format(at::MemoryFormat::ChannelsLast));
+    bh::s2_pixels(dtype_code(x.scalar_type()), x.data_ptr(), q.data_ptr(), x.size(0), (int)q.size(2), (int)q.size(3),
+                  (int)x.size(1), false, stream_for(x));
+    return q;
+  }, py::arg("x"));
+  m.def("pool_broadcast", [](at::Tensor g, int64_t h, int64_t w, double scale) {
+    TORCH_CHECK(g.is_cuda() && g.dim() == 2 && g.is_contiguous() && g.size(1) % 8 == 0 && g.element_size() == 2,
+                "conv_bn.pool_broadcast: contiguous 16-bit [n, c] with c % 8 == 0");
+    auto out = at::empty({g.size(0), g.size(1), h, w}, g.options().memory_format(at::MemoryFormat::ChannelsLast));
+    bh::pool_bcast(dtype_code(g.scalar_type()), g.data_ptr(), out.data_ptr(), g.size(0), h * w, (int)g.size(1),
+                   (float)scale, stream_for(g));
+    return out;
+  }, py::arg("g"), py::arg("h"), py::arg("w"), py::arg("scale"),
+     "channels_last [n, c, h, w] = g[n, c] * scale: the global-average-pool backward in one vectorised pass");
+  // full [n * h * w, c] (+)= quarter [n * h/2 * w/2, c] at the even pixels, in place; returns full
+  m.def("s2_scatter_add", [](at::Tensor full, at::Tensor quarter, int64_t n, int64_t h, int64_t w) {
+    TORCH_CHECK(full.is_cuda() && quarter.is_cuda() && full.is_contiguous() && quarter.is_contiguous() &&
+                    full.scalar_type() == quarter.scalar_type() && full.element_size() == 2 && full.dim() == 2 &&
+                    quarter.dim() == 2 && full.size(1) == quarter.size(1) && full.size(1) % 8 == 0 && h % 2 == 0 &&
+                    w % 2 == 0 && full.size(0) == n * h * w && quarter.size(0) == n * (h / 2) * (w / 2),
+                "conv_bn.s2_scatter_add: contiguous 16-bit [n*h*w, c] and [n*h/2*w/2, c], c % 8 == 0");
+    bh::s2_pixels(dtype_code(full.scalar_type()), full.data_ptr(), quarter.data_ptr(), n, (int)(h / 2), (int)(w / 2),
+                  (int)full.size(1), true, stream_for(full));
+    return full;
+  }, py::arg("full"), py::arg("quarter"), py::arg("n"), py::arg("h"), py::arg("w"));
   m.def("gemm_bn", &gemm_bn, py::arg("a"), py::arg("b"), py::arg("epi"), py::arg("kshift") = py::none(),
         py::arg("by") = py::none(), py::arg("bscale") = py::none(), py::arg("bshift") = py::none(),
         py::arg("bmean") = py::none(), py::arg("brelu") = true, py::arg("resid") = py::none());

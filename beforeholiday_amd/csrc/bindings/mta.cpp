@@ -708,6 +708,18 @@ void register_amp_C(pybind11::module_& root) {
     g_plans.clear();
   }, "drop the cached device-resident chunk plans (registered with atexit by the python package)");
   m.def("multi_tensor_scale", &multi_tensor_scale, "out = in * scale with overflow flag");
+  m.def("update_scale_device", [](at::Tensor scale, at::Tensor unskipped, at::Tensor overflow,
+                                  c10::optional<at::Tensor> step_flag, double factor, int64_t window, double min_scale,
+                                  double max_scale) {
+    TORCH_CHECK(scale.is_cuda() && scale.scalar_type() == at::kFloat && unskipped.scalar_type() == at::kInt &&
+                    overflow.scalar_type() == at::kInt && (!step_flag || step_flag->scalar_type() == at::kInt),
+                "update_scale_device: fp32 scale, int32 counter / flags on the GPU");
+    bh::amp_update_scale(scale.data_ptr<float>(), unskipped.data_ptr<int>(), overflow.data_ptr<int>(),
+                         step_flag ? step_flag->data_ptr<int>() : nullptr, (float)factor, (int)window, (float)min_scale,
+                         (float)max_scale, stream_for(scale));
+  }, py::arg("scale"), py::arg("unskipped"), py::arg("overflow"), py::arg("step_flag"), py::arg("factor"),
+     py::arg("window"), py::arg("min_scale"), py::arg("max_scale"),
+     "amp's device loss-scale bookkeeping of one backward pass in one launch");
   m.def("multi_tensor_scale_tensor", &multi_tensor_scale_tensor, "out = in * scale[0] (device scalar)");
   m.def("multi_tensor_sgd", &multi_tensor_sgd, "fused SGD");
   m.def("multi_tensor_axpby", &multi_tensor_axpby, "out = a*x + b*y with overflow flag");

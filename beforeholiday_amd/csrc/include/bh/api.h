@@ -126,4 +126,8 @@ void mta_lamb_stage2_standalone(const MTAView& v, int dt_p, int dt_u, const floa
                                 const float* unorm, float lr, float decay, bool use_nvlamb,
                                 hipStream_t s);
 
+// amp device loss scale: step_flag |= overflow; then the dynamic-scale update (see multi_tensor.hip)
+void amp_update_scale(float* scale, int* unskipped, const int* overflow, int* step_flag, float factor, int window,
+                      float min_scale, float max_scale, hipStream_t s);
+
 }  // namespace bh

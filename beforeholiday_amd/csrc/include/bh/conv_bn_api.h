@@ -81,4 +81,11 @@ void c1x1_run(int dt, const C1x1Args& a, hipStream_t st);
 void c1x1_sum_parts(int G, int N, const float* part, float* sums, float count, hipStream_t st,
                     const float* invstd = nullptr, float* gw = nullptr, float* gb = nullptr);
 
+// stride-2 pixels of an NHWC tensor full [n, 2 ho, 2 wo, c] <-> quarter [n, ho, wo, c] (16-bit, c % 8 == 0):
+// add = false: quarter = full[:, ::2, ::2]; add = true: full[:, ::2, ::2] += quarter
+void s2_pixels(int dt, void* full, void* quarter, int64_t n, int ho, int wo, int c, bool add, hipStream_t st);
+
+// out (channels_last [n, c, h, w], 16-bit) = g [n, c] * scale broadcast over the hw pixels (c % 8 == 0)
+void pool_bcast(int dt, const void* g, void* out, int64_t n, int64_t hw, int c, float scale, hipStream_t st);
+
 }  // namespace bh

@@ -668,4 +668,87 @@ void c1x1_sum_parts(int G, int N, const float* part, float* sums, float count, h
   if (e != hipSuccess) throw std::runtime_error(std::string("c1x1_sum_parts: ") + hipGetErrorString(e));
 }
 
+// ---- stride-2 pixel gather / scatter-add for the 1x1 stride-2 convolutions (NHWC, 16-bit) ----------------
+// out[n, yo, xo, :] = x[n, 2 yo, 2 xo, :] and full[n, 2 yo, 2 xo, :] += q[n, yo, xo, :]: one thread per 16-byte
+// channel chunk of a quarter-resolution pixel, so every access is a whole 16-byte vector (torch's strided
+// copy / add_ over the same views moved ~1.3 TB/s)
+namespace {
+template <typename T, bool ADD>
+__global__ __launch_bounds__(256) void k_s2_pixels(T* __restrict__ full, T* __restrict__ quarter, int64_t npix_q,
+                                                   int Ho, int Wo, int C8) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= npix_q * C8) return;
+  const int64_t pq = i / C8;
+  const int c8 = (int)(i - pq * C8);
+  const int64_t n = pq / ((int64_t)Ho * Wo);
+  const int rem = (int)(pq - n * Ho * Wo), yo = rem / Wo, xo = rem - yo * Wo;
+  const int64_t pf = (n * (2 * Ho) + 2 * yo) * (int64_t)(2 * Wo) + 2 * xo;
+  typedef T t8 __attribute__((ext_vector_type(8)));
+  t8* fp = reinterpret_cast<t8*>(full + pf * C8 * 8) + c8;
+  t8* qp = reinterpret_cast<t8*>(quarter + pq * C8 * 8) + c8;
+  if constexpr (ADD) {
+    t8 a = *fp;
+    const t8 b = *qp;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = from_f<T>(to_f<T>(a[j]) + to_f<T>(b[j]));
+    *fp = a;
+  } else {
+    *qp = *fp;
+  }
+}
+}  // namespace
+
+void s2_pixels(int dt, void* full, void* quarter, int64_t n, int ho, int wo, int c, bool add, hipStream_t st) {
+  if (c % 8) throw std::runtime_error("s2_pixels: channels must be a multiple of 8");
+  const int64_t npix = n * ho * wo, work = npix * (c / 8);
+  if (work == 0) return;
+  const dim3 grid((unsigned)((work + 255) / 256));
+  switch (dt) {
+    case kF16:
+      if (add) hipLaunchKernelGGL((k_s2_pixels<f16, true>), grid, dim3(256), 0, st, (f16*)full, (f16*)quarter, npix, ho, wo, c / 8);
+      else hipLaunchKernelGGL((k_s2_pixels<f16, false>), grid, dim3(256), 0, st, (f16*)full, (f16*)quarter, npix, ho, wo, c / 8);
+      break;
+    case kBF16:
+      if (add) hipLaunchKernelGGL((k_s2_pixels<bf16, true>), grid, dim3(256), 0, st, (bf16*)full, (bf16*)quarter, npix, ho, wo, c / 8);
+      else hipLaunchKernelGGL((k_s2_pixels<bf16, false>), grid, dim3(256), 0, st, (bf16*)full, (bf16*)quarter, npix, ho, wo, c / 8);
+      break;
+    default: throw std::runtime_error("s2_pixels: fp16 / bf16 only");
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("s2_pixels: ") + hipGetErrorString(e));
+}
+
+// global-average-pool backward: out[n, y, x, :] = g[n, :] * scale for a channels_last [n, c, h, w] output, one
+// 16-byte chunk per thread (torch's expand + contiguous copy from the stride-0 view ran ~1.4 TB/s)
+namespace {
+template <typename T>
+__global__ __launch_bounds__(256) void k_pool_bcast(const T* __restrict__ g, T* __restrict__ out, int64_t hw, int C8,
+                                                    int64_t total, float scale) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int64_t p = i / C8;
+  const int c8 = (int)(i - p * C8);
+  const int64_t n = p / hw;
+  typedef T t8 __attribute__((ext_vector_type(8)));
+  t8 v = *(reinterpret_cast<const t8*>(g + n * C8 * 8) + c8);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = from_f<T>(to_f<T>(v[j]) * scale);
+  *(reinterpret_cast<t8*>(out) + i) = v;
+}
+}  // namespace
+
+void pool_bcast(int dt, const void* g, void* out, int64_t n, int64_t hw, int c, float scale, hipStream_t st) {
+  if (c % 8) throw std::runtime_error("pool_bcast: channels must be a multiple of 8");
+  const int64_t total = n * hw * (c / 8);
+  if (total == 0) return;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  switch (dt) {
+    case kF16: hipLaunchKernelGGL(k_pool_bcast<f16>, grid, dim3(256), 0, st, (const f16*)g, (f16*)out, hw, c / 8, total, scale); break;
+    case kBF16: hipLaunchKernelGGL(k_pool_bcast<bf16>, grid, dim3(256), 0, st, (const bf16*)g, (bf16*)out, hw, c / 8, total, scale); break;
+    default: throw std::runtime_error("pool_bcast: fp16 / bf16 only");
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("pool_bcast: ") + hipGetErrorString(e));
+}
+
 }  // namespace bh

@@ -703,4 +703,41 @@ void upload_bytes(void* dst, const void* src, size_t bytes, hipStream_t s) {
   if (e != hipSuccess) throw std::runtime_error(std::string("upload_bytes: ") + hipGetErrorString(e));
 }
 
+// ------------------------------------------------------------------------------------
+// amp's device-resident dynamic loss scale, one backward pass's bookkeeping in one launch (reference
+// semantics: apex/amp/scaler.py:197-226): fold the pass's overflow flag into the step flag, then
+// overflow -> scale / factor (>= min), counter 0; else counter + 1 and scale * factor (<= max) when the
+// counter reaches the window (then counter 0). Replaces ~10 tiny torch ops per step.
+// ------------------------------------------------------------------------------------
+namespace {
+__global__ void k_update_scale(float* scale, int* unskipped, const int* overflow, int* step_flag, float factor,
+                               int window, float min_scale, float max_scale) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const bool ov = *overflow > 0;
+  if (step_flag && ov) *step_flag = 1;
+  const float s = *scale;
+  if (ov) {
+    float d = s / factor;
+    if (min_scale > 0.f) d = fmaxf(d, min_scale);
+    *scale = d;
+    *unskipped = 0;
+    return;
+  }
+  const int cnt = *unskipped + 1;
+  if (cnt >= window) {
+    *scale = fminf(s * factor, max_scale);
+    *unskipped = 0;
+  } else {
+    *unskipped = cnt;
+  }
+}
+}  // namespace
+
+void amp_update_scale(float* scale, int* unskipped, const int* overflow, int* step_flag, float factor, int window,
+                      float min_scale, float max_scale, hipStream_t s) {
+  hipLaunchKernelGGL(k_update_scale, dim3(1), dim3(64), 0, s, scale, unskipped, overflow, step_flag, factor, window,
+                     min_scale, max_scale);
+  check_launch("amp_update_scale");
+}
+
 }  // namespace bh

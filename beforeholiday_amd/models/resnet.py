@@ -529,6 +529,10 @@ class _GlobalAvgPoolFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         n, c, h, w = ctx.shape
+        if g.is_cuda and g.dtype in (torch.float16, torch.bfloat16) and c % 8 == 0:
+            from .._native import submodule
+
+            return submodule("conv_bn").pool_broadcast(g.contiguous(), h, w, 1.0 / (h * w))
         return (g / (h * w)).view(n, c, 1, 1).expand(n, c, h, w).contiguous(memory_format=torch.channels_last)
 
 
@@ -782,7 +786,7 @@ def _c1x1_forward_stats(x, weight, kshift, s2):
         y2d, part = conv_bn.c1x1(a2d, w2d, s2=hw, epi="stats", kshift=kshift)
         return y2d.view(n, ho, wo, k).permute(0, 3, 1, 2), part
     if s2:
-        a2d = x[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, c)
+        a2d = conv_bn.s2_gather(x).permute(0, 2, 3, 1).reshape(-1, c)
     if _own("fwd") and conv_bn.gemm_bn_supported(a2d, w2d) and not (c <= 256 and k >= 1024):
         # the MFMA-bound layers (K or N >= 512, or the small 14x14 / 7x7 grids): the tiled MFMA GEMM
         # with the statistics epilogue (kernels/gemm.hip; the ping-pong 256x256 kernel from 160 tiles),
@@ -866,8 +870,7 @@ class _Conv1DsFn(torch.autograd.Function):
                         gdx = conv_bn.gemm_bn(gd, _tr(wd_2d), "plain")[0]
                     else:
                         gdx = torch.mm(gd, wd_2d)
-                    # add_ on the strided view: `view[idx] += t` would also copy the view onto itself
-                    gx2d.view(n, h, w, c)[:, ::2, ::2, :].add_(gdx.view(n, h // 2, w // 2, c))
+                    conv_bn.s2_scatter_add(gx2d, gdx, n, h, w)
             elif conv_bn.preferred(kd, c, gd.size(0)) and conv_bn.supported(gd, wd_2d, resid=True, b_trans=True):
                 gx2d, _ = conv_bn.c1x1(gd, wd_2d, resid=gx2d, b_trans=True)
             elif _own("resid") and conv_bn.gemm_bn_supported(gd, wd_2d.t(), resid=True):
@@ -903,8 +906,7 @@ def _ds_dgrad_folded(gx2d, dsb, s2, shape):
     gxd = syncbn.backward_dgrad(g4, y4, None, mean, invstd, weight, sums, count, None, None, False, False, None)[0]
     gxd = gxd.permute(0, 2, 3, 1).reshape(-1, kd)
     if s2:
-        gx2d.view(n, h, w, c)[:, ::2, ::2, :].add_(torch.mm(gxd, Wd).view(n, h // 2, w // 2, c))
-        return gx2d
+        return conv_bn.s2_scatter_add(gx2d, torch.mm(gxd, Wd), n, h, w)
     return torch.addmm(gx2d, gxd, Wd, out=gx2d)
 
 

@@ -170,6 +170,26 @@ def sum_parts_grads(part: torch.Tensor, invstd: torch.Tensor, weight: Optional[t
     return sums, (sums[n:2 * n] * invstd).to(weight.dtype), sums[:n].to(weight.dtype, copy=True)
 
 
+def s2_gather(x: torch.Tensor) -> torch.Tensor:
+    """``x[:, :, ::2, ::2]`` of a channels_last NCHW-shaped tensor as a channels_last tensor (16-byte vector
+    accesses on the GPU; torch's strided copy otherwise)."""
+    if (x.is_cuda and x.dtype in (torch.float16, torch.bfloat16) and x.size(1) % 8 == 0 and x.size(2) % 2 == 0
+            and x.size(3) % 2 == 0 and x.is_contiguous(memory_format=torch.channels_last)):
+        return submodule("conv_bn").s2_gather(x)
+    return x[:, :, ::2, ::2].contiguous(memory_format=torch.channels_last)
+
+
+def s2_scatter_add(full2d: torch.Tensor, quarter2d: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
+    """``full[n, h, w, c]`` (as ``[n*h*w, c]``) += ``quarter`` at the even pixels, in place."""
+    c = full2d.size(1)
+    if (full2d.is_cuda and full2d.dtype in (torch.float16, torch.bfloat16) and c % 8 == 0 and h % 2 == 0
+            and w % 2 == 0 and full2d.is_contiguous() and quarter2d.is_contiguous()
+            and quarter2d.dtype == full2d.dtype):
+        return submodule("conv_bn").s2_scatter_add(full2d, quarter2d, n, h, w)
+    full2d.view(n, h, w, c)[:, ::2, ::2, :].add_(quarter2d.view(n, h // 2, w // 2, c))
+    return full2d
+
+
 def gemm_bn(a: torch.Tensor, b: torch.Tensor, epi: str = "stats", kshift=None, by=None, bscale=None, bshift=None,
             bmean=None, brelu: bool = True, resid: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """``C = a @ b.T (+ resid)`` on the tiled MFMA GEMM (kernels/gemm.hip: ping-pong 256x256, 128x128 /

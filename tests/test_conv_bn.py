@@ -343,3 +343,37 @@ def test_c1x1_large_m(KN, epi, dt):
     torch.testing.assert_close(c.float(), af @ b.float().t(), **_tol(dt))
     d = c.float() - kshift
     _stats_close(conv_bn.sum_parts(part, M)[:2 * N].cpu(), torch.cat([d.sum(0), (d * d).sum(0)]).cpu(), M)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_s2_gather_scatter_add(dtype):
+    """The 16-byte-vector stride-2 pixel gather / scatter-add of the 1x1 stride-2 convolutions vs torch's
+    strided views (bitwise: one add per element)."""
+    from beforeholiday_amd.ops import conv_bn
+
+    torch.manual_seed(0)
+    x = torch.randn(3, 40, 14, 10, device="cuda", dtype=dtype).contiguous(memory_format=torch.channels_last)
+    q = conv_bn.s2_gather(x)
+    assert q.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(q, x[:, :, ::2, ::2])
+    full = torch.randn(3 * 14 * 10, 40, device="cuda", dtype=dtype)
+    quarter = torch.randn(3 * 7 * 5, 40, device="cuda", dtype=dtype)
+    ref = full.clone()
+    ref.view(3, 14, 10, 40)[:, ::2, ::2, :].add_(quarter.view(3, 7, 5, 40))
+    out = conv_bn.s2_scatter_add(full, quarter, 3, 14, 10)
+    assert out.data_ptr() == full.data_ptr() and torch.equal(out, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_pool_broadcast(dtype):
+    """The global-average-pool backward kernel vs torch's expand + channels_last copy (fp32 scale, one
+    rounding, so equal to rounding of g / hw)."""
+    from beforeholiday_amd._native import submodule
+
+    g = torch.randn(5, 48, device="cuda", dtype=dtype)
+    out = submodule("conv_bn").pool_broadcast(g, 7, 3, 1.0 / 21)
+    ref = (g.float() / 21).view(5, 48, 1, 1).expand(5, 48, 7, 3)
+    assert out.is_contiguous(memory_format=torch.channels_last) and out.shape == (5, 48, 7, 3)
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=1e-3)
