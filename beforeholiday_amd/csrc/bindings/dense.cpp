@@ -226,7 +226,10 @@ std::vector<at::Tensor> linear_dact(const at::Tensor& dy, const at::Tensor& wt, 
     }
     return db;
   };
-  if (aux_ok && mfma_ok(dy, wt, dx) &&
+  // a plain data gradient (no activation derivative, no bias gradient) has no epilogue to fuse: the library
+  // GEMM measured 1.0-1.18x faster there (profiles/dgrad_transformer_nt_vs_hipblaslt.jsonl)
+  const bool fused_work = act != bh::kActNone || want_bgrad || g_force_mfma;
+  if (fused_work && aux_ok && mfma_ok(dy, wt, dx) &&
       prefer_mfma("linear_dact", dy, dy.size(0), wt.size(0), dy.size(1), act * 2 + (want_bgrad ? 1 : 0), run_mfma,
                   run_lib)) {
     return {dx, run_mfma()};
@@ -240,7 +243,8 @@ std::vector<at::Tensor> linear_dact(const at::Tensor& dy, const at::Tensor& wt, 
 at::Tensor linear_bias_forward(at::Tensor input, at::Tensor weight, at::Tensor bias) {
   check_cuda(input, "input");
   auto x = as2d(input.contiguous());
-  auto y = bias.defined() ? at::addmm(bias, x, weight.t()) : at::mm(x, weight.t());
+  // the MFMA GEMM with the bias in its epilogue where the static rule picks it (linear_act), else addmm
+  auto y = linear_act(x, weight.contiguous(), bias.defined() ? bias.contiguous() : bias, bh::kActNone, false)[0];
   auto shape = input.sizes().vec();
   shape.back() = weight.size(0);
   return y.view(shape);
@@ -261,7 +265,7 @@ std::vector<at::Tensor> linear_gelu_linear_forward(at::Tensor input, at::Tensor 
   auto x = as2d(input.contiguous());
   auto h = linear_act(x, weight1.contiguous(), bias1.contiguous(), bh::kActGelu, true);
   auto gelu_in = h[1], out1 = h[0];
-  auto out2 = at::addmm(bias2, out1, weight2.t());
+  auto out2 = linear_act(out1, weight2.contiguous(), bias2.contiguous(), bh::kActNone, false)[0];
   return {gelu_in, out1, out2};
 }
 
