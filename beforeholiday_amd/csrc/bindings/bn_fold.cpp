@@ -69,28 +69,20 @@ std::vector<at::Tensor> fold_reduce(const at::Tensor& W, const at::Tensor& p_ws,
   TORCH_CHECK(half_2d(W), "bn_fold.fold_reduce: W must be a contiguous fp16/bf16 [N, K] tensor");
   const int64_t N = W.size(0), K = W.size(1);
   TORCH_CHECK(p_ws.dim() == 2 && p_ws.size(1) == N * K && g_ws.dim() == 3 && g_ws.size(1) == K && g_ws.size(2) == K &&
-                  sa_ws.dim() == 2 && sa_ws.size(1) == K && sg_ws.dim() == 2 && sg_ws.size(1) == N,
+                  sa_ws.dim() == 2 && sa_ws.size(1) == K && sa_ws.size(0) == g_ws.size(0) && sg_ws.dim() == 2 &&
+                  sg_ws.size(1) == N,
               "bn_fold.fold_reduce: partial shapes");
   for (const at::Tensor* t : {&p_ws, &g_ws, &sa_ws, &sg_ws}) check_f32(*t, t->numel(), "partials");
   check_f32(mean, N, "mean");
   check_f32(invstd, N, "invstd");
   auto o = W.options().dtype(at::kFloat);
-  auto P = at::empty({N, K}, o), Gm = at::empty({K, K}, o), Sa = at::empty({K}, o), Sg = at::empty({N}, o);
-  bh::SumPartials sp;
-  const at::Tensor* parts[4] = {&p_ws, &g_ws, &sa_ws, &sg_ws};
-  at::Tensor* outs[4] = {&P, &Gm, &Sa, &Sg};
-  for (int i = 0; i < 4; ++i) {
-    sp.part[i] = parts[i]->data_ptr<float>();
-    sp.out[i] = outs[i]->data_ptr<float>();
-    sp.rows[i] = parts[i]->size(0);
-    sp.cols[i] = outs[i]->numel();
-  }
-  hipStream_t st = stream_for(W);
-  bh::sum_partials(sp, st);
+  auto P = at::empty({N, K}, o), Gm = at::empty({K, K}, o), Sa = at::empty({K}, o);
   auto sums = at::empty({2 * N}, o), bn_grads = at::empty({2 * N}, o);
-  bh::fold_sums(dtype_code(W.scalar_type()), W.data_ptr(), P.data_ptr<float>(), Sg.data_ptr<float>(),
-                mean.data_ptr<float>(), invstd.data_ptr<float>(), (int)N, (int)K, sums.data_ptr<float>(),
-                bn_grads.data_ptr<float>(), st);
+  bh::fold_reduce(dtype_code(W.scalar_type()), W.data_ptr(), p_ws.data_ptr<float>(), (int)p_ws.size(0),
+                  g_ws.data_ptr<float>(), sa_ws.data_ptr<float>(), (int)g_ws.size(0), sg_ws.data_ptr<float>(),
+                  (int)sg_ws.size(0), mean.data_ptr<float>(), invstd.data_ptr<float>(), (int)N, (int)K,
+                  P.data_ptr<float>(), Gm.data_ptr<float>(), Sa.data_ptr<float>(), sums.data_ptr<float>(),
+                  bn_grads.data_ptr<float>(), stream_for(W));
   return {P, Gm, Sa, sums, bn_grads};
 }
 
@@ -114,16 +106,11 @@ std::vector<at::Tensor> fold_finish(const at::Tensor& W, const at::Tensor& sums,
     check_f32(*weight, N, "weight");
     wp = weight->data_ptr<float>();
   }
-  auto o = W.options().dtype(at::kFloat);
-  const int dt = dtype_code(W.scalar_type());
-  hipStream_t st = stream_for(W);
-  auto abd = at::empty({3 * N}, o), BW = at::empty({N, K}, o);
-  bh::fold_coef(dt, W.data_ptr(), sums.data_ptr<float>(), count.data_ptr<float>(), mean.data_ptr<float>(),
-                invstd.data_ptr<float>(), wp, (int)N, (int)K, abd.data_ptr<float>(), BW.data_ptr<float>(), st);
-  auto X = at::mm(BW, Gm.view({K, K}));  // [N, K] = (B W) Gm, fp32
+  auto abd = at::empty({3 * N}, W.options().dtype(at::kFloat));
   auto dW = at::empty({N, K}, W.options());
-  bh::fold_final(dt, abd.data_ptr<float>(), P.data_ptr<float>(), X.data_ptr<float>(), Sa.data_ptr<float>(), (int)N,
-                 (int)K, dW.data_ptr(), st);
+  bh::fold_finish(dtype_code(W.scalar_type()), W.data_ptr(), sums.data_ptr<float>(), count.data_ptr<float>(),
+                  mean.data_ptr<float>(), invstd.data_ptr<float>(), wp, P.data_ptr<float>(), Gm.data_ptr<float>(),
+                  Sa.data_ptr<float>(), (int)N, (int)K, abd.data_ptr<float>(), dW.data_ptr(), stream_for(W));
   return {dW, abd};
 }
 

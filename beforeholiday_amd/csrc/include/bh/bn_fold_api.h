@@ -32,24 +32,17 @@ int mask_colsum_splits(int64_t M, int N);
 void mask_colsum(int dt, const void* g, const uint8_t* bits, void* g_pre, int64_t M, int N, float* colsum_part,
                  hipStream_t st);
 
-// ---- combine (one block's small-matrix algebra; see ops/bn_fold.py `FoldCombine`) ----
-// Sum the rows of up to four fp32 partial arrays part[i] [rows[i]][cols[i]] into out[i] [cols[i]] (fixed order).
-struct SumPartials {
-  const float* part[4] = {nullptr, nullptr, nullptr, nullptr};
-  float* out[4] = {nullptr, nullptr, nullptr, nullptr};
-  int64_t rows[4] = {0, 0, 0, 0}, cols[4] = {0, 0, 0, 0};
-};
-void sum_partials(const SumPartials& s, hipStream_t st);
-// sums[2N] = [Sg, rowdot(W, P) - mean * Sg] (this rank's) and bn_grads[2N] = [sums[N:] * invstd, sums[:N]]
-// (the BatchNorm's local weight / bias gradients, fp32); W [N, K] 16-bit
-void fold_sums(int dt, const void* W, const float* P, const float* Sg, const float* mean, const float* invstd, int N,
-               int K, float* sums, float* bn_grads, hipStream_t st);
-// from the (all-reduced) sums: abd[3N] = (A, B, D) -- the BatchNorm input gradient is A g + B y + D --
-// and BW [N, K] fp32 = B W   (weight may be null = 1)
-void fold_coef(int dt, const void* W, const float* sums, const float* count, const float* mean, const float* invstd,
-               const float* weight, int N, int K, float* abd, float* BW, hipStream_t st);
-// dW [N, K] 16-bit = A P + X + D (x) Sa   (X = (B W) Gm)
-void fold_final(int dt, const float* abd, const float* P, const float* X, const float* Sa, int N, int K, void* dW,
-                hipStream_t st);
+// ---- combine (ops/bn_fold.py: the small-matrix algebra, one launch per stage) ----
+// stage 1: P [N, K] = sum of the S1 rows of p_ws [S1, N K] (the fp32 weight-gradient partials), Gm [K, K] and
+// Sa [K] from g_ws [S2, K K] / sa_ws [S2, K], Sg = sum of the S3 rows of sg_ws [S3, N]; then this rank's
+// sums [2N] = [Sg, rowdot(W, P) - mean Sg] and bn_grads [2N] = [sums[N:] invstd, Sg] (fixed-order sums)
+void fold_reduce(int dt, const void* W, const float* p_ws, int S1, const float* g_ws, const float* sa_ws, int S2,
+                 const float* sg_ws, int S3, const float* mean, const float* invstd, int N, int K, float* P, float* Gm,
+                 float* Sa, float* sums, float* bn_grads, hipStream_t st);
+// stage 2, from the (all-reduced) sums: abd [3N] = (A, B, D) -- the BatchNorm input gradient is A g + B y + D --
+// and dW [N, K] (W's 16-bit type) = A P + (B W) Gm + D (x) Sa   (weight may be null = 1)
+void fold_finish(int dt, const void* W, const float* sums, const float* count, const float* mean, const float* invstd,
+                 const float* weight, const float* P, const float* Gm, const float* Sa, int N, int K, float* abd,
+                 void* dW, hipStream_t st);
 
 }  // namespace bh

@@ -275,86 +275,125 @@ __global__ __launch_bounds__(kThreads) void k_mask_colsum(const T* __restrict__ 
 // ------------------------------------------------------------------------------------------------
 // combine kernels (ops/bn_fold.py FoldCombine)
 
-constexpr int kSumLanes = 16;  // split-lanes per 64-column block of sum_partials
+// fold_reduce in one launch. Blocks [0, N): row n of P = sum of the S1 weight-gradient partial rows (CW columns x
+// L lanes over the rows, merged in lane order), Sg[n], and from them the row's sums and BatchNorm gradients:
+//   sums[n] = Sg[n], sums[N + n] = W[n] . P[n] - mean[n] Sg[n], bn_grads = (sums[N + n] invstd[n], Sg[n]).
+// Blocks [N, ..): 64-column chunks of Gm (K x K) and Sa (K), 4 lanes over their S2 partial rows.
+// Every sum runs in a fixed order: deterministic.
+constexpr int kFoldThreads = 256;
 
-__global__ __launch_bounds__(64 * kSumLanes) void k_sum_partials(SumPartials s, int b1, int b2, int b3) {
-  // blocks [0, b1) -> array 0, [b1, b2) -> 1, [b2, b3) -> 2, [b3, ..) -> 3; 64 columns per block, kSumLanes
-  // lanes over the rows (8 loads in flight each), merged in lane order through LDS
-  __shared__ float sh[kSumLanes][64];
-  const int b = blockIdx.x;
-  const int i = b < b1 ? 0 : (b < b2 ? 1 : (b < b3 ? 2 : 3));
-  const int lb = b - (i == 0 ? 0 : (i == 1 ? b1 : (i == 2 ? b2 : b3)));
-  const float* part = s.part[i];
-  const int64_t rows = s.rows[i], cols = s.cols[i];
-  const int cl = threadIdx.x & 63, lane = threadIdx.x >> 6;
-  const int64_t c = (int64_t)lb * 64 + cl;
-  float acc = 0.f;
-  if (c < cols) {
-    int64_t r = lane;
-    for (; r + 7 * kSumLanes < rows; r += 8 * kSumLanes) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[(r + u * kSumLanes) * cols + c];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc += v[u];
+template <typename T>
+__global__ __launch_bounds__(kFoldThreads) void k_fold_reduce(const T* __restrict__ W, const float* __restrict__ p_ws,
+                                                              int S1, const float* __restrict__ g_ws,
+                                                              const float* __restrict__ sa_ws, int S2,
+                                                              const float* __restrict__ sg_ws, int S3,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ invstd, int N, int K,
+                                                              float* __restrict__ P, float* __restrict__ Gm,
+                                                              float* __restrict__ Sa, float* __restrict__ sums,
+                                                              float* __restrict__ bn_grads) {
+  __shared__ float red[kFoldThreads];
+  const int tid = threadIdx.x, b = blockIdx.x;
+  if (b < N) {
+    const int n = b;
+    const int CW = K < kFoldThreads ? K : kFoldThreads, L = kFoldThreads / CW;
+    const int c = tid % CW, l = tid / CW;
+    const int64_t NK = (int64_t)N * K;
+    float d = 0.f;
+    for (int k0 = 0; k0 < K; k0 += CW) {
+      const int k = k0 + c;
+      float a = 0.f;
+      if (l < L && k < K) {
+        const float* src = p_ws + (int64_t)n * K + k;
+        int s = l;
+        for (; s + 3 * L < S1; s += 4 * L) {
+          const float u0 = src[s * NK], u1 = src[(s + L) * NK], u2 = src[(s + 2 * L) * NK], u3 = src[(s + 3 * L) * NK];
+          a += u0;
+          a += u1;
+          a += u2;
+          a += u3;
+        }
+        for (; s < S1; s += L) a += src[s * NK];
+      }
+      red[tid] = a;
+      __syncthreads();
+      if (l == 0 && k < K) {
+        float t = 0.f;
+        for (int q = 0; q < L; ++q) t += red[q * CW + c];
+        P[(int64_t)n * K + k] = t;
+        d = fmaf(to_f<T>(W[(int64_t)n * K + k]), t, d);
+      }
+      __syncthreads();
     }
-    for (; r < rows; r += kSumLanes) acc += part[r * cols + c];
+    float sg = 0.f;
+    for (int s = tid; s < S3; s += kFoldThreads) sg += sg_ws[(int64_t)s * N + n];
+    d = block_sum(d, red);
+    sg = block_sum(sg, red);
+    if (tid == 0) {
+      const float s2 = d - mean[n] * sg;
+      sums[n] = sg;
+      sums[N + n] = s2;
+      bn_grads[n] = s2 * invstd[n];
+      bn_grads[N + n] = sg;
+    }
+    return;
   }
-  sh[lane][cl] = acc;
+  // Gm / Sa chunks: 64 columns x 4 lanes over the S2 rows
+  const int nbG = (K * K + 63) / 64;
+  const int cb = b - N;
+  const bool isG = cb < nbG;
+  const float* part = isG ? g_ws : sa_ws;
+  float* out = isG ? Gm : Sa;
+  const int64_t cols = isG ? (int64_t)K * K : K;
+  const int64_t col = (int64_t)(isG ? cb : cb - nbG) * 64 + (tid & 63);
+  const int lane = tid >> 6;
+  float a = 0.f;
+  if (col < cols) {
+    int s = lane;
+    for (; s + 12 < S2; s += 16) {
+      const float u0 = part[s * cols + col], u1 = part[(s + 4) * cols + col], u2 = part[(s + 8) * cols + col],
+                  u3 = part[(s + 12) * cols + col];
+      a += u0;
+      a += u1;
+      a += u2;
+      a += u3;
+    }
+    for (; s < S2; s += 4) a += part[s * cols + col];
+  }
+  red[tid] = a;
   __syncthreads();
-  if (lane == 0 && c < cols) {
-    float t = 0.f;
-#pragma unroll
-    for (int l = 0; l < kSumLanes; ++l) t += sh[l][cl];
-    s.out[i][c] = t;
-  }
+  if (lane == 0 && col < cols) out[col] = red[tid] + red[tid + 64] + red[tid + 128] + red[tid + 192];
 }
 
+// fold_finish in one launch, block n: (A, B, D) of channel n from the all-reduced sums, then row n of
+// dW = A P + (B W) Gm + D (x) Sa in fp32 ((B W) Gm formed here: no separate fp32 GEMM), rounded once.
 template <typename T>
-__global__ __launch_bounds__(256) void k_fold_sums(const T* __restrict__ W, const float* __restrict__ P,
-                                                   const float* __restrict__ Sg, const float* __restrict__ mean,
-                                                   const float* __restrict__ invstd, int N, int K,
-                                                   float* __restrict__ sums, float* __restrict__ bn_grads) {
-  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;  // one wave per channel
-  if (n >= N) return;
-  float d = 0.f;
-  for (int k = lane; k < K; k += 64) d = fmaf(to_f<T>(W[(int64_t)n * K + k]), P[(int64_t)n * K + k], d);
-  d = wave_sum(d);
-  if (lane == 0) {
-    const float s1 = Sg[n], s2 = d - mean[n] * s1;
-    sums[n] = s1;
-    sums[N + n] = s2;
-    bn_grads[n] = s2 * invstd[n];
-    bn_grads[N + n] = s1;
-  }
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void k_fold_coef(const T* __restrict__ W, const float* __restrict__ sums,
-                                                   const float* __restrict__ count, const float* __restrict__ mean,
-                                                   const float* __restrict__ invstd, const float* __restrict__ weight,
-                                                   int N, int K, float* __restrict__ abd, float* __restrict__ BW) {
-  const int n = blockIdx.x;
+__global__ __launch_bounds__(kFoldThreads) void k_fold_finish(const T* __restrict__ W, const float* __restrict__ sums,
+                                                              const float* __restrict__ count,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ invstd,
+                                                              const float* __restrict__ weight,
+                                                              const float* __restrict__ P, const float* __restrict__ Gm,
+                                                              const float* __restrict__ Sa, int N, int K,
+                                                              float* __restrict__ abd, T* __restrict__ dW) {
+  extern __shared__ float bw[];  // B W[n, :]
+  const int n = blockIdx.x, tid = threadIdx.x;
   const float inv_n = 1.f / count[0];
   const float is = invstd[n], wv = weight ? weight[n] : 1.f;
   const float mdy = sums[n] * inv_n, mdyx = sums[N + n] * inv_n;
   const float A = is * wv, B = -is * is * A * mdyx, D = A * (mean[n] * is * is * mdyx - mdy);
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
     abd[n] = A;
     abd[N + n] = B;
     abd[2 * N + n] = D;
   }
-  for (int k = threadIdx.x; k < K; k += blockDim.x) BW[(int64_t)n * K + k] = B * to_f<T>(W[(int64_t)n * K + k]);
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void k_fold_final(const float* __restrict__ abd, const float* __restrict__ P,
-                                                    const float* __restrict__ X, const float* __restrict__ Sa, int N,
-                                                    int K, T* __restrict__ dW) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int64_t)N * K) return;
-  const int n = (int)(i / K), k = (int)(i - (int64_t)n * K);
-  dW[i] = from_f<T>(fmaf(abd[n], P[i], fmaf(abd[2 * N + n], Sa[k], X[i])));
+  for (int j = tid; j < K; j += kFoldThreads) bw[j] = B * to_f<T>(W[(int64_t)n * K + j]);
+  __syncthreads();
+  for (int k = tid; k < K; k += kFoldThreads) {
+    float x = 0.f;
+    for (int j = 0; j < K; ++j) x = fmaf(bw[j], Gm[(int64_t)j * K + k], x);
+    dW[(int64_t)n * K + k] = from_f<T>(fmaf(A, P[(int64_t)n * K + k], fmaf(D, Sa[k], x)));
+  }
 }
 
 int mask_cvb(int N) { return std::min(N / 8, 64); }
@@ -434,16 +473,6 @@ void mask_colsum(int dt, const void* g, const uint8_t* bits, void* g_pre, int64_
   if (e != hipSuccess) throw std::runtime_error(std::string("mask_colsum: ") + hipGetErrorString(e));
 }
 
-void sum_partials(const SumPartials& s, hipStream_t st) {
-  int nb[4];
-  for (int i = 0; i < 4; ++i) nb[i] = s.part[i] ? (int)((s.cols[i] + 63) / 64) : 0;
-  const int b1 = nb[0], b2 = b1 + nb[1], b3 = b2 + nb[2], tot = b3 + nb[3];
-  if (tot == 0) return;
-  hipLaunchKernelGGL(k_sum_partials, dim3(tot), dim3(64 * kSumLanes), 0, st, s, b1, b2, b3);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) throw std::runtime_error(std::string("sum_partials: ") + hipGetErrorString(e));
-}
-
 #define BH_FOLD_DT(dt, T, ...)                                   \
   switch (dt) {                                                  \
     case kF16: { using T = f16; __VA_ARGS__; } break;            \
@@ -451,29 +480,23 @@ void sum_partials(const SumPartials& s, hipStream_t st) {
     default: throw std::runtime_error("bn_fold: fp16 / bf16 only"); \
   }
 
-void fold_sums(int dt, const void* W, const float* P, const float* Sg, const float* mean, const float* invstd, int N,
-               int K, float* sums, float* bn_grads, hipStream_t st) {
-  BH_FOLD_DT(dt, T, hipLaunchKernelGGL(k_fold_sums<T>, dim3((N + 3) / 4), dim3(256), 0, st, (const T*)W, P, Sg, mean,
-                                       invstd, N, K, sums, bn_grads));
+void fold_reduce(int dt, const void* W, const float* p_ws, int S1, const float* g_ws, const float* sa_ws, int S2,
+                 const float* sg_ws, int S3, const float* mean, const float* invstd, int N, int K, float* P, float* Gm,
+                 float* Sa, float* sums, float* bn_grads, hipStream_t st) {
+  const int grid = N + (K * K + 63) / 64 + (K + 63) / 64;
+  BH_FOLD_DT(dt, T, hipLaunchKernelGGL(k_fold_reduce<T>, dim3(grid), dim3(kFoldThreads), 0, st, (const T*)W, p_ws, S1,
+                                       g_ws, sa_ws, S2, sg_ws, S3, mean, invstd, N, K, P, Gm, Sa, sums, bn_grads));
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess) throw std::runtime_error(std::string("fold_sums: ") + hipGetErrorString(e));
+  if (e != hipSuccess) throw std::runtime_error(std::string("fold_reduce: ") + hipGetErrorString(e));
 }
 
-void fold_coef(int dt, const void* W, const float* sums, const float* count, const float* mean, const float* invstd,
-               const float* weight, int N, int K, float* abd, float* BW, hipStream_t st) {
-  BH_FOLD_DT(dt, T, hipLaunchKernelGGL(k_fold_coef<T>, dim3(N), dim3(std::min(256, std::max(64, K))), 0, st,
-                                       (const T*)W, sums, count, mean, invstd, weight, N, K, abd, BW));
+void fold_finish(int dt, const void* W, const float* sums, const float* count, const float* mean, const float* invstd,
+                 const float* weight, const float* P, const float* Gm, const float* Sa, int N, int K, float* abd,
+                 void* dW, hipStream_t st) {
+  BH_FOLD_DT(dt, T, hipLaunchKernelGGL(k_fold_finish<T>, dim3(N), dim3(kFoldThreads), sizeof(float) * K, st,
+                                       (const T*)W, sums, count, mean, invstd, weight, P, Gm, Sa, N, K, abd, (T*)dW));
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess) throw std::runtime_error(std::string("fold_coef: ") + hipGetErrorString(e));
-}
-
-void fold_final(int dt, const float* abd, const float* P, const float* X, const float* Sa, int N, int K, void* dW,
-                hipStream_t st) {
-  const int64_t tot = (int64_t)N * K;
-  BH_FOLD_DT(dt, T, hipLaunchKernelGGL(k_fold_final<T>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, abd, P,
-                                       X, Sa, N, K, (T*)dW));
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) throw std::runtime_error(std::string("fold_final: ") + hipGetErrorString(e));
+  if (e != hipSuccess) throw std::runtime_error(std::string("fold_finish: ") + hipGetErrorString(e));
 }
 
 }  // namespace bh

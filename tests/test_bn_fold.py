@@ -109,6 +109,33 @@ def test_wgrad_f32_partials(shape, pro):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("N,K", [(256, 64), (512, 128), (1024, 256), (128, 512)])
+def test_fold_reduce_and_finish_kernels(N, K):
+    """The two one-launch combine stages (partial sums -> P, Gm, S_a, sums, BatchNorm gradients; then abd and
+    dW = A P + (B W) Gm + D S_a) against the fp64 references of ops/bn_fold.py."""
+    torch.manual_seed(0)
+    S1, S2, S3 = 37, 11, 5
+    dev = "cuda"
+    W = (torch.randn(N, K, device=dev) / K ** 0.5).half()
+    p_ws, g_ws = torch.randn(S1, N * K, device=dev), torch.randn(S2, K, K, device=dev)
+    sa_ws, sg_ws = torch.randn(S2, K, device=dev), torch.randn(S3, N, device=dev)
+    mean, invstd = torch.randn(N, device=dev), torch.rand(N, device=dev) + 0.5
+    P, Gm, Sa, sums, bn_grads = bn_fold.fold_reduce(W, p_ws, g_ws, sa_ws, sg_ws, mean, invstd)
+    Pr, Gr = p_ws.double().sum(0).view(N, K), g_ws.double().sum(0)
+    Sar, Sgr = sa_ws.double().sum(0), sg_ws.double().sum(0)
+    assert _rel(P, Pr) < 1e-6 and _rel(Gm, Gr) < 1e-6 and _rel(Sa, Sar) < 1e-6
+    sums_r = bn_fold.local_sums(W.cpu().double(), Pr.cpu(), Sgr.cpu(), mean.cpu().double())
+    assert _rel(sums, sums_r) < 1e-5
+    assert _rel(bn_grads, torch.cat([sums_r[N:] * invstd.cpu().double(), sums_r[:N]])) < 1e-5
+    weight, count = torch.rand(N, device=dev) + 0.5, torch.tensor([1000.0], device=dev)
+    dW, abd = bn_fold.fold_finish(W, sums, count, mean, invstd, weight, P, Gm, Sa)
+    dW_r, abd_r = bn_fold.combine(W.cpu(), P.cpu().double(), Gm.cpu().double(), Sa.cpu().double(), sums.cpu().double(),
+                                  mean.cpu().double(), invstd.cpu().double(), weight.cpu(), count.cpu())
+    assert _rel(abd, abd_r) < 1e-5
+    assert dW.dtype == W.dtype and _rel(dW, dW_r) < 2e-3
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("K,N", [(256, 64), (128, 64), (256, 128)])
 @pytest.mark.parametrize("epi", ["bwd", "plain"])
