@@ -468,6 +468,30 @@ void register_dense(pybind11::module_& root) {
     bh::transpose16(x.data_ptr(), x.size(0), x.size(1), y.data_ptr(), stream_for(x));
     return y;
   }, py::arg("x"), "x.t().contiguous() for a 2-D 16-bit tensor (64 x 64 LDS tiles, 16-byte accesses)");
+  // dW [N, K] = dy[T, N]^T @ x[T, K] on the transposed-operand ping-pong kernel (splits: 0 = automatic)
+  gm.def("weight_grad_tn", [](at::Tensor dy, at::Tensor x, int64_t splits) {
+    TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0) &&
+                    dy.scalar_type() == x.scalar_type() && dy.stride(1) == 1 && x.stride(1) == 1 &&
+                    (dy.scalar_type() == at::kHalf || dy.scalar_type() == at::kBFloat16),
+                "gemm.weight_grad_tn: dy [T, N] and x [T, K], one 16-bit dtype, unit column stride");
+    const int64_t T = dy.size(0), N = dy.size(1), K = x.size(1);
+    auto out = at::empty({N, K}, dy.options());
+    TORCH_CHECK(bh::gemm_tn_supported(N, K, T, dy.stride(0), x.stride(0), dy.data_ptr(), x.data_ptr(), out.data_ptr()),
+                "gemm.weight_grad_tn: unsupported shape (N, K % 256, T % 64, aligned rows)");
+    const int s = splits > 0 ? (int)splits : bh::gemm_tn_splits(N, K, T);
+    at::Tensor ws;
+    if (s > 1) ws = at::empty({(int64_t)s, N, K}, dy.options().dtype(at::kFloat));
+    bh::gemm_tn(dtype_code(dy.scalar_type()), dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), out.data_ptr(),
+                N, K, T, s > 1 ? ws.data_ptr<float>() : nullptr, s, stream_for(dy));
+    return out;
+  }, py::arg("dy"), py::arg("x"), py::arg("splits") = 0);
+  gm.def("weight_grad_tn_supported", [](at::Tensor dy, at::Tensor x) {
+    return dy.is_cuda() && x.is_cuda() && dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0) &&
+           dy.scalar_type() == x.scalar_type() && dy.stride(1) == 1 && x.stride(1) == 1 &&
+           (dy.scalar_type() == at::kHalf || dy.scalar_type() == at::kBFloat16) &&
+           bh::gemm_tn_supported(dy.size(1), x.size(1), dy.size(0), dy.stride(0), x.stride(0), dy.data_ptr(),
+                                 x.data_ptr(), dy.data_ptr());
+  }, py::arg("dy"), py::arg("x"));
   gm.def("mfma_enabled", &mfma_enabled);
   gm.def("set_tile_mode", &bh::gemm_set_tile_mode, "0 auto, 1 128x128, 2 256x256, 3 256x128, 4 ping-pong 256x256");
   gm.def("tile_mode", &bh::gemm_tile_mode);

@@ -53,6 +53,15 @@ void gemm_nt(int dt, const void* A, int64_t lda, const void* B, int64_t ldb, voi
 // 3 256x128 three-stage, 4 ping-pong forced (K % 64 == 0 only); default from BH_GEMM_TILE
 int gemm_tile_mode();
 void gemm_set_tile_mode(int mode);
+// C [M, N] (16-bit) = At^T . Bt for At [K, M] (row stride lda) and Bt [K, N] (row stride ldb), both contiguous
+// along M / N: a dense layer's weight gradient dY^T X (kernels/gemm_tn.hip, the ping-pong schedule with
+// K-major LDS images and transposed fragment reads). M, N % 256 == 0, K % 64 == 0. splits > 1: split-K over
+// the token axis into ws (fp32 [splits, M, N]) and a fixed-order reduction into C.
+bool gemm_tn_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const void* At, const void* Bt,
+                       const void* C);
+int gemm_tn_splits(int64_t M, int64_t N, int64_t K);
+void gemm_tn(int dt, const void* At, int64_t lda, const void* Bt, int64_t ldb, void* C, int64_t M, int64_t N,
+             int64_t K, float* ws, int splits, hipStream_t st);
 // out [C, R] = in [R, C]^T, 16-bit elements (R, C multiples of 8, 16-byte aligned)
 void transpose16(const void* in, int64_t R, int64_t C, void* out, hipStream_t st);
 // out[N] (dtype dt) = sum_r part[r][N]

@@ -218,16 +218,25 @@ def mlp_backward(use_bias: int, activation: int, grad_o, outputs, inputs) -> Lis
 # rank runs the same kernel.
 _WGRAD_MAX_ELEMS = 3072 * 800
 _WGRAD_MIN_TOKENS = 4096
+# the transposed-operand ping-pong GEMM (kernels/gemm_tn.hip, split-K over the tokens) from 1.5M-element
+# weights on: 1.28x hipBLASLt at 3072 x 1024, 1.16x / 1.12x at 4096 x 1024 / 1024 x 4096 (8192 tokens,
+# profiles/wgrad_tn_vs_hipblaslt.jsonl); the 1x1 weight-gradient kernel keeps the 1024 x 1024 projection
+_WGRAD_TN_MIN_ELEMS = 1536 * 1024
 
 
 def weight_grad(d_output: torch.Tensor, input: torch.Tensor) -> torch.Tensor:
     """``d_output^T @ input`` for 2-D ``[tokens, out]`` / ``[tokens, in]`` tensors: the dense layers'
-    weight gradient ``[out, in]`` in ``d_output``'s dtype."""
+    weight gradient ``[out, in]`` in ``d_output``'s dtype -- the transposed-operand MFMA GEMM for the large
+    weights, the 1x1 weight-gradient kernel for the smaller ones, else the library GEMM (static shape rules)."""
     M, K = d_output.shape
     C = input.size(1)
-    if (_config.get().dense_wgrad_mfma and d_output.is_cuda and d_output.dtype in (torch.float16, torch.bfloat16)
-            and input.dtype == d_output.dtype
-            and M >= _WGRAD_MIN_TOKENS and K * C <= _WGRAD_MAX_ELEMS and d_output.is_contiguous()
+    mfma = (_config.get().dense_wgrad_mfma and d_output.is_cuda and d_output.dtype in (torch.float16, torch.bfloat16)
+            and input.dtype == d_output.dtype and M >= _WGRAD_MIN_TOKENS)
+    if mfma and K * C >= _WGRAD_TN_MIN_ELEMS:
+        gm = submodule("gemm")
+        if gm.weight_grad_tn_supported(d_output, input):
+            return gm.weight_grad_tn(d_output, input, 0)
+    if (mfma and K * C <= _WGRAD_MAX_ELEMS and d_output.is_contiguous()
             and input.is_contiguous()):
         from . import conv as _conv
 

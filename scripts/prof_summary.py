@@ -70,7 +70,7 @@ def main():
     lines.append("")
     lines.append("| kernel | ms/step | share | launches/step |")
     lines.append("|---|---|---|---|")
-    for k, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:60]:
+    for k, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:150]:
         lines.append(f"| `{k}` | {t / n / 1e6:.3f} | {100.0 * t / max(busy, 1):.1f}% | {c / n:.1f} |")
     # per-launch durations (us) of the last step for the top kernels, in launch order
     last = rows[marks[-2] + 1: marks[-1] + 1] if len(marks) >= 2 else seg
