@@ -345,11 +345,29 @@ std::vector<at::Tensor> mlp_backward(int use_bias, int activation, at::Tensor gr
 // ------------------------------------------------------------------------------------------------
 // fused_weight_gradient_mlp_cuda: main_grad[N,K] += d_output[M,N]^T @ input[M,K]
 // ------------------------------------------------------------------------------------------------
+// the transposed-operand MFMA GEMM accumulating into main_grad (accum 1: fp32, 2: 16-bit) where it takes the
+// shape (a contiguous [N, K] main_grad); false: the caller runs the library GEMM
+bool wgrad_accum_tn(const at::Tensor& x, const at::Tensor& dy, at::Tensor& main_grad, int accum) {
+  if (!(x.scalar_type() == dy.scalar_type() && (x.scalar_type() == at::kHalf || x.scalar_type() == at::kBFloat16) &&
+        main_grad.is_contiguous() && main_grad.dim() == 2 && main_grad.size(0) == dy.size(1) &&
+        main_grad.size(1) == x.size(1) && x.size(0) >= 4096 &&
+        bh::gemm_tn_supported(dy.size(1), x.size(1), dy.size(0), dy.stride(0), x.stride(0), dy.data_ptr(),
+                              x.data_ptr(), main_grad.data_ptr())))
+    return false;
+  const int64_t T = dy.size(0), N = dy.size(1), K = x.size(1);
+  const int s = bh::gemm_tn_splits(N, K, T);
+  auto ws = at::empty({(int64_t)s, N, K}, dy.options().dtype(at::kFloat));
+  bh::gemm_tn(dtype_code(dy.scalar_type()), dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0),
+              main_grad.data_ptr(), N, K, T, ws.data_ptr<float>(), s, stream_for(dy), accum);
+  return true;
+}
+
 void wgrad_gemm_accum_fp32(at::Tensor input, at::Tensor d_output, at::Tensor main_grad) {
   check_cuda(input, "input");
   TORCH_CHECK(main_grad.scalar_type() == at::kFloat, "wgrad_gemm_accum_fp32: main_grad must be fp32");
   auto x = as2d(input.contiguous());
   auto dy = as2d(d_output.contiguous());
+  if (wgrad_accum_tn(x, dy, main_grad, 1)) return;
   if (x.scalar_type() == at::kFloat) {
     main_grad.addmm_(dy.t(), x);
   } else {
@@ -360,7 +378,10 @@ void wgrad_gemm_accum_fp32(at::Tensor input, at::Tensor d_output, at::Tensor mai
 void wgrad_gemm_accum_fp16(at::Tensor input, at::Tensor d_output, at::Tensor main_grad) {
   check_cuda(input, "input");
   TORCH_CHECK(main_grad.scalar_type() == input.scalar_type(), "wgrad_gemm_accum_fp16: dtype mismatch");
-  main_grad.addmm_(as2d(d_output.contiguous()).t(), as2d(input.contiguous()));
+  auto x = as2d(input.contiguous());
+  auto dy = as2d(d_output.contiguous());
+  if (wgrad_accum_tn(x, dy, main_grad, 2)) return;
+  main_grad.addmm_(dy.t(), x);
 }
 
 // activation helpers exposed for python modules (bias_gelu etc.)
@@ -485,6 +506,30 @@ void register_dense(pybind11::module_& root) {
                 N, K, T, s > 1 ? ws.data_ptr<float>() : nullptr, s, stream_for(dy));
     return out;
   }, py::arg("dy"), py::arg("x"), py::arg("splits") = 0);
+  // C [M, N] = a [M, K] @ bt [K, N] (both row-major): the data gradient dY @ W on the MFMA kernel
+  gm.def("mm_nn", [](at::Tensor a, at::Tensor bt, int64_t splits) {
+    TORCH_CHECK(a.is_cuda() && bt.is_cuda() && a.dim() == 2 && bt.dim() == 2 && a.size(1) == bt.size(0) &&
+                    a.scalar_type() == bt.scalar_type() && a.stride(1) == 1 && bt.stride(1) == 1 &&
+                    (a.scalar_type() == at::kHalf || a.scalar_type() == at::kBFloat16),
+                "gemm.mm_nn: a [M, K] and bt [K, N], one 16-bit dtype, unit column stride");
+    const int64_t M = a.size(0), K = a.size(1), N = bt.size(1);
+    auto out = at::empty({M, N}, a.options());
+    TORCH_CHECK(bh::gemm_nn_supported(M, N, K, a.stride(0), bt.stride(0), a.data_ptr(), bt.data_ptr(), out.data_ptr()),
+                "gemm.mm_nn: unsupported shape (M, N % 256, K % 64, aligned rows)");
+    const int s = splits > 0 ? (int)splits : bh::gemm_tn_splits(M, N, K);
+    at::Tensor ws;
+    if (s > 1) ws = at::empty({(int64_t)s, M, N}, a.options().dtype(at::kFloat));
+    bh::gemm_nn(dtype_code(a.scalar_type()), a.data_ptr(), a.stride(0), bt.data_ptr(), bt.stride(0), out.data_ptr(), M,
+                N, K, s > 1 ? ws.data_ptr<float>() : nullptr, s, stream_for(a));
+    return out;
+  }, py::arg("a"), py::arg("bt"), py::arg("splits") = 0);
+  gm.def("mm_nn_supported", [](at::Tensor a, at::Tensor bt) {
+    return a.is_cuda() && bt.is_cuda() && a.dim() == 2 && bt.dim() == 2 && a.size(1) == bt.size(0) &&
+           a.scalar_type() == bt.scalar_type() && a.stride(1) == 1 && bt.stride(1) == 1 &&
+           (a.scalar_type() == at::kHalf || a.scalar_type() == at::kBFloat16) &&
+           bh::gemm_nn_supported(a.size(0), bt.size(1), a.size(1), a.stride(0), bt.stride(0), a.data_ptr(),
+                                 bt.data_ptr(), a.data_ptr());
+  }, py::arg("a"), py::arg("bt"));
   gm.def("weight_grad_tn_supported", [](at::Tensor dy, at::Tensor x) {
     return dy.is_cuda() && x.is_cuda() && dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0) &&
            dy.scalar_type() == x.scalar_type() && dy.stride(1) == 1 && x.stride(1) == 1 &&

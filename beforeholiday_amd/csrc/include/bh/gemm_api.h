@@ -56,11 +56,20 @@ void gemm_set_tile_mode(int mode);
 // C [M, N] (16-bit) = At^T . Bt for At [K, M] (row stride lda) and Bt [K, N] (row stride ldb), both contiguous
 // along M / N: a dense layer's weight gradient dY^T X (kernels/gemm_tn.hip, the ping-pong schedule with
 // K-major LDS images and transposed fragment reads). M, N % 256 == 0, K % 64 == 0. splits > 1: split-K over
-// the token axis into ws (fp32 [splits, M, N]) and a fixed-order reduction into C.
+// the token axis into ws (fp32 [splits, M, N]) and a fixed-order reduction into C. accum: 0 C = result (16-bit),
+// 1 C (fp32) += result, 2 C (16-bit) += result -- the last two always through ws (fused_weight_gradient_mlp's
+// main_grad accumulation).
 bool gemm_tn_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const void* At, const void* Bt,
                        const void* C);
 int gemm_tn_splits(int64_t M, int64_t N, int64_t K);
 void gemm_tn(int dt, const void* At, int64_t lda, const void* Bt, int64_t ldb, void* C, int64_t M, int64_t N,
+             int64_t K, float* ws, int splits, hipStream_t st, int accum = 0);
+// C [M, N] (16-bit) = A . Bt for row-major A [M, K] (lda) and Bt [K, N] (ldb, N-contiguous): a dense layer's
+// data gradient dY . W, on the same kernel (A staged row-major, Bt through the transposed reads); split-K as
+// gemm_tn (gemm_tn_splits picks the count).
+bool gemm_nn_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const void* A, const void* Bt,
+                       const void* C);
+void gemm_nn(int dt, const void* A, int64_t lda, const void* Bt, int64_t ldb, void* C, int64_t M, int64_t N,
              int64_t K, float* ws, int splits, hipStream_t st);
 // out [C, R] = in [R, C]^T, 16-bit elements (R, C multiples of 8, 16-byte aligned)
 void transpose16(const void* in, int64_t R, int64_t C, void* out, hipStream_t st);

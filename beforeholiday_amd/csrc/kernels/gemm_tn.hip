@@ -81,7 +81,12 @@ struct TnArgs {
   int tiles_m, tiles_n, splits;
 };
 
-template <typename T, bool PART>
+// the row-major A image of the NN layout (k_gemm_pp's): 256 rows x 128 B, chunk XOR-swizzled by (row >> 1) & 7
+BH_DEVICE int swz(int row, int ch) { return row * 128 + ((ch ^ ((row >> 1) & 7)) << 4); }
+
+// AK: A is row-major [M, K] (K-contiguous: the NN layout, C = A . Bt, a data gradient dY . W) and staged as
+// k_gemm_pp stages it (256 rows x 128 B per K-step, ds_read_b128 fragments); else K-major At [K, M] (TN).
+template <typename T, bool PART, bool AK>
 __global__ __launch_bounds__(kThreads, 1) void k_gemm_tn(TnArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -101,7 +106,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_gemm_tn(TnArgs p) {
 
   // whole-tensor resources (the host checks K * ld * 2 < 2^32 and M, N % 256 == 0)
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<void*>(p.A), (short)0, (int)((int64_t)p.K * p.lda * 2), (int)kRsrcWord3);
+      const_cast<void*>(p.A), (short)0, (int)((int64_t)(AK ? p.M : p.K) * p.lda * 2), (int)kRsrcWord3);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(p.B), (short)0, (int)((int64_t)p.K * p.ldb * 2), (int)kRsrcWord3);
   const int lda2 = (int)p.lda * 2, ldb2 = (int)p.ldb * 2;
@@ -112,8 +117,15 @@ __global__ __launch_bounds__(kThreads, 1) void k_gemm_tn(TnArgs p) {
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int pc = 2 * wc + i;
-    const int ra = 8 * pc + (lane >> 3);
-    voffA[i] = ra * lda2 + (brow + 2 * wr * 64 + ((lane & 7) ^ fa_sw(ra)) * 8) * 2;
+    if constexpr (AK) {
+      // piece rows wr * 128 + 8 pc + lane / 8 (unit 3: + 64); chunk lane % 8 holds logical chunk
+      // (lane % 8) ^ ((row >> 1) & 7) = (lane % 8) ^ ((i << 2) | (prow >> 1)) (the piece parity is i)
+      const int prow = lane >> 3;
+      voffA[i] = (brow + wr * 128 + 8 * pc + prow) * lda2 + (((lane & 7) ^ ((i << 2) | (prow >> 1))) << 4);
+    } else {
+      const int ra = 8 * pc + (lane >> 3);
+      voffA[i] = ra * lda2 + (brow + 2 * wr * 64 + ((lane & 7) ^ fa_sw(ra)) * 8) * 2;
+    }
     const int rb = 16 * (pc & 3) + (lane >> 2);
     const int wcb = 2 * wr + (pc >> 2);
     voffB[i] = rb * ldb2 + (bcol + wcb * 64 + ((lane & 3) ^ fb_sw(rb)) * 8) * 2;
@@ -132,7 +144,11 @@ __global__ __launch_bounds__(kThreads, 1) void k_gemm_tn(TnArgs p) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int pc = 2 * wc + i;
-      if constexpr (j == 0 || j == 3) {
+      if constexpr ((j == 0 || j == 3) && AK) {
+        const int rb = wr * 128 + (j == 3 ? 64 : 0) + pc * 8;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_ptr_t)(dst + rb * 128), 16,
+                                                 voffA[i] + (j == 3 ? 64 * lda2 : 0), kt * kBK * 2, 0, 0);
+      } else if constexpr (j == 0 || j == 3) {
         const int u = 2 * wr + (j == 3 ? 1 : 0);
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, (lds_ptr_t)(dst + u * 8192 + pc * 1024), 16,
                                                  voffA[i] + (j == 3 ? 128 : 0), kt * kBK * lda2, 0, 0);
@@ -158,11 +174,19 @@ __global__ __launch_bounds__(kThreads, 1) void k_gemm_tn(TnArgs p) {
   };
   i4v af[2][4], b0[2][2], b1[2][2];
   auto read_a = [&](const char* buf, int mi) {
-    const char* img = buf + (2 * wr + mi) * 8192;
+    if constexpr (AK) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+      for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int m = 0; m < 4; ++m) af[s][m] = frag(img, 128, s, m, true);
+        for (int m = 0; m < 4; ++m)
+          af[s][m] = *reinterpret_cast<const i4v*>(buf + swz(wr * 128 + mi * 64 + m * 16 + (lane & 15), s * 4 + fq));
+    } else {
+      const char* img = buf + (2 * wr + mi) * 8192;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) af[s][m] = frag(img, 128, s, m, true);
+    }
   };
   auto read_b = [&](const char* buf, int ni, i4v (&bf)[2][2]) {
     const char* img = buf + kBOff + (ni * 4 + wc) * 4096;
@@ -250,10 +274,11 @@ __global__ __launch_bounds__(kThreads, 1) void k_gemm_tn(TnArgs p) {
   }
 }
 
-// sum of the splits' tile-major partials in split order (deterministic), rounded into the row-major C
-template <typename T>
-__global__ __launch_bounds__(256) void k_tn_reduce(const float* __restrict__ ws, T* __restrict__ C, int N, int tiles_n,
-                                                  int64_t per_split, int splits) {
+// sum of the splits' tile-major partials in split order (deterministic) into the row-major C: ACC 0 stores it
+// rounded to T, 1 adds it to an fp32 C, 2 adds it to a 16-bit C (in fp32, rounded once)
+template <typename T, int ACC>
+__global__ __launch_bounds__(256) void k_tn_reduce(const float* __restrict__ ws, void* __restrict__ Cv, int N,
+                                                  int tiles_n, int64_t per_split, int splits) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= per_split) return;
   f4v acc = *reinterpret_cast<const f4v*>(ws + i * 4);
@@ -264,10 +289,22 @@ __global__ __launch_bounds__(256) void k_tn_reduce(const float* __restrict__ ws,
   const int64_t row = (int64_t)tm * kTile + (wave >> 2) * 128 + mt * 16 + (lane & 15);
   const int col = tn * kTile + (wave & 3) * 64 + nt * 16 + 4 * (lane >> 4);
   typedef T t4 __attribute__((ext_vector_type(4)));
-  t4 o;
+  if constexpr (ACC == 1) {
+    f4v* dst = reinterpret_cast<f4v*>(reinterpret_cast<float*>(Cv) + row * N + col);
+    *dst = *dst + acc;
+  } else {
+    t4* dst = reinterpret_cast<t4*>(reinterpret_cast<T*>(Cv) + row * N + col);
+    t4 o;
+    if constexpr (ACC == 2) {
+      const t4 old = *dst;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) o[j] = from_f<T>(acc[j]);
-  *reinterpret_cast<t4*>(C + row * N + col) = o;
+      for (int j = 0; j < 4; ++j) o[j] = from_f<T>(to_f<T>(old[j]) + acc[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = from_f<T>(acc[j]);
+    }
+    *dst = o;
+  }
 }
 
 }  // namespace
@@ -280,6 +317,14 @@ bool gemm_tn_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb
          K * ldb * 2 < 0x7fffffffll && M * N < (1ll << 31);
 }
 
+bool gemm_nn_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const void* A, const void* Bt,
+                       const void* C) {
+  auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  return M > 0 && N > 0 && K > 0 && M % kTile == 0 && N % kTile == 0 && K % kBK == 0 && lda >= K && ldb >= N &&
+         lda % 8 == 0 && ldb % 8 == 0 && al(A) && al(Bt) && al(C) && M * lda * 2 < 0x7fffffffll &&
+         K * ldb * 2 < 0x7fffffffll && M * N < (1ll << 31);
+}
+
 int gemm_tn_splits(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = (M / kTile) * (N / kTile), nk = K / kBK;
   // about one round of workgroups (one per CU), at least 8 K-steps per split
@@ -288,11 +333,30 @@ int gemm_tn_splits(int64_t M, int64_t N, int64_t K) {
   return (int)s;
 }
 
+namespace {
+void run_tn(bool ak, int dt, const void* At, int64_t lda, const void* Bt, int64_t ldb, void* C, int64_t M, int64_t N,
+            int64_t K, float* ws, int splits, hipStream_t st, int accum);
+}
+
 void gemm_tn(int dt, const void* At, int64_t lda, const void* Bt, int64_t ldb, void* C, int64_t M, int64_t N,
-             int64_t K, float* ws, int splits, hipStream_t st) {
+             int64_t K, float* ws, int splits, hipStream_t st, int accum) {
   if (!gemm_tn_supported(M, N, K, lda, ldb, At, Bt, C))
     throw std::runtime_error("gemm_tn: needs M, N % 256 == 0, K % 64 == 0, ld % 8 == 0, 16-byte alignment");
-  if (splits < 1 || splits > K / kBK || (splits > 1 && !ws)) throw std::runtime_error("gemm_tn: bad split count");
+  run_tn(false, dt, At, lda, Bt, ldb, C, M, N, K, ws, splits, st, accum);
+}
+
+void gemm_nn(int dt, const void* A, int64_t lda, const void* Bt, int64_t ldb, void* C, int64_t M, int64_t N,
+             int64_t K, float* ws, int splits, hipStream_t st) {
+  if (!gemm_nn_supported(M, N, K, lda, ldb, A, Bt, C))
+    throw std::runtime_error("gemm_nn: needs M, N % 256 == 0, K % 64 == 0, ld % 8 == 0, 16-byte alignment");
+  run_tn(true, dt, A, lda, Bt, ldb, C, M, N, K, ws, splits, st, 0);
+}
+
+namespace {
+void run_tn(bool ak, int dt, const void* At, int64_t lda, const void* Bt, int64_t ldb, void* C, int64_t M, int64_t N,
+            int64_t K, float* ws, int splits, hipStream_t st, int accum) {
+  if (splits < 1 || splits > K / kBK || ((splits > 1 || accum) && !ws)) throw std::runtime_error("gemm_tn: bad split count");
+  const bool part = splits > 1 || accum != 0;  // accumulation always goes through the partials
   TnArgs a;
   a.A = At;
   a.B = Bt;
@@ -309,8 +373,13 @@ void gemm_tn(int dt, const void* At, int64_t lda, const void* Bt, int64_t ldb, v
   const unsigned grid = (unsigned)((int64_t)a.tiles_m * a.tiles_n * splits);
   auto go = [&](auto tt) {
     using T = decltype(tt);
-    if (splits > 1) hipLaunchKernelGGL((k_gemm_tn<T, true>), dim3(grid), dim3(kThreads), 0, st, a);
-    else hipLaunchKernelGGL((k_gemm_tn<T, false>), dim3(grid), dim3(kThreads), 0, st, a);
+    if (ak) {
+      if (part) hipLaunchKernelGGL((k_gemm_tn<T, true, true>), dim3(grid), dim3(kThreads), 0, st, a);
+      else hipLaunchKernelGGL((k_gemm_tn<T, false, true>), dim3(grid), dim3(kThreads), 0, st, a);
+    } else {
+      if (part) hipLaunchKernelGGL((k_gemm_tn<T, true, false>), dim3(grid), dim3(kThreads), 0, st, a);
+      else hipLaunchKernelGGL((k_gemm_tn<T, false, false>), dim3(grid), dim3(kThreads), 0, st, a);
+    }
   };
   switch (dt) {
     case kF16: go(f16{}); break;
@@ -319,16 +388,25 @@ void gemm_tn(int dt, const void* At, int64_t lda, const void* Bt, int64_t ldb, v
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("gemm_tn: ") + hipGetErrorString(e));
-  if (splits > 1) {
+  if (part) {
     const int64_t per_split = M * N / 4;  // f4v groups of one split
     const unsigned rg = (unsigned)((per_split + 255) / 256);
-    switch (dt) {
-      case kF16: hipLaunchKernelGGL(k_tn_reduce<f16>, dim3(rg), dim3(256), 0, st, ws, (f16*)C, (int)N, a.tiles_n, per_split, splits); break;
-      default: hipLaunchKernelGGL(k_tn_reduce<bf16>, dim3(rg), dim3(256), 0, st, ws, (bf16*)C, (int)N, a.tiles_n, per_split, splits); break;
-    }
+    auto red = [&](auto tt, auto accc) {
+      using T = decltype(tt);
+      constexpr int ACC = decltype(accc)::value;
+      hipLaunchKernelGGL((k_tn_reduce<T, ACC>), dim3(rg), dim3(256), 0, st, ws, C, (int)N, a.tiles_n, per_split, splits);
+    };
+    auto by_acc = [&](auto tt) {
+      if (accum == 1) red(tt, std::integral_constant<int, 1>{});
+      else if (accum == 2) red(tt, std::integral_constant<int, 2>{});
+      else red(tt, std::integral_constant<int, 0>{});
+    };
+    if (dt == kF16) by_acc(f16{});
+    else by_acc(bf16{});
     e = hipGetLastError();
     if (e != hipSuccess) throw std::runtime_error(std::string("gemm_tn reduce: ") + hipGetErrorString(e));
   }
 }
+}  // namespace
 
 }  // namespace bh
