@@ -573,18 +573,26 @@ class ParamTable {
     };
     std::vector<at::Tensor> norms;
     for (auto& kv : plain_gdt) norms.push_back(norm_of(kv.second));
+    at::Tensor gnorm;
     if (!scaled_gdt.empty()) {
       at::Tensor sn;
       if (scaled_norm.has_value()) {
-        sn = *scaled_norm;
+        sn = scaled_norm->contiguous();
+        TORCH_CHECK(sn.is_cuda() && sn.scalar_type() == at::kFloat && sn.numel() == 1,
+                    "ParamTable.lamb_step: scaled_norm must be a one-element CUDA fp32 tensor");
       } else {
         std::vector<at::Tensor> sl;
         for (auto& kv : scaled_gdt) sl.push_back(norm_of(kv.second));
         sn = sl.size() == 1 ? sl[0] : norm_of(sl);
       }
-      norms.push_back(at::mul(sn.reshape({1}), *inv_scale));
+      // the usual amp O2 case (one plain dtype at most): one blend launch, no per-step pointer list
+      at::Tensor plain = norms.size() == 1 ? norms[0] : norms.empty() ? at::Tensor() : norm_of(norms);
+      gnorm = at::empty({1}, sn.options());
+      bh::norm_blend(plain.defined() ? plain.data_ptr<float>() : nullptr, sn.data_ptr<float>(),
+                     inv_scale->data_ptr<float>(), gnorm.data_ptr<float>(), stream_for(noop));
+    } else {
+      gnorm = norms.size() == 1 ? norms[0] : norm_of(norms);
     }
-    at::Tensor gnorm = norms.size() == 1 ? norms[0] : norm_of(norms);
     for (size_t gi = 0; gi < groups_.size(); ++gi) {
       const auto& h = hyper[gi];
       TORCH_CHECK(h.size() == 8, "ParamTable.lamb_step: 8 hyper-parameters per group");

@@ -126,6 +126,10 @@ void mta_lamb_stage2_standalone(const MTAView& v, int dt_p, int dt_u, const floa
                                 const float* unorm, float lr, float decay, bool use_nvlamb,
                                 hipStream_t s);
 
+// out[0] = sqrt(plain[0]^2 + (scaled[0] inv_scale[0])^2) (plain may be null): a loss-scaled norm blended with
+// the norm of already-unscaled gradients in one launch (FusedLAMB's global gradient norm under amp)
+void norm_blend(const float* plain, const float* scaled, const float* inv_scale, float* out, hipStream_t s);
+
 // amp device loss scale: step_flag |= overflow; then the dynamic-scale update (see multi_tensor.hip)
 void amp_update_scale(float* scale, int* unskipped, const int* overflow, int* step_flag, float factor, int window,
                       float min_scale, float max_scale, hipStream_t s);

@@ -740,4 +740,18 @@ void amp_update_scale(float* scale, int* unskipped, const int* overflow, int* st
   check_launch("amp_update_scale");
 }
 
+namespace {
+__global__ void k_norm_blend(const float* plain, const float* scaled, const float* inv_scale, float* out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const float u = *scaled * *inv_scale;
+  const float p = plain ? *plain : 0.f;
+  *out = sqrtf(fmaf(p, p, u * u));
+}
+}  // namespace
+
+void norm_blend(const float* plain, const float* scaled, const float* inv_scale, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_norm_blend, dim3(1), dim3(64), 0, s, plain, scaled, inv_scale, out);
+  check_launch("norm_blend");
+}
+
 }  // namespace bh
