@@ -5,8 +5,9 @@ kernels/gemm.hip where its static rule picks it (K <= 1024), else hipBLASLt's ad
 activation pass (``gemm.linear_act``).
 Backward: the last layer's dActivation + bias gradient in one pass; every earlier layer's dActivation
 and bias gradient inside the data-gradient GEMM's epilogue (``gemm.linear_dact``); the weight
-gradients on the MFMA weight-gradient kernel where it applies (``ops.fused_dense.weight_grad``: <= ~2.4M
-elements, >= 4096 rows), hipBLASLt otherwise.
+gradients on MFMA kernels where they apply (``ops.fused_dense.weight_grad``, >= 4096 rows: the
+transposed-operand GEMM of kernels/gemm_tn.hip from 1.5M weight elements, the 1x1 weight-gradient kernel
+below that), hipBLASLt otherwise.
 The activation follows EVERY layer (including the last), like the reference.
 """
 import math

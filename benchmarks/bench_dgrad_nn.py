@@ -2,7 +2,9 @@
 the ping-pong MFMA kernel (``gemm.mm_nn``, kernels/gemm_tn.hip) vs hipBLASLt (``dy @ w``), interleaved rounds in
 one process, median us and TFLOP/s. One JSON line per shape.
 
-    python benchmarks/bench_dgrad_nn.py [--tokens 8192] [--dtype fp16]
+    python benchmarks/bench_dgrad_nn.py [--tokens 8192] [--dtype fp16] [--resnet]
+
+--resnet: the ResNet-50 (bs 256) 1x1 data gradients that still run on hipBLASLt (stage-3 / stage-4 rows).
 """
 import argparse
 import json
@@ -14,6 +16,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 SHAPES = [(3072, 1024), (1024, 1024), (4096, 1024), (1024, 4096)]  # (K = layer out, N = layer in)
+RESNET = [(50176, 1024, 256), (50176, 256, 1024), (12544, 2048, 512), (12544, 512, 2048)]  # (M, K, N)
 
 
 def timeit(fn, iters=20):
@@ -31,14 +34,15 @@ def main():
     ap.add_argument("--tokens", type=int, default=8192)
     ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16"])
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--resnet", action="store_true")
     args = ap.parse_args()
     from beforeholiday_amd._native import submodule
 
     gm = submodule("gemm")
     dt = torch.float16 if args.dtype == "fp16" else torch.bfloat16
     torch.manual_seed(0)
-    for K, N in SHAPES:
-        M = args.tokens
+    shapes = RESNET if args.resnet else [(args.tokens, K, N) for K, N in SHAPES]
+    for M, K, N in shapes:
         dy = torch.randn(M, K, device="cuda").to(dt)
         w = (torch.randn(K, N, device="cuda") / K ** 0.5).to(dt)
         flops = 2.0 * M * N * K
