@@ -229,9 +229,11 @@ std::vector<at::Tensor> merge_parts(at::Tensor part, double count, c10::optional
   const bool has_run = rmean.has_value() && rmean->defined();
   int dtw = wcode(w);
   if (!(w.has_value() && w->defined()) && has_run) dtw = dtype_code(rmean->scalar_type());
+  const int SG = bh::bn_part_segments(G);
+  at::Tensor seg_ws = SG > 1 ? at::empty({SG, 2, C}, part.options()) : at::Tensor();
   bh::bn_merge_parts(G, C, part.data_ptr<float>(), (float)count, fin, dtw, wptr(w), wptr(b),
                      has_run ? rmean->data_ptr() : nullptr, has_run ? rvar->data_ptr() : nullptr, stream_for(part),
-                     bump);
+                     bump, SG > 1 ? seg_ws.data_ptr<float>() : nullptr);
   return r;
 }
 

@@ -12,6 +12,12 @@
 
 namespace bh {
 
+// Summation order of G partial rows (per channel) shared by the BatchNorm partial-sum kernels (batchnorm.hip
+// k_merge_parts / k_merge_segs, conv_bn.hip k_sum_parts), so every path gives the same bits: SG contiguous
+// segments of ceil(G / SG) rows, each summed as 16 strided row groups added in order, then the segment
+// totals in order. From 1024 rows (a 28x28 3x3 convolution leaves ~7000) the segments are summed in parallel.
+__host__ __device__ inline int bn_part_segments(int G) { return G >= 1024 ? (G / 256 < 32 ? G / 256 : 32) : 1; }
+
 enum DType : int { kF32 = 0, kF16 = 1, kBF16 = 2, kF64 = 3, kU8 = 4, kI32 = 5, kI64 = 6, kBool = 7 };
 
 // ---------------------------------------------------------------------------------

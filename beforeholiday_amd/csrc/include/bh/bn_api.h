@@ -42,11 +42,13 @@ void bn_stats_finalize(const BNShape& s, int splits, const float* pmean, const f
 // per-channel reference K = kref (dtype dt_w; null = 0), finalized by bn_merge_sums after the reduction
 void bn_merge_sums(int C, const float* sums, const BNFinal& fin, int dt_w, const void* w, const void* b, void* rmean,
                    void* rvar, hipStream_t st);
-// single rank: sum a convolution epilogue's partials part [2][G][C] (fixed order) and finalize as
-// bn_merge_sums with element count `count` -- one launch
+// single rank: sum a convolution epilogue's partials part [2][G][C] (the fixed bn_part_segments order) and
+// finalize as bn_merge_sums with element count `count` -- one launch, or two with a segment workspace
+// seg_ws [bn_part_segments(G)][2][C] fp32 when bn_part_segments(G) > 1
 // (bump: also num_batches += 1, for a fixed momentum only)
 void bn_merge_parts(int G, int C, const float* part, float count, const BNFinal& fin, int dt_w, const void* w,
-                    const void* b, void* rmean, void* rvar, hipStream_t st, bool bump = false);
+                    const void* b, void* rmean, void* rvar, hipStream_t st, bool bump = false,
+                    float* seg_ws = nullptr);
 // merge W gathered rows [W][2C+1] into final stats (+ running stats update, scale/shift)
 void bn_merge_ranks(int W, int C, const float* gathered, const BNFinal& fin, int dt_w, const void* w,
                     const void* b, void* rmean, void* rvar, float* var_unbiased, hipStream_t st);

@@ -385,27 +385,23 @@ __global__ __launch_bounds__(kBlock) void k_merge_sums(int C, const float* __res
 }
 
 // single-rank finalize straight from a convolution epilogue's partials part [2][G][C] (sums of x - K
-// and (x - K)^2 per workgroup, K = running mean): the partial rows are summed in the same fixed order
-// as conv_bn's k_sum_parts (row group g takes rows g, g + 16, ...; the 16 groups are then added in
-// order), then finalized as k_merge_sums -- one launch instead of sum_parts + merge_sums.
+// and (x - K)^2 per workgroup, K = running mean), in the fixed order shared with conv_bn's k_sum_parts
+// (bn_part_segments): SG contiguous row segments; inside one, row group g takes rows g, g + 16, ... and the
+// 16 groups are added in order; then the segment totals in order. SG == 1: one launch (k_merge_parts).
+// SG > 1 (the 28x28 3x3 convolutions leave ~7000 partial rows, which one workgroup per 64 channels read
+// in ~20 us): the segments in parallel (k_merge_segs, grid C/64 x SG) and a finalize launch.
 constexpr int kMergeRows = 16;
-template <typename Tw>
-__global__ __launch_bounds__(64 * kMergeRows) void k_merge_parts(int G, int C, const float* __restrict__ part, float n,
-                                                                 BNFinal fin, const Tw* w, const Tw* b, Tw* rmean,
-                                                                 Tw* rvar, bool bump) {
-  // bump: this launch also advances num_batches_tracked (the host sets it only for a fixed momentum,
-  // where no thread reads the counter)
-  if (bump && fin.num_batches && blockIdx.x == 0 && threadIdx.x == 0) *fin.num_batches += 1;
-  __shared__ float sh[2][kMergeRows][64];
-  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+
+// this block's segment total of both statistics for channel lane cl (rows [g0, g1)); valid in rg == 0
+__device__ __forceinline__ void merge_rows(int G, int C, int c, int cl, int rg, int g0, int g1, const float* part,
+                                           float (*sh)[kMergeRows][64], float& s1, float& s2) {
   float a1 = 0.f, a2 = 0.f;
   if (c < C) {
     const float* p1 = part + c;
     const float* p2 = part + (int64_t)G * C + c;
-    int g = rg;
+    int g = g0 + rg;
     // 8 rows of loads in flight per lane (the adds stay in row order: same sums as the plain loop)
-    for (; g + 7 * kMergeRows < G; g += 8 * kMergeRows) {
+    for (; g + 7 * kMergeRows < g1; g += 8 * kMergeRows) {
       float u[8], v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -418,7 +414,7 @@ __global__ __launch_bounds__(64 * kMergeRows) void k_merge_parts(int G, int C, c
         a2 += v[j];
       }
     }
-    for (; g < G; g += kMergeRows) {
+    for (; g < g1; g += kMergeRows) {
       a1 += p1[(int64_t)g * C];
       a2 += p2[(int64_t)g * C];
     }
@@ -426,13 +422,18 @@ __global__ __launch_bounds__(64 * kMergeRows) void k_merge_parts(int G, int C, c
   sh[0][rg][cl] = a1;
   sh[1][rg][cl] = a2;
   __syncthreads();
-  if (rg != 0 || c >= C) return;
-  float s1 = 0.f, s2 = 0.f;
+  s1 = 0.f;
+  s2 = 0.f;
 #pragma unroll
   for (int q = 0; q < kMergeRows; ++q) {
     s1 += sh[0][q][cl];
     s2 += sh[1][q][cl];
   }
+}
+
+template <typename Tw>
+__device__ __forceinline__ void merge_finalize(int c, float s1, float s2, float n, const BNFinal& fin, const Tw* w,
+                                               const Tw* b, Tw* rmean, Tw* rvar) {
   const float kc = rmean ? to_f<Tw>(rmean[c]) : 0.f;
   const float dm = n > 0.f ? s1 / n : 0.f;
   const float mean = kc + dm;
@@ -452,6 +453,51 @@ __global__ __launch_bounds__(64 * kMergeRows) void k_merge_parts(int G, int C, c
     rmean[c] = from_f<Tw>((1.f - mom) * kc + mom * mean);
     rvar[c] = from_f<Tw>((1.f - mom) * to_f<Tw>(rvar[c]) + mom * unb);
   }
+}
+
+template <typename Tw>
+__global__ __launch_bounds__(64 * kMergeRows) void k_merge_parts(int G, int C, const float* __restrict__ part, float n,
+                                                                 BNFinal fin, const Tw* w, const Tw* b, Tw* rmean,
+                                                                 Tw* rvar, bool bump) {
+  // bump: this launch also advances num_batches_tracked (the host sets it only for a fixed momentum,
+  // where no thread reads the counter)
+  if (bump && fin.num_batches && blockIdx.x == 0 && threadIdx.x == 0) *fin.num_batches += 1;
+  __shared__ float sh[2][kMergeRows][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float s1, s2;
+  merge_rows(G, C, c, cl, rg, 0, G, part, sh, s1, s2);
+  if (rg != 0 || c >= C) return;
+  merge_finalize<Tw>(c, s1, s2, n, fin, w, b, rmean, rvar);
+}
+
+// segment totals seg[s][2][C] (blockIdx.y = s)
+__global__ __launch_bounds__(64 * kMergeRows) void k_merge_segs(int G, int C, int SG, const float* __restrict__ part,
+                                                                float* __restrict__ seg) {
+  __shared__ float sh[2][kMergeRows][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl, s = blockIdx.y;
+  const int R = (G + SG - 1) / SG, g0 = s * R, g1 = min(G, g0 + R);
+  float s1, s2;
+  merge_rows(G, C, c, cl, rg, g0, g1, part, sh, s1, s2);
+  if (rg != 0 || c >= C) return;
+  seg[((int64_t)s * 2) * C + c] = s1;
+  seg[((int64_t)s * 2 + 1) * C + c] = s2;
+}
+
+template <typename Tw>
+__global__ __launch_bounds__(kBlock) void k_merge_segs_final(int C, int SG, const float* __restrict__ seg, float n,
+                                                             BNFinal fin, const Tw* w, const Tw* b, Tw* rmean,
+                                                             Tw* rvar, bool bump) {
+  if (bump && fin.num_batches && blockIdx.x == 0 && threadIdx.x == 0) *fin.num_batches += 1;
+  const int c = blockIdx.x * kBlock + threadIdx.x;
+  if (c >= C) return;
+  float s1 = 0.f, s2 = 0.f;
+  for (int s = 0; s < SG; ++s) {
+    s1 += seg[((int64_t)s * 2) * C + c];
+    s2 += seg[((int64_t)s * 2 + 1) * C + c];
+  }
+  merge_finalize<Tw>(c, s1, s2, n, fin, w, b, rmean, rvar);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1146,11 +1192,21 @@ void bn_merge_sums(int C, const float* sums, const BNFinal& fin, int dt_w, const
 }
 
 void bn_merge_parts(int G, int C, const float* part, float count, const BNFinal& fin, int dt_w, const void* w,
-                    const void* b, void* rmean, void* rvar, hipStream_t st, bool bump) {
+                    const void* b, void* rmean, void* rvar, hipStream_t st, bool bump, float* seg_ws) {
   if (bump && fin.momentum < 0.f) throw std::runtime_error("bn_merge_parts: bump needs a fixed momentum");
-  BN_DISPATCH(dt_w, Tw,
-      hipLaunchKernelGGL((k_merge_parts<Tw>), dim3((C + 63) / 64), dim3(64 * kMergeRows), 0, st, G, C, part, count,
-                         fin, (const Tw*)w, (const Tw*)b, (Tw*)rmean, (Tw*)rvar, bump));
+  const int SG = bn_part_segments(G);
+  if (SG == 1) {
+    BN_DISPATCH(dt_w, Tw,
+        hipLaunchKernelGGL((k_merge_parts<Tw>), dim3((C + 63) / 64), dim3(64 * kMergeRows), 0, st, G, C, part, count,
+                           fin, (const Tw*)w, (const Tw*)b, (Tw*)rmean, (Tw*)rvar, bump));
+  } else {
+    if (!seg_ws) throw std::runtime_error("bn_merge_parts: G needs a segment workspace [bn_part_segments(G), 2, C]");
+    hipLaunchKernelGGL(k_merge_segs, dim3((C + 63) / 64, SG), dim3(64 * kMergeRows), 0, st, G, C, SG, part, seg_ws);
+    check_launch("bn_merge_parts (segments)");
+    BN_DISPATCH(dt_w, Tw,
+        hipLaunchKernelGGL((k_merge_segs_final<Tw>), dim3((C + kBlock - 1) / kBlock), dim3(kBlock), 0, st, C, SG,
+                           seg_ws, count, fin, (const Tw*)w, (const Tw*)b, (Tw*)rmean, (Tw*)rvar, bump));
+  }
   check_launch("bn_merge_parts");
 }
 

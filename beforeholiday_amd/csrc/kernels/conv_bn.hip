@@ -447,29 +447,38 @@ __global__ __launch_bounds__(64 * kSumRows) void k_sum_parts(int G, int N, const
                                                              float* __restrict__ gb) {
   // block = 64 columns x kSumRows row groups of one statistic (blockIdx.y); coalesced 256-byte rows,
   // a fixed order (strided per group, then the groups in order): deterministic
+  // the rows in the bn_part_segments order (one segment after the other here; bn_merge_parts sums
+  // large-G segments in parallel with the same bits)
   __shared__ float sh[kSumRows][64];
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl, which = blockIdx.y;
-  float acc = 0.f;
-  if (c < N) {
-    const float* src = part + (int64_t)which * G * N + c;
-    int g = rg;
-    // 8 rows of loads in flight per lane; the adds stay in row order (bn_merge_parts sums alike)
-    for (; g + 7 * kSumRows < G; g += 8 * kSumRows) {
-      float u[8];
+  const int SG = bn_part_segments(G), R = (G + SG - 1) / SG;
+  float t = 0.f;
+  for (int s = 0; s < SG; ++s) {
+    const int g1 = min(G, (s + 1) * R);
+    float acc = 0.f;
+    if (c < N) {
+      const float* src = part + (int64_t)which * G * N + c;
+      int g = s * R + rg;
+      // 8 rows of loads in flight per lane; the adds stay in row order
+      for (; g + 7 * kSumRows < g1; g += 8 * kSumRows) {
+        float u[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) u[j] = src[(int64_t)(g + j * kSumRows) * N];
+        for (int j = 0; j < 8; ++j) u[j] = src[(int64_t)(g + j * kSumRows) * N];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc += u[j];
+        for (int j = 0; j < 8; ++j) acc += u[j];
+      }
+      for (; g < g1; g += kSumRows) acc += src[(int64_t)g * N];
     }
-    for (; g < G; g += kSumRows) acc += src[(int64_t)g * N];
-  }
-  sh[rg][cl] = acc;
-  __syncthreads();
-  if (rg == 0 && c < N) {
-    float t = 0.f;
+    if (s > 0) __syncthreads();  // the previous segment's reads of sh are done
+    sh[rg][cl] = acc;
+    __syncthreads();
+    float st = 0.f;
 #pragma unroll
-    for (int q = 0; q < kSumRows; ++q) t += sh[q][cl];
+    for (int q = 0; q < kSumRows; ++q) st += sh[q][cl];
+    t += st;
+  }
+  if (rg == 0 && c < N) {
     sums[(int64_t)which * N + c] = t;
     if (which == 0 && gb) gb[c] = t;
     if (which == 1 && gw) gw[c] = t * invstd[c];

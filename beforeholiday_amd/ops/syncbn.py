@@ -114,7 +114,7 @@ def merge_sums(sums, weight, bias, running_mean, running_var, momentum, eps, num
 def merge_parts(part, count, weight, bias, running_mean, running_var, momentum, eps, num_batches=None, bump=False):
     """Single rank: :func:`merge_sums` straight from a convolution epilogue's partials ``part [2, G, C]``
     (sums of ``x - running_mean`` and its square per workgroup) over ``count`` elements per channel --
-    one kernel on the GPU instead of ``conv_bn.sum_parts`` + ``merge_sums``. ``bump`` (fixed momentum
+    one kernel on the GPU (two from 1024 partial rows) instead of ``conv_bn.sum_parts`` + ``merge_sums``. ``bump`` (fixed momentum
     only) also advances ``num_batches`` by one in the same launch."""
     if part.is_cuda:
         return _native().merge_parts(part, float(count), weight, bias, running_mean, running_var, momentum, eps,

@@ -417,7 +417,7 @@ def test_fused_resnet_residual_grad_folded_into_conv1(mode):
 
 
 @pytest.mark.parametrize("device", devices())
-@pytest.mark.parametrize("G,C", [(1, 64), (37, 256), (515, 2048)])
+@pytest.mark.parametrize("G,C", [(1, 64), (37, 256), (515, 2048), (1024, 64), (2048, 64), (7168, 128), (20000, 192)])
 def test_merge_parts_equals_sum_parts_then_merge_sums(device, G, C):
     """Single-rank finalize from conv-epilogue partials [2, G, C] (one kernel) == sum_parts +
     merge_sums, bit for bit (same summation order), including the running-stat update; and both match
