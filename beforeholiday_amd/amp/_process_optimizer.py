@@ -20,7 +20,10 @@ masters and write the 16-bit model parameters (the reference's mixed-precision L
 csrc/multi_tensor_lamb_mp.cu:41,248,367; FusedSGD's 4-list copy, apex/optimizers/fused_sgd.py:245-252).
 Neither the fp32 master gradients nor the separate master-to-model pass exist on that path. Anything
 that needs the master gradients before the step (``amp.master_params``, a second ``scale_loss``
-accumulating into the same step) materialises them first, so the unfused semantics are kept.
+accumulating into the same step) materialises them first, so the unfused semantics are kept. The
+path is OPT-IN (``Config.amp_fused_master_step``; the benchmarks turn it on): while a fused step is
+pending the masters reachable through ``optimizer.param_groups`` have ``.grad is None``, so gradient
+clipping or inspection must go through ``amp.master_params(optimizer)``, which materialises them.
 
 Three plans: :class:`_MasterPlan` (O2 / O5: fp32 master copies replace the 16-bit parameters inside
 the optimizer), :class:`_FusedSGDMasterPlan` (FusedSGD folds the unscale into its kernel unless
@@ -39,9 +42,10 @@ from ..ops import amp_C
 
 _LOW = (torch.float16, torch.bfloat16)
 
-# the fused mixed-precision step (module docstring; Config.amp_fused_master_step); False keeps the
-# unscale + step + copy sequence
-fused_master_step = True
+# the fused mixed-precision step (module docstring; Config.amp_fused_master_step, opt-in); False (the
+# default) keeps the reference's unscale + step + copy sequence, so the fp32 master gradients are
+# populated in optimizer.param_groups after scale_loss exits
+fused_master_step = False
 
 
 def _apply_config(c):

@@ -237,3 +237,11 @@ class LossScaler(object):
             self._loss_scale = min(self._max_loss_scale, self._loss_scale * self._scale_factor)
             self._unskipped = 0
         return should_skip
+
+
+def _apply_config(c):
+    # config.set(amp_python_scaler=...) / config.override take effect on the class flag too
+    LossScaler.has_fused_kernel = not c.amp_python_scaler
+
+
+_config.on_change(_apply_config)

@@ -40,8 +40,9 @@ class Config:
         "device-resident dynamic loss scale: no host sync per step, overflow skips on the device")))
     amp_python_scaler: bool = field(default=False, metadata=dict(env="BH_AMP_PYTHON_SCALER", doc=(
         "the reference's python-only scaler (per-tensor checks, no multi-tensor kernel); tests")))
-    amp_fused_master_step: bool = field(default=True, metadata=dict(env="BH_AMP_FUSED_MASTER", doc=(
-        "O2/O5 + FusedLAMB/FusedAdam: the step reads the scaled 16-bit grads and writes the model copy")))
+    amp_fused_master_step: bool = field(default=False, metadata=dict(env="BH_AMP_FUSED_MASTER", doc=(
+        "opt-in, O2/O5 + FusedLAMB/FusedAdam: the step reads the scaled 16-bit grads and writes the model "
+        "copy; the fp32 master .grad stay None until amp.master_params() (clip through it, not param_groups)")))
     # -- ResNet / convolution paths (models/resnet.py)
     fold_bn: bool = field(default=True, metadata=dict(env="BH_FOLD_BN", doc=(
         "BatchNorm statistics / apply folded into the convolutions")))
@@ -88,8 +89,8 @@ class Config:
         "time MFMA vs hipBLASLt per dense shape once")))
     gemm_tile: int = field(default=0, metadata=dict(env="BH_GEMM_TILE", native="gemm_tile", choices=(0, 1, 2, 3, 4),
                                                     doc="GEMM tile: 0 auto, 1 small, 2 big, 3 mid, 4 ping-pong"))
-    gemm_log: bool = field(default=False, metadata=dict(env="BH_GEMM_LOG", native="gemm_log", doc=(
-        "log the GEMM kernel picked per shape (debugging)")))
+    gemm_log: bool = field(default=False, metadata=dict(env="BH_GEMM_LOG", native="gemm_log", rank_checked=False,
+                                                        doc="log the GEMM kernel picked per shape (debugging)"))
 
     def __post_init__(self):
         for f in dataclasses.fields(self):
@@ -116,12 +117,30 @@ class Config:
         return cls(**kw)
 
     def digest(self) -> str:
-        text = ";".join(f"{f.name}={getattr(self, f.name)!r}" for f in dataclasses.fields(self))
-        return hashlib.sha256(text.encode()).hexdigest()[:16]
+        """Hash of every field that changes what a rank computes. Diagnostic fields
+        (``rank_checked=False``) are left out, and the GEMM table enters by its CONTENT, so two ranks
+        reading copies of one table at different paths agree."""
+        parts = []
+        for f in dataclasses.fields(self):
+            if not f.metadata.get("rank_checked", True):
+                continue
+            v = getattr(self, f.name)
+            if f.name == "gemm_table" and v:
+                v = _file_digest(v)
+            parts.append(f"{f.name}={v!r}")
+        return hashlib.sha256(";".join(parts).encode()).hexdigest()[:16]
 
     def native_knobs(self) -> Dict[str, int]:
         return {f.metadata["native"]: int(getattr(self, f.name)) for f in dataclasses.fields(self)
                 if "native" in f.metadata}
+
+
+def _file_digest(path: str) -> str:
+    try:
+        with open(path, "rb") as fh:
+            return "sha256:" + hashlib.sha256(fh.read()).hexdigest()
+    except OSError:
+        return "missing:" + os.path.basename(path)
 
 
 # legacy spellings of the pre-config environment values

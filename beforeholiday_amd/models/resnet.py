@@ -736,7 +736,7 @@ class _Conv1x1BNFn(torch.autograd.Function):
                     # dX = dY . W (+ the parked residual gradient), masked by the previous block's output ReLU,
                     # with its column sums: that block's tail (_ConvBNResFn) skips its mask pass
                     gx2d, part = conv_bn.c1x1(gy2d, w2d, resid=r2d, epi="mask", mbits=ml.bits, b_trans=True)
-                    ml.sg, ml.ptr = part[0], gx2d.data_ptr()
+                    ml.sg, ml.ptr, ml.ver = part[0], gx2d.data_ptr(), gx2d._version
                 elif fast and _link_ok(link, c) and conv_bn.supported(gy2d, w2d, resid=r2d is not None, epi="bwd",
                                                                       b_trans=True):
                     y2d = link.y.permute(0, 2, 3, 1).reshape(-1, c)
@@ -1056,13 +1056,15 @@ class _BNConvFn(torch.autograd.Function):
 class _MaskLink(object):
     """Hands a residual block's saved ReLU bit mask to the node that produces the gradient of that block's
     output (the next block's conv1 data gradient): it applies the mask in its epilogue and leaves the column
-    sums there (``sg``), and records the tensor it wrote (``ptr``) so the block's backward can tell that the
-    gradient it receives is exactly that one (autograd added nothing to it) and skip its own mask pass."""
+    sums there (``sg``), and records the tensor it wrote (``ptr``) and that tensor's version counter (``ver``)
+    so the block's backward can tell that the gradient it receives is exactly that one: a second consumer of
+    the block output (a feature tap, a hook, an auxiliary head) makes autograd's InputBuffer accumulate into
+    the same storage in place, which keeps the pointer but bumps the version."""
 
-    __slots__ = ("bits", "ptr", "sg", "__weakref__")
+    __slots__ = ("bits", "ptr", "ver", "sg", "__weakref__")
 
     def __init__(self, bits):
-        self.bits, self.ptr, self.sg = bits, None, None
+        self.bits, self.ptr, self.ver, self.sg = bits, None, None, None
 
 
 class _FoldCfg(object):
@@ -1179,13 +1181,14 @@ class _ConvBNResFn(torch.autograd.Function):
         N = w3.size(0)
         g_out = g_out.contiguous(memory_format=torch.channels_last)
         ml = ctx.mlink
-        if ml is not None and ml.ptr is not None and ml.ptr == g_out.data_ptr() and ml.sg is not None:
+        if ml is not None and ml.ptr is not None and ml.ptr == g_out.data_ptr() and ml.sg is not None \
+                and ml.ver == g_out._version:
             # the producer already applied the mask and summed the columns (and nothing was added since)
             g2d, sg_ws = g_out.permute(0, 2, 3, 1).reshape(-1, N), ml.sg
         else:  # (masking is idempotent: a gradient summed from a masked and an unmasked part is handled too)
             g2d, sg_ws = bn_fold.mask_colsum_partials(g_out.permute(0, 2, 3, 1).reshape(-1, N), bits)
         if ml is not None:
-            ml.ptr = ml.sg = None
+            ml.ptr = ml.sg = ml.ver = None
         g = g2d.view(n, h, w, N).permute(0, 3, 1, 2)  # bn3's masked output gradient = z's gradient
         W = w3.view(N, K)
         ps, ph = (scale_i, shift_i) if ctx.pro else (None, None)

@@ -163,6 +163,9 @@ def main():
     require_native("bench")
     if not args.host_scaler:
         config.set(amp_device_scaler=True)  # amp/scaler.py enable_device_mode: no host sync per step
+    # the fused mixed-precision LAMB / Adam step (opt-in: amp/_process_optimizer.py): the step reads the scaled
+    # fp16 gradients and writes the fp16 model copy itself; the bench never clips through param_groups
+    config.set(amp_fused_master_step=True)
     set_stats_mode(args.syncbn_stats)
     config.check_ranks()  # every rank runs the same typed configuration (raises otherwise)
     torch.manual_seed(1234 + rank)

@@ -61,6 +61,9 @@ def main():
         from beforeholiday_amd import config
 
         config.set(amp_device_scaler=True)
+    from beforeholiday_amd import config
+
+    config.set(amp_fused_master_step=True)  # opt-in fused mixed-precision step (amp/_process_optimizer.py)
     from beforeholiday_amd.parallel import DistributedDataParallel
     from beforeholiday_amd.transformer import parallel_state, tensor_parallel
 

@@ -79,7 +79,9 @@ def main():
     assert dist.get_world_size() == world
     dp = world // tp
 
-    from beforeholiday_amd import amp
+    from beforeholiday_amd import amp, config
+
+    config.set(amp_fused_master_step=True)  # opt-in fused mixed-precision step (amp/_process_optimizer.py)
     from beforeholiday_amd._native import require_native
     from beforeholiday_amd.models import GPTModel, TransformerConfig, finalize_model_grads
     from beforeholiday_amd.optimizers import FusedAdam

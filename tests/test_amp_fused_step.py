@@ -181,3 +181,37 @@ def test_fused_plan_flow_cpu(monkeypatch):
     assert not opt._amp_stash.plan.fused_pending()
     for a, b in zip(want, got):
         assert torch.equal(a, b)
+
+
+def test_default_populates_param_group_grads_cpu():
+    """The fused step is opt-in: by default the fp32 masters in ``optimizer.param_groups``
+    carry their gradients when ``scale_loss`` exits, so clipping through the param groups clips what the
+    step applies. With the fused step on, ``amp.master_params`` (the documented clipping route)
+    materialises the same gradients, and clipping through it changes the step's input."""
+    config.set(amp_device_scaler=False)
+    assert config.Config().amp_fused_master_step is False
+    x = torch.randn(16, 32).half()
+    y = torch.randint(0, 8, (16,))
+
+    amp, model, opt = _cpu_setup()
+    opt._amp_fused_ok = lambda: True  # even where the fused kernels exist, the default path is unfused
+    with amp.scale_loss(F.cross_entropy(model(x).float(), y), opt) as s:
+        s.backward()
+    group_params = [p for g in opt.param_groups for p in g["params"]]
+    assert all(p.grad is not None for p in group_params)
+    assert not opt._amp_stash.plan.fused_pending()
+    before = torch.cat([p.grad.reshape(-1) for p in group_params]).norm()
+    torch.nn.utils.clip_grad_norm_(group_params, max_norm=float(before) / 4)
+    after = torch.cat([p.grad.reshape(-1) for p in group_params]).norm()
+    torch.testing.assert_close(after, before / 4, rtol=1e-3, atol=0)
+
+    config.set(amp_fused_master_step=True)
+    amp, model, opt = _cpu_setup()
+    opt._amp_fused_ok = lambda: True
+    with amp.scale_loss(F.cross_entropy(model(x).float(), y), opt) as s:
+        s.backward()
+    assert opt._amp_stash.plan.fused_pending()
+    masters = list(amp.master_params(opt))  # materialises: the step falls back to the unfused kernels
+    assert all(p.grad is not None for p in masters)
+    assert not opt._amp_stash.plan.fused_pending()
+    torch.testing.assert_close(torch.cat([p.grad.reshape(-1) for p in masters]).norm(), before, rtol=1e-3, atol=0)

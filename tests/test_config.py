@@ -31,12 +31,12 @@ def test_set_override_and_module_globals():
     import beforeholiday_amd.models.resnet as R
 
     base = config.get()
-    with config.override(ds_fold="off", bn_res_fold="all", mask_producer="fast", amp_fused_master_step=False):
+    with config.override(ds_fold="off", bn_res_fold="all", mask_producer="fast", amp_fused_master_step=True):
         assert R._DS_FOLD is False and R._BN_RES_FOLD == "all"
         assert R._MASK_PRODUCER and not R._MASK_PRODUCER_ANY
-        assert po.fused_master_step is False
+        assert po.fused_master_step is True
         assert config.get().digest() != base.digest()
-    assert config.get() == base and R._DS_FOLD is True and po.fused_master_step is True
+    assert config.get() == base and R._DS_FOLD is True and po.fused_master_step is False
     with pytest.raises(ValueError):
         config.set(fold_apply="sideways")
     assert config.get() == base
@@ -72,3 +72,25 @@ def _ranks(rank, world):
 
 def test_check_ranks_two_gloo_ranks():
     run_distributed(_ranks, 2)
+
+
+def test_digest_ignores_diagnostics_and_table_path(tmp_path):
+    """a rank that only turns GEMM logging on, or reads the same GEMM table from another
+    path, computes the same numbers and must pass check_ranks; a different table must not."""
+    base = config.Config()
+    assert dataclasses.replace(base, gemm_log=True).digest() == base.digest()
+    a, b, c = tmp_path / "a.csv", tmp_path / "sub_b.csv", tmp_path / "c.csv"
+    a.write_text("Validator,x\nGemm,1\n")
+    b.write_text("Validator,x\nGemm,1\n")
+    c.write_text("Validator,x\nGemm,2\n")
+    da, db, dc = (dataclasses.replace(base, gemm_table=str(p)).digest() for p in (a, b, c))
+    assert da == db and da != dc
+    assert dataclasses.replace(base, fold_apply="none").digest() != base.digest()
+
+
+def test_python_scaler_flag_follows_config():
+    from beforeholiday_amd.amp.scaler import LossScaler
+
+    with config.override(amp_python_scaler=True):
+        assert LossScaler.has_fused_kernel is False
+    assert LossScaler.has_fused_kernel is (not config.get().amp_python_scaler)

@@ -265,3 +265,30 @@ def test_fused_resnet_two_ranks_equals_one_rank_double_batch(exchange):
     from _dist import run_distributed
 
     run_distributed(_net_two_ranks, 2, exchange)
+
+
+@pytest.mark.gpu
+def test_block_output_with_second_consumer():
+    """a folded block's output feeds the next block AND a second consumer (a feature tap).
+    Autograd then accumulates the tap's gradient into the next block's masked conv1 data gradient in
+    place: same storage, new version. The tail must notice (mask link version check) and redo its mask
+    + column sums, so the result matches fp32 PyTorch blocks with the same tap."""
+    R, ref_a, blk_a = _block(256, 64, 1, torch.float16)
+    torch.manual_seed(1)
+    _, ref_b, blk_b = _block(256, 64, 1, torch.float16)
+    x = torch.randn(8, 256, 56, 56, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    tap = torch.randn(8, 256, 56, 56, device="cuda")
+    xr = x.float().clone().requires_grad_()
+    xf = x.clone().requires_grad_()
+    outs = []
+    for a, b, xx in ((ref_a, ref_b, xr), (blk_a, blk_b, xf)):
+        ya = a(xx)
+        yb = b(ya)
+        loss = yb.float().square().sum() / 64 + (ya.float() * tap).sum()
+        loss.backward()
+        outs.append(yb)
+    assert _rel(outs[1], outs[0]) < 2e-2
+    assert _rel(xf.grad, xr.grad) < 6e-2
+    for blk, ref in ((blk_a, ref_a), (blk_b, ref_b)):
+        for (n, p), q in zip(blk.named_parameters(), ref.parameters()):
+            assert _rel(p.grad, q.grad) < 6e-2, n
