@@ -77,9 +77,11 @@ class Config:
         "flash kernels also for sk <= 128 (benchmarks)")))
     fused_mlp: bool = field(default=True, metadata=dict(env="BH_FUSED_MLP", doc="fused MLP block in transformer_lm"))
     flash_attn: bool = field(default=True, metadata=dict(env="BH_FLASH_ATTN", doc="flash attention in transformer_lm"))
-    dense_wgrad_mfma: bool = field(default=True, metadata=dict(env="BH_DENSE_WGRAD", doc=(
-        "dense weight gradients on the MFMA wgrad kernel")))
+    dense_wgrad_mfma: bool = field(default=True, metadata=dict(env="BH_DENSE_WGRAD", native="dense_wgrad", doc=(
+        "dense weight gradients on the MFMA kernels (gemm_tn / 1x1 wgrad, bindings/dense.cpp weight_grad)")))
     embed_native: bool = field(default=True, metadata=dict(env="BH_EMBED_NATIVE", doc="native embedding backward"))
+    ln_residual_grad: bool = field(default=True, metadata=dict(env="BH_LN_RESID", doc=(
+        "pre-LN blocks: the residual add's input gradient is summed inside the LayerNorm dx kernel")))
     gemm_table: str = field(default="", metadata=dict(env="BH_GEMM_TABLE", doc=(
         "tuned GEMM dispatch table path ('' = the packaged default)")))
     # -- native switches (pushed into the extension, bh::knob)

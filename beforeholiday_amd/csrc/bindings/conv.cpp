@@ -400,6 +400,19 @@ at::Tensor conv3x3_s2_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t H
 
 }  // namespace
 
+// The dense layers' weight gradient dW [N, K] = dy [T, N]^T . x [T, K] on the 1x1 weight-gradient kernel
+// (tokens as a 1 x 1 x T image); false when the kernel does not take the shape (dense.cpp weight_grad)
+bool dense_wgrad_conv(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out) {
+  if (!(dy.dim() == 2 && x.dim() == 2 && dy.is_contiguous() && x.is_contiguous() && dy.size(0) == x.size(0)))
+    return false;
+  const int64_t T = dy.size(0), N = dy.size(1), K = x.size(1);
+  const at::Tensor x4 = x.view({1, 1, T, K}).permute({0, 3, 1, 2});
+  const at::Tensor dy4 = dy.view({1, 1, T, N}).permute({0, 3, 1, 2});
+  if (!wgrad_supported(x4, dy4, 1, 1)) return false;
+  out = conv_wgrad(x4, dy4, 1, 1, c10::nullopt, c10::nullopt).view({N, K});
+  return true;
+}
+
 void register_conv(pybind11::module_& root) {
   auto m = root.def_submodule("conv_cuda", "direct 3x3 stride-1 NHWC convolution (MFMA implicit GEMM)");
   m.def("conv3x3_forward", &conv3x3_forward, py::arg("x"), py::arg("weight"),

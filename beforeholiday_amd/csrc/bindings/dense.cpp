@@ -2,10 +2,12 @@
 // (reference APIs: csrc/fused_dense_base.cpp:15-20, csrc/mlp.cpp:46-164,
 // csrc/megatron/fused_weight_gradient_dense.cpp).
 //
-// GEMMs go to hipBLASLt through ATen (at::addmm folds the bias into the GEMM epilogue; the fp32
-// weight-gradient accumulation uses addmm's out_dtype form so bf16/fp16 products accumulate in
-// place into the fp32 main_grad, C == D). Activation, dActivation and bias-gradient reductions are
-// the HIP kernels in kernels/dense.hip.
+// One implementation behind both the Python layers (ops/fused_dense.py) and the reference-named
+// extensions: forward GEMMs with bias / activation epilogues on the MFMA kernel (gemm.hip) where the
+// static rule picks it, data gradients through data_grad (MFMA dActivation + bias-gradient epilogue,
+// hipBLASLt for a plain dY . W where the library measured faster), weight gradients through
+// weight_grad (gemm_tn.hip for large weights, the 1x1 weight-gradient kernel for smaller ones, the
+// library GEMM otherwise). Activation, dActivation and bias-gradient passes are kernels/dense.hip.
 #include "common.h"
 #include "bh/knobs.h"
 
@@ -237,6 +239,57 @@ std::vector<at::Tensor> linear_dact(const at::Tensor& dy, const at::Tensor& wt, 
   return {dx, run_lib()};
 }
 
+// dx = (dy . w) * act'(aux) and its column sum, w [N, K] as the layer stores it. The MFMA kernel needs the
+// weight transposed ([K, N] rows), so the transpose runs only when that kernel takes the call.
+std::vector<at::Tensor> data_grad(const at::Tensor& dy, const at::Tensor& w, const at::Tensor& aux, int act,
+                                  bool want_bgrad) {
+  const bool fused_work = act != bh::kActNone || want_bgrad || g_force_mfma;
+  const bool t16 = w.dim() == 2 && w.is_contiguous() && w.element_size() == 2 && w.size(0) % 8 == 0 &&
+                   w.size(1) % 8 == 0 && w.scalar_type() == dy.scalar_type();
+  if (!fused_work || !t16 || !mfma_enabled()) {
+    auto dx = at::mm(dy, w);
+    at::Tensor db;
+    if (act != bh::kActNone || want_bgrad) db = act_backward(dx, aux, dx, act, want_bgrad);
+    return {dx, db};
+  }
+  auto wt = at::empty({w.size(1), w.size(0)}, w.options());
+  bh::transpose16(w.data_ptr(), w.size(0), w.size(1), wt.data_ptr(), stream_for(w));
+  return linear_dact(dy, wt, aux, act, want_bgrad);
+}
+
+}  // namespace
+
+bool dense_wgrad_conv(const at::Tensor& dy, const at::Tensor& x, at::Tensor& out);  // bindings/conv.cpp
+
+namespace {
+
+// The static weight-gradient rules (identical on every rank): the transposed-operand MFMA GEMM
+// (kernels/gemm_tn.hip) from 1.5M-element weights on (1.12-1.28x hipBLASLt at 8192 tokens,
+// profiles/wgrad_tn_vs_hipblaslt.jsonl), the 1x1 weight-gradient kernel up to ~2.4M elements
+// (1.05-2.4x the library at 512^2 .. 3072 x 768), both from 4096 tokens; the library GEMM otherwise.
+constexpr int64_t kWgradMinTokens = 4096, kWgradTnMinElems = 1536 * 1024, kWgradConvMaxElems = 3072 * 800;
+
+at::Tensor weight_grad(const at::Tensor& dy_in, const at::Tensor& x_in) {
+  const at::Tensor dy = as2d(dy_in), x = as2d(x_in);
+  const int64_t T = dy.size(0), N = dy.size(1), K = x.size(1);
+  const bool mfma = bh::knob("dense_wgrad", 1) != 0 && dy.scalar_type() == x.scalar_type() &&
+                    (dy.scalar_type() == at::kHalf || dy.scalar_type() == at::kBFloat16) && T >= kWgradMinTokens &&
+                    dy.stride(-1) == 1 && x.stride(-1) == 1;
+  if (mfma && N * K >= kWgradTnMinElems &&
+      bh::gemm_tn_supported(N, K, T, dy.stride(0), x.stride(0), dy.data_ptr(), x.data_ptr(), dy.data_ptr())) {
+    auto out = at::empty({N, K}, dy.options());
+    const int s = bh::gemm_tn_splits(N, K, T);
+    at::Tensor ws;
+    if (s > 1) ws = at::empty({(int64_t)s, N, K}, dy.options().dtype(at::kFloat));
+    bh::gemm_tn(dtype_code(dy.scalar_type()), dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), out.data_ptr(),
+                N, K, T, s > 1 ? ws.data_ptr<float>() : nullptr, s, stream_for(dy));
+    return out;
+  }
+  at::Tensor out;
+  if (mfma && N * K <= kWgradConvMaxElems && dense_wgrad_conv(dy, x, out)) return out;
+  return at::mm(dy.t(), x);
+}
+
 // ------------------------------------------------------------------------------------------------
 // fused_dense_cuda
 // ------------------------------------------------------------------------------------------------
@@ -254,9 +307,8 @@ std::vector<at::Tensor> linear_bias_backward(at::Tensor input, at::Tensor weight
   check_cuda(input, "input");
   auto x = as2d(input.contiguous());
   auto dy = as2d(d_output.contiguous());
-  auto d_input = at::mm(dy, weight).view(input.sizes());
-  auto d_weight = at::mm(dy.t(), x);
-  return {d_input, d_weight, bias_grad(dy)};
+  auto d_input = data_grad(dy, weight.contiguous(), at::Tensor(), bh::kActNone, false)[0].view(input.sizes());
+  return {d_input, weight_grad(dy, x), bias_grad(dy)};
 }
 
 std::vector<at::Tensor> linear_gelu_linear_forward(at::Tensor input, at::Tensor weight1, at::Tensor bias1,
@@ -276,12 +328,12 @@ std::vector<at::Tensor> linear_gelu_linear_backward(at::Tensor input, at::Tensor
   auto x = as2d(input.contiguous());
   auto dy = as2d(d_output2.contiguous());
   auto h = as2d(output1.contiguous());
-  auto d_weight2 = at::mm(dy.t(), h);
+  auto d_weight2 = weight_grad(dy, h);
   auto d_bias2 = bias_grad(dy);
-  auto dh = linear_dact(dy, weight2.t().contiguous(), as2d(gelu_in.contiguous()), bh::kActGelu, true);
+  auto dh = data_grad(dy, weight2.contiguous(), as2d(gelu_in.contiguous()), bh::kActGelu, true);
   auto d_h = dh[0], d_bias1 = dh[1];
-  auto d_weight1 = at::mm(d_h.t(), x);
-  auto d_input = at::mm(d_h, weight1).view(input.sizes());
+  auto d_weight1 = weight_grad(d_h, x);
+  auto d_input = data_grad(d_h, weight1.contiguous(), at::Tensor(), bh::kActNone, false)[0].view(input.sizes());
   return {d_input, d_weight1, d_bias1, d_weight2, d_bias2};
 }
 
@@ -328,14 +380,16 @@ std::vector<at::Tensor> mlp_backward(int use_bias, int activation, at::Tensor gr
   if (act == bh::kActNone) dpre = g;
   for (int64_t i = n - 1; i >= 0; --i) {
     const at::Tensor& x = (i == 0) ? inputs[0] : outputs[i - 1];
-    grads[1 + i] = at::mm(dpre.t(), x.contiguous());
+    grads[1 + i] = weight_grad(dpre, x.contiguous());
     if (use_bias) grads[1 + n + i] = db;
     if (i > 0) {
-      auto r = linear_dact(dpre, inputs[1 + i].t().contiguous(), outputs[i - 1].contiguous(), act, use_bias != 0);
+      auto r = data_grad(dpre, inputs[1 + i].contiguous(), outputs[i - 1].contiguous(), act, use_bias != 0);
       dpre = r[0];
       db = r[1];
     } else {
-      g = inputs[0].requires_grad() ? at::mm(dpre, inputs[1]) : at::Tensor();
+      g = inputs[0].requires_grad()
+              ? data_grad(dpre, inputs[1].contiguous(), at::Tensor(), bh::kActNone, false)[0]
+              : at::Tensor();
     }
   }
   grads[0] = inputs[0].requires_grad() ? g : at::zeros_like(inputs[0]);
@@ -436,6 +490,16 @@ void register_dense(pybind11::module_& root) {
   fd.def("linear_gelu_linear_forward", &linear_gelu_linear_forward);
   fd.def("linear_gelu_linear_backward", &linear_gelu_linear_backward);
   fd.def("act_forward", &act_forward_py, py::arg("x"), py::arg("bias"), py::arg("act"));
+  fd.def("weight_grad", [](at::Tensor dy, at::Tensor x) {
+    check_cuda(dy, "dy");
+    return weight_grad(dy, x);
+  }, py::arg("dy"), py::arg("x"), "dW = dy^T . x for 2-D [tokens, out] / [tokens, in] (static MFMA / library rule)");
+  fd.def("data_grad", [](at::Tensor dy, at::Tensor w, c10::optional<at::Tensor> aux, int act, bool want_bgrad) {
+    check_cuda(dy, "dy");
+    return data_grad(dy.contiguous(), w.contiguous(), aux.has_value() ? aux->contiguous() : at::Tensor(), act,
+                     want_bgrad);
+  }, py::arg("dy"), py::arg("w"), py::arg("aux"), py::arg("act"), py::arg("want_bgrad"),
+     "(dy . w) * act'(aux) and its column sum; w [out, in] as stored");
   fd.def("act_backward", &act_backward_py, py::arg("dy"), py::arg("aux"), py::arg("act"), py::arg("want_bgrad"));
   fd.def("embedding_backward", &embedding_bwd, py::arg("dy"), py::arg("ids"), py::arg("num_weights"),
          py::arg("padding_idx") = -1, "deterministic embedding weight gradient [num_weights, H], no host sync");

@@ -62,7 +62,7 @@ std::vector<at::Tensor> fwd_impl(at::Tensor input, at::IntArrayRef shape, at::Te
 // backward: returns (grad_input, grad_gamma, grad_beta) (grads undefined when not affine)
 std::vector<at::Tensor> bwd_impl(at::Tensor dout, at::Tensor mean, at::Tensor invvar, at::Tensor input_or_output,
                                  at::IntArrayRef shape, at::Tensor gamma, at::Tensor beta, double eps, bool rms,
-                                 bool memory_efficient) {
+                                 bool memory_efficient, at::Tensor dresid = at::Tensor()) {
   check_cuda(dout, "grad_output");
   dout = dout.contiguous();
   at::Tensor xin = input_or_output.contiguous();
@@ -70,7 +70,12 @@ std::vector<at::Tensor> bwd_impl(at::Tensor dout, at::Tensor mean, at::Tensor in
   if (beta.defined()) beta = beta.contiguous();
   auto d = dims_of(xin, shape);
   auto dx = at::empty_like(xin);
-  const bool vec = use_vec(d.n2, {dout, xin, gamma, beta, dx});
+  if (dresid.defined()) {
+    dresid = dresid.contiguous();
+    TORCH_CHECK(dresid.scalar_type() == dx.scalar_type() && dresid.numel() == dx.numel() && dresid.is_cuda(),
+                "layer_norm backward: dresid must match the input's dtype and size");
+  }
+  const bool vec = use_vec(d.n2, {dout, xin, gamma, beta, dx, dresid});
   hipStream_t s = stream_for(xin);
   // memory-efficient backward recomputes x_hat from the output: mean is not saved and never read
   const float* mp = (rms || memory_efficient) ? nullptr : mean.data_ptr<float>();
@@ -79,7 +84,7 @@ std::vector<at::Tensor> bwd_impl(at::Tensor dout, at::Tensor mean, at::Tensor in
   TORCH_CHECK(invvar.numel() == d.n1, "layer_norm backward: invvar has ", invvar.numel(), " elements, expected ", d.n1);
   bh::ln_backward_dx(d.n1, d.n2, dtype_code(dout.scalar_type()), dout.data_ptr(), dtype_code(xin.scalar_type()),
                      xin.data_ptr(), mp, invvar.data_ptr<float>(), wc(gamma), wp(gamma), wp(beta), dx.data_ptr(), rms,
-                     memory_efficient, vec, s);
+                     memory_efficient, vec, s, dresid.defined() ? dresid.data_ptr() : nullptr);
   at::Tensor gg, gb;
   if (gamma.defined()) {
     gg = at::empty_like(gamma);
@@ -117,8 +122,10 @@ std::vector<at::Tensor> rms_forward(at::Tensor input, at::IntArrayRef shape, dou
 }
 std::vector<at::Tensor> backward_affine(at::Tensor dout, at::Tensor mean, at::Tensor invvar,
                                         at::Tensor input_or_output, at::IntArrayRef shape, at::Tensor gamma,
-                                        at::Tensor beta, double eps, bool memory_efficient) {
-  return bwd_impl(dout, mean, invvar, input_or_output, shape, gamma, beta, eps, false, memory_efficient);
+                                        at::Tensor beta, double eps, bool memory_efficient,
+                                        c10::optional<at::Tensor> dresid) {
+  return bwd_impl(dout, mean, invvar, input_or_output, shape, gamma, beta, eps, false, memory_efficient,
+                  dresid.has_value() ? *dresid : at::Tensor());
 }
 at::Tensor backward(at::Tensor dout, at::Tensor mean, at::Tensor invvar, at::Tensor input_or_output,
                     at::IntArrayRef shape, double eps, bool memory_efficient) {
@@ -151,7 +158,7 @@ void register_norms(pybind11::module_& root) {
   m.def("rms_forward", &rms_forward);
   m.def("backward_affine", &backward_affine, py::arg("dout"), py::arg("mean"), py::arg("invvar"),
         py::arg("input_or_output"), py::arg("normalized_shape"), py::arg("gamma"), py::arg("beta"), py::arg("eps"),
-        py::arg("memory_efficient") = false);
+        py::arg("memory_efficient") = false, py::arg("dresid") = py::none());
   m.def("backward", &backward, py::arg("dout"), py::arg("mean"), py::arg("invvar"), py::arg("input_or_output"),
         py::arg("normalized_shape"), py::arg("eps"), py::arg("memory_efficient") = false);
   m.def("rms_backward_affine", &rms_backward_affine, py::arg("dout"), py::arg("invvar"), py::arg("input_or_output"),

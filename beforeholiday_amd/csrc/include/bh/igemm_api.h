@@ -16,10 +16,13 @@
 
 namespace bh {
 
+// (int tables: the kernel indexes them with a uniform runtime tap, which the compiler turns into
+// scalar s_load_dword from the kernel arguments; byte tables became vector global_load_ubyte + a
+// vmcnt wait on every k-step)
 struct IgemmPhase {
   int ntaps = 0, py = 0, px = 0;
-  signed char oy[9] = {}, ox[9] = {};
-  unsigned char tap[9] = {};
+  int oy[9] = {}, ox[9] = {};
+  int tap[9] = {};
 };
 
 struct IgemmArgs {

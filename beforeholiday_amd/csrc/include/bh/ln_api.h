@@ -15,7 +15,9 @@ void ln_forward(int64_t n1, int n2, int dt_x, const void* x, int dt_w, const voi
 // dx; xin is the input x, or the output y when from_output (memory-efficient mode)
 void ln_backward_dx(int64_t n1, int n2, int dt_dy, const void* dy, int dt_x, const void* xin, const float* mean,
                     const float* invvar, int dt_w, const void* gamma, const void* beta, void* dx, bool rms,
-                    bool from_output, bool vec, hipStream_t st);
+                    bool from_output, bool vec, hipStream_t st, const void* dresid = nullptr);
+// (dresid: optional [n1, n2] tensor of dx's dtype added to dx in the same pass -- the gradient the
+// residual branch of a pre-LN block sends to the same input, reference layer_norm.cuh:474 dout_resid)
 int ln_wgrad_splits(int64_t n1, int n2);
 // grad_gamma / grad_beta (may be null); partials: 2 * splits * n2 floats of scratch
 void ln_backward_wgrad(int64_t n1, int n2, int dt_dy, const void* dy, int dt_x, const void* xin, const float* mean,

@@ -167,13 +167,16 @@ __global__ __launch_bounds__(kThreads, 2) void k_gram(const T* __restrict__ a, i
     __syncthreads();
   };
   t8 va[IPT][8], vb[IPT][8];
-  if (ch0 < ch1) load(ch0, va);
-  for (int64_t ch = ch0; ch < ch1; ch += 2) {
-    if (ch + 1 < ch1) load(ch + 1, vb);
-    process(ch, va);
-    if (ch + 1 < ch1) {
-      if (ch + 2 < ch1) load(ch + 2, va);
-      process(ch + 1, vb);
+  // (prefetches unconditional, clamped to the last chunk -- re-read, never used -- so the compiler's
+  // vmcnt bookkeeping stays exact instead of merging the paths into vmcnt(0))
+  if (ch0 < ch1) {
+    const int64_t last = ch1 - 1;
+    load(ch0, va);
+    for (int64_t ch = ch0; ch < ch1; ch += 2) {
+      load(ch + 1 < ch1 ? ch + 1 : last, vb);
+      process(ch, va);
+      load(ch + 2 < ch1 ? ch + 2 : last, va);
+      if (ch + 1 < ch1) process(ch + 1, vb);
     }
   }
 

@@ -55,9 +55,9 @@ constexpr int kPix = 144;   // LDS bytes per halo pixel: 128 data + 16 pad
 constexpr int kMaxHC = 40;  // halo columns G * (lanes per image + 2) <= 40
 constexpr int kHaloBytes = (kTH + 2) * kMaxHC * kPix;
 constexpr int kWBytes = kBN * 128;
-constexpr int kHaloPer = ((kTH + 2) * kMaxHC * 8 + kThreads - 1) / kThreads;  // 16-byte pieces per thread
 constexpr int kMaxProC = 512;                 // input channels the BatchNorm prologue covers
 constexpr int kProBytes = 2 * kMaxProC * 4;   // its scale / shift in LDS
+constexpr int kOutOfRange = 0x7ff00000;       // a byte offset past every tensor the kernel reads
 
 struct Geo {
   int G, gw, HC, XT, YT, tiles, tpw;  // tpw: consecutive windows per workgroup
@@ -100,8 +100,9 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
   const T* X = reinterpret_cast<const T*>(a.x);
   const T* Wt = reinterpret_cast<const T*>(a.w);
   const int C = a.C, H = a.H, W = a.W, N = a.N;
-  const int nch = C / kCK, per_tile = nch * 9, steps = ntile * per_tile;
+  const int nch = C / kCK;
   constexpr int npieces = (kTH + 2) * HC * 8;
+  constexpr int kHaloPer = (npieces + kThreads - 1) / kThreads;  // 16-byte halo pieces per thread: 11 / 12 / 13
   if constexpr (PRO) {
     for (int c = tid; c < C; c += kThreads) {
       ss[c] = a.pro_scale[c];
@@ -123,24 +124,32 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
   };
 
   // ---- halo staging: registers (prefetch) -> LDS ----
+  // Buffer loads through a whole-tensor resource: a padding pixel gets an offset past the tensor and
+  // comes back as zeros (no select at the LDS store), the per-lane offset is 32-bit.
+  const __amdgpu_buffer_rsrc_t rsX =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(X), (short)0, (int)((int64_t)N * H * W * C * 2), 0x00020000);
   i4v hreg[kHaloPer];
-  uint32_t hmask = 0;
+  uint32_t hmask = 0;  // PRO: in-image pieces (the prologue must not turn the zero padding into relu(shift))
   int hc0 = 0;  // first input channel of the staged chunk (the prologue's scale / shift)
   auto halo_load = [&](int t, int c0) __attribute__((always_inline)) {
     int n0, y0, x0;
     origin(t, n0, y0, x0);
-    hmask = 0;
     hc0 = c0;
+    // the piece coordinates below depend on the thread only; hoisted out of the chunk loop they would
+    // hold ~2 VGPRs per piece across the whole loop (it spilled them, and every scratch reload is a
+    // vmcnt(0)): the empty asm makes them look per-chunk, so they are recomputed (~10 VALU per piece)
+    int tq = tid;
+    asm volatile("" : "+v"(tq));
 #pragma unroll
     for (int i = 0; i < kHaloPer; ++i) {
-      const int q = tid + i * kThreads, pix = q >> 3, ch = q & 7;
+      const int q = tq + i * kThreads, pix = q >> 3, ch = q & 7;
       const int hr = pix / HC, hc = pix - hr * HC;
       const int gi = hc / (GW + 2), jj = hc - gi * (GW + 2);
       const int n = n0 + gi, y = y0 - 1 + hr, x = x0 - 1 + jj;
       const bool ok = q < npieces && n < N && y >= 0 && y < H && x >= 0 && x < W;
-      const int off = ok ? ((n * H + y) * W + x) * C + c0 + ch * 8 : 0;  // < 2^31 (host check)
-      hreg[i] = *reinterpret_cast<const i4v*>(X + off);
-      hmask |= (ok ? 1u : 0u) << i;
+      const int off = ok ? (((n * H + y) * W + x) * C + c0 + ch * 8) * 2 : kOutOfRange;
+      hreg[i] = __builtin_amdgcn_raw_buffer_load_b128(rsX, off, 0, 0);
+      if constexpr (PRO) hmask = (hmask & ~(1u << i)) | ((ok ? 1u : 0u) << i);
     }
   };
   auto halo_store = [&]() __attribute__((always_inline)) {
@@ -166,30 +175,32 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
           t8 e = __builtin_bit_cast(t8, v);
 #pragma unroll
           for (int j = 0; j < 8; ++j) e[j] = from_f<T>(fmaxf(fmaf(to_f<T>(e[j]), sc[j], sh[j]), 0.f));
-          v = __builtin_bit_cast(i4v, e);
+          v = ((hmask >> i) & 1u) ? __builtin_bit_cast(i4v, e) : i4v{0, 0, 0, 0};
         }
-        *reinterpret_cast<i4v*>(halo + (q >> 3) * kPix + (q & 7) * 16) = ((hmask >> i) & 1u) ? v : i4v{0, 0, 0, 0};
+        *reinterpret_cast<i4v*>(halo + (q >> 3) * kPix + (q & 7) * 16) = v;
       }
     }
   };
   // ---- weight slice of step (chunk, r * 3 + s): W[k0 .. k0+63][r][s][c0 .. c0+63] ----
-  // Two register slots, two steps of lookahead: the slice of step t + 2 is requested at the start of
+  // Three register slots, two steps of lookahead: the slice of step t + 2 is requested at the start of
   // step t and written to LDS at the end of step t + 1, so an L2 round trip (longer than one step's
-  // 16 MFMAs per wave) never sits between the barrier of one step and the MFMAs of the next. The step
-  // loop is unrolled by two so the slots stay statically named.
-  i4v wr0[2], wr1[2];
-  auto w_load = [&](int step, i4v(&wreg)[2]) {
-    const int within = step % per_tile, chunk = within / 9, rs = within - chunk * 9;
+  // 16 MFMAs per wave) never sits between the barrier of one step and the MFMAs of the next.
+  const __amdgpu_buffer_rsrc_t rsW =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(Wt), (short)0, (int)((int64_t)a.K * 9 * C * 2), 0x00020000);
+  // per-lane part of the slice offsets (the (chunk, rs) part is uniform)
+  int wvoff[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int p = tid + i * kThreads, row = p >> 3, ch = p & 7;
-      if (FLIP)  // image row = input channel c (= w's output channel), 64 contiguous k
-        wreg[i] = *reinterpret_cast<const i4v*>(Wt + ((chunk * kCK + row) * 9 + (8 - rs)) * a.K + k0 + ch * 8);
-      else
-        wreg[i] = *reinterpret_cast<const i4v*>(Wt + ((k0 + row) * 9 + rs) * C + chunk * kCK + ch * 8);
-    }
+  for (int i = 0; i < 2; ++i) {
+    const int p = tid + i * kThreads, row = p >> 3, ch = p & 7;
+    wvoff[i] = FLIP ? (row * 9 * a.K + k0 + ch * 8) * 2 : ((k0 + row) * 9 * C + ch * 8) * 2;
+  }
+  auto w_load = [&](int chunk, int rs, i4v(&wreg)[2]) __attribute__((always_inline)) {
+    // FLIP: image row = input channel c (= w's output channel), 64 contiguous k
+    const int so = FLIP ? (chunk * kCK * 9 + (8 - rs)) * a.K * 2 : (rs * C + chunk * kCK) * 2;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) wreg[i] = __builtin_amdgcn_raw_buffer_load_b128(rsW, wvoff[i] + so, 0, 0);
   };
-  auto w_store = [&](char* buf, const i4v(&wreg)[2]) {
+  auto w_store = [&](char* buf, const i4v(&wreg)[2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int p = tid + i * kThreads;
@@ -271,72 +282,88 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
     }
   };
 
+  // ---- main loop: one iteration = one 64-channel chunk of one window = the nine (r, s) steps, with
+  // rs a compile-time constant, and every global load unconditional (the prefetch of the slice two
+  // steps ahead and of the next chunk's halo always target a valid slice / window). The compiler's
+  // vmcnt bookkeeping then stays exact: with the conditional loads of the round-5 loop it merged the
+  // paths into vmcnt(0) ahead of every weight store, so each step waited for the slice it had just
+  // requested two steps ahead (profiles/conv_pmc_r6.md). The slice of step t sits in register slot
+  // t % 3 = rs % 3 (a chunk is nine steps), in LDS buffer t & 1.
+  i4v wr[3][2];
+  const int nchunks = ntile * nch;
   zero_acc();
   halo_load(tile0, 0);
-  w_load(0, wr0);
+  w_load(0, 0, wr[0]);
   halo_store();
-  w_store(wb, wr0);
-  if (steps > 1) w_load(1, wr1);
+  w_store(wb, wr[0]);
+  w_load(0, 1, wr[1]);
   __syncthreads();
-  // step t: request slice t + 2 into `nxt2` (free: its slice t went to LDS at the end of step t - 1),
-  // compute from LDS buffer t & 1, write slice t + 1 (`nxt`, requested a step ago) to buffer (t + 1) & 1
-  auto step_body = [&](int t, i4v(&nxt2)[2], const i4v(&nxt)[2]) __attribute__((always_inline)) {
-    const int it = t / per_tile, within = t - it * per_tile;
-    const int chunk = within / 9, rs = within - chunk * 9;
-    const bool last_rs = rs == 8;
-    // the next (window, chunk) whose halo is prefetched during this chunk
-    const bool more = chunk + 1 < nch || it + 1 < ntile;
-    if (t + 2 < steps) w_load(t + 2, nxt2);
-    if (rs == 0 && more) {
-      if (chunk + 1 < nch) halo_load(tile0 + it, (chunk + 1) * kCK);
-      else halo_load(tile0 + it + 1, 0);
-    }
-    const char* wcur = wb + (t & 1) * kWBytes;
-    const int r = rs / 3, s = rs - r * 3;
-    const char* hb0 = halo + ((2 * wave + r) * HC + hcol + s) * kPix;  // window row 2w, offset (r, s)
-    const char* hb1 = hb0 + HC * kPix;                                    // window row 2w + 1
-    // fragments of k-step kk + 1 are read while the MFMAs of kk run (two register sets)
-    auto frags = [&](int kk, i4v (&f)[4]) {
-      const int ch = 2 * kk + h;
-      if (FLIP) {
-        f[0] = frag_tr(wcur, 16 * kk + 8 * h, 0, lane);
-        f[1] = frag_tr(wcur, 16 * kk + 8 * h, 32, lane);
-      } else {
-        f[0] = *reinterpret_cast<const i4v*>(wcur + wsw(r32, ch));
-        f[1] = *reinterpret_cast<const i4v*>(wcur + wsw(32 + r32, ch));
-      }
-      f[2] = *reinterpret_cast<const i4v*>(hb0 + ch * 16);
-      f[3] = *reinterpret_cast<const i4v*>(hb1 + ch * 16);
-    };
-    i4v fa[4], fb[4];
-    frags(0, fa);
+  for (int cidx = 0; cidx < nchunks; ++cidx) {
+    const int it = cidx / nch, chunk = cidx - it * nch;
+    const int nchunk = chunk + 1 == nch ? 0 : chunk + 1;  // chunk of the slices after rs = 8
+    // the (window, chunk) whose halo is prefetched during this chunk: the next one, or this window's
+    // first chunk again after the last (loaded, stored, never read)
+    const int htile = (chunk + 1 == nch && it + 1 < ntile) ? tile0 + it + 1 : tile0 + it;
+    const char* wbase = wb + (cidx & 1) * kWBytes;  // buffer of rs = 0 (9 is odd: parity flips per chunk)
 #pragma unroll
-    for (int kk = 0; kk < 4; kk += 2) {
-      frags(kk + 1, fb);
-      acc[0][0] = Mfma32<T>::run(fa[2], fa[0], acc[0][0]);
-      acc[0][1] = Mfma32<T>::run(fa[3], fa[0], acc[0][1]);
-      acc[1][0] = Mfma32<T>::run(fa[2], fa[1], acc[1][0]);
-      acc[1][1] = Mfma32<T>::run(fa[3], fa[1], acc[1][1]);
-      if (kk + 2 < 4) frags(kk + 2, fa);
-      acc[0][0] = Mfma32<T>::run(fb[2], fb[0], acc[0][0]);
-      acc[0][1] = Mfma32<T>::run(fb[3], fb[0], acc[0][1]);
-      acc[1][0] = Mfma32<T>::run(fb[2], fb[1], acc[1][0]);
-      acc[1][1] = Mfma32<T>::run(fb[3], fb[1], acc[1][1]);
+    for (int rs = 0; rs < 9; ++rs) {
+      if (rs + 2 < 9) w_load(chunk, rs + 2, wr[(rs + 2) % 3]);
+      else w_load(nchunk, rs + 2 - 9, wr[(rs + 2) % 3]);
+      if (rs == 0) halo_load(htile, nchunk * kCK);
+      const char* wcur = (rs & 1) ? wb + kWBytes - (wbase - wb) : wbase;  // buffer (t & 1)
+      const int r = rs / 3, s = rs - r * 3;
+      const char* hb0 = halo + ((2 * wave + r) * HC + hcol + s) * kPix;  // window row 2w, offset (r, s)
+      const char* hb1 = hb0 + HC * kPix;                                    // window row 2w + 1
+      auto frags = [&](int kk, i4v (&f)[4]) __attribute__((always_inline)) {
+        const int ch = 2 * kk + h;
+        if (FLIP) {
+          f[0] = frag_tr(wcur, 16 * kk + 8 * h, 0, lane);
+          f[1] = frag_tr(wcur, 16 * kk + 8 * h, 32, lane);
+        } else {
+          f[0] = *reinterpret_cast<const i4v*>(wcur + wsw(r32, ch));
+          f[1] = *reinterpret_cast<const i4v*>(wcur + wsw(32 + r32, ch));
+        }
+        f[2] = *reinterpret_cast<const i4v*>(hb0 + ch * 16);
+        f[3] = *reinterpret_cast<const i4v*>(hb1 + ch * 16);
+      };
+      // software pipeline over the four k-steps with two fragment sets: the reads of k-step kk + 2 are
+      // issued right after the MFMAs of kk (which free that set) and before those of kk + 1, so each
+      // read group has four MFMAs (>= 128 cycles) to land; the scheduling barriers keep the compiler
+      // from sinking the reads behind the MFMAs and reusing one set (read, lgkmcnt(0), 4 MFMAs, ...)
+      auto mfma4 = [&](const i4v (&f)[4]) __attribute__((always_inline)) {
+        acc[0][0] = Mfma32<T>::run(f[2], f[0], acc[0][0]);
+        acc[0][1] = Mfma32<T>::run(f[3], f[0], acc[0][1]);
+        acc[1][0] = Mfma32<T>::run(f[2], f[1], acc[1][0]);
+        acc[1][1] = Mfma32<T>::run(f[3], f[1], acc[1][1]);
+      };
+      i4v fa[4], fb[4];
+      frags(0, fa);
+      frags(1, fb);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma4(fa);
+      __builtin_amdgcn_sched_barrier(0);
+      frags(2, fa);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma4(fb);
+      __builtin_amdgcn_sched_barrier(0);
+      frags(3, fb);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma4(fa);
+      mfma4(fb);
+      __builtin_amdgcn_sched_barrier(0);
+      // slice t + 1 (requested a step ago) into the other buffer: every wave finished reading it at the
+      // barrier that ended step t - 1
+      w_store(wb + kWBytes - (wcur - wb), wr[(rs + 1) % 3]);
+      if (rs == 8) {
+        __syncthreads();  // every wave is done with this chunk's halo
+        halo_store();
+        if (chunk + 1 == nch) {  // window done: results out, accumulators reset
+          epilogue(tile0 + it);
+          zero_acc();
+        }
+      }
+      __syncthreads();
     }
-    if (t + 1 < steps) w_store(wb + ((t + 1) & 1) * kWBytes, nxt);
-    if (last_rs && chunk + 1 == nch) {  // window done: results out, accumulators reset
-      epilogue(tile0 + it);
-      zero_acc();
-    }
-    if (last_rs && more) {
-      __syncthreads();  // every wave is done with this chunk's halo
-      halo_store();
-    }
-    __syncthreads();
-  };
-  for (int t = 0; t < steps; t += 2) {
-    step_body(t, wr0, wr1);
-    if (t + 1 < steps) step_body(t + 1, wr1, wr0);
   }
   if constexpr (EPI == kConvEpiStats || EPI == kConvEpiBwd) {
     // per-workgroup partial of each statistic: lane halves, then the 4 waves (LDS, the halo is free)
@@ -386,7 +413,8 @@ bool conv3x3_supported(const Conv3x3Args& a) {
   if (a.epi == kConvEpiBwd && (!a.by || !al(a.by) || !a.bscale || !a.bshift || !a.bmean)) return false;
   if (a.epi == kConvEpiAffine && (!a.a_scale || !a.a_shift || a.pro_scale)) return false;
   return a.N > 0 && a.H > 0 && a.W > 0 && a.C > 0 && a.K > 0 && a.C % kCK == 0 && a.K % kBN == 0 && al(a.x) &&
-         al(a.w) && al(a.y) && pix * a.C < (1ll << 31) && pix * a.K < (1ll << 31);  // 32-bit offsets
+         al(a.w) && al(a.y) && pix * a.C * 2 + 128 < kOutOfRange && pix * a.K < (1ll << 31) &&
+         (int64_t)a.K * 9 * a.C * 2 < kOutOfRange;  // 32-bit byte offsets in the buffer loads
 }
 
 namespace {

@@ -401,13 +401,17 @@ __global__ __launch_bounds__(kThreads, 2) void k_c1x1(C1x1Args p, Geo g) {
       if constexpr (RES || EPI == kC1x1Bwd || EPI == kC1x1Mask) __builtin_amdgcn_sched_barrier(0);
     }
   };
-  if (total > 0) load(0, a0, y0);
-  for (int i = 0; i < total; i += 2) {
-    if (i + 1 < total) load(i + 1, a1, y1);
-    process(i, a0, y0);
-    if (i + 1 < total) {
-      if (i + 2 < total) load(i + 2, a0, y0);
-      process(i + 1, a1, y1);
+  // prefetches are unconditional (clamped to the last strip: re-read, never used), so the compiler's
+  // vmcnt bookkeeping stays exact across iterations; behind `if (i + 1 < total)` it merged the paths
+  // into a full vmcnt(0) drain before each strip's A rows (profiles/conv_pmc_r6.md)
+  if (total > 0) {
+    const int last = total - 1;
+    load(0, a0, y0);
+    for (int i = 0; i < total; i += 2) {
+      load(min(i + 1, last), a1, y1);
+      process(i, a0, y0);
+      load(min(i + 2, last), a0, y0);
+      if (i + 1 < total) process(i + 1, a1, y1);
     }
   }
 

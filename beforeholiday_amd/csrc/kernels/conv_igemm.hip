@@ -176,21 +176,22 @@ __global__ __launch_bounds__(kThreads, 2) void k_igemm(IgemmArgs a, int tiles_m)
   b_load(0, br);
   b_store(buf0, br);
   __syncthreads();  // weight slice 0 (and the prologue constants) visible
+  // Every prefetch is unconditional (past the last k-step it re-reads the last one, never used): with the
+  // loads behind `if (s + 1 < steps)` the compiler's vmcnt bookkeeping merged the two paths and waited
+  // for EVERYTHING (vmcnt(0)) ahead of each weight store, including the A fragments just requested for
+  // the next k-step (profiles/conv_pmc_r6.md). (The compute of the odd tail step stays conditional: it
+  // issues no global load.)
+  const int last = steps - 1;
   for (int s = 0; s < steps; s += 2) {
-    if (s + 1 < steps) {
-      a_load(s + 1, a1, m1);
-      b_load(s + 1, br);
-    }
+    a_load(min(s + 1, last), a1, m1);
+    b_load(min(s + 1, last), br);
     compute(buf0, a0, m0, s);
-    if (s + 1 < steps) b_store(buf1, br);
+    b_store(buf1, br);
     __syncthreads();
-    if (s + 1 >= steps) break;
-    if (s + 2 < steps) {
-      a_load(s + 2, a0, m0);
-      b_load(s + 2, br);
-    }
-    compute(buf1, a1, m1, s + 1);
-    if (s + 2 < steps) b_store(buf0, br);
+    a_load(min(s + 2, last), a0, m0);
+    b_load(min(s + 2, last), br);
+    if (s + 1 < steps) compute(buf1, a1, m1, s + 1);
+    b_store(buf0, br);
     __syncthreads();
   }
 
@@ -344,9 +345,9 @@ IgemmArgs igemm_conv3x3_s2_fwd(const void* x, const void* w, void* y, int N, int
   IgemmPhase& p = a.ph[0];
   p.ntaps = 9;
   for (int t = 0; t < 9; ++t) {
-    p.oy[t] = (signed char)(t / 3 - 1);
-    p.ox[t] = (signed char)(t % 3 - 1);
-    p.tap[t] = (unsigned char)t;
+    p.oy[t] = t / 3 - 1;
+    p.ox[t] = t % 3 - 1;
+    p.tap[t] = t;
   }
   return a;
 }
@@ -382,9 +383,9 @@ IgemmArgs igemm_conv3x3_s2_dgrad(const void* dy, const void* wt, void* dx, int N
       if ((rr & 1) == py) continue;  // parity: 2 yo + rr - 1 == 2 i + py needs rr odd for py = 0, even for 1
       for (int sc = 0; sc < 3; ++sc) {
         if ((sc & 1) == px) continue;
-        p.oy[p.ntaps] = (signed char)((py + 1 - rr) / 2);
-        p.ox[p.ntaps] = (signed char)((px + 1 - sc) / 2);
-        p.tap[p.ntaps] = (unsigned char)(rr * 3 + sc);
+        p.oy[p.ntaps] = (py + 1 - rr) / 2;
+        p.ox[p.ntaps] = (px + 1 - sc) / 2;
+        p.tap[p.ntaps] = rr * 3 + sc;
         ++p.ntaps;
       }
     }

@@ -289,13 +289,16 @@ __global__ __launch_bounds__(256) void k_stem_wgrad(const T* __restrict__ x, con
       }
     }
   };
-  if (blockIdx.x < nrows) load_row(blockIdx.x);
+  // (prefetches unconditional, clamped to the last row -- re-read, never used -- so the compiler's vmcnt
+  // bookkeeping stays exact instead of merging the paths into vmcnt(0))
+  if (nrows <= 0) return;
+  load_row(min((int)blockIdx.x, nrows - 1));
   __syncthreads();  // zero padding written
   store_row();
   __syncthreads();
   for (int row = blockIdx.x; row < nrows; row += gridDim.x) {
     const int next = row + gridDim.x;
-    if (next < nrows) load_row(next);
+    load_row(min(next, nrows - 1));
 #pragma unroll
     for (int ks = 0; ks < kOW / 16; ++ks) {
       // A = dY^T: lane (channel 32 mt + (lane & 31), half h) gets pixels 16 ks + 8 h .. + 7

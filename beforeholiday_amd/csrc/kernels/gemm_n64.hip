@@ -77,7 +77,11 @@ __global__ __launch_bounds__(kThreads) void k_gemm_n64(const T* __restrict__ A, 
 #pragma unroll
     for (int s = 0; s < KS; ++s) a[s] = __builtin_nontemporal_load(reinterpret_cast<const i4v*>(src + 16 * s));
   };
-  if (strip < strips) load(strip);
+  // prefetches are unconditional (clamped to the last strip: re-read, never used) so the compiler's
+  // vmcnt bookkeeping stays exact: the wait for a[] then leaves the previous strip's stores in flight
+  // instead of draining them (a conditional load merged into vmcnt(0), profiles/conv_pmc_r6.md)
+  if (strips <= 0) return;
+  load(min(strip, strips - 1));
   for (; strip < strips; strip += stride) {
     f16v acc[2];
 #pragma unroll
@@ -102,7 +106,7 @@ __global__ __launch_bounds__(kThreads) void k_gemm_n64(const T* __restrict__ A, 
       }
     }
     const int next = strip + stride;
-    if (next < strips) load(next);  // the a[] registers are free once the MFMAs above have read them
+    load(min(next, strips - 1));  // the a[] registers are free once the MFMAs above have read them
     // lane holds C[8 j + 4 h + i][32 t + r] in acc[t][4 j + i]: per store, lanes 0-31 write one
     // 64-byte row segment. (Swapping the operands so each lane holds four consecutive columns, one
     // 8-byte store per row, measured slower: 0.072 vs 0.055 ms at K = 64 -- 32 rows per store.)

@@ -161,7 +161,7 @@ __global__ __launch_bounds__(kBlock) void k_ln_bwd_dx(const Tdy* __restrict__ dy
                                                       const float* __restrict__ mean_in,
                                                       const float* __restrict__ invvar_in, const Tw* __restrict__ g,
                                                       const Tw* __restrict__ b, T* __restrict__ dx, int64_t n1, int n2,
-                                                      bool from_output, bool vec) {
+                                                      bool from_output, bool vec, const T* __restrict__ dres) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
   if (row >= n1) return;
@@ -205,6 +205,12 @@ __global__ __launch_bounds__(kBlock) void k_ln_bwd_dx(const Tdy* __restrict__ dy
     float o[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) o[k] = invvar * (dg[j][k] - m1 - xh[j][k] * m2);
+    if (dres) {  // + the residual branch's gradient of the same input, one rounding
+      float rv[8];
+      load8(dres + row * n2, col, n2, vec, rv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] += rv[k];
+    }
     store8(dx + row * n2, col, n2, vec, o);
   }
 }
@@ -214,7 +220,8 @@ __global__ __launch_bounds__(kBlock) void k_ln_bwd_dx_long(const Tdy* __restrict
                                                            const float* __restrict__ mean_in,
                                                            const float* __restrict__ invvar_in,
                                                            const Tw* __restrict__ g, const Tw* __restrict__ b,
-                                                           T* __restrict__ dx, int n2, bool from_output) {
+                                                           T* __restrict__ dx, int n2, bool from_output,
+                                                           const T* __restrict__ dres) {
   __shared__ float red[kBlock / kWave];
   const int64_t row = blockIdx.x;
   const float mean = (RMS || from_output) ? 0.f : mean_in[row];  // memory-efficient: mean not saved
@@ -238,7 +245,8 @@ __global__ __launch_bounds__(kBlock) void k_ln_bwd_dx_long(const Tdy* __restrict
   const float m2 = block_sum(s2, red) / (float)n2;
   for (int i = threadIdx.x; i < n2; i += kBlock) {
     const float dgv = to_f<Tdy>(dy[row * n2 + i]) * (g ? to_f<Tw>(g[i]) : 1.f);
-    dx[row * n2 + i] = from_f<T>(invvar * (dgv - m1 - xhat(i) * m2));
+    const float rv = dres ? to_f<T>(dres[row * n2 + i]) : 0.f;
+    dx[row * n2 + i] = from_f<T>(invvar * (dgv - m1 - xhat(i) * m2) + rv);
   }
 }
 
@@ -392,7 +400,7 @@ void ln_forward(int64_t n1, int n2, int dt_x, const void* x, int dt_w, const voi
 
 void ln_backward_dx(int64_t n1, int n2, int dt_dy, const void* dy, int dt_x, const void* xin, const float* mean,
                     const float* invvar, int dt_w, const void* gamma, const void* beta, void* dx, bool rms,
-                    bool from_output, bool vec, hipStream_t st) {
+                    bool from_output, bool vec, hipStream_t st, const void* dresid) {
   if (n1 == 0 || n2 == 0) return;
   if (dt_w < 0) dt_w = dt_x;
   const int vpt = vpt_for(n2, 4);
@@ -402,17 +410,17 @@ void ln_backward_dx(int64_t n1, int n2, int dt_dy, const void* dy, int dt_x, con
         LN_VPT_DISPATCH(vpt, V,
             if (rms) hipLaunchKernelGGL((k_ln_bwd_dx<T, Tw, Tdy, V, true>), dim3(grid), dim3(kBlock), 0, st,
                                         (const Tdy*)dy, (const T*)xin, mean, invvar, (const Tw*)gamma,
-                                        (const Tw*)beta, (T*)dx, n1, n2, from_output, vec);
+                                        (const Tw*)beta, (T*)dx, n1, n2, from_output, vec, (const T*)dresid);
             else hipLaunchKernelGGL((k_ln_bwd_dx<T, Tw, Tdy, V, false>), dim3(grid), dim3(kBlock), 0, st,
                                     (const Tdy*)dy, (const T*)xin, mean, invvar, (const Tw*)gamma, (const Tw*)beta,
-                                    (T*)dx, n1, n2, from_output, vec));
+                                    (T*)dx, n1, n2, from_output, vec, (const T*)dresid));
       } else {
         if (rms) hipLaunchKernelGGL((k_ln_bwd_dx_long<T, Tw, Tdy, true>), dim3(n1), dim3(kBlock), 0, st,
                                     (const Tdy*)dy, (const T*)xin, mean, invvar, (const Tw*)gamma, (const Tw*)beta,
-                                    (T*)dx, n2, from_output);
+                                    (T*)dx, n2, from_output, (const T*)dresid);
         else hipLaunchKernelGGL((k_ln_bwd_dx_long<T, Tw, Tdy, false>), dim3(n1), dim3(kBlock), 0, st,
                                 (const Tdy*)dy, (const T*)xin, mean, invvar, (const Tw*)gamma, (const Tw*)beta,
-                                (T*)dx, n2, from_output);
+                                (T*)dx, n2, from_output, (const T*)dresid);
       })));
   check_launch("ln_backward_dx");
 }

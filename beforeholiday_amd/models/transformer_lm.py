@@ -22,6 +22,7 @@ import torch
 from .. import config as _config
 import torch.nn.functional as F
 
+from ..normalization import ResidualGradLink
 from ..ops import fused_dense as _fd
 from ..transformer import parallel_state, tensor_parallel
 from ..transformer.enums import AttnMaskType, AttnType, LayerType, ModelType
@@ -387,9 +388,9 @@ class ParallelAttention(MegatronModule):
         return self.dense(ctx)
 
 
-def bias_dropout_add(x, bias, residual, prob: float, training: bool, model_parallel: bool = False):
+def bias_dropout_add(x, bias, residual, prob: float, training: bool, model_parallel: bool = False, resid_link=None):
     """residual + dropout(x + bias): one fused HIP pass on GPU (ops/fused_dense.py), PyTorch on CPU."""
-    return _fd.bias_dropout_add(x, bias, residual, prob, training, model_parallel)
+    return _fd.bias_dropout_add(x, bias, residual, prob, training, model_parallel, resid_link)
 
 
 class ParallelTransformerLayer(MegatronModule):
@@ -415,17 +416,28 @@ class ParallelTransformerLayer(MegatronModule):
             self.post_inter_attention_layernorm = LayerNorm(config.hidden_size, **ln)
         self.mlp = ParallelMLP(config, init_method, output_layer_init_method)
 
-    def _bda(self, out, bias, residual):
+    def _bda(self, out, bias, residual, link=None):
         # sequence parallel: each TP rank holds a different sequence shard -> its own dropout mask
         # (Megatron forks the model-parallel RNG here); otherwise the replicas must agree
-        return bias_dropout_add(out, bias, residual, self.hidden_dropout, self.training, self.sequence_parallel)
+        return bias_dropout_add(out, bias, residual, self.hidden_dropout, self.training, self.sequence_parallel,
+                                link)
+
+    def _link(self, x):
+        """Pre-LN: x feeds both the LayerNorm and the residual add, so its two gradients are summed by
+        the LayerNorm backward kernel (normalization.ResidualGradLink; Config.ln_residual_grad)."""
+        if (self.apply_residual_connection_post_layernorm or not _config.get().ln_residual_grad or not x.is_cuda
+                or not x.requires_grad or not torch.is_grad_enabled()):
+            return None
+        return ResidualGradLink()
 
     def forward(self, hidden_states, attention_mask, encoder_output=None, enc_dec_attn_mask=None):
-        ln_out = self.input_layernorm(hidden_states)
+        link = self._link(hidden_states)
+        ln_out = self.input_layernorm(hidden_states, resid_link=link)
         attn_out, attn_bias = self.self_attention(ln_out, attention_mask)
         residual = ln_out if self.apply_residual_connection_post_layernorm else hidden_states
-        ln_in = self._bda(attn_out, attn_bias, residual)
-        ln_out = self.post_attention_layernorm(ln_in)
+        ln_in = self._bda(attn_out, attn_bias, residual, link)
+        link = self._link(ln_in) if self.layer_type != LayerType.decoder else None
+        ln_out = self.post_attention_layernorm(ln_in, resid_link=link)
         if self.layer_type == LayerType.decoder:
             attn_out, attn_bias = self.inter_attention(ln_out, enc_dec_attn_mask, encoder_output=encoder_output)
             residual = ln_out if self.apply_residual_connection_post_layernorm else ln_in
@@ -433,7 +445,7 @@ class ParallelTransformerLayer(MegatronModule):
             ln_out = self.post_inter_attention_layernorm(ln_in)
         mlp_out, mlp_bias = self.mlp(ln_out)
         residual = ln_out if self.apply_residual_connection_post_layernorm else ln_in
-        return self._bda(mlp_out, mlp_bias, residual)
+        return self._bda(mlp_out, mlp_bias, residual, link)
 
 
 def get_num_layers(config: TransformerConfig, is_encoder_and_decoder_model: bool = False) -> int:

@@ -30,12 +30,38 @@ def manual_rms_norm(input, normalized_shape, weight, eps):
     return weight * input
 
 
+class ResidualGradLink(object):
+    """Pairs a pre-LN block's LayerNorm with the bias-dropout-add that takes the LayerNorm's INPUT as its
+    residual (models/transformer_lm.py ``ParallelTransformerLayer``). The add's backward parks its residual
+    gradient here instead of returning it, and the LayerNorm backward adds it inside its dx kernel: autograd
+    then never sums the two branch gradients of that input in a separate pass (the reference's fused
+    norm-add LayerNorm backward, apex/contrib/csrc/multihead_attn/layer_norm.cuh:474,566,603).
+
+    ``armed`` is set by the add's forward (only its native path parks gradients); the LayerNorm backward
+    raises if an armed link holds no gradient (the add's backward did not run first), so a changed graph
+    fails loudly instead of dropping the residual gradient."""
+
+    __slots__ = ("armed", "g")
+
+    def __init__(self):
+        self.armed, self.g = False, None
+
+    def take(self):
+        if not self.armed:
+            return None
+        g, self.g, self.armed = self.g, None, False
+        if g is None:
+            raise RuntimeError("ResidualGradLink: the residual add's backward did not run before the LayerNorm's")
+        return g
+
+
 class FusedLayerNormAffineFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, input, weight, bias, normalized_shape, eps, memory_efficient=False):
+    def forward(ctx, input, weight, bias, normalized_shape, eps, memory_efficient=False, resid_link=None):
         ctx.normalized_shape = normalized_shape
         ctx.eps = eps
         ctx.memory_efficient = memory_efficient
+        ctx.resid_link = resid_link
         input_ = input.contiguous()
         weight_ = weight.contiguous()
         bias_ = bias.contiguous()
@@ -49,10 +75,13 @@ class FusedLayerNormAffineFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_output):
         input_or_output, weight_, bias_, mean, invvar = ctx.saved_tensors
+        link = getattr(ctx, "resid_link", None)
+        dres = link.take() if link is not None else None
         grad_input, grad_weight, grad_bias = _ln.backward_affine(
             grad_output.contiguous(), mean, invvar, input_or_output, ctx.normalized_shape, weight_, bias_, ctx.eps,
-            ctx.memory_efficient)
-        return grad_input, grad_weight, grad_bias, None, None, None
+            ctx.memory_efficient, dres)
+        # (as many gradients as inputs: callers that do not pass resid_link apply six)
+        return (grad_input, grad_weight, grad_bias, None, None, None, None)[:len(ctx.needs_input_grad)]
 
 
 class FusedRMSNormAffineFunction(torch.autograd.Function):
@@ -77,10 +106,11 @@ class FusedRMSNormAffineFunction(torch.autograd.Function):
 
 class FusedLayerNormAffineMixedDtypesFunction(FusedLayerNormAffineFunction):
     @staticmethod
-    def forward(ctx, input, weight, bias, normalized_shape, eps, memory_efficient=False):
+    def forward(ctx, input, weight, bias, normalized_shape, eps, memory_efficient=False, resid_link=None):
         ctx.normalized_shape = normalized_shape
         ctx.eps = eps
         ctx.memory_efficient = memory_efficient
+        ctx.resid_link = resid_link
         input_ = input.contiguous()
         weight_ = weight.contiguous()
         bias_ = bias.contiguous()
@@ -146,10 +176,10 @@ class FusedRMSNormFunction(torch.autograd.Function):
         return grad_input, None, None, None
 
 
-def fused_layer_norm_affine(input, weight, bias, normalized_shape, eps=1e-6, memory_efficient=False):
+def fused_layer_norm_affine(input, weight, bias, normalized_shape, eps=1e-6, memory_efficient=False, resid_link=None):
     args = _cast_if_autocast_enabled(input, weight, bias, normalized_shape, eps, memory_efficient)
     with torch.amp.autocast("cuda", enabled=False):
-        return FusedLayerNormAffineFunction.apply(*args)
+        return FusedLayerNormAffineFunction.apply(*args, resid_link)
 
 
 def fused_layer_norm(input, normalized_shape, eps=1e-6, memory_efficient=False):
@@ -213,10 +243,13 @@ class FusedLayerNorm(torch.nn.Module):
             init.ones_(self.weight)
             init.zeros_(self.bias)
 
-    def forward(self, input):
+    def forward(self, input, resid_link=None):
+        """``resid_link`` (:class:`ResidualGradLink`, affine only): the residual add that takes ``input``
+        parks its gradient there and this backward adds it inside the dx kernel."""
         if self.elementwise_affine:
             return fused_layer_norm_affine(input, self.weight, self.bias, self.normalized_shape, self.eps,
-                                           self.memory_efficient)
+                                           self.memory_efficient, resid_link)
+        assert resid_link is None, "resid_link needs the affine LayerNorm"
         return fused_layer_norm(input, self.normalized_shape, self.eps, self.memory_efficient)
 
     def extra_repr(self):

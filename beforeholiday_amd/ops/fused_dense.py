@@ -1,8 +1,13 @@
 """``fused_dense_cuda`` / ``mlp_cuda`` / ``fused_weight_gradient_mlp_cuda`` ops.
 
-GPU tensors run ``beforeholiday_amd._C`` (GEMMs on hipBLASLt via ATen, activation / dActivation /
-bias-grad passes in kernels/dense.hip); CPU tensors run the PyTorch reference below with the same
-semantics (exact-erf GELU; ReLU / sigmoid derivatives taken from the activation output).
+GPU tensors run ``beforeholiday_amd._C`` -- the SAME native entry points that ``import fused_dense_cuda``
+/ ``mlp_cuda`` reach after ``install_apex_aliases()`` (bindings/dense.cpp): forward GEMMs with the bias /
+GELU epilogue on the MFMA kernel (kernels/gemm.hip) where its static rule picks it, data gradients with
+the dActivation + bias-gradient epilogue on the MFMA kernel (hipBLASLt for a plain dY . W), weight
+gradients on the transposed-operand MFMA GEMM (kernels/gemm_tn.hip) or the 1x1 weight-gradient kernel
+(static shape rules, ``weight_grad``), activation / bias-gradient passes in kernels/dense.hip. CPU
+tensors run the PyTorch reference below with the same semantics (exact-erf GELU; ReLU / sigmoid
+derivatives taken from the activation output).
 """
 from typing import List, Optional
 
@@ -76,13 +81,6 @@ def _gemm_ok(*ts):
     return all(t.is_cuda and t.dtype in (torch.float16, torch.bfloat16) for t in ts) and len({t.dtype for t in ts}) == 1
 
 
-def _transposed(w):
-    """w.t().contiguous() through the LDS-tiled transpose kernel (16-byte accesses) where it applies."""
-    if w.dim() == 2 and w.is_contiguous() and w.size(0) % 8 == 0 and w.size(1) % 8 == 0 and w.element_size() == 2:
-        return submodule("gemm").transpose(w)
-    return w.t().contiguous()
-
-
 def linear_bias_forward(input, weight, bias):
     """y = x . W^T + b. 16-bit GPU tensors: the MFMA GEMM with the bias in its epilogue where the static
     dispatch rule of kernels/gemm.hip picks it (K <= 1024, ``gemm.linear_act``), hipBLASLt's addmm
@@ -97,18 +95,12 @@ def linear_bias_forward(input, weight, bias):
 
 
 def linear_bias_backward(input, weight, d_output):
-    """(d_input, d_weight, d_bias). 16-bit GPU tensors: the weight gradient on the MFMA weight-gradient
-    kernel (``weight_grad``: <= ~2.4M-element weights, >= 4096 tokens), the input gradient through
-    ``gemm.linear_dact`` (its rule keeps hipBLASLt for a plain data gradient, where the library
-    measured 1.0-1.18x faster: profiles/dgrad_transformer_nt_vs_hipblaslt.jsonl), the bias gradient as
-    one column-sum pass."""
+    """(d_input, d_weight, d_bias). GPU: one native call (bindings/dense.cpp): the weight gradient by
+    the static MFMA rule (``weight_grad``), the input gradient through ``data_grad`` (hipBLASLt for a
+    plain data gradient, where the library measured 1.0-1.18x faster:
+    profiles/dgrad_transformer_nt_vs_hipblaslt.jsonl), the bias gradient as one column-sum pass."""
     if input.is_cuda:
-        if _gemm_ok(input, weight, d_output):
-            dy = d_output.reshape(-1, d_output.size(-1)).contiguous()
-            x = input.reshape(-1, input.size(-1)).contiguous()
-            dx = submodule("gemm").linear_dact(dy, _transposed(weight), None, ACT_NONE, False)[0]
-            return dx.view(input.shape), weight_grad(dy, x), bias_grad(dy)
-        return _fd().linear_bias_backward(input, weight, d_output)
+        return tuple(_fd().linear_bias_backward(input, weight, d_output))
     dy = d_output.reshape(-1, d_output.size(-1))
     x = input.reshape(-1, input.size(-1))
     return (dy.mm(weight).view(input.shape), dy.t().mm(x), dy.sum(0))
@@ -132,20 +124,11 @@ def linear_gelu_linear_forward(input, weight1, bias1, weight2, bias2):
 
 
 def linear_gelu_linear_backward(input, gelu_in, output1, weight1, weight2, d_output2):
-    """Returns (d_input, d_weight1, d_bias1, d_weight2, d_bias2) — with the dGELU applied. On 16-bit GPU
-    tensors: d(gelu_in) and d_bias1 from one ``gemm.linear_dact`` (dGELU + bias-gradient epilogue), the
-    weight gradients on the MFMA weight-gradient kernel (``weight_grad``)."""
+    """Returns (d_input, d_weight1, d_bias1, d_weight2, d_bias2) -- with the dGELU applied. GPU: one
+    native call: d(gelu_in) and d_bias1 from one MFMA GEMM with the dGELU + bias-gradient epilogue, the
+    weight gradients by the static MFMA rule (bindings/dense.cpp)."""
     if input.is_cuda:
-        if _gemm_ok(input, weight1, weight2, d_output2):
-            gm = submodule("gemm")
-            x = input.reshape(-1, input.size(-1)).contiguous()
-            dy = d_output2.reshape(-1, d_output2.size(-1)).contiguous()
-            h = output1.reshape(-1, output1.size(-1)).contiguous()
-            d_h, d_b1 = gm.linear_dact(dy, _transposed(weight2), gelu_in.reshape(-1, gelu_in.size(-1)).contiguous(),
-                                       ACT_GELU, True)
-            d_in = gm.linear_dact(d_h, _transposed(weight1), None, ACT_NONE, False)[0]
-            return d_in.view(input.shape), weight_grad(d_h, x), d_b1, weight_grad(dy, h), bias_grad(dy)
-        return _fd().linear_gelu_linear_backward(input, gelu_in, output1, weight1, weight2, d_output2)
+        return tuple(_fd().linear_gelu_linear_backward(input, gelu_in, output1, weight1, weight2, d_output2))
     x = input.reshape(-1, input.size(-1))
     dy = d_output2.reshape(-1, d_output2.size(-1))
     d_w2 = dy.t().mm(output1)
@@ -168,34 +151,11 @@ def mlp_forward(use_bias: int, activation: int, inputs: List[torch.Tensor]) -> L
 
 
 def mlp_backward(use_bias: int, activation: int, grad_o, outputs, inputs) -> List[torch.Tensor]:
-    """Gradients for ``inputs``. On the GPU one native call (dActivation + bias gradient inside the
-    data-gradient GEMM's epilogue); the weight gradients of 16-bit layers then go to the MFMA
-    weight-gradient kernel where it applies (``weight_grad``) instead of hipBLASLt."""
+    """Gradients for ``inputs``. On the GPU one native call (bindings/dense.cpp mlp_backward): the
+    dActivation + bias gradient inside the data-gradient GEMM's epilogue, the weight gradients by the
+    static MFMA rule (``weight_grad``)."""
     if inputs[0].is_cuda:
-        if not (_gemm_ok(*inputs) and _gemm_ok(grad_o, *outputs)):
-            return submodule("mlp_cuda").backward(use_bias, activation, grad_o, list(outputs), list(inputs))
-        gm = submodule("gemm")
-        n = (len(inputs) - 1) // 2 if use_bias else len(inputs) - 1
-        act = {0: ACT_NONE, 1: ACT_RELU, 2: ACT_SIGMOID}[activation]
-        grads = [None] * len(inputs)
-        g = grad_o.contiguous()
-        if act == ACT_NONE:
-            dpre, db = g, (bias_grad(g) if use_bias else None)
-        else:
-            dpre, db = act_backward(g, outputs[n - 1].contiguous(), act, bool(use_bias))
-        for i in range(n - 1, -1, -1):
-            x = (inputs[0] if i == 0 else outputs[i - 1]).contiguous()
-            grads[1 + i] = weight_grad(dpre, x)
-            if use_bias:
-                grads[1 + n + i] = db
-            if i > 0:
-                dpre, db = gm.linear_dact(dpre, _transposed(inputs[1 + i]), outputs[i - 1].contiguous(), act,
-                                          bool(use_bias))
-            else:
-                g = (gm.linear_dact(dpre, _transposed(inputs[1]), None, ACT_NONE, False)[0]
-                     if inputs[0].requires_grad else None)
-        grads[0] = g if g is not None else torch.zeros_like(inputs[0])
-        return grads
+        return submodule("mlp_cuda").backward(use_bias, activation, grad_o, list(outputs), list(inputs))
     n = (len(inputs) - 1) // 2 if use_bias else len(inputs) - 1
     act = {0: ACT_NONE, 1: ACT_RELU, 2: ACT_SIGMOID}[activation]
     grads = [None] * len(inputs)
@@ -211,39 +171,14 @@ def mlp_backward(use_bias: int, activation: int, grad_o, outputs, inputs) -> Lis
     return grads
 
 
-# the MFMA weight-gradient kernel (kernels/conv_wgrad.hip, tokens as a 1 x 1 x M image) beats the library
-# GEMM on the transposed-operand product dW = dY^T . X when the weight has at most ~2.4M elements and
-# there are >= 4096 tokens: 1.05-2.4x at 512^2 - 3072 x 768, parity at 3072 x 1024, 0.88x at 4096 x 1024
-# (profiles/wgrad_transformer_shapes.jsonl, with the 256 x 256 wide tiles). A static shape rule: every
-# rank runs the same kernel.
-_WGRAD_MAX_ELEMS = 3072 * 800
-_WGRAD_MIN_TOKENS = 4096
-# the transposed-operand ping-pong GEMM (kernels/gemm_tn.hip, split-K over the tokens) from 1.5M-element
-# weights on: 1.28x hipBLASLt at 3072 x 1024, 1.16x / 1.12x at 4096 x 1024 / 1024 x 4096 (8192 tokens,
-# profiles/wgrad_tn_vs_hipblaslt.jsonl); the 1x1 weight-gradient kernel keeps the 1024 x 1024 projection
-_WGRAD_TN_MIN_ELEMS = 1536 * 1024
-
-
 def weight_grad(d_output: torch.Tensor, input: torch.Tensor) -> torch.Tensor:
     """``d_output^T @ input`` for 2-D ``[tokens, out]`` / ``[tokens, in]`` tensors: the dense layers'
-    weight gradient ``[out, in]`` in ``d_output``'s dtype -- the transposed-operand MFMA GEMM for the large
-    weights, the 1x1 weight-gradient kernel for the smaller ones, else the library GEMM (static shape rules)."""
-    M, K = d_output.shape
-    C = input.size(1)
-    mfma = (_config.get().dense_wgrad_mfma and d_output.is_cuda and d_output.dtype in (torch.float16, torch.bfloat16)
-            and input.dtype == d_output.dtype and M >= _WGRAD_MIN_TOKENS)
-    if mfma and K * C >= _WGRAD_TN_MIN_ELEMS:
-        gm = submodule("gemm")
-        if gm.weight_grad_tn_supported(d_output, input):
-            return gm.weight_grad_tn(d_output, input, 0)
-    if (mfma and K * C <= _WGRAD_MAX_ELEMS and d_output.is_contiguous()
-            and input.is_contiguous()):
-        from . import conv as _conv
-
-        x4 = input.view(1, 1, M, C).permute(0, 3, 1, 2)
-        dy4 = d_output.view(1, 1, M, K).permute(0, 3, 1, 2)
-        if _conv.wgrad_supported(x4, dy4, 1):
-            return submodule("conv_cuda").conv_wgrad(x4, dy4, 1, 1).view(K, C)
+    weight gradient ``[out, in]`` in ``d_output``'s dtype. GPU: bindings/dense.cpp ``weight_grad`` (the
+    transposed-operand MFMA GEMM from 1.5M-element weights, the 1x1 weight-gradient kernel up to ~2.4M
+    elements, both from 4096 tokens, else the library GEMM; static shape rules, the same on every rank
+    and for the reference-named extensions)."""
+    if d_output.is_cuda:
+        return _fd().weight_grad(d_output, input)
     return d_output.t().matmul(input)
 
 
@@ -268,7 +203,7 @@ class _BiasDropoutAddFn(torch.autograd.Function):
     reference: apex/transformer/testing/standalone_transformer_lm.py:188-207 bias_dropout_add)."""
 
     @staticmethod
-    def forward(ctx, x, bias, residual, p, model_parallel=False):
+    def forward(ctx, x, bias, residual, p, model_parallel=False, resid_link=None):
         # host-side seed stream (no device sync): "replicated" is identical on every TP rank,
         # "model-parallel" differs per TP rank (sequence-parallel shards); see random.dropout_seed
         from ..transformer.tensor_parallel.random import dropout_seed
@@ -278,6 +213,10 @@ class _BiasDropoutAddFn(torch.autograd.Function):
         ctx.save_for_backward(keep)
         ctx.p = p
         ctx.has_bias = bias is not None
+        # normalization.ResidualGradLink: the LayerNorm that also reads `residual` adds its gradient in-kernel
+        ctx.resid_link = resid_link if residual.requires_grad else None
+        if ctx.resid_link is not None:
+            ctx.resid_link.armed, ctx.resid_link.g = True, None
         return out.view_as(x)
 
     @staticmethod
@@ -285,7 +224,10 @@ class _BiasDropoutAddFn(torch.autograd.Function):
         (keep,) = ctx.saved_tensors
         want_b = ctx.has_bias and ctx.needs_input_grad[1]
         dx, db = _fd().dropout_backward(dout, keep, ctx.p, want_b)
-        return dx.view_as(dout), (db if want_b else None), dout, None, None
+        dres = dout
+        if ctx.resid_link is not None:
+            ctx.resid_link.g, dres = dout, None
+        return dx.view_as(dout), (db if want_b else None), dres, None, None, None
 
 
 def _bda_native_ok(x, bias, residual) -> bool:
@@ -297,16 +239,20 @@ def _bda_native_ok(x, bias, residual) -> bool:
 
 
 def bias_dropout_add(x: torch.Tensor, bias: Optional[torch.Tensor], residual: torch.Tensor, prob: float,
-                     training: bool, model_parallel: bool = False) -> torch.Tensor:
+                     training: bool, model_parallel: bool = False, resid_link=None) -> torch.Tensor:
     """``residual + dropout(x + bias, prob, training)``; fused HIP kernels on GPU, PyTorch otherwise.
 
     ``model_parallel=True`` (sequence parallelism: every TP rank holds a different shard) draws the
     mask from the per-TP-rank stream -- the fused kernel's model-parallel seed stream, or the
     tracker's "model-parallel-rng" state for the PyTorch fallback; otherwise TP replicas draw
-    identical masks from the replicated stream."""
+    identical masks from the replicated stream.
+
+    ``resid_link`` (normalization.ResidualGradLink, native path only): ``residual``'s gradient is parked
+    there for the LayerNorm that also reads ``residual`` (its backward adds it in-kernel) instead of being
+    returned to autograd."""
     p = float(prob) if training else 0.0
     if _bda_native_ok(x, bias, residual):
-        return _BiasDropoutAddFn.apply(x, bias, residual, p, bool(model_parallel))
+        return _BiasDropoutAddFn.apply(x, bias, residual, p, bool(model_parallel), resid_link)
     if model_parallel and training and prob > 0:
         from ..transformer.tensor_parallel.random import get_cuda_rng_tracker
 

@@ -98,11 +98,18 @@ def _mean_or_empty(mean, ref):
     return mean if mean is not None else ref.new_empty(0, dtype=torch.float32)
 
 
-def backward_affine(dout, mean, invvar, input_or_output, normalized_shape, gamma, beta, eps, memory_efficient=False):
+def backward_affine(dout, mean, invvar, input_or_output, normalized_shape, gamma, beta, eps, memory_efficient=False,
+                    dresid=None):
+    """(grad_input, grad_gamma, grad_beta). ``dresid`` (input-shaped, the input's dtype): a gradient the
+    residual branch sends to the same input, added to grad_input inside the dx kernel (one rounding, no
+    separate add pass: the reference's MHA LayerNorm ``dout_resid``, layer_norm.cuh:474,566,603)."""
     if dout.is_cuda:
         return _n().backward_affine(dout, _mean_or_empty(mean, dout), invvar, input_or_output, normalized_shape, gamma, beta, eps,
-                                    memory_efficient)
-    return _ref_bwd(dout, mean, invvar, input_or_output, normalized_shape, gamma, beta, eps, False, memory_efficient)
+                                    memory_efficient, dresid)
+    gi, gg, gb = _ref_bwd(dout, mean, invvar, input_or_output, normalized_shape, gamma, beta, eps, False, memory_efficient)
+    if dresid is not None:
+        gi = (gi.float() + dresid.float()).to(gi.dtype)
+    return gi, gg, gb
 
 
 def backward(dout, mean, invvar, input_or_output, normalized_shape, eps, memory_efficient=False):

@@ -67,3 +67,98 @@ class GraphedStep:
         """Drop the graph (and its memory pool); the next call captures again."""
         self.graph = None
         self.out = None
+
+
+def training_state(*roots, model=None, optimizer=None):
+    """Every device tensor a training step mutates, for :func:`capture_checked`'s save / restore:
+    the model's parameters and buffers, the optimizer's parameters (amp's fp32 masters) and state,
+    and the tensor attributes (one level deep) of the optimizer, its amp stash and every extra root
+    (loss scalers: device scale / counters / flags; device step counters). Deduplicated by storage
+    pointer + shape."""
+    out, seen = [], set()
+
+    def add(t):
+        if isinstance(t, torch.Tensor) and t.is_cuda and t.numel() > 0:
+            key = (t.data_ptr(), tuple(t.shape), t.dtype)
+            if key not in seen:
+                seen.add(key)
+                out.append(t)
+
+    if model is not None:
+        for t in list(model.parameters()) + list(model.buffers()):
+            add(t)
+    if optimizer is not None:
+        for g in optimizer.param_groups:
+            for p in g["params"]:
+                add(p)
+        for st in optimizer.state.values():
+            for v in (st.values() if isinstance(st, dict) else ()):
+                add(v)
+        roots = roots + (optimizer, getattr(optimizer, "_amp_stash", None))
+    for r in roots:
+        if r is None:
+            continue
+        for v in vars(r).values():
+            if isinstance(v, (list, tuple)):
+                for x in v:
+                    add(x)
+            else:
+                add(v)
+    return out
+
+
+def capture_checked(fn: Callable[[], torch.Tensor], state, watch=(), warmup: int = 2, group=None):
+    """Capture ``fn`` (a training step returning its loss) and PROVE the replay before using it.
+
+    1. capture (a failure on any rank is agreed on by all ranks before anyone replays a collective);
+    2. save ``state`` (:func:`training_state`), replay once, record the loss and ``watch``; restore the
+       saved state, run ``fn`` eagerly, compare loss and ``watch`` BITWISE;
+    3. one MIN all-reduce of the verdict: every rank keeps the graph, or every rank runs eager in this
+       same process (collectives stay matched: the agreement is an eager collective on all ranks).
+
+    Returns ``(runner, report)``: the :class:`GraphedStep` or ``fn`` itself, and a dict for logs. The
+    check costs two steps and one copy of the state; it runs at every world size (world 1 included)."""
+    import torch.distributed as dist
+
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+
+    def agree(ok: bool) -> bool:
+        if not multi:
+            return ok
+        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+        return bool(int(t.item()))
+
+    g = GraphedStep(fn, warmup=warmup)
+    err = None
+    try:
+        g.capture()
+        ok = True
+    except Exception as e:  # noqa: BLE001 - any capture failure means: run eager
+        ok, err = False, f"{type(e).__name__}: {e}"
+        g.reset()
+        torch.cuda.synchronize()
+    if not agree(ok):
+        return fn, {"graph": "eager (capture failed on some rank)", "error": err}
+    saved = [t.detach().clone() for t in state]
+    torch.cuda.synchronize()
+    loss_g = g().detach().clone()
+    got = [loss_g] + [w.detach().clone() for w in watch]
+    with torch.no_grad():
+        for t, s in zip(state, saved):
+            t.copy_(s)
+    loss_e = fn().detach().clone()
+    want = [loss_e] + [w.detach().clone() for w in watch]
+    torch.cuda.synchronize()
+    diffs = [i for i, (a, b) in enumerate(zip(got, want)) if not (a.shape == b.shape and torch.equal(a, b))]
+    same = not diffs
+    del saved
+    if not agree(same):
+        g.reset()
+        detail = [(i, tuple(got[i].shape), float((got[i].float() - want[i].float()).abs().max()))
+                  for i in diffs[:6]]
+        return fn, {"graph": "eager (replay != eager step on some rank)", "capture_ms": round(g.capture_ms, 1),
+                    "mismatch": detail, "loss_graph": float(loss_g), "loss_eager": float(loss_e)}
+    return g, {"graph": "captured (replay == eager step, bitwise, every rank)", "capture_ms": round(g.capture_ms, 1),
+               "state_tensors": len(state)}

@@ -89,9 +89,12 @@ def parse():
                     help="dynamic loss scale read on the host every step (the reference's .item() per step); "
                          "default: device-resident scale, overflow skipped by the fused optimizer's noop flag")
     ap.add_argument("--graph", default="auto", choices=["auto", "off", "on"],
-                    help="replay the whole training step as one captured HIP graph (utils/graphs.py); auto: on for "
-                         "a single rank (no collectives inside the step), off with ranks to synchronise (RCCL "
-                         "buckets and the IPC statistics exchange, whose epoch counters advance on the host)")
+                    help="replay the whole training step as one captured HIP graph (utils/graphs.py capture_checked: "
+                         "after capture every rank replays one step and runs one eager step from the same saved "
+                         "state, and all ranks keep the graph only if both agree bitwise everywhere, else all run "
+                         "eager in this process); auto: on for one rank, and for several ranks on RCCL when the SyncBN "
+                         "exchange is the IPC PeerAllReduce (its epoch lives in device memory) -- the DDP bucket "
+                         "all-reduces are captured RCCL calls; off: eager")
     ap.add_argument("--conv3x3", default="auto", choices=["auto", "miopen", "direct"],
                     help="stride-1 3x3 convolution forward / data gradient: the direct MFMA kernel "
                          "(kernels/conv.hip), MIOpen, or the faster per shape (auto)")
@@ -179,11 +182,12 @@ def main():
     global_batch = args.batch * world
     # the whole step as one HIP graph (the loss scale must live on the device: FusedLAMB / FusedSGD with the
     # device scaler, or a static scale -- O4 / O5 -- for FusedAdam, whose lr / step then stay on the device
-    # too: capturable=True). By default with one rank only: several ranks can capture too (--graph on: the
-    # IPC statistics exchange keeps its epoch on the device, RCCL all-reduces capture -- tests/test_rccl_world1.py),
-    # but that path has not been measured on an 8-GPU node, and the step is GPU-bound (graph vs eager +1 %)
-    graph_ok = world == 1 and not args.host_scaler and (args.optimizer != "adam" or args.opt_level in ("O4", "O5"))
-    use_graph = args.graph == "on" or (args.graph == "auto" and graph_ok)
+    # too: capturable=True). Several ranks capture too when every collective inside the step can be captured:
+    # the DDP buckets' RCCL all-reduces and the IPC SyncBN exchange (device-resident epoch,
+    # tests/test_rccl_world1.py); capture_checked proves the replay against an eager step on every rank first
+    step_ok = not args.host_scaler and (args.optimizer != "adam" or args.opt_level in ("O4", "O5"))
+    multi_ok = world == 1 or (args.backend == "nccl" and bn_exchange in ("ipc", "none"))
+    use_graph = args.graph == "on" or (args.graph == "auto" and step_ok and multi_ok)
     if args.optimizer == "lamb":
         opt = FusedLAMB(model.parameters(), lr=4e-3 * global_batch / 4096, weight_decay=0.01)
     elif args.optimizer == "adam":
@@ -238,14 +242,15 @@ def main():
             print(f"[bench] warmup {i + 1}/{args.warmup}: {(time.perf_counter() - tw) * 1e3:.1f} ms",
                   file=sys.stderr, flush=True)
     run = step
-    capture_ms = None
+    graph_report = {"graph": "eager"}
     if use_graph:
-        from beforeholiday_amd.utils import GraphedStep
+        from beforeholiday_amd.amp._amp_state import _amp_state
+        from beforeholiday_amd.utils import capture_checked, training_state
 
-        run = GraphedStep(step, warmup=2).capture()
-        capture_ms = round(run.capture_ms, 1)
+        state = training_state(*_amp_state.loss_scalers, model=model, optimizer=opt)
+        run, graph_report = capture_checked(step, state, watch=list(model.parameters())[:4] + list(model.parameters())[-2:])
         if rank == 0:
-            print(f"[bench] captured the step as a HIP graph in {capture_ms} ms", file=sys.stderr, flush=True)
+            print(f"[bench] {graph_report}", file=sys.stderr, flush=True)
         run()
     if world > 1:
         dist.barrier()
@@ -308,7 +313,8 @@ def main():
             "syncbn_stats": args.syncbn_stats,
             "syncbn_exchange": bn_exchange,
             "loss_scaler": "host" if args.host_scaler else "device",
-            "hip_graph": use_graph,
+            "hip_graph": run is not step,
+            "graph_check": graph_report.get("graph"),
             "gemm_table": dict(gemm_tuning.status(), loaded=bool(gemm_tuned)),
             "comm_ms_per_step": comm,
         }), flush=True)

@@ -37,6 +37,14 @@ def main():
                     geo = {"Li3ELi14ELi2E": "3x3 56x56", "Li3ELi7ELi4E": "3x3 28x28", "Li3ELi4ELi7E": "3x3 14x14",
                            "Li3ELi2ELi7E": "3x3 7x7", "Li1ELi28ELi1E": "1x1"}
                     name = "conv_wgrad<" + next((v for k, v in geo.items() if k in name), "?") + ">"
+                elif "k_igemm" in name:
+                    name = "igemm<s2 3x3 " + ("dgrad" if "Lb0ELb0E" in name or "Lb0ELb1E" in name else "fwd") + ">"
+                elif "k_c1x1" in name:
+                    name = "c1x1<strip 1x1>"
+                elif "k_gemm_n64" in name:
+                    name = "gemm_n64<1x1 K=64>"
+                elif "k_stem" in name:
+                    name = "stem<" + ("wgrad" if "wgrad" in name else "fwd") + ">"
                 else:
                     continue
                 vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -53,6 +61,9 @@ def main():
             # per-SIMD share of the GPU-active cycles (GRBM_GUI_ACTIVE summed over 8 XCDs, 1024 SIMDs)
             util = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["GRBM_GUI_ACTIVE"] / 8 * 1024)
             print(f"| {k} | MFMA utilisation (busy / (GUI_ACTIVE/8 x 1024 SIMDs)) | {util:.3f} |")
+        if m.get("SQ_INSTS_MFMA") and "SQ_INSTS_VALU" in m:
+            # (SQ_INSTS_VALU counts the MFMAs too)
+            print(f"| {k} | non-MFMA VALU per MFMA | {(m['SQ_INSTS_VALU'] - m['SQ_INSTS_MFMA']) / m['SQ_INSTS_MFMA']:.2f} |")
         if "SQ_LDS_BANK_CONFLICT" in m and m.get("SQ_LDS_IDX_ACTIVE"):
             print(f"| {k} | LDS bank-conflict cycles / LDS active | {m['SQ_LDS_BANK_CONFLICT'] / m['SQ_LDS_IDX_ACTIVE']:.3f} |")
         if "TCC_HIT_sum" in m and (m["TCC_HIT_sum"] + m.get("TCC_MISS_sum", 0)):

@@ -5,6 +5,8 @@ CPU: the algebra itself (P, Gm, sums -> dW, da, dgamma, dbeta, dz) against autog
 conv -> batch_norm -> + z -> ReLU in fp64. GPU: each kernel (Gram with / without the BatchNorm prologue, mask +
 column sums, fp32 weight-gradient partials, the strip GEMM's prologue + residual + bias + backward-sums
 epilogue) against an fp32 PyTorch reference, and the fused bottleneck tail against the per-layer path."""
+import os
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -243,8 +245,16 @@ def test_fused_tail_accuracy_vs_fp32(cfg, loss):
             errs[on] = e
     finally:
         R._BN_RES_FOLD = old
+    if os.environ.get("BH_FOLD_ERR_LOG"):  # the measured errors behind the gate (profiles/)
+        import json
+
+        with open(os.environ["BH_FOLD_ERR_LOG"], "a") as fh:
+            fh.write(json.dumps({"cfg": list(cfg), "loss": loss, "folded": errs[True], "per_layer": errs[False]}) + "\n")
+    # measured (profiles/fold_vs_per_layer_errors_r6.jsonl, 4 blocks x 2 losses, every gradient): the folded
+    # tail's relative error vs fp32 is at most 1.002x the per-layer path's -- the gate allows 1% (+1e-4 for
+    # gradients that are exactly zero in both)
     for n in errs[False]:
-        assert errs[True][n] <= 1.25 * errs[False][n] + 3e-3, (n, errs[True][n], errs[False][n])
+        assert errs[True][n] <= 1.01 * errs[False][n] + 1e-4, (n, errs[True][n], errs[False][n])
 
 
 @pytest.mark.gpu

@@ -23,7 +23,8 @@ def test_from_env_parses_and_validates():
         config.Config(own_gemm="fwd,oops")
     with pytest.raises(TypeError):
         config.Config(gemm_tile=True)
-    assert config.Config().native_knobs() == {"dense_mfma": 1, "dense_tune": 0, "gemm_tile": 0, "gemm_log": 0}
+    assert config.Config().native_knobs() == {"dense_wgrad": 1, "dense_mfma": 1, "dense_tune": 0, "gemm_tile": 0,
+                                             "gemm_log": 0}
 
 
 def test_set_override_and_module_globals():

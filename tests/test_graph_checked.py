@@ -1,0 +1,175 @@
+"""Self-checked whole-step capture (utils/graphs.py ``capture_checked``), the path ``bench.py --graph auto``
+takes at every world size: capture, then one replay and one eager step from the same saved state must
+agree bitwise on every rank before the graph is used, else every rank runs eager in the same process.
+
+* one GPU, RCCL world 1: fused-SyncBN bottleneck ResNet, amp O2, FusedLAMB, device loss scale, DDP with
+  the collectives forced (the bucket all-reduces are captured RCCL calls);
+* two processes on one GPU: the SyncBN statistics exchanged over the HIP-IPC PeerAllReduce INSIDE the
+  captured forward + backward + LAMB step, the agreement collective on gloo (no DDP: gloo collectives
+  cannot be captured, each rank trains on its own batch);
+* CPU: a replay that does not reproduce the eager step is rejected (fake graph)."""
+import os
+import socket
+import traceback
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from tests._dist import run_distributed
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _small_resnet(pg=None):
+    # the fused ResNet-50 blocks at one block per stage, 224 x 224 input: every kernel is an own
+    # deterministic one (a 64 x 64 input sends the stem to MIOpen, whose weight gradient is not bitwise
+    # repeatable -- the check then rightly refuses the graph); tests/test_determinism.py uses the same net
+    from beforeholiday_amd.models import resnet as R
+
+    return R.resnet50_fused(process_group=pg, layers=(1, 1, 1, 1), num_classes=10)
+
+
+def _build_step(rank, pg=None, ddp=False):
+    from beforeholiday_amd import amp, config
+    from beforeholiday_amd.optimizers import FusedLAMB
+    from beforeholiday_amd.parallel import DistributedDataParallel
+
+    config.set(amp_device_scaler=True, amp_fused_master_step=True)
+    torch.manual_seed(0)
+    model = _small_resnet(pg).cuda().to(memory_format=torch.channels_last)
+    opt = FusedLAMB(model.parameters(), lr=1e-3, weight_decay=0.01)
+    model, opt = amp.initialize(model, opt, opt_level="O2", keep_batchnorm_fp32=True, verbosity=0)
+    if ddp:
+        model = DistributedDataParallel(model, bucket_cap_mb=1, force_collectives=True, gradient_as_bucket_view=True)
+    torch.manual_seed(100 + rank)
+    x = torch.randn(16, 3, 224, 224, device="cuda", dtype=torch.float16).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (16,), device="cuda")
+
+    def step():
+        loss = F.cross_entropy(model(x), y)
+        with amp.scale_loss(loss, opt) as scaled:
+            scaled.backward()
+        opt.step()
+        opt.zero_grad()
+        return loss
+
+    return model, opt, step
+
+
+def _check(model, opt, step):
+    from beforeholiday_amd.amp._amp_state import _amp_state
+    from beforeholiday_amd.utils import capture_checked, training_state
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    state = training_state(*_amp_state.loss_scalers, model=model, optimizer=opt)
+    run, rep = capture_checked(step, state, watch=list(model.parameters()))
+    assert run is not step, rep
+    assert rep["graph"].startswith("captured"), rep
+    # two more replays against two eager steps from the same state
+    saved = [t.detach().clone() for t in state]
+    lg = [run().detach().clone() for _ in range(2)]
+    pg = [p.detach().clone() for p in model.parameters()]
+    with torch.no_grad():
+        for t, s in zip(state, saved):
+            t.copy_(s)
+    le = [step().detach().clone() for _ in range(2)]
+    for a, b in zip(lg, le):
+        assert torch.equal(a, b)
+    for a, b in zip(pg, model.parameters()):
+        assert torch.equal(a, b.detach())
+    from beforeholiday_amd import amp
+
+    amp.deactivate()
+
+
+def _rccl_world1(port, err_q):
+    try:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                device_id=torch.device("cuda", 0))
+        model, opt, step = _build_step(0, ddp=True)
+        _check(model, opt, step)
+        dist.destroy_process_group()
+    except Exception:
+        err_q.put(traceback.format_exc())
+        raise
+
+
+@pytest.mark.gpu
+def test_checked_capture_rccl_ddp_world1():
+    import torch.multiprocessing as mp
+
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    p = ctx.Process(target=_rccl_world1, args=(_free_port(), q))
+    p.start()
+    p.join(timeout=280)
+    if p.is_alive():
+        p.kill()
+        raise AssertionError("RCCL world-1 capture worker timed out")
+    if not q.empty():
+        raise AssertionError(q.get())
+    assert p.exitcode == 0
+
+
+def _ipc_two_ranks(rank, world):
+    from beforeholiday_amd.contrib.peer_memory import build_peer_allreduce
+
+    torch.cuda.set_device(0)
+    red = build_peer_allreduce(capacity=1 << 13)
+    assert red is not None, "IPC peer memory unavailable"
+    model, opt, step = _build_step(rank, pg=red)
+    _check(model, opt, step)
+    red.check()
+
+
+@pytest.mark.gpu
+def test_checked_capture_ipc_syncbn_two_procs():
+    run_distributed(_ipc_two_ranks, 2)
+
+
+def test_capture_checked_rejects_mismatch_cpu(monkeypatch):
+    from beforeholiday_amd.utils import graphs
+
+    w = torch.zeros(3)
+
+    def step():
+        w.add_(1.0)
+        return w.sum()
+
+    class Fake:
+        def __init__(self, fn, warmup=2, pool=None):
+            self.capture_ms = 0.0
+
+        def capture(self):
+            return self
+
+        def reset(self):
+            pass
+
+        def __call__(self):  # the "replay" skips the update
+            return w.sum()
+
+    monkeypatch.setattr(graphs, "GraphedStep", Fake)
+    monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
+    run, rep = graphs.capture_checked(step, [w], watch=[w])
+    assert run is step and rep["graph"].startswith("eager"), rep
+    assert torch.equal(w, torch.ones(3))  # restored, then ONE eager step
+
+    class Good(Fake):
+        def __call__(self):
+            return step()
+
+    monkeypatch.setattr(graphs, "GraphedStep", Good)
+    run, rep = graphs.capture_checked(step, [w], watch=[w])
+    assert isinstance(run, Good) and rep["graph"].startswith("captured"), rep

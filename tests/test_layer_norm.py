@@ -100,3 +100,37 @@ def test_autocast_gpu():
     with torch.autocast("cuda", dtype=torch.bfloat16):
         y = m(x)
     assert y.dtype == torch.bfloat16
+
+
+@pytest.mark.parametrize("device", devices())
+@pytest.mark.parametrize("n2", [1024, 63, 12288])
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_ln_backward_residual_grad(device, n2, dtype):
+    """backward_affine(..., dresid): grad_input = LN backward + the residual branch's gradient, summed in
+    fp32 in the dx kernel (wave-per-row and long-row kernels), against fp32 PyTorch autograd of
+    y = LN(x), loss = <y, dy> + <x, dr>."""
+    from beforeholiday_amd.ops import fused_layer_norm_cuda as ln
+
+    if device == "cpu" and dtype != torch.float32:
+        dtype_c = torch.float32
+    else:
+        dtype_c = dtype
+    torch.manual_seed(0)
+    x = torch.randn(37, n2, device=device).to(dtype_c)
+    w = (1 + 0.1 * torch.randn(n2, device=device)).to(dtype_c)
+    b = (0.1 * torch.randn(n2, device=device)).to(dtype_c)
+    dy = torch.randn(37, n2, device=device).to(dtype_c)
+    dr = torch.randn(37, n2, device=device).to(dtype_c)
+    out, mean, invvar = ln.forward_affine(x, (n2,), w, b, 1e-5)
+    gi, gw, gb = ln.backward_affine(dy, mean, invvar, x, (n2,), w, b, 1e-5, False, dr)
+    xr = x.float().requires_grad_()
+    wr, br = w.float().requires_grad_(), b.float().requires_grad_()
+    yr = torch.nn.functional.layer_norm(xr, (n2,), wr, br, 1e-5)
+    ((yr * dy.float()).sum() + (xr * dr.float()).sum()).backward()
+    tol = dict(rtol=2e-2, atol=2e-2) if dtype_c != torch.float32 else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(gi.float(), xr.grad, **tol)
+    torch.testing.assert_close(gw.float(), wr.grad, rtol=5e-2, atol=5e-2)
+    torch.testing.assert_close(gb.float(), br.grad, rtol=5e-2, atol=5e-2)
+    # the same result as the unfused sum, within one rounding of the 16-bit output
+    g0 = ln.backward_affine(dy, mean, invvar, x, (n2,), w, b, 1e-5, False)[0]
+    torch.testing.assert_close(gi.float(), (g0.float() + dr.float()), rtol=1e-2, atol=1e-2)

@@ -45,26 +45,32 @@ def _block(inplanes, planes, stride, dt, pg=None):
 @pytest.mark.parametrize("cfg", [(256, 64, 1, 56), (64, 64, 1, 56), (256, 128, 2, 56), (512, 128, 1, 28),
                                  (1024, 256, 1, 14)])
 def test_folded_bottleneck_matches_fp32(cfg, dt):
+    import copy
+
     inplanes, planes, stride, hw = cfg
     R, ref, blk = _block(inplanes, planes, stride, dt)
     x = torch.randn(8, inplanes, hw, hw, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
     assert blk._fold_ok(x)
     xr = x.float().clone().requires_grad_()
     xf = x.clone().requires_grad_()
-    out_r, out_f = ref(xr), blk(xf)
-    tol = 1e-2 if dt == torch.float16 else 4e-2
-    assert _rel(out_f, out_r) < tol
+    # the measured baseline: the same PyTorch block run in the 16-bit dtype (conv + BatchNorm in dt, as
+    # cuDNN / MIOpen would), against fp32 -- the folded block may be at most 1.5x as far from fp32 (+ 2e-3)
+    ref_lp = copy.deepcopy(ref).to(memory_format=torch.channels_last).to(dt)
+    xl = x.clone().requires_grad_()
+    out_r, out_f, out_l = ref(xr), blk(xf), ref_lp(xl)
+    def gate(e, base):
+        return e <= 1.5 * base + 2e-3
+    assert gate(_rel(out_f, out_r), _rel(out_l, out_r)), (_rel(out_f, out_r), _rel(out_l, out_r))
     g = torch.randn_like(out_r)
     out_r.backward(g)
     out_f.backward(g.to(dt))
-    # gradients pass through three BatchNorm backwards (each subtracts two rank-1 terms from the
-    # incoming gradient), which amplifies the 16-bit rounding of the activations ~3x
-    assert _rel(xf.grad, xr.grad) < 4 * tol
-    for (n, p), q in zip(blk.named_parameters(), ref.parameters()):
-        assert _rel(p.grad, q.grad) < 4 * tol, n
-    for (n, b), q in zip(blk.named_buffers(), ref.buffers()):
+    out_l.backward(g.to(dt))
+    assert gate(_rel(xf.grad, xr.grad), _rel(xl.grad, xr.grad)), (_rel(xf.grad, xr.grad), _rel(xl.grad, xr.grad))
+    for (n, p), q, l in zip(blk.named_parameters(), ref.parameters(), ref_lp.parameters()):
+        assert gate(_rel(p.grad, q.grad), _rel(l.grad, q.grad)), (n, _rel(p.grad, q.grad), _rel(l.grad, q.grad))
+    for (n, b), q, l in zip(blk.named_buffers(), ref.buffers(), ref_lp.buffers()):
         if "running" in n:
-            assert _rel(b, q) < tol, n
+            assert gate(_rel(b, q), _rel(l, q)), (n, _rel(b, q), _rel(l, q))
         elif "num_batches" in n:
             assert int(b) == int(q), n
 
