@@ -60,6 +60,9 @@ class Config:
         "comma list of {fwd, bwd, plain, resid}: strip/ping-pong GEMMs instead of hipBLASLt")))
     conv_tune: bool = field(default=False, metadata=dict(env="BH_CONV_TUNE", doc=(
         "time own vs MIOpen per conv shape (rank 0's pick broadcast)")))
+    conv3x3_bwd_epi: bool = field(default=False, metadata=dict(env="BH_CONV3X3_BWD_EPI", doc=(
+        "stride-1 3x3 data gradient of a BatchNorm-prologue conv reduces that BatchNorm's backward sums "
+        "in its epilogue (no separate reduction pass)")))
     conv_wgrad: str = field(default="own", metadata=dict(env="BH_CONV_WGRAD", choices=("own", "miopen"),
                                                          doc="weight gradients of the stride-1 convs"))
     conv1x1_s2: str = field(default="wgrad", metadata=dict(env="BH_CONV1X1_S2", choices=("wgrad", "gather", "miopen"),

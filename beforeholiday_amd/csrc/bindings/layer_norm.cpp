@@ -82,6 +82,17 @@ std::vector<at::Tensor> bwd_impl(at::Tensor dout, at::Tensor mean, at::Tensor in
   TORCH_CHECK(rms || memory_efficient || mean.numel() == d.n1, "layer_norm backward: mean has ", mean.numel(),
               " elements, expected ", d.n1);
   TORCH_CHECK(invvar.numel() == d.n1, "layer_norm backward: invvar has ", invvar.numel(), " elements, expected ", d.n1);
+  const int fblocks = gamma.defined() ? bh::ln_bwd_fused_blocks(d.n1, d.n2) : 0;
+  if (fblocks > 0) {  // one pass for dx and the parameter gradients
+    at::Tensor gg = at::empty_like(gamma), gb;
+    if (!rms && beta.defined()) gb = at::empty_like(beta);
+    auto part = at::empty({2 * (int64_t)fblocks * d.n2}, xin.options().dtype(at::kFloat));
+    bh::ln_backward_fused(d.n1, d.n2, dtype_code(dout.scalar_type()), dout.data_ptr(), dtype_code(xin.scalar_type()),
+                          xin.data_ptr(), mp, invvar.data_ptr<float>(), wc(gamma), wp(gamma), wp(beta), dx.data_ptr(),
+                          gg.data_ptr(), gb.defined() ? gb.data_ptr() : nullptr, part.data_ptr<float>(), fblocks, rms,
+                          memory_efficient, vec, s, dresid.defined() ? dresid.data_ptr() : nullptr);
+    return {dx, gg, gb};
+  }
   bh::ln_backward_dx(d.n1, d.n2, dtype_code(dout.scalar_type()), dout.data_ptr(), dtype_code(xin.scalar_type()),
                      xin.data_ptr(), mp, invvar.data_ptr<float>(), wc(gamma), wp(gamma), wp(beta), dx.data_ptr(), rms,
                      memory_efficient, vec, s, dresid.defined() ? dresid.data_ptr() : nullptr);

@@ -19,6 +19,13 @@ void ln_backward_dx(int64_t n1, int n2, int dt_dy, const void* dy, int dt_x, con
 // (dresid: optional [n1, n2] tensor of dx's dtype added to dx in the same pass -- the gradient the
 // residual branch of a pre-LN block sends to the same input, reference layer_norm.cuh:474 dout_resid)
 int ln_wgrad_splits(int64_t n1, int n2);
+// dx AND grad_gamma / grad_beta from one pass over dy and x (rows <= 2048 elements): 0 when the shape is not
+// covered, else the number of partial rows (partials: 2 * blocks * n2 floats of scratch)
+int ln_bwd_fused_blocks(int64_t n1, int n2);
+void ln_backward_fused(int64_t n1, int n2, int dt_dy, const void* dy, int dt_x, const void* xin, const float* mean,
+                       const float* invvar, int dt_w, const void* gamma, const void* beta, void* dx, void* grad_gamma,
+                       void* grad_beta, float* partials, int blocks, bool rms, bool from_output, bool vec,
+                       hipStream_t st, const void* dresid);
 // grad_gamma / grad_beta (may be null); partials: 2 * splits * n2 floats of scratch
 void ln_backward_wgrad(int64_t n1, int n2, int dt_dy, const void* dy, int dt_x, const void* xin, const float* mean,
                        const float* invvar, int dt_w, const void* gamma, const void* beta, void* grad_gamma,

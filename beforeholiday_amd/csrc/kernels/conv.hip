@@ -53,7 +53,6 @@ constexpr int kBN = 64;     // output channels per workgroup
 constexpr int kCK = 64;     // input channels per chunk
 constexpr int kPix = 144;   // LDS bytes per halo pixel: 128 data + 16 pad
 constexpr int kMaxHC = 40;  // halo columns G * (lanes per image + 2) <= 40
-constexpr int kHaloBytes = (kTH + 2) * kMaxHC * kPix;
 constexpr int kWBytes = kBN * 128;
 constexpr int kMaxProC = 512;                 // input channels the BatchNorm prologue covers
 constexpr int kProBytes = 2 * kMaxProC * 4;   // its scale / shift in LDS
@@ -88,10 +87,17 @@ template <typename T, bool FLIP, int G, bool PRO, int EPI>
 __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
   // window geometry as compile-time constants (the halo address math divides by them)
   constexpr int GW = 32 / G, HC = G * (GW + 2);
-  __shared__ __attribute__((aligned(16))) char smem[kHaloBytes + 2 * kWBytes + (PRO ? kProBytes : 0)];
+  // the plain epilogue stores from the transposed accumulator layout (8-byte channel runs per lane); the
+  // statistics epilogues keep the pixel-per-register layout (their per-channel sums stay in-lane)
+  constexpr bool SW = EPI == kConvEpiPlain;
+  // weight-slice buffers: 3 where the LDS budget of two workgroups per CU allows (the next step's first
+  // fragments are then read BEFORE the barrier that ends a step), 2 for the 40-column G = 4 halo
+  constexpr int NB = G == 4 ? 2 : 3;
+  constexpr int kHaloB = (kTH + 2) * HC * kPix;
+  __shared__ __attribute__((aligned(16))) char smem[kHaloB + NB * kWBytes + (PRO ? kProBytes : 0)];
   char* halo = smem;
-  char* wb = smem + kHaloBytes;
-  float* ss = reinterpret_cast<float*>(smem + kHaloBytes + 2 * kWBytes);  // PRO: scale[C], shift[C]
+  char* wb = smem + kHaloB;
+  float* ss = reinterpret_cast<float*>(smem + kHaloB + NB * kWBytes);  // PRO: scale[C], shift[C]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r32 = lane & 31, h = lane >> 5;
   const int tile0 = blockIdx.x * g.tpw;
@@ -243,6 +249,30 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
   auto epilogue = [&](int t) __attribute__((always_inline)) {
     int n0, y0, x0;
     origin(t, n0, y0, x0);
+    if constexpr (SW) {
+      // swapped operands: lane (r32, h) holds pixel r32 of window row 2 wave + pb, channels
+      // k0 + 32 kb + 8 g + 4 h .. + 3 in acc[kb][pb][4 g .. 4 g + 3]: one 8-byte store per 4 channels
+      // (16 stores per wave and window instead of 64 2-byte ones)
+      typedef T t4 __attribute__((ext_vector_type(4)));
+      const int gp = r32 / GW, xp = r32 - gp * GW;
+      const int n = n0 + gp, x = x0 + xp;
+#pragma unroll
+      for (int pb = 0; pb < 2; ++pb) {
+        const int y = y0 + 2 * wave + pb;
+        if (y >= H || n >= N || x >= W) continue;
+        const int off = ((n * H + y) * W + x) * a.K + k0 + 4 * h;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            t4 o;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[i] = from_f<T>(acc[kb][pb][4 * g + i]);
+            *reinterpret_cast<t4*>(Y + off + 32 * kb + 8 * g) = o;
+          }
+      }
+      return;
+    }
 #pragma unroll
     for (int pb = 0; pb < 2; ++pb) {
       const int y = y0 + 2 * wave + pb;
@@ -291,78 +321,139 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
   // t % 3 = rs % 3 (a chunk is nine steps), in LDS buffer t & 1.
   i4v wr[3][2];
   const int nchunks = ntile * nch;
+  // fragments of k-step kk of step rs from weight buffer wcur (image rows: output channels, or for FLIP
+  // the reduction channels read transposed) and the halo at offset (rs / 3, rs % 3)
+  auto frags = [&](const char* wcur, int rs, int kk, i4v (&f)[4]) __attribute__((always_inline)) {
+    const int r = rs / 3, s = rs - r * 3;
+    const char* hb0 = halo + ((2 * wave + r) * HC + hcol + s) * kPix;  // window row 2w, offset (r, s)
+    const char* hb1 = hb0 + HC * kPix;                                    // window row 2w + 1
+    const int ch = 2 * kk + h;
+    if (FLIP) {
+      f[0] = frag_tr(wcur, 16 * kk + 8 * h, 0, lane);
+      f[1] = frag_tr(wcur, 16 * kk + 8 * h, 32, lane);
+    } else {
+      f[0] = *reinterpret_cast<const i4v*>(wcur + wsw(r32, ch));
+      f[1] = *reinterpret_cast<const i4v*>(wcur + wsw(32 + r32, ch));
+    }
+    f[2] = *reinterpret_cast<const i4v*>(hb0 + ch * 16);
+    f[3] = *reinterpret_cast<const i4v*>(hb1 + ch * 16);
+  };
+  auto mfma4 = [&](const i4v (&f)[4]) __attribute__((always_inline)) {
+    // acc[kb][pb]: SW puts the weights (output channels) on the MFMA rows, the pixels on the lanes
+    if constexpr (SW) {
+      acc[0][0] = Mfma32<T>::run(f[0], f[2], acc[0][0]);
+      acc[0][1] = Mfma32<T>::run(f[0], f[3], acc[0][1]);
+      acc[1][0] = Mfma32<T>::run(f[1], f[2], acc[1][0]);
+      acc[1][1] = Mfma32<T>::run(f[1], f[3], acc[1][1]);
+    } else {
+      acc[0][0] = Mfma32<T>::run(f[2], f[0], acc[0][0]);
+      acc[0][1] = Mfma32<T>::run(f[3], f[0], acc[0][1]);
+      acc[1][0] = Mfma32<T>::run(f[2], f[1], acc[1][0]);
+      acc[1][1] = Mfma32<T>::run(f[3], f[1], acc[1][1]);
+    }
+  };
+  // software pipeline over the four k-steps with two fragment sets: the reads of k-step kk + 2 are issued
+  // right after the MFMAs of kk (which free that set) and before those of kk + 1, so each read group has
+  // four MFMAs (>= 128 cycles) to land; the scheduling barriers keep the compiler from sinking the reads
+  // behind the MFMAs and reusing one set (read, lgkmcnt(0), 4 MFMAs, ...). fa / fb hold k-steps 0 / 1.
+  i4v fa[4], fb[4];
+  auto mfma_step = [&](const char* wcur, int rs) __attribute__((always_inline)) {
+    __builtin_amdgcn_sched_barrier(0);
+    mfma4(fa);
+    __builtin_amdgcn_sched_barrier(0);
+    frags(wcur, rs, 2, fa);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma4(fb);
+    __builtin_amdgcn_sched_barrier(0);
+    frags(wcur, rs, 3, fb);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma4(fa);
+    mfma4(fb);
+    __builtin_amdgcn_sched_barrier(0);
+  };
   zero_acc();
   halo_load(tile0, 0);
-  w_load(0, 0, wr[0]);
-  halo_store();
-  w_store(wb, wr[0]);
-  w_load(0, 1, wr[1]);
-  __syncthreads();
-  for (int cidx = 0; cidx < nchunks; ++cidx) {
-    const int it = cidx / nch, chunk = cidx - it * nch;
-    const int nchunk = chunk + 1 == nch ? 0 : chunk + 1;  // chunk of the slices after rs = 8
-    // the (window, chunk) whose halo is prefetched during this chunk: the next one, or this window's
-    // first chunk again after the last (loaded, stored, never read)
-    const int htile = (chunk + 1 == nch && it + 1 < ntile) ? tile0 + it + 1 : tile0 + it;
-    const char* wbase = wb + (cidx & 1) * kWBytes;  // buffer of rs = 0 (9 is odd: parity flips per chunk)
+  if constexpr (NB == 3) {
+    // Three LDS weight buffers (slice t in buffer t % 3 = rs % 3) and register slots (slice t in slot
+    // t % 3): slice t + 3 is requested at the start of step t and written to LDS at the end of step t + 1,
+    // so each step ends with: store slice t + 2, read the first two k-steps' fragments of step t + 1 (its
+    // slice was published by the previous barrier), barrier -- and the MFMAs of step t + 1 start right at
+    // the barrier instead of behind an LDS round trip. (Not across a chunk boundary: the halo changes.)
+    w_load(0, 0, wr[0]);
+    w_load(0, 1, wr[1]);
+    halo_store();
+    w_store(wb, wr[0]);
+    w_store(wb + kWBytes, wr[1]);
+    w_load(0, 2, wr[2]);
+    __syncthreads();
+    for (int cidx = 0; cidx < nchunks; ++cidx) {
+      const int it = cidx / nch, chunk = cidx - it * nch;
+      const int nchunk = chunk + 1 == nch ? 0 : chunk + 1;  // chunk of the slices after rs = 8
+      // the (window, chunk) whose halo is prefetched during this chunk: the next one, or this window's
+      // first chunk again after the last (loaded, stored, never read)
+      const int htile = (chunk + 1 == nch && it + 1 < ntile) ? tile0 + it + 1 : tile0 + it;
 #pragma unroll
-    for (int rs = 0; rs < 9; ++rs) {
-      if (rs + 2 < 9) w_load(chunk, rs + 2, wr[(rs + 2) % 3]);
-      else w_load(nchunk, rs + 2 - 9, wr[(rs + 2) % 3]);
-      if (rs == 0) halo_load(htile, nchunk * kCK);
-      const char* wcur = (rs & 1) ? wb + kWBytes - (wbase - wb) : wbase;  // buffer (t & 1)
-      const int r = rs / 3, s = rs - r * 3;
-      const char* hb0 = halo + ((2 * wave + r) * HC + hcol + s) * kPix;  // window row 2w, offset (r, s)
-      const char* hb1 = hb0 + HC * kPix;                                    // window row 2w + 1
-      auto frags = [&](int kk, i4v (&f)[4]) __attribute__((always_inline)) {
-        const int ch = 2 * kk + h;
-        if (FLIP) {
-          f[0] = frag_tr(wcur, 16 * kk + 8 * h, 0, lane);
-          f[1] = frag_tr(wcur, 16 * kk + 8 * h, 32, lane);
+      for (int rs = 0; rs < 9; ++rs) {
+        if (rs + 3 < 9) w_load(chunk, rs + 3, wr[rs % 3]);
+        else w_load(nchunk, rs + 3 - 9, wr[rs % 3]);
+        if (rs == 0) halo_load(htile, nchunk * kCK);
+        const char* wcur = wb + (rs % 3) * kWBytes;
+        if (rs == 0) {
+          frags(wcur, 0, 0, fa);
+          frags(wcur, 0, 1, fb);
+        }
+        mfma_step(wcur, rs);
+        w_store(wb + ((rs + 2) % 3) * kWBytes, wr[(rs + 2) % 3]);  // slice t + 2 (requested at step t - 1)
+        if (rs < 8) {
+          const char* wnext = wb + ((rs + 1) % 3) * kWBytes;
+          frags(wnext, rs + 1, 0, fa);
+          frags(wnext, rs + 1, 1, fb);
         } else {
-          f[0] = *reinterpret_cast<const i4v*>(wcur + wsw(r32, ch));
-          f[1] = *reinterpret_cast<const i4v*>(wcur + wsw(32 + r32, ch));
+          __syncthreads();  // every wave is done with this chunk's halo
+          halo_store();
+          if (chunk + 1 == nch) {  // window done: results out, accumulators reset
+            epilogue(tile0 + it);
+            zero_acc();
+          }
         }
-        f[2] = *reinterpret_cast<const i4v*>(hb0 + ch * 16);
-        f[3] = *reinterpret_cast<const i4v*>(hb1 + ch * 16);
-      };
-      // software pipeline over the four k-steps with two fragment sets: the reads of k-step kk + 2 are
-      // issued right after the MFMAs of kk (which free that set) and before those of kk + 1, so each
-      // read group has four MFMAs (>= 128 cycles) to land; the scheduling barriers keep the compiler
-      // from sinking the reads behind the MFMAs and reusing one set (read, lgkmcnt(0), 4 MFMAs, ...)
-      auto mfma4 = [&](const i4v (&f)[4]) __attribute__((always_inline)) {
-        acc[0][0] = Mfma32<T>::run(f[2], f[0], acc[0][0]);
-        acc[0][1] = Mfma32<T>::run(f[3], f[0], acc[0][1]);
-        acc[1][0] = Mfma32<T>::run(f[2], f[1], acc[1][0]);
-        acc[1][1] = Mfma32<T>::run(f[3], f[1], acc[1][1]);
-      };
-      i4v fa[4], fb[4];
-      frags(0, fa);
-      frags(1, fb);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma4(fa);
-      __builtin_amdgcn_sched_barrier(0);
-      frags(2, fa);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma4(fb);
-      __builtin_amdgcn_sched_barrier(0);
-      frags(3, fb);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma4(fa);
-      mfma4(fb);
-      __builtin_amdgcn_sched_barrier(0);
-      // slice t + 1 (requested a step ago) into the other buffer: every wave finished reading it at the
-      // barrier that ended step t - 1
-      w_store(wb + kWBytes - (wcur - wb), wr[(rs + 1) % 3]);
-      if (rs == 8) {
-        __syncthreads();  // every wave is done with this chunk's halo
-        halo_store();
-        if (chunk + 1 == nch) {  // window done: results out, accumulators reset
-          epilogue(tile0 + it);
-          zero_acc();
-        }
+        __syncthreads();
       }
-      __syncthreads();
+    }
+  } else {
+    // two LDS weight buffers: slice t + 2 requested at the start of step t (register slot t % 3), slice
+    // t + 1 written to buffer (t + 1) & 1 at its end
+    w_load(0, 0, wr[0]);
+    halo_store();
+    w_store(wb, wr[0]);
+    w_load(0, 1, wr[1]);
+    __syncthreads();
+    for (int cidx = 0; cidx < nchunks; ++cidx) {
+      const int it = cidx / nch, chunk = cidx - it * nch;
+      const int nchunk = chunk + 1 == nch ? 0 : chunk + 1;
+      const int htile = (chunk + 1 == nch && it + 1 < ntile) ? tile0 + it + 1 : tile0 + it;
+      const char* wbase = wb + (cidx & 1) * kWBytes;  // buffer of rs = 0 (9 is odd: parity flips per chunk)
+#pragma unroll
+      for (int rs = 0; rs < 9; ++rs) {
+        if (rs + 2 < 9) w_load(chunk, rs + 2, wr[(rs + 2) % 3]);
+        else w_load(nchunk, rs + 2 - 9, wr[(rs + 2) % 3]);
+        if (rs == 0) halo_load(htile, nchunk * kCK);
+        const char* wcur = (rs & 1) ? wb + kWBytes - (wbase - wb) : wbase;  // buffer (t & 1)
+        frags(wcur, rs, 0, fa);
+        frags(wcur, rs, 1, fb);
+        mfma_step(wcur, rs);
+        // slice t + 1 (requested a step ago) into the other buffer: every wave finished reading it at
+        // the barrier that ended step t - 1
+        w_store(wb + kWBytes - (wcur - wb), wr[(rs + 1) % 3]);
+        if (rs == 8) {
+          __syncthreads();  // every wave is done with this chunk's halo
+          halo_store();
+          if (chunk + 1 == nch) {
+            epilogue(tile0 + it);
+            zero_acc();
+          }
+        }
+        __syncthreads();
+      }
     }
   }
   if constexpr (EPI == kConvEpiStats || EPI == kConvEpiBwd) {

@@ -215,6 +215,106 @@ __global__ __launch_bounds__(kBlock) void k_ln_bwd_dx(const Tdy* __restrict__ dy
   }
 }
 
+// backward dx AND the parameter-gradient partials in one pass: every wave walks rows blockIdx.x * 4 + wave,
+// + 4 gridDim.x, ... with the same per-row math as k_ln_bwd_dx, and keeps dy * x_hat and dy for its lane's
+// columns in registers; the block sums its four waves through LDS into ONE partial row (pg[block][n2],
+// pb[block][n2]) for k_ln_wgrad_finalize. dy and x are read once for dx and the gradients together (the
+// separate k_ln_wgrad_partials pass re-read both).
+template <typename T, typename Tw, typename Tdy, int VPT, bool RMS>
+__global__ __launch_bounds__(kBlock) void k_ln_bwd_fused(const Tdy* __restrict__ dy, const T* __restrict__ xin,
+                                                         const float* __restrict__ mean_in,
+                                                         const float* __restrict__ invvar_in, const Tw* __restrict__ g,
+                                                         const Tw* __restrict__ b, T* __restrict__ dx, int64_t n1,
+                                                         int n2, bool from_output, bool vec,
+                                                         const T* __restrict__ dres, float* __restrict__ pg,
+                                                         float* __restrict__ pb) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [waves][2][VPT * 512]
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x >> 6;
+  constexpr int kCols = VPT * kWave * 8;
+  float ag[VPT][8], ab[VPT][8], gv[VPT][8], bv[VPT][8];
+#pragma unroll
+  for (int j = 0; j < VPT; ++j) {
+    const int col = (j * kWave + lane) * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ag[j][k] = ab[j][k] = 0.f;
+    if (g) load8(g, col, n2, vec, gv[j]);
+    else
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gv[j][k] = 1.f;
+    if (from_output && b && !RMS) load8(b, col, n2, vec, bv[j]);
+  }
+  const float inv_n = 1.f / (float)n2;
+  for (int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + wave; row < n1; row += (int64_t)gridDim.x * kRowsPerBlock) {
+    const float mean = (RMS || from_output) ? 0.f : mean_in[row];
+    const float invvar = invvar_in[row];
+    float xh[VPT][8], dg[VPT][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int col = (j * kWave + lane) * 8;
+      float dv[8], xv[8];
+      load8(dy + row * n2, col, n2, vec, dv);
+      load8(xin + row * n2, col, n2, vec, xv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float gg = gv[j][k];
+        float h;
+        if (from_output) {
+          const float yv = (b && !RMS) ? xv[k] - bv[j][k] : xv[k];
+          h = (gg != 0.f) ? yv / gg : 0.f;
+        } else {
+          h = (xv[k] - mean) * invvar;
+        }
+        const bool ok = col + k < n2;
+        xh[j][k] = ok ? h : 0.f;
+        const float d = ok ? dv[k] : 0.f;
+        dg[j][k] = d * gg;
+        ag[j][k] = fmaf(d, xh[j][k], ag[j][k]);
+        ab[j][k] += d;
+        s1 += dg[j][k];
+        s2 = fmaf(dg[j][k], xh[j][k], s2);
+      }
+    }
+    const float m1 = RMS ? 0.f : wave_sum(s1) * inv_n;
+    const float m2 = wave_sum(s2) * inv_n;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int col = (j * kWave + lane) * 8;
+      if (col >= n2) break;
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = invvar * (dg[j][k] - m1 - xh[j][k] * m2);
+      if (dres) {
+        float rv[8];
+        load8(dres + row * n2, col, n2, vec, rv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] += rv[k];
+      }
+      store8(dx + row * n2, col, n2, vec, o);
+    }
+  }
+  // the block's four waves -> one partial row (fixed order: deterministic)
+  float* mine = red + (size_t)wave * 2 * kCols;
+#pragma unroll
+  for (int j = 0; j < VPT; ++j)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      mine[(j * kWave + lane) * 8 + k] = ag[j][k];
+      mine[kCols + (j * kWave + lane) * 8 + k] = ab[j][k];
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < n2; c += kBlock) {
+    float sg = 0.f, sb = 0.f;
+#pragma unroll
+    for (int w = 0; w < kRowsPerBlock; ++w) {
+      sg += red[(size_t)w * 2 * kCols + c];
+      sb += red[(size_t)w * 2 * kCols + kCols + c];
+    }
+    pg[(int64_t)blockIdx.x * n2 + c] = sg;
+    pb[(int64_t)blockIdx.x * n2 + c] = sb;
+  }
+}
+
 template <typename T, typename Tw, typename Tdy, bool RMS>
 __global__ __launch_bounds__(kBlock) void k_ln_bwd_dx_long(const Tdy* __restrict__ dy, const T* __restrict__ xin,
                                                            const float* __restrict__ mean_in,
@@ -423,6 +523,38 @@ void ln_backward_dx(int64_t n1, int n2, int dt_dy, const void* dy, int dt_x, con
                                 (T*)dx, n2, from_output, (const T*)dresid);
       })));
   check_launch("ln_backward_dx");
+}
+
+int ln_bwd_fused_blocks(int64_t n1, int n2) {
+  // wave-per-row rows only (x_hat and dy * gamma in registers, <= 2048 columns), >= 8 rows per wave, and
+  // about one block per CU: 256 partial rows for the finalize
+  if (n2 > 2048 || vpt_for(n2, 4) == 0) return 0;
+  const int64_t by_rows = n1 / (8 * kRowsPerBlock);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(256, by_rows));
+}
+
+void ln_backward_fused(int64_t n1, int n2, int dt_dy, const void* dy, int dt_x, const void* xin, const float* mean,
+                       const float* invvar, int dt_w, const void* gamma, const void* beta, void* dx, void* grad_gamma,
+                       void* grad_beta, float* partials, int blocks, bool rms, bool from_output, bool vec,
+                       hipStream_t st, const void* dresid) {
+  if (n1 == 0 || n2 == 0) return;
+  if (dt_w < 0) dt_w = dt_x;
+  const int vpt = vpt_for(n2, 4);
+  if (!vpt || blocks < 1) throw std::runtime_error("ln_backward_fused: row too long");
+  float* pg = partials;
+  float* pb = partials + (int64_t)blocks * n2;
+  const size_t shm = sizeof(float) * kRowsPerBlock * 2 * vpt * kWave * 8;
+  LN_DISPATCH(dt_x, T, LN_DISPATCH(dt_w, Tw, LN_DISPATCH(dt_dy, Tdy,
+      LN_VPT_DISPATCH(vpt, V,
+          if (rms) hipLaunchKernelGGL((k_ln_bwd_fused<T, Tw, Tdy, V, true>), dim3(blocks), dim3(kBlock), shm, st,
+                                      (const Tdy*)dy, (const T*)xin, mean, invvar, (const Tw*)gamma, (const Tw*)beta,
+                                      (T*)dx, n1, n2, from_output, vec, (const T*)dresid, pg, pb);
+          else hipLaunchKernelGGL((k_ln_bwd_fused<T, Tw, Tdy, V, false>), dim3(blocks), dim3(kBlock), shm, st,
+                                  (const Tdy*)dy, (const T*)xin, mean, invvar, (const Tw*)gamma, (const Tw*)beta,
+                                  (T*)dx, n1, n2, from_output, vec, (const T*)dresid, pg, pb));
+      hipLaunchKernelGGL((k_ln_wgrad_finalize<Tw>), dim3((n2 + 63) / 64), dim3(64 * kColsumLanes), 0, st, n2, blocks,
+                         pg, pb, (Tw*)grad_gamma, (Tw*)grad_beta))));
+  check_launch("ln_backward_fused");
 }
 
 int ln_wgrad_splits(int64_t n1, int n2) {

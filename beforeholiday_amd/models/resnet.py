@@ -1017,6 +1017,13 @@ class _BNConvFn(torch.autograd.Function):
         g_conv = None
         if ctx.R == 3 and ctx.stride == 2:
             dA = bhconv.conv3x3_s2_dgrad(gy, conv_w, (h, w))
+        elif ctx.R == 3 and _config.get().conv3x3_bwd_epi and gy.dtype in (torch.float16, torch.bfloat16) \
+                and C % 64 == 0 and conv_w.size(0) % 64 == 0 and y.is_contiguous(memory_format=torch.channels_last):
+            # the direct kernel's backward epilogue: this BatchNorm's backward sums from the data gradient as
+            # it leaves the accumulators (no k_bwd_reduce pass over dA and y)
+            from .._native import submodule
+
+            dA, part = submodule("conv_cuda").conv3x3_bn_dgrad(gy, conv_w, y, scale, shift, mean, True)
         elif ctx.R == 3:
             dA = bhconv.conv3x3_dgrad(gy, conv_w)
         else:

@@ -32,25 +32,34 @@ class GraphedStep:
     under capture; each call replays the graph and returns the tensors ``fn`` returned during capture
     (refreshed in place by the replay)."""
 
-    def __init__(self, fn: Callable[[], Any], warmup: int = 3, pool=None):
+    def __init__(self, fn: Callable[[], Any], warmup: int = 3, pool=None, before: Optional[Callable[[], Any]] = None):
         self.fn = fn
         self.warmup = warmup
         self.pool = pool
+        self.before = before
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.out = None
         self.capture_ms = 0.0
 
     def capture(self) -> "GraphedStep":
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
+        # warm-up and capture run on ONE side stream; ``before`` runs there first (DDP re-registers its
+        # gradient hooks there: autograd runs a hooked parameter's AccumulateGrad node on the stream the
+        # node was created on, and a node created on the default stream is not part of a capture on
+        # another one -- the replay then misses those accumulations)
+        # A caller already on a side stream (bench.py builds DDP and trains on one) captures right there.
+        cur = torch.cuda.current_stream()
+        side = cur if cur != torch.cuda.default_stream() else torch.cuda.Stream()
+        side.wait_stream(cur)
         with torch.cuda.stream(side):
+            if self.before is not None:
+                self.before()
             for _ in range(self.warmup):
                 self.fn()
-        torch.cuda.current_stream().wait_stream(side)
+        cur.wait_stream(side)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self.pool):
+        with torch.cuda.graph(g, pool=self.pool, stream=side):
             self.out = self.fn()
         torch.cuda.synchronize()
         self.capture_ms = (time.perf_counter() - t0) * 1e3
@@ -107,7 +116,19 @@ def training_state(*roots, model=None, optimizer=None):
     return out
 
 
-def capture_checked(fn: Callable[[], torch.Tensor], state, watch=(), warmup: int = 2, group=None):
+def _rehook_ddp(model):
+    """Re-register the gradient hooks of every beforeholiday_amd DDP module in ``model`` on the current
+    stream (see GraphedStep.capture)."""
+    from ..parallel.distributed import DistributedDataParallel
+
+    if model is None:
+        return
+    for m in model.modules():
+        if isinstance(m, DistributedDataParallel) and m._collectives:
+            m._refresh_params()
+
+
+def capture_checked(fn: Callable[[], torch.Tensor], state, watch=(), warmup: int = 2, group=None, model=None):
     """Capture ``fn`` (a training step returning its loss) and PROVE the replay before using it.
 
     1. capture (a failure on any rank is agreed on by all ranks before anyone replays a collective);
@@ -130,7 +151,7 @@ def capture_checked(fn: Callable[[], torch.Tensor], state, watch=(), warmup: int
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
         return bool(int(t.item()))
 
-    g = GraphedStep(fn, warmup=warmup)
+    g = GraphedStep(fn, warmup=warmup, before=lambda: _rehook_ddp(model))
     err = None
     try:
         g.capture()
@@ -153,12 +174,24 @@ def capture_checked(fn: Callable[[], torch.Tensor], state, watch=(), warmup: int
     torch.cuda.synchronize()
     diffs = [i for i, (a, b) in enumerate(zip(got, want)) if not (a.shape == b.shape and torch.equal(a, b))]
     same = not diffs
+    rep = {}
+    if diffs:
+        # diagnosis: is the eager step itself bitwise repeatable from the same state? (a non-deterministic
+        # kernel -- float atomics, a timed algorithm pick -- makes any replay check fail)
+        with torch.no_grad():
+            for t, s_ in zip(state, saved):
+                t.copy_(s_)
+        fn()
+        again = [w.detach().clone() for w in watch]
+        rep["eager_repeatable"] = all(torch.equal(a, b) for a, b in zip(again, want[1:]))
+        rep["mismatch"] = [(i, tuple(got[i].shape), float((got[i].float() - want[i].float()).abs().max()))
+                           for i in diffs[:6]]
+        rep["n_mismatch"] = len(diffs)
     del saved
     if not agree(same):
         g.reset()
-        detail = [(i, tuple(got[i].shape), float((got[i].float() - want[i].float()).abs().max()))
-                  for i in diffs[:6]]
-        return fn, {"graph": "eager (replay != eager step on some rank)", "capture_ms": round(g.capture_ms, 1),
-                    "mismatch": detail, "loss_graph": float(loss_g), "loss_eager": float(loss_e)}
+        rep.update({"graph": "eager (replay != eager step on some rank)", "capture_ms": round(g.capture_ms, 1),
+                    "loss_graph": float(loss_g), "loss_eager": float(loss_e)})
+        return fn, rep
     return g, {"graph": "captured (replay == eager step, bitwise, every rank)", "capture_ms": round(g.capture_ms, 1),
                "state_tensors": len(state)}

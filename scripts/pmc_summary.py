@@ -4,6 +4,7 @@ import collections
 import csv
 import glob
 import os
+import re
 import sys
 
 
@@ -30,7 +31,8 @@ def main():
                 elif "attn_bwd" in name:
                     name = "attn_bwd"
                 elif "k_conv3x3" in name:
-                    kind = "dgrad" if "Lb1E" in name else "fwd"
+                    # the first template bool after the dtype is FLIP (the data gradient)
+                    kind = "dgrad" if re.search(r"k_conv3x3I(DF16_|DF16b)Lb1E", name) else "fwd"
                     g = "G4" if "Li4E" in name else ("G2" if "Li2E" in name else "G1")
                     name = f"conv3x3_{kind}<{g}>"
                 elif "k_conv_wgrad" in name:

@@ -69,7 +69,7 @@ def _check(model, opt, step):
         step()
     torch.cuda.synchronize()
     state = training_state(*_amp_state.loss_scalers, model=model, optimizer=opt)
-    run, rep = capture_checked(step, state, watch=list(model.parameters()))
+    run, rep = capture_checked(step, state, watch=list(model.parameters()), model=model)
     assert run is not step, rep
     assert rep["graph"].startswith("captured"), rep
     # two more replays against two eager steps from the same state
@@ -96,8 +96,9 @@ def _rccl_world1(port, err_q):
         torch.cuda.set_device(0)
         dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                                 device_id=torch.device("cuda", 0))
-        model, opt, step = _build_step(0, ddp=True)
-        _check(model, opt, step)
+        with torch.cuda.stream(torch.cuda.Stream()):  # as bench.py: DDP built and trained on a side stream
+            model, opt, step = _build_step(0, ddp=True)
+            _check(model, opt, step)
         dist.destroy_process_group()
     except Exception:
         err_q.put(traceback.format_exc())
@@ -148,7 +149,7 @@ def test_capture_checked_rejects_mismatch_cpu(monkeypatch):
         return w.sum()
 
     class Fake:
-        def __init__(self, fn, warmup=2, pool=None):
+        def __init__(self, fn, warmup=2, pool=None, before=None):
             self.capture_ms = 0.0
 
         def capture(self):

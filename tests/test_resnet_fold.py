@@ -298,3 +298,30 @@ def test_block_output_with_second_consumer():
     for blk, ref in ((blk_a, ref_a), (blk_b, ref_b)):
         for (n, p), q in zip(blk.named_parameters(), ref.parameters()):
             assert _rel(p.grad, q.grad) < 6e-2, n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [(256, 64, 1, 56), (1024, 256, 1, 14)])
+def test_conv3x3_bwd_epilogue_matches_reduce_pass(cfg):
+    """Config.conv3x3_bwd_epi: bn1's backward sums from the 3x3 data-gradient epilogue (as the
+    accumulators leave) == the separate k_bwd_reduce pass over (dA, y) -- same block, same gradients
+    up to fp32 summation order."""
+    from beforeholiday_amd import config
+
+    inplanes, planes, stride, hw = cfg
+    R, _, blk = _block(inplanes, planes, stride, torch.float16)
+    x = torch.randn(8, inplanes, hw, hw, device="cuda").half().contiguous(memory_format=torch.channels_last)
+    state0 = {k: v.clone() for k, v in blk.state_dict().items()}
+    outs = []
+    for on in (True, False):
+        config.set(conv3x3_bwd_epi=on)
+        blk.load_state_dict(state0)
+        xx = x.clone().requires_grad_()
+        o = blk(xx)
+        (o.float().square().sum() / x.shape[0]).backward()
+        outs.append((xx.grad.clone(), [p.grad.clone() for p in blk.parameters()]))
+        for p in blk.parameters():
+            p.grad = None
+    assert _rel(outs[0][0], outs[1][0]) < 2e-3
+    for a, b in zip(outs[0][1], outs[1][1]):
+        assert _rel(a, b) < 2e-3
