@@ -94,6 +94,12 @@ class Config:
         "time MFMA vs hipBLASLt per dense shape once")))
     gemm_tile: int = field(default=0, metadata=dict(env="BH_GEMM_TILE", native="gemm_tile", choices=(0, 1, 2, 3, 4),
                                                     doc="GEMM tile: 0 auto, 1 small, 2 big, 3 mid, 4 ping-pong"))
+    conv3x3_nb: int = field(default=2, metadata=dict(env="BH_CONV3X3_NB", native="conv3x3_nb", choices=(2, 3), doc=(
+        "direct 3x3 conv: LDS weight buffers (3: next step's fragments pre-read; measured 0.5% slower "
+        "end to end, profiles/conv3x3_nb_sw_ab_r6.txt)")))
+    conv3x3_sw: bool = field(default=False, metadata=dict(env="BH_CONV3X3_SW", native="conv3x3_sw", doc=(
+        "direct 3x3 conv, plain epilogue: operands swapped so it stores 8-byte channel runs (measured "
+        "slower, profiles/conv3x3_nb_sw_ab_r6.txt)")))
     gemm_log: bool = field(default=False, metadata=dict(env="BH_GEMM_LOG", native="gemm_log", rank_checked=False,
                                                         doc="log the GEMM kernel picked per shape (debugging)"))
 

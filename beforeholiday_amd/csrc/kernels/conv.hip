@@ -15,6 +15,7 @@
 // written to LDS, so no select waits on a load in front of the MFMAs.
 #include "bh/api.h"
 #include "bh/conv_api.h"
+#include "bh/knobs.h"
 #include "bh/device.h"
 
 #include <algorithm>
@@ -83,16 +84,16 @@ BH_DEVICE i4v frag_tr(const char* img, int r0, int m0, int lane) {
 // w [K_w][3][3][C_w], computing conv with W'[c][r][s][k] = w[k][2-r][2-s][c]. The slice of each
 // step is then a [k_w rows][c_w contiguous] block of w, staged as it lies and read as the MFMA A
 // operand through ds_read_b64_tr_b16 -- no transposed weight copy is ever materialised.
-template <typename T, bool FLIP, int G, bool PRO, int EPI>
+template <typename T, bool FLIP, int G, bool PRO, int EPI, int NB_ = 3, bool SW_ = true>
 __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
   // window geometry as compile-time constants (the halo address math divides by them)
   constexpr int GW = 32 / G, HC = G * (GW + 2);
   // the plain epilogue stores from the transposed accumulator layout (8-byte channel runs per lane); the
   // statistics epilogues keep the pixel-per-register layout (their per-channel sums stay in-lane)
-  constexpr bool SW = EPI == kConvEpiPlain;
+  constexpr bool SW = SW_ && EPI == kConvEpiPlain;
   // weight-slice buffers: 3 where the LDS budget of two workgroups per CU allows (the next step's first
   // fragments are then read BEFORE the barrier that ends a step), 2 for the 40-column G = 4 halo
-  constexpr int NB = G == 4 ? 2 : 3;
+  constexpr int NB = G == 4 ? 2 : NB_;
   constexpr int kHaloB = (kTH + 2) * HC * kPix;
   __shared__ __attribute__((aligned(16))) char smem[kHaloB + NB * kWBytes + (PRO ? kProBytes : 0)];
   char* halo = smem;
@@ -543,18 +544,27 @@ void conv3x3_run(int dt, const Conv3x3Args& a, bool flip, hipStream_t st) {
   if (!flip && a.epi == kConvEpiBwd) throw std::runtime_error("conv3x3_forward: no backward epilogue");
   if (flip && a.epi == kConvEpiAffine) throw std::runtime_error("conv3x3_dgrad: no affine epilogue");
   const Launch l = plan(a);
+  // pipeline variants (A/B knobs, Config.conv3x3_nb / conv3x3_sw): weight buffers 3 (next step's first
+  // fragments read before the barrier) or 2; the plain epilogue from the transposed accumulator layout
+  const int nb = knob("conv3x3_nb", 2) == 3 ? 3 : 2;
+  const bool sw = knob("conv3x3_sw", 0) != 0;
   auto launch = [&](auto tt, auto gg) {
     using T = typename decltype(tt)::type;
     constexpr int GG = decltype(gg)::value;
     auto L = [&](auto kern) { hipLaunchKernelGGL(kern, l.grid, dim3(kThreads), 0, st, a, l.g); };
     if (flip) {
       if (a.epi == kConvEpiBwd) L(k_conv3x3<T, true, GG, false, kConvEpiBwd>);
+      else if (nb == 2 && !sw) L(k_conv3x3<T, true, GG, false, kConvEpiPlain, 2, false>);
+      else if (nb == 2) L(k_conv3x3<T, true, GG, false, kConvEpiPlain, 2, true>);
+      else if (!sw) L(k_conv3x3<T, true, GG, false, kConvEpiPlain, 3, false>);
       else L(k_conv3x3<T, true, GG, false, kConvEpiPlain>);
     } else if (a.pro_scale) {
-      if (a.epi == kConvEpiStats) L(k_conv3x3<T, false, GG, true, kConvEpiStats>);
+      if (a.epi == kConvEpiStats && nb == 2) L(k_conv3x3<T, false, GG, true, kConvEpiStats, 2>);
+      else if (a.epi == kConvEpiStats) L(k_conv3x3<T, false, GG, true, kConvEpiStats>);
       else L(k_conv3x3<T, false, GG, true, kConvEpiPlain>);
     } else {
-      if (a.epi == kConvEpiStats) L(k_conv3x3<T, false, GG, false, kConvEpiStats>);
+      if (a.epi == kConvEpiStats && nb == 2) L(k_conv3x3<T, false, GG, false, kConvEpiStats, 2>);
+      else if (a.epi == kConvEpiStats) L(k_conv3x3<T, false, GG, false, kConvEpiStats>);
       else if (a.epi == kConvEpiAffine) L(k_conv3x3<T, false, GG, false, kConvEpiAffine>);
       else L(k_conv3x3<T, false, GG, false, kConvEpiPlain>);
     }

@@ -34,8 +34,28 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16"])
+    ap.add_argument("--ab", action="store_true",
+                    help="pipeline variants (Config.conv3x3_nb x conv3x3_sw) of OUR kernel, interleaved twice on one box")
     args = ap.parse_args()
     from beforeholiday_amd.ops import conv as bhconv
+
+    if args.ab:
+        from beforeholiday_amd import config
+
+        dt = torch.float16 if args.dtype == "fp16" else torch.bfloat16
+        data = []
+        for C, H, cnt in SHAPES:
+            x = torch.randn(args.batch, C, H, H, device="cuda", dtype=dt).contiguous(memory_format=torch.channels_last)
+            w = (torch.randn(C, C, 3, 3, device="cuda", dtype=dt) * 0.02).contiguous(memory_format=torch.channels_last)
+            data.append((x, w, torch.randn_like(x), cnt))
+        for rep in range(2):
+            for nb, sw in ((3, True), (2, True), (2, False), (3, False)):
+                config.set(conv3x3_nb=nb, conv3x3_sw=sw)
+                f = sum(timeit(lambda: bhconv.conv3x3(x, w)) * cnt for x, w, dy, cnt in data)
+                d = sum(timeit(lambda: bhconv.conv3x3_dgrad(dy, w)) * cnt for x, w, dy, cnt in data)
+                print(json.dumps({"rep": rep, "nb": nb, "sw": sw, "fwd_ms": round(f, 3), "dgrad_ms": round(d, 3)}),
+                      flush=True)
+        return
 
     torch.backends.cudnn.benchmark = False
     dt = torch.float16 if args.dtype == "fp16" else torch.bfloat16

@@ -354,3 +354,61 @@ def test_fused_dense_mfma_paths_large(dtype):
         torch.testing.assert_close(x.grad.float(), xr3.grad, rtol=tol["rtol"], atol=2 * tol["atol"])
         for p, r in zip(list(mlp.weights) + list(mlp.biases), ws):
             torch.testing.assert_close(p.grad.float(), r.grad, rtol=tol["rtol"], atol=tol["atol"] * 20)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+def test_reference_named_extensions_match_fp32(dt):
+    """``import fused_dense_cuda`` / ``mlp_cuda`` after install_apex_aliases() reach the same native entry
+    points as the Python layers (bindings/dense.cpp weight_grad / data_grad): linear_bias_backward,
+    linear_gelu_linear_backward and mlp backward against fp32 autograd, at a token count (8192) where the
+    weight gradients take the MFMA kernels (gemm_tn for the 1024 x 2048 weights, the 1x1 wgrad kernel for
+    the 512 x 1024 one)."""
+    import importlib
+
+    import beforeholiday_amd
+
+    beforeholiday_amd.install_apex_aliases()
+    fd = importlib.import_module("fused_dense_cuda")
+    mlp = importlib.import_module("mlp_cuda")
+    torch.manual_seed(0)
+    T, K, N = 8192, 1024, 2048
+    x = (torch.randn(T, K, device="cuda") * 0.5).to(dt)
+    w = (torch.randn(N, K, device="cuda") / K ** 0.5).to(dt)
+    b = (torch.randn(N, device="cuda") * 0.1).to(dt)
+    dy = torch.randn(T, N, device="cuda").to(dt)
+
+    def rel(a, r):
+        return float((a.float() - r).norm() / r.norm().clamp_min(1e-12))
+
+    xr, wr, br = (t.float().requires_grad_() for t in (x, w, b))
+    (torch.nn.functional.linear(xr, wr, br) * dy.float()).sum().backward()
+    dx, dw, db = fd.linear_bias_backward(x, w, dy)
+    assert rel(dx, xr.grad) < 1e-2 and rel(dw, wr.grad) < 1e-2 and rel(db, br.grad) < 1e-2
+
+    w2 = (torch.randn(512, N, device="cuda") / N ** 0.5).to(dt)
+    b2 = (torch.randn(512, device="cuda") * 0.1).to(dt)
+    dy2 = torch.randn(T, 512, device="cuda").to(dt)
+    gelu_in, out1, out2 = fd.linear_gelu_linear_forward(x, w, b, w2, b2)
+    xr, wr, br, w2r, b2r = (t.float().requires_grad_() for t in (x, w, b, w2, b2))
+    o2 = torch.nn.functional.linear(torch.nn.functional.gelu(torch.nn.functional.linear(xr, wr, br)), w2r, b2r)
+    (o2 * dy2.float()).sum().backward()
+    g = fd.linear_gelu_linear_backward(x, gelu_in, out1, w, w2, dy2)
+    for got, want in zip(g, (xr.grad, wr.grad, br.grad, w2r.grad, b2r.grad)):
+        assert rel(got, want) < 2e-2
+
+    # mlp_cuda: two ReLU layers with biases
+    ws = [w, w2]
+    bs = [b, b2]
+    outs = mlp.forward(1, 1, [x] + ws + bs)
+    xr = x.float().requires_grad_()
+    wsr = [t.float().requires_grad_() for t in ws]
+    bsr = [t.float().requires_grad_() for t in bs]
+    h = xr
+    for wi, bi in zip(wsr, bsr):
+        h = torch.relu(torch.nn.functional.linear(h, wi, bi))
+    (h * dy2.float()).sum().backward()
+    x_req = x.clone().requires_grad_()
+    grads = mlp.backward(1, 1, dy2, outs, [x_req] + ws + bs)
+    for got, want in zip(grads, [xr.grad] + [t.grad for t in wsr] + [t.grad for t in bsr]):
+        assert rel(got, want) < 2e-2
