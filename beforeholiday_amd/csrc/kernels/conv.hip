@@ -93,8 +93,16 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
   constexpr bool SW = SW_ && EPI == kConvEpiPlain;
   // weight-slice buffers: 3 where the LDS budget of two workgroups per CU allows (the next step's first
   // fragments are then read BEFORE the barrier that ends a step), 2 for the 40-column G = 4 halo
-  constexpr int NB = G == 4 ? 2 : NB_;
-  constexpr int kHaloB = (kTH + 2) * HC * kPix;
+  constexpr int NB = G == 1 ? NB_ : 2;
+  // halo row stride and the byte shift of each image block: with G images side by side the 16-lane
+  // groups of ds_read_b128 ({0-3, 12-15, 20-27}, {4-11, 16-19, 28-31}, + 32) span two images, and at the
+  // plain 144-byte slot pitch image 1's pixels land on image 0's banks (2-way at G = 2, 3-way at G = 4).
+  // Block b = pix / (GW + 2) of the halo (image b % G of row b / G) is shifted by b * kImgShift bytes:
+  // 224 B makes every group conflict free at G = 2; at G = 4 that would not fit two workgroups' LDS,
+  // 32 B leaves 2-way (exhaustive search over the shifts).
+  constexpr int kImgShift = G == 2 ? 224 : G == 4 ? 32 : 0;
+  constexpr int RS = HC * kPix + G * kImgShift;
+  constexpr int kHaloB = (kTH + 2) * RS;
   __shared__ __attribute__((aligned(16))) char smem[kHaloB + NB * kWBytes + (PRO ? kProBytes : 0)];
   char* halo = smem;
   char* wb = smem + kHaloB;
@@ -184,7 +192,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
           for (int j = 0; j < 8; ++j) e[j] = from_f<T>(fmaxf(fmaf(to_f<T>(e[j]), sc[j], sh[j]), 0.f));
           v = ((hmask >> i) & 1u) ? __builtin_bit_cast(i4v, e) : i4v{0, 0, 0, 0};
         }
-        *reinterpret_cast<i4v*>(halo + (q >> 3) * kPix + (q & 7) * 16) = v;
+        const int pix = q >> 3;
+        *reinterpret_cast<i4v*>(halo + pix * kPix + (pix / (GW + 2)) * kImgShift + (q & 7) * 16) = v;
       }
     }
   };
@@ -225,7 +234,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
         for (int i = 0; i < 16; ++i) acc[kb][pb][i] = 0.f;
   };
   const int gi = r32 / GW, jl = r32 - gi * GW;
-  const int hcol = gi * (GW + 2) + jl;  // this lane's halo column at s = 0
+  const int hlane = (gi * (GW + 2) + jl) * kPix + gi * kImgShift;  // this lane's halo pixel at s = 0
   T* Y = reinterpret_cast<T*>(a.y);
   const T* BY = reinterpret_cast<const T*>(a.by);
   // Output tile of the wave, D[pixel][channel] (the MFMA's A operand is the halo, B the weights):
@@ -326,8 +335,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
   // the reduction channels read transposed) and the halo at offset (rs / 3, rs % 3)
   auto frags = [&](const char* wcur, int rs, int kk, i4v (&f)[4]) __attribute__((always_inline)) {
     const int r = rs / 3, s = rs - r * 3;
-    const char* hb0 = halo + ((2 * wave + r) * HC + hcol + s) * kPix;  // window row 2w, offset (r, s)
-    const char* hb1 = hb0 + HC * kPix;                                    // window row 2w + 1
+    const char* hb0 = halo + (2 * wave + r) * RS + s * kPix + hlane;  // window row 2w, offset (r, s)
+    const char* hb1 = hb0 + RS;                                         // window row 2w + 1
     const int ch = 2 * kk + h;
     if (FLIP) {
       f[0] = frag_tr(wcur, 16 * kk + 8 * h, 0, lane);

@@ -17,5 +17,6 @@ for counters in "SQ_WAVES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIV
   if [ $rc -ne 0 ]; then echo "pass $i rc=$rc, stopping"; exit $rc; fi
 done
 python3 scripts/pmc_summary.py gpurun_out/pmcr > gpurun_out/pmcr_summary.md
+python3 scripts/pmc_summary.py gpurun_out/pmcr --table > gpurun_out/pmcr_table.md
 rm -rf gpurun_out/pmcr/p*/
 head -5 gpurun_out/pmcr_summary.md

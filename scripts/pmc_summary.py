@@ -33,7 +33,9 @@ def main():
                 elif "k_conv3x3" in name:
                     # the first template bool after the dtype is FLIP (the data gradient)
                     kind = "dgrad" if re.search(r"k_conv3x3I(DF16_|DF16b)Lb1E", name) else "fwd"
-                    g = "G4" if "Li4E" in name else ("G2" if "Li2E" in name else "G1")
+                    # G is the first int template argument (the weight-buffer count NB also is an int)
+                    gm = re.search(r"k_conv3x3I(?:DF16_|DF16b)Lb[01]ELi(\d)E", name)
+                    g = "G" + (gm.group(1) if gm else "?")
                     name = f"conv3x3_{kind}<{g}>"
                 elif "k_conv_wgrad" in name:
                     geo = {"Li3ELi14ELi2E": "3x3 56x56", "Li3ELi7ELi4E": "3x3 28x28", "Li3ELi4ELi7E": "3x3 14x14",
@@ -51,6 +53,27 @@ def main():
                     continue
                 vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
                 vals[name]["duration_us"].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    if "--table" in sys.argv:  # one row per kernel family: the derived ratios only
+        print("| kernel | dispatches | us / dispatch | MFMA util | non-MFMA VALU / MFMA | LDS conflict share | "
+              "L2 hit | wait share of wave cycles |")
+        print("|---|---|---|---|---|---|---|---|")
+        for k in sorted(vals):
+            m = {c: sum(v) / len(v) for c, v in vals[k].items()}
+            n = len(vals[k]["duration_us"]) // max(1, len([c for c in vals[k] if c != "duration_us"]))
+
+            def f(x):
+                return "-" if x is None else f"{x:.2f}"
+            util = (m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["GRBM_GUI_ACTIVE"] / 8 * 1024)
+                    if "SQ_VALU_MFMA_BUSY_CYCLES" in m and m.get("GRBM_GUI_ACTIVE") else None)
+            valu = ((m["SQ_INSTS_VALU"] - m["SQ_INSTS_MFMA"]) / m["SQ_INSTS_MFMA"]
+                    if m.get("SQ_INSTS_MFMA") and "SQ_INSTS_VALU" in m else None)
+            lds = (m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"]
+                   if "SQ_LDS_BANK_CONFLICT" in m and m.get("SQ_LDS_IDX_ACTIVE") else None)
+            l2 = (m["TCC_HIT_sum"] / (m["TCC_HIT_sum"] + m["TCC_MISS_sum"])
+                  if "TCC_HIT_sum" in m and (m["TCC_HIT_sum"] + m.get("TCC_MISS_sum", 0)) else None)
+            wait = m["SQ_WAIT_ANY"] / m["SQ_WAVE_CYCLES"] if m.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in m else None
+            print(f"| {k} | {n} | {m['duration_us']:.1f} | {f(util)} | {f(valu)} | {f(lds)} | {f(l2)} | {f(wait)} |")
+        return
     print("| kernel | counter | mean per dispatch |")
     print("|---|---|---|")
     for k in sorted(vals):

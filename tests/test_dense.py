@@ -410,5 +410,9 @@ def test_reference_named_extensions_match_fp32(dt):
     (h * dy2.float()).sum().backward()
     x_req = x.clone().requires_grad_()
     grads = mlp.backward(1, 1, dy2, outs, [x_req] + ws + bs)
+    # two ReLU masks taken from 16-bit activations: an exact 16-bit pipeline (fp32 accumulation, every
+    # output rounded) is itself 1.2 % (fp16) / 3.2 % (bf16) from fp32 autograd in dx at this shape
+    # (emulated on the CPU), so the bf16 gate is looser
+    tol = 2e-2 if dt == torch.float16 else 4e-2
     for got, want in zip(grads, [xr.grad] + [t.grad for t in wsr] + [t.grad for t in bsr]):
-        assert rel(got, want) < 2e-2
+        assert rel(got, want) < tol
