@@ -6,9 +6,16 @@ so timing a region never stalls the host or drains the queue (the reference sync
 at every start and stop). Intervals pile up as event pairs and are resolved lazily: ``elapsed`` waits for
 the last recorded stop event only, then sums ``start.elapsed_time(stop)`` over the pairs. Without a GPU the
 same interface runs on ``time.perf_counter``.
+
+An interval is tied to the stream it started on: stopping it from another stream raises (the event pair
+would measure nothing meaningful), and work on streams the timed stream does not wait on is not counted.
+``_Timers(sync=True)`` (or ``BH_TIMERS_SYNC=1``) restores the reference's device-synchronised wall-clock
+timing for regions that include host or side-stream work. Closed intervals are folded into the total
+whenever more than ``_FOLD_AT`` are pending, for the ones whose stop event has already completed.
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import Dict, Iterable, List, Optional, Tuple
 
@@ -19,26 +26,45 @@ def _on_device() -> bool:
     return torch.cuda.is_available() and torch.cuda.is_initialized()
 
 
+_FOLD_AT = 64  # closed intervals pending before the completed ones are folded into the total
+
+
 class _Interval:
-    """One started (and maybe stopped) interval: a pair of HIP events, or two perf_counter stamps."""
+    """One started (and maybe stopped) interval: a pair of HIP events on one stream, or two perf_counter
+    stamps (no GPU, or sync mode: the device is synchronised at both ends, as the reference does)."""
 
-    __slots__ = ("dev", "t0", "t1")
+    __slots__ = ("dev", "sync", "stream", "t0", "t1")
 
-    def __init__(self):
-        self.dev = _on_device()
+    def __init__(self, sync: bool = False):
+        on = _on_device()
+        self.sync = sync and on
+        self.dev = on and not sync
+        self.stream = None
         if self.dev:
+            self.stream = torch.cuda.current_stream()
             self.t0 = torch.cuda.Event(enable_timing=True)
-            self.t0.record()
+            self.t0.record(self.stream)
         else:
+            if self.sync:
+                torch.cuda.synchronize()
             self.t0 = time.perf_counter()
         self.t1 = None
 
-    def close(self):
+    def close(self, name: str = "?"):
         if self.dev:
+            cur = torch.cuda.current_stream()
+            if cur != self.stream:
+                raise RuntimeError(f"timer {name!r} started on {self.stream} and stopped on {cur}: an event pair "
+                                   "across streams measures nothing (time each stream separately, or sync mode)")
             self.t1 = torch.cuda.Event(enable_timing=True)
-            self.t1.record()
+            self.t1.record(self.stream)
         else:
+            if self.sync:
+                torch.cuda.synchronize()
             self.t1 = time.perf_counter()
+
+    def done(self) -> bool:
+        return not self.dev or self.t1.query()
 
     def seconds(self) -> float:
         if self.dev:
@@ -48,8 +74,9 @@ class _Interval:
 
 
 class _Timer:
-    def __init__(self, name: str):
+    def __init__(self, name: str, sync: bool = False):
         self.name = name
+        self.sync = sync
         self._done: List[_Interval] = []  # closed intervals not yet folded into _total
         self._open: Optional[_Interval] = None
         self._total = 0.0  # seconds of resolved intervals
@@ -61,14 +88,22 @@ class _Timer:
     def start(self):
         if self._open is not None:
             raise RuntimeError(f"timer {self.name!r} is already running")
-        self._open = _Interval()
+        self._open = _Interval(self.sync)
 
     def stop(self):
         if self._open is None:
             raise RuntimeError(f"timer {self.name!r} was not started")
-        self._open.close()
+        self._open.close(self.name)
         self._done.append(self._open)
         self._open = None
+        if len(self._done) > _FOLD_AT:  # fold the finished pairs (no wait) so they do not pile up
+            keep = []
+            for iv in self._done:
+                if iv.done():
+                    self._total += iv.seconds()
+                else:
+                    keep.append(iv)
+            self._done = keep
 
     def reset(self):
         self._done.clear()
@@ -97,13 +132,14 @@ class _Timer:
 class _Timers:
     """``timers(name)`` returns (creating on first use) the named :class:`_Timer`."""
 
-    def __init__(self):
+    def __init__(self, sync: Optional[bool] = None):
         self.timers: Dict[str, _Timer] = {}
+        self.sync = os.environ.get("BH_TIMERS_SYNC", "0") == "1" if sync is None else sync
 
     def __call__(self, name: str) -> _Timer:
         t = self.timers.get(name)
         if t is None:
-            t = self.timers[name] = _Timer(name)
+            t = self.timers[name] = _Timer(name, self.sync)
         return t
 
     def _values(self, names: Iterable[str], normalizer: float, reset: bool) -> List[Tuple[str, float]]:

@@ -100,3 +100,38 @@ def test_pipeline_timers(device, capsys):
     w = _W()
     timers.write(["fwd"], w, 7)
     assert w.rows == [("fwd-time", 7)]
+
+
+def test_pipeline_timers_fold_and_sync_mode():
+    """Closed intervals are folded once more than _FOLD_AT pile up (the total is unchanged), and the
+    sync-mode timers (reference wall-clock semantics) accumulate like the event timers."""
+    import time
+
+    from beforeholiday_amd.transformer.pipeline_parallel import _timers as tm
+
+    timers = tm._Timers(sync=True)
+    t = timers("step")
+    for _ in range(tm._FOLD_AT + 5):
+        t.start()
+        t.stop()
+    assert len(t._done) <= tm._FOLD_AT
+    t.start()
+    time.sleep(0.005)
+    t.stop()
+    assert t.elapsed() >= 0.005
+
+
+@pytest.mark.gpu
+def test_pipeline_timer_rejects_cross_stream_stop():
+    """An interval started on one stream and stopped on another raises instead of timing nothing."""
+    from beforeholiday_amd.transformer.pipeline_parallel._timers import _Timers
+
+    torch.cuda.init()
+    t = _Timers()("x")
+    t.start()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with pytest.raises(RuntimeError, match="across streams"):
+            t.stop()
+    t.stop()
+    assert t.elapsed() >= 0.0
