@@ -100,6 +100,9 @@ class Config:
     conv3x3_sw: bool = field(default=False, metadata=dict(env="BH_CONV3X3_SW", native="conv3x3_sw", doc=(
         "direct 3x3 conv, plain epilogue: operands swapped so it stores 8-byte channel runs (measured "
         "slower, profiles/conv3x3_nb_sw_ab_r6.txt)")))
+    igemm_lds: bool = field(default=False, metadata=dict(env="BH_IGEMM_LDS", native="igemm_lds", doc=(
+        "stride-2 3x3 implicit GEMM: both operands staged in LDS by LDS-DMA (measured slower than the "
+        "register-staged A fragments, profiles/igemm_lds_ab_r6.txt)")))
     gemm_log: bool = field(default=False, metadata=dict(env="BH_GEMM_LOG", native="gemm_log", rank_checked=False,
                                                         doc="log the GEMM kernel picked per shape (debugging)"))
 

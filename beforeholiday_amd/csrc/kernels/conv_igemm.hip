@@ -19,6 +19,7 @@
 #include "bh/api.h"
 #include "bh/device.h"
 #include "bh/igemm_api.h"
+#include "bh/knobs.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -54,6 +55,62 @@ constexpr int kCK = 64;            // input channels per k-step
 constexpr int kRS = kCK * 2 + 16;  // LDS bytes per staged weight row
 constexpr int kMaxProC = 512;
 constexpr int kOutOfRange = 0x7ff00000;  // a byte offset past every tensor the kernel reads
+
+// output + statistics epilogue shared by both kernels: acc[m][t][v] is output pixel 32 m + 8 (v >> 2) + 4 h +
+// (v & 3) of the wave's MW rows, channel 32 t + r; red: >= 8 NC floats of LDS no wave still reads
+template <typename T, int NC, int MW, bool STATS>
+BH_DEVICE void igemm_epilogue(const IgemmArgs& a, const IgemmPhase& ph, f16v (&acc)[MW / 32][NC / 32], int mt,
+                              int o0, int tiles_m, float* red) {
+  constexpr int NT = NC / 32, MT = MW / 32;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int HWg = a.Hg * a.Wg;
+  const int64_t P = (int64_t)a.N * HWg;
+  T* __restrict__ Y = reinterpret_cast<T*>(a.y);
+  float s1[NT], s2[NT], e0[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    s1[t] = s2[t] = 0.f;
+    e0[t] = (STATS && a.kshift) ? a.kshift[o0 + 32 * t + r] : 0.f;
+  }
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int64_t p = (int64_t)mt * (kWaves * MW) + wave * MW + 32 * m + 8 * (v >> 2) + 4 * h + (v & 3);
+      if (p >= P) continue;
+      const int n = (int)(p / HWg), rem = (int)(p - (int64_t)n * HWg), i = rem / a.Wg, j = rem - i * a.Wg;
+      const int64_t off = (((int64_t)n * a.Hy + i * a.so + ph.py) * a.Wy + j * a.so + ph.px) * a.Nout + o0 + r;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const T o = from_f<T>(acc[m][t][v]);
+        Y[off + 32 * t] = o;
+        if constexpr (STATS) {
+          const float d = to_f<T>(o) - e0[t];
+          s1[t] += d;
+          s2[t] = fmaf(d, d, s2[t]);
+        }
+      }
+    }
+  if constexpr (STATS) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      s1[t] += __shfl_xor(s1[t], 32);
+      s2[t] += __shfl_xor(s2[t], 32);
+      if (h == 0) {
+        red[(wave * 2) * NC + 32 * t + r] = s1[t];
+        red[(wave * 2 + 1) * NC + 32 * t + r] = s2[t];
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < 2 * NC; c += kThreads) {
+      const int stat = c / NC, col = c - stat * NC;
+      float u = 0.f;
+#pragma unroll
+      for (int q = 0; q < kWaves; ++q) u += red[(q * 2 + stat) * NC + col];
+      a.part[((int64_t)stat * tiles_m + mt) * a.Nout + o0 + col] = u;
+    }
+  }
+}
 
 template <typename T, int NC, int MW, bool PRO, bool STATS>
 __global__ __launch_bounds__(kThreads, 2) void k_igemm(IgemmArgs a, int tiles_m) {
@@ -195,53 +252,194 @@ __global__ __launch_bounds__(kThreads, 2) void k_igemm(IgemmArgs a, int tiles_m)
     __syncthreads();
   }
 
-  // ---- epilogue ----
-  T* __restrict__ Y = reinterpret_cast<T*>(a.y);
-  float s1[NT], s2[NT], e0[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    s1[t] = s2[t] = 0.f;
-    e0[t] = (STATS && a.kshift) ? a.kshift[o0 + 32 * t + r] : 0.f;
+  // ---- epilogue ---- (the weight buffers are free: every wave passed the loop's last barrier)
+  igemm_epilogue<T, NC, MW, STATS>(a, ph, acc, mt, o0, tiles_m, reinterpret_cast<float*>(smem));
+}
+
+
+// ---- LDS-staged variant (Config.igemm_lds) ----
+// Both operands of a k-step arrive by LDS-DMA (buffer_load ... lds: 16 B per lane through whole-tensor
+// resources; a tap outside the image gets an out-of-range offset and lands as zeros) in 144-byte pixel /
+// weight-row slots (conflict-free ds_read_b128 fragments), double buffered with ONE barrier per k-step.
+// No operand passes through VGPRs on its way in, and the A fragments come from LDS instead of
+// fragment-shaped global loads (16 B of each of 32 pixels per instruction), which keep the waves of the
+// register-staged kernel waiting on memory (MFMA ~20 %, profiles/conv_pmc_r6.md). 128 output pixels x NC
+// channels per workgroup, 32 pixels x NC per wave, as k_igemm<NC, 32>. Measured SLOWER (data gradient
+// 1.1-1.2x, forward with the prologue 1.05-1.18x the time; -0.5 % per ResNet-50 step,
+// profiles/igemm_lds_ab_r6.txt): the double-buffered stages cost the third workgroup per CU (LDS) and
+// every 16-MFMA k-step waits for its DMA at a barrier; so it stays behind Config.igemm_lds (default off).
+constexpr int kSlot = 144;
+constexpr int kTileP = kWaves * 32;
+constexpr unsigned kRsrcWord3 = 0x00020000u;
+typedef int i4s __attribute__((ext_vector_type(4)));
+
+// one LDS-DMA instruction (lane-linear 16 B at LDS byte address lds) through resource rs: inline asm, so the
+// compiler does not order its LDS write against reads of the other buffer (it would put a vmcnt(0) in
+// front of every ds_read); the kernel orders them (vmcnt + barrier at the k-step boundary)
+BH_DEVICE void dma16(i4s rs, int voff, unsigned lds) {
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %0, %2, 0 offen lds" ::"v"(voff),
+      "s"(lds), "s"(rs)
+      : "memory", "m0");
+}
+BH_DEVICE i4s rsrc(const void* base, int64_t bytes) {
+  const uint64_t b = reinterpret_cast<uint64_t>(base);
+  return i4s{(int)(uint32_t)b, (int)((b >> 32) & 0xffff), (int)(uint32_t)bytes, (int)kRsrcWord3};
+}
+BH_DEVICE unsigned lds_u32(const void* p) {
+  return (unsigned)(uintptr_t)((const __attribute__((address_space(3))) char*)p);
+}
+template <int N> BH_DEVICE void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+BH_DEVICE void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <typename T, int NC, bool PRO, bool STATS>
+__global__ __launch_bounds__(kThreads, 2) void k_igemm_lds(IgemmArgs a, int tiles_m) {
+  constexpr int NT = NC / 32;
+  constexpr int PA = kTileP * kSlot / 1024, PB = NC * kSlot / 1024;  // 1-KiB DMA pieces (18, 18 / 9)
+  static_assert(kTileP * kSlot % 1024 == 0 && NC * kSlot % 1024 == 0, "slot images are whole pieces");
+  // A pieces wave + 4 i (i < NPA) and B pieces wave + 4 j (j < NPB) of a stage per wave
+  constexpr int STAGE = (PA + PB) * 1024, NPA = (PA + kWaves - 1) / kWaves, NPB = (PB + kWaves - 1) / kWaves;
+  constexpr int NPW = NPA + NPB;
+  using V8 = typename Mfi<T>::v8;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + (PRO ? 8 * kMaxProC : 0)];
+  const int mt = blockIdx.x;
+  if (mt >= tiles_m) return;  // (whole workgroup, before any barrier)
+  const IgemmPhase& ph = a.ph[blockIdx.z];
+  const int o0 = blockIdx.y * NC;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Ha = a.Ha, Wa = a.Wa, Ca = a.Ca;
+  const int HWg = a.Hg * a.Wg;
+  const int64_t P = (int64_t)a.N * HWg;
+  float* ss = reinterpret_cast<float*>(smem + 2 * STAGE);
+  if constexpr (PRO) {
+    for (int c = tid; c < Ca; c += kThreads) {
+      ss[c] = a.pro_scale[c];
+      ss[kMaxProC + c] = a.pro_shift[c];
+    }
   }
+  const i4s rsA = rsrc(a.a, (int64_t)a.N * Ha * Wa * Ca * 2);
+  const i4s rsB = rsrc(a.b, (int64_t)a.Nout * a.taps_total * Ca * 2);
+  constexpr int kBadYX = 0x40004000;  // a (y, x) base no tap brings inside the image
+  // pixel (row / column base of the tap grid, packed 16:16) and source offset of a tile pixel
+  auto pixel = [&](int slot, int& yx, int& off) __attribute__((always_inline)) {
+    const int64_t p = (int64_t)mt * kTileP + slot;
+    if (p >= P) {
+      yx = kBadYX;
+      off = 0;
+      return;
+    }
+    const int pn = (int)(p / HWg), rem = (int)(p - (int64_t)pn * HWg), pi = rem / a.Wg, pj = rem - pi * a.Wg;
+    yx = ((pi * a.sa) << 16) | (pj * a.sa);
+    off = ((pn * Ha + pi * a.sa) * Wa + pj * a.sa) * Ca * 2;
+  };
+  // this lane's part of its pieces: piece pc of an image fills bytes [1024 pc + 16 lane, +16) of it, i.e.
+  // chunk ch of slot sl (ch 8 = the slot's pad: stays an out-of-range read)
+  int pyx[NPA], poff[NPW];
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+  for (int i = 0; i < NPW; ++i) {
+    const bool isa = i < NPA;
+    const int pc = wave + kWaves * (isa ? i : i - NPA);
+    const int byte = pc * 1024 + 16 * lane, sl = byte / kSlot, ch = (byte - sl * kSlot) >> 4;
+    poff[i] = -1;
+    if (isa) {
+      pyx[i] = kBadYX;
+      if (pc < PA && ch < 8) {
+        pixel(sl, pyx[i], poff[i]);
+        poff[i] += ch * 16;
+      }
+    } else if (pc < PB && ch < 8) {
+      poff[i] = (o0 + sl) * a.taps_total * Ca * 2 + ch * 16;
+    }
+  }
+  // the compute pixel of this lane (PRO: padding taps stay zero, in-image ones get the BatchNorm)
+  int cyx = kBadYX, coff = 0;
+  if constexpr (PRO) pixel(wave * 32 + r, cyx, coff);
+  (void)coff;
+  const int nch = Ca / kCK, steps = ph.ntaps * nch;
+  auto in_image = [&](int yx, int oy, int ox) __attribute__((always_inline)) {
+    const int yi = (yx >> 16) + oy, xi = (yx & 0xffff) + ox;
+    return yi >= 0 && yi < Ha && xi >= 0 && xi < Wa;
+  };
+  auto issue = [&](int s, char* stage) __attribute__((always_inline)) {
+    const int t = s / nch, c = s - t * nch;
+    const int oy = ph.oy[t], ox = ph.ox[t], tap = ph.tap[t];
+    const int adel = ((oy * Wa + ox) * Ca + c * kCK) * 2, bdel = (tap * Ca + c * kCK) * 2;
 #pragma unroll
-    for (int v = 0; v < 16; ++v) {
-      const int64_t p = (int64_t)mt * (kWaves * MW) + wave * MW + 32 * m + 8 * (v >> 2) + 4 * h + (v & 3);
-      if (p >= P) continue;
-      const int n = (int)(p / HWg), rem = (int)(p - (int64_t)n * HWg), i = rem / a.Wg, j = rem - i * a.Wg;
-      const int64_t off = (((int64_t)n * a.Hy + i * a.so + ph.py) * a.Wy + j * a.so + ph.px) * a.Nout + o0 + r;
+    for (int i = 0; i < NPA; ++i) {
+      const int pc = wave + kWaves * i;
+      if (pc < PA)  // (wave-uniform; only the last i can fail)
+        dma16(rsA, in_image(pyx[i], oy, ox) ? poff[i] + adel : kOutOfRange,
+              __builtin_amdgcn_readfirstlane(lds_u32(stage + pc * 1024)));
+    }
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const T o = from_f<T>(acc[m][t][v]);
-        Y[off + 32 * t] = o;
-        if constexpr (STATS) {
-          const float d = to_f<T>(o) - e0[t];
-          s1[t] += d;
-          s2[t] = fmaf(d, d, s2[t]);
+    for (int j = 0; j < NPB; ++j) {
+      const int pc = wave + kWaves * j;
+      if (pc < PB)
+        dma16(rsB, poff[NPA + j] >= 0 ? poff[NPA + j] + bdel : kOutOfRange,
+              __builtin_amdgcn_readfirstlane(lds_u32(stage + (PA + pc) * 1024)));
+    }
+  };
+
+  f16v acc[1][NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[0][t][i] = 0.f;
+
+  auto compute = [&](const char* stage, int s) __attribute__((always_inline)) {
+    const char* as = stage + (wave * 32 + r) * kSlot + 16 * h;
+    const char* bs = stage + PA * 1024 + r * kSlot + 16 * h;
+    bool ok = true;
+    int cb = 0;
+    if constexpr (PRO) {
+      const int t = s / nch, c = s - t * nch;
+      ok = in_image(cyx, ph.oy[t], ph.ox[t]);
+      cb = c * kCK + 8 * h;
+    }
+    // every fragment of the step first (4 A + 4 NT B reads in flight), then the MFMAs
+    i4v av[4], bv[4][NT];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      av[ks] = *reinterpret_cast<const i4v*>(as + 32 * ks);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) bv[ks][t] = *reinterpret_cast<const i4v*>(bs + 32 * t * kSlot + 32 * ks);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if constexpr (PRO) {
+        if (ok) {
+          const float* sc = ss + cb + 16 * ks;
+          V8 v = __builtin_bit_cast(V8, av[ks]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = from_f<T>(fmaxf(fmaf(to_f<T>(v[j]), sc[j], sc[kMaxProC + j]), 0.f));
+          av[ks] = __builtin_bit_cast(i4v, v);
         }
       }
-    }
-  if constexpr (STATS) {
-    float* red = reinterpret_cast<float*>(smem);  // [waves][2][NC] (the weight buffers are free)
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      s1[t] += __shfl_xor(s1[t], 32);
-      s2[t] += __shfl_xor(s2[t], 32);
-      if (h == 0) {
-        red[(wave * 2) * NC + 32 * t + r] = s1[t];
-        red[(wave * 2 + 1) * NC + 32 * t + r] = s2[t];
-      }
+      for (int t = 0; t < NT; ++t) acc[0][t] = Mfi<T>::run(av[ks], bv[ks][t], acc[0][t]);
     }
-    __syncthreads();
-    for (int c = tid; c < 2 * NC; c += kThreads) {
-      const int stat = c / NC, col = c - stat * NC;
-      float u = 0.f;
-#pragma unroll
-      for (int q = 0; q < kWaves; ++q) u += red[(q * 2 + stat) * NC + col];
-      a.part[((int64_t)stat * tiles_m + mt) * a.Nout + o0 + col] = u;
-    }
+  };
+
+  // k-step s computes from stage s & 1 while the DMA of step s + 1 fills the other stage; every issue is
+  // unconditional (past the last step it re-reads the last one into the free stage, never used)
+  const int last = steps - 1;
+  issue(0, smem);
+  for (int s = 0; s < steps; ++s) {
+    wait_vm<0>();   // this wave's pieces of step s have landed ...
+    lds_barrier();  // ... and everyone's; everyone is done reading the other stage (step s - 1)
+    issue(min(s + 1, last), smem + ((s + 1) & 1) * STAGE);
+    compute(smem + (s & 1) * STAGE, s);
   }
+  wait_vm<0>();  // no DMA may land in LDS after the workgroup has ended
+  __syncthreads();  // every wave done with the stages (the statistics reduction reuses them)
+  igemm_epilogue<T, NC, 32, STATS>(a, ph, acc, mt, o0, tiles_m, reinterpret_cast<float*>(smem));
 }
 
 struct Plan {
@@ -293,10 +491,20 @@ void igemm_run(int dt, const IgemmArgs& a, hipStream_t st) {
   const Plan pl = make_plan(a);
   const dim3 grid((unsigned)pl.tiles_m, (unsigned)(a.Nout / pl.NC), (unsigned)a.nphase);
   const bool pro = a.pro_scale != nullptr, stats = a.part != nullptr;
+  const bool lds = knob("igemm_lds", 0) != 0;  // Config.igemm_lds: the LDS-staged kernel (NC = 128 plans)
   auto go = [&](auto tt, auto nc, auto mw) {
     using T = typename decltype(tt)::type;
     constexpr int NC = decltype(nc)::value, MW = decltype(mw)::value;
     auto L = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(kThreads), 0, st, a, pl.tiles_m); };
+    if constexpr (MW == 32 && NC == 128) {
+      if (lds) {
+        if (pro && stats) L(k_igemm_lds<T, NC, true, true>);
+        else if (pro) L(k_igemm_lds<T, NC, true, false>);
+        else if (stats) L(k_igemm_lds<T, NC, false, true>);
+        else L(k_igemm_lds<T, NC, false, false>);
+        return;
+      }
+    }
     if constexpr (MW == 32) {
       if (pro && stats) L(k_igemm<T, NC, MW, true, true>);
       else if (pro) L(k_igemm<T, NC, MW, true, false>);

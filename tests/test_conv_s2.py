@@ -105,3 +105,30 @@ def test_s2_large_grid_and_repeatable():
     wr = w.float().requires_grad_()
     torch.nn.functional.conv2d(x.float(), wr, stride=2, padding=1).backward(dy.float())
     assert _rel(dw0, wr.grad) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pro", [False, True])
+def test_s2_lds_staged_kernel_matches_register_staged(pro):
+    """Config.igemm_lds: the LDS-DMA-staged implicit GEMM (k_igemm_lds) and the register-staged one
+    (k_igemm) compute the same sums in the same order per output (fp32 accumulation over the same k-steps),
+    so forward (with / without the BatchNorm prologue, with statistics) and data gradient agree bitwise."""
+    from beforeholiday_amd import config
+    from beforeholiday_amd.ops import conv as bhconv
+
+    n, c, h, k = 4, 256, 28, 256
+    x, w, dy = _data(n, c, h, k, torch.float16, seed=3)
+    g = torch.Generator(device="cuda").manual_seed(4)
+    sc = (torch.rand(c, device="cuda", generator=g) + 0.5) if pro else None
+    sh = (torch.randn(c, device="cuda", generator=g) * 0.2) if pro else None
+    outs = {}
+    for lds in (False, True):
+        with config.override(igemm_lds=lds):
+            y, part = bhconv.conv3x3_s2(x, w, pro_scale=sc, pro_shift=sh, stats=True)
+            dx = bhconv.conv3x3_s2_dgrad(dy, w, (h, h))
+        torch.cuda.synchronize()
+        outs[lds] = (y, part, dx)
+    for a, b in zip(outs[False], outs[True]):
+        assert torch.equal(a, b)
+    ref = _conv_ref(torch.relu(x.float() * sc[None, :, None, None] + sh[None, :, None, None]) if pro else x, w)
+    assert _rel(outs[True][0], ref) < 1e-2
