@@ -30,6 +30,27 @@ def _seed():
     return s
 
 
+def _tp_rank() -> int:
+    try:
+        from ...transformer import parallel_state
+
+        if parallel_state.model_parallel_is_initialized():
+            return parallel_state.get_tensor_model_parallel_rank()
+    except Exception:  # noqa: BLE001 - parallel_state unavailable / uninitialised
+        pass
+    return 0
+
+
+def _seed_pair():
+    """(host seed, device step seed or None): device step seeds (utils/graph_rng.py) when a captured step
+    is being replayed, the host Philox seed otherwise."""
+    from ...utils import graph_rng
+
+    if graph_rng.active():
+        return graph_rng.next_salt(_tp_rank()), graph_rng.step_seed()
+    return _seed(), None
+
+
 class MaskSoftmaxDropoutFn(torch.autograd.Function):
     """scores [B*heads, sq, sk] -> dropout(softmax(masked scores))."""
 
@@ -121,15 +142,17 @@ class FusedSelfAttnFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, qkv, heads, scale, mask, mask_mode, p, training, fill=float("-inf"), bits=None):
-        seed = _seed()
+        seed, sd = _seed_pair()
+        ctx.seed_dev = sd
         fa = submodule("fused_attention")
         q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
-        short = _short_ok(qkv.size(0), mask_mode, fill)
+        short = _short_ok(qkv.size(0), mask_mode, fill) and sd is None  # (device seeds: flash kernels only)
         if short:
             out = fa.forward(q, k, v, mask_mode, mask, heads, scale, p, training, seed)
             lse = torch.empty(0)
         else:
-            out, lse = fa.flash_forward(q, k, v, mask_mode, mask, heads, scale, p, training, seed, fill, bits)
+            out, lse = fa.flash_forward(q, k, v, mask_mode, mask, heads, scale, p, training, seed, fill, bits,
+                                        seed_dev=sd)
         ctx.save_for_backward(qkv, mask if mask is not None else torch.empty(0), out if not short else torch.empty(0),
                               lse, bits if bits is not None else torch.empty(0))
         ctx.args = (heads, scale, mask_mode, p, training, seed, mask is not None, fill, short, bits is not None)
@@ -148,7 +171,8 @@ class FusedSelfAttnFn(torch.autograd.Function):
                         dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2])
         else:
             fa.flash_backward(dout.contiguous(), q, k, v, out, lse, mask_mode, m, heads, scale, p, training, seed,
-                              fill, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2], bits if has_bits else None)
+                              fill, dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2], bits if has_bits else None,
+                              seed_dev=ctx.seed_dev)
         return dqkv, None, None, None, None, None, None, None, None
 
 
@@ -157,15 +181,16 @@ class FusedEncdecAttnFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, q, kv, heads, scale, mask, mask_mode, p, training):
-        seed = _seed()
+        seed, sd = _seed_pair()
+        ctx.seed_dev = sd
         fa = submodule("fused_attention")
-        short = _short_ok(kv.size(0), mask_mode, float("-inf"))
+        short = _short_ok(kv.size(0), mask_mode, float("-inf")) and sd is None
         if short:
             out = fa.forward(q, kv[:, :, 0], kv[:, :, 1], mask_mode, mask, heads, scale, p, training, seed)
             lse = torch.empty(0)
         else:
             out, lse = fa.flash_forward(q, kv[:, :, 0], kv[:, :, 1], mask_mode, mask, heads, scale, p, training, seed,
-                                        float("-inf"))
+                                        float("-inf"), seed_dev=sd)
         ctx.save_for_backward(q, kv, mask if mask is not None else torch.empty(0), out if not short else torch.empty(0),
                               lse)
         ctx.args = (heads, scale, mask_mode, p, training, seed, mask is not None, short)
@@ -184,7 +209,7 @@ class FusedEncdecAttnFn(torch.autograd.Function):
                         dq, dkv[:, :, 0], dkv[:, :, 1])
         else:
             fa.flash_backward(dout.contiguous(), q, kv[:, :, 0], kv[:, :, 1], out, lse, mask_mode, m, heads, scale, p,
-                              training, seed, float("-inf"), dq, dkv[:, :, 0], dkv[:, :, 1])
+                              training, seed, float("-inf"), dq, dkv[:, :, 0], dkv[:, :, 1], seed_dev=ctx.seed_dev)
         return dq, dkv, None, None, None, None, None, None
 
 

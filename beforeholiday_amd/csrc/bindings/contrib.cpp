@@ -414,11 +414,21 @@ at::Tensor flash_mask_bits_op(at::Tensor mask) {
   return mb;
 }
 
+// seed_dev: an int64 [1] device tensor (utils/graph_rng.py) that keys the dropout with the step seed
+void attach_seed_dev(bh::AttnArgs& a, const at::Tensor& q, const c10::optional<at::Tensor>& seed_dev) {
+  if (!seed_dev.has_value() || !seed_dev->defined()) return;
+  TORCH_CHECK(seed_dev->scalar_type() == at::kLong && seed_dev->numel() == 1 && seed_dev->device() == q.device(),
+              "flash attention: seed_dev must be an int64 [1] tensor on q's device");
+  a.seed_dev = seed_dev->data_ptr<int64_t>();
+}
+
 std::vector<at::Tensor> flash_fwd(at::Tensor q, at::Tensor k, at::Tensor v, int mask_mode,
                                   c10::optional<at::Tensor> mask, int64_t heads, double scale, double p, bool training,
-                                  int64_t seed, double mask_fill, c10::optional<at::Tensor> bits) {
+                                  int64_t seed, double mask_fill, c10::optional<at::Tensor> bits,
+                                  c10::optional<at::Tensor> seed_dev) {
   at::Tensor mk;
   auto a = attn_args(q, k, v, mask_mode, mask, heads, scale, p, training, seed, mk, /*flash=*/true);
+  attach_seed_dev(a, q, seed_dev);
   a.mask_fill = (float)mask_fill;
   at::Tensor mb;
   attach_mask_bits(a, q, bits, mb);
@@ -432,9 +442,11 @@ std::vector<at::Tensor> flash_fwd(at::Tensor q, at::Tensor k, at::Tensor v, int 
 
 void flash_bwd(at::Tensor dout, at::Tensor q, at::Tensor k, at::Tensor v, at::Tensor o, at::Tensor lse, int mask_mode,
                c10::optional<at::Tensor> mask, int64_t heads, double scale, double p, bool training, int64_t seed,
-               double mask_fill, at::Tensor dq, at::Tensor dk, at::Tensor dv, c10::optional<at::Tensor> bits) {
+               double mask_fill, at::Tensor dq, at::Tensor dk, at::Tensor dv, c10::optional<at::Tensor> bits,
+               c10::optional<at::Tensor> seed_dev) {
   at::Tensor mk;
   auto a = attn_args(q, k, v, mask_mode, mask, heads, scale, p, training, seed, mk, /*flash=*/true);
+  attach_seed_dev(a, q, seed_dev);
   a.mask_fill = (float)mask_fill;
   at::Tensor mb;
   attach_mask_bits(a, q, bits, mb);
@@ -536,11 +548,13 @@ void register_contrib(pybind11::module_& root) {
   namespace py = pybind11;
   fa.def("flash_forward", &flash_fwd, "any-length attention forward -> (o, lse)", py::arg("q"), py::arg("k"),
          py::arg("v"), py::arg("mask_mode"), py::arg("mask"), py::arg("heads"), py::arg("scale"), py::arg("p"),
-         py::arg("training"), py::arg("seed"), py::arg("mask_fill"), py::arg("bits") = py::none());
+         py::arg("training"), py::arg("seed"), py::arg("mask_fill"), py::arg("bits") = py::none(),
+         py::arg("seed_dev") = py::none());
   fa.def("flash_backward", &flash_bwd, "any-length attention backward into dq / dk / dv", py::arg("dout"),
          py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("lse"), py::arg("mask_mode"),
          py::arg("mask"), py::arg("heads"), py::arg("scale"), py::arg("p"), py::arg("training"), py::arg("seed"),
-         py::arg("mask_fill"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("bits") = py::none());
+         py::arg("mask_fill"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("bits") = py::none(),
+         py::arg("seed_dev") = py::none());
   fa.def("flash_varlen_forward", &flash_varlen_fwd, "packed variable-length attention forward -> (o, lse)",
          py::arg("q"), py::arg("k"), py::arg("v"), py::arg("cu_seqlens"), py::arg("max_s"), py::arg("causal"),
          py::arg("scale"), py::arg("p"), py::arg("training"), py::arg("seed"));

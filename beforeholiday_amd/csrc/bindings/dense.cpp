@@ -58,7 +58,8 @@ at::Tensor bias_grad(const at::Tensor& dy) { return act_backward(dy, at::Tensor(
 // Megatron bias-dropout-add: out = residual + dropout(x + bias); returns (out, keep bits uint8 [numel/8]).
 // p == 0 (or eval) -> keep is an empty tensor and no dropout is applied.
 std::vector<at::Tensor> bias_dropout_add(const at::Tensor& x, const c10::optional<at::Tensor>& bias,
-                                         const at::Tensor& residual, double p, int64_t seed) {
+                                         const at::Tensor& residual, double p, int64_t seed,
+                                         const c10::optional<at::Tensor>& seed_dev) {
   check_cuda(x, "x");
   TORCH_CHECK(residual.sizes() == x.sizes() && residual.scalar_type() == x.scalar_type(),
               "bias_dropout_add: residual must match x in shape and dtype");
@@ -71,11 +72,17 @@ std::vector<at::Tensor> bias_dropout_add(const at::Tensor& x, const c10::optiona
     b = bias->contiguous();
     TORCH_CHECK(b.numel() == N && b.scalar_type() == x.scalar_type() && al16(b), "bias_dropout_add: bad bias");
   }
+  const int64_t* sd = nullptr;  // device step seed (utils/graph_rng.py)
+  if (seed_dev.has_value() && seed_dev->defined()) {
+    TORCH_CHECK(seed_dev->scalar_type() == at::kLong && seed_dev->numel() == 1 && seed_dev->device() == x.device(),
+                "bias_dropout_add: seed_dev must be an int64 [1] tensor on x's device");
+    sd = seed_dev->data_ptr<int64_t>();
+  }
   auto out = at::empty_like(xc);
   at::Tensor keep = at::empty({p > 0.0 ? xc.numel() / 8 : 0}, xc.options().dtype(at::kByte));
   bh::dense_bias_dropout_add(dtype_code(xc.scalar_type()), xc.data_ptr(), b.defined() ? b.data_ptr() : nullptr,
                              rc.data_ptr(), out.data_ptr(), p > 0.0 ? keep.data_ptr<uint8_t>() : nullptr, M, (int)N,
-                             (float)p, (uint32_t)seed, stream_for(xc));
+                             (float)p, (uint32_t)seed, stream_for(xc), sd);
   return {out, keep};
 }
 
@@ -508,7 +515,8 @@ void register_dense(pybind11::module_& root) {
     return bias_grad(dy.contiguous());
   }, py::arg("dy"), "column sum of dy[..., N] over all leading dims (fp32 accumulation, dy dtype out)");
   fd.def("bias_dropout_add", &bias_dropout_add, py::arg("x"), py::arg("bias"), py::arg("residual"), py::arg("p"),
-         py::arg("seed"), "out = residual + dropout(x + bias) in one pass; returns (out, keep bits)");
+         py::arg("seed"), py::arg("seed_dev") = py::none(),
+         "out = residual + dropout(x + bias) in one pass; returns (out, keep bits)");
   fd.def("dropout_backward", &dropout_backward, py::arg("dy"), py::arg("keep"), py::arg("p"), py::arg("want_bgrad"),
          "dx = dy * keep / (1 - p) with the bias gradient sum(dx) from the same pass; returns (dx, bgrad)");
   auto mlp = root.def_submodule("mlp_cuda", "N-layer MLP");

@@ -30,6 +30,9 @@ struct AttnArgs {
   float scale = 1.f, p_drop = 0.f;
   bool training = false;
   uint64_t seed = 0, offset = 0;
+  // device-resident step seed (utils/graph_rng.py: a captured step replays with a fresh one): the
+  // dropout then keys on seed ^ (*seed_dev * golden ratio), read once per row hash (scalar load)
+  const int64_t* seed_dev = nullptr;
   // backward
   const void* dout = nullptr;
   int64_t do_st = 0, do_sbh = 0;

@@ -21,7 +21,8 @@ void dense_act_backward(int dt, const void* dy, const void* aux, void* dx, void*
 // out[M,N] = residual + dropout(x + bias[N]) (bias may be null); keep: uint8 [M*N/8] keep bits (null: no
 // dropout, p ignored). N % 8 == 0, 16-byte aligned pointers. Bits are a seed-keyed hash of the element index.
 void dense_bias_dropout_add(int dt, const void* x, const void* bias, const void* residual, void* out, uint8_t* keep,
-                            int64_t M, int N, float p, uint32_t seed, hipStream_t st);
+                            int64_t M, int N, float p, uint32_t seed, hipStream_t st,
+                            const int64_t* seed_dev = nullptr);  // device step seed (utils/graph_rng.py)
 // dx = dy * keep * keep_scale (dx may be null), bgrad[N] = sum_m dx (null: skip); N % 8 == 0, aligned.
 void dense_dropout_backward(int dt, const void* dy, const uint8_t* keep, float keep_scale, void* dx, void* bgrad,
                             float* part, int splits, int64_t M, int N, hipStream_t st);

@@ -37,6 +37,11 @@
 namespace bh {
 namespace {
 
+// the dropout seed of a launch: the host seed, keyed by the device step seed when one is given
+BH_DEVICE uint64_t eff_seed(const AttnArgs& a) {
+  return a.seed_dev ? a.seed ^ ((uint64_t)*a.seed_dev * 0x9E3779B97F4A7C15ull) : a.seed;
+}
+
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef __bf16 b8v __attribute__((ext_vector_type(8)));
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -174,7 +179,7 @@ BH_DEVICE void softmax_rows(f4v (&S)[NT], const AttnArgs& a, int b, int qbase, i
 
 // keep flags of the 4 rows (4-row group starting at qrow4) for key col
 BH_DEVICE float4 keep4(const AttnArgs& a, int bh, int qrow4, int col, int skt) {
-  Philox ph(a.seed, ((uint64_t)bh * (uint64_t)a.sq + (uint64_t)qrow4) * (uint64_t)skt + (uint64_t)col, a.offset);
+  Philox ph(eff_seed(a), ((uint64_t)bh * (uint64_t)a.sq + (uint64_t)qrow4) * (uint64_t)skt + (uint64_t)col, a.offset);
   const float4 u = ph.uniform4();
   const float pk = 1.f - a.p_drop;
   return make_float4(u.x <= pk, u.y <= pk, u.z <= pk, u.w <= pk);
@@ -606,8 +611,8 @@ BH_DEVICE uint32_t mix32(uint32_t x) {
   return x;
 }
 BH_DEVICE uint32_t row_hash(const AttnArgs& a, int bh, int q) {
-  return mix32((uint32_t)a.seed ^ mix32((uint32_t)(a.seed >> 32) ^ ((uint32_t)bh * 0x9E3779B1u) ^
-                                        ((uint32_t)q * 0x85EBCA77u)));
+  const uint64_t s = eff_seed(a);
+  return mix32((uint32_t)s ^ mix32((uint32_t)(s >> 32) ^ ((uint32_t)bh * 0x9E3779B1u) ^ ((uint32_t)q * 0x85EBCA77u)));
 }
 // one 32-bit hash per (query, key pair): keys 2i and 2i+1 use its low / high 16 bits, so the
 // query-on-lane kernels (forward, dQ) hash once per two scores; thresh is (1 - p) * 65536. The row

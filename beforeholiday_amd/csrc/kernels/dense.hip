@@ -91,7 +91,10 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_bias_dropout_add(const T* __restrict__ x, const T* __restrict__ bias,
                                                           const T* __restrict__ res, T* __restrict__ out,
                                                           uint8_t* __restrict__ keep, int64_t total, int N,
-                                                          uint32_t thresh, float scale, uint32_t seed) {
+                                                          uint32_t thresh, float scale, uint32_t seed,
+                                                          const int64_t* __restrict__ seed_dev) {
+  // a device step seed (graph replay) keys the host seed; read once (scalar load)
+  if (seed_dev) seed ^= (uint32_t)(((uint64_t)*seed_dev * 0x9E3779B97F4A7C15ull) >> 32);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
   for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < total; i += stride) {
     float v[8], r[8];
@@ -309,7 +312,7 @@ void dense_act_backward(int dt, const void* dy, const void* aux, void* dx, void*
 }
 
 void dense_bias_dropout_add(int dt, const void* x, const void* bias, const void* residual, void* out, uint8_t* keep,
-                            int64_t M, int N, float p, uint32_t seed, hipStream_t st) {
+                            int64_t M, int N, float p, uint32_t seed, hipStream_t st, const int64_t* seed_dev) {
   const int64_t total = M * (int64_t)N;
   if (total == 0) return;
   if (N % 8 != 0) throw std::runtime_error("dense_bias_dropout_add: N % 8 != 0");
@@ -320,7 +323,7 @@ void dense_bias_dropout_add(int dt, const void* x, const void* bias, const void*
   const float scale = keep ? 1.f / (1.f - p) : 1.f;
   DN_DISPATCH(dt, T, hipLaunchKernelGGL((k_bias_dropout_add<T>), dim3((unsigned)blocks), dim3(256), 0, st,
                                         (const T*)x, (const T*)bias, (const T*)residual, (T*)out, keep, total, N,
-                                        thresh, scale, seed));
+                                        thresh, scale, seed, seed_dev));
   check_launch("dense_bias_dropout_add");
 }
 

@@ -207,9 +207,19 @@ class _BiasDropoutAddFn(torch.autograd.Function):
         # host-side seed stream (no device sync): "replicated" is identical on every TP rank,
         # "model-parallel" differs per TP rank (sequence-parallel shards); see random.dropout_seed
         from ..transformer.tensor_parallel.random import dropout_seed
+        from ..utils import graph_rng
 
-        seed = dropout_seed(model_parallel)
-        out, keep = _fd().bias_dropout_add(x, bias, residual, p, seed)
+        sd = None
+        if graph_rng.active():  # replayable: a per-call salt + the device step seed (utils/graph_rng.py)
+            stream = 0
+            if model_parallel:
+                from ..transformer import parallel_state
+
+                stream = 1 + parallel_state.get_tensor_model_parallel_rank()
+            seed, sd = graph_rng.next_salt(stream) & 0xFFFFFFFF, graph_rng.step_seed()
+        else:
+            seed = dropout_seed(model_parallel)
+        out, keep = _fd().bias_dropout_add(x, bias, residual, p, seed, sd)
         ctx.save_for_backward(keep)
         ctx.p = p
         ctx.has_bias = bias is not None

@@ -163,12 +163,17 @@ def capture_checked(fn: Callable[[], torch.Tensor], state, watch=(), warmup: int
     if not agree(ok):
         return fn, {"graph": "eager (capture failed on some rank)", "error": err}
     saved = [t.detach().clone() for t in state]
+    # torch's own dropout draws from the device generator, whose (seed, offset) the replay advances on the
+    # host: the eager step restarts from the same generator state as the replay
+    rng = torch.cuda.get_rng_state() if torch.cuda.is_available() else None
     torch.cuda.synchronize()
     loss_g = g().detach().clone()
     got = [loss_g] + [w.detach().clone() for w in watch]
     with torch.no_grad():
         for t, s in zip(state, saved):
             t.copy_(s)
+    if rng is not None:
+        torch.cuda.set_rng_state(rng)
     loss_e = fn().detach().clone()
     want = [loss_e] + [w.detach().clone() for w in watch]
     torch.cuda.synchronize()
@@ -181,6 +186,8 @@ def capture_checked(fn: Callable[[], torch.Tensor], state, watch=(), warmup: int
         with torch.no_grad():
             for t, s_ in zip(state, saved):
                 t.copy_(s_)
+        if rng is not None:
+            torch.cuda.set_rng_state(rng)
         fn()
         again = [w.detach().clone() for w in watch]
         rep["eager_repeatable"] = all(torch.equal(a, b) for a, b in zip(again, want[1:]))

@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--layers", type=int, default=24)
     ap.add_argument("--opt-level", default="O2", choices=["O2", "O5"])
     ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="replay the step as one HIP graph (utils/graphs.py capture_checked; dropout seeds from "
+                         "the device, utils/graph_rng.py); auto = one rank")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU")
     from beforeholiday_amd.utils import gemm_tuning
@@ -92,7 +95,14 @@ def main():
     loss_mask = (torch.rand(B, S, device="cuda", generator=g) < 0.15).float()
     nsp = torch.randint(0, 2, (B,), device="cuda", generator=g)
 
+    from beforeholiday_amd.utils import graph_rng
+
+    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
+    if use_graph:
+        graph_rng.enable(seed=rank)  # replayable dropout seeds: a per-call salt + a device step seed
+
     def step():
+        graph_rng.new_step()
         lm_loss, nsp_logits = model(tokens, mask, tokentype_ids=types, lm_labels=labels)
         loss = (lm_loss.float() * loss_mask).sum() / loss_mask.sum() + F.cross_entropy(nsp_logits.float(), nsp)
         with amp.scale_loss(loss, opt) as scaled:
@@ -103,6 +113,18 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    run = step
+    graph_report = {"graph": "eager"}
+    if use_graph:
+        from beforeholiday_amd.amp._amp_state import _amp_state
+        from beforeholiday_amd.utils import capture_checked, training_state
+
+        state = training_state(*_amp_state.loss_scalers, model=model, optimizer=opt) + graph_rng.state_tensors()
+        params = list(model.parameters())
+        run, graph_report = capture_checked(step, state, watch=params[:4] + params[-2:], model=model)
+        if rank == 0:
+            print(f"[bench_bert] {graph_report}", file=sys.stderr, flush=True)
+        run()
     if os.environ.get("BH_HOST_PROFILE") == "1":  # CPU-side op profile: a blocking op has a long self time
         from torch.profiler import ProfilerActivity, profile
         torch.cuda.synchronize()
@@ -151,7 +173,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step()
+        loss = run()
     torch.cuda.synchronize()
     dist.barrier()
     el = torch.tensor([time.perf_counter() - t0], device="cuda", dtype=torch.float64)
@@ -167,7 +189,8 @@ def main():
             "config": {"model": f"BERT-large ({args.layers} layers, {nparams / 1e6:.0f}M params) + FusedLayerNorm + "
                        "FusedLAMB", "global_batch": B * world, "seq_len": S, "parallelism": f"dp{world}",
                        "final_loss": round(float(loss), 4)},
-            "gemm_table": gemm_tuning.status()}), flush=True)
+            "gemm_table": gemm_tuning.status(), "hip_graph": run is not step,
+            "graph_check": graph_report.get("graph")}), flush=True)
     gemm_tuning.finish(args.gemm_table, rank)
     dist.destroy_process_group()
 

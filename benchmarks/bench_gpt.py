@@ -41,6 +41,10 @@ def main():
     ap.add_argument("--sp", action="store_true", help="sequence parallelism inside the TP group")
     ap.add_argument("--opt-level", default="O5", choices=["O2", "O5"])
     ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="replay the step as one HIP graph (utils/graphs.py capture_checked; dropout seeds from "
+                         "the device, utils/graph_rng.py); auto = one rank at O5 (static loss scale: FusedAdam "
+                         "keeps lr / step on the device, capturable=True)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI; gloo only to rehearse multi-rank TP/SP on one GPU")
     from beforeholiday_amd.utils import gemm_tuning
@@ -99,7 +103,12 @@ def main():
                             bias_gelu_fusion=True, sequence_parallel=args.sp and tp > 1)
     model = GPTModel(cfg, parallel_output=True).cuda()
     nparams_local = sum(p.numel() for p in model.parameters())
-    opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=0.01)
+    from beforeholiday_amd.utils import graph_rng
+
+    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1 and args.opt_level == "O5")
+    if use_graph:
+        graph_rng.enable(seed=rank)  # replayable dropout seeds: a per-call salt + a device step seed
+    opt = FusedAdam(model.parameters(), lr=1e-4, weight_decay=0.01, capturable=use_graph)
     model, opt = amp.initialize(model, opt, opt_level=args.opt_level, verbosity=0)
     if dp > 1:
         model = DistributedDataParallel(model, process_group=parallel_state.get_data_parallel_group())
@@ -112,6 +121,7 @@ def main():
     mask, _, pos = get_ltor_masks_and_position_ids(tokens, -1, False, False, False)
 
     def step():
+        graph_rng.new_step()
         loss = model(tokens, pos, mask, labels=labels).float().mean()
         with amp.scale_loss(loss, opt) as scaled:
             scaled.backward()
@@ -123,11 +133,23 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    run = step
+    graph_report = {"graph": "eager"}
+    if use_graph:
+        from beforeholiday_amd.amp._amp_state import _amp_state
+        from beforeholiday_amd.utils import capture_checked, training_state
+
+        state = training_state(*_amp_state.loss_scalers, model=model, optimizer=opt) + graph_rng.state_tensors()
+        params = list(model.parameters())
+        run, graph_report = capture_checked(step, state, watch=params[:4] + params[-2:], model=model)
+        if rank == 0:
+            print(f"[bench_gpt] {graph_report}", file=sys.stderr, flush=True)
+        run()
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = step()
+        loss = run()
     torch.cuda.synchronize()
     dist.barrier()
     el = torch.tensor([time.perf_counter() - t0], device="cuda", dtype=torch.float64)
@@ -148,7 +170,8 @@ def main():
                        "+ FusedAdam", "global_batch": B * dp, "seq_len": S,
                        "parallelism": f"tp{tp}{'-sp' if cfg.sequence_parallel else ''}-dp{dp}",
                        "final_loss": round(float(loss.detach()), 4)},
-            "gemm_table": gemm_tuning.status()}), flush=True)
+            "gemm_table": gemm_tuning.status(), "hip_graph": run is not step,
+            "graph_check": graph_report.get("graph")}), flush=True)
     gemm_tuning.finish(args.gemm_table, rank)
     dist.destroy_process_group()
 
