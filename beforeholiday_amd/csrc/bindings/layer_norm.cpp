@@ -2,6 +2,7 @@
 // Kernels: kernels/layer_norm.hip.
 #include "common.h"
 
+#include "bh/knobs.h"
 #include "bh/ln_api.h"
 
 namespace bhb {
@@ -82,7 +83,8 @@ std::vector<at::Tensor> bwd_impl(at::Tensor dout, at::Tensor mean, at::Tensor in
   TORCH_CHECK(rms || memory_efficient || mean.numel() == d.n1, "layer_norm backward: mean has ", mean.numel(),
               " elements, expected ", d.n1);
   TORCH_CHECK(invvar.numel() == d.n1, "layer_norm backward: invvar has ", invvar.numel(), " elements, expected ", d.n1);
-  const int fblocks = gamma.defined() ? bh::ln_bwd_fused_blocks(d.n1, d.n2) : 0;
+  // Config.ln_bwd_fused: dx and the parameter-gradient partials in one pass (else two)
+  const int fblocks = gamma.defined() && bh::knob("ln_bwd_fused", 1) ? bh::ln_bwd_fused_blocks(d.n1, d.n2) : 0;
   if (fblocks > 0) {  // one pass for dx and the parameter gradients
     at::Tensor gg = at::empty_like(gamma), gb;
     if (!rms && beta.defined()) gb = at::empty_like(beta);

@@ -244,30 +244,47 @@ __global__ __launch_bounds__(kBlock) void k_ln_bwd_fused(const Tdy* __restrict__
     if (from_output && b && !RMS) load8(b, col, n2, vec, bv[j]);
   }
   const float inv_n = 1.f / (float)n2;
-  for (int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + wave; row < n1; row += (int64_t)gridDim.x * kRowsPerBlock) {
-    const float mean = (RMS || from_output) ? 0.f : mean_in[row];
-    const float invvar = invvar_in[row];
+  // software-pipelined over the wave's rows: the next row's dy, x, residual gradient and statistics are
+  // requested (clamped row: unconditional loads) before this row's math, so each wave keeps two rows of
+  // loads in flight instead of two dependent round trips per row (one wave per SIMD: latency bound)
+  const int64_t stride = (int64_t)gridDim.x * kRowsPerBlock;
+  float dvA[VPT][8], xvA[VPT][8], rvA[VPT][8], meanA = 0.f, invA = 0.f;
+  auto load_row = [&](int64_t r, float (&dv)[VPT][8], float (&xv)[VPT][8], float (&rv)[VPT][8], float& mean,
+                      float& invvar) __attribute__((always_inline)) {
+    mean = (RMS || from_output) ? 0.f : mean_in[r];
+    invvar = invvar_in[r];
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int col = (j * kWave + lane) * 8;
+      load8(dy + r * n2, col, n2, vec, dv[j]);
+      load8(xin + r * n2, col, n2, vec, xv[j]);
+      if (dres) load8(dres + r * n2, col, n2, vec, rv[j]);
+    }
+  };
+  int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + wave;
+  if (row < n1) load_row(row, dvA, xvA, rvA, meanA, invA);
+  for (; row < n1; row += stride) {
+    float dvB[VPT][8], xvB[VPT][8], rvB[VPT][8], meanB, invB;
+    load_row(min(row + stride, n1 - 1), dvB, xvB, rvB, meanB, invB);
+    const float mean = meanA, invvar = invA;
     float xh[VPT][8], dg[VPT][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < VPT; ++j) {
       const int col = (j * kWave + lane) * 8;
-      float dv[8], xv[8];
-      load8(dy + row * n2, col, n2, vec, dv);
-      load8(xin + row * n2, col, n2, vec, xv);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float gg = gv[j][k];
         float h;
         if (from_output) {
-          const float yv = (b && !RMS) ? xv[k] - bv[j][k] : xv[k];
+          const float yv = (b && !RMS) ? xvA[j][k] - bv[j][k] : xvA[j][k];
           h = (gg != 0.f) ? yv / gg : 0.f;
         } else {
-          h = (xv[k] - mean) * invvar;
+          h = (xvA[j][k] - mean) * invvar;
         }
         const bool ok = col + k < n2;
         xh[j][k] = ok ? h : 0.f;
-        const float d = ok ? dv[k] : 0.f;
+        const float d = ok ? dvA[j][k] : 0.f;
         dg[j][k] = d * gg;
         ag[j][k] = fmaf(d, xh[j][k], ag[j][k]);
         ab[j][k] += d;
@@ -283,15 +300,19 @@ __global__ __launch_bounds__(kBlock) void k_ln_bwd_fused(const Tdy* __restrict__
       if (col >= n2) break;
       float o[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = invvar * (dg[j][k] - m1 - xh[j][k] * m2);
-      if (dres) {
-        float rv[8];
-        load8(dres + row * n2, col, n2, vec, rv);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] += rv[k];
-      }
+      for (int k = 0; k < 8; ++k) o[k] = invvar * (dg[j][k] - m1 - xh[j][k] * m2) + (dres ? rvA[j][k] : 0.f);
       store8(dx + row * n2, col, n2, vec, o);
     }
+#pragma unroll
+    for (int j = 0; j < VPT; ++j)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        dvA[j][k] = dvB[j][k];
+        xvA[j][k] = xvB[j][k];
+        rvA[j][k] = rvB[j][k];
+      }
+    meanA = meanB;
+    invA = invB;
   }
   // the block's four waves -> one partial row (fixed order: deterministic)
   float* mine = red + (size_t)wave * 2 * kCols;
@@ -473,6 +494,14 @@ int vpt_for(int n2, int max_vpt) {
     case 16: { constexpr int V = 16; __VA_ARGS__; } break; \
     default: break;                                    \
   }
+// the fused backward keeps ~10 register rows: rows of <= 2048 columns (vpt <= 4, ln_bwd_fused_blocks)
+#define LN_VPT4_DISPATCH(vpt, V, ...)                 \
+  switch (vpt) {                                       \
+    case 1: { constexpr int V = 1; __VA_ARGS__; } break; \
+    case 2: { constexpr int V = 2; __VA_ARGS__; } break; \
+    case 4: { constexpr int V = 4; __VA_ARGS__; } break; \
+    default: break;                                    \
+  }
 
 }  // namespace
 
@@ -545,7 +574,7 @@ void ln_backward_fused(int64_t n1, int n2, int dt_dy, const void* dy, int dt_x, 
   float* pb = partials + (int64_t)blocks * n2;
   const size_t shm = sizeof(float) * kRowsPerBlock * 2 * vpt * kWave * 8;
   LN_DISPATCH(dt_x, T, LN_DISPATCH(dt_w, Tw, LN_DISPATCH(dt_dy, Tdy,
-      LN_VPT_DISPATCH(vpt, V,
+      LN_VPT4_DISPATCH(vpt, V,
           if (rms) hipLaunchKernelGGL((k_ln_bwd_fused<T, Tw, Tdy, V, true>), dim3(blocks), dim3(kBlock), shm, st,
                                       (const Tdy*)dy, (const T*)xin, mean, invvar, (const Tw*)gamma, (const Tw*)beta,
                                       (T*)dx, n1, n2, from_output, vec, (const T*)dresid, pg, pb);

@@ -1,5 +1,6 @@
 """FusedLayerNorm backward at the transformer shape (8192 tokens x 1024, fp16): us per backward
-(data gradient + gamma / beta gradients), for sweeping BH_LN_WGRAD_ROWS / BH_LN_WGRAD_WGS."""
+(data gradient + gamma / beta gradients), for sweeping BH_LN_WGRAD_ROWS / BH_LN_WGRAD_WGS; the one-pass
+fused backward (Config.ln_bwd_fused) and the two-pass one, interleaved in one process."""
 import json
 import os
 import sys
@@ -10,9 +11,18 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+    from beforeholiday_amd import config
+
+    for rep in range(2):
+        for fused in (True, False):
+            with config.override(ln_bwd_fused=fused):
+                run({"rep": rep, "ln_bwd_fused": fused})
+
+
+def run(out):
     from beforeholiday_amd.normalization import FusedLayerNorm
 
-    out = {"rows": os.environ.get("BH_LN_WGRAD_ROWS", "8"), "wgs": os.environ.get("BH_LN_WGRAD_WGS", "512")}
+    out.update({"rows": os.environ.get("BH_LN_WGRAD_ROWS", "8"), "wgs": os.environ.get("BH_LN_WGRAD_WGS", "512")})
     for dtype in (torch.float16, torch.bfloat16):
         ln = FusedLayerNorm(1024).cuda().to(dtype)
         x = torch.randn(8192, 1024, device="cuda", dtype=dtype, requires_grad=True)
