@@ -131,13 +131,28 @@ def dropout_seed(model_parallel: bool = False) -> int:
     return int(torch.randint(0, 2 ** 31 - 1, (1,), generator=g).item())
 
 
+_GRAPH_RNG_CALLS = "graph_rng.calls"
+
+
 def get_dropout_seed_states():
-    return {k: g.get_state() for k, g in _DROPOUT_SEED_GENS.items()}
+    """The fused-dropout seed streams, and (device step seeds, utils/graph_rng.py) the per-step call
+    counter that picks the next salt, so a checkpoint recompute redraws the forward's masks."""
+    from ...utils import graph_rng
+
+    states = {k: g.get_state() for k, g in _DROPOUT_SEED_GENS.items()}
+    if graph_rng.active():
+        states[_GRAPH_RNG_CALLS] = graph_rng._calls
+    return states
 
 
 def set_dropout_seed_states(states):
+    from ...utils import graph_rng
+
     for k, st in states.items():
-        _DROPOUT_SEED_GENS.setdefault(k, torch.Generator()).set_state(st)
+        if k == _GRAPH_RNG_CALLS:
+            graph_rng._calls = st
+        else:
+            _DROPOUT_SEED_GENS.setdefault(k, torch.Generator()).set_state(st)
 
 
 def get_cuda_rng_tracker():

@@ -102,3 +102,28 @@ def test_captured_step_replays_eager_bits_and_advances():
         assert int(seed) == int(s0) + 2
     finally:
         graph_rng.disable()
+
+
+def test_checkpoint_recompute_reuses_salts():
+    """An activation-checkpoint recompute (tensor_parallel.random.CheckpointFunction) replays the per-step
+    call counter, so the recomputed dropout calls get the forward's salts (same masks)."""
+    from beforeholiday_amd.transformer.tensor_parallel.random import checkpoint
+    from beforeholiday_amd.utils import graph_rng
+
+    seen = []
+
+    def f(x):
+        seen.append(graph_rng.next_salt())
+        return x * 2
+
+    graph_rng._step_seed, graph_rng._calls = torch.zeros(1, dtype=torch.int64), 0  # CPU stand-in
+    try:
+        x = torch.randn(4, requires_grad=True)
+        y = checkpoint(f, False, x)
+        after = graph_rng._calls
+        y.sum().backward()
+        assert len(seen) == 2 and seen[0] == seen[1]
+        assert graph_rng._calls == after  # the backward's own counter is restored after the recompute
+        assert torch.equal(x.grad, torch.full((4,), 2.0))
+    finally:
+        graph_rng.disable()
