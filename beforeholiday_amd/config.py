@@ -100,8 +100,9 @@ class Config:
     conv3x3_sw: bool = field(default=False, metadata=dict(env="BH_CONV3X3_SW", native="conv3x3_sw", doc=(
         "direct 3x3 conv, plain epilogue: operands swapped so it stores 8-byte channel runs (measured "
         "slower, profiles/conv3x3_nb_sw_ab_r6.txt)")))
-    ln_bwd_fused: bool = field(default=True, metadata=dict(env="BH_LN_BWD_FUSED", native="ln_bwd_fused", doc=(
-        "LayerNorm backward: dx and the gamma / beta partials in one row-pipelined pass (else two passes)")))
+    ln_bwd_fused: bool = field(default=False, metadata=dict(env="BH_LN_BWD_FUSED", native="ln_bwd_fused", doc=(
+        "LayerNorm backward: dx and the gamma / beta partials in one row-pipelined pass (else two passes; "
+        "the two-pass backward measured 0.6 % faster per BERT-large step, profiles/ln_bwd_fused_ab_r6.txt)")))
     igemm_lds: bool = field(default=False, metadata=dict(env="BH_IGEMM_LDS", native="igemm_lds", doc=(
         "stride-2 3x3 implicit GEMM: both operands staged in LDS by LDS-DMA (measured slower than the "
         "register-staged A fragments, profiles/igemm_lds_ab_r6.txt)")))

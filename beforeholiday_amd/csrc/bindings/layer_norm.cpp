@@ -83,8 +83,9 @@ std::vector<at::Tensor> bwd_impl(at::Tensor dout, at::Tensor mean, at::Tensor in
   TORCH_CHECK(rms || memory_efficient || mean.numel() == d.n1, "layer_norm backward: mean has ", mean.numel(),
               " elements, expected ", d.n1);
   TORCH_CHECK(invvar.numel() == d.n1, "layer_norm backward: invvar has ", invvar.numel(), " elements, expected ", d.n1);
-  // Config.ln_bwd_fused: dx and the parameter-gradient partials in one pass (else two)
-  const int fblocks = gamma.defined() && bh::knob("ln_bwd_fused", 1) ? bh::ln_bwd_fused_blocks(d.n1, d.n2) : 0;
+  // Config.ln_bwd_fused: dx and the parameter-gradient partials in one pass (else two; measured faster in
+  // BERT-large, profiles/ln_bwd_fused_ab_r6.txt)
+  const int fblocks = gamma.defined() && bh::knob("ln_bwd_fused", 0) ? bh::ln_bwd_fused_blocks(d.n1, d.n2) : 0;
   if (fblocks > 0) {  // one pass for dx and the parameter gradients
     at::Tensor gg = at::empty_like(gamma), gb;
     if (!rms && beta.defined()) gb = at::empty_like(beta);

@@ -24,7 +24,7 @@ def test_from_env_parses_and_validates():
     with pytest.raises(TypeError):
         config.Config(gemm_tile=True)
     assert config.Config().native_knobs() == {"dense_wgrad": 1, "dense_mfma": 1, "dense_tune": 0, "gemm_tile": 0,
-                                             "conv3x3_nb": 2, "conv3x3_sw": 0, "ln_bwd_fused": 1, "igemm_lds": 0, "gemm_log": 0}
+                                             "conv3x3_nb": 2, "conv3x3_sw": 0, "ln_bwd_fused": 0, "igemm_lds": 0, "gemm_log": 0}
 
 
 def test_set_override_and_module_globals():
