@@ -132,34 +132,42 @@ __global__ __launch_bounds__(kThreads, 2) void k_igemm(IgemmArgs a, int tiles_m)
       ss[kMaxProC + c] = a.pro_shift[c];
     }
   }
-  // this lane's A pixel of each 32-row sub-strip
-  int pn[MT], pi[MT], pj[MT];
-  bool pv[MT];
+  // this lane's A pixel of each 32-row sub-strip: byte offset of its tap-grid origin (lane half included)
+  // and that origin's (row, column) packed 16:16 (a pixel past the grid: a row no tap brings inside)
+  int pbase[MT], pyx[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
     const int64_t p = (int64_t)mt * (kWaves * MW) + wave * MW + 32 * m + r;
-    pv[m] = p < P;
-    const int pp = pv[m] ? (int)p : 0;
-    pn[m] = pp / HWg;
-    const int rem = pp - pn[m] * HWg;
-    pi[m] = rem / a.Wg;
-    pj[m] = rem - pi[m] * a.Wg;
+    const int pp = p < P ? (int)p : 0;
+    const int pn = pp / HWg, rem = pp - pn * HWg, pi = rem / a.Wg, pj = rem - pi * a.Wg;
+    pbase[m] = ((pn * Ha + pi * a.sa) * Wa + pj * a.sa) * Ca * 2 + 16 * h;
+    pyx[m] = p < P ? ((pi * a.sa) << 16) | (pj * a.sa) : 0x40004000;
   }
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(a.a), 0, (int)((int64_t)a.N * Ha * Wa * Ca * 2), 0x00020000);
-  const T* __restrict__ Bw = reinterpret_cast<const T*>(a.b);
+  // weights through a buffer resource too: the per-thread part of each piece's offset is fixed for the
+  // kernel, the (tap, chunk) part rides in soffset (no 64-bit address math per k-step)
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(a.b), 0, (int)((int64_t)a.Nout * a.taps_total * Ca * 2), 0x00020000);
+  int bvoff[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int q = tid + i * kThreads, row = q >> 3, ch = q & 7;
+    bvoff[i] = ((o0 + row) * a.taps_total * Ca + ch * 8) * 2;
+  }
   const int nch = Ca / kCK, steps = ph.ntaps * nch;
 
   // A fragments of k-step s: ar[m][ks] = channels 16 ks + 8 h .. + 7 of the tap's input pixel
   auto a_load = [&](int s, i4v(&ar)[MT][4], uint32_t& msk) __attribute__((always_inline)) {
     const int t = s / nch, c = s - t * nch;
     const int oy = ph.oy[t], ox = ph.ox[t];
+    const int del = ((oy * Wa + ox) * Ca + c * kCK) * 2;  // (uniform)
     msk = 0;
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      const int yi = pi[m] * a.sa + oy, xi = pj[m] * a.sa + ox;
-      const bool ok = pv[m] && yi >= 0 && yi < Ha && xi >= 0 && xi < Wa;
-      const int off = ok ? (((pn[m] * Ha + yi) * Wa + xi) * Ca + c * kCK + 8 * h) * 2 : kOutOfRange;
+      const int yi = (pyx[m] >> 16) + oy, xi = (pyx[m] & 0xffff) + ox;
+      const bool ok = yi >= 0 && yi < Ha && xi >= 0 && xi < Wa;
+      const int off = ok ? pbase[m] + del : kOutOfRange;
       msk |= (ok ? 1u : 0u) << m;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) ar[m][ks] = __builtin_amdgcn_raw_buffer_load_b128(rsA, off + 32 * ks, 0, 0);
@@ -168,12 +176,9 @@ __global__ __launch_bounds__(kThreads, 2) void k_igemm(IgemmArgs a, int tiles_m)
   // weight slice of k-step s: rows o0 .. o0 + NC - 1, channels c * 64 .. + 63 of tap tap[t]
   auto b_load = [&](int s, i4v(&br)[NB]) __attribute__((always_inline)) {
     const int t = s / nch, c = s - t * nch;
-    const int tap = ph.tap[t];
+    const int so = (ph.tap[t] * Ca + c * kCK) * 2;
 #pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int q = tid + i * kThreads, row = q >> 3, ch = q & 7;
-      br[i] = *reinterpret_cast<const i4v*>(Bw + ((int64_t)(o0 + row) * a.taps_total + tap) * Ca + c * kCK + ch * 8);
-    }
+    for (int i = 0; i < NB; ++i) br[i] = __builtin_amdgcn_raw_buffer_load_b128(rsB, bvoff[i], so, 0);
   };
   auto b_store = [&](char* buf, const i4v(&br)[NB]) __attribute__((always_inline)) {
 #pragma unroll
@@ -478,6 +483,7 @@ bool igemm_supported(const IgemmArgs& a) {
   }
   // 32-bit buffer offsets for a (the out-of-range sentinel sits past it), 32-bit pixel indices
   if ((int64_t)a.N * a.Ha * a.Wa * a.Ca * 2 + 128 >= kOutOfRange) return false;
+  if ((int64_t)a.Nout * a.taps_total * a.Ca * 2 >= kOutOfRange) return false;  // 32-bit weight offsets
   if ((int64_t)a.N * a.Hg * a.Wg >= (1ll << 31)) return false;
   if (a.pro_scale && (!a.pro_shift || a.Ca > kMaxProC)) return false;
   if (a.part && a.nphase != 1) return false;
