@@ -26,6 +26,17 @@ from typing import Any, Callable, Optional
 import torch
 
 
+def _amp_c():
+    """The native multi-tensor module, or None (no extension: the CPU reference paths)."""
+    try:
+        from .._native import submodule
+
+        m = submodule("amp_C")
+    except Exception:  # noqa: BLE001 - extension not built / not importable
+        return None
+    return m if hasattr(m, "defer_capture_uploads") else None
+
+
 class GraphedStep:
     """``step = GraphedStep(fn); out = step()`` -- ``fn()`` runs ``warmup`` times eagerly on a side
     stream (so lazy initialisation, bucket building and plan caches reach steady state), then once
@@ -59,8 +70,18 @@ class GraphedStep:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self.pool, stream=side):
-            self.out = self.fn()
+        # multi-tensor chunk plans made under capture are uploaded once after it, not by kernel-argument
+        # launches inside the graph (bindings/mta.cpp defer_capture_uploads)
+        amp_c = _amp_c()
+        if amp_c is not None:
+            amp_c.defer_capture_uploads(True)
+        try:
+            with torch.cuda.graph(g, pool=self.pool, stream=side):
+                self.out = self.fn()
+        finally:
+            if amp_c is not None:
+                amp_c.defer_capture_uploads(False)
+                amp_c.flush_capture_uploads()
         torch.cuda.synchronize()
         self.capture_ms = (time.perf_counter() - t0) * 1e3
         self.graph = g
@@ -80,7 +101,8 @@ class GraphedStep:
 
 def training_state(*roots, model=None, optimizer=None):
     """Every device tensor a training step mutates, for :func:`capture_checked`'s save / restore:
-    the model's parameters and buffers, the optimizer's parameters (amp's fp32 masters) and state,
+    the model's parameters and buffers, the optimizer's parameters (amp's fp32 masters), their group's
+    device hyper-parameters and state,
     and the tensor attributes (one level deep) of the optimizer, its amp stash and every extra root
     (loss scalers: device scale / counters / flags; device step counters). Deduplicated by storage
     pointer + shape."""
@@ -100,6 +122,9 @@ def training_state(*roots, model=None, optimizer=None):
         for g in optimizer.param_groups:
             for p in g["params"]:
                 add(p)
+            for k, v in g.items():  # device hyper-parameters (capturable FusedAdam: lr and step tensors)
+                if k != "params":
+                    add(v)
         for st in optimizer.state.values():
             for v in (st.values() if isinstance(st, dict) else ()):
                 add(v)

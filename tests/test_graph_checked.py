@@ -186,3 +186,55 @@ def test_capture_checked_rejects_mismatch_cpu(monkeypatch):
     monkeypatch.setattr(graphs, "GraphedStep", Good)
     run, rep = graphs.capture_checked(step, [w], watch=[w])
     assert isinstance(run, Good) and rep["graph"].startswith("captured"), rep
+
+
+@pytest.mark.gpu
+def test_training_state_includes_group_device_hyperparameters():
+    """Capturable FusedAdam keeps lr and step as device tensors in its param groups: capture_checked must save
+    and restore them too (missing them made the GPT-2 replay-vs-eager check fail for the wrong reason)."""
+    from beforeholiday_amd.optimizers import FusedAdam
+    from beforeholiday_amd.utils import training_state
+
+    p = torch.nn.Parameter(torch.randn(64, device="cuda"))
+    opt = FusedAdam([p], lr=1e-3, capturable=True)
+    state = training_state(optimizer=opt)
+    ptrs = {t.data_ptr() for t in state}
+    g = opt.param_groups[0]
+    assert g["step"].data_ptr() in ptrs and g["lr"].data_ptr() in ptrs
+
+
+@pytest.mark.gpu
+def test_capture_defers_multi_tensor_plan_uploads():
+    """A chunk plan made under capture (new tensors from the graph pool) is uploaded once after the capture
+    (bindings/mta.cpp defer_capture_uploads / flush_capture_uploads) instead of by launches inside the graph,
+    and the replay computes the right values from it."""
+    from beforeholiday_amd._native import submodule
+
+    amp_C = submodule("amp_C")
+    xs = [torch.randn(1000 + 37 * i, device="cuda") for i in range(5)]
+    ys = [torch.empty_like(x) for x in xs]
+    flag = torch.zeros(1, dtype=torch.int, device="cuda")
+
+    def fn():
+        zs = [x * 1.0 for x in xs]  # fresh graph-pool tensors: a plan the cache has not seen
+        amp_C.multi_tensor_scale(65536, flag, [zs, ys], 0.5)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()  # warm-up (eager plan)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    amp_C.defer_capture_uploads(True)
+    try:
+        with torch.cuda.graph(g, stream=s):
+            fn()
+    finally:
+        amp_C.defer_capture_uploads(False)
+    assert amp_C.flush_capture_uploads() >= 1
+    for y in ys:
+        y.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    for x, y in zip(xs, ys):
+        assert torch.equal(y, x * 0.5)
