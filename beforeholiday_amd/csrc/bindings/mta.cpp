@@ -27,12 +27,6 @@ std::mutex g_plan_mu;
 // were torn down (an exit-time segfault). clear_plan_cache() releases them while torch is alive.
 auto& g_plans = *new std::unordered_map<std::vector<int64_t>, MTAPlan, KeyHash>();
 constexpr size_t kMaxPlans = 4096;
-// Deferred plan uploads (utils/graphs.py GraphedStep): while set, a plan created under capture is NOT
-// uploaded by kernel-argument launches recorded into the graph (they would re-upload the same bytes on
-// every replay: 65 launches per BERT-large step); its (device, host) pair waits here and
-// flush_capture_uploads() copies them once, after the capture and before the first replay.
-bool g_defer_uploads = false;
-auto& g_pending = *new std::vector<std::pair<at::Tensor, at::Tensor>>();
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -138,8 +132,7 @@ const MTAPlan& get_plan(const std::vector<std::vector<at::Tensor>>& lists, int64
     }
 
   at::Tensor devbuf = at::empty({(int64_t)bytes}, lists[0][0].options().dtype(at::kByte));
-  if (in_capture && g_defer_uploads) g_pending.emplace_back(devbuf, host);
-  else if (in_capture) bh::upload_bytes(devbuf.data_ptr(), host.data_ptr(), bytes, stream);
+  if (in_capture) bh::upload_bytes(devbuf.data_ptr(), host.data_ptr(), bytes, stream);
   else devbuf.copy_(host, /*non_blocking=*/true);
 
   MTAPlan plan;
@@ -722,17 +715,6 @@ void register_amp_C(pybind11::module_& root) {
     std::lock_guard<std::mutex> lock(g_plan_mu);
     g_plans.clear();
   }, "drop the cached device-resident chunk plans (registered with atexit by the python package)");
-  m.def("defer_capture_uploads", [](bool on) {
-    std::lock_guard<std::mutex> lock(g_plan_mu);
-    g_defer_uploads = on;
-  }, "while on, plans created under stream capture wait for flush_capture_uploads() (see mta.cpp)");
-  m.def("flush_capture_uploads", [] {
-    std::lock_guard<std::mutex> lock(g_plan_mu);
-    for (auto& pr : g_pending) pr.first.copy_(pr.second);  // (outside any capture: a plain H2D copy)
-    const int64_t n = (int64_t)g_pending.size();
-    g_pending.clear();
-    return n;
-  }, "upload the plans deferred during a capture; returns how many");
   m.def("multi_tensor_scale", &multi_tensor_scale, "out = in * scale with overflow flag");
   m.def("update_scale_device", [](at::Tensor scale, at::Tensor unskipped, at::Tensor overflow,
                                   c10::optional<at::Tensor> step_flag, double factor, int64_t window, double min_scale,

@@ -26,17 +26,6 @@ from typing import Any, Callable, Optional
 import torch
 
 
-def _amp_c():
-    """The native multi-tensor module, or None (no extension: the CPU reference paths)."""
-    try:
-        from .._native import submodule
-
-        m = submodule("amp_C")
-    except Exception:  # noqa: BLE001 - extension not built / not importable
-        return None
-    return m if hasattr(m, "defer_capture_uploads") else None
-
-
 class GraphedStep:
     """``step = GraphedStep(fn); out = step()`` -- ``fn()`` runs ``warmup`` times eagerly on a side
     stream (so lazy initialisation, bucket building and plan caches reach steady state), then once
@@ -70,18 +59,8 @@ class GraphedStep:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         g = torch.cuda.CUDAGraph()
-        # multi-tensor chunk plans made under capture are uploaded once after it, not by kernel-argument
-        # launches inside the graph (bindings/mta.cpp defer_capture_uploads)
-        amp_c = _amp_c()
-        if amp_c is not None:
-            amp_c.defer_capture_uploads(True)
-        try:
-            with torch.cuda.graph(g, pool=self.pool, stream=side):
-                self.out = self.fn()
-        finally:
-            if amp_c is not None:
-                amp_c.defer_capture_uploads(False)
-                amp_c.flush_capture_uploads()
+        with torch.cuda.graph(g, pool=self.pool, stream=side):
+            self.out = self.fn()
         torch.cuda.synchronize()
         self.capture_ms = (time.perf_counter() - t0) * 1e3
         self.graph = g

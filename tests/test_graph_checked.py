@@ -202,39 +202,3 @@ def test_training_state_includes_group_device_hyperparameters():
     g = opt.param_groups[0]
     assert g["step"].data_ptr() in ptrs and g["lr"].data_ptr() in ptrs
 
-
-@pytest.mark.gpu
-def test_capture_defers_multi_tensor_plan_uploads():
-    """A chunk plan made under capture (new tensors from the graph pool) is uploaded once after the capture
-    (bindings/mta.cpp defer_capture_uploads / flush_capture_uploads) instead of by launches inside the graph,
-    and the replay computes the right values from it."""
-    from beforeholiday_amd._native import submodule
-
-    amp_C = submodule("amp_C")
-    xs = [torch.randn(1000 + 37 * i, device="cuda") for i in range(5)]
-    ys = [torch.empty_like(x) for x in xs]
-    flag = torch.zeros(1, dtype=torch.int, device="cuda")
-
-    def fn():
-        zs = [x * 1.0 for x in xs]  # fresh graph-pool tensors: a plan the cache has not seen
-        amp_C.multi_tensor_scale(65536, flag, [zs, ys], 0.5)
-
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        fn()  # warm-up (eager plan)
-    torch.cuda.current_stream().wait_stream(s)
-    g = torch.cuda.CUDAGraph()
-    amp_C.defer_capture_uploads(True)
-    try:
-        with torch.cuda.graph(g, stream=s):
-            fn()
-    finally:
-        amp_C.defer_capture_uploads(False)
-    assert amp_C.flush_capture_uploads() >= 1
-    for y in ys:
-        y.zero_()
-    g.replay()
-    torch.cuda.synchronize()
-    for x, y in zip(xs, ys):
-        assert torch.equal(y, x * 0.5)
