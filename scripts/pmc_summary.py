@@ -15,7 +15,13 @@ def main():
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 name = r.get("Kernel_Name", "?")
-                if "k_gemm_pp" in name:
+                if "k_gemm_tn" in name:
+                    # template <T, PART, AK>: PART = split-K partials, AK = the NN (A row-major) layout
+                    part = "Lb1E" in name.split("k_gemm_tn")[1][:12]
+                    name = "gemm_tn<" + ("split" if part else "unsplit") + ">"
+                elif "k_tn_reduce" in name:
+                    name = "tn_reduce"
+                elif "k_gemm_pp" in name:
                     name = "gemm_pp<256x256>"
                 elif "gemm_nt" in name:
                     big = "Li8ELi4E" in name or "Cfg<2, 4, 8, 4, 2>" in name
