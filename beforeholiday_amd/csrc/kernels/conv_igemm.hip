@@ -72,25 +72,38 @@ BH_DEVICE void igemm_epilogue(const IgemmArgs& a, const IgemmPhase& ph, f16v (&a
     s1[t] = s2[t] = 0.f;
     e0[t] = (STATS && a.kshift) ? a.kshift[o0 + 32 * t + r] : 0.f;
   }
+  // pixel -> (image, row, column) by two divisions per strip, then stepping: the 16 pixels of a lane are
+  // pb + 0..3, 8..11, 16..19, 24..27 (grid < 2^31 pixels, igemm_supported); a 64-bit division per pixel
+  // cost ~2 VALU per MFMA
 #pragma unroll
-  for (int m = 0; m < MT; ++m)
+  for (int m = 0; m < MT; ++m) {
+    const int pb = mt * (kWaves * MW) + wave * MW + 32 * m + 4 * h;
+    const int n0 = pb / HWg, rem0 = pb - n0 * HWg, i0 = rem0 / a.Wg, j0 = rem0 - i0 * a.Wg;
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
-      const int64_t p = (int64_t)mt * (kWaves * MW) + wave * MW + 32 * m + 8 * (v >> 2) + 4 * h + (v & 3);
-      if (p >= P) continue;
-      const int n = (int)(p / HWg), rem = (int)(p - (int64_t)n * HWg), i = rem / a.Wg, j = rem - i * a.Wg;
+      const int d = 8 * (v >> 2) + (v & 3);
+      if ((int64_t)pb + d >= P) continue;
+      int n = n0, i = i0, j = j0 + d;
+      while (j >= a.Wg) {
+        j -= a.Wg;
+        if (++i == a.Hg) {
+          i = 0;
+          ++n;
+        }
+      }
       const int64_t off = (((int64_t)n * a.Hy + i * a.so + ph.py) * a.Wy + j * a.so + ph.px) * a.Nout + o0 + r;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const T o = from_f<T>(acc[m][t][v]);
         Y[off + 32 * t] = o;
         if constexpr (STATS) {
-          const float d = to_f<T>(o) - e0[t];
-          s1[t] += d;
-          s2[t] = fmaf(d, d, s2[t]);
+          const float dd = to_f<T>(o) - e0[t];
+          s1[t] += dd;
+          s2[t] = fmaf(dd, dd, s2[t]);
         }
       }
     }
+  }
   if constexpr (STATS) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
