@@ -236,6 +236,10 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
   const int gi = r32 / GW, jl = r32 - gi * GW;
   const int hlane = (gi * (GW + 2) + jl) * kPix + gi * kImgShift;  // this lane's halo pixel at s = 0
   T* Y = reinterpret_cast<T*>(a.y);
+  // the pixel-per-register epilogues store through a buffer resource: a 32-bit byte offset per store instead
+  // of 64-bit address math (conv3x3_supported keeps N H W K * 2 below kOutOfRange)
+  const __amdgpu_buffer_rsrc_t rsY =
+      __builtin_amdgcn_make_buffer_rsrc(Y, (short)0, (int)((int64_t)N * H * W * a.K * 2), 0x00020000);
   const T* BY = reinterpret_cast<const T*>(a.by);
   // Output tile of the wave, D[pixel][channel] (the MFMA's A operand is the halo, B the weights):
   // lane (r32, h) holds channel k0 + 32 kb + r32 of pixels 8 (v >> 2) + 4 h + (v & 3) of window row
@@ -305,7 +309,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_conv3x3(Conv3x3Args a, Geo g) {
             if (a.r && a.r_mul) xv *= rv;
           }
           const T o = from_f<T>(xv);
-          Y[off + 32 * kb] = o;
+          __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, o), rsY, (off + 32 * kb) * 2, 0, 0);
           const float f = to_f<T>(o);  // statistics of the value as stored
           if constexpr (EPI == kConvEpiStats) {
             const float d = f - e0[kb];
@@ -514,7 +518,7 @@ bool conv3x3_supported(const Conv3x3Args& a) {
   if (a.epi == kConvEpiBwd && (!a.by || !al(a.by) || !a.bscale || !a.bshift || !a.bmean)) return false;
   if (a.epi == kConvEpiAffine && (!a.a_scale || !a.a_shift || a.pro_scale)) return false;
   return a.N > 0 && a.H > 0 && a.W > 0 && a.C > 0 && a.K > 0 && a.C % kCK == 0 && a.K % kBN == 0 && al(a.x) &&
-         al(a.w) && al(a.y) && pix * a.C * 2 + 128 < kOutOfRange && pix * a.K < (1ll << 31) &&
+         al(a.w) && al(a.y) && pix * a.C * 2 + 128 < kOutOfRange && pix * a.K * 2 < kOutOfRange &&
          (int64_t)a.K * 9 * a.C * 2 < kOutOfRange;  // 32-bit byte offsets in the buffer loads
 }
 
