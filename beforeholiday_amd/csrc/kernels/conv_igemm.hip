@@ -65,7 +65,9 @@ BH_DEVICE void igemm_epilogue(const IgemmArgs& a, const IgemmPhase& ph, f16v (&a
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
   const int HWg = a.Hg * a.Wg;
   const int64_t P = (int64_t)a.N * HWg;
-  T* __restrict__ Y = reinterpret_cast<T*>(a.y);
+  // stores through a buffer resource: 32-bit byte offsets (igemm_supported keeps the output below kOutOfRange)
+  const __amdgpu_buffer_rsrc_t rsY = __builtin_amdgcn_make_buffer_rsrc(
+      a.y, (short)0, (int)((int64_t)a.N * a.Hy * a.Wy * a.Nout * 2), 0x00020000);
   float s1[NT], s2[NT], e0[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -91,11 +93,11 @@ BH_DEVICE void igemm_epilogue(const IgemmArgs& a, const IgemmPhase& ph, f16v (&a
           ++n;
         }
       }
-      const int64_t off = (((int64_t)n * a.Hy + i * a.so + ph.py) * a.Wy + j * a.so + ph.px) * a.Nout + o0 + r;
+      const int off = ((n * a.Hy + i * a.so + ph.py) * a.Wy + j * a.so + ph.px) * a.Nout + o0 + r;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const T o = from_f<T>(acc[m][t][v]);
-        Y[off + 32 * t] = o;
+        __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, o), rsY, (off + 32 * t) * 2, 0, 0);
         if constexpr (STATS) {
           const float dd = to_f<T>(o) - e0[t];
           s1[t] += dd;
@@ -497,6 +499,7 @@ bool igemm_supported(const IgemmArgs& a) {
   // 32-bit buffer offsets for a (the out-of-range sentinel sits past it), 32-bit pixel indices
   if ((int64_t)a.N * a.Ha * a.Wa * a.Ca * 2 + 128 >= kOutOfRange) return false;
   if ((int64_t)a.Nout * a.taps_total * a.Ca * 2 >= kOutOfRange) return false;  // 32-bit weight offsets
+  if ((int64_t)a.N * a.Hy * a.Wy * a.Nout * 2 >= kOutOfRange) return false;     // 32-bit output offsets
   if ((int64_t)a.N * a.Hg * a.Wg >= (1ll << 31)) return false;
   if (a.pro_scale && (!a.pro_shift || a.Ca > kMaxProC)) return false;
   if (a.part && a.nphase != 1) return false;
